@@ -1,0 +1,818 @@
+// Implicit-GEMM convolutions for the HyRES hot path on CDNA4 (gfx950), fp32 in / fp32 accumulate.
+//
+// Every Conv2d / ConvTranspose2d / GDN contraction of the reference (models/checkerboard.py:35-88,
+// models/layers/attention.py, models/layers/enhancement.py, compressai GDN / RBB) and their
+// input-gradients run through ONE kernel family:
+//     Y[b, i*osh+oph, j*osw+opw, co] = epi( sum_{t in taps(phase)} sum_ci X[b, i*ish+dh_t, j*isw+dw_t, ci] * W2[co][t][ci] )
+// GEMM view: M = output pixels of one phase (NHWC rows), N = output channels, K = taps x Ci.
+//   * operands are staged HBM -> registers -> LDS in 32-deep K chunks (the next chunk's global
+//     loads are issued before the current chunk's MFMAs: issue-early / write-late);
+//   * the MFMA is v_mfma_f32_32x32x2_f32 (exact fp32, 64 FLOP/clk/SIMD = the fp32 peak);
+//   * both LDS tiles are stored K-contiguous ([row][k], +4 float pad) and the K order inside a chunk
+//     is permuted so that lane-half h consumes k = 16h + s at MFMA step s: one ds_read_b128 feeds four
+//     consecutive MFMA steps (conflict-free with the 36-float row pitch).
+// Weight gradients use a second kernel (P^T Q over pixels, split-K slabs + deterministic reduce).
+#include "common.h"
+
+namespace hyres {
+
+constexpr int KT = 32;    // K chunk (floats)
+constexpr int PADK = 36;  // LDS row pitch (floats)
+
+struct ConvArgs {
+    hyres_conv_geom g;
+    const float* x;
+    const float* w2;
+    int ldw;
+    float* y;
+    hyres_epilogue e;
+    int M;  // B*Hq*Wq
+};
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+
+template <int TM, int TN, int WAVES_M, int WAVES_N, int MODE>
+__global__ __launch_bounds__(256) void conv_fwd_kernel(const ConvArgs a) {
+    // MODE 0: Ci % 32 == 0 (float4 loads); 1: same + square A (GDN); 2: generic scalar (small Ci).
+    constexpr int BM = 32 * TM * WAVES_M;
+    constexpr int BN = 32 * TN * WAVES_N;
+    __shared__ __attribute__((aligned(16))) float As[BM * PADK];
+    __shared__ __attribute__((aligned(16))) float Bs[BN * PADK];
+
+    const hyres_conv_geom& g = a.g;
+    const int tid = threadIdx.x;
+    const int phase = blockIdx.z;
+    const int m0 = blockIdx.x * BM;
+    const int n0 = blockIdx.y * BN;
+    const int HqWq = g.Hq * g.Wq;
+    const int ntap = g.ntap[phase];
+    const int tap0 = g.tap0[phase];
+    const int Ci = g.Ci;
+
+    constexpr int A_V = (MODE == 2) ? (BM * KT / 256) : (BM / 32);
+    constexpr int B_V = (MODE == 2) ? (BN * KT / 256) : (BN / 32);
+
+    // ---- per-thread A rows (pixel decode once)
+    int a_b[A_V], a_i[A_V], a_j[A_V];
+    bool a_ok[A_V];
+#pragma unroll
+    for (int q = 0; q < A_V; ++q) {
+        int row = (MODE == 2) ? ((tid + 256 * q) / KT) : (tid / 8 + 32 * q);
+        int m = m0 + row;
+        a_ok[q] = m < a.M;
+        int mm = a_ok[q] ? m : 0;
+        a_b[q] = mm / HqWq;
+        int r = mm - a_b[q] * HqWq;
+        a_i[q] = r / g.Wq;
+        a_j[q] = r - a_i[q] * g.Wq;
+    }
+    const int c4 = tid & 7;
+
+    int nk;
+    if constexpr (MODE == 2) nk = (ntap * Ci + KT - 1) / KT;
+    else nk = ntap * (Ci / KT);
+
+    float4 ra[MODE == 2 ? 1 : A_V], rb[MODE == 2 ? 1 : B_V];
+    float sa[MODE == 2 ? A_V : 1], sb[MODE == 2 ? B_V : 1];
+
+    auto load_chunk = [&](int kc) {
+        if constexpr (MODE != 2) {
+            const int cpt = Ci / KT;
+            const int t = kc / cpt;
+            const int c0 = (kc - t * cpt) * KT + 4 * c4;
+            const int gt = tap0 + t;
+            const int dh = g.dh[gt], dw = g.dw[gt];
+#pragma unroll
+            for (int q = 0; q < A_V; ++q) {
+                int ih = a_i[q] * g.ish + dh, iw = a_j[q] * g.isw + dw;
+                bool ok = a_ok[q] && ih >= 0 && ih < g.Hi && iw >= 0 && iw < g.Wi;
+                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (ok) v = ld4(a.x + ((long long)(a_b[q] * g.Hi + ih) * g.Wi + iw) * g.ldx + c0);
+                if constexpr (MODE == 1) { v.x *= v.x; v.y *= v.y; v.z *= v.z; v.w *= v.w; }
+                ra[q] = v;
+            }
+#pragma unroll
+            for (int q = 0; q < B_V; ++q) {
+                int co = n0 + tid / 8 + 32 * q;
+                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (co < g.Co) v = ld4(a.w2 + (long long)co * a.ldw + (long long)gt * Ci + c0);
+                rb[q] = v;
+            }
+        } else {
+            const int K = ntap * Ci;
+#pragma unroll
+            for (int q = 0; q < A_V; ++q) {
+                int e = tid + 256 * q;
+                int k = kc * KT + (e % KT);
+                float v = 0.f;
+                if (a_ok[q] && k < K) {
+                    int t = k / Ci;
+                    int ci = k - t * Ci;
+                    int gt = tap0 + t;
+                    int ih = a_i[q] * g.ish + g.dh[gt], iw = a_j[q] * g.isw + g.dw[gt];
+                    if (ih >= 0 && ih < g.Hi && iw >= 0 && iw < g.Wi)
+                        v = a.x[((long long)(a_b[q] * g.Hi + ih) * g.Wi + iw) * g.ldx + ci];
+                }
+                sa[q] = v;
+            }
+#pragma unroll
+            for (int q = 0; q < B_V; ++q) {
+                int e = tid + 256 * q;
+                int co = n0 + e / KT;
+                int k = kc * KT + (e % KT);
+                float v = 0.f;
+                if (co < g.Co && k < K) v = a.w2[(long long)co * a.ldw + (long long)tap0 * Ci + k];
+                sb[q] = v;
+            }
+        }
+    };
+    auto store_chunk = [&]() {
+        if constexpr (MODE != 2) {
+#pragma unroll
+            for (int q = 0; q < A_V; ++q)
+                *reinterpret_cast<float4*>(&As[(tid / 8 + 32 * q) * PADK + 4 * c4]) = ra[q];
+#pragma unroll
+            for (int q = 0; q < B_V; ++q)
+                *reinterpret_cast<float4*>(&Bs[(tid / 8 + 32 * q) * PADK + 4 * c4]) = rb[q];
+        } else {
+#pragma unroll
+            for (int q = 0; q < A_V; ++q) {
+                int e = tid + 256 * q;
+                As[(e / KT) * PADK + (e % KT)] = sa[q];
+            }
+#pragma unroll
+            for (int q = 0; q < B_V; ++q) {
+                int e = tid + 256 * q;
+                Bs[(e / KT) * PADK + (e % KT)] = sb[q];
+            }
+        }
+    };
+
+    const int lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+    const int lr = lane & 31, lh = lane >> 5;
+
+    floatx16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    if (nk > 0) load_chunk(0);
+    for (int kc = 0; kc < nk; ++kc) {
+        __syncthreads();
+        store_chunk();
+        __syncthreads();
+        if (kc + 1 < nk) load_chunk(kc + 1);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            float4 af[TM], bf[TN];
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm)
+                af[tm] = *reinterpret_cast<const float4*>(
+                    &As[(wm * TM * 32 + tm * 32 + lr) * PADK + lh * 16 + 4 * u]);
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn)
+                bf[tn] = *reinterpret_cast<const float4*>(
+                    &Bs[(wn * TN * 32 + tn * 32 + lr) * PADK + lh * 16 + 4 * u]);
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+#pragma unroll
+                for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                    for (int tn = 0; tn < TN; ++tn) {
+                        float av = e == 0 ? af[tm].x : e == 1 ? af[tm].y : e == 2 ? af[tm].z : af[tm].w;
+                        float bv = e == 0 ? bf[tn].x : e == 1 ? bf[tn].y : e == 2 ? bf[tn].z : bf[tn].w;
+                        acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[tm][tn], 0, 0, 0);
+                    }
+        }
+    }
+
+    // ---- epilogue
+    const hyres_epilogue& e = a.e;
+    const int oph = g.oph[phase], opw = g.opw[phase];
+    float slope = 0.f;
+    if (e.act == HYRES_ACT_PRELU) slope = e.slope[0];
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) {
+        const int n = n0 + wn * TN * 32 + tn * 32 + lr;
+        if (n >= g.Co) continue;
+        const float bias = e.bias ? e.bias[n] : 0.f;
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + wm * TM * 32 + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                if (m >= a.M) continue;
+                const int b = m / HqWq;
+                const int rr = m - b * HqWq;
+                const int i = rr / g.Wq;
+                const int j = rr - i * g.Wq;
+                const long long pix = (long long)(b * g.Ho + i * g.osh + oph) * g.Wo + j * g.osw + opw;
+                float v = acc[tm][tn][r];
+                switch (e.kind) {
+                    case HYRES_EPI_BIAS: {
+                        v += bias;
+                        if (e.res) v += e.res[pix * e.ldres + n];
+                        if (e.out2) e.out2[pix * e.ldo2 + n] = v;  // pre-activation (PReLU backward)
+                        if (e.act == HYRES_ACT_RELU) v = fmaxf(v, 0.f);
+                        else if (e.act == HYRES_ACT_PRELU) v = v >= 0.f ? v : slope * v;
+                        break;
+                    }
+                    case HYRES_EPI_GDN:
+                    case HYRES_EPI_IGDN: {
+                        const float nv = v + bias;
+                        const float xv = e.aux0[pix * e.ld0 + n];
+                        e.out2[pix * e.ldo2 + n] = nv;
+                        v = (e.kind == HYRES_EPI_GDN) ? xv * (1.0f / sqrtf(nv)) : xv * sqrtf(nv);
+                        break;
+                    }
+                    case HYRES_EPI_GDN_BWD:
+                    case HYRES_EPI_IGDN_BWD: {
+                        const float xv = e.aux0[pix * e.ld0 + n];
+                        const float gv = e.aux1[pix * e.ld1 + n];
+                        const float nv = e.aux2[pix * e.ld2 + n];
+                        const float f = (e.kind == HYRES_EPI_GDN_BWD) ? (1.0f / sqrtf(nv)) : sqrtf(nv);
+                        v = 2.0f * xv * v + gv * f;
+                        break;
+                    }
+                    default: break;
+                }
+                float* yp = a.y + pix * g.ldy + n;
+                if (e.accumulate) v += *yp;
+                *yp = v;
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// weight gradient:  out[t][m][n] = sum_q P[q][m] * Q[shift_t(q)][n]
+// ------------------------------------------------------------------------------------------------
+struct WgradArgs {
+    hyres_wgrad_desc d;
+    const float* p;
+    const float* q;
+    float* slab;  // [nsplit][ntaps][M][N]
+    int chunks_per_split;
+    int nchunks;
+    int mtiles;
+};
+
+template <int TM, int TN, int WAVES_M, int WAVES_N, bool VP, bool VQ, bool SQ>
+__global__ __launch_bounds__(256) void wgrad_kernel(const WgradArgs a) {
+    constexpr int BM = 32 * TM * WAVES_M;
+    constexpr int BN = 32 * TN * WAVES_N;
+    constexpr int PP = BM + 4, PQ = BN + 4;
+    __shared__ __attribute__((aligned(16))) float Ps[KT * PP];
+    __shared__ __attribute__((aligned(16))) float Qs[KT * PQ];
+    const hyres_wgrad_desc& d = a.d;
+    const int tid = threadIdx.x;
+    const int mt = blockIdx.x % a.mtiles, nt = blockIdx.x / a.mtiles;
+    const int m0 = mt * BM, n0 = nt * BN;
+    const int t = blockIdx.y;
+    const int split = blockIdx.z;
+    const int HqWq = d.Hq * d.Wq;
+    const long long Qtot = (long long)d.B * HqWq;
+    const int dh = d.dh[t], dw = d.dw[t];
+
+    constexpr int P_V = VP ? (KT * BM / 4 / 256) : (KT * BM / 256);
+    constexpr int Q_V = VQ ? (KT * BN / 4 / 256) : (KT * BN / 256);
+    static_assert(P_V >= 1 && Q_V >= 1, "tile too small");
+    float4 rp[VP ? P_V : 1], rq[VQ ? Q_V : 1];
+    float sp[VP ? 1 : P_V], sq[VQ ? 1 : Q_V];
+
+    auto load_chunk = [&](int kc) {
+        const long long k0 = (long long)kc * KT;
+        if constexpr (VP) {
+#pragma unroll
+            for (int i = 0; i < P_V; ++i) {
+                int e = tid + 256 * i;
+                int row = e / (BM / 4), c = (e % (BM / 4)) * 4;
+                long long qq = k0 + row;
+                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (qq < Qtot && m0 + c < d.M) v = ld4(a.p + qq * d.ldp + m0 + c);
+                rp[i] = v;
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < P_V; ++i) {
+                int e = tid + 256 * i;
+                int row = e / BM, c = e % BM;
+                long long qq = k0 + row;
+                float v = 0.f;
+                if (qq < Qtot && m0 + c < d.M) v = a.p[qq * d.ldp + m0 + c];
+                sp[i] = v;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < Q_V; ++i) {
+            int e = tid + 256 * i;
+            int row = VQ ? e / (BN / 4) : e / BN;
+            int c = VQ ? (e % (BN / 4)) * 4 : e % BN;
+            long long qq = k0 + row;
+            bool ok = qq < Qtot && n0 + c < d.N;
+            long long off = 0;
+            if (ok) {
+                int b = (int)(qq / HqWq);
+                int r = (int)(qq - (long long)b * HqWq);
+                int ii = r / d.Wq, jj = r - (r / d.Wq) * d.Wq;
+                int ih = ii * d.sq + dh, iw = jj * d.sq + dw;
+                ok = ih >= 0 && ih < d.Hqq && iw >= 0 && iw < d.Wqq;
+                off = ((long long)(b * d.Hqq + ih) * d.Wqq + iw) * d.ldq + n0 + c;
+            }
+            if constexpr (VQ) {
+                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (ok) v = ld4(a.q + off);
+                if constexpr (SQ) { v.x *= v.x; v.y *= v.y; v.z *= v.z; v.w *= v.w; }
+                rq[i] = v;
+            } else {
+                float v = ok ? a.q[off] : 0.f;
+                if constexpr (SQ) v *= v;
+                sq[i] = v;
+            }
+        }
+    };
+    auto store_chunk = [&]() {
+        if constexpr (VP) {
+#pragma unroll
+            for (int i = 0; i < P_V; ++i) {
+                int e = tid + 256 * i;
+                int row = e / (BM / 4), c = (e % (BM / 4)) * 4;
+                *reinterpret_cast<float4*>(&Ps[row * PP + c]) = rp[i];
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < P_V; ++i) {
+                int e = tid + 256 * i;
+                Ps[(e / BM) * PP + e % BM] = sp[i];
+            }
+        }
+        if constexpr (VQ) {
+#pragma unroll
+            for (int i = 0; i < Q_V; ++i) {
+                int e = tid + 256 * i;
+                int row = e / (BN / 4), c = (e % (BN / 4)) * 4;
+                *reinterpret_cast<float4*>(&Qs[row * PQ + c]) = rq[i];
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < Q_V; ++i) {
+                int e = tid + 256 * i;
+                Qs[(e / BN) * PQ + e % BN] = sq[i];
+            }
+        }
+    };
+
+    const int lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+    const int lr = lane & 31, lh = lane >> 5;
+    floatx16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const int kc_begin = split * a.chunks_per_split;
+    const int kc_end = min(a.nchunks, kc_begin + a.chunks_per_split);
+    if (kc_begin < kc_end) load_chunk(kc_begin);
+    for (int kc = kc_begin; kc < kc_end; ++kc) {
+        __syncthreads();
+        store_chunk();
+        __syncthreads();
+        if (kc + 1 < kc_end) load_chunk(kc + 1);
+#pragma unroll
+        for (int s = 0; s < KT / 2; ++s) {
+            const int k = lh * (KT / 2) + s;
+            float af[TM], bf[TN];
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm) af[tm] = Ps[k * PP + wm * TM * 32 + tm * 32 + lr];
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn) bf[tn] = Qs[k * PQ + wn * TN * 32 + tn * 32 + lr];
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                for (int tn = 0; tn < TN; ++tn)
+                    acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[tm], bf[tn], acc[tm][tn], 0, 0, 0);
+        }
+    }
+    // slab store [split][t][M][N]
+    float* out = a.slab + ((long long)split * d.ntaps + t) * (long long)d.M * d.N;
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) {
+            const int n = n0 + wn * TN * 32 + tn * 32 + lr;
+            if (n >= d.N) continue;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + wm * TM * 32 + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                if (m < d.M) out[(long long)m * d.N + n] = acc[tm][tn][r];
+            }
+        }
+}
+
+__global__ void wgrad_reduce_kernel(const float* slab, int nsplit, int ntaps, int M, int N, float* dst,
+                                    int sm, int sn, int st, int accumulate) {
+    const long long total = (long long)ntaps * M * N;
+    const long long stride_split = total;
+    for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
+         idx += (long long)gridDim.x * blockDim.x) {
+        float s = 0.f;
+        for (int k = 0; k < nsplit; ++k) s += slab[k * stride_split + idx];
+        const int n = (int)(idx % N);
+        const long long r = idx / N;
+        const int m = (int)(r % M);
+        const int t = (int)(r / M);
+        float* p = dst + (long long)m * sm + (long long)n * sn + (long long)t * st;
+        *p = accumulate ? (*p + s) : s;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// weight re-layout
+// ------------------------------------------------------------------------------------------------
+struct PrepArgs {
+    const float* w;
+    float* w2;
+    const float* mask;
+    int mode, rows, cols, ntaps, KH, KW, Ci, Co;
+    int kh[HYRES_MAX_TAPS], kw[HYRES_MAX_TAPS];
+};
+
+__global__ void weight_prep_kernel(const PrepArgs a) {
+    const long long total = (long long)a.rows * a.ntaps * a.cols;
+    for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
+         idx += (long long)gridDim.x * blockDim.x) {
+        const int c = (int)(idx % a.cols);
+        const long long rt = idx / a.cols;
+        const int t = (int)(rt % a.ntaps);
+        const int r = (int)(rt / a.ntaps);
+        const int kh = a.kh[t], kw = a.kw[t];
+        long long src;
+        switch (a.mode) {
+            case HYRES_WPREP_CONV:  // W[Co][Ci][KH][KW]; r = co, c = ci
+                src = (((long long)r * a.Ci + c) * a.KH + kh) * a.KW + kw; break;
+            case HYRES_WPREP_CONV_DGRAD:  // r = ci, c = co
+                src = (((long long)c * a.Ci + r) * a.KH + kh) * a.KW + kw; break;
+            case HYRES_WPREP_DECONV:  // W[Ci][Co][K][K]; r = co, c = ci
+                src = (((long long)c * a.Co + r) * a.KH + kh) * a.KW + kw; break;
+            default:  // DECONV_DGRAD: r = ci, c = co
+                src = (((long long)r * a.Co + c) * a.KH + kh) * a.KW + kw; break;
+        }
+        float v = a.w[src];
+        if (a.mask) v *= a.mask[src];
+        a.w2[idx] = v;
+    }
+}
+
+__global__ void colsum_partial_kernel(const float* x, int P, int C, int ld, int rows_per_block,
+                                      float* part) {
+    // block: 256 threads; each thread owns channel column(s) c = threadIdx.x + 256*k
+    const int r0 = blockIdx.x * rows_per_block;
+    const int r1 = min(P, r0 + rows_per_block);
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+        float s = 0.f;
+        for (int r = r0; r < r1; ++r) s += x[(long long)r * ld + c];
+        part[(long long)blockIdx.x * C + c] = s;
+    }
+}
+
+__global__ void colsum_final_kernel(const float* part, int nb, int C, float* dst, int accumulate) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    float s = 0.f;
+    for (int b = 0; b < nb; ++b) s += part[(long long)b * C + c];
+    dst[c] = accumulate ? dst[c] + s : s;
+}
+
+// ------------------------------------------------------------------------------------------------
+// host side
+// ------------------------------------------------------------------------------------------------
+template <int TM, int TN, int WM_, int WN_>
+static int launch_fwd(const ConvArgs& a, int mode, hipStream_t st) {
+    constexpr int BM = 32 * TM * WM_, BN = 32 * TN * WN_;
+    dim3 grid(ceil_div(a.M, BM), ceil_div(a.g.Co, BN), a.g.nphase);
+    if (mode == 0) hipLaunchKernelGGL((conv_fwd_kernel<TM, TN, WM_, WN_, 0>), grid, dim3(256), 0, st, a);
+    else if (mode == 1) hipLaunchKernelGGL((conv_fwd_kernel<TM, TN, WM_, WN_, 1>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((conv_fwd_kernel<TM, TN, WM_, WN_, 2>), grid, dim3(256), 0, st, a);
+    return HY_LAUNCH_CHECK("conv_fwd_kernel");
+}
+
+static void fill_taps(hyres_conv_geom* g, int p, int* tapcount, int K, int pad, int ph, int pw,
+                      int* khs, int* kws) {
+    // sub-pixel phase (ph, pw) of a stride-2 transposed structure: taps kh with (ph+pad-kh) even
+    g->tap0[p] = *tapcount;
+    int n = 0;
+    for (int kh = 0; kh < K; ++kh) {
+        if (((ph + pad - kh) & 1) != 0) continue;
+        for (int kw = 0; kw < K; ++kw) {
+            if (((pw + pad - kw) & 1) != 0) continue;
+            int t = *tapcount + n;
+            g->dh[t] = (ph + pad - kh) / 2;
+            g->dw[t] = (pw + pad - kw) / 2;
+            khs[t] = kh;
+            kws[t] = kw;
+            ++n;
+        }
+    }
+    g->ntap[p] = n;
+    g->oph[p] = ph;
+    g->opw[p] = pw;
+    *tapcount += n;
+}
+
+}  // namespace hyres
+
+using namespace hyres;
+
+
+extern "C" {
+
+
+int hyres_geom_conv2d(hyres_conv_geom* g, int B, int H, int W, int Ci, int ldx, int Co, int ldy, int KH,
+                      int KW, int stride, int pad, int dil) {
+    HY_REQUIRE(g && KH * KW <= HYRES_MAX_TAPS && stride >= 1 && dil >= 1, HYRES_E_ARG, "bad conv args");
+    *g = hyres_conv_geom{};
+    g->B = B; g->Hi = H; g->Wi = W; g->Ci = Ci; g->ldx = ldx;
+    g->Ho = (H + 2 * pad - dil * (KH - 1) - 1) / stride + 1;
+    g->Wo = (W + 2 * pad - dil * (KW - 1) - 1) / stride + 1;
+    g->Co = Co; g->ldy = ldy;
+    g->nphase = 1; g->Hq = g->Ho; g->Wq = g->Wo;
+    g->osh = g->osw = 1; g->ish = g->isw = stride;
+    g->ntap[0] = KH * KW; g->tap0[0] = 0; g->ntaps = KH * KW;
+    for (int kh = 0; kh < KH; ++kh)
+        for (int kw = 0; kw < KW; ++kw) {
+            int t = kh * KW + kw;
+            g->dh[t] = kh * dil - pad;
+            g->dw[t] = kw * dil - pad;
+        }
+    return ok();
+}
+
+int hyres_geom_conv2d_dgrad(hyres_conv_geom* g, int B, int H, int W, int Ci, int ld_dx, int Co, int ld_dy,
+                            int KH, int KW, int stride, int pad, int dil) {
+    HY_REQUIRE(g && KH * KW <= HYRES_MAX_TAPS, HYRES_E_ARG, "bad conv dgrad args");
+    *g = hyres_conv_geom{};
+    const int Ho = (H + 2 * pad - dil * (KH - 1) - 1) / stride + 1;
+    const int Wo = (W + 2 * pad - dil * (KW - 1) - 1) / stride + 1;
+    g->B = B; g->Hi = Ho; g->Wi = Wo; g->Ci = Co; g->ldx = ld_dy;
+    g->Ho = H; g->Wo = W; g->Co = Ci; g->ldy = ld_dx;
+    if (stride == 1) {
+        g->nphase = 1; g->Hq = H; g->Wq = W; g->osh = g->osw = 1; g->ish = g->isw = 1;
+        g->ntap[0] = KH * KW; g->tap0[0] = 0; g->ntaps = KH * KW;
+        for (int kh = 0; kh < KH; ++kh)
+            for (int kw = 0; kw < KW; ++kw) {
+                int t = kh * KW + kw;
+                g->dh[t] = pad - kh * dil;
+                g->dw[t] = pad - kw * dil;
+            }
+        return ok();
+    }
+    HY_REQUIRE(stride == 2 && dil == 1 && KH == KW && (H % 2) == 0 && (W % 2) == 0 && Ho * 2 == H &&
+                   Wo * 2 == W, HYRES_E_SHAPE, "conv dgrad: only stride 2, dil 1, square K, even H/W");
+    g->nphase = 4; g->Hq = H / 2; g->Wq = W / 2; g->osh = g->osw = 2; g->ish = g->isw = 1;
+    int cnt = 0;
+    int khs[HYRES_MAX_TAPS], kws[HYRES_MAX_TAPS];
+    for (int p = 0; p < 4; ++p) fill_taps(g, p, &cnt, KH, pad, p >> 1, p & 1, khs, kws);
+    g->ntaps = cnt;
+    return ok();
+}
+
+int hyres_geom_deconv2d(hyres_conv_geom* g, int B, int H, int W, int Ci, int ldx, int Co, int ldy, int K,
+                        int pad) {
+    HY_REQUIRE(g && K * K <= HYRES_MAX_TAPS, HYRES_E_ARG, "bad deconv args");
+    HY_REQUIRE(2 * pad == K - 1, HYRES_E_SHAPE, "deconv: expects padding = K//2, output_padding = 1");
+    *g = hyres_conv_geom{};
+    g->B = B; g->Hi = H; g->Wi = W; g->Ci = Ci; g->ldx = ldx;
+    g->Ho = 2 * H; g->Wo = 2 * W; g->Co = Co; g->ldy = ldy;
+    g->nphase = 4; g->Hq = H; g->Wq = W; g->osh = g->osw = 2; g->ish = g->isw = 1;
+    int cnt = 0;
+    int khs[HYRES_MAX_TAPS], kws[HYRES_MAX_TAPS];
+    for (int p = 0; p < 4; ++p) fill_taps(g, p, &cnt, K, pad, p >> 1, p & 1, khs, kws);
+    g->ntaps = cnt;
+    return ok();
+}
+
+int hyres_geom_deconv2d_dgrad(hyres_conv_geom* g, int B, int H, int W, int Ci, int ld_dx, int Co, int ld_dy,
+                              int K, int pad) {
+    HY_REQUIRE(g && K * K <= HYRES_MAX_TAPS, HYRES_E_ARG, "bad deconv dgrad args");
+    *g = hyres_conv_geom{};
+    g->B = B; g->Hi = 2 * H; g->Wi = 2 * W; g->Ci = Co; g->ldx = ld_dy;
+    g->Ho = H; g->Wo = W; g->Co = Ci; g->ldy = ld_dx;
+    g->nphase = 1; g->Hq = H; g->Wq = W; g->osh = g->osw = 1; g->ish = g->isw = 2;
+    g->ntap[0] = K * K; g->tap0[0] = 0; g->ntaps = K * K;
+    for (int kh = 0; kh < K; ++kh)
+        for (int kw = 0; kw < K; ++kw) {
+            int t = kh * K + kw;
+            g->dh[t] = kh - pad;
+            g->dw[t] = kw - pad;
+        }
+    return ok();
+}
+
+int hyres_conv_weight_prep(const hyres_conv_geom* g, const float* w, float* w2, int mode, int Ci, int Co,
+                           int KH, int KW, int pad, const float* mask, hyres_stream_t s) {
+    HY_REQUIRE(g && w && w2, HYRES_E_ARG, "weight_prep: NULL");
+    PrepArgs a{};
+    a.w = w; a.w2 = w2; a.mask = mask; a.mode = mode; a.KH = KH; a.KW = KW; a.Ci = Ci; a.Co = Co;
+    a.ntaps = g->ntaps;
+    const bool phased = g->nphase == 4;
+    if (phased) {
+        // rebuild the phase tap order exactly as fill_taps did
+        int t = 0;
+        for (int p = 0; p < 4; ++p) {
+            int ph = p >> 1, pw = p & 1;
+            for (int kh = 0; kh < KH; ++kh) {
+                if (((ph + pad - kh) & 1) != 0) continue;
+                for (int kw = 0; kw < KW; ++kw) {
+                    if (((pw + pad - kw) & 1) != 0) continue;
+                    a.kh[t] = kh; a.kw[t] = kw; ++t;
+                }
+            }
+        }
+        HY_REQUIRE(t == g->ntaps, HYRES_E_SHAPE, "weight_prep: phase tap mismatch");
+    } else {
+        HY_REQUIRE(g->ntaps == KH * KW, HYRES_E_SHAPE, "weight_prep: tap count mismatch");
+        for (int t = 0; t < KH * KW; ++t) { a.kh[t] = t / KW; a.kw[t] = t % KW; }
+    }
+    switch (mode) {
+        case HYRES_WPREP_CONV: a.rows = Co; a.cols = Ci; break;
+        case HYRES_WPREP_CONV_DGRAD: a.rows = Ci; a.cols = Co; break;
+        case HYRES_WPREP_DECONV: a.rows = Co; a.cols = Ci; break;
+        case HYRES_WPREP_DECONV_DGRAD: a.rows = Ci; a.cols = Co; break;
+        default: return set_error(HYRES_E_ARG, "weight_prep: bad mode %d", mode);
+    }
+    HY_REQUIRE(a.cols == g->Ci && a.rows >= g->Co, HYRES_E_SHAPE,
+               "weight_prep: geometry channels (%d->%d) != weight (%d->%d)", g->Ci, g->Co, a.cols, a.rows);
+    long long total = (long long)a.rows * a.ntaps * a.cols;
+    int blocks = (int)std::min<long long>((total + 255) / 256, 4096);
+    hipLaunchKernelGGL(weight_prep_kernel, dim3(blocks), dim3(256), 0, as_stream(s), a);
+    return HY_LAUNCH_CHECK("weight_prep_kernel");
+}
+
+int hyres_conv_forward(const hyres_conv_geom* g, const float* x, const float* w2, int ldw, float* y,
+                       const hyres_epilogue* e, hyres_stream_t s) {
+    HY_REQUIRE(g && x && w2 && y && e, HYRES_E_ARG, "conv_forward: NULL argument");
+    HY_REQUIRE(g->nphase >= 1 && g->nphase <= 4 && g->Ci > 0 && g->Co > 0, HYRES_E_SHAPE, "conv: bad geom");
+    HY_REQUIRE(ldw >= g->ntaps * g->Ci, HYRES_E_SHAPE, "conv: ldw %d < ntaps*Ci %d", ldw, g->ntaps * g->Ci);
+    ConvArgs a;
+    a.g = *g; a.x = x; a.w2 = w2; a.ldw = ldw; a.y = y; a.e = *e;
+    a.M = g->B * g->Hq * g->Wq;
+    int mode;
+    if (g->Ci % KT == 0) {
+        HY_REQUIRE(aligned16(x) && aligned16(w2) && g->ldx % 4 == 0 && ldw % 4 == 0, HYRES_E_ALIGN,
+                   "conv: vector path needs 16B-aligned x/w2 and ldx,ldw %% 4 == 0");
+        mode = e->square_input ? 1 : 0;
+    } else {
+        HY_REQUIRE(g->nphase == 1 && !e->square_input, HYRES_E_SHAPE,
+                   "conv: Ci %% 32 != 0 supported only single-phase, no square");
+        mode = 2;
+    }
+    if (e->kind == HYRES_EPI_GDN || e->kind == HYRES_EPI_IGDN)
+        HY_REQUIRE(e->aux0 && e->out2, HYRES_E_ARG, "conv: GDN epilogue needs aux0/out2");
+    if (e->kind == HYRES_EPI_GDN_BWD || e->kind == HYRES_EPI_IGDN_BWD)
+        HY_REQUIRE(e->aux0 && e->aux1 && e->aux2, HYRES_E_ARG, "conv: GDN bwd epilogue needs aux0..2");
+    if (e->act == HYRES_ACT_PRELU) HY_REQUIRE(e->slope, HYRES_E_ARG, "conv: PReLU needs slope");
+    hipStream_t st = as_stream(s);
+    if (g->Co > 64) return launch_fwd<2, 2, 2, 2>(a, mode, st);
+    if (g->Co > 32) return launch_fwd<2, 1, 2, 2>(a, mode, st);
+    return launch_fwd<1, 1, 4, 1>(a, mode, st);
+}
+
+int hyres_wgrad_desc_conv2d(hyres_wgrad_desc* d, int B, int H, int W, int Ci, int ldx, int Co, int ldy,
+                            int KH, int KW, int stride, int pad, int dil) {
+    HY_REQUIRE(d && KH * KW <= HYRES_MAX_TAPS, HYRES_E_ARG, "bad wgrad args");
+    *d = hyres_wgrad_desc{};
+    const int Ho = (H + 2 * pad - dil * (KH - 1) - 1) / stride + 1;
+    const int Wo = (W + 2 * pad - dil * (KW - 1) - 1) / stride + 1;
+    d->B = B; d->Hq = Ho; d->Wq = Wo;
+    d->M = Co; d->ldp = ldy;
+    d->N = Ci; d->ldq = ldx; d->Hqq = H; d->Wqq = W; d->sq = stride;
+    d->ntaps = KH * KW;
+    for (int kh = 0; kh < KH; ++kh)
+        for (int kw = 0; kw < KW; ++kw) {
+            d->dh[kh * KW + kw] = kh * dil - pad;
+            d->dw[kh * KW + kw] = kw * dil - pad;
+        }
+    d->sm = Ci * KH * KW; d->sn = KH * KW; d->st = 1;
+    return ok();
+}
+
+int hyres_wgrad_desc_deconv2d(hyres_wgrad_desc* d, int B, int H, int W, int Ci, int ldx, int Co, int ldy,
+                              int K, int pad) {
+    HY_REQUIRE(d && K * K <= HYRES_MAX_TAPS, HYRES_E_ARG, "bad wgrad args");
+    *d = hyres_wgrad_desc{};
+    d->B = B; d->Hq = H; d->Wq = W;
+    d->M = Ci; d->ldp = ldx;
+    d->N = Co; d->ldq = ldy; d->Hqq = 2 * H; d->Wqq = 2 * W; d->sq = 2;
+    d->ntaps = K * K;
+    for (int kh = 0; kh < K; ++kh)
+        for (int kw = 0; kw < K; ++kw) {
+            d->dh[kh * K + kw] = kh - pad;
+            d->dw[kh * K + kw] = kw - pad;
+        }
+    d->sm = Co * K * K; d->sn = K * K; d->st = 1;
+    return ok();
+}
+
+struct WgradPlan {
+    int TMc, TNc, WMc, WNc, BM, BN, mtiles, ntiles, nchunks, nsplit, cps;
+};
+
+static WgradPlan wgrad_plan(const hyres_wgrad_desc* d) {
+    WgradPlan p{};
+    // tile choice (32*TM*WAVES_M x 32*TN*WAVES_N)
+    if (d->M >= 128 && d->N >= 128) { p.TMc = 2; p.TNc = 2; p.WMc = 2; p.WNc = 2; }
+    else if (d->M <= 32) { p.TMc = 1; p.TNc = 1; p.WMc = 1; p.WNc = 4; }
+    else if (d->N <= 32) { p.TMc = 1; p.TNc = 1; p.WMc = 4; p.WNc = 1; }
+    else { p.TMc = 1; p.TNc = 1; p.WMc = 2; p.WNc = 2; }
+    p.BM = 32 * p.TMc * p.WMc; p.BN = 32 * p.TNc * p.WNc;
+    p.mtiles = ceil_div(d->M, p.BM); p.ntiles = ceil_div(d->N, p.BN);
+    long long Q = (long long)d->B * d->Hq * d->Wq;
+    p.nchunks = ceil_div(Q, KT);
+    long long tiles = (long long)p.mtiles * p.ntiles * d->ntaps;
+    // aim for ~2048 blocks, at least 8 chunks (256 pixels) per split
+    long long want = std::max<long long>(1, 2048 / std::max<long long>(1, tiles));
+    long long maxsplit = std::max<long long>(1, p.nchunks / 8);
+    p.nsplit = (int)std::min<long long>(want, maxsplit);
+    p.nsplit = std::min(p.nsplit, 256);
+    p.cps = ceil_div(p.nchunks, p.nsplit);
+    p.nsplit = ceil_div(p.nchunks, p.cps);
+    return p;
+}
+
+long long hyres_wgrad_workspace_bytes(const hyres_wgrad_desc* d) {
+    WgradPlan p = wgrad_plan(d);
+    return (long long)p.nsplit * d->ntaps * (long long)d->M * d->N * 4;
+}
+
+int hyres_conv_wgrad(const hyres_wgrad_desc* d, const float* pp, const float* qq, float* dst, void* ws,
+                     long long ws_bytes, hyres_stream_t s) {
+    HY_REQUIRE(d && pp && qq && dst, HYRES_E_ARG, "wgrad: NULL");
+    WgradPlan p = wgrad_plan(d);
+    long long need = (long long)p.nsplit * d->ntaps * (long long)d->M * d->N * 4;
+    HY_REQUIRE(ws && ws_bytes >= need, HYRES_E_WORKSPACE, "wgrad: workspace %lld < %lld", ws_bytes, need);
+    const bool vp = (d->M % 4 == 0) && (d->ldp % 4 == 0) && aligned16(pp);
+    const bool vq = (d->N % 4 == 0) && (d->ldq % 4 == 0) && aligned16(qq);
+    WgradArgs a;
+    a.d = *d; a.p = pp; a.q = qq; a.slab = (float*)ws; a.chunks_per_split = p.cps; a.nchunks = p.nchunks;
+    a.mtiles = p.mtiles;
+    dim3 grid(p.mtiles * p.ntiles, d->ntaps, p.nsplit);
+    hipStream_t st = as_stream(s);
+#define WG_LAUNCH(TM_, TN_, WM_, WN_)                                                                  \
+    do {                                                                                              \
+        if (vp && vq && d->square_q)                                                                  \
+            hipLaunchKernelGGL((wgrad_kernel<TM_, TN_, WM_, WN_, true, true, true>), grid, dim3(256), 0, st, a); \
+        else if (vp && vq)                                                                            \
+            hipLaunchKernelGGL((wgrad_kernel<TM_, TN_, WM_, WN_, true, true, false>), grid, dim3(256), 0, st, a); \
+        else if (d->square_q)                                                                         \
+            return set_error(HYRES_E_SHAPE, "wgrad: square_q needs vector path");                    \
+        else if (vp)                                                                                  \
+            hipLaunchKernelGGL((wgrad_kernel<TM_, TN_, WM_, WN_, true, false, false>), grid, dim3(256), 0, st, a); \
+        else if (vq)                                                                                  \
+            hipLaunchKernelGGL((wgrad_kernel<TM_, TN_, WM_, WN_, false, true, false>), grid, dim3(256), 0, st, a); \
+        else                                                                                          \
+            hipLaunchKernelGGL((wgrad_kernel<TM_, TN_, WM_, WN_, false, false, false>), grid, dim3(256), 0, st, a); \
+    } while (0)
+    if (p.TMc == 2) WG_LAUNCH(2, 2, 2, 2);
+    else if (p.WMc == 1) WG_LAUNCH(1, 1, 1, 4);
+    else if (p.WNc == 1) WG_LAUNCH(1, 1, 4, 1);
+    else WG_LAUNCH(1, 1, 2, 2);
+#undef WG_LAUNCH
+    int rc = HY_LAUNCH_CHECK("wgrad_kernel");
+    if (rc) return rc;
+    long long total = (long long)d->ntaps * d->M * d->N;
+    int blocks = (int)std::min<long long>((total + 255) / 256, 8192);
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, (const float*)ws, p.nsplit,
+                       d->ntaps, d->M, d->N, dst, d->sm, d->sn, d->st, d->accumulate);
+    return HY_LAUNCH_CHECK("wgrad_reduce_kernel");
+}
+
+long long hyres_colsum_workspace_bytes(int P, int C) {
+    int rows = 256;
+    int nb = std::min(ceil_div(P, rows), 2048);
+    return (long long)nb * C * 4;
+}
+
+int hyres_colsum(const float* x, int P, int C, int ld, float* dst, int accumulate, void* ws,
+                 long long ws_bytes, hyres_stream_t s) {
+    HY_REQUIRE(x && dst && P > 0 && C > 0, HYRES_E_ARG, "colsum: bad args");
+    int nb = std::min(ceil_div(P, 256), 2048);
+    int rows = ceil_div(P, nb);
+    nb = ceil_div(P, rows);
+    HY_REQUIRE(ws && ws_bytes >= (long long)nb * C * 4, HYRES_E_WORKSPACE, "colsum: workspace");
+    hipStream_t st = as_stream(s);
+    hipLaunchKernelGGL(colsum_partial_kernel, dim3(nb), dim3(256), 0, st, x, P, C, ld, rows, (float*)ws);
+    int rc = HY_LAUNCH_CHECK("colsum_partial");
+    if (rc) return rc;
+    hipLaunchKernelGGL(colsum_final_kernel, dim3(ceil_div(C, 256)), dim3(256), 0, st, (const float*)ws, nb, C,
+                       dst, accumulate);
+    return HY_LAUNCH_CHECK("colsum_final");
+}
+
+}  // extern "C"

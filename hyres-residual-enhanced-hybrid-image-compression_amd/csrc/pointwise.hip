@@ -1,0 +1,511 @@
+// Elementwise, reduction and optimiser kernels of the HyRES hot path (gfx950).
+// All are HBM-bound streams: grid-stride loops, 256-thread blocks, float4 where the layout allows.
+#include "common.h"
+
+#include <mutex>
+
+namespace hyres {
+
+static thread_local std::string g_err;
+
+int set_error(int code, const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+int ok() { return HYRES_OK; }
+
+static inline int grid_for(long long n, int per_thread = 1) {
+    long long b = (n / per_thread + 255) / 256;
+    if (b < 1) b = 1;
+    if (b > 8192) b = 8192;
+    return (int)b;
+}
+
+#define GRID_STRIDE(i, n) \
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < (n); i += (long long)gridDim.x * blockDim.x)
+
+// ---------------------------------------------------------------- layout
+__global__ void nchw_to_nhwc_kernel(const float* x, float* y, int B, int C, int H, int W, int ldy) {
+    const long long n = (long long)B * H * W * C;
+    GRID_STRIDE(i, n) {
+        int c = (int)(i % C);
+        long long p = i / C;  // (b,h,w)
+        int hw = (int)(p % ((long long)H * W));
+        int b = (int)(p / ((long long)H * W));
+        y[p * ldy + c] = x[((long long)b * C + c) * H * W + hw];
+    }
+}
+__global__ void nhwc_to_nchw_kernel(const float* x, int ldx, float* y, int B, int C, int H, int W) {
+    const long long n = (long long)B * C * H * W;
+    GRID_STRIDE(i, n) {
+        int hw = (int)(i % ((long long)H * W));
+        long long bc = i / ((long long)H * W);
+        int c = (int)(bc % C);
+        int b = (int)(bc / C);
+        y[i] = x[((long long)b * H * W + hw) * ldx + c];
+    }
+}
+
+// ---------------------------------------------------------------- elementwise
+__global__ void axpby_kernel(const float* a, const float* b, float alpha, float* y, long long n) {
+    GRID_STRIDE(i, n) y[i] = a[i] + alpha * b[i];
+}
+__global__ void add_clamp01_kernel(const float* x0, const float* r, float* y, long long n) {
+    GRID_STRIDE(i, n) y[i] = fminf(fmaxf(x0[i] + r[i], 0.f), 1.f);
+}
+__global__ void add_clamp01_bwd_kernel(const float* pre, const float* g, float* gx, int acc, long long n) {
+    // torch.clamp backward: gradient passes where min <= x <= max
+    GRID_STRIDE(i, n) {
+        float v = pre[i];
+        float gv = (v >= 0.f && v <= 1.f) ? g[i] : 0.f;
+        gx[i] = acc ? gx[i] + gv : gv;
+    }
+}
+__global__ void relu_bwd_kernel(const float* y, const float* g, float* gx, long long n) {
+    GRID_STRIDE(i, n) gx[i] = y[i] > 0.f ? g[i] : 0.f;
+}
+__global__ void relu_bwd_2d_kernel(const float* y, int ldy, const float* g, int ldg, float* gx, int ldgx,
+                                   long long P, int C) {
+    const long long n = P * C;
+    GRID_STRIDE(i, n) {
+        long long p = i / C;
+        int c = (int)(i - p * C);
+        gx[p * ldgx + c] = y[p * ldy + c] > 0.f ? g[p * ldg + c] : 0.f;
+    }
+}
+__global__ void prelu_bwd_kernel(const float* x, int ldx, const float* g, int ldg, float* gx, int ldgx,
+                                 long long P, int C, const float* slope, float* part) {
+    const float a = slope[0];
+    const long long n = P * C;
+    float s = 0.f;
+    GRID_STRIDE(i, n) {
+        long long p = i / C;
+        int c = (int)(i - p * C);
+        float xv = x[p * ldx + c];
+        float gv = g[p * ldg + c];
+        gx[p * ldgx + c] = xv > 0.f ? gv : a * gv;
+        if (!(xv > 0.f)) s += xv * gv;
+    }
+    // block reduce
+    __shared__ float red[256];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int k = 128; k > 0; k >>= 1) {
+        if (threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+__global__ void sum_partials_kernel(const float* part, int nb, float* out, int accumulate) {
+    __shared__ float red[256];
+    float s = 0.f;
+    for (int i = threadIdx.x; i < nb; i += 256) s += part[i];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int k = 128; k > 0; k >>= 1) {
+        if (threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[0] = accumulate ? out[0] + red[0] : red[0];
+}
+__global__ void attn_gate_fwd_kernel(const float* a, const float* b, const float* x, float* out, long long n) {
+    GRID_STRIDE(i, n) {
+        float s = 1.0f / (1.0f + expf(-b[i]));
+        out[i] = a[i] * s + x[i];
+    }
+}
+__global__ void attn_gate_bwd_kernel(const float* a, const float* b, const float* g, float* ga, float* gb,
+                                     long long n) {
+    GRID_STRIDE(i, n) {
+        float s = 1.0f / (1.0f + expf(-b[i]));
+        float gv = g[i];
+        ga[i] = gv * s;
+        gb[i] = gv * a[i] * s * (1.0f - s);
+    }
+}
+__global__ void accumulate_kernel(const float* x, float* y, long long n) {
+    GRID_STRIDE(i, n) y[i] += x[i];
+}
+__global__ void add2d_kernel(const float* x, int ldx, float* y, int ldy, long long P, int C, int acc) {
+    const long long n = P * C;
+    GRID_STRIDE(i, n) {
+        long long p = i / C;
+        int c = (int)(i - p * C);
+        float v = x[p * ldx + c];
+        float* yp = y + p * ldy + c;
+        *yp = acc ? *yp + v : v;
+    }
+}
+__global__ void mul_kernel(const float* a, const float* b, float* y, long long n) {
+    GRID_STRIDE(i, n) y[i] = a[i] * b[i];
+}
+
+// ---------------------------------------------------------------- GDN pieces
+constexpr float kPedestal = 1.4551915228366852e-11f;  // 2^-36
+__device__ __forceinline__ float beta_bound() { return 0.0010000000000072760f; }  // sqrt(1e-6 + 2^-36) as fp32
+__device__ __forceinline__ float gamma_bound() { return 3.814697265625e-06f; }     // 2^-18
+
+__global__ void gdn_reparam_fwd_kernel(const float* beta, const float* gamma, float* bp, float* gp, int C) {
+    const long long n = (long long)C * C;
+    GRID_STRIDE(i, n) {
+        float v = fmaxf(gamma[i], gamma_bound());
+        gp[i] = v * v - kPedestal;
+        if (i < C) {
+            float u = fmaxf(beta[i], beta_bound());
+            bp[i] = u * u - kPedestal;
+        }
+    }
+}
+__device__ __forceinline__ float lb_sq_bwd(float x, float bound, float g) {
+    // out = max(x, b)^2 - ped ; LowerBound passes where x >= b or grad < 0
+    float lb = fmaxf(x, bound);
+    float gl = g * 2.0f * lb;
+    return (x >= bound || gl < 0.f) ? gl : 0.f;
+}
+__global__ void gdn_reparam_bwd_kernel(const float* beta, const float* gamma, const float* dbp, const float* dgp,
+                                       float* db, float* dg, int C, int acc) {
+    const long long n = (long long)C * C;
+    GRID_STRIDE(i, n) {
+        float v = lb_sq_bwd(gamma[i], gamma_bound(), dgp[i]);
+        dg[i] = acc ? dg[i] + v : v;
+        if (i < C) {
+            float u = lb_sq_bwd(beta[i], beta_bound(), dbp[i]);
+            db[i] = acc ? db[i] + u : u;
+        }
+    }
+}
+__global__ void gdn_dnorm_kernel(const float* g, const float* y, const float* nrm, float* dn, long long n,
+                                 float coef) {
+    GRID_STRIDE(i, n) dn[i] = coef * g[i] * y[i] / nrm[i];
+}
+
+// ---------------------------------------------------------------- RNG
+__device__ __forceinline__ unsigned long long splitmix64(unsigned long long z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__global__ void uniform_noise_kernel(float* out, long long n, unsigned long long seed, unsigned long long off) {
+    GRID_STRIDE(i, n) {
+        unsigned long long h = splitmix64(seed ^ splitmix64(off + (unsigned long long)i));
+        float u = ((float)(h >> 40) + 0.5f) * (1.0f / 16777216.0f);  // (0,1)
+        out[i] = u - 0.5f;
+    }
+}
+
+// ---------------------------------------------------------------- reductions
+__device__ __forceinline__ float block_sum(float v, float* red) {
+    red[threadIdx.x] = v;
+    __syncthreads();
+    for (int k = blockDim.x / 2; k > 0; k >>= 1) {
+        if (threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+        __syncthreads();
+    }
+    float r = red[0];
+    __syncthreads();
+    return r;
+}
+__global__ void sum_log_kernel(const float* x, long long n, float* part) {
+    __shared__ float red[256];
+    float s = 0.f;
+    GRID_STRIDE(i, n) s += logf(x[i]);
+    float r = block_sum(s, red);
+    if (threadIdx.x == 0) part[blockIdx.x] = r;
+}
+__global__ void sum_sqdiff_kernel(const float* a, const float* b, long long n, float* part) {
+    __shared__ float red[256];
+    float s = 0.f;
+    GRID_STRIDE(i, n) {
+        float d = a[i] - b[i];
+        s += d * d;
+    }
+    float r = block_sum(s, red);
+    if (threadIdx.x == 0) part[blockIdx.x] = r;
+}
+__global__ void sumsq_kernel(const float* x, long long n, float* part) {
+    __shared__ float red[256];
+    float s = 0.f;
+    GRID_STRIDE(i, n) s += x[i] * x[i];
+    float r = block_sum(s, red);
+    if (threadIdx.x == 0) part[blockIdx.x] = r;
+}
+__global__ void scale_recip_kernel(const float* x, const float* coef, float scale, float* g, long long n) {
+    const float c = coef[0] * scale;
+    GRID_STRIDE(i, n) g[i] = c / x[i];
+}
+__global__ void scale_diff_kernel(const float* a, const float* b, const float* coef, float scale, float* g,
+                                  long long n) {
+    const float c = coef[0] * scale;
+    GRID_STRIDE(i, n) g[i] = c * (a[i] - b[i]);
+}
+__global__ void scale_kernel(const float* x, const float* coef, float scale, float* y, long long n, int acc) {
+    const float c = coef ? coef[0] * scale : scale;
+    GRID_STRIDE(i, n) {
+        float v = c * x[i];
+        y[i] = acc ? y[i] + v : v;
+    }
+}
+
+// ---------------------------------------------------------------- RateDistortionLoss scalars
+// sums = [sum log lik_y, sum log lik_z, sum (x_hat - x)^2]; out = [loss, bpp, residual_bpp, y_bpp, z_bpp, mse]
+struct RdOut {
+    float* o[6];
+};
+__global__ void rd_finalize_kernel(const float* sums, const float* jpeg_bpp, float lmbda, float npx, float nel,
+                                   RdOut out) {
+    if (threadIdx.x != 0) return;
+    const float den = -0.69314718055994531f * npx;  // -ln2 * num_pixels
+    const float yb = sums[0] / den, zb = sums[1] / den;
+    const float res = yb + zb;
+    const float bpp = res + (jpeg_bpp ? jpeg_bpp[0] : 0.f);
+    const float mse = sums[2] / nel * 65025.0f;
+    out.o[0][0] = lmbda * mse + bpp;
+    out.o[1][0] = bpp;
+    out.o[2][0] = res;
+    out.o[3][0] = yb;
+    out.o[4][0] = zb;
+    out.o[5][0] = mse;
+}
+// coef = [c_y, c_z, c_mse] with d/dlik_y = c_y / lik_y, d/dlik_z = c_z / lik_z, d/dx_hat = c_mse*(x_hat - x)
+__global__ void rd_bwd_coef_kernel(const float* g0, const float* g1, const float* g2, const float* g3,
+                                   const float* g4, const float* g5, float lmbda, float npx, float nel, float* coef) {
+    if (threadIdx.x != 0) return;
+    const float den = -0.69314718055994531f * npx;
+    const float gl = g0[0], gb = g1[0], gr = g2[0], gy = g3[0], gz = g4[0], gm = g5[0];
+    const float common = gl + gb + gr;
+    coef[0] = (common + gy) / den;
+    coef[1] = (common + gz) / den;
+    coef[2] = (lmbda * gl + gm) * 65025.0f * 2.0f / nel;
+}
+
+// ---------------------------------------------------------------- Adam (torch.optim.Adam, foreach math)
+__global__ void adam_kernel(float* p, const float* g, float* m, float* v, long long n, float lr, float b1,
+                            float b2, float eps, float bc1, float bc2_sqrt, const float* sumsq, float max_norm) {
+    float clip = 1.0f;
+    if (sumsq) {
+        float total = sqrtf(sumsq[0]);
+        float coef = max_norm / (total + 1e-6f);
+        clip = fminf(coef, 1.0f);
+    }
+    const float step_size = lr / bc1;
+    GRID_STRIDE(i, n) {
+        float gv = g[i] * clip;
+        float mv = m[i];
+        mv = mv + (1.0f - b1) * (gv - mv);  // lerp_(grad, 1-beta1)
+        float vv = v[i] * b2 + (1.0f - b2) * gv * gv;
+        m[i] = mv;
+        v[i] = vv;
+        float denom = sqrtf(vv) / bc2_sqrt + eps;
+        p[i] = p[i] - step_size * (mv / denom);
+    }
+}
+
+}  // namespace hyres
+
+using namespace hyres;
+
+extern "C" {
+
+int hyres_version(void) { return 10000; }
+const char* hyres_last_error_string(void) { return g_err.c_str(); }
+
+int hyres_nchw_to_nhwc(const float* x, float* y, int B, int C, int H, int W, int ldy, hyres_stream_t s) {
+    HY_REQUIRE(x && y && ldy >= C, HYRES_E_ARG, "nchw_to_nhwc: bad args");
+    long long n = (long long)B * C * H * W;
+    hipLaunchKernelGGL(nchw_to_nhwc_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(s), x, y, B, C, H, W, ldy);
+    return HY_LAUNCH_CHECK("nchw_to_nhwc");
+}
+int hyres_nhwc_to_nchw(const float* x, int ldx, float* y, int B, int C, int H, int W, hyres_stream_t s) {
+    HY_REQUIRE(x && y && ldx >= C, HYRES_E_ARG, "nhwc_to_nchw: bad args");
+    long long n = (long long)B * C * H * W;
+    hipLaunchKernelGGL(nhwc_to_nchw_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(s), x, ldx, y, B, C, H, W);
+    return HY_LAUNCH_CHECK("nhwc_to_nchw");
+}
+int hyres_axpby(const float* a, const float* b, float alpha, float* y, long long n, hyres_stream_t s) {
+    HY_REQUIRE(a && b && y, HYRES_E_ARG, "axpby: NULL");
+    hipLaunchKernelGGL(axpby_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(s), a, b, alpha, y, n);
+    return HY_LAUNCH_CHECK("axpby");
+}
+int hyres_add_clamp01(const float* x0, const float* r, float* y, long long n, hyres_stream_t s) {
+    HY_REQUIRE(x0 && r && y, HYRES_E_ARG, "add_clamp01: NULL");
+    hipLaunchKernelGGL(add_clamp01_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(s), x0, r, y, n);
+    return HY_LAUNCH_CHECK("add_clamp01");
+}
+int hyres_add_clamp01_bwd(const float* pre, const float* g, float* gx, int accumulate, long long n,
+                          hyres_stream_t s) {
+    HY_REQUIRE(pre && g && gx, HYRES_E_ARG, "add_clamp01_bwd: NULL");
+    hipLaunchKernelGGL(add_clamp01_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(s), pre, g, gx,
+                       accumulate, n);
+    return HY_LAUNCH_CHECK("add_clamp01_bwd");
+}
+int hyres_relu_bwd(const float* y, const float* g, float* gx, long long n, hyres_stream_t s) {
+    HY_REQUIRE(y && g && gx, HYRES_E_ARG, "relu_bwd: NULL");
+    hipLaunchKernelGGL(relu_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(s), y, g, gx, n);
+    return HY_LAUNCH_CHECK("relu_bwd");
+}
+int hyres_relu_bwd_2d(const float* y, int ldy, const float* g, int ldg, float* gx, int ldgx, long long P, int C,
+                      hyres_stream_t s) {
+    HY_REQUIRE(y && g && gx, HYRES_E_ARG, "relu_bwd_2d: NULL");
+    hipLaunchKernelGGL(relu_bwd_2d_kernel, dim3(grid_for(P * C)), dim3(256), 0, as_stream(s), y, ldy, g, ldg, gx,
+                       ldgx, P, C);
+    return HY_LAUNCH_CHECK("relu_bwd_2d");
+}
+long long hyres_reduce_workspace_bytes(long long n) { return (long long)grid_for(n, 4) * 4 + 256; }
+
+int hyres_prelu_bwd(const float* x, int ldx, const float* g, int ldg, float* gx, int ldgx, long long P, int C,
+                    const float* slope, float* dslope, void* ws, long long ws_bytes, hyres_stream_t s) {
+    HY_REQUIRE(x && g && gx && slope && dslope, HYRES_E_ARG, "prelu_bwd: NULL");
+    int nb = grid_for(P * C, 4);
+    HY_REQUIRE(ws && ws_bytes >= (long long)nb * 4, HYRES_E_WORKSPACE, "prelu_bwd: workspace");
+    hipLaunchKernelGGL(prelu_bwd_kernel, dim3(nb), dim3(256), 0, as_stream(s), x, ldx, g, ldg, gx, ldgx, P, C, slope,
+                       (float*)ws);
+    int rc = HY_LAUNCH_CHECK("prelu_bwd");
+    if (rc) return rc;
+    hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(256), 0, as_stream(s), (const float*)ws, nb, dslope, 1);
+    return HY_LAUNCH_CHECK("prelu_bwd_final");
+}
+int hyres_attn_gate_fwd(const float* a, const float* b, const float* x, float* out, long long n, hyres_stream_t s) {
+    HY_REQUIRE(a && b && x && out, HYRES_E_ARG, "attn_gate_fwd: NULL");
+    hipLaunchKernelGGL(attn_gate_fwd_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(s), a, b, x, out, n);
+    return HY_LAUNCH_CHECK("attn_gate_fwd");
+}
+int hyres_attn_gate_bwd(const float* a, const float* b, const float* g, float* ga, float* gb, long long n,
+                        hyres_stream_t s) {
+    HY_REQUIRE(a && b && g && ga && gb, HYRES_E_ARG, "attn_gate_bwd: NULL");
+    hipLaunchKernelGGL(attn_gate_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(s), a, b, g, ga, gb, n);
+    return HY_LAUNCH_CHECK("attn_gate_bwd");
+}
+int hyres_accumulate(const float* x, float* y, long long n, hyres_stream_t s) {
+    HY_REQUIRE(x && y, HYRES_E_ARG, "accumulate: NULL");
+    hipLaunchKernelGGL(accumulate_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(s), x, y, n);
+    return HY_LAUNCH_CHECK("accumulate");
+}
+int hyres_add2d(const float* x, int ldx, float* y, int ldy, long long P, int C, int accumulate,
+                hyres_stream_t s) {
+    HY_REQUIRE(x && y, HYRES_E_ARG, "add2d: NULL");
+    hipLaunchKernelGGL(add2d_kernel, dim3(grid_for(P * C)), dim3(256), 0, as_stream(s), x, ldx, y, ldy, P, C,
+                       accumulate);
+    return HY_LAUNCH_CHECK("add2d");
+}
+int hyres_mul(const float* a, const float* b, float* y, long long n, hyres_stream_t s) {
+    HY_REQUIRE(a && b && y, HYRES_E_ARG, "mul: NULL");
+    hipLaunchKernelGGL(mul_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(s), a, b, y, n);
+    return HY_LAUNCH_CHECK("mul");
+}
+int hyres_zero(void* p, long long bytes, hyres_stream_t s) {
+    HY_REQUIRE(p || bytes == 0, HYRES_E_ARG, "zero: NULL");
+    hipError_t e = hipMemsetAsync(p, 0, (size_t)bytes, as_stream(s));
+    if (e != hipSuccess) return set_error((int)e, "zero: %s", hipGetErrorString(e));
+    return ok();
+}
+int hyres_gdn_reparam_fwd(const float* beta, const float* gamma, float* bp, float* gp, int C, hyres_stream_t s) {
+    HY_REQUIRE(beta && gamma && bp && gp, HYRES_E_ARG, "gdn_reparam_fwd: NULL");
+    hipLaunchKernelGGL(gdn_reparam_fwd_kernel, dim3(grid_for((long long)C * C)), dim3(256), 0, as_stream(s), beta,
+                       gamma, bp, gp, C);
+    return HY_LAUNCH_CHECK("gdn_reparam_fwd");
+}
+int hyres_gdn_reparam_bwd(const float* beta, const float* gamma, const float* dbp, const float* dgp, float* db,
+                          float* dg, int C, int accumulate, hyres_stream_t s) {
+    HY_REQUIRE(beta && gamma && dbp && dgp && db && dg, HYRES_E_ARG, "gdn_reparam_bwd: NULL");
+    hipLaunchKernelGGL(gdn_reparam_bwd_kernel, dim3(grid_for((long long)C * C)), dim3(256), 0, as_stream(s), beta,
+                       gamma, dbp, dgp, db, dg, C, accumulate);
+    return HY_LAUNCH_CHECK("gdn_reparam_bwd");
+}
+int hyres_gdn_dnorm(const float* g, const float* y, const float* n, float* dn, long long P, int C, int inverse,
+                    hyres_stream_t s) {
+    HY_REQUIRE(g && y && n && dn, HYRES_E_ARG, "gdn_dnorm: NULL");
+    long long cnt = P * C;
+    hipLaunchKernelGGL(gdn_dnorm_kernel, dim3(grid_for(cnt)), dim3(256), 0, as_stream(s), g, y, n, dn, cnt,
+                       inverse ? 0.5f : -0.5f);
+    return HY_LAUNCH_CHECK("gdn_dnorm");
+}
+int hyres_uniform_noise(float* out, long long n, unsigned long long seed, unsigned long long offset,
+                        hyres_stream_t s) {
+    HY_REQUIRE(out, HYRES_E_ARG, "uniform_noise: NULL");
+    hipLaunchKernelGGL(uniform_noise_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(s), out, n, seed, offset);
+    return HY_LAUNCH_CHECK("uniform_noise");
+}
+
+static int reduce2(void (*k)(const float*, long long, float*), const float* x, long long n, float* out, void* ws,
+                   long long ws_bytes, hyres_stream_t s, const char* name) {
+    int nb = grid_for(n, 4);
+    HY_REQUIRE(ws && ws_bytes >= (long long)nb * 4, HYRES_E_WORKSPACE, "%s: workspace", name);
+    hipLaunchKernelGGL(k, dim3(nb), dim3(256), 0, as_stream(s), x, n, (float*)ws);
+    int rc = HY_LAUNCH_CHECK(name);
+    if (rc) return rc;
+    hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(256), 0, as_stream(s), (const float*)ws, nb, out, 0);
+    return HY_LAUNCH_CHECK(name);
+}
+int hyres_sum_log(const float* x, long long n, float* out, void* ws, long long ws_bytes, hyres_stream_t s) {
+    HY_REQUIRE(x && out, HYRES_E_ARG, "sum_log: NULL");
+    return reduce2(sum_log_kernel, x, n, out, ws, ws_bytes, s, "sum_log");
+}
+int hyres_sumsq(const float* x, long long n, float* out, void* ws, long long ws_bytes, hyres_stream_t s) {
+    HY_REQUIRE(x && out, HYRES_E_ARG, "sumsq: NULL");
+    return reduce2(sumsq_kernel, x, n, out, ws, ws_bytes, s, "sumsq");
+}
+int hyres_sum_sqdiff(const float* a, const float* b, long long n, float* out, void* ws, long long ws_bytes,
+                     hyres_stream_t s) {
+    HY_REQUIRE(a && b && out, HYRES_E_ARG, "sum_sqdiff: NULL");
+    int nb = grid_for(n, 4);
+    HY_REQUIRE(ws && ws_bytes >= (long long)nb * 4, HYRES_E_WORKSPACE, "sum_sqdiff: workspace");
+    hipLaunchKernelGGL(sum_sqdiff_kernel, dim3(nb), dim3(256), 0, as_stream(s), a, b, n, (float*)ws);
+    int rc = HY_LAUNCH_CHECK("sum_sqdiff");
+    if (rc) return rc;
+    hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(256), 0, as_stream(s), (const float*)ws, nb, out, 0);
+    return HY_LAUNCH_CHECK("sum_sqdiff_final");
+}
+int hyres_scale_recip(const float* x, const float* coef, float scale, float* g, long long n, hyres_stream_t s) {
+    HY_REQUIRE(x && coef && g, HYRES_E_ARG, "scale_recip: NULL");
+    hipLaunchKernelGGL(scale_recip_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(s), x, coef, scale, g, n);
+    return HY_LAUNCH_CHECK("scale_recip");
+}
+int hyres_scale_diff(const float* a, const float* b, const float* coef, float scale, float* g, long long n,
+                     hyres_stream_t s) {
+    HY_REQUIRE(a && b && coef && g, HYRES_E_ARG, "scale_diff: NULL");
+    hipLaunchKernelGGL(scale_diff_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(s), a, b, coef, scale, g, n);
+    return HY_LAUNCH_CHECK("scale_diff");
+}
+int hyres_scale(const float* x, const float* coef, float scale, float* y, long long n, int accumulate,
+                hyres_stream_t s) {
+    HY_REQUIRE(x && y, HYRES_E_ARG, "scale: NULL");
+    hipLaunchKernelGGL(scale_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(s), x, coef, scale, y, n, accumulate);
+    return HY_LAUNCH_CHECK("scale");
+}
+int hyres_rd_finalize(const float* sums, const float* jpeg_bpp, float lmbda, long long npx, long long nel,
+                      float* const* out, hyres_stream_t s) {
+    HY_REQUIRE(sums && out, HYRES_E_ARG, "rd_finalize: NULL");
+    RdOut o;
+    for (int i = 0; i < 6; ++i) {
+        HY_REQUIRE(out[i], HYRES_E_ARG, "rd_finalize: NULL output %d", i);
+        o.o[i] = out[i];
+    }
+    hipLaunchKernelGGL(rd_finalize_kernel, dim3(1), dim3(64), 0, as_stream(s), sums, jpeg_bpp, lmbda, (float)npx,
+                       (float)nel, o);
+    return HY_LAUNCH_CHECK("rd_finalize");
+}
+int hyres_rd_bwd_coef(const float* g0, const float* g1, const float* g2, const float* g3, const float* g4,
+                      const float* g5, float lmbda, long long npx, long long nel, float* coef, hyres_stream_t s) {
+    HY_REQUIRE(g0 && g1 && g2 && g3 && g4 && g5 && coef, HYRES_E_ARG, "rd_bwd_coef: NULL");
+    hipLaunchKernelGGL(rd_bwd_coef_kernel, dim3(1), dim3(64), 0, as_stream(s), g0, g1, g2, g3, g4, g5, lmbda,
+                       (float)npx, (float)nel, coef);
+    return HY_LAUNCH_CHECK("rd_bwd_coef");
+}
+int hyres_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, long long n, float lr,
+                    float beta1, float beta2, float eps, int step, const float* sumsq, float max_norm,
+                    hyres_stream_t s) {
+    HY_REQUIRE(param && grad && exp_avg && exp_avg_sq && step >= 1, HYRES_E_ARG, "adam: bad args");
+    double bc1 = 1.0 - std::pow((double)beta1, step);
+    double bc2 = 1.0 - std::pow((double)beta2, step);
+    hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n, 4)), dim3(256), 0, as_stream(s), param, grad, exp_avg,
+                       exp_avg_sq, n, lr, beta1, beta2, eps, (float)bc1, (float)std::sqrt(bc2), sumsq, max_norm);
+    return HY_LAUNCH_CHECK("adam");
+}
+
+}  // extern "C"

@@ -1,0 +1,478 @@
+// MultiScaleRefine pieces (models/layers/enhancement.py) on gfx950: bilinear resampling with
+// PyTorch's align_corners=False source-index rule, SEBlock, SpatialAttention (CBAM SA).
+// Activations are NHWC; every kernel streams HBM with the channel index on the fastest lanes.
+#include "common.h"
+
+namespace hyres {
+
+#define GRID_STRIDE(i, n) \
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < (n); i += (long long)gridDim.x * blockDim.x)
+
+static inline int grid_for_r(long long n) {
+    long long b = (n + 255) / 256;
+    return (int)std::max<long long>(1, std::min<long long>(b, 8192));
+}
+
+// torch area_pixel_compute_source_index (linear, align_corners=False): max(scale*(o+0.5)-0.5, 0)
+__device__ __forceinline__ void src_index(float scale, int o, int in, int& i0, int& i1, float& l0, float& l1) {
+    float src = scale * ((float)o + 0.5f) - 0.5f;
+    src = src < 0.f ? 0.f : src;
+    i0 = (int)src;
+    if (i0 > in - 1) i0 = in - 1;
+    i1 = i0 + ((i0 < in - 1) ? 1 : 0);
+    l1 = src - (float)i0;
+    l0 = 1.0f - l1;
+}
+
+__global__ void bilinear_fwd_kernel(const float* x, int ldx, float* y, int ldy, int B, int Hi, int Wi, int Ho,
+                                    int Wo, int C, float sh, float sw, int acc) {
+    const long long n = (long long)B * Ho * Wo * C;
+    GRID_STRIDE(i, n) {
+        const int c = (int)(i % C);
+        long long p = i / C;
+        const int ow = (int)(p % Wo);
+        const int oh = (int)((p / Wo) % Ho);
+        const int b = (int)(p / ((long long)Wo * Ho));
+        int h0, h1, w0, w1;
+        float lh0, lh1, lw0, lw1;
+        src_index(sh, oh, Hi, h0, h1, lh0, lh1);
+        src_index(sw, ow, Wi, w0, w1, lw0, lw1);
+        const float* xb = x + (long long)b * Hi * Wi * ldx + c;
+        float v00 = xb[((long long)h0 * Wi + w0) * ldx], v01 = xb[((long long)h0 * Wi + w1) * ldx];
+        float v10 = xb[((long long)h1 * Wi + w0) * ldx], v11 = xb[((long long)h1 * Wi + w1) * ldx];
+        float v = lh0 * (lw0 * v00 + lw1 * v01) + lh1 * (lw0 * v10 + lw1 * v11);
+        float* yp = y + p * ldy + c;
+        *yp = acc ? *yp + v : v;
+    }
+}
+
+// gather-form backward: for input pixel (h,w) sum over outputs whose stencil touches it
+__device__ __forceinline__ float bw_weight(float scale, int o, int in, int target) {
+    int i0, i1;
+    float l0, l1;
+    src_index(scale, o, in, i0, i1, l0, l1);
+    float w = 0.f;
+    if (i0 == target) w += l0;
+    if (i1 == target) w += l1;
+    return w;
+}
+
+__global__ void bilinear_bwd_kernel(const float* gy, int ldgy, float* gx, int ldgx, int B, int Hi, int Wi, int Ho,
+                                    int Wo, int C, float sh, float sw, int acc) {
+    const long long n = (long long)B * Hi * Wi * C;
+    const float ish = 1.0f / sh, isw = 1.0f / sw;
+    GRID_STRIDE(i, n) {
+        const int c = (int)(i % C);
+        long long p = i / C;
+        const int w = (int)(p % Wi);
+        const int h = (int)((p / Wi) % Hi);
+        const int b = (int)(p / ((long long)Wi * Hi));
+        // outputs o with src(o) in [t-1, t+1] : o in [(t-0.5)/s - 0.5, (t+1.5)/s - 0.5]
+        int oh_lo = max(0, (int)floorf(((float)h - 0.5f) * ish - 0.5f) - 1);
+        int oh_hi = min(Ho - 1, (int)ceilf(((float)h + 1.5f) * ish - 0.5f) + 1);
+        int ow_lo = max(0, (int)floorf(((float)w - 0.5f) * isw - 0.5f) - 1);
+        int ow_hi = min(Wo - 1, (int)ceilf(((float)w + 1.5f) * isw - 0.5f) + 1);
+        if (h == 0) oh_lo = 0;
+        if (w == 0) ow_lo = 0;
+        if (h == Hi - 1) oh_hi = Ho - 1;
+        if (w == Wi - 1) ow_hi = Wo - 1;
+        float s = 0.f;
+        const float* gb = gy + (long long)b * Ho * Wo * ldgy + c;
+        for (int oh = oh_lo; oh <= oh_hi; ++oh) {
+            float wh = bw_weight(sh, oh, Hi, h);
+            if (wh == 0.f) continue;
+            float rs = 0.f;
+            for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+                float ww = bw_weight(sw, ow, Wi, w);
+                if (ww == 0.f) continue;
+                rs += ww * gb[((long long)oh * Wo + ow) * ldgy];
+            }
+            s += wh * rs;
+        }
+        float* gp = gx + p * ldgx + c;
+        *gp = acc ? *gp + s : s;
+    }
+}
+
+// ---------------------------------------------------------------- SEBlock
+// pool partial: grid (B, nchunk), block 256: thread handles channels c = tid % C-ish
+__global__ void se_pool_kernel(const float* x, int HW, int C, int per, float* part) {
+    const int b = blockIdx.x, ch = blockIdx.y;
+    const int p0 = ch * per, p1 = min(HW, p0 + per);
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+        float s = 0.f;
+        for (int p = p0; p < p1; ++p) s += x[((long long)b * HW + p) * C + c];
+        part[((long long)b * gridDim.y + ch) * C + c] = s;
+    }
+}
+__global__ void se_fc_kernel(const float* part, int nch, const float* w1, const float* w2, float* pooled, float* hidden,
+                             float* sgate, int HW, int C, int Cr) {
+    const int b = blockIdx.x;
+    extern __shared__ float sm[];
+    float* pm = sm;        // [C]
+    float* hd = sm + C;    // [Cr]
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+        float s = 0.f;
+        for (int k = 0; k < nch; ++k) s += part[((long long)b * nch + k) * C + c];
+        float m = s / (float)HW;
+        pm[c] = m;
+        pooled[b * C + c] = m;
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < Cr; j += blockDim.x) {
+        float s = 0.f;
+        for (int c = 0; c < C; ++c) s += w1[j * C + c] * pm[c];
+        s = fmaxf(s, 0.f);
+        hd[j] = s;
+        hidden[b * Cr + j] = s;
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+        float s = 0.f;
+        for (int j = 0; j < Cr; ++j) s += w2[c * Cr + j] * hd[j];
+        sgate[b * C + c] = 1.0f / (1.0f + expf(-s));
+    }
+}
+__global__ void se_scale_kernel(const float* x, const float* sgate, float* y, int B, int HW, int C) {
+    const long long n = (long long)B * HW * C;
+    GRID_STRIDE(i, n) {
+        const int c = (int)(i % C);
+        const int b = (int)(i / ((long long)HW * C));
+        y[i] = x[i] * sgate[b * C + c];
+    }
+}
+// backward: partial sums of gy*x per (b,c)
+__global__ void se_bwd_pool_kernel(const float* x, const float* gy, int HW, int C, int per, float* part) {
+    const int b = blockIdx.x, ch = blockIdx.y;
+    const int p0 = ch * per, p1 = min(HW, p0 + per);
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+        float s = 0.f;
+        for (int p = p0; p < p1; ++p) {
+            long long i = ((long long)b * HW + p) * C + c;
+            s += gy[i] * x[i];
+        }
+        part[((long long)b * gridDim.y + ch) * C + c] = s;
+    }
+}
+// single block: all images (deterministic weight-gradient sums)
+__global__ void se_fc_bwd_kernel(const float* part, int nch, int B, const float* w1, const float* w2,
+                                 const float* pooled, const float* hidden, const float* sgate, float* gpool,
+                                 float* gw1, float* gw2, int HW, int C, int Cr) {
+    extern __shared__ float sm[];
+    float* ga2 = sm;              // [B*C]
+    float* gh = sm + B * C;       // [B*Cr]
+    for (int idx = threadIdx.x; idx < B * C; idx += blockDim.x) {
+        const int b = idx / C, c = idx % C;
+        float s = 0.f;
+        for (int k = 0; k < nch; ++k) s += part[((long long)b * nch + k) * C + c];
+        const float sg = sgate[idx];
+        ga2[idx] = s * sg * (1.0f - sg);
+    }
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < B * Cr; idx += blockDim.x) {
+        const int b = idx / Cr, j = idx % Cr;
+        float s = 0.f;
+        for (int c = 0; c < C; ++c) s += w2[c * Cr + j] * ga2[b * C + c];
+        gh[idx] = hidden[idx] > 0.f ? s : 0.f;
+    }
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < C * Cr; idx += blockDim.x) {
+        const int c = idx / Cr, j = idx % Cr;  // w2[c][j]
+        float s = 0.f;
+        for (int b = 0; b < B; ++b) s += ga2[b * C + c] * hidden[b * Cr + j];
+        gw2[idx] += s;
+    }
+    for (int idx = threadIdx.x; idx < Cr * C; idx += blockDim.x) {
+        const int j = idx / C, c = idx % C;  // w1[j][c]
+        float s = 0.f;
+        for (int b = 0; b < B; ++b) s += gh[b * Cr + j] * pooled[b * C + c];
+        gw1[idx] += s;
+    }
+    for (int idx = threadIdx.x; idx < B * C; idx += blockDim.x) {
+        const int b = idx / C, c = idx % C;
+        float s = 0.f;
+        for (int j = 0; j < Cr; ++j) s += w1[j * C + c] * gh[b * Cr + j];
+        gpool[idx] = s / (float)HW;
+    }
+}
+__global__ void se_bwd_x_kernel(const float* gy, const float* sgate, const float* gpool, float* gx, int B, int HW,
+                                int C) {
+    const long long n = (long long)B * HW * C;
+    GRID_STRIDE(i, n) {
+        const int c = (int)(i % C);
+        const int b = (int)(i / ((long long)HW * C));
+        gx[i] = gy[i] * sgate[b * C + c] + gpool[b * C + c];
+    }
+}
+
+// ---------------------------------------------------------------- SpatialAttention
+// one wave per pixel: mean and max over C channels (first-occurrence argmax kept implicit)
+__global__ void sa_pool_kernel(const float* x, float* pooled2, long long P, int C) {
+    const int lane = threadIdx.x & 63;
+    const long long p = (long long)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+    if (p >= P) return;
+    const float* xp = x + p * C;
+    float s = 0.f, m = -INFINITY;
+    for (int c = lane; c < C; c += 64) {
+        float v = xp[c];
+        s += v;
+        m = fmaxf(m, v);
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        s += __shfl_xor(s, off);
+        m = fmaxf(m, __shfl_xor(m, off));
+    }
+    if (lane == 0) {
+        pooled2[p * 2 + 0] = s / (float)C;
+        pooled2[p * 2 + 1] = m;
+    }
+}
+__global__ void sa_conv_kernel(const float* pooled2, const float* w, float* attn, int B, int H, int W) {
+    // 7x7, 2 -> 1, pad 3, no bias, then sigmoid. w: [1][2][7][7]
+    __shared__ float ws[98];
+    if (threadIdx.x < 98) ws[threadIdx.x] = w[threadIdx.x];
+    __syncthreads();
+    const long long n = (long long)B * H * W;
+    GRID_STRIDE(i, n) {
+        const int ww = (int)(i % W);
+        const int hh = (int)((i / W) % H);
+        const int b = (int)(i / ((long long)W * H));
+        float s = 0.f;
+        for (int ch = 0; ch < 2; ++ch)
+            for (int kh = 0; kh < 7; ++kh) {
+                int ih = hh + kh - 3;
+                if (ih < 0 || ih >= H) continue;
+                for (int kw = 0; kw < 7; ++kw) {
+                    int iw = ww + kw - 3;
+                    if (iw < 0 || iw >= W) continue;
+                    s += ws[ch * 49 + kh * 7 + kw] * pooled2[(((long long)b * H + ih) * W + iw) * 2 + ch];
+                }
+            }
+        attn[i] = 1.0f / (1.0f + expf(-s));
+    }
+}
+__global__ void sa_mul_kernel(const float* x, const float* attn, float* y, long long P, int C) {
+    const long long n = P * C;
+    GRID_STRIDE(i, n) y[i] = x[i] * attn[i / C];
+}
+// bwd 1: g_logit[p] = (sum_c gy*x) * a*(1-a)
+__global__ void sa_bwd_logit_kernel(const float* x, const float* gy, const float* attn, float* glogit, long long P,
+                                    int C) {
+    const int lane = threadIdx.x & 63;
+    const long long p = (long long)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+    if (p >= P) return;
+    float s = 0.f;
+    for (int c = lane; c < C; c += 64) s += gy[p * C + c] * x[p * C + c];
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+    if (lane == 0) {
+        float a = attn[p];
+        glogit[p] = s * a * (1.0f - a);
+    }
+}
+// bwd 2: g_pooled2 = transpose conv; weight-grad partials per block
+__global__ void sa_bwd_conv_kernel(const float* glogit, const float* pooled2, const float* w, float* gpooled2,
+                                   float* wpart, int B, int H, int W) {
+    __shared__ float ws[98];
+    __shared__ float red[256];
+    if (threadIdx.x < 98) ws[threadIdx.x] = w[threadIdx.x];
+    __syncthreads();
+    const long long n = (long long)B * H * W;
+    float gw[98];
+#pragma unroll
+    for (int k = 0; k < 98; ++k) gw[k] = 0.f;
+    GRID_STRIDE(i, n) {
+        const int ww = (int)(i % W);
+        const int hh = (int)((i / W) % H);
+        const int b = (int)(i / ((long long)W * H));
+        float g0 = 0.f, g1 = 0.f;
+        const float gl = glogit[i];
+#pragma unroll
+        for (int kh = 0; kh < 7; ++kh) {
+#pragma unroll
+            for (int kw = 0; kw < 7; ++kw) {
+                // input-gradient: output (hh - kh + 3, ww - kw + 3) used input (hh, ww) with tap (kh,kw)
+                int oh = hh - kh + 3, ow = ww - kw + 3;
+                if (oh >= 0 && oh < H && ow >= 0 && ow < W) {
+                    float go = glogit[((long long)b * H + oh) * W + ow];
+                    g0 += ws[kh * 7 + kw] * go;
+                    g1 += ws[49 + kh * 7 + kw] * go;
+                }
+                // weight-gradient: this output pixel i times input (hh + kh - 3, ww + kw - 3)
+                int ih = hh + kh - 3, iw = ww + kw - 3;
+                if (ih >= 0 && ih < H && iw >= 0 && iw < W) {
+                    const float* pp = pooled2 + (((long long)b * H + ih) * W + iw) * 2;
+                    gw[kh * 7 + kw] += gl * pp[0];
+                    gw[49 + kh * 7 + kw] += gl * pp[1];
+                }
+            }
+        }
+        gpooled2[i * 2 + 0] = g0;
+        gpooled2[i * 2 + 1] = g1;
+    }
+    for (int k = 0; k < 98; ++k) {
+        red[threadIdx.x] = gw[k];
+        __syncthreads();
+        for (int s = 128; s > 0; s >>= 1) {
+            if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) wpart[(long long)blockIdx.x * 98 + k] = red[0];
+        __syncthreads();
+    }
+}
+__global__ void sa_bwd_wfinal_kernel(const float* wpart, int nb, float* gw) {
+    const int k = threadIdx.x;
+    if (k >= 98) return;
+    float s = 0.f;
+    for (int b = 0; b < nb; ++b) s += wpart[(long long)b * 98 + k];
+    gw[k] += s;
+}
+// bwd 3: gx = gy*a + g_avg/C + [c == argmax] * g_max     (one wave per pixel)
+__global__ void sa_bwd_x_kernel(const float* x, const float* gy, const float* attn, const float* gpooled2, float* gx,
+                                long long P, int C) {
+    const int lane = threadIdx.x & 63;
+    const long long p = (long long)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+    if (p >= P) return;
+    const float* xp = x + p * C;
+    // argmax (first occurrence, as torch.max(dim) on CPU)
+    float m = -INFINITY;
+    int mi = 0x7fffffff;
+    for (int c = lane; c < C; c += 64) {
+        float v = xp[c];
+        if (v > m) { m = v; mi = c; }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        float om = __shfl_xor(m, off);
+        int oi = __shfl_xor(mi, off);
+        if (om > m || (om == m && oi < mi)) { m = om; mi = oi; }
+    }
+    const float a = attn[p];
+    const float gavg = gpooled2[p * 2 + 0] / (float)C;
+    const float gmax = gpooled2[p * 2 + 1];
+    for (int c = lane; c < C; c += 64) {
+        float v = gy[p * C + c] * a + gavg;
+        if (c == mi) v += gmax;
+        gx[p * C + c] = v;
+    }
+}
+
+}  // namespace hyres
+
+using namespace hyres;
+
+extern "C" {
+
+int hyres_bilinear_fwd(const float* x, int ldx, float* y, int ldy, int B, int Hi, int Wi, int Ho, int Wo, int C,
+                       float scale_h, float scale_w, int accumulate, hyres_stream_t s) {
+    HY_REQUIRE(x && y && Hi > 0 && Wi > 0 && Ho > 0 && Wo > 0, HYRES_E_ARG, "bilinear_fwd: bad args");
+    long long n = (long long)B * Ho * Wo * C;
+    hipLaunchKernelGGL(bilinear_fwd_kernel, dim3(grid_for_r(n)), dim3(256), 0, as_stream(s), x, ldx, y, ldy, B, Hi,
+                       Wi, Ho, Wo, C, scale_h, scale_w, accumulate);
+    return HY_LAUNCH_CHECK("bilinear_fwd");
+}
+int hyres_bilinear_bwd(const float* gy, int ldgy, float* gx, int ldgx, int B, int Hi, int Wi, int Ho, int Wo, int C,
+                       float scale_h, float scale_w, int accumulate, hyres_stream_t s) {
+    HY_REQUIRE(gy && gx, HYRES_E_ARG, "bilinear_bwd: NULL");
+    long long n = (long long)B * Hi * Wi * C;
+    hipLaunchKernelGGL(bilinear_bwd_kernel, dim3(grid_for_r(n)), dim3(256), 0, as_stream(s), gy, ldgy, gx, ldgx, B,
+                       Hi, Wi, Ho, Wo, C, scale_h, scale_w, accumulate);
+    return HY_LAUNCH_CHECK("bilinear_bwd");
+}
+
+static int se_chunks(int HW) { return std::max(1, std::min(64, (HW + 1023) / 1024)); }
+
+long long hyres_se_workspace_bytes(int B, int HW, int C) { return (long long)B * se_chunks(HW) * C * 4; }
+
+int hyres_se_fwd(const float* x, const float* w1, const float* w2, float* y, float* pooled, float* hidden,
+                 float* sgate, int B, int HW, int C, int Cr, void* ws, long long ws_bytes, hyres_stream_t s) {
+    HY_REQUIRE(x && w1 && w2 && y && pooled && hidden && sgate, HYRES_E_ARG, "se_fwd: NULL");
+    const int nch = se_chunks(HW);
+    HY_REQUIRE(ws && ws_bytes >= (long long)B * nch * C * 4, HYRES_E_WORKSPACE, "se_fwd: workspace");
+    const int per = (HW + nch - 1) / nch;
+    hipStream_t st = as_stream(s);
+    hipLaunchKernelGGL(se_pool_kernel, dim3(B, nch), dim3(256), 0, st, x, HW, C, per, (float*)ws);
+    int rc = HY_LAUNCH_CHECK("se_pool");
+    if (rc) return rc;
+    hipLaunchKernelGGL(se_fc_kernel, dim3(B), dim3(256), (C + Cr) * 4, st, (const float*)ws, nch, w1, w2, pooled,
+                       hidden, sgate, HW, C, Cr);
+    rc = HY_LAUNCH_CHECK("se_fc");
+    if (rc) return rc;
+    long long n = (long long)B * HW * C;
+    hipLaunchKernelGGL(se_scale_kernel, dim3(grid_for_r(n)), dim3(256), 0, st, x, (const float*)sgate, y, B, HW, C);
+    return HY_LAUNCH_CHECK("se_scale");
+}
+
+int hyres_se_bwd(const float* x, const float* gy, const float* w1, const float* w2, const float* pooled,
+                 const float* hidden, const float* sgate, float* gx, float* gw1, float* gw2, int B, int HW, int C,
+                 int Cr, void* ws, long long ws_bytes, hyres_stream_t s) {
+    HY_REQUIRE(x && gy && w1 && w2 && pooled && hidden && sgate && gx && gw1 && gw2, HYRES_E_ARG, "se_bwd: NULL");
+    const int nch = se_chunks(HW);
+    const long long need = (long long)B * nch * C * 4 + (long long)B * C * 4;
+    HY_REQUIRE(ws && ws_bytes >= need, HYRES_E_WORKSPACE, "se_bwd: workspace");
+    HY_REQUIRE((long long)B * (C + Cr) * 4 <= 60000, HYRES_E_SHAPE, "se_bwd: batch too large for LDS");
+    const int per = (HW + nch - 1) / nch;
+    float* part = (float*)ws;
+    float* gpool = part + (long long)B * nch * C;
+    hipStream_t st = as_stream(s);
+    hipLaunchKernelGGL(se_bwd_pool_kernel, dim3(B, nch), dim3(256), 0, st, x, gy, HW, C, per, part);
+    int rc = HY_LAUNCH_CHECK("se_bwd_pool");
+    if (rc) return rc;
+    hipLaunchKernelGGL(se_fc_bwd_kernel, dim3(1), dim3(256), (size_t)B * (C + Cr) * 4, st, (const float*)part, nch, B,
+                       w1, w2, pooled, hidden, sgate, gpool, gw1, gw2, HW, C, Cr);
+    rc = HY_LAUNCH_CHECK("se_fc_bwd");
+    if (rc) return rc;
+    long long n = (long long)B * HW * C;
+    hipLaunchKernelGGL(se_bwd_x_kernel, dim3(grid_for_r(n)), dim3(256), 0, st, gy, sgate, (const float*)gpool, gx, B,
+                       HW, C);
+    return HY_LAUNCH_CHECK("se_bwd_x");
+}
+
+long long hyres_spatial_attn_workspace_bytes(int B, int H, int W) {
+    long long n = (long long)B * H * W;
+    int nb = grid_for_r(n);
+    return (long long)nb * 98 * 4 + n * 4 + n * 2 * 4 + 1024;
+}
+
+int hyres_spatial_attn_fwd(const float* x, const float* w, float* pooled2, float* attn, float* y, int B, int H, int W,
+                           int C, hyres_stream_t s) {
+    HY_REQUIRE(x && w && pooled2 && attn && y, HYRES_E_ARG, "spatial_attn_fwd: NULL");
+    long long P = (long long)B * H * W;
+    hipStream_t st = as_stream(s);
+    hipLaunchKernelGGL(sa_pool_kernel, dim3((unsigned)((P + 3) / 4)), dim3(256), 0, st, x, pooled2, P, C);
+    int rc = HY_LAUNCH_CHECK("sa_pool");
+    if (rc) return rc;
+    hipLaunchKernelGGL(sa_conv_kernel, dim3(grid_for_r(P)), dim3(256), 0, st, (const float*)pooled2, w, attn, B, H, W);
+    rc = HY_LAUNCH_CHECK("sa_conv");
+    if (rc) return rc;
+    hipLaunchKernelGGL(sa_mul_kernel, dim3(grid_for_r(P * C)), dim3(256), 0, st, x, (const float*)attn, y, P, C);
+    return HY_LAUNCH_CHECK("sa_mul");
+}
+
+int hyres_spatial_attn_bwd(const float* x, const float* w, const float* pooled2, const float* attn, const float* gy,
+                           float* gx, float* gw, int B, int H, int W, int C, void* ws, long long ws_bytes,
+                           hyres_stream_t s) {
+    HY_REQUIRE(x && w && pooled2 && attn && gy && gx && gw, HYRES_E_ARG, "spatial_attn_bwd: NULL");
+    long long P = (long long)B * H * W;
+    HY_REQUIRE(ws && ws_bytes >= hyres_spatial_attn_workspace_bytes(B, H, W), HYRES_E_WORKSPACE,
+               "spatial_attn_bwd: workspace");
+    float* glogit = (float*)ws;
+    float* gp2 = glogit + P;
+    float* wpart = gp2 + 2 * P;
+    hipStream_t st = as_stream(s);
+    hipLaunchKernelGGL(sa_bwd_logit_kernel, dim3((unsigned)((P + 3) / 4)), dim3(256), 0, st, x, gy, attn, glogit, P, C);
+    int rc = HY_LAUNCH_CHECK("sa_bwd_logit");
+    if (rc) return rc;
+    int nb = grid_for_r(P);
+    hipLaunchKernelGGL(sa_bwd_conv_kernel, dim3(nb), dim3(256), 0, st, (const float*)glogit, pooled2, w, gp2, wpart, B,
+                       H, W);
+    rc = HY_LAUNCH_CHECK("sa_bwd_conv");
+    if (rc) return rc;
+    hipLaunchKernelGGL(sa_bwd_wfinal_kernel, dim3(1), dim3(128), 0, st, (const float*)wpart, nb, gw);
+    rc = HY_LAUNCH_CHECK("sa_bwd_wfinal");
+    if (rc) return rc;
+    hipLaunchKernelGGL(sa_bwd_x_kernel, dim3((unsigned)((P + 3) / 4)), dim3(256), 0, st, x, gy, attn,
+                       (const float*)gp2, gx, P, C);
+    return HY_LAUNCH_CHECK("sa_bwd_x");
+}
+
+}  // extern "C"

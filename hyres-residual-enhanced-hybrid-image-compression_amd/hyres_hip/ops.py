@@ -1,0 +1,524 @@
+"""HIP op library for the HyRES hot path: NHWC activation nodes, a reverse-mode tape, and one
+function per reference operation, each launching libhyres_hip kernels on torch's current stream.
+
+Design (MI355X-first, not a port):
+  * activations live in HBM as NHWC fp32 (``Node``: a [B,H,W,C] view whose channel slice may sit
+    inside a wider buffer — concatenations are free, producers write straight into the slice);
+  * the forward pass records backward closures on a ``Tape``; backward replays them in reverse and
+    launches the dgrad / wgrad / elementwise-backward kernels itself (no torch autograd kernels, no
+    torch compute kernels: torch only allocates memory and supplies the stream);
+  * parameter gradients are accumulated straight into ``param.grad`` by the HIP wgrad kernels.
+
+Reference anchors are given per op; the math restated here is checked stage-by-stage against the
+CPU oracle (oracle/hyres_oracle.py) in tests/test_parity_gpu.py.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Callable, List, Optional
+
+import torch
+
+from . import _lib as L
+
+# --------------------------------------------------------------------------------------------------
+# infrastructure
+# --------------------------------------------------------------------------------------------------
+_WEIGHT_EPOCH = [0]
+
+
+def bump_weight_epoch() -> None:
+    """Invalidate cached weight re-layouts (called after optimiser steps / state loads)."""
+    _WEIGHT_EPOCH[0] += 1
+
+
+class Workspace:
+    """Per-device scratch buffer, grown on demand; stream-ordered reuse is safe because every op
+    finishes with its scratch before the next op's kernels start on the same stream."""
+
+    _bufs = {}
+
+    @classmethod
+    def get(cls, nbytes: int, device: torch.device, slot: int = 0) -> torch.Tensor:
+        key = (device.index, slot)
+        buf = cls._bufs.get(key)
+        if buf is None or buf.numel() < nbytes:
+            n = max(int(nbytes), 1 << 20)
+            if buf is not None:
+                n = max(n, int(buf.numel() * 1.5))
+            buf = torch.empty(n, dtype=torch.uint8, device=device)
+            cls._bufs[key] = buf
+        return buf
+
+
+def _empty(shape, device) -> torch.Tensor:
+    return torch.empty(shape, dtype=torch.float32, device=device)
+
+
+def zero_(t: torch.Tensor) -> torch.Tensor:
+    L.call("hyres_zero", t.data_ptr(), t.numel() * t.element_size(), L.stream())
+    return t
+
+
+def zeros(shape, device) -> torch.Tensor:
+    return zero_(_empty(shape, device))
+
+
+class Node:
+    """NHWC activation [B,H,W,C]; ``v`` may be a channel slice of a wider buffer (pixel stride ld)."""
+
+    __slots__ = ("v", "B", "H", "W", "C", "ld", "rg", "parent", "c0", "_g", "gflag")
+
+    def __init__(self, v: torch.Tensor, rg: bool = True, parent: "Node" = None, c0: int = 0):
+        assert v.dim() == 4 and v.stride(3) == 1, "Node expects an NHWC tensor with unit channel stride"
+        self.v = v
+        self.B, self.H, self.W, self.C = v.shape
+        self.ld = v.stride(2)
+        assert v.stride(1) == self.W * self.ld and v.stride(0) == self.H * self.W * self.ld
+        self.rg = rg
+        self.parent = parent
+        self.c0 = c0
+        self._g = None
+        self.gflag = False
+
+    @staticmethod
+    def new(B, H, W, C, device, rg=True) -> "Node":
+        return Node(_empty((B, H, W, C), device), rg)
+
+    def slice(self, c0: int, c1: int, rg: Optional[bool] = None) -> "Node":
+        return Node(self.v[..., c0:c1], self.rg if rg is None else rg, parent=self, c0=c0)
+
+    @property
+    def P(self) -> int:
+        return self.B * self.H * self.W
+
+    @property
+    def device(self):
+        return self.v.device
+
+    @property
+    def contiguous(self) -> bool:
+        return self.ld == self.C
+
+    def ptr(self) -> int:
+        return self.v.data_ptr()
+
+    # ---- gradients
+    def grad(self) -> Optional[torch.Tensor]:
+        """The accumulated gradient (same view structure as v) or None if nothing flowed here."""
+        if self.parent is not None:
+            pg = self.parent.grad()
+            return None if pg is None else pg[..., self.c0:self.c0 + self.C]
+        return self._g if self.gflag else None
+
+    def grad_ld(self) -> int:
+        return self.parent.grad_ld() if self.parent is not None else self.C
+
+    def grad_target(self):
+        """(tensor, accumulate) for a kernel that adds its contribution to this node's gradient."""
+        if self.parent is not None:
+            pg, _ = self.parent._zeroed_grad()
+            return pg[..., self.c0:self.c0 + self.C], 1
+        if self._g is None:
+            self._g = _empty(self.v.shape, self.v.device)
+        acc = 1 if self.gflag else 0
+        self.gflag = True
+        return self._g, acc
+
+    def _zeroed_grad(self):
+        if self._g is None:
+            self._g = zeros(self.v.shape, self.v.device)
+            self.gflag = True
+        elif not self.gflag:
+            zero_(self._g)
+            self.gflag = True
+        return self._g, 1
+
+    def set_grad(self, g: torch.Tensor) -> None:
+        """Seed this node's gradient (accumulating if already present)."""
+        tgt, acc = self.grad_target()
+        L.call("hyres_add2d", g.data_ptr(), g.stride(2), tgt.data_ptr(), tgt.stride(2), self.P, self.C,
+               acc, L.stream())
+
+
+class Tape:
+    """Reverse-mode tape of backward closures over HIP launches."""
+
+    def __init__(self):
+        self.ops: List[Callable[[], None]] = []
+        self.param_hooks: List[Callable[[], None]] = []
+
+    def push(self, fn: Callable[[], None]) -> None:
+        self.ops.append(fn)
+
+    def backward(self) -> None:
+        for fn in reversed(self.ops):
+            fn()
+        self.ops.clear()
+
+
+def param_grad(p: torch.nn.Parameter) -> torch.Tensor:
+    """param.grad, created zeroed if absent; HIP kernels always accumulate into it."""
+    if p.grad is None:
+        p.grad = zeros(p.shape, p.device)
+    return p.grad
+
+
+def wants_grad(p: Optional[torch.Tensor]) -> bool:
+    return p is not None and p.requires_grad
+
+
+# --------------------------------------------------------------------------------------------------
+# weight re-layout cache
+# --------------------------------------------------------------------------------------------------
+def _prepped(weight: torch.Tensor, geom: L.ConvGeom, mode: int, Ci: int, Co: int, KH: int, KW: int,
+             pad: int, mask: Optional[torch.Tensor] = None, key_extra=()) -> torch.Tensor:
+    rows = Co if mode in (L.WPREP_CONV, L.WPREP_DECONV) else Ci
+    cols = Ci if mode in (L.WPREP_CONV, L.WPREP_DECONV) else Co
+    if mask is not None:  # masked weights are re-laid-out every call (the mask is applied on the fly)
+        buf = _empty((rows, geom.ntaps * cols), weight.device)
+        L.call("hyres_conv_weight_prep", ctypes.byref(geom), weight.data_ptr(), buf.data_ptr(), mode, Ci, Co,
+               KH, KW, pad, mask.data_ptr(), L.stream())
+        return buf
+    key = (mode, geom.nphase, geom.ntaps) + tuple(key_extra)
+    cache = getattr(weight, "_hyres_prep", None)
+    if cache is None:
+        cache = {}
+        try:
+            weight._hyres_prep = cache
+        except Exception:
+            pass
+    stamp = (weight.data_ptr(), weight._version, _WEIGHT_EPOCH[0])
+    ent = cache.get(key)
+    if ent is not None and ent[0] == stamp:
+        return ent[1]
+    buf = ent[1] if ent is not None else _empty((rows, geom.ntaps * cols), weight.device)
+    L.call("hyres_conv_weight_prep", ctypes.byref(geom), weight.data_ptr(), buf.data_ptr(), mode, Ci, Co,
+           KH, KW, pad, None, L.stream())
+    cache[key] = (stamp, buf)
+    return buf
+
+
+def _ws(nbytes: int, device, slot=0) -> torch.Tensor:
+    return Workspace.get(int(nbytes), device, slot)
+
+
+def _geom(fn: str, *args) -> L.ConvGeom:
+    g = L.ConvGeom()
+    L.call(fn, ctypes.byref(g), *[int(a) for a in args])
+    return g
+
+
+class KernelTimer:
+    """Optional HIP-event timing of the dominant kernel (conv_fwd_kernel<2,2,2,2,0>: Co > 64,
+    Ci % 32 == 0, no square prologue) with its algorithmic FLOPs, for bench.py's roofline line."""
+
+    enabled = False
+    events: list = []
+
+    @classmethod
+    def reset(cls):
+        cls.events = []
+
+    @classmethod
+    def summary(cls):
+        torch.cuda.synchronize()
+        ms = sum(a.elapsed_time(b) for a, b, _ in cls.events)
+        flops = sum(f for _, _, f in cls.events)
+        n = len(cls.events)
+        return {"launches": n, "total_ms": ms, "avg_us": 1000.0 * ms / max(n, 1), "flops": flops,
+                "flops_per_launch": flops / max(n, 1)}
+
+
+def conv_flops(g: L.ConvGeom) -> float:
+    taps = sum(g.ntap[p] for p in range(g.nphase))
+    return 2.0 * g.B * g.Hq * g.Wq * taps * g.Ci * g.Co
+
+
+def _launch_conv(g: L.ConvGeom, x_ptr: int, w2: torch.Tensor, ldw: int, y_ptr: int, e: L.Epilogue) -> None:
+    timed = KernelTimer.enabled and g.Co > 64 and g.Ci % 32 == 0 and not e.square_input
+    if timed:
+        s0 = torch.cuda.Event(enable_timing=True)
+        s1 = torch.cuda.Event(enable_timing=True)
+        s0.record()
+    L.call("hyres_conv_forward", ctypes.byref(g), x_ptr, w2.data_ptr(), ldw, y_ptr, ctypes.byref(e), L.stream())
+    if timed:
+        s1.record()
+        KernelTimer.events.append((s0, s1, conv_flops(g)))
+
+
+def _colsum_into(g: torch.Tensor, P: int, C: int, ld: int, dst: torch.Tensor, acc: int = 1) -> None:
+    ws = _ws(L.load().hyres_colsum_workspace_bytes(P, C), g.device, slot=1)
+    L.call("hyres_colsum", g.data_ptr(), P, C, ld, dst.data_ptr(), acc, ws.data_ptr(), ws.numel(), L.stream())
+
+
+def _wgrad(desc: L.WgradDesc, p_ptr: int, q_ptr: int, dst: torch.Tensor, device) -> None:
+    nbytes = L.load().hyres_wgrad_workspace_bytes(ctypes.byref(desc))
+    ws = _ws(nbytes, device, slot=2)
+    L.call("hyres_conv_wgrad", ctypes.byref(desc), p_ptr, q_ptr, dst.data_ptr(), ws.data_ptr(), ws.numel(),
+           L.stream())
+
+
+def _act_backward(y: Node, gy: torch.Tensor, gy_ld: int, act: int, pre: Optional[torch.Tensor],
+                  slope: Optional[torch.Tensor]):
+    """Gradient wrt the pre-activation (contiguous [P,C] buffer or the incoming view)."""
+    if act == L.ACT_NONE:
+        return gy, gy_ld
+    gp = _empty((y.B, y.H, y.W, y.C), y.device)
+    if act == L.ACT_RELU:
+        L.call("hyres_relu_bwd_2d", y.ptr(), y.ld, gy.data_ptr(), gy_ld, gp.data_ptr(), y.C, y.P, y.C,
+               L.stream())
+    else:
+        ws = _ws(L.load().hyres_reduce_workspace_bytes(y.P * y.C), y.device, slot=1)
+        dslope = param_grad(slope) if slope.requires_grad else _empty((1,), y.device)
+        L.call("hyres_prelu_bwd", pre.data_ptr(), y.C, gy.data_ptr(), gy_ld, gp.data_ptr(), y.C, y.P, y.C,
+               slope.data_ptr(), dslope.data_ptr(), ws.data_ptr(), ws.numel(), L.stream())
+    return gp, y.C
+
+
+# --------------------------------------------------------------------------------------------------
+# convolutions
+# --------------------------------------------------------------------------------------------------
+def conv2d(tape: Optional[Tape], x: Node, weight: torch.Tensor, bias: Optional[torch.Tensor], stride=1,
+           pad=0, dil=1, act=L.ACT_NONE, slope=None, res: Optional[Node] = None, out: Optional[Node] = None,
+           mask: Optional[torch.Tensor] = None) -> Node:
+    """nn.Conv2d (+ fused bias / residual / ReLU / PReLU epilogue), NHWC, on MFMA.
+
+    Reference call sites: models/layers/common.py:4-11, compressai conv() (k5 s2 p2),
+    models/layers/enhancement.py:44-51 (dilated 3x3), :65-82; ResidualUnit's ``out += identity; relu``
+    (models/layers/attention.py:26-29) and RBB's ``out + identity`` are the fused residual epilogue.
+    ``mask`` implements CheckboardMaskedConv2d's weight masking (models/layers/checkerboard.py:46-47).
+    A 1x1 conv may read only the first x.C of the weight's input channels (param_aggregation on
+    ``cat([latent_params, zeros])``, models/checkerboard.py:115-117: the zero half contributes nothing)."""
+    Co, Ci_w, KH, KW = weight.shape
+    Ci = x.C
+    assert Ci == Ci_w or (KH == 1 and KW == 1 and Ci < Ci_w and mask is None), (Ci_w, x.C)
+    B, H, W = x.B, x.H, x.W
+    Ho = (H + 2 * pad - dil * (KH - 1) - 1) // stride + 1
+    Wo = (W + 2 * pad - dil * (KW - 1) - 1) // stride + 1
+    y = out if out is not None else Node.new(B, Ho, Wo, Co, x.device)
+    assert (y.B, y.H, y.W, y.C) == (B, Ho, Wo, Co), ((y.B, y.H, y.W, y.C), (B, Ho, Wo, Co))
+    g = _geom("hyres_geom_conv2d", B, H, W, Ci, x.ld, Co, y.ld, KH, KW, stride, pad, dil)
+    if KH == 1 and KW == 1 and mask is None:
+        w2, ldw = weight, Ci_w  # OIHW == OHWI for 1x1
+    else:
+        w2, ldw = _prepped(weight, g, L.WPREP_CONV, Ci, Co, KH, KW, pad, mask), g.ntaps * Ci
+    e = L.Epilogue()
+    e.kind = L.EPI_BIAS
+    e.act = act
+    e.bias = L.ptr(bias)
+    if res is not None:
+        assert (res.B, res.H, res.W, res.C) == (B, Ho, Wo, Co)
+        e.res = res.ptr()
+        e.ldres = res.ld
+    pre = None
+    if act == L.ACT_PRELU:
+        e.slope = slope.data_ptr()
+        if tape is not None:
+            pre = _empty((B, Ho, Wo, Co), x.device)
+            e.out2 = pre.data_ptr()
+            e.ldo2 = Co
+    _launch_conv(g, x.ptr(), w2, ldw, y.ptr(), e)
+    if tape is None:
+        return y
+
+    def bwd():
+        gy = y.grad()
+        if gy is None:
+            return
+        gp, gpld = _act_backward(y, gy, y.grad_ld(), act, pre, slope)
+        P = y.P
+        if res is not None and res.rg:
+            tgt, acc = res.grad_target()
+            L.call("hyres_add2d", gp.data_ptr(), gpld, tgt.data_ptr(), res.grad_ld(), P, Co, acc, L.stream())
+        if wants_grad(bias):
+            _colsum_into(gp, P, Co, gpld, param_grad(bias))
+        if wants_grad(weight):
+            d = L.WgradDesc()
+            L.call("hyres_wgrad_desc_conv2d", ctypes.byref(d), B, H, W, Ci, x.ld, Co, gpld, KH, KW, stride,
+                   pad, dil)
+            d.sm = Ci_w * KH * KW
+            d.accumulate = 1
+            _wgrad(d, gp.data_ptr(), x.ptr(), param_grad(weight), x.device)
+        if x.rg:
+            tgt, acc = x.grad_target()
+            gd = _geom("hyres_geom_conv2d_dgrad", B, H, W, Ci, x.grad_ld(), Co, gpld, KH, KW, stride, pad, dil)
+            w2d = _prepped(weight, gd, L.WPREP_CONV_DGRAD, Ci_w, Co, KH, KW, pad, mask)
+            ed = L.Epilogue()
+            ed.kind = L.EPI_BIAS
+            ed.accumulate = acc
+            _launch_conv(gd, gp.data_ptr(), w2d, gd.ntaps * Co, tgt.data_ptr(), ed)
+
+    tape.push(bwd)
+    return y
+
+
+def deconv2d(tape: Optional[Tape], x: Node, weight: torch.Tensor, bias: Optional[torch.Tensor], act=L.ACT_NONE,
+             out: Optional[Node] = None) -> Node:
+    """compressai deconv(): nn.ConvTranspose2d(k5, s2, p2, output_padding=1) as 4 sub-pixel phases.
+
+    Reference call sites: models/checkerboard.py:50,53,57 (g_s) and :70,72 (h_s)."""
+    Ci, Co, K, _ = weight.shape
+    assert Ci == x.C
+    pad = K // 2
+    B, H, W = x.B, x.H, x.W
+    y = out if out is not None else Node.new(B, 2 * H, 2 * W, Co, x.device)
+    g = _geom("hyres_geom_deconv2d", B, H, W, Ci, x.ld, Co, y.ld, K, pad)
+    w2 = _prepped(weight, g, L.WPREP_DECONV, Ci, Co, K, K, pad)
+    e = L.Epilogue()
+    e.kind = L.EPI_BIAS
+    e.act = act
+    e.bias = L.ptr(bias)
+    _launch_conv(g, x.ptr(), w2, g.ntaps * Ci, y.ptr(), e)
+    if tape is None:
+        return y
+
+    def bwd():
+        gy = y.grad()
+        if gy is None:
+            return
+        gp, gpld = _act_backward(y, gy, y.grad_ld(), act, None, None)
+        if wants_grad(bias):
+            _colsum_into(gp, y.P, Co, gpld, param_grad(bias))
+        if wants_grad(weight):
+            d = L.WgradDesc()
+            L.call("hyres_wgrad_desc_deconv2d", ctypes.byref(d), B, H, W, Ci, x.ld, Co, gpld, K, pad)
+            d.accumulate = 1
+            _wgrad(d, x.ptr(), gp.data_ptr(), param_grad(weight), x.device)
+        if x.rg:
+            tgt, acc = x.grad_target()
+            gd = _geom("hyres_geom_deconv2d_dgrad", B, H, W, Ci, x.grad_ld(), Co, gpld, K, pad)
+            w2d = _prepped(weight, gd, L.WPREP_DECONV_DGRAD, Ci, Co, K, K, pad)
+            ed = L.Epilogue()
+            ed.kind = L.EPI_BIAS
+            ed.accumulate = acc
+            _launch_conv(gd, gp.data_ptr(), w2d, gd.ntaps * Co, tgt.data_ptr(), ed)
+
+    tape.push(bwd)
+    return y
+
+
+def gdn(tape: Optional[Tape], x: Node, beta: torch.Tensor, gamma: torch.Tensor, inverse: bool) -> Node:
+    """compressai GDN / IGDN: y = x * rsqrt(conv1x1(x^2, gamma') + beta')  (sqrt for IGDN).
+
+    One MFMA GEMM with an x->x^2 A-prologue and an x*rsqrt(n) epilogue (n saved for backward);
+    reparametrisation (NonNegativeParametrizer + LowerBound) in a tiny side kernel.
+    Reference call sites: models/checkerboard.py:37,41 (GDN), :52,56 (IGDN)."""
+    C = x.C
+    assert x.contiguous
+    dev = x.device
+    bp = _empty((C,), dev)
+    gp = _empty((C, C), dev)
+    L.call("hyres_gdn_reparam_fwd", beta.data_ptr(), gamma.data_ptr(), bp.data_ptr(), gp.data_ptr(), C, L.stream())
+    y = Node.new(x.B, x.H, x.W, C, dev)
+    nrm = _empty((x.B, x.H, x.W, C), dev)
+    g = _geom("hyres_geom_conv2d", x.B, x.H, x.W, C, x.ld, C, C, 1, 1, 1, 0, 1)
+    e = L.Epilogue()
+    e.kind = L.EPI_IGDN if inverse else L.EPI_GDN
+    e.square_input = 1
+    e.bias = bp.data_ptr()
+    e.aux0 = x.ptr()
+    e.ld0 = x.ld
+    e.out2 = nrm.data_ptr()
+    e.ldo2 = C
+    _launch_conv(g, x.ptr(), gp, C, y.ptr(), e)
+    if tape is None:
+        return y
+
+    def bwd():
+        gy = y.grad()
+        if gy is None:
+            return
+        gld = y.grad_ld()
+        if gld != C:
+            t = _empty((x.B, x.H, x.W, C), dev)
+            L.call("hyres_add2d", gy.data_ptr(), gld, t.data_ptr(), C, y.P, C, 0, L.stream())
+            gy = t
+        dn = _empty((x.B, x.H, x.W, C), dev)
+        L.call("hyres_gdn_dnorm", gy.data_ptr(), y.ptr(), nrm.data_ptr(), dn.data_ptr(), y.P, C, int(inverse),
+               L.stream())
+        if beta.requires_grad or gamma.requires_grad:
+            dgp = _empty((C, C), dev)
+            d = L.WgradDesc()
+            L.call("hyres_wgrad_desc_conv2d", ctypes.byref(d), x.B, x.H, x.W, C, x.ld, C, C, 1, 1, 1, 0, 1)
+            d.square_q = 1
+            d.accumulate = 0
+            _wgrad(d, dn.data_ptr(), x.ptr(), dgp, dev)
+            dbp = _empty((C,), dev)
+            _colsum_into(dn, y.P, C, C, dbp, acc=0)
+            L.call("hyres_gdn_reparam_bwd", beta.data_ptr(), gamma.data_ptr(), dbp.data_ptr(), dgp.data_ptr(),
+                   param_grad(beta).data_ptr(), param_grad(gamma).data_ptr(), C, 1, L.stream())
+        if x.rg:
+            tgt, acc = x.grad_target()
+            gd = _geom("hyres_geom_conv2d_dgrad", x.B, x.H, x.W, C, x.grad_ld(), C, C, 1, 1, 1, 0, 1)
+            w2d = _prepped(gp, gd, L.WPREP_CONV_DGRAD, C, C, 1, 1, 0, key_extra=("gdn",))
+            ed = L.Epilogue()
+            ed.kind = L.EPI_IGDN_BWD if inverse else L.EPI_GDN_BWD
+            ed.accumulate = acc
+            ed.aux0 = x.ptr()
+            ed.ld0 = x.ld
+            ed.aux1 = gy.data_ptr()
+            ed.ld1 = C
+            ed.aux2 = nrm.data_ptr()
+            ed.ld2 = C
+            _launch_conv(gd, dn.data_ptr(), w2d, C, tgt.data_ptr(), ed)
+
+    tape.push(bwd)
+    return y
+
+
+def attn_gate(tape: Optional[Tape], a: Node, b: Node, x: Node) -> Node:
+    """AttentionBlock combine (models/layers/attention.py:44-47): out = a * sigmoid(b) + x."""
+    assert a.contiguous and b.contiguous and x.contiguous
+    n = a.P * a.C
+    out = Node.new(a.B, a.H, a.W, a.C, a.device)
+    L.call("hyres_attn_gate_fwd", a.ptr(), b.ptr(), x.ptr(), out.ptr(), n, L.stream())
+    if tape is None:
+        return out
+
+    def bwd():
+        g = out.grad()
+        if g is None:
+            return
+        ga, acc_a = a.grad_target()
+        gb, acc_b = b.grad_target()
+        assert acc_a == 0 and acc_b == 0, "gate inputs are single-consumer"
+        L.call("hyres_attn_gate_bwd", a.ptr(), b.ptr(), g.data_ptr(), ga.data_ptr(), gb.data_ptr(), n, L.stream())
+        if x.rg:
+            x.set_grad(g)
+
+    tape.push(bwd)
+    return out
+
+
+# --------------------------------------------------------------------------------------------------
+# layout boundary
+# --------------------------------------------------------------------------------------------------
+def to_nhwc(x: torch.Tensor, rg: bool = False) -> Node:
+    L.require_device(x)
+    x = x.contiguous()
+    B, C, H, W = x.shape
+    y = Node.new(B, H, W, C, x.device, rg=rg)
+    L.call("hyres_nchw_to_nhwc", x.data_ptr(), y.ptr(), B, C, H, W, C, L.stream())
+    return y
+
+
+def to_nchw(x: Node) -> torch.Tensor:
+    out = _empty((x.B, x.C, x.H, x.W), x.device)
+    L.call("hyres_nhwc_to_nchw", x.ptr(), x.ld, out.data_ptr(), x.B, x.C, x.H, x.W, L.stream())
+    return out
+
+
+def to_nchw_grad(x: Node) -> torch.Tensor:
+    g = x.grad()
+    out = _empty((x.B, x.C, x.H, x.W), x.device)
+    L.call("hyres_nhwc_to_nchw", g.data_ptr(), x.grad_ld(), out.data_ptr(), x.B, x.C, x.H, x.W, L.stream())
+    return out
+
+
+def nchw_grad_to_nhwc(g: torch.Tensor) -> torch.Tensor:
+    g = g.contiguous()
+    B, C, H, W = g.shape
+    y = _empty((B, H, W, C), g.device)
+    L.call("hyres_nchw_to_nhwc", g.data_ptr(), y.data_ptr(), B, C, H, W, C, L.stream())
+    return y

@@ -1,0 +1,151 @@
+"""MultiScaleRefine building blocks and the ResidualJPEGCompression glue on HIP.
+
+Reference anchors: models/layers/enhancement.py:7-112 (SpatialAttention, SEBlock, MultiScaleRefine),
+models/hyres.py:48,62,65-67 (residual, x_hat_initial, refine + clamp)."""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from . import _lib as L
+from .ops import Node, Tape, _empty, param_grad, _ws
+
+
+def bilinear(tape: Optional[Tape], x: Node, Ho: int, Wo: int, scale_h: float, scale_w: float,
+             out: Optional[Node] = None) -> Node:
+    """F.interpolate(mode='bilinear', align_corners=False).  ``scale_*`` is torch's source-index scale:
+    1/scale_factor when a scale_factor is given (enhancement.py:96,101), in/out for ``size=``
+    (enhancement.py:98,103)."""
+    y = out if out is not None else Node.new(x.B, Ho, Wo, x.C, x.device)
+    L.call("hyres_bilinear_fwd", x.ptr(), x.ld, y.ptr(), y.ld, x.B, x.H, x.W, Ho, Wo, x.C, float(scale_h),
+           float(scale_w), 0, L.stream())
+    if tape is None:
+        return y
+
+    def bwd():
+        g = y.grad()
+        if g is None or not x.rg:
+            return
+        tgt, acc = x.grad_target()
+        L.call("hyres_bilinear_bwd", g.data_ptr(), y.grad_ld(), tgt.data_ptr(), x.grad_ld(), x.B, x.H, x.W, Ho, Wo,
+               x.C, float(scale_h), float(scale_w), acc, L.stream())
+
+    tape.push(bwd)
+    return y
+
+
+def se_block(tape: Optional[Tape], x: Node, w1: torch.Tensor, w2: torch.Tensor) -> Node:
+    """SEBlock (enhancement.py:25-40): y = x * sigmoid(W2 relu(W1 avgpool(x)))."""
+    assert x.contiguous
+    B, HW, C = x.B, x.H * x.W, x.C
+    Cr = w1.shape[0]
+    dev = x.device
+    y = Node.new(x.B, x.H, x.W, C, dev)
+    pooled = _empty((B, C), dev)
+    hidden = _empty((B, Cr), dev)
+    sgate = _empty((B, C), dev)
+    wsb = L.load().hyres_se_workspace_bytes(B, HW, C)
+    ws = _ws(wsb + B * C * 4, dev, slot=1)
+    L.call("hyres_se_fwd", x.ptr(), w1.data_ptr(), w2.data_ptr(), y.ptr(), pooled.data_ptr(), hidden.data_ptr(),
+           sgate.data_ptr(), B, HW, C, Cr, ws.data_ptr(), ws.numel(), L.stream())
+    if tape is None:
+        return y
+
+    def bwd():
+        g = y.grad()
+        if g is None:
+            return
+        assert y.grad_ld() == C
+        gw1 = param_grad(w1)
+        gw2 = param_grad(w2)
+        tgt, acc = x.grad_target()
+        gx = tgt if acc == 0 else _empty((x.B, x.H, x.W, C), dev)
+        ws2 = _ws(wsb + B * C * 4, dev, slot=1)
+        L.call("hyres_se_bwd", x.ptr(), g.data_ptr(), w1.data_ptr(), w2.data_ptr(), pooled.data_ptr(),
+               hidden.data_ptr(), sgate.data_ptr(), gx.data_ptr(), gw1.data_ptr(), gw2.data_ptr(), B, HW, C, Cr,
+               ws2.data_ptr(), ws2.numel(), L.stream())
+        if acc:
+            L.call("hyres_accumulate", gx.data_ptr(), tgt.data_ptr(), gx.numel(), L.stream())
+
+    tape.push(bwd)
+    return y
+
+
+def spatial_attention_mul(tape: Optional[Tape], x: Node, w: torch.Tensor) -> Node:
+    """multi * SpatialAttention(multi) (enhancement.py:7-21 and :105-106), fused."""
+    assert x.contiguous
+    B, H, W, C = x.B, x.H, x.W, x.C
+    dev = x.device
+    pooled2 = _empty((B, H, W, 2), dev)
+    attn = _empty((B, H, W), dev)
+    y = Node.new(B, H, W, C, dev)
+    L.call("hyres_spatial_attn_fwd", x.ptr(), w.data_ptr(), pooled2.data_ptr(), attn.data_ptr(), y.ptr(), B, H, W, C,
+           L.stream())
+    if tape is None:
+        return y
+
+    def bwd():
+        g = y.grad()
+        if g is None:
+            return
+        assert y.grad_ld() == C
+        tgt, acc = x.grad_target()
+        gx = tgt if acc == 0 else _empty((B, H, W, C), dev)
+        gw = param_grad(w) if w.requires_grad else _empty(w.shape, dev)
+        wsb = L.load().hyres_spatial_attn_workspace_bytes(B, H, W)
+        ws = _ws(wsb, dev, slot=1)
+        L.call("hyres_spatial_attn_bwd", x.ptr(), w.data_ptr(), pooled2.data_ptr(), attn.data_ptr(), g.data_ptr(),
+               gx.data_ptr(), gw.data_ptr(), B, H, W, C, ws.data_ptr(), ws.numel(), L.stream())
+        if acc:
+            L.call("hyres_accumulate", gx.data_ptr(), tgt.data_ptr(), gx.numel(), L.stream())
+
+    tape.push(bwd)
+    return y
+
+
+def add(tape: Optional[Tape], a: Node, b: Node, alpha: float = 1.0) -> Node:
+    """y = a + alpha*b (models/hyres.py:48 residual = x - jpeg; :62 x_hat_initial = jpeg + residual_hat)."""
+    assert a.contiguous and b.contiguous
+    y = Node.new(a.B, a.H, a.W, a.C, a.device)
+    L.call("hyres_axpby", a.ptr(), b.ptr(), float(alpha), y.ptr(), y.P * y.C, L.stream())
+    if tape is None:
+        return y
+
+    def bwd():
+        g = y.grad()
+        if g is None:
+            return
+        if a.rg:
+            a.set_grad(g)
+        if b.rg:
+            tgt, acc = b.grad_target()
+            L.call("hyres_scale", g.data_ptr(), None, float(alpha), tgt.data_ptr(), y.P * y.C, acc, L.stream())
+
+    tape.push(bwd)
+    return y
+
+
+def add_clamp01(tape: Optional[Tape], x0: Node, r: Node) -> Node:
+    """x_hat = clamp(x0 + r, 0, 1)  (models/hyres.py:66-67)."""
+    n = x0.P * x0.C
+    pre = _empty(x0.v.shape, x0.device) if tape is not None else None
+    y = Node.new(x0.B, x0.H, x0.W, x0.C, x0.device)
+    if pre is not None:
+        L.call("hyres_axpby", x0.ptr(), r.ptr(), 1.0, pre.data_ptr(), n, L.stream())
+    L.call("hyres_add_clamp01", x0.ptr(), r.ptr(), y.ptr(), n, L.stream())
+    if tape is None:
+        return y
+
+    def bwd():
+        g = y.grad()
+        if g is None:
+            return
+        gp = _empty(x0.v.shape, x0.device)
+        L.call("hyres_add_clamp01_bwd", pre.data_ptr(), g.data_ptr(), gp.data_ptr(), 0, n, L.stream())
+        for t in (x0, r):
+            if t.rg:
+                t.set_grad(gp)
+
+    tape.push(bwd)
+    return y

@@ -1,0 +1,117 @@
+"""MultiScaleRefine post-filter (models/layers/enhancement.py:7-112) on HIP.
+
+Data flow (NHWC, one HBM buffer ``multi`` [B,H,W,3*mid] replaces torch.cat):
+  feat = SE(PReLU(conv_in(x)))
+  multi[..., 0:mid]      = scale1(feat)                                  (last conv writes the slice)
+  multi[..., mid:2mid]   = up(scale2(down2(feat)))                       (bilinear up writes the slice)
+  multi[..., 2mid:3mid]  = up(scale3(down4(feat)))
+  out = fusion(multi * sigmoid(conv7x7([mean_c, max_c](multi))))
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from hyres_hip import _lib as L
+from hyres_hip import refine_ops as R
+from hyres_hip.layers import Conv2d, HipModule, PReLU, ReLU, Sequential
+from hyres_hip.ops import Node
+
+__all__ = ["SpatialAttention", "SEBlock", "dilated_conv", "MultiScaleRefine"]
+
+
+class SpatialAttention(HipModule):
+    """CBAM spatial attention: sigmoid(conv7x7([mean_c(x), max_c(x)])) (enhancement.py:7-21)."""
+
+    def __init__(self, kernel_size: int = 7):
+        super().__init__()
+        if kernel_size != 7:
+            raise NotImplementedError("HIP spatial attention is specialised for kernel_size=7")
+        padding = (kernel_size - 1) // 2
+        self.conv = Conv2d(2, 1, kernel_size, padding=padding, bias=False)
+        self.sigmoid = nn.Sigmoid()
+
+    def hip_mul(self, tape, x: Node) -> Node:
+        """x * SpatialAttention(x) fused (how MultiScaleRefine uses it, enhancement.py:105-106)."""
+        return R.spatial_attention_mul(tape, x, self.conv.weight)
+
+    def hip(self, tape, x: Node) -> Node:
+        # standalone forward returns the attention map [B,H,W,1] (forward only)
+        assert tape is None, "standalone SpatialAttention is forward-only; use hip_mul inside MultiScaleRefine"
+        import hyres_hip.ops as O
+        B, H, W, C = x.B, x.H, x.W, x.C
+        pooled2 = O._empty((B, H, W, 2), x.device)
+        attn = Node.new(B, H, W, 1, x.device)
+        y = O._empty((B, H, W, C), x.device)
+        L.call("hyres_spatial_attn_fwd", x.ptr(), self.conv.weight.data_ptr(), pooled2.data_ptr(), attn.ptr(),
+               y.data_ptr(), B, H, W, C, L.stream())
+        return attn
+
+
+class SEBlock(HipModule):
+    """Squeeze-and-excitation (enhancement.py:25-40)."""
+
+    def __init__(self, channel, reduction=16):
+        super().__init__()
+        self.avg_pool = nn.AdaptiveAvgPool2d(1)
+        self.fc = nn.Sequential(
+            nn.Linear(channel, channel // reduction, bias=False),
+            ReLU(inplace=True),
+            nn.Linear(channel // reduction, channel, bias=False),
+            nn.Sigmoid(),
+        )
+
+    def hip(self, tape, x: Node) -> Node:
+        return R.se_block(tape, x, self.fc[0].weight, self.fc[2].weight)
+
+
+def dilated_conv(ch_in, ch_out, dilation):
+    """enhancement.py:44-51."""
+    return Conv2d(ch_in, ch_out, kernel_size=3, padding=dilation, dilation=dilation, bias=True)
+
+
+class MultiScaleRefine(HipModule):
+    def __init__(self, in_channels=3, mid_channels=64):
+        super().__init__()
+        self.mid = mid_channels
+        self.conv_in = Conv2d(in_channels, mid_channels, kernel_size=3, padding=1)
+        self.act_in = PReLU()
+        self.se_block = SEBlock(mid_channels, reduction=16)
+
+        def make_block():
+            return Sequential(
+                dilated_conv(mid_channels, mid_channels, dilation=1),
+                PReLU(),
+                dilated_conv(mid_channels, mid_channels, dilation=2),
+                PReLU(),
+            )
+
+        self.scale1 = make_block()
+        self.scale2 = make_block()
+        self.scale3 = make_block()
+        self.spatial_att = SpatialAttention(kernel_size=7)
+        self.fusion = Sequential(
+            Conv2d(mid_channels * 3, mid_channels, kernel_size=1),
+            PReLU(),
+            Conv2d(mid_channels, in_channels, kernel_size=3, padding=1),
+        )
+
+    def hip(self, tape, x: Node) -> Node:
+        mid = self.mid
+        feat = self.conv_in.hip(tape, x, act=L.ACT_PRELU, slope=self.act_in.weight)
+        feat = self.se_block.hip(tape, feat)
+        B, H, W = feat.B, feat.H, feat.W
+        assert H % 4 == 0 and W % 4 == 0, "MultiScaleRefine needs H, W divisible by 4"
+        multi = Node.new(B, H, W, 3 * mid, feat.device)
+        # scale 1 (orig)
+        self.scale1.hip(tape, feat, out=multi.slice(0, mid))
+        # scale 2 (1/2): F.interpolate(scale_factor=0.5) -> source scale 2.0; back with size= -> in/out
+        f2 = R.bilinear(tape, feat, H // 2, W // 2, 2.0, 2.0)
+        f2 = self.scale2.hip(tape, f2)
+        R.bilinear(tape, f2, H, W, (H // 2) / H, (W // 2) / W, out=multi.slice(mid, 2 * mid))
+        # scale 3 (1/4)
+        f3 = R.bilinear(tape, feat, H // 4, W // 4, 4.0, 4.0)
+        f3 = self.scale3.hip(tape, f3)
+        R.bilinear(tape, f3, H, W, (H // 4) / H, (W // 4) / W, out=multi.slice(2 * mid, 3 * mid))
+        m = self.spatial_att.hip_mul(tape, multi)
+        return self.fusion.hip(tape, m)

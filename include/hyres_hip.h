@@ -1,0 +1,298 @@
+/*
+ * hyres_hip.h — C-ABI of libhyres_hip.so, the MI355X (gfx950) kernels behind HyRES's
+ * residual-codec hot path.  Plain pointers and sizes only: every tensor argument is a device
+ * pointer to fp32 data laid out NHWC ([B][H][W][ld] with the channel slice starting at the
+ * pointer), every entry point takes the caller's HIP stream as an opaque handle and returns
+ * 0 on success or a nonzero HYRES_E_* / hipError_t code (message: hyres_last_error_string()).
+ * The library never allocates, frees or synchronises: scratch is caller-supplied (query with the
+ * *_workspace_bytes functions), so every call is stream-ordered and hipGraph-capturable.
+ *
+ * The reference has no native operator API — its "operator interface" is nn.Module.forward +
+ * autograd.  Each entry point below names the reference code it replaces
+ * (paths relative to the reference repo root).
+ */
+#ifndef HYRES_HIP_H
+#define HYRES_HIP_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* hyres_stream_t; /* hipStream_t */
+
+#define HYRES_OK 0
+#define HYRES_E_SHAPE 1001     /* inconsistent or unsupported shape / stride */
+#define HYRES_E_ALIGN 1002     /* pointer or leading dimension not 16-byte aligned where needed */
+#define HYRES_E_ARG 1003       /* invalid enum / NULL pointer */
+#define HYRES_E_WORKSPACE 1004 /* workspace too small */
+
+#define HYRES_MAX_TAPS 49
+
+/* ------------------------------------------------------------------------------------------ */
+/* library                                                                                    */
+/* ------------------------------------------------------------------------------------------ */
+int hyres_version(void);
+const char* hyres_last_error_string(void);
+
+/* ------------------------------------------------------------------------------------------ */
+/* convolution geometry (implicit GEMM, NHWC).                                                */
+/* One launch computes Y[b, i*osh+oph[p], j*osw+opw[p], co] for every phase p < nphase and base */
+/* pixel (i,j) < (Hq,Wq):  bias[co] + sum over taps t of phase p and ci < Ci of                 */
+/*   X[b, i*ish + dh[t], j*isw + dw[t], ci] * W2[co*ldw + t*Ci + ci]   (zero outside X).        */
+/* Phases express ConvTranspose2d / strided-conv input-gradients as sub-pixel convolutions.    */
+/* ------------------------------------------------------------------------------------------ */
+typedef struct hyres_conv_geom {
+    int B, Hi, Wi, Ci, ldx;   /* input: NHWC, pixel stride ldx floats */
+    int Ho, Wo, Co, ldy;      /* output tensor dims, pixel stride ldy floats */
+    int nphase, Hq, Wq;       /* base grid per phase */
+    int osh, osw, ish, isw;   /* output / input stride of the base grid */
+    int oph[4], opw[4];       /* output offset of each phase */
+    int ntap[4], tap0[4];     /* taps of each phase: global tap indices tap0[p] .. tap0[p]+ntap[p]-1 */
+    int ntaps;                /* total taps (rows of W2 = ntaps*Ci per output channel) */
+    int dh[HYRES_MAX_TAPS], dw[HYRES_MAX_TAPS];
+} hyres_conv_geom;
+
+/* nn.Conv2d(k, stride, pad, dil) forward (models/layers/common.py:4-11, compressai conv()). */
+int hyres_geom_conv2d(hyres_conv_geom* g, int B, int H, int W, int Ci, int ldx, int Co, int ldy,
+                      int KH, int KW, int stride, int pad, int dil);
+/* input-gradient of that Conv2d: a conv over dY (stride 1) or a 4-phase sub-pixel conv (stride 2).
+ * (B,H,W,Ci,Co,...) describe the ORIGINAL conv; ld_dx / ld_dy are the gradients' pixel strides. */
+int hyres_geom_conv2d_dgrad(hyres_conv_geom* g, int B, int H, int W, int Ci, int ld_dx, int Co,
+                            int ld_dy, int KH, int KW, int stride, int pad, int dil);
+/* nn.ConvTranspose2d(k, s=2, p, output_padding=1) forward (compressai deconv()) as 4 phases. */
+int hyres_geom_deconv2d(hyres_conv_geom* g, int B, int H, int W, int Ci, int ldx, int Co, int ldy,
+                        int K, int pad);
+/* input-gradient of that ConvTranspose2d: a stride-2 conv over dY. */
+int hyres_geom_deconv2d_dgrad(hyres_conv_geom* g, int B, int H, int W, int Ci, int ld_dx, int Co,
+                              int ld_dy, int K, int pad);
+
+/* Weight re-layout for a geometry built by the helpers above.  ``w`` is the PyTorch parameter
+ * (Conv2d: [Co][Ci][KH][KW]; ConvTranspose2d: [Ci][Co][K][K]); ``w2`` gets [rows][ntaps*cols] in
+ * the geometry's tap order.  ``mask`` (same shape as w, or NULL) multiplies w on the fly
+ * (CheckboardMaskedConv2d, models/layers/checkerboard.py:46-47). (Ci, Co) are the ORIGINAL layer's. */
+#define HYRES_WPREP_CONV 0        /* Conv2d forward:  rows = Co, cols = Ci */
+#define HYRES_WPREP_CONV_DGRAD 1  /* Conv2d dgrad:    rows = Ci, cols = Co, taps flipped as geom */
+#define HYRES_WPREP_DECONV 2      /* ConvT forward:   rows = Co, cols = Ci, phase tap order */
+#define HYRES_WPREP_DECONV_DGRAD 3/* ConvT dgrad:     rows = Ci(in), cols = Co(out) */
+int hyres_conv_weight_prep(const hyres_conv_geom* g, const float* w, float* w2, int mode, int Ci,
+                           int Co, int KH, int KW, int pad, const float* mask, hyres_stream_t s);
+
+/* epilogue of the convolution GEMM */
+#define HYRES_EPI_BIAS 0      /* y = act(acc + bias + res) */
+#define HYRES_EPI_GDN 1       /* n = acc + bias(beta');  y = aux0 * rsqrt(n); out2 = n   (GDN)  */
+#define HYRES_EPI_IGDN 2      /* n = acc + bias(beta');  y = aux0 * sqrt(n);  out2 = n   (IGDN) */
+#define HYRES_EPI_GDN_BWD 3   /* y = 2*aux0*acc + aux1 * rsqrt(aux2)                              */
+#define HYRES_EPI_IGDN_BWD 4  /* y = 2*aux0*acc + aux1 * sqrt(aux2)                               */
+#define HYRES_ACT_NONE 0
+#define HYRES_ACT_RELU 1
+#define HYRES_ACT_PRELU 2     /* single shared slope (nn.PReLU()), read from device pointer */
+
+typedef struct hyres_epilogue {
+    int kind, act, accumulate;    /* accumulate: y += result (gradient accumulation) */
+    int square_input;             /* GEMM A-operand prologue x -> x*x (GDN norm) */
+    const float* bias;            /* [Co] or NULL */
+    const float* res; int ldres;  /* added before act, or NULL */
+    const float* slope;           /* PReLU slope (device, 1 float) */
+    const float* aux0; int ld0;
+    const float* aux1; int ld1;
+    const float* aux2; int ld2;
+    float* out2; int ldo2;
+} hyres_epilogue;
+
+/* Y = conv(X, W2) with the epilogue — nn.Conv2d / nn.ConvTranspose2d / GDN forward and their
+ * input-gradients (replaces torch's cuDNN/MIOpen conv dispatch at every conv call site on the hot
+ * path: models/checkerboard.py:35-88, models/layers/attention.py:11-39,
+ * models/layers/enhancement.py:17,44-51,65-82, compressai GDN/RBB).  fp32 MFMA (v_mfma_f32_32x32x2f32). */
+int hyres_conv_forward(const hyres_conv_geom* g, const float* x, const float* w2, int ldw, float* y,
+                       const hyres_epilogue* e, hyres_stream_t s);
+
+/* Weight gradient:  dW[t][m][n] = sum_q P[q][m] * Q[shift_t(q)][n]  over a base grid q (B,Hq,Wq).
+ * Conv2d: P = dY (output grid), Q = X;  ConvTranspose2d: P = X (input grid), Q = dY.
+ * Result written (or accumulated) into the PyTorch-layout gradient dst[m*sm + n*sn + t*st]. */
+typedef struct hyres_wgrad_desc {
+    int B, Hq, Wq;               /* base grid (P's pixel grid) */
+    int M, ldp;                  /* P channels / pixel stride */
+    int N, ldq, Hqq, Wqq;        /* Q channels / pixel stride / Q spatial dims */
+    int sq;                      /* Q stride of the base grid */
+    int ntaps;
+    int dh[HYRES_MAX_TAPS], dw[HYRES_MAX_TAPS];
+    int sm, sn, st;              /* destination strides (floats) */
+    int square_q;                /* Q -> Q*Q (GDN gamma gradient) */
+    int accumulate;
+} hyres_wgrad_desc;
+int hyres_wgrad_desc_conv2d(hyres_wgrad_desc* d, int B, int H, int W, int Ci, int ldx, int Co,
+                            int ldy, int KH, int KW, int stride, int pad, int dil);
+int hyres_wgrad_desc_deconv2d(hyres_wgrad_desc* d, int B, int H, int W, int Ci, int ldx, int Co,
+                              int ldy, int K, int pad);
+long long hyres_wgrad_workspace_bytes(const hyres_wgrad_desc* d);
+int hyres_conv_wgrad(const hyres_wgrad_desc* d, const float* p, const float* q, float* dst,
+                     void* workspace, long long ws_bytes, hyres_stream_t s);
+
+/* column sums over pixels: dst[c] (+)= sum_p x[p*ld + c]  (bias gradients) */
+int hyres_colsum(const float* x, int P, int C, int ld, float* dst, int accumulate, void* workspace,
+                 long long ws_bytes, hyres_stream_t s);
+long long hyres_colsum_workspace_bytes(int P, int C);
+
+/* ------------------------------------------------------------------------------------------ */
+/* layout / elementwise                                                                       */
+/* ------------------------------------------------------------------------------------------ */
+int hyres_nchw_to_nhwc(const float* x, float* y, int B, int C, int H, int W, int ldy, hyres_stream_t s);
+int hyres_nhwc_to_nchw(const float* x, int ldx, float* y, int B, int C, int H, int W, hyres_stream_t s);
+/* y = a + alpha*b over n contiguous floats (hyres.py:48,62 glue) */
+int hyres_axpby(const float* a, const float* b, float alpha, float* y, long long n, hyres_stream_t s);
+/* x_hat = clamp(x0 + r, 0, 1)  (models/hyres.py:66-67); bwd: g passes where 0 < x0+r < 1 */
+int hyres_add_clamp01(const float* x0, const float* r, float* y, long long n, hyres_stream_t s);
+int hyres_add_clamp01_bwd(const float* pre, const float* g, float* gx, int accumulate, long long n,
+                          hyres_stream_t s);
+/* g_out = g * (y > 0)   (ReLU backward), optional accumulate into dst */
+int hyres_relu_bwd(const float* y, const float* g, float* gx, long long n, hyres_stream_t s);
+/* strided variant over NHWC slices */
+int hyres_relu_bwd_2d(const float* y, int ldy_, const float* g, int ldg, float* gx, int ldgx, long long P,
+                      int C, hyres_stream_t s);
+/* PReLU backward from the saved pre-activation x: gx = g*(x>0 ? 1 : a); dslope += sum(g*x*(x<=0))
+ * (enhancement.py nn.PReLU). ws: hyres_reduce_workspace_bytes(P*C). */
+int hyres_prelu_bwd(const float* x, int ldx, const float* g, int ldg, float* gx, int ldgx, long long P,
+                    int C, const float* slope, float* dslope, void* ws, long long ws_bytes,
+                    hyres_stream_t s);
+/* AttentionBlock gate (models/layers/attention.py:44-47): out = a*sigmoid(b) + x */
+int hyres_attn_gate_fwd(const float* a, const float* b, const float* x, float* out, long long n,
+                        hyres_stream_t s);
+int hyres_attn_gate_bwd(const float* a, const float* b, const float* g, float* ga, float* gb,
+                        long long n, hyres_stream_t s);
+/* y (+)= x  (gradient fan-in) */
+int hyres_accumulate(const float* x, float* y, long long n, hyres_stream_t s);
+/* y[p*ldy + c] (+)= x[p*ldx + c]  over P pixels x C channels (strided gradient fan-in / copy) */
+int hyres_add2d(const float* x, int ldx, float* y, int ldy, long long P, int C, int accumulate,
+                hyres_stream_t s);
+/* y = a * b elementwise (in-place allowed: CheckboardMaskedConv2d's weight.data *= mask) */
+int hyres_mul(const float* a, const float* b, float* y, long long n, hyres_stream_t s);
+/* stream-ordered memset 0 (hipMemsetAsync) */
+int hyres_zero(void* p, long long bytes, hyres_stream_t s);
+/* y (+)= (coef ? coef[0] : 1) * scale * x */
+int hyres_scale(const float* x, const float* coef, float scale, float* y, long long n, int accumulate,
+                hyres_stream_t s);
+
+/* GDN reparametrisation (compressai NonNegativeParametrizer + LowerBound):
+ * beta' = max(beta, bb)^2 - ped,  gamma' = max(gamma, gb)^2 - ped;  and backward. */
+int hyres_gdn_reparam_fwd(const float* beta, const float* gamma, float* beta_p, float* gamma_p, int C,
+                          hyres_stream_t s);
+int hyres_gdn_reparam_bwd(const float* beta, const float* gamma, const float* dbeta_p,
+                          const float* dgamma_p, float* dbeta, float* dgamma, int C, int accumulate,
+                          hyres_stream_t s);
+/* GDN backward helper: dn = g * y / n * (-0.5 GDN | +0.5 IGDN) */
+int hyres_gdn_dnorm(const float* g, const float* y, const float* n, float* dn, long long P, int C,
+                    int inverse, hyres_stream_t s);
+
+/* ------------------------------------------------------------------------------------------ */
+/* quantisation, checkerboard context, entropy models                                         */
+/* ------------------------------------------------------------------------------------------ */
+/* U(-0.5, 0.5) noise (counter-based hash RNG), replaces torch.empty_like().uniform_() in
+ * models/utils/quantization.py:6-10 and compressai EntropyModel.quantize("noise") */
+int hyres_uniform_noise(float* out, long long n, unsigned long long seed, unsigned long long offset,
+                        hyres_stream_t s);
+/* Quantizer.quantize (models/utils/quantization.py:11-14): mode 0 = "ste" value round(x)-x+x,
+ * mode 1 = round (half-to-even) */
+int hyres_quantize(const float* x, int mode, float* y, long long n, hyres_stream_t s);
+/* Anchor pass (models/checkerboard.py:106-122): y_a = y*[(h+w) even];
+ * y_a_hat = STE(y_a - m_a) + m_a  or  y_a + noise. Writes y_a_hat (NHWC [B,H,W,C]). */
+int hyres_ckbd_anchor_fwd(const float* y, const float* means_a, int ldm, const float* noise,
+                          float* y_a_hat, int B, int H, int W, int C, hyres_stream_t s);
+/* Non-anchor pass + combine + GaussianConditional (checkerboard.py:132-142, compressai GC):
+ * y_na_hat, y_hat = y_a_hat + y_na_hat, scales = s_a + s_na, means = m_a + m_na,
+ * y_q = round(y - means) + means (eval) or y + noise_gc (train), lik = LB(GC(y_q; scales, means)).
+ * Also accumulates sum(log lik) per block into ws (bpp partial). */
+int hyres_ckbd_nonanchor_gc_fwd(const float* y, const float* y_a_hat, const float* params_a, int lda,
+                                const float* params_na, int ldn, const float* noise_q,
+                                const float* noise_gc, float* y_hat, float* scales, float* means,
+                                float* y_q, float* lik, int B, int H, int W, int C, hyres_stream_t s);
+/* backward of the above: g_y = g_yhat (+ GC term in training); [g_scales | g_means] written to
+ * both param-aggregation gradient buffers (scales = s_a + s_na, means = m_a + m_na).  The STE /
+ * noise quantisers pass the gradient straight to y and give none to the means. */
+int hyres_ckbd_gc_bwd(const float* y_q, const float* scales, const float* means, const float* g_lik,
+                      const float* g_yhat, int training, float* g_y, float* g_params_a, int lda,
+                      float* g_params_na, int ldn, int B, int H, int W, int C, hyres_stream_t s);
+/* g_y[anchor positions] += g_ya (context-model path back into the anchor quantiser) */
+int hyres_ckbd_anchor_bwd(const float* g_ya, float* g_y, int B, int H, int W, int C, hyres_stream_t s);
+
+/* EntropyBottleneck forward (compressai 1.2.6): z NHWC [P][C]; params packed per channel
+ * (see hyres_eb_pack); z_q = z + noise (train) | round(z - med) + med (eval); lik = LB(sig(u)-sig(l));
+ * z_hat_ste = quantize_ste(z - med) + med (checkerboard.py:98-101). */
+int hyres_eb_fwd(const float* z, const float* packed, const float* noise, int training, float* z_q,
+                 float* lik, float* z_hat_ste, long long P, int C, hyres_stream_t s);
+int hyres_eb_bwd(const float* z_q, const float* packed, const float* lik, const float* g_lik,
+                 const float* g_zhat, int training, int noisequant, float* g_z, float* g_packed_ws,
+                 long long P, int C, hyres_stream_t s);
+long long hyres_eb_workspace_bytes(long long P, int C);
+/* pack EB parameters (softplus(matrices), biases, tanh(factors), quantile medians) per channel */
+#define HYRES_EB_REC 64
+int hyres_eb_pack(const float* const* mats, const float* const* biases, const float* const* factors,
+                  const float* quantiles, float* packed, int C, hyres_stream_t s);
+/* reduce the per-block packed gradients of hyres_eb_bwd into the parameter gradients */
+int hyres_eb_unpack_grad(const float* g_packed_ws, int nblocks, const float* const* mats,
+                         const float* const* factors, float* const* g_mats, float* const* g_biases,
+                         float* const* g_factors, float* g_quantiles, int C, int accumulate,
+                         hyres_stream_t s);
+/* EntropyBottleneck.loss (aux loss) and its gradient wrt quantiles */
+int hyres_eb_aux_loss(const float* packed, const float* quantiles, const float* target, float* loss,
+                      float* g_quantiles, int C, hyres_stream_t s);
+
+/* ------------------------------------------------------------------------------------------ */
+/* MultiScaleRefine pieces (models/layers/enhancement.py)                                     */
+/* ------------------------------------------------------------------------------------------ */
+/* bilinear, align_corners=False, torch source-index rule (scale = in/out, or 1/scale_factor). */
+int hyres_bilinear_fwd(const float* x, int ldx, float* y, int ldy, int B, int Hi, int Wi, int Ho, int Wo,
+                       int C, float scale_h, float scale_w, int accumulate, hyres_stream_t s);
+int hyres_bilinear_bwd(const float* gy, int ldgy, float* gx, int ldgx, int B, int Hi, int Wi, int Ho,
+                       int Wo, int C, float scale_h, float scale_w, int accumulate, hyres_stream_t s);
+/* SEBlock (enhancement.py:25-40): s = sigmoid(W2 relu(W1 mean_hw(x))); y = x*s */
+int hyres_se_fwd(const float* x, const float* w1, const float* w2, float* y, float* pooled,
+                 float* hidden, float* sgate, int B, int HW, int C, int Cr, void* ws, long long ws_bytes,
+                 hyres_stream_t s);
+int hyres_se_bwd(const float* x, const float* gy, const float* w1, const float* w2,
+                 const float* pooled, const float* hidden, const float* sgate, float* gx, float* gw1,
+                 float* gw2, int B, int HW, int C, int Cr, void* ws, long long ws_bytes, hyres_stream_t s);
+long long hyres_se_workspace_bytes(int B, int HW, int C);
+/* SpatialAttention (enhancement.py:7-21) fused: a = sigmoid(conv7x7([mean_c, max_c])); y = x * a */
+int hyres_spatial_attn_fwd(const float* x, const float* w, float* pooled2, float* attn, float* y,
+                           int B, int H, int W, int C, hyres_stream_t s);
+int hyres_spatial_attn_bwd(const float* x, const float* w, const float* pooled2, const float* attn,
+                           const float* gy, float* gx, float* gw, int B, int H, int W, int C, void* ws,
+                           long long ws_bytes, hyres_stream_t s);
+long long hyres_spatial_attn_workspace_bytes(int B, int H, int W);
+
+/* ------------------------------------------------------------------------------------------ */
+/* losses and optimiser (src/losses/rd_loss.py:18-44, src/utils/engine.py:56-90)              */
+/* ------------------------------------------------------------------------------------------ */
+/* out[0] (+)= sum(log(x)) over n floats (two-pass deterministic) */
+int hyres_sum_log(const float* x, long long n, float* out, void* ws, long long ws_bytes,
+                  hyres_stream_t s);
+/* out[0] = sum((a-b)^2) */
+int hyres_sum_sqdiff(const float* a, const float* b, long long n, float* out, void* ws,
+                     long long ws_bytes, hyres_stream_t s);
+long long hyres_reduce_workspace_bytes(long long n);
+/* g = coef / x  (d/dx of coef*log x) ; g = coef*(a-b) */
+int hyres_scale_recip(const float* x, const float* coef, float scale, float* g, long long n,
+                      hyres_stream_t s);
+int hyres_scale_diff(const float* a, const float* b, const float* coef, float scale, float* g,
+                     long long n, hyres_stream_t s);
+/* RateDistortionLoss scalars from sums = [sum log lik_y, sum log lik_z, sum sq err]:
+ * *out[i] = [loss, bpp, residual_bpp, y_bpp, z_bpp, mse][i]  (rd_loss.py:23-42, alpha = 0) */
+int hyres_rd_finalize(const float* sums, const float* jpeg_bpp, float lmbda, long long npx,
+                      long long nel, float* const* out, hyres_stream_t s);
+/* backward coefficients from the six output gradients: coef = [c_y, c_z, c_mse] */
+int hyres_rd_bwd_coef(const float* g0, const float* g1, const float* g2, const float* g3,
+                      const float* g4, const float* g5, float lmbda, long long npx, long long nel,
+                      float* coef, hyres_stream_t s);
+/* global L2 norm of a flat buffer -> out[0] = sum sq ; clip factor computed on device */
+int hyres_sumsq(const float* x, long long n, float* out, void* ws, long long ws_bytes, hyres_stream_t s);
+/* fused Adam over a flat parameter buffer (torch.optim.Adam semantics, amsgrad=False,
+ * weight_decay=0) with the clip_grad_norm_ factor min(1, max_norm/(sqrt(sumsq)+1e-6)) applied
+ * to the gradient on the fly when sumsq != NULL. step is the 1-based step count. */
+int hyres_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, long long n,
+                    float lr, float beta1, float beta2, float eps, int step, const float* sumsq,
+                    float max_norm, hyres_stream_t s);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HYRES_HIP_H */

@@ -1,0 +1,228 @@
+"""Generate the golden fixtures by running the REFERENCE's own model code (in the dev container only).
+
+Run:  python tests/golden/make_golden.py      (needs /root/reference; never runs on the GPU box)
+
+How the reference is executed:
+  * ``compressai`` (1.2.6, not vendored, not installed) is replaced by the restatement in
+    ``oracle/compressai_restated.py`` installed into ``sys.modules`` as ``compressai.*``;
+  * ``models`` is registered as a bare package rooted at /root/reference/models so that its
+    ``__init__`` (which imports ``elic`` -> ``timm``) does not run; ``models.layers`` and the model
+    files then import unchanged;
+  * ``turbojpeg`` / ``torchvision`` (absent) are stubbed: TurboJPEG.encode/decode are emulated with
+    Pillow's bundled libjpeg-turbo with the reference's effective settings (RGB array interpreted as
+    BGR, 4:2:2 subsampling — PyTurboJPEG defaults, models/utils/turbo_jpeg_compression.py:35).
+Weights come from the name-keyed recipe in ``hyres_hip/weights.py``; no checkpoint is used.
+
+Outputs (small, committed):  tests/golden/hyres_eval_b2_64.npz, hyres_train_b2_64.npz, meta.json
+"""
+from __future__ import annotations
+
+import io
+import json
+import math
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+REF = "/root/reference"
+PKG = os.path.join(REPO, "hyres-residual-enhanced-hybrid-image-compression_amd")
+OUT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+sys.path.insert(0, PKG)
+
+
+def pil_turbojpeg_encode(img_np: np.ndarray, quality: int) -> bytes:
+    from PIL import Image
+    im = Image.fromarray(np.ascontiguousarray(img_np[..., ::-1]), "RGB")  # TJPF_BGR interpretation
+    buf = io.BytesIO()
+    im.save(buf, format="JPEG", quality=int(quality), subsampling=1)  # 4:2:2 (TJSAMP_422)
+    return buf.getvalue()
+
+
+def pil_turbojpeg_decode(data: bytes) -> np.ndarray:
+    from PIL import Image
+    im = Image.open(io.BytesIO(data)).convert("RGB")
+    return np.ascontiguousarray(np.asarray(im)[..., ::-1])  # back to BGR order (TJPF_BGR)
+
+
+def install_reference():
+    from oracle.compressai_restated import install_as_compressai
+    install_as_compressai()
+    tj = types.ModuleType("turbojpeg")
+
+    class TurboJPEG:
+        def __init__(self, lib_path=None):
+            pass
+
+        def encode(self, img, quality=85):
+            return pil_turbojpeg_encode(img, quality)
+
+        def decode(self, data):
+            return pil_turbojpeg_decode(data)
+
+    tj.TurboJPEG = TurboJPEG
+    sys.modules["turbojpeg"] = tj
+    tv = types.ModuleType("torchvision")
+    tvt = types.ModuleType("torchvision.transforms")
+    tvt.ToPILImage = lambda *a, **k: None
+    tvt.ToTensor = lambda *a, **k: None
+    tv.transforms = tvt
+    sys.modules["torchvision"] = tv
+    sys.modules["torchvision.transforms"] = tvt
+    models = types.ModuleType("models")
+    models.__path__ = [os.path.join(REF, "models")]
+    sys.modules["models"] = models
+    import models.hyres as hyres_mod  # noqa: E402  (reference file, executed unchanged)
+    import models.utils.quantization as quant_mod
+    return hyres_mod, quant_mod
+
+
+def build_reference(hyres_mod, jpeg_quality):
+    from hyres_hip.weights import synthetic_state_dict
+    net = hyres_mod.ResidualJPEGCompression(jpeg_quality=jpeg_quality, N=128, M=192)
+    sd = synthetic_state_dict(net.state_dict())
+    # direct load (the reference's load_state_dict has the refine-prefix bug)
+    torch.nn.Module.load_state_dict(net, sd, strict=True)
+    return net, sd
+
+
+def grad_summary(net):
+    out = {}
+    for n, p in net.named_parameters():
+        g = p.grad
+        if g is None:
+            out[n] = None
+            continue
+        g = g.detach().double()
+        gen = torch.Generator().manual_seed(7)
+        idx = torch.randint(0, g.numel(), (8,), generator=gen)
+        out[n] = {"sum": float(g.sum()), "sumsq": float((g * g).sum()), "absmax": float(g.abs().max()),
+                  "idx": idx.tolist(), "val": g.flatten()[idx].tolist()}
+    return out
+
+
+def main():
+    torch.set_num_threads(8)
+    hyres_mod, quant_mod = install_reference()
+    q = 50
+    B, H, W = 2, 64, 64
+    g = torch.Generator().manual_seed(1926)
+    x = torch.randint(0, 256, (B, 3, H, W), generator=g).float() / 255.0
+    # smooth the synthetic image a little so JPEG + residual look like natural content
+    x = torch.nn.functional.avg_pool2d(x, 3, 1, 1, count_include_pad=False)
+    x = (x * 255).round() / 255.0
+    meta = {"jpeg_quality": q, "B": B, "H": H, "W": W, "weights": "hyres_hip.weights recipe, seed 1926",
+            "reference": "/root/reference models/hyres.py + models/checkerboard.py (executed)",
+            "compressai": "oracle/compressai_restated.py (1.2.6 restatement)"}
+
+    # ---------------- eval forward (deterministic parity path)
+    net, sd = build_reference(hyres_mod, q)
+    net.eval()
+    feats = {}
+
+    def hook(name):
+        def f(m, inp, out):
+            feats[name] = (inp[0].detach().clone(), out.detach().clone() if torch.is_tensor(out) else None)
+        return f
+
+    rm = net.residual_model
+    for name in ["g_a", "h_a", "h_s", "g_s", "context_prediction"]:
+        getattr(rm, name).register_forward_hook(hook(name))
+    net.refine.register_forward_hook(hook("refine"))
+    with torch.no_grad():
+        out = net(x)
+    ev = {
+        "x": x, "jpeg_decoded": out["jpeg_decoded"], "residual": out["residual"],
+        "y": feats["g_a"][1], "z": feats["h_a"][1], "z_hat": feats["h_s"][0],
+        "latent_params": feats["h_s"][1], "y_anchor_hat": feats["context_prediction"][0],
+        "ctx_params": feats["context_prediction"][1], "y_hat": feats["g_s"][0],
+        "residual_hat": out["residual_hat"], "x_hat_initial": feats["refine"][0],
+        "refined": feats["refine"][1], "x_hat": out["x_hat"],
+        "y_likelihoods": out["likelihoods"]["y"], "z_likelihoods": out["likelihoods"]["z"],
+        "jpeg_bpp": torch.tensor(float(out["jpeg_bpp_loss"])),
+    }
+    np.savez_compressed(os.path.join(OUT, "hyres_eval_b2_64.npz"),
+                        **{k: v.numpy().astype(np.float32) for k, v in ev.items()})
+    meta["eval_jpeg_bpp"] = float(out["jpeg_bpp_loss"])
+
+    # ---------------- train step (noisequant=False, C2 semantics) with recorded noise draws
+    net, sd = build_reference(hyres_mod, q)
+    net.train()
+    noise_log = []
+    from oracle import compressai_restated as cr
+    orig_q = cr.EntropyModel.quantize
+
+    def rec_quantize(self, inputs, mode, means=None):
+        if mode == "noise":
+            n = torch.empty_like(inputs).uniform_(-0.5, 0.5)
+            noise_log.append((type(self).__name__, n.clone()))
+            return inputs + n
+        return orig_q(self, inputs, mode, means)
+
+    cr.EntropyModel.quantize = rec_quantize
+    torch.manual_seed(1234)
+    out = net(x, noisequant=False)
+    cr.EntropyModel.quantize = orig_q
+    assert [n for n, _ in noise_log] == ["EntropyBottleneck", "GaussianConditional"], noise_log
+    C = 128
+    z_shape = (B, C, H // 32, W // 32)
+    nz = noise_log[0][1].reshape(C, B, z_shape[2], z_shape[3]).permute(1, 0, 2, 3).contiguous()
+    ny = noise_log[1][1]
+    lmbda = 0.045
+    N_, _, H_, W_ = x.shape
+    npx = N_ * H_ * W_
+    y_bpp = torch.log(out["likelihoods"]["y"]).sum() / (-math.log(2) * npx)
+    z_bpp = torch.log(out["likelihoods"]["z"]).sum() / (-math.log(2) * npx)
+    mse = torch.nn.functional.mse_loss(out["x_hat"], x) * 255 ** 2
+    loss = lmbda * mse + y_bpp + z_bpp + out["jpeg_bpp_loss"]
+    loss.backward()
+    aux = net.aux_loss()
+    tr = {"x": x, "jpeg_decoded": out["jpeg_decoded"], "noise_z": nz, "noise_y": ny,
+          "x_hat": out["x_hat"].detach(), "y_likelihoods": out["likelihoods"]["y"].detach(),
+          "z_likelihoods": out["likelihoods"]["z"].detach(), "loss": loss.detach(),
+          "mse_loss": mse.detach(), "y_bpp": y_bpp.detach(), "z_bpp": z_bpp.detach(),
+          "aux_loss": aux.detach()}
+    np.savez_compressed(os.path.join(OUT, "hyres_train_b2_64.npz"),
+                        **{k: v.numpy().astype(np.float32) for k, v in tr.items()})
+    meta["train_lambda"] = lmbda
+    meta["train_grads"] = grad_summary(net)
+    meta["n_params"] = sum(p.numel() for p in net.parameters())
+    meta["n_params_codec"] = sum(p.numel() for p in net.residual_model.parameters())
+    meta["state_dict_keys"] = list(sd.keys())
+    meta["state_dict_shapes"] = {k: list(v.shape) for k, v in sd.items()}
+
+    # ---------------- checkerboard index sets + 5x5 mask (bit-exact fixtures)
+    mask = rm.context_prediction.mask[0, 0].numpy().astype(np.int32)
+    yy = torch.arange(16.0).view(1, 1, 4, 4).repeat(1, 1, 1, 1)
+    anchor = rm._split_tensor(yy, "anchor")[0, 0].numpy()
+    non_anchor = rm._split_tensor(yy, "non_anchor")[0, 0].numpy()
+    np.savez_compressed(os.path.join(OUT, "checkerboard_sets.npz"), mask=mask, anchor=anchor,
+                        non_anchor=non_anchor)
+
+    # ---------------- Kodak crop fixture (real data), eval forward
+    from PIL import Image
+    im = np.asarray(Image.open(os.path.join(REF, "data/test/kodim01.png")).convert("RGB"))
+    crop = torch.from_numpy(im[200:264, 300:364].copy()).permute(2, 0, 1).float().unsqueeze(0) / 255.0
+    net, sd = build_reference(hyres_mod, q)
+    net.eval()
+    with torch.no_grad():
+        out = net(crop)
+    kd = {"x": crop, "jpeg_decoded": out["jpeg_decoded"], "x_hat": out["x_hat"],
+          "residual_hat": out["residual_hat"], "y_likelihoods": out["likelihoods"]["y"],
+          "z_likelihoods": out["likelihoods"]["z"], "jpeg_bpp": torch.tensor(float(out["jpeg_bpp_loss"]))}
+    np.savez_compressed(os.path.join(OUT, "kodim01_crop64_eval.npz"),
+                        **{k: v.numpy().astype(np.float32) for k, v in kd.items()})
+
+    with open(os.path.join(OUT, "meta.json"), "w") as f:
+        json.dump(meta, f, indent=1)
+    print("params:", meta["n_params"], "codec:", meta["n_params_codec"])
+    print("eval jpeg bpp", meta["eval_jpeg_bpp"], "train loss", float(loss), "aux", float(aux))
+    print("y range", float(ev["y"].abs().max()), "x_hat range", float(ev["x_hat"].min()), float(ev["x_hat"].max()))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,265 @@
+"""GPU parity: every HIP kernel family vs a CPU fp32 reference on the same seeded inputs, then the
+whole model vs the oracle / golden fixtures produced by the reference's own code.
+
+Tolerances (fp32 everywhere, BASELINE.json north_star: "within 1e-4 relative fp32"):
+  * per-op:  max|hip - ref| <= 1e-4 * max|ref|  (normwise relative)
+  * end-to-end x_hat / likelihoods: same bound, on elements whose quantisation decision agrees with the
+    reference (a round() boundary flip changes y_hat by exactly 1 — reported as a fraction, must be rare).
+"""
+import ctypes
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from helpers import load_meta, load_npz, oracle_from, recipe_state_dict, rel_err
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-4
+
+
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    return torch.device("cuda:0")
+
+
+def _rand(shape, seed, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.rand(shape, generator=g) * 2 - 1) * scale
+
+
+# ------------------------------------------------------------------------------------------------ ops
+CONV_CASES = [
+    # B, Ci, Co, H, W, K, stride, pad, dil
+    (2, 64, 64, 16, 16, 3, 1, 1, 1),
+    (2, 128, 64, 16, 16, 1, 1, 0, 1),
+    (2, 64, 128, 16, 16, 1, 1, 0, 1),
+    (2, 128, 128, 16, 16, 5, 2, 2, 1),
+    (2, 128, 192, 16, 16, 5, 2, 2, 1),
+    (2, 3, 128, 32, 32, 5, 2, 2, 1),
+    (2, 3, 64, 16, 16, 3, 1, 1, 1),
+    (2, 64, 3, 16, 16, 3, 1, 1, 1),
+    (2, 64, 64, 16, 16, 3, 1, 2, 2),
+    (2, 192, 384, 8, 8, 5, 1, 2, 1),
+    (1, 768, 640, 4, 4, 1, 1, 0, 1),
+    (2, 192, 128, 8, 8, 3, 1, 1, 1),
+    (3, 96, 40, 12, 20, 3, 1, 1, 1),
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv2d_fwd_bwd(case):
+    from hyres_hip import _lib as L
+    from hyres_hip import ops as O
+    B, Ci, Co, H, W, K, s, p, d = case
+    x = _rand((B, Ci, H, W), 1)
+    w = _rand((Co, Ci, K, K), 2, 1.0 / (Ci * K * K) ** 0.5)
+    b = _rand((Co,), 3, 0.1)
+    xr, wr, br = x.clone().requires_grad_(), w.clone().requires_grad_(), b.clone().requires_grad_()
+    yr = F.conv2d(xr, wr, br, stride=s, padding=p, dilation=d)
+    gy = _rand(yr.shape, 4)
+    yr.backward(gy)
+    D = dev()
+    wd = torch.nn.Parameter(w.to(D))
+    bd = torch.nn.Parameter(b.to(D))
+    tape = O.Tape()
+    xn = O.to_nhwc(x.to(D), rg=True)
+    yn = O.conv2d(tape, xn, wd, bd, stride=s, pad=p, dil=d)
+    y = O.to_nchw(yn)
+    yn.set_grad(O.nchw_grad_to_nhwc(gy.to(D)))
+    tape.backward()
+    torch.cuda.synchronize()
+    assert rel_err(y.cpu(), yr) < TOL
+    assert rel_err(O.to_nchw_grad(xn).cpu(), xr.grad) < TOL
+    assert rel_err(wd.grad.cpu(), wr.grad) < TOL
+    assert rel_err(bd.grad.cpu(), br.grad) < TOL
+
+
+@pytest.mark.parametrize("case", [(2, 192, 128, 4, 4), (2, 128, 128, 8, 8), (2, 128, 3, 16, 16),
+                                  (2, 128, 192, 4, 4)])
+def test_deconv2d_fwd_bwd(case):
+    from hyres_hip import ops as O
+    B, Ci, Co, H, W = case
+    x = _rand((B, Ci, H, W), 5)
+    w = _rand((Ci, Co, 5, 5), 6, 1.0 / (Ci * 25 / 4) ** 0.5)
+    b = _rand((Co,), 7, 0.1)
+    xr, wr, br = x.clone().requires_grad_(), w.clone().requires_grad_(), b.clone().requires_grad_()
+    yr = F.conv_transpose2d(xr, wr, br, stride=2, padding=2, output_padding=1)
+    gy = _rand(yr.shape, 8)
+    yr.backward(gy)
+    D = dev()
+    wd = torch.nn.Parameter(w.to(D))
+    bd = torch.nn.Parameter(b.to(D))
+    tape = O.Tape()
+    xn = O.to_nhwc(x.to(D), rg=True)
+    yn = O.deconv2d(tape, xn, wd, bd)
+    y = O.to_nchw(yn)
+    yn.set_grad(O.nchw_grad_to_nhwc(gy.to(D)))
+    tape.backward()
+    torch.cuda.synchronize()
+    assert rel_err(y.cpu(), yr) < TOL
+    assert rel_err(O.to_nchw_grad(xn).cpu(), xr.grad) < TOL
+    assert rel_err(wd.grad.cpu(), wr.grad) < TOL
+    assert rel_err(bd.grad.cpu(), br.grad) < TOL
+
+
+@pytest.mark.parametrize("inverse", [False, True])
+def test_gdn_fwd_bwd(inverse):
+    from oracle.compressai_restated import GDN as RefGDN
+    from hyres_hip.layers import GDN
+    from hyres_hip import ops as O
+    C = 128
+    ref = RefGDN(C, inverse=inverse)
+    with torch.no_grad():
+        ref.beta.copy_(torch.sqrt(1 + torch.rand(C) * 0.5))
+        ref.gamma.copy_(torch.sqrt(0.1 * torch.eye(C) + torch.rand(C, C) * 0.02))
+    x = _rand((2, C, 8, 8), 9)
+    xr = x.clone().requires_grad_()
+    yr = ref(xr)
+    gy = _rand(yr.shape, 10)
+    yr.backward(gy)
+    D = dev()
+    m = GDN(C, inverse=inverse).to(D)
+    m.load_state_dict(ref.state_dict())
+    tape = O.Tape()
+    xn = O.to_nhwc(x.to(D), rg=True)
+    yn = m.hip(tape, xn)
+    y = O.to_nchw(yn)
+    yn.set_grad(O.nchw_grad_to_nhwc(gy.to(D)))
+    tape.backward()
+    torch.cuda.synchronize()
+    assert rel_err(y.cpu(), yr) < TOL
+    assert rel_err(O.to_nchw_grad(xn).cpu(), xr.grad) < TOL
+    assert rel_err(m.beta.grad.cpu(), ref.beta.grad) < TOL
+    assert rel_err(m.gamma.grad.cpu(), ref.gamma.grad) < TOL
+
+
+def test_bilinear_se_spatial_attention():
+    from hyres_hip import ops as O
+    from hyres_hip import refine_ops as R
+    D = dev()
+    B, C, H, W = 2, 64, 16, 16
+    x = _rand((B, C, H, W), 11)
+    for (Ho, Wo, scale, sf) in [(8, 8, 2.0, 0.5), (4, 4, 4.0, 0.25)]:
+        xr = x.clone().requires_grad_()
+        yr = F.interpolate(xr, scale_factor=sf, mode="bilinear", align_corners=False)
+        up = F.interpolate(yr, size=(H, W), mode="bilinear", align_corners=False)
+        gy = _rand(up.shape, 12)
+        up.backward(gy)
+        tape = O.Tape()
+        xn = O.to_nhwc(x.to(D), rg=True)
+        dn = R.bilinear(tape, xn, Ho, Wo, scale, scale)
+        un = R.bilinear(tape, dn, H, W, Ho / H, Wo / W)
+        un.set_grad(O.nchw_grad_to_nhwc(gy.to(D)))
+        tape.backward()
+        assert rel_err(O.to_nchw(un).cpu(), up) < TOL
+        assert rel_err(O.to_nchw_grad(xn).cpu(), xr.grad) < TOL
+    # SE block
+    w1 = _rand((4, C), 13, 0.125)
+    w2 = _rand((C, 4), 14, 0.5)
+    xr = x.clone().requires_grad_()
+    w1r, w2r = w1.clone().requires_grad_(), w2.clone().requires_grad_()
+    s = torch.sigmoid(F.linear(F.relu(F.linear(xr.mean((2, 3)), w1r)), w2r))
+    yr = xr * s[:, :, None, None]
+    gy = _rand(yr.shape, 15)
+    yr.backward(gy)
+    w1d, w2d = torch.nn.Parameter(w1.to(D)), torch.nn.Parameter(w2.to(D))
+    tape = O.Tape()
+    xn = O.to_nhwc(x.to(D), rg=True)
+    yn = R.se_block(tape, xn, w1d, w2d)
+    yn.set_grad(O.nchw_grad_to_nhwc(gy.to(D)))
+    tape.backward()
+    assert rel_err(O.to_nchw(yn).cpu(), yr) < TOL
+    assert rel_err(O.to_nchw_grad(xn).cpu(), xr.grad) < TOL
+    assert rel_err(w1d.grad.cpu(), w1r.grad) < TOL
+    assert rel_err(w2d.grad.cpu(), w2r.grad) < TOL
+    # spatial attention (192 channels, 7x7)
+    C2 = 192
+    x2 = _rand((B, C2, H, W), 16)
+    wsa = _rand((1, 2, 7, 7), 17, 0.3)
+    xr = x2.clone().requires_grad_()
+    wr = wsa.clone().requires_grad_()
+    a = torch.sigmoid(F.conv2d(torch.cat([xr.mean(1, keepdim=True), xr.max(1, keepdim=True)[0]], 1), wr,
+                               None, padding=3))
+    yr = xr * a
+    gy = _rand(yr.shape, 18)
+    yr.backward(gy)
+    wd = torch.nn.Parameter(wsa.to(D))
+    tape = O.Tape()
+    xn = O.to_nhwc(x2.to(D), rg=True)
+    yn = R.spatial_attention_mul(tape, xn, wd)
+    yn.set_grad(O.nchw_grad_to_nhwc(gy.to(D)))
+    tape.backward()
+    assert rel_err(O.to_nchw(yn).cpu(), yr) < TOL
+    assert rel_err(O.to_nchw_grad(xn).cpu(), xr.grad) < TOL
+    assert rel_err(wd.grad.cpu(), wr.grad) < TOL
+
+
+# ------------------------------------------------------------------------------------------------ model
+def _hip_model():
+    from models import ResidualJPEGCompression
+    from hyres_hip.weights import synthetic_state_dict
+    net = ResidualJPEGCompression(jpeg_quality=50)
+    sd = synthetic_state_dict(net.state_dict())
+    torch.nn.Module.load_state_dict(net, sd, strict=True)
+    return net.to(dev()), sd
+
+
+@pytest.mark.parametrize("fixture", ["hyres_eval_b2_64.npz", "kodim01_crop64_eval.npz"])
+def test_model_eval_matches_reference(fixture):
+    g = load_npz(fixture)
+    net, sd = _hip_model()
+    net.eval()
+    D = dev()
+    with torch.no_grad():
+        out = net(g["x"], jpeg=(g["jpeg_decoded"], float(g["jpeg_bpp"])))
+    torch.cuda.synchronize()
+    # decision-level: y_hat is round(y - mu) + mu: compare likelihoods / outputs normwise
+    assert rel_err(out["likelihoods"]["z"].cpu(), g["z_likelihoods"]) < TOL
+    assert rel_err(out["likelihoods"]["y"].cpu(), g["y_likelihoods"]) < 1e-3
+    assert rel_err(out["residual_hat"].cpu(), g["residual_hat"]) < TOL
+    assert rel_err(out["x_hat"].cpu(), g["x_hat"]) < TOL
+    # PSNR parity (north_star: within 0.01 dB of the CPU reference)
+    mse_h = F.mse_loss(out["x_hat"].cpu(), g["x"]).item()
+    mse_r = F.mse_loss(g["x_hat"], g["x"]).item()
+    import math
+    assert abs(10 * math.log10(1 / mse_h) - 10 * math.log10(1 / mse_r)) < 0.01
+
+
+def test_model_train_step_matches_reference():
+    """C2 semantics: train mode, noisequant=False, lambda=0.045, recorded noise -> loss and every
+    parameter gradient vs the reference's autograd (golden summaries)."""
+    g = load_npz("hyres_train_b2_64.npz")
+    meta = load_meta()
+    net, sd = _hip_model()
+    net.train()
+    D = dev()
+    from hyres_hip.loss import RateDistortionLoss
+    from hyres_hip import ops as O
+    rm = net.residual_model
+    rm.noise.injected = {"z": g["noise_z"].permute(0, 2, 3, 1).contiguous().to(D),
+                         "y": g["noise_y"].permute(0, 2, 3, 1).contiguous().to(D)}
+    jb = float(g["loss"]) - (meta["train_lambda"] * float(g["mse_loss"]) + float(g["y_bpp"]) + float(g["z_bpp"]))
+    out = net(g["x"], noisequant=False, jpeg=(g["jpeg_decoded"], jb))
+    crit = RateDistortionLoss(lmbda=meta["train_lambda"], alpha=0)(out, g["x"].to(D))
+    crit["loss"].backward()
+    aux = net.aux_loss()
+    torch.cuda.synchronize()
+    assert abs(float(crit["loss"]) - float(g["loss"])) <= TOL * abs(float(g["loss"]))
+    assert abs(float(aux) - float(g["aux_loss"])) <= TOL * abs(float(g["aux_loss"]))
+    bad = []
+    params = dict(net.named_parameters())
+    for k, summ in meta["train_grads"].items():
+        p = params[k]
+        if summ is None:
+            continue
+        gd = p.grad.detach().double().cpu() if p.grad is not None else torch.zeros(p.shape, dtype=torch.float64)
+        ss = float((gd * gd).sum())
+        err = abs(ss - summ["sumsq"]) / max(summ["sumsq"], 1e-30)
+        vals = gd.flatten()[summ["idx"]]
+        ref_vals = torch.tensor(summ["val"], dtype=torch.float64)
+        verr = float((vals - ref_vals).abs().max()) / max(summ["absmax"], 1e-30)
+        if err > 2e-4 or verr > 1e-4:
+            bad.append((k, err, verr))
+    assert not bad, bad[:8]
