@@ -248,18 +248,66 @@ def test_model_train_step_matches_reference():
     torch.cuda.synchronize()
     assert abs(float(crit["loss"]) - float(g["loss"])) <= TOL * abs(float(g["loss"]))
     assert abs(float(aux) - float(g["aux_loss"])) <= TOL * abs(float(g["aux_loss"]))
+    # fp64 oracle gradients (the golden summaries come from the fp32 reference run; the oracle is pinned
+    # to them in test_oracle_golden.py).  Gradient accumulated through ~80 layers: tensors must agree
+    # normwise to 1e-3; the scalar PReLU slopes are sums of sign-mixed terms g*x (x<=0), so their
+    # error is bounded relative to the sum of |terms| (a cancelled sum amplifies fp32 rounding).
+    g64, prelu_terms = _oracle_grads_fp64(g, meta, jb)
     bad = []
     params = dict(net.named_parameters())
-    for k, summ in meta["train_grads"].items():
+    for k, ref in g64.items():
         p = params[k]
-        if summ is None:
-            continue
         gd = p.grad.detach().double().cpu() if p.grad is not None else torch.zeros(p.shape, dtype=torch.float64)
-        ss = float((gd * gd).sum())
-        err = abs(ss - summ["sumsq"]) / max(summ["sumsq"], 1e-30)
-        vals = gd.flatten()[summ["idx"]]
-        ref_vals = torch.tensor(summ["val"], dtype=torch.float64)
-        verr = float((vals - ref_vals).abs().max()) / max(summ["absmax"], 1e-30)
-        if err > 2e-4 or verr > 1e-4:
-            bad.append((k, err, verr))
+        scale = float(ref.abs().max())
+        if scale == 0.0:
+            continue
+        err = float((gd - ref).abs().max())
+        if k in prelu_terms:
+            if err > 5e-4 * prelu_terms[k]:
+                bad.append((k, err, prelu_terms[k]))
+        elif err > 1e-3 * scale:
+            bad.append((k, err / scale))
+        summ = meta["train_grads"].get(k)
+        if summ is not None and k not in prelu_terms:
+            ss = float((gd * gd).sum())
+            if abs(ss - summ["sumsq"]) > 2e-3 * max(summ["sumsq"], 1e-30):
+                bad.append((k, "sumsq", ss, summ["sumsq"]))
     assert not bad, bad[:8]
+
+
+def _oracle_grads_fp64(g, meta, jpeg_bpp):
+    from oracle import Oracle, rd_loss
+    sd = recipe_state_dict()
+    sd2 = {}
+    params = []
+    for k, v in sd.items():
+        t = v.clone().double() if v.is_floating_point() else v.clone()
+        if t.is_floating_point() and not k.endswith(("pedestal", "bound", "mask", "target", "scale_bound",
+                                                      "scale_table")):
+            t.requires_grad_(True)
+            params.append(k)
+        sd2[k] = t
+    captured = []
+
+    class Rec(Oracle):
+        @staticmethod
+        def prelu(x, a):
+            y = F.prelu(x, a)
+            if y.requires_grad:
+                y.register_hook(lambda gg, x=x, a=a: captured.append((a, x.detach(), gg.detach())))
+            return y
+
+    orc = Rec(sd2)
+    torch.set_num_threads(8)
+    noise = {"z": g["noise_z"].double(), "y": g["noise_y"].double()}
+    out = orc.forward(g["x"].double(), g["jpeg_decoded"].double(), 0.0, training=True, noise=noise)
+    out["jpeg_bpp_loss"] = torch.tensor(jpeg_bpp, dtype=torch.float64)
+    crit = rd_loss(out, g["x"].double(), meta["train_lambda"])
+    crit["loss"].backward()
+    grads = {k: sd2[k].grad for k in params if sd2[k].grad is not None}
+    by_id = {id(sd2[k]): k for k in params}
+    terms = {}
+    for a, x, gg in captured:
+        k = by_id[id(a)]
+        terms[k] = terms.get(k, 0.0) + float((gg * x).abs()[x <= 0].sum())
+    return grads, terms
