@@ -470,24 +470,64 @@ __global__ void weight_prep_kernel(const PrepArgs a) {
     }
 }
 
-__global__ void colsum_partial_kernel(const float* x, int P, int C, int ld, int rows_per_block,
-                                      float* part) {
-    // block: 256 threads; each thread owns channel column(s) c = threadIdx.x + 256*k
+// Column sums of a [P][C] (pixel stride ld) matrix, deterministic two-pass.
+// Pass 1: a block owns a row range; its 256 threads are laid out TR x TC over (rows, channel groups of
+// VEC floats) so every wave reads whole contiguous rows; the TR partial rows are folded through LDS.
+template <int VEC>
+__global__ __launch_bounds__(256) void colsum_partial_kernel(const float* x, int P, int C, int ld,
+                                                             int rows_per_block, float* part) {
+    __shared__ float red[256 * VEC];
+    const int groups = C / VEC;                       // channel groups
+    const int TC = groups < 256 ? groups : 256;        // threads across channels
+    const int TR = 256 / TC;                           // threads across rows
+    const int tc = threadIdx.x % TC, tr = threadIdx.x / TC;
     const int r0 = blockIdx.x * rows_per_block;
     const int r1 = min(P, r0 + rows_per_block);
-    for (int c = threadIdx.x; c < C; c += blockDim.x) {
-        float s = 0.f;
-        for (int r = r0; r < r1; ++r) s += x[(long long)r * ld + c];
-        part[(long long)blockIdx.x * C + c] = s;
+    for (int g0 = 0; g0 < groups; g0 += TC) {
+        const int gi = g0 + tc;
+        float acc[VEC];
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) acc[v] = 0.f;
+        if (tr < TR && gi < groups) {
+            for (int r = r0 + tr; r < r1; r += TR) {
+                const float* p = x + (long long)r * ld + gi * VEC;
+                if constexpr (VEC == 4) {
+                    float4 q = *reinterpret_cast<const float4*>(p);
+                    acc[0] += q.x; acc[1] += q.y; acc[2] += q.z; acc[3] += q.w;
+                } else {
+                    acc[0] += p[0];
+                }
+            }
+        }
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) red[threadIdx.x * VEC + v] = acc[v];
+        __syncthreads();
+        if (tr == 0 && gi < groups) {
+            for (int k = 1; k < TR; ++k)
+#pragma unroll
+                for (int v = 0; v < VEC; ++v) acc[v] += red[(k * TC + tc) * VEC + v];
+#pragma unroll
+            for (int v = 0; v < VEC; ++v) part[(long long)blockIdx.x * C + gi * VEC + v] = acc[v];
+        }
+        __syncthreads();
     }
 }
 
-__global__ void colsum_final_kernel(const float* part, int nb, int C, float* dst, int accumulate) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
+// Pass 2: block handles 64 columns; 4 thread rows split the partials, folded through LDS.
+__global__ __launch_bounds__(256) void colsum_final_kernel(const float* part, int nb, int C, float* dst,
+                                                           int accumulate) {
+    __shared__ float red[256];
+    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int q = threadIdx.x >> 6;
     float s = 0.f;
-    for (int b = 0; b < nb; ++b) s += part[(long long)b * C + c];
-    dst[c] = accumulate ? dst[c] + s : s;
+    if (c < C)
+        for (int b = q; b < nb; b += 4) s += part[(long long)b * C + c];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    if (q == 0 && c < C) {
+        s = red[threadIdx.x] + red[threadIdx.x + 64] + red[threadIdx.x + 128] + red[threadIdx.x + 192];
+        dst[c] = accumulate ? dst[c] + s : s;
+    }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -793,25 +833,31 @@ int hyres_conv_wgrad(const hyres_wgrad_desc* d, const float* pp, const float* qq
     return HY_LAUNCH_CHECK("wgrad_reduce_kernel");
 }
 
-long long hyres_colsum_workspace_bytes(int P, int C) {
-    int rows = 256;
-    int nb = std::min(ceil_div(P, rows), 2048);
-    return (long long)nb * C * 4;
+static int colsum_blocks(int P) {
+    // >= 128 rows per block, at most 512 partial rows
+    int nb = std::max(1, std::min(ceil_div(P, 128), 512));
+    int rows = ceil_div(P, nb);
+    return ceil_div(P, rows);
 }
+
+long long hyres_colsum_workspace_bytes(int P, int C) { return (long long)colsum_blocks(P) * C * 4; }
 
 int hyres_colsum(const float* x, int P, int C, int ld, float* dst, int accumulate, void* ws,
                  long long ws_bytes, hyres_stream_t s) {
     HY_REQUIRE(x && dst && P > 0 && C > 0, HYRES_E_ARG, "colsum: bad args");
-    int nb = std::min(ceil_div(P, 256), 2048);
-    int rows = ceil_div(P, nb);
-    nb = ceil_div(P, rows);
+    const int nb = colsum_blocks(P);
+    const int rows = ceil_div(P, nb);
     HY_REQUIRE(ws && ws_bytes >= (long long)nb * C * 4, HYRES_E_WORKSPACE, "colsum: workspace");
     hipStream_t st = as_stream(s);
-    hipLaunchKernelGGL(colsum_partial_kernel, dim3(nb), dim3(256), 0, st, x, P, C, ld, rows, (float*)ws);
+    const bool vec = (C % 4 == 0) && (ld % 4 == 0) && aligned16(x);
+    if (vec)
+        hipLaunchKernelGGL(colsum_partial_kernel<4>, dim3(nb), dim3(256), 0, st, x, P, C, ld, rows, (float*)ws);
+    else
+        hipLaunchKernelGGL(colsum_partial_kernel<1>, dim3(nb), dim3(256), 0, st, x, P, C, ld, rows, (float*)ws);
     int rc = HY_LAUNCH_CHECK("colsum_partial");
     if (rc) return rc;
-    hipLaunchKernelGGL(colsum_final_kernel, dim3(ceil_div(C, 256)), dim3(256), 0, st, (const float*)ws, nb, C,
-                       dst, accumulate);
+    hipLaunchKernelGGL(colsum_final_kernel, dim3(ceil_div(C, 64)), dim3(256), 0, st, (const float*)ws, nb, C, dst,
+                       accumulate);
     return HY_LAUNCH_CHECK("colsum_final");
 }
 

@@ -320,12 +320,19 @@ __global__ void sa_bwd_conv_kernel(const float* glogit, const float* pooled2, co
         __syncthreads();
     }
 }
+// one block per weight tap: 256 threads fold the per-block partials (deterministic order)
 __global__ void sa_bwd_wfinal_kernel(const float* wpart, int nb, float* gw) {
-    const int k = threadIdx.x;
-    if (k >= 98) return;
+    __shared__ float red[256];
+    const int k = blockIdx.x;
     float s = 0.f;
-    for (int b = 0; b < nb; ++b) s += wpart[(long long)b * 98 + k];
-    gw[k] += s;
+    for (int b = threadIdx.x; b < nb; b += 256) s += wpart[(long long)b * 98 + k];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) gw[k] += red[0];
 }
 // bwd 3: gx = gy*a + g_avg/C + [c == argmax] * g_max     (one wave per pixel)
 __global__ void sa_bwd_x_kernel(const float* x, const float* gy, const float* attn, const float* gpooled2, float* gx,
@@ -467,7 +474,7 @@ int hyres_spatial_attn_bwd(const float* x, const float* w, const float* pooled2,
                        H, W);
     rc = HY_LAUNCH_CHECK("sa_bwd_conv");
     if (rc) return rc;
-    hipLaunchKernelGGL(sa_bwd_wfinal_kernel, dim3(1), dim3(128), 0, st, (const float*)wpart, nb, gw);
+    hipLaunchKernelGGL(sa_bwd_wfinal_kernel, dim3(98), dim3(256), 0, st, (const float*)wpart, nb, gw);
     rc = HY_LAUNCH_CHECK("sa_bwd_wfinal");
     if (rc) return rc;
     hipLaunchKernelGGL(sa_bwd_x_kernel, dim3((unsigned)((P + 3) / 4)), dim3(256), 0, st, x, gy, attn,

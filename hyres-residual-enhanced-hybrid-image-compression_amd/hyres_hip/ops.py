@@ -157,6 +157,27 @@ class Tape:
         self.ops.clear()
 
 
+class Trace:
+    """Debug/parity hook: when ``Trace.nodes`` is a dict, named activations are kept (by reference) so
+    tests can read their values (``value``) and, after backward, their gradients (``grad``)."""
+
+    nodes = None
+
+    @classmethod
+    def add(cls, name: str, node: "Node") -> None:
+        if cls.nodes is not None:
+            cls.nodes[name] = node
+
+    @classmethod
+    def value(cls, name: str) -> torch.Tensor:
+        return to_nchw(cls.nodes[name])
+
+    @classmethod
+    def grad(cls, name: str) -> Optional[torch.Tensor]:
+        n = cls.nodes[name]
+        return None if n.grad() is None else to_nchw_grad(n)
+
+
 def param_grad(p: torch.nn.Parameter) -> torch.Tensor:
     """param.grad, created zeroed if absent; HIP kernels always accumulate into it."""
     if p.grad is None:

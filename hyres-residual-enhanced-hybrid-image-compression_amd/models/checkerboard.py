@@ -62,6 +62,7 @@ class LightWeightCheckerboard(CompressionModel):
     # ------------------------------------------------------------------ HIP graph
     def hip(self, tape, x: Node, training: bool, noisequant: bool):
         M = self.M
+        T = O.Trace
         y = self.g_a.hip(tape, x)
         z = self.h_a.hip(tape, y)
         z_hat, z_lik = self.entropy_bottleneck.hip(tape, z, training, noisequant, self.noise)
@@ -76,6 +77,9 @@ class LightWeightCheckerboard(CompressionModel):
         y_hat, y_lik = E.checkerboard_nonanchor_gc(tape, y, ya_hat, params_a, params_na, training, noisequant,
                                                    self.noise)
         x_hat = self.g_s.hip(tape, y_hat)
+        for name, n in (("y", y), ("z", z), ("z_hat", z_hat), ("latent_params", latent), ("y_anchor_hat", ya_hat),
+                        ("ctx_params", ctx), ("y_hat", y_hat), ("residual_hat", x_hat)):
+            T.add(name, n)
         return x_hat, y_lik, z_lik
 
     def forward(self, x, noisequant=False):

@@ -40,6 +40,8 @@ class ResidualJPEGCompression(CompressionModel):
         x0 = R.add(tape, jpeg, residual_hat)                              # hyres.py:62
         refined = self.refine.hip(tape, x0)                               # hyres.py:65
         x_hat = R.add_clamp01(tape, x0, refined)                          # hyres.py:66-67
+        O.Trace.add("x_hat_initial", x0)
+        O.Trace.add("x_hat", x_hat)
         return x_hat, y_lik, z_lik, residual, residual_hat
 
     def forward_device(self, x: torch.Tensor, jpeg_decoded: torch.Tensor, jpeg_bpp: float = 0.0,

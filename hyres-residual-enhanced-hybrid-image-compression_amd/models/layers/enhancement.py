@@ -114,4 +114,9 @@ class MultiScaleRefine(HipModule):
         f3 = self.scale3.hip(tape, f3)
         R.bilinear(tape, f3, H, W, (H // 4) / H, (W // 4) / W, out=multi.slice(2 * mid, 3 * mid))
         m = self.spatial_att.hip_mul(tape, multi)
-        return self.fusion.hip(tape, m)
+        out = self.fusion.hip(tape, m)
+        from hyres_hip.ops import Trace
+        for name, n in (("refine_feat", feat), ("refine_f2", f2), ("refine_f3", f3), ("refine_multi", multi),
+                        ("refine_multi_att", m), ("refined", out)):
+            Trace.add(name, n)
+        return out

@@ -313,9 +313,11 @@ class Oracle:
         f1 = block(feat, "scale1")
         f2 = F.interpolate(feat, scale_factor=0.5, mode="bilinear", align_corners=False)
         f2 = block(f2, "scale2")
+        T["refine_f2"] = f2
         f2 = F.interpolate(f2, size=feat.shape[2:], mode="bilinear", align_corners=False)
         f3 = F.interpolate(feat, scale_factor=0.25, mode="bilinear", align_corners=False)
         f3 = block(f3, "scale3")
+        T["refine_f3"] = f3
         f3 = F.interpolate(f3, size=feat.shape[2:], mode="bilinear", align_corners=False)
         multi = torch.cat([f1, f2, f3], 1)
         T["refine_multi"] = multi
@@ -325,6 +327,7 @@ class Oracle:
                                       None, padding=3))
         T["refine_attn"] = attn
         multi = multi * attn
+        T["refine_multi_att"] = multi
         out = self.prelu(self.conv(multi, k + "fusion.0"), self.p(k + "fusion.1.weight"))
         out = self.conv(out, k + "fusion.2", padding=1)
         T["refined"] = out
@@ -344,6 +347,9 @@ class Oracle:
         refined = self.refine(x0, T)
         x_hat = torch.clamp(x0 + refined, 0, 1)
         T["x_hat"] = x_hat
+        for v in T.values():  # keep activation gradients for stage-wise parity diagnostics
+            if torch.is_tensor(v) and v.requires_grad:
+                v.retain_grad()
         return {"x_hat": x_hat, "likelihoods": res["likelihoods"],
                 "jpeg_bpp_loss": torch.tensor(jpeg_bpp), "jpeg_decoded": jpeg_decoded,
                 "residual": residual, "residual_hat": residual_hat}
