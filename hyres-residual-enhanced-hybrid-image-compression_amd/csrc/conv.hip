@@ -26,22 +26,134 @@ struct ConvArgs {
     int ldw;
     float* y;
     hyres_epilogue e;
-    int M;  // B*Hq*Wq
+    int M;       // B*Hq*Wq
+    int nsplit;  // split-K factor (1 = fused epilogue)
+    int cps;     // K chunks per split
+    float* slab; // [nsplit][nphase][M][Co] partials when nsplit > 1
+    int vec4;    // every epilogue operand 16B aligned with ld % 4 == 0 and Co % 4 == 0
 };
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+
+struct EpiChannel {
+    float bias, slope;
+};
+
+__device__ __forceinline__ EpiChannel epi_channel(const hyres_epilogue& e, int n) {
+    EpiChannel c;
+    c.bias = e.bias ? e.bias[n] : 0.f;
+    c.slope = (e.act == HYRES_ACT_PRELU) ? e.slope[0] : 0.f;
+    return c;
+}
+
+// Apply the epilogue to one GEMM result v for output pixel ``pix`` / channel n and store it.
+__device__ __forceinline__ void epi_store(const hyres_epilogue& e, float* y, int ldy, long long pix, int n, float v,
+                                          const EpiChannel& c) {
+    switch (e.kind) {
+        case HYRES_EPI_BIAS: {
+            v += c.bias;
+            if (e.res) v += e.res[pix * e.ldres + n];
+            if (e.out2) e.out2[pix * e.ldo2 + n] = v;  // pre-activation (PReLU backward)
+            if (e.act == HYRES_ACT_RELU) v = fmaxf(v, 0.f);
+            else if (e.act == HYRES_ACT_PRELU) v = v >= 0.f ? v : c.slope * v;
+            break;
+        }
+        case HYRES_EPI_GDN:
+        case HYRES_EPI_IGDN: {
+            const float nv = v + c.bias;
+            const float xv = e.aux0[pix * e.ld0 + n];
+            e.out2[pix * e.ldo2 + n] = nv;
+            v = (e.kind == HYRES_EPI_GDN) ? xv * (1.0f / sqrtf(nv)) : xv * sqrtf(nv);
+            break;
+        }
+        case HYRES_EPI_GDN_BWD:
+        case HYRES_EPI_IGDN_BWD: {
+            const float xv = e.aux0[pix * e.ld0 + n];
+            const float gv = e.aux1[pix * e.ld1 + n];
+            const float nv = e.aux2[pix * e.ld2 + n];
+            const float f = (e.kind == HYRES_EPI_GDN_BWD) ? (1.0f / sqrtf(nv)) : sqrtf(nv);
+            v = 2.0f * xv * v + gv * f;
+            break;
+        }
+        default: break;
+    }
+    float* yp = y + pix * ldy + n;
+    if (e.accumulate) v += *yp;
+    *yp = v;
+}
+
+__device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+
+// float4 variant of epi_store for channels n..n+3 (all operands 16B aligned).
+__device__ __forceinline__ void epi_store4(const hyres_epilogue& e, float* y, int ldy, long long pix, int n, float4 v,
+                                           float slope) {
+    float o[4] = {v.x, v.y, v.z, v.w};
+    switch (e.kind) {
+        case HYRES_EPI_BIAS: {
+            if (e.bias) { const float4 b = ld4(e.bias + n); o[0] += b.x; o[1] += b.y; o[2] += b.z; o[3] += b.w; }
+            if (e.res) {
+                const float4 r = ld4(e.res + pix * e.ldres + n);
+                o[0] += r.x; o[1] += r.y; o[2] += r.z; o[3] += r.w;
+            }
+            if (e.out2) st4(e.out2 + pix * e.ldo2 + n, make_float4(o[0], o[1], o[2], o[3]));
+            if (e.act == HYRES_ACT_RELU) {
+#pragma unroll
+                for (int c = 0; c < 4; ++c) o[c] = fmaxf(o[c], 0.f);
+            } else if (e.act == HYRES_ACT_PRELU) {
+#pragma unroll
+                for (int c = 0; c < 4; ++c) o[c] = o[c] >= 0.f ? o[c] : slope * o[c];
+            }
+            break;
+        }
+        case HYRES_EPI_GDN:
+        case HYRES_EPI_IGDN: {
+            const float4 b = e.bias ? ld4(e.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+            const float4 x = ld4(e.aux0 + pix * e.ld0 + n);
+            const float nv[4] = {o[0] + b.x, o[1] + b.y, o[2] + b.z, o[3] + b.w};
+            const float xv[4] = {x.x, x.y, x.z, x.w};
+            st4(e.out2 + pix * e.ldo2 + n, make_float4(nv[0], nv[1], nv[2], nv[3]));
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                o[c] = (e.kind == HYRES_EPI_GDN) ? xv[c] * (1.0f / sqrtf(nv[c])) : xv[c] * sqrtf(nv[c]);
+            break;
+        }
+        case HYRES_EPI_GDN_BWD:
+        case HYRES_EPI_IGDN_BWD: {
+            const float4 x = ld4(e.aux0 + pix * e.ld0 + n);
+            const float4 gg = ld4(e.aux1 + pix * e.ld1 + n);
+            const float4 nn = ld4(e.aux2 + pix * e.ld2 + n);
+            const float xv[4] = {x.x, x.y, x.z, x.w}, gv[4] = {gg.x, gg.y, gg.z, gg.w}, nv[4] = {nn.x, nn.y, nn.z, nn.w};
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const float f = (e.kind == HYRES_EPI_GDN_BWD) ? (1.0f / sqrtf(nv[c])) : sqrtf(nv[c]);
+                o[c] = 2.0f * xv[c] * o[c] + gv[c] * f;
+            }
+            break;
+        }
+        default: break;
+    }
+    float* yp = y + pix * ldy + n;
+    if (e.accumulate) {
+        const float4 p = ld4(yp);
+        o[0] += p.x; o[1] += p.y; o[2] += p.z; o[3] += p.w;
+    }
+    st4(yp, make_float4(o[0], o[1], o[2], o[3]));
+}
 
 template <int TM, int TN, int WAVES_M, int WAVES_N, int MODE>
 __global__ __launch_bounds__(256) void conv_fwd_kernel(const ConvArgs a) {
     // MODE 0: Ci % 32 == 0 (float4 loads); 1: same + square A (GDN); 2: generic scalar (small Ci).
     constexpr int BM = 32 * TM * WAVES_M;
     constexpr int BN = 32 * TN * WAVES_N;
-    __shared__ __attribute__((aligned(16))) float As[BM * PADK];
-    __shared__ __attribute__((aligned(16))) float Bs[BN * PADK];
+    constexpr int SMEM = ((BM + BN) * PADK > BM * (32 * WAVES_N + 8)) ? (BM + BN) * PADK : BM * (32 * WAVES_N + 8);
+    __shared__ __attribute__((aligned(16))) float smem[SMEM];
+    float* const As = smem;
+    float* const Bs = smem + BM * PADK;
 
     const hyres_conv_geom& g = a.g;
     const int tid = threadIdx.x;
-    const int phase = blockIdx.z;
+    const int phase = blockIdx.z / a.nsplit;
+    const int split = blockIdx.z - phase * a.nsplit;
     const int m0 = blockIdx.x * BM;
     const int n0 = blockIdx.y * BN;
     const int HqWq = g.Hq * g.Wq;
@@ -160,12 +272,14 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const ConvArgs a) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    if (nk > 0) load_chunk(0);
-    for (int kc = 0; kc < nk; ++kc) {
+    const int kbeg = (a.nsplit > 1) ? min(nk, split * a.cps) : 0;
+    const int kend = (a.nsplit > 1) ? min(nk, kbeg + a.cps) : nk;
+    if (kbeg < kend) load_chunk(kbeg);
+    for (int kc = kbeg; kc < kend; ++kc) {
         __syncthreads();
         store_chunk();
         __syncthreads();
-        if (kc + 1 < nk) load_chunk(kc + 1);
+        if (kc + 1 < kend) load_chunk(kc + 1);
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             float4 af[TM], bf[TN];
@@ -190,61 +304,83 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const ConvArgs a) {
         }
     }
 
-    // ---- epilogue
-    const hyres_epilogue& e = a.e;
+    // ---- epilogue: stage the accumulators through LDS one TN column slice at a time (static register
+    // indices), then apply the epilogue row-major: consecutive threads cover consecutive channels of
+    // one NHWC pixel row (float4 when every operand is 16B aligned), each row decoded once.
+    constexpr int CW = 32 * WAVES_N, CP = CW + 8;  // +8: the two lane halves hit disjoint banks
+    float* Cs = smem;
+    const bool split_k = a.nsplit > 1;
+    float* slab = split_k ? a.slab + ((long long)(split * g.nphase + phase) * a.M) * g.Co : nullptr;
+    const bool linear = g.nphase == 1 && g.osh == 1 && g.osw == 1 && g.Ho == g.Hq && g.Wo == g.Wq;
     const int oph = g.oph[phase], opw = g.opw[phase];
-    float slope = 0.f;
-    if (e.act == HYRES_ACT_PRELU) slope = e.slope[0];
+    const float slope = (a.e.act == HYRES_ACT_PRELU) ? a.e.slope[0] : 0.f;
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn) {
-        const int n = n0 + wn * TN * 32 + tn * 32 + lr;
-        if (n >= g.Co) continue;
-        const float bias = e.bias ? e.bias[n] : 0.f;
+        __syncthreads();
 #pragma unroll
-        for (int tm = 0; tm < TM; ++tm) {
+        for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int m = m0 + wm * TM * 32 + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-                if (m >= a.M) continue;
+            for (int r = 0; r < 16; ++r)
+                Cs[(wm * TM * 32 + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh) * CP + wn * 32 + lr] = acc[tm][tn][r];
+        __syncthreads();
+        for (int idx = tid; idx < BM * (CW / 4); idx += 256) {
+            const int row = idx / (CW / 4);
+            const int col = 4 * (idx - row * (CW / 4));
+            const int m = m0 + row;
+            const int n = n0 + (col >> 5) * TN * 32 + tn * 32 + (col & 31);
+            if (m >= a.M || n >= g.Co) continue;
+            const float4 v = *reinterpret_cast<const float4*>(&Cs[row * CP + col]);
+            if (split_k) {
+                float* sp = slab + (long long)m * g.Co + n;
+                if (a.vec4) {
+                    *reinterpret_cast<float4*>(sp) = v;
+                } else {
+                    sp[0] = v.x;
+                    if (n + 1 < g.Co) sp[1] = v.y;
+                    if (n + 2 < g.Co) sp[2] = v.z;
+                    if (n + 3 < g.Co) sp[3] = v.w;
+                }
+                continue;
+            }
+            long long pix = m;
+            if (!linear) {
                 const int b = m / HqWq;
                 const int rr = m - b * HqWq;
                 const int i = rr / g.Wq;
                 const int j = rr - i * g.Wq;
-                const long long pix = (long long)(b * g.Ho + i * g.osh + oph) * g.Wo + j * g.osw + opw;
-                float v = acc[tm][tn][r];
-                switch (e.kind) {
-                    case HYRES_EPI_BIAS: {
-                        v += bias;
-                        if (e.res) v += e.res[pix * e.ldres + n];
-                        if (e.out2) e.out2[pix * e.ldo2 + n] = v;  // pre-activation (PReLU backward)
-                        if (e.act == HYRES_ACT_RELU) v = fmaxf(v, 0.f);
-                        else if (e.act == HYRES_ACT_PRELU) v = v >= 0.f ? v : slope * v;
-                        break;
-                    }
-                    case HYRES_EPI_GDN:
-                    case HYRES_EPI_IGDN: {
-                        const float nv = v + bias;
-                        const float xv = e.aux0[pix * e.ld0 + n];
-                        e.out2[pix * e.ldo2 + n] = nv;
-                        v = (e.kind == HYRES_EPI_GDN) ? xv * (1.0f / sqrtf(nv)) : xv * sqrtf(nv);
-                        break;
-                    }
-                    case HYRES_EPI_GDN_BWD:
-                    case HYRES_EPI_IGDN_BWD: {
-                        const float xv = e.aux0[pix * e.ld0 + n];
-                        const float gv = e.aux1[pix * e.ld1 + n];
-                        const float nv = e.aux2[pix * e.ld2 + n];
-                        const float f = (e.kind == HYRES_EPI_GDN_BWD) ? (1.0f / sqrtf(nv)) : sqrtf(nv);
-                        v = 2.0f * xv * v + gv * f;
-                        break;
-                    }
-                    default: break;
-                }
-                float* yp = a.y + pix * g.ldy + n;
-                if (e.accumulate) v += *yp;
-                *yp = v;
+                pix = (long long)(b * g.Ho + i * g.osh + oph) * g.Wo + j * g.osw + opw;
+            }
+            if (a.vec4) {
+                epi_store4(a.e, a.y, g.ldy, pix, n, v, slope);
+            } else {
+                const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+                    if (n + c < g.Co) epi_store(a.e, a.y, g.ldy, pix, n + c, vv[c], epi_channel(a.e, n + c));
             }
         }
+    }
+}
+
+// split-K reduction + epilogue: one thread per (phase, m, n)
+__global__ void conv_splitk_reduce_kernel(const ConvArgs a) {
+    const hyres_conv_geom& g = a.g;
+    const long long per_phase = (long long)a.M * g.Co;
+    const long long total = per_phase * g.nphase;
+    const int HqWq = g.Hq * g.Wq;
+    for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
+         idx += (long long)gridDim.x * blockDim.x) {
+        const int phase = (int)(idx / per_phase);
+        const long long r = idx - phase * per_phase;
+        const int m = (int)(r / g.Co);
+        const int n = (int)(r - (long long)m * g.Co);
+        float v = 0.f;
+        for (int s = 0; s < a.nsplit; ++s) v += a.slab[((long long)(s * g.nphase + phase) * a.M + m) * g.Co + n];
+        const int b = m / HqWq;
+        const int rr = m - b * HqWq;
+        const int i = rr / g.Wq, j = rr - (rr / g.Wq) * g.Wq;
+        const long long pix = (long long)(b * g.Ho + i * g.osh + g.oph[phase]) * g.Wo + j * g.osw + g.opw[phase];
+        epi_store(a.e, a.y, g.ldy, pix, n, v, epi_channel(a.e, n));
     }
 }
 
@@ -536,15 +672,14 @@ __global__ __launch_bounds__(256) void colsum_final_kernel(const float* part, in
 template <int TM, int TN, int WM_, int WN_>
 static int launch_fwd(const ConvArgs& a, int mode, hipStream_t st) {
     constexpr int BM = 32 * TM * WM_, BN = 32 * TN * WN_;
-    dim3 grid(ceil_div(a.M, BM), ceil_div(a.g.Co, BN), a.g.nphase);
+    dim3 grid(ceil_div(a.M, BM), ceil_div(a.g.Co, BN), a.g.nphase * a.nsplit);
     if (mode == 0) hipLaunchKernelGGL((conv_fwd_kernel<TM, TN, WM_, WN_, 0>), grid, dim3(256), 0, st, a);
     else if (mode == 1) hipLaunchKernelGGL((conv_fwd_kernel<TM, TN, WM_, WN_, 1>), grid, dim3(256), 0, st, a);
     else hipLaunchKernelGGL((conv_fwd_kernel<TM, TN, WM_, WN_, 2>), grid, dim3(256), 0, st, a);
     return HY_LAUNCH_CHECK("conv_fwd_kernel");
 }
 
-static void fill_taps(hyres_conv_geom* g, int p, int* tapcount, int K, int pad, int ph, int pw,
-                      int* khs, int* kws) {
+static void fill_taps(hyres_conv_geom* g, int p, int* tapcount, int K, int pad, int ph, int pw) {
     // sub-pixel phase (ph, pw) of a stride-2 transposed structure: taps kh with (ph+pad-kh) even
     g->tap0[p] = *tapcount;
     int n = 0;
@@ -555,8 +690,8 @@ static void fill_taps(hyres_conv_geom* g, int p, int* tapcount, int K, int pad, 
             int t = *tapcount + n;
             g->dh[t] = (ph + pad - kh) / 2;
             g->dw[t] = (pw + pad - kw) / 2;
-            khs[t] = kh;
-            kws[t] = kw;
+            g->kh[t] = kh;
+            g->kw[t] = kw;
             ++n;
         }
     }
@@ -566,13 +701,26 @@ static void fill_taps(hyres_conv_geom* g, int p, int* tapcount, int K, int pad, 
     *tapcount += n;
 }
 
+static void dense_taps(hyres_conv_geom* g, int KH, int KW, int sgn, int dil, int pad) {
+    // one phase, taps in (kh, kw) raster order; offset = sgn * (k*dil - pad)
+    g->ntap[0] = KH * KW;
+    g->tap0[0] = 0;
+    g->ntaps = KH * KW;
+    for (int kh = 0; kh < KH; ++kh)
+        for (int kw = 0; kw < KW; ++kw) {
+            int t = kh * KW + kw;
+            g->dh[t] = sgn * (kh * dil - pad);
+            g->dw[t] = sgn * (kw * dil - pad);
+            g->kh[t] = kh;
+            g->kw[t] = kw;
+        }
+}
+
 }  // namespace hyres
 
 using namespace hyres;
 
-
 extern "C" {
-
 
 int hyres_geom_conv2d(hyres_conv_geom* g, int B, int H, int W, int Ci, int ldx, int Co, int ldy, int KH,
                       int KW, int stride, int pad, int dil) {
@@ -584,13 +732,7 @@ int hyres_geom_conv2d(hyres_conv_geom* g, int B, int H, int W, int Ci, int ldx, 
     g->Co = Co; g->ldy = ldy;
     g->nphase = 1; g->Hq = g->Ho; g->Wq = g->Wo;
     g->osh = g->osw = 1; g->ish = g->isw = stride;
-    g->ntap[0] = KH * KW; g->tap0[0] = 0; g->ntaps = KH * KW;
-    for (int kh = 0; kh < KH; ++kh)
-        for (int kw = 0; kw < KW; ++kw) {
-            int t = kh * KW + kw;
-            g->dh[t] = kh * dil - pad;
-            g->dw[t] = kw * dil - pad;
-        }
+    dense_taps(g, KH, KW, 1, dil, pad);
     return ok();
 }
 
@@ -604,21 +746,14 @@ int hyres_geom_conv2d_dgrad(hyres_conv_geom* g, int B, int H, int W, int Ci, int
     g->Ho = H; g->Wo = W; g->Co = Ci; g->ldy = ld_dx;
     if (stride == 1) {
         g->nphase = 1; g->Hq = H; g->Wq = W; g->osh = g->osw = 1; g->ish = g->isw = 1;
-        g->ntap[0] = KH * KW; g->tap0[0] = 0; g->ntaps = KH * KW;
-        for (int kh = 0; kh < KH; ++kh)
-            for (int kw = 0; kw < KW; ++kw) {
-                int t = kh * KW + kw;
-                g->dh[t] = pad - kh * dil;
-                g->dw[t] = pad - kw * dil;
-            }
+        dense_taps(g, KH, KW, -1, dil, pad);  // dX[h] += dY[h + pad - k*dil] W[k]
         return ok();
     }
     HY_REQUIRE(stride == 2 && dil == 1 && KH == KW && (H % 2) == 0 && (W % 2) == 0 && Ho * 2 == H &&
                    Wo * 2 == W, HYRES_E_SHAPE, "conv dgrad: only stride 2, dil 1, square K, even H/W");
     g->nphase = 4; g->Hq = H / 2; g->Wq = W / 2; g->osh = g->osw = 2; g->ish = g->isw = 1;
     int cnt = 0;
-    int khs[HYRES_MAX_TAPS], kws[HYRES_MAX_TAPS];
-    for (int p = 0; p < 4; ++p) fill_taps(g, p, &cnt, KH, pad, p >> 1, p & 1, khs, kws);
+    for (int p = 0; p < 4; ++p) fill_taps(g, p, &cnt, KH, pad, p >> 1, p & 1);
     g->ntaps = cnt;
     return ok();
 }
@@ -632,8 +767,7 @@ int hyres_geom_deconv2d(hyres_conv_geom* g, int B, int H, int W, int Ci, int ldx
     g->Ho = 2 * H; g->Wo = 2 * W; g->Co = Co; g->ldy = ldy;
     g->nphase = 4; g->Hq = H; g->Wq = W; g->osh = g->osw = 2; g->ish = g->isw = 1;
     int cnt = 0;
-    int khs[HYRES_MAX_TAPS], kws[HYRES_MAX_TAPS];
-    for (int p = 0; p < 4; ++p) fill_taps(g, p, &cnt, K, pad, p >> 1, p & 1, khs, kws);
+    for (int p = 0; p < 4; ++p) fill_taps(g, p, &cnt, K, pad, p >> 1, p & 1);
     g->ntaps = cnt;
     return ok();
 }
@@ -645,40 +779,41 @@ int hyres_geom_deconv2d_dgrad(hyres_conv_geom* g, int B, int H, int W, int Ci, i
     g->B = B; g->Hi = 2 * H; g->Wi = 2 * W; g->Ci = Co; g->ldx = ld_dy;
     g->Ho = H; g->Wo = W; g->Co = Ci; g->ldy = ld_dx;
     g->nphase = 1; g->Hq = H; g->Wq = W; g->osh = g->osw = 1; g->ish = g->isw = 2;
-    g->ntap[0] = K * K; g->tap0[0] = 0; g->ntaps = K * K;
-    for (int kh = 0; kh < K; ++kh)
-        for (int kw = 0; kw < K; ++kw) {
-            int t = kh * K + kw;
-            g->dh[t] = kh - pad;
-            g->dw[t] = kw - pad;
+    dense_taps(g, K, K, 1, 1, pad);  // dX[i] += dY[2i - pad + k] W[k]
+    return ok();
+}
+
+int hyres_geom_filter_taps(hyres_conv_geom* g, const unsigned char* keep, int KW) {
+    HY_REQUIRE(g && keep && KW > 0, HYRES_E_ARG, "filter_taps: bad args");
+    hyres_conv_geom o = *g;
+    int cnt = 0;
+    for (int p = 0; p < g->nphase; ++p) {
+        o.tap0[p] = cnt;
+        int n = 0;
+        for (int t = g->tap0[p]; t < g->tap0[p] + g->ntap[p]; ++t) {
+            if (!keep[g->kh[t] * KW + g->kw[t]]) continue;
+            o.dh[cnt] = g->dh[t]; o.dw[cnt] = g->dw[t]; o.kh[cnt] = g->kh[t]; o.kw[cnt] = g->kw[t];
+            ++cnt;
+            ++n;
         }
+        o.ntap[p] = n;
+    }
+    o.ntaps = cnt;
+    *g = o;
     return ok();
 }
 
 int hyres_conv_weight_prep(const hyres_conv_geom* g, const float* w, float* w2, int mode, int Ci, int Co,
                            int KH, int KW, int pad, const float* mask, hyres_stream_t s) {
     HY_REQUIRE(g && w && w2, HYRES_E_ARG, "weight_prep: NULL");
+    (void)pad;
     PrepArgs a{};
     a.w = w; a.w2 = w2; a.mask = mask; a.mode = mode; a.KH = KH; a.KW = KW; a.Ci = Ci; a.Co = Co;
     a.ntaps = g->ntaps;
-    const bool phased = g->nphase == 4;
-    if (phased) {
-        // rebuild the phase tap order exactly as fill_taps did
-        int t = 0;
-        for (int p = 0; p < 4; ++p) {
-            int ph = p >> 1, pw = p & 1;
-            for (int kh = 0; kh < KH; ++kh) {
-                if (((ph + pad - kh) & 1) != 0) continue;
-                for (int kw = 0; kw < KW; ++kw) {
-                    if (((pw + pad - kw) & 1) != 0) continue;
-                    a.kh[t] = kh; a.kw[t] = kw; ++t;
-                }
-            }
-        }
-        HY_REQUIRE(t == g->ntaps, HYRES_E_SHAPE, "weight_prep: phase tap mismatch");
-    } else {
-        HY_REQUIRE(g->ntaps == KH * KW, HYRES_E_SHAPE, "weight_prep: tap count mismatch");
-        for (int t = 0; t < KH * KW; ++t) { a.kh[t] = t / KW; a.kw[t] = t % KW; }
+    for (int t = 0; t < g->ntaps; ++t) {
+        HY_REQUIRE(g->kh[t] < KH && g->kw[t] < KW, HYRES_E_SHAPE, "weight_prep: tap %d outside %dx%d", t, KH, KW);
+        a.kh[t] = g->kh[t];
+        a.kw[t] = g->kw[t];
     }
     switch (mode) {
         case HYRES_WPREP_CONV: a.rows = Co; a.cols = Ci; break;
@@ -695,14 +830,62 @@ int hyres_conv_weight_prep(const hyres_conv_geom* g, const float* w, float* w2, 
     return HY_LAUNCH_CHECK("weight_prep_kernel");
 }
 
+struct ConvPlan {
+    int BM, BN, nsplit, cps;
+};
+
+static ConvPlan conv_plan(const hyres_conv_geom* g) {
+    ConvPlan p{};
+    p.BM = 128;
+    p.BN = g->Co > 64 ? 128 : (g->Co > 32 ? 64 : 32);
+    const long long M = (long long)g->B * g->Hq * g->Wq;
+    long long blocks = (long long)ceil_div(M, p.BM) * ceil_div(g->Co, p.BN) * g->nphase;
+    int maxtap = 0;
+    for (int ph = 0; ph < g->nphase; ++ph) maxtap = std::max(maxtap, g->ntap[ph]);
+    const int nk = (g->Ci % KT == 0) ? maxtap * (g->Ci / KT) : ceil_div((long long)maxtap * g->Ci, KT);
+    p.nsplit = 1;
+    p.cps = nk;
+    if (blocks < 512 && nk >= 8) {
+        // split K so that ~512 blocks are in flight, at least 4 chunks per split
+        int want = (int)std::min<long long>(ceil_div(512, blocks), 64);
+        int ns = std::max(1, std::min(want, nk / 4));
+        p.cps = ceil_div(nk, ns);
+        p.nsplit = ceil_div(nk, p.cps);
+    }
+    return p;
+}
+
+long long hyres_conv_workspace_bytes(const hyres_conv_geom* g) {
+    if (!g) return 0;
+    ConvPlan p = conv_plan(g);
+    if (p.nsplit <= 1) return 0;
+    return (long long)p.nsplit * g->nphase * ((long long)g->B * g->Hq * g->Wq) * g->Co * 4;
+}
+
 int hyres_conv_forward(const hyres_conv_geom* g, const float* x, const float* w2, int ldw, float* y,
-                       const hyres_epilogue* e, hyres_stream_t s) {
+                       const hyres_epilogue* e, void* ws, long long ws_bytes, hyres_stream_t s) {
     HY_REQUIRE(g && x && w2 && y && e, HYRES_E_ARG, "conv_forward: NULL argument");
     HY_REQUIRE(g->nphase >= 1 && g->nphase <= 4 && g->Ci > 0 && g->Co > 0, HYRES_E_SHAPE, "conv: bad geom");
     HY_REQUIRE(ldw >= g->ntaps * g->Ci, HYRES_E_SHAPE, "conv: ldw %d < ntaps*Ci %d", ldw, g->ntaps * g->Ci);
     ConvArgs a;
     a.g = *g; a.x = x; a.w2 = w2; a.ldw = ldw; a.y = y; a.e = *e;
     a.M = g->B * g->Hq * g->Wq;
+    ConvPlan plan = conv_plan(g);
+    a.nsplit = 1;
+    a.cps = 0;
+    a.slab = nullptr;
+    {
+        auto al = [](const void* p, int ld) { return p == nullptr || (aligned16(p) && ld % 4 == 0); };
+        a.vec4 = g->Co % 4 == 0 && al(y, g->ldy) && al(e->bias, 4) && al(e->res, e->ldres) && al(e->out2, e->ldo2) &&
+                 al(e->aux0, e->ld0) && al(e->aux1, e->ld1) && al(e->aux2, e->ld2);
+    }
+    const long long need = hyres_conv_workspace_bytes(g);
+    if (plan.nsplit > 1 && ws && ws_bytes >= need) {  // without workspace: single pass (correct, slower)
+        a.nsplit = plan.nsplit;
+        a.cps = plan.cps;
+        a.slab = (float*)ws;
+        if (!aligned16(ws)) a.vec4 = 0;
+    }
     int mode;
     if (g->Ci % KT == 0) {
         HY_REQUIRE(aligned16(x) && aligned16(w2) && g->ldx % 4 == 0 && ldw % 4 == 0, HYRES_E_ALIGN,
@@ -719,9 +902,15 @@ int hyres_conv_forward(const hyres_conv_geom* g, const float* x, const float* w2
         HY_REQUIRE(e->aux0 && e->aux1 && e->aux2, HYRES_E_ARG, "conv: GDN bwd epilogue needs aux0..2");
     if (e->act == HYRES_ACT_PRELU) HY_REQUIRE(e->slope, HYRES_E_ARG, "conv: PReLU needs slope");
     hipStream_t st = as_stream(s);
-    if (g->Co > 64) return launch_fwd<2, 2, 2, 2>(a, mode, st);
-    if (g->Co > 32) return launch_fwd<2, 1, 2, 2>(a, mode, st);
-    return launch_fwd<1, 1, 4, 1>(a, mode, st);
+    int rc;
+    if (g->Co > 64) rc = launch_fwd<2, 2, 2, 2>(a, mode, st);
+    else if (g->Co > 32) rc = launch_fwd<2, 1, 2, 2>(a, mode, st);
+    else rc = launch_fwd<1, 1, 4, 1>(a, mode, st);
+    if (rc || a.nsplit == 1) return rc;
+    long long total = (long long)a.M * g->Co * g->nphase;
+    int blocks = (int)std::min<long long>((total + 255) / 256, 8192);
+    hipLaunchKernelGGL(conv_splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, a);
+    return HY_LAUNCH_CHECK("conv_splitk_reduce_kernel");
 }
 
 int hyres_wgrad_desc_conv2d(hyres_wgrad_desc* d, int B, int H, int W, int Ci, int ldx, int Co, int ldy,

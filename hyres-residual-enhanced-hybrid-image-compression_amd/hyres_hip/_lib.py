@@ -28,7 +28,8 @@ class ConvGeom(ctypes.Structure):
                  "osh", "osw", "ish", "isw")] + [
         ("oph", ctypes.c_int * 4), ("opw", ctypes.c_int * 4), ("ntap", ctypes.c_int * 4),
         ("tap0", ctypes.c_int * 4), ("ntaps", ctypes.c_int),
-        ("dh", ctypes.c_int * MAX_TAPS), ("dw", ctypes.c_int * MAX_TAPS)]
+        ("dh", ctypes.c_int * MAX_TAPS), ("dw", ctypes.c_int * MAX_TAPS),
+        ("kh", ctypes.c_int * MAX_TAPS), ("kw", ctypes.c_int * MAX_TAPS)]
 
 
 class Epilogue(ctypes.Structure):
@@ -65,8 +66,11 @@ _SIGS = {
     "hyres_geom_conv2d_dgrad": (_I, [ctypes.POINTER(ConvGeom)] + [_I] * 12),
     "hyres_geom_deconv2d": (_I, [ctypes.POINTER(ConvGeom)] + [_I] * 9),
     "hyres_geom_deconv2d_dgrad": (_I, [ctypes.POINTER(ConvGeom)] + [_I] * 9),
+    "hyres_geom_filter_taps": (_I, [ctypes.POINTER(ConvGeom), ctypes.POINTER(ctypes.c_ubyte), _I]),
     "hyres_conv_weight_prep": (_I, [ctypes.POINTER(ConvGeom), _P, _P, _I, _I, _I, _I, _I, _I, _P, _P]),
-    "hyres_conv_forward": (_I, [ctypes.POINTER(ConvGeom), _P, _P, _I, _P, ctypes.POINTER(Epilogue), _P]),
+    "hyres_conv_forward": (_I, [ctypes.POINTER(ConvGeom), _P, _P, _I, _P, ctypes.POINTER(Epilogue), _P, _LL,
+                                _P]),
+    "hyres_conv_workspace_bytes": (_LL, [ctypes.POINTER(ConvGeom)]),
     "hyres_wgrad_desc_conv2d": (_I, [ctypes.POINTER(WgradDesc)] + [_I] * 12),
     "hyres_wgrad_desc_deconv2d": (_I, [ctypes.POINTER(WgradDesc)] + [_I] * 9),
     "hyres_wgrad_workspace_bytes": (_LL, [ctypes.POINTER(WgradDesc)]),

@@ -230,16 +230,43 @@ def _geom(fn: str, *args) -> L.ConvGeom:
     return g
 
 
+def _live_taps(mask: torch.Tensor):
+    """Host copy of a spatial mask's live taps (KH*KW uint8), cached on the mask tensor.  Valid when the
+    mask is the same for every (out, in) channel pair, as CheckboardMaskedConv2d's is."""
+    keep = getattr(mask, "_hyres_keep", None)
+    if keep is None:
+        m = mask.detach().to("cpu")
+        KW = m.shape[-1]
+        plane = m[0, 0]
+        assert torch.equal((m != 0), (plane != 0).expand_as(m)), "mask must be channel-independent"
+        keep = ((ctypes.c_ubyte * plane.numel())(*[int(v != 0) for v in plane.flatten().tolist()]), KW)
+        try:
+            mask._hyres_keep = keep
+        except Exception:
+            pass
+    return keep
+
+
+def _filter_taps(g: L.ConvGeom, mask: Optional[torch.Tensor]) -> L.ConvGeom:
+    if mask is not None:
+        keep, KW = _live_taps(mask)
+        L.call("hyres_geom_filter_taps", ctypes.byref(g), keep, KW)
+    return g
+
+
 class KernelTimer:
     """Optional HIP-event timing of the dominant kernel (conv_fwd_kernel<2,2,2,2,0>: Co > 64,
     Ci % 32 == 0, no square prologue) with its algorithmic FLOPs, for bench.py's roofline line."""
 
     enabled = False
+    all_convs = False  # record every conv launch (layer table), not only the dominant variant
     events: list = []
+    table: list = []
 
     @classmethod
     def reset(cls):
         cls.events = []
+        cls.table = []
 
     @classmethod
     def summary(cls):
@@ -256,16 +283,35 @@ def conv_flops(g: L.ConvGeom) -> float:
     return 2.0 * g.B * g.Hq * g.Wq * taps * g.Ci * g.Co
 
 
+def conv_bytes(g: L.ConvGeom, e: L.Epilogue) -> float:
+    """Algorithmic HBM bytes: input read once, weights once, output written (read too if accumulating),
+    residual / aux operands read once."""
+    px_in = g.B * g.Hi * g.Wi
+    px_out = g.B * g.Hq * g.Wq * g.nphase
+    b = 4.0 * (px_in * g.Ci + g.ntaps * g.Ci * g.Co + px_out * g.Co * (2 if e.accumulate else 1))
+    b += 4.0 * px_out * g.Co * sum(1 for p in (e.res, e.aux0, e.aux1, e.aux2, e.out2) if p)
+    return b
+
+
 def _launch_conv(g: L.ConvGeom, x_ptr: int, w2: torch.Tensor, ldw: int, y_ptr: int, e: L.Epilogue) -> None:
-    timed = KernelTimer.enabled and g.Co > 64 and g.Ci % 32 == 0 and not e.square_input
+    dominant = g.Co > 64 and g.Ci % 32 == 0 and not e.square_input
+    timed = KernelTimer.enabled and (dominant or KernelTimer.all_convs)
     if timed:
         s0 = torch.cuda.Event(enable_timing=True)
         s1 = torch.cuda.Event(enable_timing=True)
         s0.record()
-    L.call("hyres_conv_forward", ctypes.byref(g), x_ptr, w2.data_ptr(), ldw, y_ptr, ctypes.byref(e), L.stream())
+    nb = L.load().hyres_conv_workspace_bytes(ctypes.byref(g))
+    ws = _ws(nb, w2.device, slot=6) if nb > 0 else None
+    L.call("hyres_conv_forward", ctypes.byref(g), x_ptr, w2.data_ptr(), ldw, y_ptr, ctypes.byref(e),
+           None if ws is None else ws.data_ptr(), 0 if ws is None else ws.numel(), L.stream())
     if timed:
         s1.record()
-        KernelTimer.events.append((s0, s1, conv_flops(g)))
+        if dominant:
+            KernelTimer.events.append((s0, s1, conv_flops(g)))
+        if KernelTimer.all_convs:
+            desc = (f"B{g.B} {g.Hi}x{g.Wi}x{g.Ci}->{g.Ho}x{g.Wo}x{g.Co} taps{g.ntaps} ph{g.nphase} "
+                    f"s{g.ish} epi{e.kind}{'+acc' if e.accumulate else ''}{'+res' if e.res else ''}")
+            KernelTimer.table.append((desc, s0, s1, conv_flops(g), conv_bytes(g, e)))
 
 
 def _colsum_into(g: torch.Tensor, P: int, C: int, ld: int, dst: torch.Tensor, acc: int = 1) -> None:
@@ -319,7 +365,7 @@ def conv2d(tape: Optional[Tape], x: Node, weight: torch.Tensor, bias: Optional[t
     Wo = (W + 2 * pad - dil * (KW - 1) - 1) // stride + 1
     y = out if out is not None else Node.new(B, Ho, Wo, Co, x.device)
     assert (y.B, y.H, y.W, y.C) == (B, Ho, Wo, Co), ((y.B, y.H, y.W, y.C), (B, Ho, Wo, Co))
-    g = _geom("hyres_geom_conv2d", B, H, W, Ci, x.ld, Co, y.ld, KH, KW, stride, pad, dil)
+    g = _filter_taps(_geom("hyres_geom_conv2d", B, H, W, Ci, x.ld, Co, y.ld, KH, KW, stride, pad, dil), mask)
     if KH == 1 and KW == 1 and mask is None:
         w2, ldw = weight, Ci_w  # OIHW == OHWI for 1x1
     else:
@@ -363,7 +409,8 @@ def conv2d(tape: Optional[Tape], x: Node, weight: torch.Tensor, bias: Optional[t
             _wgrad(d, gp.data_ptr(), x.ptr(), param_grad(weight), x.device)
         if x.rg:
             tgt, acc = x.grad_target()
-            gd = _geom("hyres_geom_conv2d_dgrad", B, H, W, Ci, x.grad_ld(), Co, gpld, KH, KW, stride, pad, dil)
+            gd = _filter_taps(_geom("hyres_geom_conv2d_dgrad", B, H, W, Ci, x.grad_ld(), Co, gpld, KH, KW, stride,
+                                    pad, dil), mask)
             w2d = _prepped(weight, gd, L.WPREP_CONV_DGRAD, Ci_w, Co, KH, KW, pad, mask)
             ed = L.Epilogue()
             ed.kind = L.EPI_BIAS

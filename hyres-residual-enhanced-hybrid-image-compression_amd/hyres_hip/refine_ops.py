@@ -107,7 +107,7 @@ def spatial_attention_mul(tape: Optional[Tape], x: Node, w: torch.Tensor) -> Nod
 def add(tape: Optional[Tape], a: Node, b: Node, alpha: float = 1.0) -> Node:
     """y = a + alpha*b (models/hyres.py:48 residual = x - jpeg; :62 x_hat_initial = jpeg + residual_hat)."""
     assert a.contiguous and b.contiguous
-    y = Node.new(a.B, a.H, a.W, a.C, a.device)
+    y = Node.new(a.B, a.H, a.W, a.C, a.device, rg=a.rg or b.rg)
     L.call("hyres_axpby", a.ptr(), b.ptr(), float(alpha), y.ptr(), y.P * y.C, L.stream())
     if tape is None:
         return y

@@ -50,7 +50,12 @@ typedef struct hyres_conv_geom {
     int ntap[4], tap0[4];     /* taps of each phase: global tap indices tap0[p] .. tap0[p]+ntap[p]-1 */
     int ntaps;                /* total taps (rows of W2 = ntaps*Ci per output channel) */
     int dh[HYRES_MAX_TAPS], dw[HYRES_MAX_TAPS];
+    int kh[HYRES_MAX_TAPS], kw[HYRES_MAX_TAPS]; /* kernel element each tap reads (weight re-layout) */
 } hyres_conv_geom;
+
+/* Keep only the taps whose kernel element (kh, kw) has keep[kh*KW + kw] != 0 (order preserved).
+ * CheckboardMaskedConv2d's forward/dgrad run on its 12 live taps of 25. */
+int hyres_geom_filter_taps(hyres_conv_geom* g, const unsigned char* keep, int KW);
 
 /* nn.Conv2d(k, stride, pad, dil) forward (models/layers/common.py:4-11, compressai conv()). */
 int hyres_geom_conv2d(hyres_conv_geom* g, int B, int H, int W, int Ci, int ldx, int Co, int ldy,
@@ -104,7 +109,10 @@ typedef struct hyres_epilogue {
  * path: models/checkerboard.py:35-88, models/layers/attention.py:11-39,
  * models/layers/enhancement.py:17,44-51,65-82, compressai GDN/RBB).  fp32 MFMA (v_mfma_f32_32x32x2f32). */
 int hyres_conv_forward(const hyres_conv_geom* g, const float* x, const float* w2, int ldw, float* y,
-                       const hyres_epilogue* e, hyres_stream_t s);
+                       const hyres_epilogue* e, void* workspace, long long ws_bytes, hyres_stream_t s);
+/* Scratch for split-K on small-M layers (0 = none needed).  Passing a NULL / short workspace is
+ * valid: the launch then runs unsplit (same result, fewer blocks in flight). */
+long long hyres_conv_workspace_bytes(const hyres_conv_geom* g);
 
 /* Weight gradient:  dW[t][m][n] = sum_q P[q][m] * Q[shift_t(q)][n]  over a base grid q (B,Hq,Wq).
  * Conv2d: P = dY (output grid), Q = X;  ConvTranspose2d: P = X (input grid), Q = dY.

@@ -196,6 +196,38 @@ def test_bilinear_se_spatial_attention():
     assert rel_err(wd.grad.cpu(), wr.grad) < TOL
 
 
+def test_checkerboard_masked_conv():
+    """CheckboardMaskedConv2d: weight masked in place, forward/dgrad on the 12 live taps, dense dW."""
+    from hyres_hip import ops as O
+    from models.layers.checkerboard import CheckboardMaskedConv2d
+    D = dev()
+    torch.manual_seed(5)
+    m = CheckboardMaskedConv2d(192, 384, kernel_size=5, padding=2, stride=1)
+    w0 = m.weight.detach().clone()
+    x = _rand((2, 192, 8, 8), 31)
+    gy = _rand((2, 384, 8, 8), 32)
+    wr = w0.clone().requires_grad_(True)
+    br = m.bias.detach().clone().requires_grad_(True)
+    xr = x.clone().requires_grad_(True)
+    with torch.no_grad():
+        wr.mul_(m.mask)  # reference: weight.data *= mask, then a dense conv
+    yr = F.conv2d(xr, wr, br, padding=2)
+    yr.backward(gy)
+    m = m.to(D)
+    tape = O.Tape()
+    xn = O.to_nhwc(x.to(D), rg=True)
+    yn = m.hip(tape, xn)
+    yn.set_grad(O.nchw_grad_to_nhwc(gy.to(D)))
+    tape.backward()
+    torch.cuda.synchronize()
+    assert torch.equal(m.weight.detach().cpu(), (w0 * m.mask.cpu()))  # in-place mask applied
+    assert rel_err(O.to_nchw(yn).cpu(), yr) < TOL
+    assert rel_err(O.to_nchw_grad(xn).cpu(), xr.grad) < TOL
+    assert rel_err(m.weight.grad.cpu(), wr.grad) < TOL  # dense over all 25 taps
+    assert float(wr.grad[:, :, 0, 0].abs().max()) > 0  # (a masked tap still gets a gradient)
+    assert rel_err(m.bias.grad.cpu(), br.grad) < TOL
+
+
 @pytest.mark.parametrize("branch", ["scale1", "scale2", "scale3"])
 def test_refine_branch_fwd_bwd(branch):
     """One MultiScaleRefine branch (bilinear down -> conv+PReLU -> dilated conv+PReLU -> bilinear up) vs fp64."""
