@@ -14,6 +14,8 @@
 // Weight gradients use a second kernel (P^T Q over pixels, split-K slabs + deterministic reduce).
 #include "common.h"
 
+#include <utility>
+
 namespace hyres {
 
 constexpr int KT = 32;    // K chunk (floats)
@@ -385,7 +387,14 @@ __global__ void conv_splitk_reduce_kernel(const ConvArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// weight gradient:  out[t][m][n] = sum_q P[q][m] * Q[shift_t(q)][n]
+// weight gradient:  out[t][m][n] = sum_q P[q][m] * Q[shift_t(q)][n]      (K = pixels q)
+//   * a block owns one (m-tile, n-tile, group of NT taps, pixel split); the P chunk is staged once
+//     and reused by all NT taps, only the shifted Q chunk is re-gathered per tap (L1/L2-hot);
+//   * ``tapn``: taps folded into the column dimension (c = t*N + n) for N <= 16 (3-channel images),
+//     so a 32-wide MFMA column tile is not 90% padding;
+//   * blocks of one pixel split are consecutive in logical order and mapped onto one XCD so their
+//     shared P/Q rows hit that XCD's L2;
+//   * split-K partials go to a [nsplit][ntaps][M][N] slab, reduced deterministically.
 // ------------------------------------------------------------------------------------------------
 struct WgradArgs {
     hyres_wgrad_desc d;
@@ -394,10 +403,21 @@ struct WgradArgs {
     float* slab;  // [nsplit][ntaps][M][N]
     int chunks_per_split;
     int nchunks;
-    int mtiles;
+    int mtiles, ntiles, ngroups;
+    int nblocks;  // logical blocks (grid padded to a multiple of 8 for the XCD remap)
+    int tapn;
 };
 
-template <int TM, int TN, int WAVES_M, int WAVES_N, bool VP, bool VQ, bool SQ>
+template <typename F, int... Is>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, Is...>) {
+    (f(std::integral_constant<int, Is>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+    static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+template <int TM, int TN, int WAVES_M, int WAVES_N, int NT, bool VP, bool VQ, bool SQ>
 __global__ __launch_bounds__(256) void wgrad_kernel(const WgradArgs a) {
     constexpr int BM = 32 * TM * WAVES_M;
     constexpr int BN = 32 * TN * WAVES_N;
@@ -406,13 +426,20 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgradArgs a) {
     __shared__ __attribute__((aligned(16))) float Qs[KT * PQ];
     const hyres_wgrad_desc& d = a.d;
     const int tid = threadIdx.x;
-    const int mt = blockIdx.x % a.mtiles, nt = blockIdx.x / a.mtiles;
+    // XCD-aware order: hardware block b runs on XCD b % 8; give each XCD a contiguous logical range
+    const int bid = blockIdx.x;
+    const int lb = (bid & 7) * (gridDim.x >> 3) + (bid >> 3);
+    if (lb >= a.nblocks) return;
+    int rr = lb;
+    const int mt = rr % a.mtiles; rr /= a.mtiles;
+    const int nt = rr % a.ntiles; rr /= a.ntiles;
+    const int grp = rr % a.ngroups;
+    const int split = rr / a.ngroups;
     const int m0 = mt * BM, n0 = nt * BN;
-    const int t = blockIdx.y;
-    const int split = blockIdx.z;
+    const int t0 = grp * NT;
     const int HqWq = d.Hq * d.Wq;
     const long long Qtot = (long long)d.B * HqWq;
-    const int dh = d.dh[t], dw = d.dw[t];
+    const bool tapn = a.tapn != 0;
 
     constexpr int P_V = VP ? (KT * BM / 4 / 256) : (KT * BM / 256);
     constexpr int Q_V = VQ ? (KT * BN / 4 / 256) : (KT * BN / 256);
@@ -420,14 +447,44 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgradArgs a) {
     float4 rp[VP ? P_V : 1], rq[VQ ? Q_V : 1];
     float sp[VP ? 1 : P_V], sq[VQ ? 1 : Q_V];
 
-    auto load_chunk = [&](int kc) {
+    // per-thread Q rows/columns (fixed for the whole kernel) and the pixel decode of the current chunk
+    int q_row[Q_V], q_col[Q_V], q_tap[Q_V];
+#pragma unroll
+    for (int i = 0; i < Q_V; ++i) {
+        const int e = tid + 256 * i;
+        q_row[i] = VQ ? e / (BN / 4) : e / BN;
+        const int c = n0 + (VQ ? (e % (BN / 4)) * 4 : e % BN);
+        if (!VQ && tapn) {
+            q_tap[i] = c / d.N;
+            q_col[i] = c - q_tap[i] * d.N;
+        } else {
+            q_tap[i] = 0;
+            q_col[i] = c;
+        }
+    }
+    int q_b[Q_V], q_i[Q_V], q_j[Q_V];
+    auto decode_rows = [&](int kc) {
+#pragma unroll
+        for (int i = 0; i < Q_V; ++i) {
+            const long long qq = (long long)kc * KT + q_row[i];
+            if (qq < Qtot) {
+                q_b[i] = (int)(qq / HqWq);
+                const int r = (int)(qq - (long long)q_b[i] * HqWq);
+                q_i[i] = r / d.Wq;
+                q_j[i] = r - q_i[i] * d.Wq;
+            } else {
+                q_b[i] = -1; q_i[i] = 0; q_j[i] = 0;
+            }
+        }
+    };
+    auto load_p = [&](int kc) {
         const long long k0 = (long long)kc * KT;
         if constexpr (VP) {
 #pragma unroll
             for (int i = 0; i < P_V; ++i) {
-                int e = tid + 256 * i;
-                int row = e / (BM / 4), c = (e % (BM / 4)) * 4;
-                long long qq = k0 + row;
+                const int e = tid + 256 * i;
+                const int row = e / (BM / 4), c = (e % (BM / 4)) * 4;
+                const long long qq = k0 + row;
                 float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
                 if (qq < Qtot && m0 + c < d.M) v = ld4(a.p + qq * d.ldp + m0 + c);
                 rp[i] = v;
@@ -435,29 +492,25 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgradArgs a) {
         } else {
 #pragma unroll
             for (int i = 0; i < P_V; ++i) {
-                int e = tid + 256 * i;
-                int row = e / BM, c = e % BM;
-                long long qq = k0 + row;
+                const int e = tid + 256 * i;
+                const int row = e / BM, c = e % BM;
+                const long long qq = k0 + row;
                 float v = 0.f;
                 if (qq < Qtot && m0 + c < d.M) v = a.p[qq * d.ldp + m0 + c];
                 sp[i] = v;
             }
         }
+    };
+    auto load_q = [&](int t) {
 #pragma unroll
         for (int i = 0; i < Q_V; ++i) {
-            int e = tid + 256 * i;
-            int row = VQ ? e / (BN / 4) : e / BN;
-            int c = VQ ? (e % (BN / 4)) * 4 : e % BN;
-            long long qq = k0 + row;
-            bool ok = qq < Qtot && n0 + c < d.N;
+            const int tt = tapn ? q_tap[i] : t;
+            bool ok = q_b[i] >= 0 && q_col[i] < d.N && tt < d.ntaps;
             long long off = 0;
             if (ok) {
-                int b = (int)(qq / HqWq);
-                int r = (int)(qq - (long long)b * HqWq);
-                int ii = r / d.Wq, jj = r - (r / d.Wq) * d.Wq;
-                int ih = ii * d.sq + dh, iw = jj * d.sq + dw;
+                const int ih = q_i[i] * d.sq + d.dh[tt], iw = q_j[i] * d.sq + d.dw[tt];
                 ok = ih >= 0 && ih < d.Hqq && iw >= 0 && iw < d.Wqq;
-                off = ((long long)(b * d.Hqq + ih) * d.Wqq + iw) * d.ldq + n0 + c;
+                off = ((long long)(q_b[i] * d.Hqq + ih) * d.Wqq + iw) * d.ldq + q_col[i];
             }
             if constexpr (VQ) {
                 float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -471,33 +524,34 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgradArgs a) {
             }
         }
     };
-    auto store_chunk = [&]() {
+    auto store_p = [&]() {
         if constexpr (VP) {
 #pragma unroll
             for (int i = 0; i < P_V; ++i) {
-                int e = tid + 256 * i;
-                int row = e / (BM / 4), c = (e % (BM / 4)) * 4;
+                const int e = tid + 256 * i;
+                const int row = e / (BM / 4), c = (e % (BM / 4)) * 4;
                 *reinterpret_cast<float4*>(&Ps[row * PP + c]) = rp[i];
             }
         } else {
 #pragma unroll
             for (int i = 0; i < P_V; ++i) {
-                int e = tid + 256 * i;
+                const int e = tid + 256 * i;
                 Ps[(e / BM) * PP + e % BM] = sp[i];
             }
         }
+    };
+    auto store_q = [&]() {
         if constexpr (VQ) {
 #pragma unroll
             for (int i = 0; i < Q_V; ++i) {
-                int e = tid + 256 * i;
-                int row = e / (BN / 4), c = (e % (BN / 4)) * 4;
-                *reinterpret_cast<float4*>(&Qs[row * PQ + c]) = rq[i];
+                const int e = tid + 256 * i;
+                *reinterpret_cast<float4*>(&Qs[q_row[i] * PQ + (e % (BN / 4)) * 4]) = rq[i];
             }
         } else {
 #pragma unroll
             for (int i = 0; i < Q_V; ++i) {
-                int e = tid + 256 * i;
-                Qs[(e / BN) * PQ + e % BN] = sq[i];
+                const int e = tid + 256 * i;
+                Qs[q_row[i] * PQ + e % BN] = sq[i];
             }
         }
     };
@@ -505,67 +559,116 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgradArgs a) {
     const int lane = tid & 63, wave = tid >> 6;
     const int wm = wave / WAVES_N, wn = wave % WAVES_N;
     const int lr = lane & 31, lh = lane >> 5;
-    floatx16 acc[TM][TN];
+    floatx16 acc[NT][TM][TN];
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+    for (int j = 0; j < NT; ++j)
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
+        for (int i = 0; i < TM; ++i)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+            for (int k = 0; k < TN; ++k)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[j][i][k][r] = 0.f;
 
     const int kc_begin = split * a.chunks_per_split;
     const int kc_end = min(a.nchunks, kc_begin + a.chunks_per_split);
-    if (kc_begin < kc_end) load_chunk(kc_begin);
+    if (kc_begin < kc_end) {
+        decode_rows(kc_begin);
+        load_p(kc_begin);
+        load_q(t0);
+    }
     for (int kc = kc_begin; kc < kc_end; ++kc) {
-        __syncthreads();
-        store_chunk();
-        __syncthreads();
-        if (kc + 1 < kc_end) load_chunk(kc + 1);
+        static_for<NT>([&](auto J) {
+            constexpr int j = decltype(J)::value;
+            __syncthreads();
+            if (j == 0) store_p();
+            store_q();
+            __syncthreads();
+            if (j + 1 < NT) {
+                load_q(t0 + j + 1);
+            } else if (kc + 1 < kc_end) {
+                decode_rows(kc + 1);
+                load_p(kc + 1);
+                load_q(t0);
+            }
 #pragma unroll
-        for (int s = 0; s < KT / 2; ++s) {
-            const int k = lh * (KT / 2) + s;
-            float af[TM], bf[TN];
+            for (int s = 0; s < KT / 2; ++s) {
+                const int k = lh * (KT / 2) + s;
+                float af[TM], bf[TN];
 #pragma unroll
-            for (int tm = 0; tm < TM; ++tm) af[tm] = Ps[k * PP + wm * TM * 32 + tm * 32 + lr];
+                for (int tm = 0; tm < TM; ++tm) af[tm] = Ps[k * PP + wm * TM * 32 + tm * 32 + lr];
 #pragma unroll
-            for (int tn = 0; tn < TN; ++tn) bf[tn] = Qs[k * PQ + wn * TN * 32 + tn * 32 + lr];
+                for (int tn = 0; tn < TN; ++tn) bf[tn] = Qs[k * PQ + wn * TN * 32 + tn * 32 + lr];
+#pragma unroll
+                for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                    for (int tn = 0; tn < TN; ++tn)
+                        acc[j][tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[tm], bf[tn], acc[j][tm][tn], 0, 0, 0);
+            }
+        });
+    }
+    // slab store [split][t][M][N]
+    const long long MN = (long long)d.M * d.N;
+    static_for<NT>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) {
+            const int c = n0 + wn * TN * 32 + tn * 32 + lr;
+            int t = t0 + j, n = c;
+            if (tapn) { t = c / d.N; n = c - t * d.N; }
+            if (n >= d.N || t >= d.ntaps) continue;
+            float* out = a.slab + ((long long)split * d.ntaps + t) * MN + n;
 #pragma unroll
             for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
-                for (int tn = 0; tn < TN; ++tn)
-                    acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[tm], bf[tn], acc[tm][tn], 0, 0, 0);
+                for (int r = 0; r < 16; ++r) {
+                    const int m = m0 + wm * TM * 32 + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                    if (m < d.M) out[(long long)m * d.N] = acc[j][tm][tn][r];
+                }
         }
-    }
-    // slab store [split][t][M][N]
-    float* out = a.slab + ((long long)split * d.ntaps + t) * (long long)d.M * d.N;
-#pragma unroll
-    for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-        for (int tn = 0; tn < TN; ++tn) {
-            const int n = n0 + wn * TN * 32 + tn * 32 + lr;
-            if (n >= d.N) continue;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int m = m0 + wm * TM * 32 + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-                if (m < d.M) out[(long long)m * d.N + n] = acc[tm][tn][r];
-            }
-        }
+    });
 }
 
-__global__ void wgrad_reduce_kernel(const float* slab, int nsplit, int ntaps, int M, int N, float* dst,
-                                    int sm, int sn, int st, int accumulate) {
+// deterministic split-K reduce: 16 float4 lanes x 16 split groups per block (64 outputs per block)
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* slab, int nsplit, int ntaps, int M, int N,
+                                                           float* dst, int sm, int sn, int st, int accumulate) {
+    __shared__ float red[16][65];
     const long long total = (long long)ntaps * M * N;
-    const long long stride_split = total;
-    for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
-         idx += (long long)gridDim.x * blockDim.x) {
-        float s = 0.f;
-        for (int k = 0; k < nsplit; ++k) s += slab[k * stride_split + idx];
-        const int n = (int)(idx % N);
-        const long long r = idx / N;
-        const int m = (int)(r % M);
-        const int t = (int)(r / M);
-        float* p = dst + (long long)m * sm + (long long)n * sn + (long long)t * st;
-        *p = accumulate ? (*p + s) : s;
+    const int lx = threadIdx.x & 15, ly = threadIdx.x >> 4;
+    const long long base = (long long)blockIdx.x * 64 + 4 * lx;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    if ((total & 3) == 0) {
+        if (base < total)
+            for (int k = ly; k < nsplit; k += 16) {
+                const float4 v = ld4(slab + k * total + base);
+                s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+            }
+    } else {
+        for (int k = ly; k < nsplit; k += 16) {
+            const float* p = slab + k * total + base;
+            if (base + 0 < total) s.x += p[0];
+            if (base + 1 < total) s.y += p[1];
+            if (base + 2 < total) s.z += p[2];
+            if (base + 3 < total) s.w += p[3];
+        }
+    }
+    red[ly][4 * lx + 0] = s.x;
+    red[ly][4 * lx + 1] = s.y;
+    red[ly][4 * lx + 2] = s.z;
+    red[ly][4 * lx + 3] = s.w;
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        const long long idx = (long long)blockIdx.x * 64 + threadIdx.x;
+        if (idx < total) {
+            float v = 0.f;
+#pragma unroll
+            for (int g = 0; g < 16; ++g) v += red[g][threadIdx.x];
+            const int n = (int)(idx % N);
+            const long long r = idx / N;
+            const int m = (int)(r % M);
+            const int t = (int)(r / M);
+            float* p = dst + (long long)m * sm + (long long)n * sn + (long long)t * st;
+            *p = accumulate ? (*p + v) : v;
+        }
     }
 }
 
@@ -949,75 +1052,111 @@ int hyres_wgrad_desc_deconv2d(hyres_wgrad_desc* d, int B, int H, int W, int Ci, 
     return ok();
 }
 
+}  // extern "C"
+
+namespace hyres {
+
 struct WgradPlan {
-    int TMc, TNc, WMc, WNc, BM, BN, mtiles, ntiles, nchunks, nsplit, cps;
+    int TMc, TNc, WMc, WNc, NT, BM, BN, mtiles, ntiles, ngroups, nchunks, nsplit, cps, tapn, nblocks;
 };
 
 static WgradPlan wgrad_plan(const hyres_wgrad_desc* d) {
     WgradPlan p{};
-    // tile choice (32*TM*WAVES_M x 32*TN*WAVES_N)
-    if (d->M >= 128 && d->N >= 128) { p.TMc = 2; p.TNc = 2; p.WMc = 2; p.WNc = 2; }
+    p.NT = 1;
+    p.tapn = (d->N <= 16 && d->ntaps > 1 && !d->square_q) ? 1 : 0;
+    const int ncols = p.tapn ? d->ntaps * d->N : d->N;
+    if (p.tapn) {
+        if (ncols <= 32) { p.TMc = 1; p.TNc = 1; p.WMc = 4; p.WNc = 1; }
+        else { p.TMc = 1; p.TNc = 1; p.WMc = 2; p.WNc = 2; }
+    } else if (d->M >= 128 && d->N >= 128) { p.TMc = 2; p.TNc = 2; p.WMc = 2; p.WNc = 2; }
+    else if (d->M >= 128 && d->N >= 64 && d->ntaps == 1) { p.TMc = 2; p.TNc = 1; p.WMc = 2; p.WNc = 2; }
     else if (d->M <= 32) { p.TMc = 1; p.TNc = 1; p.WMc = 1; p.WNc = 4; }
     else if (d->N <= 32) { p.TMc = 1; p.TNc = 1; p.WMc = 4; p.WNc = 1; }
-    else { p.TMc = 1; p.TNc = 1; p.WMc = 2; p.WNc = 2; }
+    else {
+        p.TMc = 1; p.TNc = 1; p.WMc = 2; p.WNc = 2;
+        p.NT = (d->ntaps % 9 == 0) ? 9 : (d->ntaps % 5 == 0) ? 5 : 1;
+    }
     p.BM = 32 * p.TMc * p.WMc; p.BN = 32 * p.TNc * p.WNc;
-    p.mtiles = ceil_div(d->M, p.BM); p.ntiles = ceil_div(d->N, p.BN);
-    long long Q = (long long)d->B * d->Hq * d->Wq;
+    p.mtiles = ceil_div(d->M, p.BM); p.ntiles = ceil_div(ncols, p.BN);
+    p.ngroups = p.tapn ? 1 : ceil_div(d->ntaps, p.NT);
+    const long long Q = (long long)d->B * d->Hq * d->Wq;
     p.nchunks = ceil_div(Q, KT);
-    long long tiles = (long long)p.mtiles * p.ntiles * d->ntaps;
-    // aim for ~2048 blocks, at least 8 chunks (256 pixels) per split
-    long long want = std::max<long long>(1, 2048 / std::max<long long>(1, tiles));
-    long long maxsplit = std::max<long long>(1, p.nchunks / 8);
-    p.nsplit = (int)std::min<long long>(want, maxsplit);
-    p.nsplit = std::min(p.nsplit, 256);
+    const long long tiles = (long long)p.mtiles * p.ntiles * p.ngroups;
+    // ~1024 blocks, >= 8 chunks (256 pixels) per split, <= 512 splits
+    const long long want = std::max<long long>(1, (1024 + tiles - 1) / tiles);
+    const long long maxsplit = std::max<long long>(1, p.nchunks / 8);
+    p.nsplit = (int)std::min<long long>(std::min<long long>(want, maxsplit), 512);
     p.cps = ceil_div(p.nchunks, p.nsplit);
     p.nsplit = ceil_div(p.nchunks, p.cps);
+    p.nblocks = (int)(tiles * p.nsplit);
     return p;
 }
 
-long long hyres_wgrad_workspace_bytes(const hyres_wgrad_desc* d) {
-    WgradPlan p = wgrad_plan(d);
-    return (long long)p.nsplit * d->ntaps * (long long)d->M * d->N * 4;
+// Small-M stride-1 gradients are computed transposed with negated shifts so that the 3-channel
+// operand becomes the (tap-folded) column side:  out[t][m][n] = sum_q' Q[q'][n] * P[q' - shift_t][m].
+static bool wgrad_swap(const hyres_wgrad_desc* d) {
+    return d->M <= 16 && d->N > 16 && d->ntaps > 1 && d->sq == 1 && d->Hqq == d->Hq && d->Wqq == d->Wq &&
+           !d->square_q;
 }
 
-int hyres_conv_wgrad(const hyres_wgrad_desc* d, const float* pp, const float* qq, float* dst, void* ws,
+static hyres_wgrad_desc wgrad_swapped(const hyres_wgrad_desc* d) {
+    hyres_wgrad_desc e = *d;
+    e.M = d->N; e.ldp = d->ldq;
+    e.N = d->M; e.ldq = d->ldp;
+    for (int t = 0; t < d->ntaps; ++t) { e.dh[t] = -d->dh[t]; e.dw[t] = -d->dw[t]; }
+    e.sm = d->sn; e.sn = d->sm;
+    return e;
+}
+
+template <int TM, int TN, int WM_, int WN_, int NT>
+static void launch_wgrad(const WgradArgs& a, bool vp, bool vq, bool sqr, dim3 grid, hipStream_t st) {
+    if (vp && vq && sqr) hipLaunchKernelGGL((wgrad_kernel<TM, TN, WM_, WN_, NT, true, true, true>), grid, dim3(256), 0, st, a);
+    else if (vp && vq) hipLaunchKernelGGL((wgrad_kernel<TM, TN, WM_, WN_, NT, true, true, false>), grid, dim3(256), 0, st, a);
+    else if (vp) hipLaunchKernelGGL((wgrad_kernel<TM, TN, WM_, WN_, NT, true, false, false>), grid, dim3(256), 0, st, a);
+    else if (vq) hipLaunchKernelGGL((wgrad_kernel<TM, TN, WM_, WN_, NT, false, true, false>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((wgrad_kernel<TM, TN, WM_, WN_, NT, false, false, false>), grid, dim3(256), 0, st, a);
+}
+
+}  // namespace hyres
+
+extern "C" {
+
+long long hyres_wgrad_workspace_bytes(const hyres_wgrad_desc* d) {
+    hyres_wgrad_desc e = wgrad_swap(d) ? wgrad_swapped(d) : *d;
+    WgradPlan p = wgrad_plan(&e);
+    return (long long)p.nsplit * e.ntaps * (long long)e.M * e.N * 4;
+}
+
+int hyres_conv_wgrad(const hyres_wgrad_desc* d0, const float* pp, const float* qq, float* dst, void* ws,
                      long long ws_bytes, hyres_stream_t s) {
-    HY_REQUIRE(d && pp && qq && dst, HYRES_E_ARG, "wgrad: NULL");
+    HY_REQUIRE(d0 && pp && qq && dst, HYRES_E_ARG, "wgrad: NULL");
+    const bool swap = wgrad_swap(d0);
+    const hyres_wgrad_desc dd = swap ? wgrad_swapped(d0) : *d0;
+    const hyres_wgrad_desc* d = &dd;
+    if (swap) std::swap(pp, qq);
     WgradPlan p = wgrad_plan(d);
     long long need = (long long)p.nsplit * d->ntaps * (long long)d->M * d->N * 4;
     HY_REQUIRE(ws && ws_bytes >= need, HYRES_E_WORKSPACE, "wgrad: workspace %lld < %lld", ws_bytes, need);
     const bool vp = (d->M % 4 == 0) && (d->ldp % 4 == 0) && aligned16(pp);
-    const bool vq = (d->N % 4 == 0) && (d->ldq % 4 == 0) && aligned16(qq);
+    const bool vq = !p.tapn && (d->N % 4 == 0) && (d->ldq % 4 == 0) && aligned16(qq);
+    HY_REQUIRE(!d->square_q || (vp && vq), HYRES_E_SHAPE, "wgrad: square_q needs the vector path");
     WgradArgs a;
     a.d = *d; a.p = pp; a.q = qq; a.slab = (float*)ws; a.chunks_per_split = p.cps; a.nchunks = p.nchunks;
-    a.mtiles = p.mtiles;
-    dim3 grid(p.mtiles * p.ntiles, d->ntaps, p.nsplit);
+    a.mtiles = p.mtiles; a.ntiles = p.ntiles; a.ngroups = p.ngroups; a.nblocks = p.nblocks; a.tapn = p.tapn;
+    dim3 grid(ceil_div(p.nblocks, 8) * 8);
     hipStream_t st = as_stream(s);
-#define WG_LAUNCH(TM_, TN_, WM_, WN_)                                                                  \
-    do {                                                                                              \
-        if (vp && vq && d->square_q)                                                                  \
-            hipLaunchKernelGGL((wgrad_kernel<TM_, TN_, WM_, WN_, true, true, true>), grid, dim3(256), 0, st, a); \
-        else if (vp && vq)                                                                            \
-            hipLaunchKernelGGL((wgrad_kernel<TM_, TN_, WM_, WN_, true, true, false>), grid, dim3(256), 0, st, a); \
-        else if (d->square_q)                                                                         \
-            return set_error(HYRES_E_SHAPE, "wgrad: square_q needs vector path");                    \
-        else if (vp)                                                                                  \
-            hipLaunchKernelGGL((wgrad_kernel<TM_, TN_, WM_, WN_, true, false, false>), grid, dim3(256), 0, st, a); \
-        else if (vq)                                                                                  \
-            hipLaunchKernelGGL((wgrad_kernel<TM_, TN_, WM_, WN_, false, true, false>), grid, dim3(256), 0, st, a); \
-        else                                                                                          \
-            hipLaunchKernelGGL((wgrad_kernel<TM_, TN_, WM_, WN_, false, false, false>), grid, dim3(256), 0, st, a); \
-    } while (0)
-    if (p.TMc == 2) WG_LAUNCH(2, 2, 2, 2);
-    else if (p.WMc == 1) WG_LAUNCH(1, 1, 1, 4);
-    else if (p.WNc == 1) WG_LAUNCH(1, 1, 4, 1);
-    else WG_LAUNCH(1, 1, 2, 2);
-#undef WG_LAUNCH
+    const bool sqr = d->square_q != 0;
+    if (p.TMc == 2 && p.TNc == 2) launch_wgrad<2, 2, 2, 2, 1>(a, vp, vq, sqr, grid, st);
+    else if (p.TMc == 2) launch_wgrad<2, 1, 2, 2, 1>(a, vp, vq, sqr, grid, st);
+    else if (p.WMc == 1) launch_wgrad<1, 1, 1, 4, 1>(a, vp, vq, sqr, grid, st);
+    else if (p.WNc == 1) launch_wgrad<1, 1, 4, 1, 1>(a, vp, vq, sqr, grid, st);
+    else if (p.NT == 9) launch_wgrad<1, 1, 2, 2, 9>(a, vp, vq, sqr, grid, st);
+    else if (p.NT == 5) launch_wgrad<1, 1, 2, 2, 5>(a, vp, vq, sqr, grid, st);
+    else launch_wgrad<1, 1, 2, 2, 1>(a, vp, vq, sqr, grid, st);
     int rc = HY_LAUNCH_CHECK("wgrad_kernel");
     if (rc) return rc;
-    long long total = (long long)d->ntaps * d->M * d->N;
-    int blocks = (int)std::min<long long>((total + 255) / 256, 8192);
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, (const float*)ws, p.nsplit,
+    const long long total = (long long)d->ntaps * d->M * d->N;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(ceil_div(total, 64)), dim3(256), 0, st, (const float*)ws, p.nsplit,
                        d->ntaps, d->M, d->N, dst, d->sm, d->sn, d->st, d->accumulate);
     return HY_LAUNCH_CHECK("wgrad_reduce_kernel");
 }

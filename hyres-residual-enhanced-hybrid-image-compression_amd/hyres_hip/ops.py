@@ -322,8 +322,22 @@ def _colsum_into(g: torch.Tensor, P: int, C: int, ld: int, dst: torch.Tensor, ac
 def _wgrad(desc: L.WgradDesc, p_ptr: int, q_ptr: int, dst: torch.Tensor, device) -> None:
     nbytes = L.load().hyres_wgrad_workspace_bytes(ctypes.byref(desc))
     ws = _ws(nbytes, device, slot=2)
+    timed = KernelTimer.enabled and KernelTimer.all_convs
+    if timed:
+        s0 = torch.cuda.Event(enable_timing=True)
+        s1 = torch.cuda.Event(enable_timing=True)
+        s0.record()
     L.call("hyres_conv_wgrad", ctypes.byref(desc), p_ptr, q_ptr, dst.data_ptr(), ws.data_ptr(), ws.numel(),
            L.stream())
+    if timed:
+        s1.record()
+        d = desc
+        q = d.B * d.Hq * d.Wq
+        flops = 2.0 * q * d.ntaps * d.M * d.N
+        nbytes_alg = 4.0 * (q * d.M + d.B * d.Hqq * d.Wqq * d.N + d.ntaps * d.M * d.N)
+        name = (f"WGRAD B{d.B} P {d.Hq}x{d.Wq}x{d.M} Q {d.Hqq}x{d.Wqq}x{d.N} taps{d.ntaps} sq{d.sq}"
+                f"{' sqr' if d.square_q else ''}")
+        KernelTimer.table.append((name, s0, s1, flops, nbytes_alg))
 
 
 def _act_backward(y: Node, gy: torch.Tensor, gy_ld: int, act: int, pre: Optional[torch.Tensor],

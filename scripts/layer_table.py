@@ -52,7 +52,7 @@ def main():
         e[0] += 1
         e[1] += ms
     tot = sum(v[1] for v in agg.values())
-    print(f"total conv time {tot:.2f} ms, {sum(v[0] for v in agg.values())} launches")
+    print(f"total conv+wgrad time {tot:.2f} ms, {sum(v[0] for v in agg.values())} launches")
     print(f"{'ms':>7} {'n':>3} {'us/launch':>9} {'TF/s':>7} {'GB/s':>7}  geometry")
     for d, (n, ms, fl, by) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
         us = 1000 * ms / n

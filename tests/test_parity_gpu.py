@@ -45,6 +45,9 @@ CONV_CASES = [
     (1, 768, 640, 4, 4, 1, 1, 0, 1),
     (2, 192, 128, 8, 8, 3, 1, 1, 1),
     (3, 96, 40, 12, 20, 3, 1, 1, 1),
+    (2, 64, 96, 16, 16, 5, 1, 2, 1),   # wgrad: 5 fused taps per block
+    (2, 5, 48, 12, 12, 3, 1, 1, 1),    # wgrad: taps folded into N (N=5)
+    (2, 48, 5, 12, 12, 3, 1, 1, 1),    # wgrad: small-M swap (M=5)
 ]
 
 
