@@ -37,7 +37,8 @@ class FlatParams:
             cur += (p.numel() + 3) // 4 * 4
         self.numel = cur
         self.data = torch.empty(cur, dtype=torch.float32, device=dev)
-        self.grad = O.zeros((cur,), dev)
+        # CPU buffers only exist for the gloo tests of the reducer (host plumbing, no compute)
+        self.grad = O.zeros((cur,), dev) if dev.type == "cuda" else torch.zeros(cur, dtype=torch.float32)
         for p, o in zip(self.params, offs):
             k = p.numel()
             view = self.data[o:o + k].view_as(p)
@@ -51,7 +52,10 @@ class FlatParams:
         for p, o in zip(self.params, self.offsets):
             if p.grad is None or p.grad.data_ptr() != self.grad.data_ptr() + 4 * o:
                 p.grad = self.grad[o:o + p.numel()].view_as(p)
-        O.zero_(self.grad)
+        if self.grad.is_cuda:
+            O.zero_(self.grad)
+        else:
+            self.grad.zero_()
 
 
 class FusedAdam(torch.optim.Optimizer):

@@ -1,0 +1,121 @@
+"""CPU, world_size 2 over gloo: the data-parallel gradient path (hyres_hip/ddp.py) that replaces the
+reference's nn.DataParallel (src/training.py:211-212, src/utils/dataset_utils.py:76-82).
+
+* FlatGradReducer averages the flat gradient buffer across ranks bucket by bucket (odd sizes, bucket
+  boundaries inside parameters);
+* broadcast_parameters makes every rank start from rank 0's weights;
+* the semantic claim of SURVEY.md §8(e): with equal shards, averaging the per-rank gradients of the
+  per-rank RD loss (src/losses/rd_loss.py:18-44 normalises by the LOCAL N*H*W) equals the gradient of
+  the global-batch loss.  Checked with the oracle on the committed reference fixture batch (2 images,
+  one per rank).
+"""
+import os
+import socket
+import sys
+import types
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _init(rank, world, port):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(2)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+
+def _reducer_worker(rank, world, port):
+    _init(rank, world, port)
+    try:
+        from hyres_hip.ddp import FlatGradReducer, broadcast_parameters
+        from hyres_hip.optim import FlatParams
+        shapes = [(7,), (3, 5), (129,), (2, 2, 3), (1,), (64, 3)]
+        gen = torch.Generator().manual_seed(100 + rank)  # ranks start from different weights
+        params = [torch.nn.Parameter(torch.randn(s, generator=gen)) for s in shapes]
+        mod = torch.nn.Module()
+        for i, p in enumerate(params):
+            mod.register_parameter(f"p{i}", p)
+        mod.register_buffer("buf", torch.full((5,), float(rank)))
+        broadcast_parameters(mod)
+        g0 = torch.Generator().manual_seed(100)
+        ref = [torch.randn(s, generator=g0) for s in shapes]
+        for p, r in zip(params, ref):
+            assert torch.equal(p.data, r)
+        assert torch.equal(mod.buf, torch.zeros(5))
+        flat = FlatParams(params)
+        for i, p in enumerate(params):
+            p.grad.copy_(torch.arange(p.numel(), dtype=torch.float32).view_as(p) * (rank + 1) + i)
+        red = FlatGradReducer(flat, world, bucket_bytes=40)  # 10 floats per bucket: boundaries inside params
+        assert len(red.buckets) > len(params)
+        red.all_reduce()
+        mean_scale = sum(r + 1 for r in range(world)) / world
+        for i, p in enumerate(params):
+            want = torch.arange(p.numel(), dtype=torch.float32).view_as(p) * mean_scale + i
+            assert torch.allclose(p.grad, want, rtol=0, atol=1e-6), i
+        # params are views of the flat buffer; the 16-byte alignment padding stays zero
+        for p, o in zip(params, flat.offsets):
+            assert p.data.data_ptr() == flat.data.data_ptr() + 4 * o
+    finally:
+        dist.destroy_process_group()
+
+
+def _grad_vector(orc_sd, keys):
+    out = []
+    for k in keys:
+        t = orc_sd[k]
+        out.append(torch.zeros(t.numel()) if t.grad is None else t.grad.detach().reshape(-1).clone())
+    return torch.cat(out)
+
+
+def _oracle_grads(x, jpeg, lmbda, jpeg_bpp):
+    from helpers import oracle_from, recipe_state_dict, _is_param_key
+    from oracle import rd_loss
+    sd = recipe_state_dict()
+    orc, sd2 = oracle_from(sd, requires_grad=True)
+    out = orc.forward(x, jpeg, jpeg_bpp, training=False)
+    out["jpeg_bpp_loss"] = torch.tensor(jpeg_bpp)
+    rd_loss(out, x, lmbda)["loss"].backward()
+    keys = [k for k in sd2 if _is_param_key(k) and sd2[k].is_floating_point() and sd2[k].requires_grad]
+    return _grad_vector(sd2, keys), keys
+
+
+def _sharded_worker(rank, world, port):
+    _init(rank, world, port)
+    try:
+        sys.path.insert(0, HERE)
+        from helpers import load_meta, load_npz
+        from hyres_hip.ddp import FlatGradReducer
+        g = load_npz("hyres_eval_b2_64.npz")
+        meta = load_meta()
+        lmbda = meta["train_lambda"]
+        jb = float(g["jpeg_bpp"])
+        x, jpeg = g["x"], g["jpeg_decoded"]
+        assert x.shape[0] == world
+        vec, keys = _oracle_grads(x[rank:rank + 1], jpeg[rank:rank + 1], lmbda, jb)
+        flat = types.SimpleNamespace(grad=vec, numel=vec.numel())
+        FlatGradReducer(flat, world, bucket_bytes=1 << 20).all_reduce()
+        if rank == 0:
+            full, _ = _oracle_grads(x, jpeg, lmbda, jb)
+            err = float((vec - full).norm() / full.norm())
+            assert err < 1e-5, err
+    finally:
+        dist.destroy_process_group()
+
+
+def test_flat_grad_reducer_gloo_world2():
+    mp.spawn(_reducer_worker, args=(2, _free_port()), nprocs=2, join=True)
+
+
+def test_sharded_gradient_equals_global_batch_gloo_world2():
+    mp.spawn(_sharded_worker, args=(2, _free_port()), nprocs=2, join=True)
