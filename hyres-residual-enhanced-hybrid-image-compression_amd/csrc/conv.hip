@@ -142,7 +142,7 @@ __device__ __forceinline__ void epi_store4(const hyres_epilogue& e, float* y, in
     st4(yp, make_float4(o[0], o[1], o[2], o[3]));
 }
 
-template <int TM, int TN, int WAVES_M, int WAVES_N, int MODE>
+template <int TM, int TN, int WAVES_M, int WAVES_N, int MODE, bool SPLITK>
 __global__ __launch_bounds__(256) void conv_fwd_kernel(const ConvArgs a) {
     // MODE 0: Ci % 32 == 0 (float4 loads); 1: same + square A (GDN); 2: generic scalar (small Ci).
     constexpr int BM = 32 * TM * WAVES_M;
@@ -154,8 +154,9 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const ConvArgs a) {
 
     const hyres_conv_geom& g = a.g;
     const int tid = threadIdx.x;
-    const int phase = blockIdx.z / a.nsplit;
-    const int split = blockIdx.z - phase * a.nsplit;
+    const int nsplit = SPLITK ? a.nsplit : 1;
+    const int phase = blockIdx.z / nsplit;
+    const int split = blockIdx.z - phase * nsplit;
     const int m0 = blockIdx.x * BM;
     const int n0 = blockIdx.y * BN;
     const int HqWq = g.Hq * g.Wq;
@@ -274,8 +275,8 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const ConvArgs a) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    const int kbeg = (a.nsplit > 1) ? min(nk, split * a.cps) : 0;
-    const int kend = (a.nsplit > 1) ? min(nk, kbeg + a.cps) : nk;
+    const int kbeg = SPLITK ? min(nk, split * a.cps) : 0;
+    const int kend = SPLITK ? min(nk, kbeg + a.cps) : nk;
     if (kbeg < kend) load_chunk(kbeg);
     for (int kc = kbeg; kc < kend; ++kc) {
         __syncthreads();
@@ -311,7 +312,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const ConvArgs a) {
     // one NHWC pixel row (float4 when every operand is 16B aligned), each row decoded once.
     constexpr int CW = 32 * WAVES_N, CP = CW + 8;  // +8: the two lane halves hit disjoint banks
     float* Cs = smem;
-    const bool split_k = a.nsplit > 1;
+    constexpr bool split_k = SPLITK;
     float* slab = split_k ? a.slab + ((long long)(split * g.nphase + phase) * a.M) * g.Co : nullptr;
     const bool linear = g.nphase == 1 && g.osh == 1 && g.osw == 1 && g.Ho == g.Hq && g.Wo == g.Wq;
     const int oph = g.oph[phase], opw = g.opw[phase];
@@ -332,7 +333,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const ConvArgs a) {
             const int n = n0 + (col >> 5) * TN * 32 + tn * 32 + (col & 31);
             if (m >= a.M || n >= g.Co) continue;
             const float4 v = *reinterpret_cast<const float4*>(&Cs[row * CP + col]);
-            if (split_k) {
+            if constexpr (split_k) {
                 float* sp = slab + (long long)m * g.Co + n;
                 if (a.vec4) {
                     *reinterpret_cast<float4*>(sp) = v;
@@ -776,9 +777,16 @@ template <int TM, int TN, int WM_, int WN_>
 static int launch_fwd(const ConvArgs& a, int mode, hipStream_t st) {
     constexpr int BM = 32 * TM * WM_, BN = 32 * TN * WN_;
     dim3 grid(ceil_div(a.M, BM), ceil_div(a.g.Co, BN), a.g.nphase * a.nsplit);
-    if (mode == 0) hipLaunchKernelGGL((conv_fwd_kernel<TM, TN, WM_, WN_, 0>), grid, dim3(256), 0, st, a);
-    else if (mode == 1) hipLaunchKernelGGL((conv_fwd_kernel<TM, TN, WM_, WN_, 1>), grid, dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((conv_fwd_kernel<TM, TN, WM_, WN_, 2>), grid, dim3(256), 0, st, a);
+    // split-K launches are a separate instantiation (partials to the slab, no epilogue)
+    if (a.nsplit > 1) {
+        if (mode == 0) hipLaunchKernelGGL((conv_fwd_kernel<TM, TN, WM_, WN_, 0, true>), grid, dim3(256), 0, st, a);
+        else if (mode == 1) hipLaunchKernelGGL((conv_fwd_kernel<TM, TN, WM_, WN_, 1, true>), grid, dim3(256), 0, st, a);
+        else hipLaunchKernelGGL((conv_fwd_kernel<TM, TN, WM_, WN_, 2, true>), grid, dim3(256), 0, st, a);
+    } else {
+        if (mode == 0) hipLaunchKernelGGL((conv_fwd_kernel<TM, TN, WM_, WN_, 0, false>), grid, dim3(256), 0, st, a);
+        else if (mode == 1) hipLaunchKernelGGL((conv_fwd_kernel<TM, TN, WM_, WN_, 1, false>), grid, dim3(256), 0, st, a);
+        else hipLaunchKernelGGL((conv_fwd_kernel<TM, TN, WM_, WN_, 2, false>), grid, dim3(256), 0, st, a);
+    }
     return HY_LAUNCH_CHECK("conv_fwd_kernel");
 }
 

@@ -255,8 +255,9 @@ def _filter_taps(g: L.ConvGeom, mask: Optional[torch.Tensor]) -> L.ConvGeom:
 
 
 class KernelTimer:
-    """Optional HIP-event timing of the dominant kernel (conv_fwd_kernel<2,2,2,2,0>: Co > 64,
-    Ci % 32 == 0, no square prologue) with its algorithmic FLOPs, for bench.py's roofline line."""
+    """Optional HIP-event timing of the dominant kernel (conv_fwd_kernel<2,2,2,2,0,false>: Co > 64,
+    Ci % 32 == 0, no square prologue, fused epilogue) with its algorithmic FLOPs/bytes, for bench.py's
+    roofline line."""
 
     enabled = False
     all_convs = False  # record every conv launch (layer table), not only the dominant variant
@@ -271,11 +272,12 @@ class KernelTimer:
     @classmethod
     def summary(cls):
         torch.cuda.synchronize()
-        ms = sum(a.elapsed_time(b) for a, b, _ in cls.events)
-        flops = sum(f for _, _, f in cls.events)
+        ms = sum(ev[0].elapsed_time(ev[1]) for ev in cls.events)
+        flops = sum(ev[2] for ev in cls.events)
+        nbytes = sum(ev[3] for ev in cls.events)
         n = len(cls.events)
         return {"launches": n, "total_ms": ms, "avg_us": 1000.0 * ms / max(n, 1), "flops": flops,
-                "flops_per_launch": flops / max(n, 1)}
+                "flops_per_launch": flops / max(n, 1), "bytes_per_launch": nbytes / max(n, 1)}
 
 
 def conv_flops(g: L.ConvGeom) -> float:
@@ -294,20 +296,21 @@ def conv_bytes(g: L.ConvGeom, e: L.Epilogue) -> float:
 
 
 def _launch_conv(g: L.ConvGeom, x_ptr: int, w2: torch.Tensor, ldw: int, y_ptr: int, e: L.Epilogue) -> None:
-    dominant = g.Co > 64 and g.Ci % 32 == 0 and not e.square_input
+    nb = L.load().hyres_conv_workspace_bytes(ctypes.byref(g))  # > 0 iff the launch is split-K
+    # the roofline kernel: conv_fwd_kernel<2,2,2,2,0,false> (Co > 64, Ci % 32 == 0, fused epilogue)
+    dominant = g.Co > 64 and g.Ci % 32 == 0 and not e.square_input and nb == 0
     timed = KernelTimer.enabled and (dominant or KernelTimer.all_convs)
     if timed:
         s0 = torch.cuda.Event(enable_timing=True)
         s1 = torch.cuda.Event(enable_timing=True)
         s0.record()
-    nb = L.load().hyres_conv_workspace_bytes(ctypes.byref(g))
     ws = _ws(nb, w2.device, slot=6) if nb > 0 else None
     L.call("hyres_conv_forward", ctypes.byref(g), x_ptr, w2.data_ptr(), ldw, y_ptr, ctypes.byref(e),
            None if ws is None else ws.data_ptr(), 0 if ws is None else ws.numel(), L.stream())
     if timed:
         s1.record()
         if dominant:
-            KernelTimer.events.append((s0, s1, conv_flops(g)))
+            KernelTimer.events.append((s0, s1, conv_flops(g), conv_bytes(g, e)))
         if KernelTimer.all_convs:
             desc = (f"B{g.B} {g.Hi}x{g.Wi}x{g.Ci}->{g.Ho}x{g.Wo}x{g.Co} taps{g.ntaps} ph{g.nphase} "
                     f"s{g.ish} epi{e.kind}{'+acc' if e.accumulate else ''}{'+res' if e.res else ''}")
