@@ -58,6 +58,7 @@ __device__ __forceinline__ void epi_store(const hyres_epilogue& e, float* y, int
             if (e.out2) e.out2[pix * e.ldo2 + n] = v;  // pre-activation (PReLU backward)
             if (e.act == HYRES_ACT_RELU) v = fmaxf(v, 0.f);
             else if (e.act == HYRES_ACT_PRELU) v = v >= 0.f ? v : c.slope * v;
+            else if (e.act == HYRES_ACT_RELU_MASK) v = e.aux0[pix * e.ld0 + n] > 0.f ? v : 0.f;
             break;
         }
         case HYRES_EPI_GDN:
@@ -104,6 +105,12 @@ __device__ __forceinline__ void epi_store4(const hyres_epilogue& e, float* y, in
             } else if (e.act == HYRES_ACT_PRELU) {
 #pragma unroll
                 for (int c = 0; c < 4; ++c) o[c] = o[c] >= 0.f ? o[c] : slope * o[c];
+            } else if (e.act == HYRES_ACT_RELU_MASK) {
+                const float4 y = ld4(e.aux0 + pix * e.ld0 + n);
+                o[0] = y.x > 0.f ? o[0] : 0.f;
+                o[1] = y.y > 0.f ? o[1] : 0.f;
+                o[2] = y.z > 0.f ? o[2] : 0.f;
+                o[3] = y.w > 0.f ? o[3] : 0.f;
             }
             break;
         }
@@ -407,6 +414,7 @@ struct WgradArgs {
     int mtiles, ntiles, ngroups;
     int nblocks;  // logical blocks (grid padded to a multiple of 8 for the XCD remap)
     int tapn;
+    float* bias_slab;  // [nsplit][M] column sums of P (the bias gradient) or NULL
 };
 
 template <typename F, int... Is>
@@ -570,6 +578,9 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgradArgs a) {
 #pragma unroll
                 for (int r = 0; r < 16; ++r) acc[j][i][k][r] = 0.f;
 
+    // bias gradient = column sums of P over all pixels: one column tile / tap group per split does it
+    const bool do_bias = a.bias_slab != nullptr && nt == 0 && grp == 0;
+    float bsum = 0.f;
     const int kc_begin = split * a.chunks_per_split;
     const int kc_end = min(a.nchunks, kc_begin + a.chunks_per_split);
     if (kc_begin < kc_end) {
@@ -584,6 +595,10 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgradArgs a) {
             if (j == 0) store_p();
             store_q();
             __syncthreads();
+            if (j == 0 && do_bias && tid < BM) {
+#pragma unroll 8
+                for (int k = 0; k < KT; ++k) bsum += Ps[k * PP + tid];
+            }
             if (j + 1 < NT) {
                 load_q(t0 + j + 1);
             } else if (kc + 1 < kc_end) {
@@ -607,6 +622,7 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgradArgs a) {
             }
         });
     }
+    if (do_bias && tid < BM && m0 + tid < d.M) a.bias_slab[(long long)split * d.M + m0 + tid] = bsum;
     // slab store [split][t][M][N]
     const long long MN = (long long)d.M * d.N;
     static_for<NT>([&](auto J) {
@@ -639,6 +655,7 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* slab, in
     float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
     if ((total & 3) == 0) {
         if (base < total)
+#pragma unroll 4
             for (int k = ly; k < nsplit; k += 16) {
                 const float4 v = ld4(slab + k * total + base);
                 s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
@@ -1012,6 +1029,8 @@ int hyres_conv_forward(const hyres_conv_geom* g, const float* x, const float* w2
     if (e->kind == HYRES_EPI_GDN_BWD || e->kind == HYRES_EPI_IGDN_BWD)
         HY_REQUIRE(e->aux0 && e->aux1 && e->aux2, HYRES_E_ARG, "conv: GDN bwd epilogue needs aux0..2");
     if (e->act == HYRES_ACT_PRELU) HY_REQUIRE(e->slope, HYRES_E_ARG, "conv: PReLU needs slope");
+    if (e->act == HYRES_ACT_RELU_MASK)
+        HY_REQUIRE(e->aux0 && e->kind == HYRES_EPI_BIAS, HYRES_E_ARG, "conv: ReLU mask needs aux0, BIAS epilogue");
     hipStream_t st = as_stream(s);
     int rc;
     if (g->Co > 64) rc = launch_fwd<2, 2, 2, 2>(a, mode, st);
@@ -1129,28 +1148,39 @@ static void launch_wgrad(const WgradArgs& a, bool vp, bool vq, bool sqr, dim3 gr
 
 extern "C" {
 
-long long hyres_wgrad_workspace_bytes(const hyres_wgrad_desc* d) {
-    hyres_wgrad_desc e = wgrad_swap(d) ? wgrad_swapped(d) : *d;
-    WgradPlan p = wgrad_plan(&e);
-    return (long long)p.nsplit * e.ntaps * (long long)e.M * e.N * 4;
+static long long wgrad_slab_floats(const hyres_wgrad_desc* e, const WgradPlan& p) {
+    return (long long)p.nsplit * e->ntaps * (long long)e->M * e->N;
 }
 
-int hyres_conv_wgrad(const hyres_wgrad_desc* d0, const float* pp, const float* qq, float* dst, void* ws,
-                     long long ws_bytes, hyres_stream_t s) {
+long long hyres_wgrad_workspace_bytes(const hyres_wgrad_desc* d) {
+    const bool swap = wgrad_swap(d);
+    hyres_wgrad_desc e = swap ? wgrad_swapped(d) : *d;
+    WgradPlan p = wgrad_plan(&e);
+    // + the bias-gradient partials: [nsplit][M] in the kernel, or colsum partials when swapped
+    const long long bias = swap ? hyres_colsum_workspace_bytes(d->B * d->Hq * d->Wq, d->M) / 4 + 4
+                                : (long long)p.nsplit * e.M + 4;
+    return (wgrad_slab_floats(&e, p) + bias) * 4;
+}
+
+int hyres_conv_wgrad(const hyres_wgrad_desc* d0, const float* pp, const float* qq, float* dst, float* dbias,
+                     void* ws, long long ws_bytes, hyres_stream_t s) {
     HY_REQUIRE(d0 && pp && qq && dst, HYRES_E_ARG, "wgrad: NULL");
+    const long long need = hyres_wgrad_workspace_bytes(d0);
+    HY_REQUIRE(ws && ws_bytes >= need, HYRES_E_WORKSPACE, "wgrad: workspace %lld < %lld", ws_bytes, need);
+    const float* p_orig = pp;
     const bool swap = wgrad_swap(d0);
     const hyres_wgrad_desc dd = swap ? wgrad_swapped(d0) : *d0;
     const hyres_wgrad_desc* d = &dd;
     if (swap) std::swap(pp, qq);
     WgradPlan p = wgrad_plan(d);
-    long long need = (long long)p.nsplit * d->ntaps * (long long)d->M * d->N * 4;
-    HY_REQUIRE(ws && ws_bytes >= need, HYRES_E_WORKSPACE, "wgrad: workspace %lld < %lld", ws_bytes, need);
+    float* bias_ws = (float*)ws + wgrad_slab_floats(d, p);
     const bool vp = (d->M % 4 == 0) && (d->ldp % 4 == 0) && aligned16(pp);
     const bool vq = !p.tapn && (d->N % 4 == 0) && (d->ldq % 4 == 0) && aligned16(qq);
     HY_REQUIRE(!d->square_q || (vp && vq), HYRES_E_SHAPE, "wgrad: square_q needs the vector path");
     WgradArgs a;
     a.d = *d; a.p = pp; a.q = qq; a.slab = (float*)ws; a.chunks_per_split = p.cps; a.nchunks = p.nchunks;
     a.mtiles = p.mtiles; a.ntiles = p.ntiles; a.ngroups = p.ngroups; a.nblocks = p.nblocks; a.tapn = p.tapn;
+    a.bias_slab = (dbias && !swap) ? bias_ws : nullptr;
     dim3 grid(ceil_div(p.nblocks, 8) * 8);
     hipStream_t st = as_stream(s);
     const bool sqr = d->square_q != 0;
@@ -1166,7 +1196,17 @@ int hyres_conv_wgrad(const hyres_wgrad_desc* d0, const float* pp, const float* q
     const long long total = (long long)d->ntaps * d->M * d->N;
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(ceil_div(total, 64)), dim3(256), 0, st, (const float*)ws, p.nsplit,
                        d->ntaps, d->M, d->N, dst, d->sm, d->sn, d->st, d->accumulate);
-    return HY_LAUNCH_CHECK("wgrad_reduce_kernel");
+    rc = HY_LAUNCH_CHECK("wgrad_reduce_kernel");
+    if (rc || !dbias) return rc;
+    if (swap) {  // P (= dY) is the tap-folded side here: plain column sums
+        const int P = d0->B * d0->Hq * d0->Wq;
+        return hyres_colsum(p_orig, P, d0->M, d0->ldp, dbias, d0->accumulate, bias_ws,
+                            hyres_colsum_workspace_bytes(P, d0->M), s);
+    }
+    // [nsplit][M] partials = a [nsplit][1][M][1] slab: the same parallel deterministic reduce
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(ceil_div(d->M, 64)), dim3(256), 0, st, (const float*)bias_ws, p.nsplit,
+                       1, d->M, 1, dbias, 1, 0, 0, d->accumulate);
+    return HY_LAUNCH_CHECK("wgrad_reduce_kernel(bias)");
 }
 
 static int colsum_blocks(int P) {

@@ -24,12 +24,15 @@ __device__ __forceinline__ void src_index(float scale, int o, int in, int& i0, i
     l0 = 1.0f - l1;
 }
 
+// VEC channels per thread (4: float4 when C, ld % 4 == 0 and 16B-aligned pointers)
+template <int VEC>
 __global__ void bilinear_fwd_kernel(const float* x, int ldx, float* y, int ldy, int B, int Hi, int Wi, int Ho,
                                     int Wo, int C, float sh, float sw, int acc) {
-    const long long n = (long long)B * Ho * Wo * C;
+    const int CG = C / VEC;
+    const long long n = (long long)B * Ho * Wo * CG;
     GRID_STRIDE(i, n) {
-        const int c = (int)(i % C);
-        long long p = i / C;
+        const int c = (int)(i % CG) * VEC;
+        const long long p = i / CG;
         const int ow = (int)(p % Wo);
         const int oh = (int)((p / Wo) % Ho);
         const int b = (int)(p / ((long long)Wo * Ho));
@@ -38,11 +41,28 @@ __global__ void bilinear_fwd_kernel(const float* x, int ldx, float* y, int ldy, 
         src_index(sh, oh, Hi, h0, h1, lh0, lh1);
         src_index(sw, ow, Wi, w0, w1, lw0, lw1);
         const float* xb = x + (long long)b * Hi * Wi * ldx + c;
-        float v00 = xb[((long long)h0 * Wi + w0) * ldx], v01 = xb[((long long)h0 * Wi + w1) * ldx];
-        float v10 = xb[((long long)h1 * Wi + w0) * ldx], v11 = xb[((long long)h1 * Wi + w1) * ldx];
-        float v = lh0 * (lw0 * v00 + lw1 * v01) + lh1 * (lw0 * v10 + lw1 * v11);
+        const float* p00 = xb + ((long long)h0 * Wi + w0) * ldx;
+        const float* p01 = xb + ((long long)h0 * Wi + w1) * ldx;
+        const float* p10 = xb + ((long long)h1 * Wi + w0) * ldx;
+        const float* p11 = xb + ((long long)h1 * Wi + w1) * ldx;
         float* yp = y + p * ldy + c;
-        *yp = acc ? *yp + v : v;
+        if constexpr (VEC == 4) {
+            const float4 a = *reinterpret_cast<const float4*>(p00), bq = *reinterpret_cast<const float4*>(p01);
+            const float4 cq = *reinterpret_cast<const float4*>(p10), d = *reinterpret_cast<const float4*>(p11);
+            float4 v;
+            v.x = lh0 * (lw0 * a.x + lw1 * bq.x) + lh1 * (lw0 * cq.x + lw1 * d.x);
+            v.y = lh0 * (lw0 * a.y + lw1 * bq.y) + lh1 * (lw0 * cq.y + lw1 * d.y);
+            v.z = lh0 * (lw0 * a.z + lw1 * bq.z) + lh1 * (lw0 * cq.z + lw1 * d.z);
+            v.w = lh0 * (lw0 * a.w + lw1 * bq.w) + lh1 * (lw0 * cq.w + lw1 * d.w);
+            if (acc) {
+                const float4 o = *reinterpret_cast<const float4*>(yp);
+                v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+            }
+            *reinterpret_cast<float4*>(yp) = v;
+        } else {
+            const float v = lh0 * (lw0 * p00[0] + lw1 * p01[0]) + lh1 * (lw0 * p10[0] + lw1 * p11[0]);
+            *yp = acc ? *yp + v : v;
+        }
     }
 }
 
@@ -57,13 +77,15 @@ __device__ __forceinline__ float bw_weight(float scale, int o, int in, int targe
     return w;
 }
 
+template <int VEC>
 __global__ void bilinear_bwd_kernel(const float* gy, int ldgy, float* gx, int ldgx, int B, int Hi, int Wi, int Ho,
                                     int Wo, int C, float sh, float sw, int acc) {
-    const long long n = (long long)B * Hi * Wi * C;
+    const int CG = C / VEC;
+    const long long n = (long long)B * Hi * Wi * CG;
     const float ish = 1.0f / sh, isw = 1.0f / sw;
     GRID_STRIDE(i, n) {
-        const int c = (int)(i % C);
-        long long p = i / C;
+        const int c = (int)(i % CG) * VEC;
+        const long long p = i / CG;
         const int w = (int)(p % Wi);
         const int h = (int)((p / Wi) % Hi);
         const int b = (int)(p / ((long long)Wi * Hi));
@@ -76,21 +98,35 @@ __global__ void bilinear_bwd_kernel(const float* gy, int ldgy, float* gx, int ld
         if (w == 0) ow_lo = 0;
         if (h == Hi - 1) oh_hi = Ho - 1;
         if (w == Wi - 1) ow_hi = Wo - 1;
-        float s = 0.f;
+        float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
         const float* gb = gy + (long long)b * Ho * Wo * ldgy + c;
         for (int oh = oh_lo; oh <= oh_hi; ++oh) {
-            float wh = bw_weight(sh, oh, Hi, h);
+            const float wh = bw_weight(sh, oh, Hi, h);
             if (wh == 0.f) continue;
-            float rs = 0.f;
+            float4 rs = make_float4(0.f, 0.f, 0.f, 0.f);
             for (int ow = ow_lo; ow <= ow_hi; ++ow) {
-                float ww = bw_weight(sw, ow, Wi, w);
+                const float ww = bw_weight(sw, ow, Wi, w);
                 if (ww == 0.f) continue;
-                rs += ww * gb[((long long)oh * Wo + ow) * ldgy];
+                const float* q = gb + ((long long)oh * Wo + ow) * ldgy;
+                if constexpr (VEC == 4) {
+                    const float4 v = *reinterpret_cast<const float4*>(q);
+                    rs.x += ww * v.x; rs.y += ww * v.y; rs.z += ww * v.z; rs.w += ww * v.w;
+                } else {
+                    rs.x += ww * q[0];
+                }
             }
-            s += wh * rs;
+            s.x += wh * rs.x; s.y += wh * rs.y; s.z += wh * rs.z; s.w += wh * rs.w;
         }
         float* gp = gx + p * ldgx + c;
-        *gp = acc ? *gp + s : s;
+        if constexpr (VEC == 4) {
+            if (acc) {
+                const float4 o = *reinterpret_cast<const float4*>(gp);
+                s.x += o.x; s.y += o.y; s.z += o.z; s.w += o.w;
+            }
+            *reinterpret_cast<float4*>(gp) = s;
+        } else {
+            *gp = acc ? *gp + s.x : s.x;
+        }
     }
 }
 
@@ -206,25 +242,33 @@ __global__ void se_bwd_x_kernel(const float* gy, const float* sgate, const float
 }
 
 // ---------------------------------------------------------------- SpatialAttention
-// one wave per pixel: mean and max over C channels (first-occurrence argmax kept implicit)
-__global__ void sa_pool_kernel(const float* x, float* pooled2, long long P, int C) {
+// One wave per pixel (C <= 256, C % 4 == 0: float4 per lane): channel mean, max and the first-occurrence
+// argmax (torch.max(dim=1) on CPU keeps the first maximal index; the backward routes g_max there).
+__global__ void sa_pool_kernel(const float* x, float* pooled2, int* amax, long long P, int C) {
     const int lane = threadIdx.x & 63;
     const long long p = (long long)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
     if (p >= P) return;
     const float* xp = x + p * C;
     float s = 0.f, m = -INFINITY;
-    for (int c = lane; c < C; c += 64) {
-        float v = xp[c];
-        s += v;
-        m = fmaxf(m, v);
+    int mi = 0x7fffffff;
+    for (int c = 4 * lane; c < C; c += 256) {
+        const float4 v = *reinterpret_cast<const float4*>(xp + c);
+        s += (v.x + v.y) + (v.z + v.w);
+        if (v.x > m) { m = v.x; mi = c; }
+        if (v.y > m) { m = v.y; mi = c + 1; }
+        if (v.z > m) { m = v.z; mi = c + 2; }
+        if (v.w > m) { m = v.w; mi = c + 3; }
     }
     for (int off = 32; off > 0; off >>= 1) {
         s += __shfl_xor(s, off);
-        m = fmaxf(m, __shfl_xor(m, off));
+        const float om = __shfl_xor(m, off);
+        const int oi = __shfl_xor(mi, off);
+        if (om > m || (om == m && oi < mi)) { m = om; mi = oi; }
     }
     if (lane == 0) {
         pooled2[p * 2 + 0] = s / (float)C;
         pooled2[p * 2 + 1] = m;
+        amax[p] = mi;
     }
 }
 __global__ void sa_conv_kernel(const float* pooled2, const float* w, float* attn, int B, int H, int W) {
@@ -251,9 +295,17 @@ __global__ void sa_conv_kernel(const float* pooled2, const float* w, float* attn
         attn[i] = 1.0f / (1.0f + expf(-s));
     }
 }
+// y = x * attn[p], float4 over channels (C % 4 == 0)
 __global__ void sa_mul_kernel(const float* x, const float* attn, float* y, long long P, int C) {
-    const long long n = P * C;
-    GRID_STRIDE(i, n) y[i] = x[i] * attn[i / C];
+    const int C4 = C >> 2;
+    const long long n = P * C4;
+    GRID_STRIDE(i, n) {
+        const long long p = i / C4;
+        const float a = attn[p];
+        float4 v = reinterpret_cast<const float4*>(x)[i];
+        v.x *= a; v.y *= a; v.z *= a; v.w *= a;
+        reinterpret_cast<float4*>(y)[i] = v;
+    }
 }
 // bwd 1: g_logit[p] = (sum_c gy*x) * a*(1-a)
 __global__ void sa_bwd_logit_kernel(const float* x, const float* gy, const float* attn, float* glogit, long long P,
@@ -262,18 +314,22 @@ __global__ void sa_bwd_logit_kernel(const float* x, const float* gy, const float
     const long long p = (long long)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
     if (p >= P) return;
     float s = 0.f;
-    for (int c = lane; c < C; c += 64) s += gy[p * C + c] * x[p * C + c];
+    for (int c = 4 * lane; c < C; c += 256) {
+        const float4 g = *reinterpret_cast<const float4*>(gy + p * C + c);
+        const float4 v = *reinterpret_cast<const float4*>(x + p * C + c);
+        s += (g.x * v.x + g.y * v.y) + (g.z * v.z + g.w * v.w);
+    }
     for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
     if (lane == 0) {
         float a = attn[p];
         glogit[p] = s * a * (1.0f - a);
     }
 }
-// bwd 2: g_pooled2 = transpose conv; weight-grad partials per block
-__global__ void sa_bwd_conv_kernel(const float* glogit, const float* pooled2, const float* w, float* gpooled2,
-                                   float* wpart, int B, int H, int W) {
+// bwd 2: g_pooled2 = transpose conv; weight-grad partials per block (wave shuffles, one barrier)
+__global__ __launch_bounds__(256) void sa_bwd_conv_kernel(const float* glogit, const float* pooled2, const float* w,
+                                                          float* gpooled2, float* wpart, int B, int H, int W) {
     __shared__ float ws[98];
-    __shared__ float red[256];
+    __shared__ float red[4][98];
     if (threadIdx.x < 98) ws[threadIdx.x] = w[threadIdx.x];
     __syncthreads();
     const long long n = (long long)B * H * W;
@@ -309,16 +365,17 @@ __global__ void sa_bwd_conv_kernel(const float* glogit, const float* pooled2, co
         gpooled2[i * 2 + 0] = g0;
         gpooled2[i * 2 + 1] = g1;
     }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
     for (int k = 0; k < 98; ++k) {
-        red[threadIdx.x] = gw[k];
-        __syncthreads();
-        for (int s = 128; s > 0; s >>= 1) {
-            if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
-            __syncthreads();
-        }
-        if (threadIdx.x == 0) wpart[(long long)blockIdx.x * 98 + k] = red[0];
-        __syncthreads();
+        float v = gw[k];
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+        if (lane == 0) red[wave][k] = v;
     }
+    __syncthreads();
+    if (threadIdx.x < 98)
+        wpart[(long long)blockIdx.x * 98 + threadIdx.x] =
+            (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]);
 }
 // one block per weight tap: 256 threads fold the per-block partials (deterministic order)
 __global__ void sa_bwd_wfinal_kernel(const float* wpart, int nb, float* gw) {
@@ -334,32 +391,24 @@ __global__ void sa_bwd_wfinal_kernel(const float* wpart, int nb, float* gw) {
     }
     if (threadIdx.x == 0) gw[k] += red[0];
 }
-// bwd 3: gx = gy*a + g_avg/C + [c == argmax] * g_max     (one wave per pixel)
-__global__ void sa_bwd_x_kernel(const float* x, const float* gy, const float* attn, const float* gpooled2, float* gx,
+// bwd 3: gx = gy*a + g_avg/C + [c == argmax] * g_max     (float4 over channels; argmax saved by the pool)
+__global__ void sa_bwd_x_kernel(const float* gy, const float* attn, const float* gpooled2, const int* amax, float* gx,
                                 long long P, int C) {
-    const int lane = threadIdx.x & 63;
-    const long long p = (long long)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
-    if (p >= P) return;
-    const float* xp = x + p * C;
-    // argmax (first occurrence, as torch.max(dim) on CPU)
-    float m = -INFINITY;
-    int mi = 0x7fffffff;
-    for (int c = lane; c < C; c += 64) {
-        float v = xp[c];
-        if (v > m) { m = v; mi = c; }
-    }
-    for (int off = 32; off > 0; off >>= 1) {
-        float om = __shfl_xor(m, off);
-        int oi = __shfl_xor(mi, off);
-        if (om > m || (om == m && oi < mi)) { m = om; mi = oi; }
-    }
-    const float a = attn[p];
-    const float gavg = gpooled2[p * 2 + 0] / (float)C;
-    const float gmax = gpooled2[p * 2 + 1];
-    for (int c = lane; c < C; c += 64) {
-        float v = gy[p * C + c] * a + gavg;
-        if (c == mi) v += gmax;
-        gx[p * C + c] = v;
+    const int C4 = C >> 2;
+    const long long n = P * C4;
+    GRID_STRIDE(i, n) {
+        const long long p = i / C4;
+        const int c = (int)(i - p * C4) * 4;
+        const float a = attn[p];
+        const float gavg = gpooled2[p * 2 + 0] / (float)C;
+        const float gmax = gpooled2[p * 2 + 1];
+        const int mi = amax[p];
+        float4 v = reinterpret_cast<const float4*>(gy)[i];
+        v.x = v.x * a + gavg + (c == mi ? gmax : 0.f);
+        v.y = v.y * a + gavg + (c + 1 == mi ? gmax : 0.f);
+        v.z = v.z * a + gavg + (c + 2 == mi ? gmax : 0.f);
+        v.w = v.w * a + gavg + (c + 3 == mi ? gmax : 0.f);
+        reinterpret_cast<float4*>(gx)[i] = v;
     }
 }
 
@@ -372,17 +421,27 @@ extern "C" {
 int hyres_bilinear_fwd(const float* x, int ldx, float* y, int ldy, int B, int Hi, int Wi, int Ho, int Wo, int C,
                        float scale_h, float scale_w, int accumulate, hyres_stream_t s) {
     HY_REQUIRE(x && y && Hi > 0 && Wi > 0 && Ho > 0 && Wo > 0, HYRES_E_ARG, "bilinear_fwd: bad args");
-    long long n = (long long)B * Ho * Wo * C;
-    hipLaunchKernelGGL(bilinear_fwd_kernel, dim3(grid_for_r(n)), dim3(256), 0, as_stream(s), x, ldx, y, ldy, B, Hi,
-                       Wi, Ho, Wo, C, scale_h, scale_w, accumulate);
+    const bool vec = C % 4 == 0 && ldx % 4 == 0 && ldy % 4 == 0 && aligned16(x) && aligned16(y);
+    long long n = (long long)B * Ho * Wo * (vec ? C / 4 : C);
+    if (vec)
+        hipLaunchKernelGGL(bilinear_fwd_kernel<4>, dim3(grid_for_r(n)), dim3(256), 0, as_stream(s), x, ldx, y, ldy, B,
+                           Hi, Wi, Ho, Wo, C, scale_h, scale_w, accumulate);
+    else
+        hipLaunchKernelGGL(bilinear_fwd_kernel<1>, dim3(grid_for_r(n)), dim3(256), 0, as_stream(s), x, ldx, y, ldy, B,
+                           Hi, Wi, Ho, Wo, C, scale_h, scale_w, accumulate);
     return HY_LAUNCH_CHECK("bilinear_fwd");
 }
 int hyres_bilinear_bwd(const float* gy, int ldgy, float* gx, int ldgx, int B, int Hi, int Wi, int Ho, int Wo, int C,
                        float scale_h, float scale_w, int accumulate, hyres_stream_t s) {
     HY_REQUIRE(gy && gx, HYRES_E_ARG, "bilinear_bwd: NULL");
-    long long n = (long long)B * Hi * Wi * C;
-    hipLaunchKernelGGL(bilinear_bwd_kernel, dim3(grid_for_r(n)), dim3(256), 0, as_stream(s), gy, ldgy, gx, ldgx, B,
-                       Hi, Wi, Ho, Wo, C, scale_h, scale_w, accumulate);
+    const bool vec = C % 4 == 0 && ldgy % 4 == 0 && ldgx % 4 == 0 && aligned16(gy) && aligned16(gx);
+    long long n = (long long)B * Hi * Wi * (vec ? C / 4 : C);
+    if (vec)
+        hipLaunchKernelGGL(bilinear_bwd_kernel<4>, dim3(grid_for_r(n)), dim3(256), 0, as_stream(s), gy, ldgy, gx, ldgx,
+                           B, Hi, Wi, Ho, Wo, C, scale_h, scale_w, accumulate);
+    else
+        hipLaunchKernelGGL(bilinear_bwd_kernel<1>, dim3(grid_for_r(n)), dim3(256), 0, as_stream(s), gy, ldgy, gx, ldgx,
+                           B, Hi, Wi, Ho, Wo, C, scale_h, scale_w, accumulate);
     return HY_LAUNCH_CHECK("bilinear_bwd");
 }
 
@@ -440,25 +499,29 @@ long long hyres_spatial_attn_workspace_bytes(int B, int H, int W) {
     return (long long)nb * 98 * 4 + n * 4 + n * 2 * 4 + 1024;
 }
 
-int hyres_spatial_attn_fwd(const float* x, const float* w, float* pooled2, float* attn, float* y, int B, int H, int W,
-                           int C, hyres_stream_t s) {
-    HY_REQUIRE(x && w && pooled2 && attn && y, HYRES_E_ARG, "spatial_attn_fwd: NULL");
+int hyres_spatial_attn_fwd(const float* x, const float* w, float* pooled2, int* argmax, float* attn, float* y, int B,
+                           int H, int W, int C, hyres_stream_t s) {
+    HY_REQUIRE(x && w && pooled2 && argmax && attn && y, HYRES_E_ARG, "spatial_attn_fwd: NULL");
+    HY_REQUIRE(C % 4 == 0 && C <= 1024 && aligned16(x) && aligned16(y), HYRES_E_ALIGN,
+               "spatial_attn: C %% 4 == 0 and 16B-aligned x/y required");
     long long P = (long long)B * H * W;
     hipStream_t st = as_stream(s);
-    hipLaunchKernelGGL(sa_pool_kernel, dim3((unsigned)((P + 3) / 4)), dim3(256), 0, st, x, pooled2, P, C);
+    hipLaunchKernelGGL(sa_pool_kernel, dim3((unsigned)((P + 3) / 4)), dim3(256), 0, st, x, pooled2, argmax, P, C);
     int rc = HY_LAUNCH_CHECK("sa_pool");
     if (rc) return rc;
     hipLaunchKernelGGL(sa_conv_kernel, dim3(grid_for_r(P)), dim3(256), 0, st, (const float*)pooled2, w, attn, B, H, W);
     rc = HY_LAUNCH_CHECK("sa_conv");
     if (rc) return rc;
-    hipLaunchKernelGGL(sa_mul_kernel, dim3(grid_for_r(P * C)), dim3(256), 0, st, x, (const float*)attn, y, P, C);
+    hipLaunchKernelGGL(sa_mul_kernel, dim3(grid_for_r(P * C / 4)), dim3(256), 0, st, x, (const float*)attn, y, P, C);
     return HY_LAUNCH_CHECK("sa_mul");
 }
 
-int hyres_spatial_attn_bwd(const float* x, const float* w, const float* pooled2, const float* attn, const float* gy,
-                           float* gx, float* gw, int B, int H, int W, int C, void* ws, long long ws_bytes,
-                           hyres_stream_t s) {
-    HY_REQUIRE(x && w && pooled2 && attn && gy && gx && gw, HYRES_E_ARG, "spatial_attn_bwd: NULL");
+int hyres_spatial_attn_bwd(const float* x, const float* w, const float* pooled2, const int* argmax, const float* attn,
+                           const float* gy, float* gx, float* gw, int B, int H, int W, int C, void* ws,
+                           long long ws_bytes, hyres_stream_t s) {
+    HY_REQUIRE(x && w && pooled2 && argmax && attn && gy && gx && gw, HYRES_E_ARG, "spatial_attn_bwd: NULL");
+    HY_REQUIRE(C % 4 == 0 && C <= 1024 && aligned16(x) && aligned16(gy) && aligned16(gx), HYRES_E_ALIGN,
+               "spatial_attn: C %% 4 == 0 and 16B-aligned x/gy/gx required");
     long long P = (long long)B * H * W;
     HY_REQUIRE(ws && ws_bytes >= hyres_spatial_attn_workspace_bytes(B, H, W), HYRES_E_WORKSPACE,
                "spatial_attn_bwd: workspace");
@@ -477,8 +540,8 @@ int hyres_spatial_attn_bwd(const float* x, const float* w, const float* pooled2,
     hipLaunchKernelGGL(sa_bwd_wfinal_kernel, dim3(98), dim3(256), 0, st, (const float*)wpart, nb, gw);
     rc = HY_LAUNCH_CHECK("sa_bwd_wfinal");
     if (rc) return rc;
-    hipLaunchKernelGGL(sa_bwd_x_kernel, dim3((unsigned)((P + 3) / 4)), dim3(256), 0, st, x, gy, attn,
-                       (const float*)gp2, gx, P, C);
+    hipLaunchKernelGGL(sa_bwd_x_kernel, dim3(grid_for_r(P * C / 4)), dim3(256), 0, st, gy, attn, (const float*)gp2,
+                       argmax, gx, P, C);
     return HY_LAUNCH_CHECK("sa_bwd_x");
 }
 

@@ -18,7 +18,7 @@ LIB_PATH = os.path.join(HERE, "libhyres_hip.so")
 MAX_TAPS = 49
 WPREP_CONV, WPREP_CONV_DGRAD, WPREP_DECONV, WPREP_DECONV_DGRAD = 0, 1, 2, 3
 EPI_BIAS, EPI_GDN, EPI_IGDN, EPI_GDN_BWD, EPI_IGDN_BWD = 0, 1, 2, 3, 4
-ACT_NONE, ACT_RELU, ACT_PRELU = 0, 1, 2
+ACT_NONE, ACT_RELU, ACT_PRELU, ACT_RELU_MASK = 0, 1, 2, 3
 EB_REC = 64
 
 
@@ -74,7 +74,7 @@ _SIGS = {
     "hyres_wgrad_desc_conv2d": (_I, [ctypes.POINTER(WgradDesc)] + [_I] * 12),
     "hyres_wgrad_desc_deconv2d": (_I, [ctypes.POINTER(WgradDesc)] + [_I] * 9),
     "hyres_wgrad_workspace_bytes": (_LL, [ctypes.POINTER(WgradDesc)]),
-    "hyres_conv_wgrad": (_I, [ctypes.POINTER(WgradDesc), _P, _P, _P, _P, _LL, _P]),
+    "hyres_conv_wgrad": (_I, [ctypes.POINTER(WgradDesc), _P, _P, _P, _P, _P, _LL, _P]),
     "hyres_colsum": (_I, [_P, _I, _I, _I, _P, _I, _P, _LL, _P]),
     "hyres_colsum_workspace_bytes": (_LL, [_I, _I]),
     "hyres_nchw_to_nhwc": (_I, [_P, _P, _I, _I, _I, _I, _I, _P]),
@@ -113,8 +113,8 @@ _SIGS = {
     "hyres_se_fwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _LL, _P]),
     "hyres_se_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _LL, _P]),
     "hyres_se_workspace_bytes": (_LL, [_I, _I, _I]),
-    "hyres_spatial_attn_fwd": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _P]),
-    "hyres_spatial_attn_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _LL, _P]),
+    "hyres_spatial_attn_fwd": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P]),
+    "hyres_spatial_attn_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _LL, _P]),
     "hyres_spatial_attn_workspace_bytes": (_LL, [_I, _I, _I]),
     "hyres_sum_log": (_I, [_P, _LL, _P, _P, _LL, _P]),
     "hyres_sum_sqdiff": (_I, [_P, _P, _LL, _P, _P, _LL, _P]),

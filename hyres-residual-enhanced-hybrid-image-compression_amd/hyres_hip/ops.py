@@ -67,7 +67,7 @@ def zeros(shape, device) -> torch.Tensor:
 class Node:
     """NHWC activation [B,H,W,C]; ``v`` may be a channel slice of a wider buffer (pixel stride ld)."""
 
-    __slots__ = ("v", "B", "H", "W", "C", "ld", "rg", "parent", "c0", "_g", "gflag")
+    __slots__ = ("v", "B", "H", "W", "C", "ld", "rg", "parent", "c0", "_g", "gflag", "relu_out", "gmasked")
 
     def __init__(self, v: torch.Tensor, rg: bool = True, parent: "Node" = None, c0: int = 0):
         assert v.dim() == 4 and v.stride(3) == 1, "Node expects an NHWC tensor with unit channel stride"
@@ -80,6 +80,11 @@ class Node:
         self.c0 = c0
         self._g = None
         self.gflag = False
+        # ReLU-backward fusion: ``relu_out`` = v is the output of a ReLU fused into its producer;
+        # ``gmasked`` = the gradient accumulated so far already carries the ReLU mask (set by a consumer
+        # whose input-gradient epilogue applied it as the FIRST contribution; cleared by any later one).
+        self.relu_out = False
+        self.gmasked = False
 
     @staticmethod
     def new(B, H, W, C, device, rg=True) -> "Node":
@@ -122,10 +127,21 @@ class Node:
         if self._g is None:
             self._g = _empty(self.v.shape, self.v.device)
         acc = 1 if self.gflag else 0
+        if acc:
+            self.gmasked = False  # a later, unmasked contribution: the producer re-applies the mask
         self.gflag = True
         return self._g, acc
 
+    def relu_mask_epilogue(self, e: "L.Epilogue", acc: int) -> None:
+        """Let an input-gradient conv writing this node's gradient apply the ReLU mask (first writer)."""
+        if acc == 0 and self.relu_out and self.parent is None:
+            e.act = L.ACT_RELU_MASK
+            e.aux0 = self.ptr()
+            e.ld0 = self.ld
+            self.gmasked = True
+
     def _zeroed_grad(self):
+        self.gmasked = False  # the caller accumulates an unmasked contribution
         if self._g is None:
             self._g = zeros(self.v.shape, self.v.device)
             self.gflag = True
@@ -322,7 +338,9 @@ def _colsum_into(g: torch.Tensor, P: int, C: int, ld: int, dst: torch.Tensor, ac
     L.call("hyres_colsum", g.data_ptr(), P, C, ld, dst.data_ptr(), acc, ws.data_ptr(), ws.numel(), L.stream())
 
 
-def _wgrad(desc: L.WgradDesc, p_ptr: int, q_ptr: int, dst: torch.Tensor, device) -> None:
+def _wgrad(desc: L.WgradDesc, p_ptr: int, q_ptr: int, dst: torch.Tensor, device,
+           dbias: Optional[torch.Tensor] = None) -> None:
+    """Weight gradient (+ the bias gradient = column sums of P when ``dbias`` is given, conv2d only)."""
     nbytes = L.load().hyres_wgrad_workspace_bytes(ctypes.byref(desc))
     ws = _ws(nbytes, device, slot=2)
     timed = KernelTimer.enabled and KernelTimer.all_convs
@@ -330,8 +348,8 @@ def _wgrad(desc: L.WgradDesc, p_ptr: int, q_ptr: int, dst: torch.Tensor, device)
         s0 = torch.cuda.Event(enable_timing=True)
         s1 = torch.cuda.Event(enable_timing=True)
         s0.record()
-    L.call("hyres_conv_wgrad", ctypes.byref(desc), p_ptr, q_ptr, dst.data_ptr(), ws.data_ptr(), ws.numel(),
-           L.stream())
+    L.call("hyres_conv_wgrad", ctypes.byref(desc), p_ptr, q_ptr, dst.data_ptr(),
+           None if dbias is None else dbias.data_ptr(), ws.data_ptr(), ws.numel(), L.stream())
     if timed:
         s1.record()
         d = desc
@@ -346,7 +364,7 @@ def _wgrad(desc: L.WgradDesc, p_ptr: int, q_ptr: int, dst: torch.Tensor, device)
 def _act_backward(y: Node, gy: torch.Tensor, gy_ld: int, act: int, pre: Optional[torch.Tensor],
                   slope: Optional[torch.Tensor]):
     """Gradient wrt the pre-activation (contiguous [P,C] buffer or the incoming view)."""
-    if act == L.ACT_NONE:
+    if act == L.ACT_NONE or (act == L.ACT_RELU and y.gmasked):
         return gy, gy_ld
     gp = _empty((y.B, y.H, y.W, y.C), y.device)
     if act == L.ACT_RELU:
@@ -403,6 +421,7 @@ def conv2d(tape: Optional[Tape], x: Node, weight: torch.Tensor, bias: Optional[t
             e.out2 = pre.data_ptr()
             e.ldo2 = Co
     _launch_conv(g, x.ptr(), w2, ldw, y.ptr(), e)
+    y.relu_out = act == L.ACT_RELU
     if tape is None:
         return y
 
@@ -415,7 +434,7 @@ def conv2d(tape: Optional[Tape], x: Node, weight: torch.Tensor, bias: Optional[t
         if res is not None and res.rg:
             tgt, acc = res.grad_target()
             L.call("hyres_add2d", gp.data_ptr(), gpld, tgt.data_ptr(), res.grad_ld(), P, Co, acc, L.stream())
-        if wants_grad(bias):
+        if wants_grad(bias) and not wants_grad(weight):
             _colsum_into(gp, P, Co, gpld, param_grad(bias))
         if wants_grad(weight):
             d = L.WgradDesc()
@@ -423,7 +442,8 @@ def conv2d(tape: Optional[Tape], x: Node, weight: torch.Tensor, bias: Optional[t
                    pad, dil)
             d.sm = Ci_w * KH * KW
             d.accumulate = 1
-            _wgrad(d, gp.data_ptr(), x.ptr(), param_grad(weight), x.device)
+            _wgrad(d, gp.data_ptr(), x.ptr(), param_grad(weight), x.device,
+                   param_grad(bias) if wants_grad(bias) else None)
         if x.rg:
             tgt, acc = x.grad_target()
             gd = _filter_taps(_geom("hyres_geom_conv2d_dgrad", B, H, W, Ci, x.grad_ld(), Co, gpld, KH, KW, stride,
@@ -432,6 +452,7 @@ def conv2d(tape: Optional[Tape], x: Node, weight: torch.Tensor, bias: Optional[t
             ed = L.Epilogue()
             ed.kind = L.EPI_BIAS
             ed.accumulate = acc
+            x.relu_mask_epilogue(ed, acc)
             _launch_conv(gd, gp.data_ptr(), w2d, gd.ntaps * Co, tgt.data_ptr(), ed)
 
     tape.push(bwd)
@@ -455,6 +476,7 @@ def deconv2d(tape: Optional[Tape], x: Node, weight: torch.Tensor, bias: Optional
     e.act = act
     e.bias = L.ptr(bias)
     _launch_conv(g, x.ptr(), w2, g.ntaps * Ci, y.ptr(), e)
+    y.relu_out = act == L.ACT_RELU
     if tape is None:
         return y
 
@@ -477,6 +499,7 @@ def deconv2d(tape: Optional[Tape], x: Node, weight: torch.Tensor, bias: Optional
             ed = L.Epilogue()
             ed.kind = L.EPI_BIAS
             ed.accumulate = acc
+            x.relu_mask_epilogue(ed, acc)
             _launch_conv(gd, gp.data_ptr(), w2d, gd.ntaps * Co, tgt.data_ptr(), ed)
 
     tape.push(bwd)

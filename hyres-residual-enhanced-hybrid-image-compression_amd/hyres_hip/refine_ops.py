@@ -78,10 +78,11 @@ def spatial_attention_mul(tape: Optional[Tape], x: Node, w: torch.Tensor) -> Nod
     B, H, W, C = x.B, x.H, x.W, x.C
     dev = x.device
     pooled2 = _empty((B, H, W, 2), dev)
+    argmax = torch.empty((B, H, W), dtype=torch.int32, device=dev)
     attn = _empty((B, H, W), dev)
     y = Node.new(B, H, W, C, dev)
-    L.call("hyres_spatial_attn_fwd", x.ptr(), w.data_ptr(), pooled2.data_ptr(), attn.data_ptr(), y.ptr(), B, H, W, C,
-           L.stream())
+    L.call("hyres_spatial_attn_fwd", x.ptr(), w.data_ptr(), pooled2.data_ptr(), argmax.data_ptr(), attn.data_ptr(),
+           y.ptr(), B, H, W, C, L.stream())
     if tape is None:
         return y
 
@@ -95,8 +96,9 @@ def spatial_attention_mul(tape: Optional[Tape], x: Node, w: torch.Tensor) -> Nod
         gw = param_grad(w) if w.requires_grad else _empty(w.shape, dev)
         wsb = L.load().hyres_spatial_attn_workspace_bytes(B, H, W)
         ws = _ws(wsb, dev, slot=1)
-        L.call("hyres_spatial_attn_bwd", x.ptr(), w.data_ptr(), pooled2.data_ptr(), attn.data_ptr(), g.data_ptr(),
-               gx.data_ptr(), gw.data_ptr(), B, H, W, C, ws.data_ptr(), ws.numel(), L.stream())
+        L.call("hyres_spatial_attn_bwd", x.ptr(), w.data_ptr(), pooled2.data_ptr(), argmax.data_ptr(),
+               attn.data_ptr(), g.data_ptr(), gx.data_ptr(), gw.data_ptr(), B, H, W, C, ws.data_ptr(), ws.numel(),
+               L.stream())
         if acc:
             L.call("hyres_accumulate", gx.data_ptr(), tgt.data_ptr(), gx.numel(), L.stream())
 

@@ -41,10 +41,11 @@ class SpatialAttention(HipModule):
         import hyres_hip.ops as O
         B, H, W, C = x.B, x.H, x.W, x.C
         pooled2 = O._empty((B, H, W, 2), x.device)
+        argmax = torch.empty((B, H, W), dtype=torch.int32, device=x.device)
         attn = Node.new(B, H, W, 1, x.device)
         y = O._empty((B, H, W, C), x.device)
-        L.call("hyres_spatial_attn_fwd", x.ptr(), self.conv.weight.data_ptr(), pooled2.data_ptr(), attn.ptr(),
-               y.data_ptr(), B, H, W, C, L.stream())
+        L.call("hyres_spatial_attn_fwd", x.ptr(), self.conv.weight.data_ptr(), pooled2.data_ptr(), argmax.data_ptr(),
+               attn.ptr(), y.data_ptr(), B, H, W, C, L.stream())
         return attn
 
 

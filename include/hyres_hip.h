@@ -91,6 +91,8 @@ int hyres_conv_weight_prep(const hyres_conv_geom* g, const float* w, float* w2, 
 #define HYRES_ACT_NONE 0
 #define HYRES_ACT_RELU 1
 #define HYRES_ACT_PRELU 2     /* single shared slope (nn.PReLU()), read from device pointer */
+#define HYRES_ACT_RELU_MASK 3 /* ReLU backward fused into an input-gradient: y = (aux0 > 0) ? y : 0,
+                                 aux0 = the ReLU output of the layer whose gradient is produced */
 
 typedef struct hyres_epilogue {
     int kind, act, accumulate;    /* accumulate: y += result (gradient accumulation) */
@@ -133,8 +135,10 @@ int hyres_wgrad_desc_conv2d(hyres_wgrad_desc* d, int B, int H, int W, int Ci, in
 int hyres_wgrad_desc_deconv2d(hyres_wgrad_desc* d, int B, int H, int W, int Ci, int ldx, int Co,
                               int ldy, int K, int pad);
 long long hyres_wgrad_workspace_bytes(const hyres_wgrad_desc* d);
+/* dbias (optional, may be NULL): dbias[m] (+)= sum_q P[q][m] — the Conv2d bias gradient when P = dY
+ * (replaces the separate colsum for conv layers; fused into the weight-gradient kernel). */
 int hyres_conv_wgrad(const hyres_wgrad_desc* d, const float* p, const float* q, float* dst,
-                     void* workspace, long long ws_bytes, hyres_stream_t s);
+                     float* dbias, void* workspace, long long ws_bytes, hyres_stream_t s);
 
 /* column sums over pixels: dst[c] (+)= sum_p x[p*ld + c]  (bias gradients) */
 int hyres_colsum(const float* x, int P, int C, int ld, float* dst, int accumulate, void* workspace,
@@ -260,12 +264,14 @@ int hyres_se_bwd(const float* x, const float* gy, const float* w1, const float* 
                  const float* pooled, const float* hidden, const float* sgate, float* gx, float* gw1,
                  float* gw2, int B, int HW, int C, int Cr, void* ws, long long ws_bytes, hyres_stream_t s);
 long long hyres_se_workspace_bytes(int B, int HW, int C);
-/* SpatialAttention (enhancement.py:7-21) fused: a = sigmoid(conv7x7([mean_c, max_c])); y = x * a */
-int hyres_spatial_attn_fwd(const float* x, const float* w, float* pooled2, float* attn, float* y,
-                           int B, int H, int W, int C, hyres_stream_t s);
-int hyres_spatial_attn_bwd(const float* x, const float* w, const float* pooled2, const float* attn,
-                           const float* gy, float* gx, float* gw, int B, int H, int W, int C, void* ws,
-                           long long ws_bytes, hyres_stream_t s);
+/* SpatialAttention (enhancement.py:7-21) fused: a = sigmoid(conv7x7([mean_c, max_c])); y = x * a.
+ * pooled2 [P][2] and argmax [P] (first maximal channel, torch.max semantics) are saved for backward.
+ * C % 4 == 0, 16B-aligned x/y/gy/gx. */
+int hyres_spatial_attn_fwd(const float* x, const float* w, float* pooled2, int* argmax, float* attn,
+                           float* y, int B, int H, int W, int C, hyres_stream_t s);
+int hyres_spatial_attn_bwd(const float* x, const float* w, const float* pooled2, const int* argmax,
+                           const float* attn, const float* gy, float* gx, float* gw, int B, int H, int W,
+                           int C, void* ws, long long ws_bytes, hyres_stream_t s);
 long long hyres_spatial_attn_workspace_bytes(int B, int H, int W);
 
 /* ------------------------------------------------------------------------------------------ */

@@ -1,0 +1,52 @@
+"""Microbenchmark one conv geometry (forward, fused epilogue) with HIP events; for PMC passes.
+
+    python scripts/conv_micro.py [--B 16 --H 128 --Ci 64 --Co 64 --K 3 --stride 1 --iters 50]
+"""
+import argparse
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "hyres-residual-enhanced-hybrid-image-compression_amd"))
+
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--B", type=int, default=16)
+    ap.add_argument("--H", type=int, default=128)
+    ap.add_argument("--Ci", type=int, default=64)
+    ap.add_argument("--Co", type=int, default=64)
+    ap.add_argument("--K", type=int, default=3)
+    ap.add_argument("--stride", type=int, default=1)
+    ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--relu", action="store_true")
+    a = ap.parse_args()
+    from hyres_hip import _lib as L
+    from hyres_hip import ops as O
+    dev = torch.device("cuda:0")
+    x = O.Node(torch.randn(a.B, a.H, a.H, a.Ci, device=dev), rg=False)
+    w = torch.randn(a.Co, a.Ci, a.K, a.K, device=dev) / (a.Ci * a.K * a.K) ** 0.5
+    b = torch.randn(a.Co, device=dev)
+    act = L.ACT_RELU if a.relu else L.ACT_NONE
+    for _ in range(3):
+        y = O.conv2d(None, x, w, b, stride=a.stride, pad=a.K // 2, act=act)
+    torch.cuda.synchronize()
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(a.iters):
+        y = O.conv2d(None, x, w, b, stride=a.stride, pad=a.K // 2, act=act, out=y)
+    e1.record()
+    torch.cuda.synchronize()
+    us = 1000 * e0.elapsed_time(e1) / a.iters
+    Ho = y.H
+    flops = 2.0 * a.B * Ho * Ho * a.K * a.K * a.Ci * a.Co
+    byts = 4.0 * (a.B * a.H * a.H * a.Ci + a.B * Ho * Ho * a.Co + a.K * a.K * a.Ci * a.Co)
+    print(f"conv B{a.B} {a.H}x{a.H}x{a.Ci} -> {Ho}x{Ho}x{a.Co} K{a.K} s{a.stride}: {us:.1f} us, "
+          f"{flops / us / 1e6:.1f} TFLOP/s, {byts / us / 1e3:.0f} GB/s")
+
+
+if __name__ == "__main__":
+    main()
