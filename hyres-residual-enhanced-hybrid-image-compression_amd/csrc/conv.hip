@@ -33,6 +33,7 @@ struct ConvArgs {
     int cps;     // K chunks per split
     float* slab; // [nsplit][nphase][M][Co] partials when nsplit > 1
     int vec4;    // every epilogue operand 16B aligned with ld % 4 == 0 and Co % 4 == 0
+    int w_bytes; // bytes of W2 (buffer-resource range)
 };
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
@@ -197,29 +198,52 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const ConvArgs a) {
     float4 ra[MODE == 2 ? 1 : A_V], rb[MODE == 2 ? 1 : B_V];
     float sa[MODE == 2 ? A_V : 1], sb[MODE == 2 ? B_V : 1];
 
+    // vector path: raw buffer loads (out-of-range offset -> 0, no branches). The X resource starts at
+    // the block's first image so 32-bit byte offsets suffice (host checks 3 images < 2 GB).
+    const int b0 = m0 / HqWq;
+    const long long img = (long long)g.Hi * g.Wi * g.ldx;
+    const long long xrem = ((long long)g.B - b0) * img * 4;
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(a.x + (long long)b0 * img), (short)0, (int)(xrem < 0x7FFFFFF0LL ? xrem : 0x7FFFFFF0LL), 0x00020000);
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)a.w2, (short)0, a.w_bytes, 0x00020000);
+    int a_base[MODE == 2 ? 1 : A_V];  // element offset of image row 0 of this row's image, rel. to b0
+    if constexpr (MODE != 2) {
+#pragma unroll
+        for (int q = 0; q < A_V; ++q) {
+            a_base[q] = (int)((a_b[q] - b0) * img);
+            a_i[q] *= g.ish;
+            a_j[q] *= g.isw;
+        }
+    }
+    // tap offsets of this phase in LDS (uniform broadcast reads instead of indexed kernarg loads)
+    __shared__ int2 tapoff[HYRES_MAX_TAPS];
+    for (int i = tid; i < ntap; i += 256) tapoff[i] = make_int2(g.dh[tap0 + i], g.dw[tap0 + i]);
+    __syncthreads();
+    // (tap, channel) of the next chunk to load, advanced incrementally (no division per chunk)
+    int ld_t = 0, ld_c = 0;
+
     auto load_chunk = [&](int kc) {
         if constexpr (MODE != 2) {
-            const int cpt = Ci / KT;
-            const int t = kc / cpt;
-            const int c0 = (kc - t * cpt) * KT + 4 * c4;
-            const int gt = tap0 + t;
-            const int dh = g.dh[gt], dw = g.dw[gt];
+            const int2 o = tapoff[ld_t];
+            const int c0 = ld_c + 4 * c4;
+            const int gt = tap0 + ld_t;
 #pragma unroll
             for (int q = 0; q < A_V; ++q) {
-                int ih = a_i[q] * g.ish + dh, iw = a_j[q] * g.isw + dw;
-                bool ok = a_ok[q] && ih >= 0 && ih < g.Hi && iw >= 0 && iw < g.Wi;
-                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (ok) v = ld4(a.x + ((long long)(a_b[q] * g.Hi + ih) * g.Wi + iw) * g.ldx + c0);
+                const int ih = a_i[q] + o.x, iw = a_j[q] + o.y;
+                const bool ok = a_ok[q] && (unsigned)ih < (unsigned)g.Hi && (unsigned)iw < (unsigned)g.Wi;
+                const int off = ok ? (a_base[q] + (ih * g.Wi + iw) * g.ldx + c0) * 4 : (int)0x80000000;
+                float4 v = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
                 if constexpr (MODE == 1) { v.x *= v.x; v.y *= v.y; v.z *= v.z; v.w *= v.w; }
                 ra[q] = v;
             }
 #pragma unroll
             for (int q = 0; q < B_V; ++q) {
-                int co = n0 + tid / 8 + 32 * q;
-                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (co < g.Co) v = ld4(a.w2 + (long long)co * a.ldw + (long long)gt * Ci + c0);
-                rb[q] = v;
+                const int co = n0 + tid / 8 + 32 * q;
+                const int off = co < g.Co ? (co * a.ldw + gt * Ci + c0) * 4 : (int)0x80000000;
+                rb[q] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(wr, off, 0, 0));
             }
+            ld_c += KT;
+            if (ld_c == Ci) { ld_c = 0; ++ld_t; }
         } else {
             const int K = ntap * Ci;
 #pragma unroll
@@ -284,6 +308,11 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const ConvArgs a) {
 
     const int kbeg = SPLITK ? min(nk, split * a.cps) : 0;
     const int kend = SPLITK ? min(nk, kbeg + a.cps) : nk;
+    if constexpr (MODE != 2) {
+        const int cpt = Ci / KT;
+        ld_t = kbeg / cpt;
+        ld_c = (kbeg - ld_t * cpt) * KT;
+    }
     if (kbeg < kend) load_chunk(kbeg);
     for (int kc = kbeg; kc < kend; ++kc) {
         __syncthreads();
@@ -1013,6 +1042,13 @@ int hyres_conv_forward(const hyres_conv_geom* g, const float* x, const float* w2
         a.cps = plan.cps;
         a.slab = (float*)ws;
         if (!aligned16(ws)) a.vec4 = 0;
+    }
+    {
+        const long long wb = (long long)g->Co * ldw * 4;
+        const long long img_bytes = (long long)g->Hi * g->Wi * g->ldx * 4;
+        HY_REQUIRE(wb < 0x7FFFFFF0LL && 3 * img_bytes < 0x7FFFFFF0LL && (long long)g->Ho * g->Wo * g->ldy < 0x7FFFFFFFLL,
+                   HYRES_E_SHAPE, "conv: per-image tensor too large for 32-bit offsets");
+        a.w_bytes = (int)wb;
     }
     int mode;
     if (g->Ci % KT == 0) {
