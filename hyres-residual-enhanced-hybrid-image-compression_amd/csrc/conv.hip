@@ -501,6 +501,8 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgradArgs a) {
         }
     }
     int q_b[Q_V], q_i[Q_V], q_j[Q_V];
+    // pixel decode of each thread's Q rows: divisions once (first chunk of the split), then stepped by KT
+    // pixels per chunk in raster order (q_b = -1 past the end)
     auto decode_rows = [&](int kc) {
 #pragma unroll
         for (int i = 0; i < Q_V; ++i) {
@@ -513,6 +515,16 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgradArgs a) {
             } else {
                 q_b[i] = -1; q_i[i] = 0; q_j[i] = 0;
             }
+        }
+    };
+    auto step_rows = [&]() {
+#pragma unroll
+        for (int i = 0; i < Q_V; ++i) {
+            if (q_b[i] < 0) continue;
+            int j = q_j[i] + KT, ii = q_i[i], b = q_b[i];
+            while (j >= d.Wq) { j -= d.Wq; ++ii; }
+            while (ii >= d.Hq) { ii -= d.Hq; ++b; }
+            q_j[i] = j; q_i[i] = ii; q_b[i] = b < d.B ? b : -1;
         }
     };
     auto load_p = [&](int kc) {
@@ -631,7 +643,7 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgradArgs a) {
             if (j + 1 < NT) {
                 load_q(t0 + j + 1);
             } else if (kc + 1 < kc_end) {
-                decode_rows(kc + 1);
+                step_rows();
                 load_p(kc + 1);
                 load_q(t0);
             }
