@@ -362,6 +362,69 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const ConvArgs a) {
             for (int r = 0; r < 16; ++r)
                 Cs[(wm * TM * 32 + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh) * CP + wn * 32 + lr] = acc[tm][tn][r];
         __syncthreads();
+        if constexpr (!split_k) {
+            // fast path (BIAS epilogue, float4 operands): the residual / old-y / ReLU-mask loads of U
+            // iterations are issued before any of them is consumed, so U loads per thread are in flight
+            if (a.vec4 && a.e.kind == HYRES_EPI_BIAS) {
+                constexpr int ITER = BM * (CW / 4) / 256;
+                constexpr int U = ITER >= 4 ? 4 : ITER;
+                static_assert(ITER % U == 0, "epilogue tiling");
+                const hyres_epilogue& e = a.e;
+                for (int it0 = 0; it0 < ITER; it0 += U) {
+                    float4 v[U], rs[U], yo[U], mk[U], bs[U];
+                    long long px[U];
+                    int nn[U];
+                    bool ok[U];
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const int idx = tid + 256 * (it0 + u);
+                        const int row = idx / (CW / 4);
+                        const int col = 4 * (idx - row * (CW / 4));
+                        const int m = m0 + row;
+                        const int n = n0 + (col >> 5) * TN * 32 + tn * 32 + (col & 31);
+                        ok[u] = m < a.M && n < g.Co;
+                        nn[u] = n;
+                        v[u] = *reinterpret_cast<const float4*>(&Cs[row * CP + col]);
+                        long long pix = m;
+                        if (!linear) {
+                            const int b = m / HqWq;
+                            const int rr = m - b * HqWq;
+                            const int i = rr / g.Wq;
+                            const int j = rr - i * g.Wq;
+                            pix = (long long)(b * g.Ho + i * g.osh + oph) * g.Wo + j * g.osw + opw;
+                        }
+                        px[u] = pix;
+                        const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+                        bs[u] = (ok[u] && e.bias) ? ld4(e.bias + n) : z4;
+                        rs[u] = (ok[u] && e.res) ? ld4(e.res + pix * e.ldres + n) : z4;
+                        yo[u] = (ok[u] && e.accumulate) ? ld4(a.y + pix * g.ldy + n) : z4;
+                        mk[u] = (ok[u] && e.act == HYRES_ACT_RELU_MASK) ? ld4(e.aux0 + pix * e.ld0 + n) : z4;
+                    }
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        if (!ok[u]) continue;
+                        float o[4] = {v[u].x + bs[u].x + rs[u].x, v[u].y + bs[u].y + rs[u].y,
+                                      v[u].z + bs[u].z + rs[u].z, v[u].w + bs[u].w + rs[u].w};
+                        if (e.out2) st4(e.out2 + px[u] * e.ldo2 + nn[u], make_float4(o[0], o[1], o[2], o[3]));
+                        if (e.act == HYRES_ACT_RELU) {
+#pragma unroll
+                            for (int c = 0; c < 4; ++c) o[c] = fmaxf(o[c], 0.f);
+                        } else if (e.act == HYRES_ACT_PRELU) {
+#pragma unroll
+                            for (int c = 0; c < 4; ++c) o[c] = o[c] >= 0.f ? o[c] : slope * o[c];
+                        } else if (e.act == HYRES_ACT_RELU_MASK) {
+                            o[0] = mk[u].x > 0.f ? o[0] : 0.f;
+                            o[1] = mk[u].y > 0.f ? o[1] : 0.f;
+                            o[2] = mk[u].z > 0.f ? o[2] : 0.f;
+                            o[3] = mk[u].w > 0.f ? o[3] : 0.f;
+                        }
+                        st4(a.y + px[u] * g.ldy + nn[u],
+                            make_float4(o[0] + yo[u].x, o[1] + yo[u].y, o[2] + yo[u].z, o[3] + yo[u].w));
+                    }
+                }
+                continue;
+            }
+        }
         for (int idx = tid; idx < BM * (CW / 4); idx += 256) {
             const int row = idx / (CW / 4);
             const int col = 4 * (idx - row * (CW / 4));
