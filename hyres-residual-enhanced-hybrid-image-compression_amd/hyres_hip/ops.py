@@ -171,6 +171,7 @@ class Tape:
         for fn in reversed(self.ops):
             fn()
         self.ops.clear()
+        SideStream.join()  # side-stream weight gradients complete before anyone reads .grad
 
 
 class Trace:
@@ -338,11 +339,56 @@ def _colsum_into(g: torch.Tensor, P: int, C: int, ld: int, dst: torch.Tensor, ac
     L.call("hyres_colsum", g.data_ptr(), P, C, ld, dst.data_ptr(), acc, ws.data_ptr(), ws.numel(), L.stream())
 
 
+class SideStream:
+    """Weight gradients are independent of the input-gradient chain: conv/deconv wgrads run on a side
+    HIP stream (forked from the main stream at the point their operands are ready, joined at the end of
+    the tape backward), filling CUs the latency-bound dgrad chain and small-grid layers leave idle.
+    Operand tensors are ``record_stream``-ed so the caching allocator does not recycle them early;
+    the side stream owns workspace slot 2."""
+
+    enabled = True
+    _streams = {}
+    used = False
+
+    @classmethod
+    def get(cls, device: torch.device) -> torch.cuda.Stream:
+        st = cls._streams.get(device.index)
+        if st is None:
+            st = torch.cuda.Stream(device=device)
+            cls._streams[device.index] = st
+        return st
+
+    @classmethod
+    def join(cls) -> None:
+        """Make the current stream wait for all side-stream work (end of backward)."""
+        if not cls.used:
+            return
+        for idx, st in cls._streams.items():
+            torch.cuda.current_stream(torch.device("cuda", idx)).wait_stream(st)
+        cls.used = False
+
+
 def _wgrad(desc: L.WgradDesc, p_ptr: int, q_ptr: int, dst: torch.Tensor, device,
-           dbias: Optional[torch.Tensor] = None) -> None:
-    """Weight gradient (+ the bias gradient = column sums of P when ``dbias`` is given, conv2d only)."""
+           dbias: Optional[torch.Tensor] = None, keep=(), side: bool = False) -> None:
+    """Weight gradient (+ the bias gradient = column sums of P when ``dbias`` is given, conv2d only).
+    ``side``: run on the side stream (``keep`` = tensors whose memory the kernels read)."""
+    side = side and SideStream.enabled and device.type == "cuda"
+    if side:
+        main = torch.cuda.current_stream(device)
+        st = SideStream.get(device)
+        st.wait_stream(main)
+        for t in tuple(keep) + (dst,) + ((dbias,) if dbias is not None else ()):
+            t.record_stream(st)
+        SideStream.used = True
+        with torch.cuda.stream(st):
+            _wgrad_launch(desc, p_ptr, q_ptr, dst, device, dbias, slot=2)
+    else:
+        _wgrad_launch(desc, p_ptr, q_ptr, dst, device, dbias, slot=7)
+
+
+def _wgrad_launch(desc, p_ptr, q_ptr, dst, device, dbias, slot):
     nbytes = L.load().hyres_wgrad_workspace_bytes(ctypes.byref(desc))
-    ws = _ws(nbytes, device, slot=2)
+    ws = _ws(nbytes, device, slot=slot)
     timed = KernelTimer.enabled and KernelTimer.all_convs
     if timed:
         s0 = torch.cuda.Event(enable_timing=True)
@@ -443,7 +489,7 @@ def conv2d(tape: Optional[Tape], x: Node, weight: torch.Tensor, bias: Optional[t
             d.sm = Ci_w * KH * KW
             d.accumulate = 1
             _wgrad(d, gp.data_ptr(), x.ptr(), param_grad(weight), x.device,
-                   param_grad(bias) if wants_grad(bias) else None)
+                   param_grad(bias) if wants_grad(bias) else None, keep=(gp, x.v), side=True)
         if x.rg:
             tgt, acc = x.grad_target()
             gd = _filter_taps(_geom("hyres_geom_conv2d_dgrad", B, H, W, Ci, x.grad_ld(), Co, gpld, KH, KW, stride,
@@ -491,7 +537,7 @@ def deconv2d(tape: Optional[Tape], x: Node, weight: torch.Tensor, bias: Optional
             d = L.WgradDesc()
             L.call("hyres_wgrad_desc_deconv2d", ctypes.byref(d), B, H, W, Ci, x.ld, Co, gpld, K, pad)
             d.accumulate = 1
-            _wgrad(d, x.ptr(), gp.data_ptr(), param_grad(weight), x.device)
+            _wgrad(d, x.ptr(), gp.data_ptr(), param_grad(weight), x.device, keep=(gp, x.v), side=True)
         if x.rg:
             tgt, acc = x.grad_target()
             gd = _geom("hyres_geom_deconv2d_dgrad", B, H, W, Ci, x.grad_ld(), Co, gpld, K, pad)

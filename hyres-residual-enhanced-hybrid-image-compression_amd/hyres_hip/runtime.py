@@ -55,7 +55,7 @@ class TapeFunction(torch.autograd.Function):
             if node is None or g is None:
                 continue
             node.set_grad(O.nchw_grad_to_nhwc(g))
-        tape.backward()
+        tape.backward()  # joins the side stream (weight gradients) at its end
         in_grads = []
         for node in ctx.in_nodes:
             if node is None or not node.rg or node.grad() is None:
