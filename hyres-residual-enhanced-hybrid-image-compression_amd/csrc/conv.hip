@@ -486,6 +486,36 @@ __global__ void conv_splitk_reduce_kernel(const ConvArgs a) {
     }
 }
 
+// float4 variant (vec4 launches): 4 channels per thread, split loads unrolled, float4 epilogue
+__global__ __launch_bounds__(256) void conv_splitk_reduce4_kernel(const ConvArgs a) {
+    const hyres_conv_geom& g = a.g;
+    const int C4 = g.Co >> 2;
+    const long long per_phase = (long long)a.M * C4;
+    const long long total = per_phase * g.nphase;
+    const long long sstride = (long long)g.nphase * a.M * g.Co;
+    const int HqWq = g.Hq * g.Wq;
+    const float slope = (a.e.act == HYRES_ACT_PRELU) ? a.e.slope[0] : 0.f;
+    for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
+         idx += (long long)gridDim.x * blockDim.x) {
+        const int phase = (int)(idx / per_phase);
+        const long long r = idx - phase * per_phase;
+        const int m = (int)(r / C4);
+        const int n = 4 * (int)(r - (long long)m * C4);
+        const float* sp = a.slab + ((long long)phase * a.M + m) * g.Co + n;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 4
+        for (int s = 0; s < a.nsplit; ++s) {
+            const float4 u = ld4(sp + s * sstride);
+            v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
+        }
+        const int b = m / HqWq;
+        const int rr = m - b * HqWq;
+        const int i = rr / g.Wq, j = rr - (rr / g.Wq) * g.Wq;
+        const long long pix = (long long)(b * g.Ho + i * g.osh + g.oph[phase]) * g.Wo + j * g.osw + g.opw[phase];
+        epi_store4(a.e, a.y, g.ldy, pix, n, v, slope);
+    }
+}
+
 // ------------------------------------------------------------------------------------------------
 // weight gradient:  out[t][m][n] = sum_q P[q][m] * Q[shift_t(q)][n]      (K = pixels q)
 //   * a block owns one (m-tile, n-tile, group of NT taps, pixel split); the P chunk is staged once
@@ -1149,6 +1179,11 @@ int hyres_conv_forward(const hyres_conv_geom* g, const float* x, const float* w2
     else rc = launch_fwd<1, 1, 4, 1>(a, mode, st);
     if (rc || a.nsplit == 1) return rc;
     long long total = (long long)a.M * g->Co * g->nphase;
+    if (a.vec4) {
+        int blocks = (int)std::min<long long>((total / 4 + 255) / 256, 8192);
+        hipLaunchKernelGGL(conv_splitk_reduce4_kernel, dim3(blocks), dim3(256), 0, st, a);
+        return HY_LAUNCH_CHECK("conv_splitk_reduce4_kernel");
+    }
     int blocks = (int)std::min<long long>((total + 255) / 256, 8192);
     hipLaunchKernelGGL(conv_splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, a);
     return HY_LAUNCH_CHECK("conv_splitk_reduce_kernel");

@@ -177,6 +177,37 @@ __global__ void se_scale_kernel(const float* x, const float* sgate, float* y, in
         y[i] = x[i] * sgate[b * C + c];
     }
 }
+// float4 variants (C % 4 == 0, 256 % (C/4) == 0): 256 threads = (C/4 channel groups) x (pixel lanes),
+// every thread busy, deterministic LDS fold over the pixel lanes. SQ: sum of gy*x (backward) instead of x.
+template <bool PROD>
+__global__ __launch_bounds__(256) void se_pool4_kernel(const float* x, const float* gy, int HW, int C, int per,
+                                                       float* part) {
+    __shared__ float4 red[256];
+    const int b = blockIdx.x, ch = blockIdx.y;
+    const int G = C >> 2, PL = 256 / G;
+    const int g = threadIdx.x % G, lane = threadIdx.x / G;
+    const int p0 = ch * per, p1 = min(HW, p0 + per);
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int p = p0 + lane; p < p1; p += PL) {
+        const long long i = ((long long)b * HW + p) * C + 4 * g;
+        float4 v = *reinterpret_cast<const float4*>(x + i);
+        if constexpr (PROD) {
+            const float4 q = *reinterpret_cast<const float4*>(gy + i);
+            v.x *= q.x; v.y *= q.y; v.z *= q.z; v.w *= q.w;
+        }
+        s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    red[threadIdx.x] = s;
+    __syncthreads();
+    if (threadIdx.x < G) {
+        float4 t = red[threadIdx.x];
+        for (int l = 1; l < PL; ++l) {
+            const float4 u = red[l * G + threadIdx.x];
+            t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+        }
+        *reinterpret_cast<float4*>(part + ((long long)b * gridDim.y + ch) * C + 4 * threadIdx.x) = t;
+    }
+}
 // backward: partial sums of gy*x per (b,c)
 __global__ void se_bwd_pool_kernel(const float* x, const float* gy, int HW, int C, int per, float* part) {
     const int b = blockIdx.x, ch = blockIdx.y;
@@ -456,7 +487,11 @@ int hyres_se_fwd(const float* x, const float* w1, const float* w2, float* y, flo
     HY_REQUIRE(ws && ws_bytes >= (long long)B * nch * C * 4, HYRES_E_WORKSPACE, "se_fwd: workspace");
     const int per = (HW + nch - 1) / nch;
     hipStream_t st = as_stream(s);
-    hipLaunchKernelGGL(se_pool_kernel, dim3(B, nch), dim3(256), 0, st, x, HW, C, per, (float*)ws);
+    if (C % 4 == 0 && C <= 1024 && 256 % (C / 4) == 0 && aligned16(x))
+        hipLaunchKernelGGL(se_pool4_kernel<false>, dim3(B, nch), dim3(256), 0, st, x, (const float*)nullptr, HW, C,
+                           per, (float*)ws);
+    else
+        hipLaunchKernelGGL(se_pool_kernel, dim3(B, nch), dim3(256), 0, st, x, HW, C, per, (float*)ws);
     int rc = HY_LAUNCH_CHECK("se_pool");
     if (rc) return rc;
     hipLaunchKernelGGL(se_fc_kernel, dim3(B), dim3(256), (C + Cr) * 4, st, (const float*)ws, nch, w1, w2, pooled,
@@ -480,7 +515,10 @@ int hyres_se_bwd(const float* x, const float* gy, const float* w1, const float* 
     float* part = (float*)ws;
     float* gpool = part + (long long)B * nch * C;
     hipStream_t st = as_stream(s);
-    hipLaunchKernelGGL(se_bwd_pool_kernel, dim3(B, nch), dim3(256), 0, st, x, gy, HW, C, per, part);
+    if (C % 4 == 0 && C <= 1024 && 256 % (C / 4) == 0 && aligned16(x) && aligned16(gy))
+        hipLaunchKernelGGL(se_pool4_kernel<true>, dim3(B, nch), dim3(256), 0, st, x, gy, HW, C, per, part);
+    else
+        hipLaunchKernelGGL(se_bwd_pool_kernel, dim3(B, nch), dim3(256), 0, st, x, gy, HW, C, per, part);
     int rc = HY_LAUNCH_CHECK("se_bwd_pool");
     if (rc) return rc;
     hipLaunchKernelGGL(se_fc_bwd_kernel, dim3(1), dim3(256), (size_t)B * (C + Cr) * 4, st, (const float*)part, nch, B,
