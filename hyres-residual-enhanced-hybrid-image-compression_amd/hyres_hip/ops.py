@@ -40,7 +40,8 @@ class Workspace:
 
     @classmethod
     def get(cls, nbytes: int, device: torch.device, slot: int = 0) -> torch.Tensor:
-        key = (device.index, slot)
+        # per (device, slot, stream): concurrent branches / the side stream never share scratch
+        key = (device.index, slot, torch.cuda.current_stream(device).cuda_stream if device.type == "cuda" else 0)
         buf = cls._bufs.get(key)
         if buf is None or buf.numel() < nbytes:
             n = max(int(nbytes), 1 << 20)
@@ -643,6 +644,82 @@ def attn_gate(tape: Optional[Tape], a: Node, b: Node, x: Node) -> Node:
 
     tape.push(bwd)
     return out
+
+
+# --------------------------------------------------------------------------------------------------
+# concurrent branches
+# --------------------------------------------------------------------------------------------------
+class BranchStreams:
+    """HIP streams for independent sub-graphs (AttentionBlock's two branches, MultiScaleRefine's three
+    scales): a branch's kernels run concurrently with the other branches' in forward and backward."""
+
+    enabled = True
+    _streams = {}
+
+    @classmethod
+    def get(cls, device: torch.device, k: int) -> torch.cuda.Stream:
+        key = (device.index, k)
+        st = cls._streams.get(key)
+        if st is None:
+            st = torch.cuda.Stream(device=device)
+            cls._streams[key] = st
+        return st
+
+
+def run_branches(tape: Optional[Tape], x: Node, fns) -> list:
+    """``[fn(tape, x_k) for fn in fns]`` with branch k > 0 on its own stream.
+
+    Branch k > 0 reads x through a proxy node with a private gradient buffer; in backward the branches'
+    closures are enqueued on their streams (so their kernels overlap), and a join closure (pushed first,
+    so it runs last) makes the current stream wait for them and adds the proxies' gradients into x's.
+    Forward ends with the current stream waiting for every branch."""
+    if not BranchStreams.enabled or x.device.type != "cuda" or len(fns) < 2:
+        return [fn(tape, x) for fn in fns]
+    dev = x.device
+    main = torch.cuda.current_stream(dev)
+    n = len(fns)
+    proxies = [x] + [Node(x.v, rg=x.rg) for _ in range(n - 1)]
+    streams = [main] + [BranchStreams.get(dev, k) for k in range(1, n)]
+    if tape is not None:
+        def join_bwd():
+            cur = torch.cuda.current_stream(dev)
+            for k in range(1, n):
+                cur.wait_stream(streams[k])
+                g = proxies[k].grad()
+                if g is not None and x.rg:
+                    g.record_stream(cur)
+                    x.set_grad(g)
+        tape.push(join_bwd)
+    fork = torch.cuda.Event()
+    fork.record(main)  # x is ready here; branch 0 is enqueued on main after this point
+    outs = [fns[0](tape, proxies[0])]
+    for k in range(1, n):
+        st = streams[k]
+        st.wait_event(fork)
+        x.v.record_stream(st)
+        cell = {}
+        if tape is not None:
+            def leave(cell=cell):
+                torch.cuda.set_stream(cell["prev"])
+            tape.push(leave)
+        torch.cuda.set_stream(st)
+        try:
+            outs.append(fns[k](tape, proxies[k]))
+        finally:
+            torch.cuda.set_stream(main)
+        if tape is not None:
+            def enter(st=st, cell=cell):
+                cur = torch.cuda.current_stream(dev)
+                cell["prev"] = cur
+                st.wait_stream(cur)
+                torch.cuda.set_stream(st)
+            tape.push(enter)
+        o = outs[-1]
+        if isinstance(o, Node):
+            o.v.record_stream(main)
+    for k in range(1, n):
+        main.wait_stream(streams[k])
+    return outs
 
 
 # --------------------------------------------------------------------------------------------------

@@ -41,11 +41,16 @@ class AttentionBlock(HipModule):
         self.conv_b = nn.Sequential(ResidualUnit(N), ResidualUnit(N), ResidualUnit(N), conv1x1(N, N))
 
     def hip(self, tape, x):
-        a = x
-        for ru in self.conv_a:
-            a = ru.hip(tape, a)
-        b = x
-        for ru in list(self.conv_b)[:3]:
-            b = ru.hip(tape, b)
-        b = self.conv_b[3].hip(tape, b)
+        def branch_a(tape, a):
+            for ru in self.conv_a:
+                a = ru.hip(tape, a)
+            return a
+
+        def branch_b(tape, b):
+            for ru in list(self.conv_b)[:3]:
+                b = ru.hip(tape, b)
+            return self.conv_b[3].hip(tape, b)
+
+        # the two branches are independent: run them on two HIP streams (forward and backward)
+        a, b = O.run_branches(tape, x, [branch_a, branch_b])
         return O.attn_gate(tape, a, b, x)

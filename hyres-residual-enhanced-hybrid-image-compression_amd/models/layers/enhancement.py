@@ -15,6 +15,7 @@ import torch.nn as nn
 from hyres_hip import _lib as L
 from hyres_hip import refine_ops as R
 from hyres_hip.layers import Conv2d, HipModule, PReLU, ReLU, Sequential
+from hyres_hip import ops as O
 from hyres_hip.ops import Node
 
 __all__ = ["SpatialAttention", "SEBlock", "dilated_conv", "MultiScaleRefine"]
@@ -104,16 +105,25 @@ class MultiScaleRefine(HipModule):
         B, H, W = feat.B, feat.H, feat.W
         assert H % 4 == 0 and W % 4 == 0, "MultiScaleRefine needs H, W divisible by 4"
         multi = Node.new(B, H, W, 3 * mid, feat.device)
-        # scale 1 (orig)
-        self.scale1.hip(tape, feat, out=multi.slice(0, mid))
-        # scale 2 (1/2): F.interpolate(scale_factor=0.5) -> source scale 2.0; back with size= -> in/out
-        f2 = R.bilinear(tape, feat, H // 2, W // 2, 2.0, 2.0)
-        f2 = self.scale2.hip(tape, f2)
-        R.bilinear(tape, f2, H, W, (H // 2) / H, (W // 2) / W, out=multi.slice(mid, 2 * mid))
-        # scale 3 (1/4)
-        f3 = R.bilinear(tape, feat, H // 4, W // 4, 4.0, 4.0)
-        f3 = self.scale3.hip(tape, f3)
-        R.bilinear(tape, f3, H, W, (H // 4) / H, (W // 4) / W, out=multi.slice(2 * mid, 3 * mid))
+
+        def scale1(tape, f):  # scale 1 (orig), written into multi[..., 0:mid]
+            self.scale1.hip(tape, f, out=multi.slice(0, mid))
+            return None
+
+        def scale2(tape, f):  # 1/2: F.interpolate(scale_factor=0.5) -> source scale 2.0; back with size=
+            f2 = R.bilinear(tape, f, H // 2, W // 2, 2.0, 2.0)
+            f2 = self.scale2.hip(tape, f2)
+            R.bilinear(tape, f2, H, W, (H // 2) / H, (W // 2) / W, out=multi.slice(mid, 2 * mid))
+            return f2
+
+        def scale3(tape, f):  # 1/4
+            f3 = R.bilinear(tape, f, H // 4, W // 4, 4.0, 4.0)
+            f3 = self.scale3.hip(tape, f3)
+            R.bilinear(tape, f3, H, W, (H // 4) / H, (W // 4) / W, out=multi.slice(2 * mid, 3 * mid))
+            return f3
+
+        # the three scales are independent: three HIP streams, disjoint channel slices of ``multi``
+        _, f2, f3 = O.run_branches(tape, feat, [scale1, scale2, scale3])
         m = self.spatial_att.hip_mul(tape, multi)
         out = self.fusion.hip(tape, m)
         from hyres_hip.ops import Trace
