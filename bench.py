@@ -41,6 +41,8 @@ def parse():
     ap.add_argument("--jpeg-quality", type=int, default=50)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=20.0)
+    ap.add_argument("--no-graph", action="store_true", help="eager launches instead of HIP-graph replay")
+    ap.add_argument("--no-eval", action="store_true", help="skip the encode+decode (eval) legs")
     return ap.parse_args()
 
 
@@ -82,15 +84,54 @@ def cpu_baseline(args, budget_s):
 PMC_TRAFFIC = os.path.join(REPO, "profiles", "r1_pmc_traffic.json")
 
 
-def traffic_bytes_per_launch():
-    """HBM bytes per conv_fwd_kernel<2,2,2,2,0,false> launch from the committed rocprofv3 PMC passes of this
-    same command (scripts/pmc_traffic.py: 2 x FETCH_SIZE + WRITE_SIZE, separate passes, gfx950
-    FETCH_SIZE correction); None when that summary is absent."""
+def traffic_bytes_per_launch(kernel):
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC passes of this same
+    command (scripts/pmc_traffic.py: 2 x FETCH_SIZE + WRITE_SIZE, separate passes, gfx950 FETCH_SIZE
+    correction); None when that summary is absent or was collected for another kernel."""
     try:
         with open(PMC_TRAFFIC) as f:
-            return json.load(f)["traffic_bytes_per_launch"]
+            d = json.load(f)
+        if kernel is None or kernel not in d["kernel"]:
+            return None
+        return d["traffic_bytes_per_launch"]
     except (OSError, KeyError, ValueError):
         return None
+
+
+def eval_legs(net, x, jpeg, jpeg_bpp, args, reps=20):
+    """Encode+decode (eval forward, SURVEY §8d: "Mpix/s = B*H*W / wall time of one step: forward (eval)
+    for encode+decode") at the bench batch (configs[1] shape) and at Kodak size 768x512 (configs[4],
+    fp32), device-only (JPEG precomputed), HIP-graph replay and eager."""
+    from hyres_hip.graphs import CapturedStep
+    net.eval()
+    res = {}
+    g = torch.Generator().manual_seed(1926)
+    xk = torch.randint(0, 256, (1, 3, 512, 768), generator=g).float() / 255.0
+    jk, bk = net.jpeg(xk)
+    dev = x.device
+    for tag, xe, je, be in (("bs%d_%dx%d" % (x.shape[0], x.shape[2], x.shape[3]), x, jpeg, jpeg_bpp),
+                            ("kodak_1x768x512", xk.to(dev), jk.to(dev), bk)):
+        cap = CapturedStep(net, xe, je, be)
+        torch.cuda.synchronize()
+        t0 = time.time()
+        for _ in range(reps):
+            cap.replay()
+        torch.cuda.synchronize()
+        ms = (time.time() - t0) * 1000 / reps
+        with torch.no_grad():
+            for _ in range(2):
+                net.forward_device(xe, je, be)
+            torch.cuda.synchronize()
+            t0 = time.time()
+            for _ in range(5):
+                net.forward_device(xe, je, be)
+            torch.cuda.synchronize()
+        ems = (time.time() - t0) * 1000 / 5
+        npx = xe.shape[0] * xe.shape[2] * xe.shape[3]
+        res[tag] = {"ms": round(ms, 3), "mpix_s": round(npx / ms / 1e3, 3), "eager_ms": round(ems, 3)}
+        del cap
+    net.train()
+    return res
 
 
 def main():
@@ -133,10 +174,23 @@ def main():
     x = x_cpu.to(dev)
     jpeg = jpeg_cpu.to(dev)
 
-    def step():
+    graphed = None
+    if not args.no_graph:
+        # forward + RD loss + backward captured once as a HIP graph (hyres_hip.graphs); the optimiser,
+        # the RCCL all-reduce and the aux step stay eager (a handful of launches)
+        from hyres_hip.graphs import CapturedStep
+        graphed = CapturedStep(net, x, jpeg, jpeg_bpp, noisequant=False, criterion=crit, zero_grad=opt.zero_grad)
+
+    def fwd_bwd(eager=False):
+        if graphed is not None and not eager:
+            return graphed.replay()[1]
         out = net.forward_device(x, jpeg, jpeg_bpp, noisequant=False)
         c = crit(out, x)
         c["loss"].backward()
+        return c
+
+    def step(eager=False):
+        c = fwd_bwd(eager)
         if reducer is not None:
             reducer.all_reduce()
         opt.step()
@@ -153,18 +207,23 @@ def main():
     if dist:
         tdist.barrier()
     torch.cuda.synchronize()
-    # dominant-kernel roofline, measured live: HIP events (torch's current stream = the stream every
-    # hyres_* launch goes to, hyres_hip._lib.stream()) around each conv_fwd_kernel<2,2,2,2,0,false> launch
-    O.KernelTimer.reset()
     t0 = time.time()
     for i in range(args.steps):
-        O.KernelTimer.enabled = i == args.steps - 1  # last timed step only: ~300 events perturb < 1%
         c = step()
     torch.cuda.synchronize()
     if dist:
         tdist.barrier()
     torch.cuda.synchronize()
     elapsed = time.time() - t0
+    loss_val = float(c["loss"])
+    # dominant-kernel roofline, measured live with HIP events (on the stream each conv launch goes to:
+    # torch's current stream, also inside the branch streams) around every conv_fwd_kernel launch of one
+    # eager step of the same workload right after the timed region (a graph replay cannot carry
+    # per-kernel host events); the instantiation with the largest total time is reported
+    O.KernelTimer.reset()
+    O.KernelTimer.enabled = True
+    step(eager=True)
+    torch.cuda.synchronize()
     O.KernelTimer.enabled = False
     if dist:
         t = torch.tensor([elapsed], device=dev)
@@ -175,12 +234,15 @@ def main():
 
     ks = O.KernelTimer.summary()
     achieved = ks["flops"] / (ks["total_ms"] * 1e-3) / 1e12 if ks["total_ms"] > 0 else 0.0
-    loss_val = float(c["loss"])
+
 
     if rank != 0:
         if dist:
             tdist.destroy_process_group()
         return
+    evals = None
+    if world == 1 and not args.no_eval:
+        evals = eval_legs(net, x, jpeg, jpeg_bpp, args)
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, args.cpu_baseline_seconds)
@@ -200,13 +262,17 @@ def main():
         "config": {"workload": "C2: ResidualJPEGCompression N=128 M=192 train step, lambda=0.045, "
                                "noisequant=False, JPEG q50 precomputed on host",
                    "global_batch": B * world, "image": [S, S], "parallelism": f"dp{world}"},
-        "roofline": {"bound": "mfma", "kernel": "conv_fwd_kernel<2,2,2,2,0,false> (implicit-GEMM conv, fp32 MFMA, fused epilogue)",
+        "roofline": {"bound": "mfma", "kernel": f"{ks['kernel']} (implicit-GEMM conv, fp32 MFMA, fused epilogue)",
                      "achieved": round(achieved, 3), "peak": MI355X_FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved / MI355X_FP32_PEAK_TFLOPS, 4),
-                     "traffic": traffic_bytes_per_launch(),
+                     "traffic": traffic_bytes_per_launch(ks["kernel"]),
                      "launches_per_step": ks["launches"], "avg_launch_us": round(ks["avg_us"], 2),
                      "flops_per_launch": ks["flops_per_launch"],
-                     "algorithmic_bytes_per_launch": ks["bytes_per_launch"]},
+                     "algorithmic_bytes_per_launch": ks["bytes_per_launch"],
+                     "timing": "HIP events around each launch of one eager step after the timed region",
+                     "ms_by_variant": ks.get("by_variant_ms")},
+        "graph": not args.no_graph,
+        "eval": evals,
         "cpu_baseline": cpu,
         "jpeg_host_ms_per_image": round(jpeg_ms, 3),
         "loss": loss_val,

@@ -199,6 +199,21 @@ __global__ void uniform_noise_kernel(float* out, long long n, unsigned long long
     }
 }
 
+// Graph-replayable draw: the seed lives in device memory and is advanced after the draw by
+// seed_advance_kernel (stream-ordered), so every replay of a captured HIP graph draws fresh noise.
+__global__ void uniform_noise_dev_kernel(float* out, long long n, const unsigned long long* seed_dev,
+                                         unsigned long long salt) {
+    const unsigned long long seed = splitmix64(*seed_dev ^ salt);
+    GRID_STRIDE(i, n) {
+        unsigned long long h = splitmix64(seed ^ splitmix64((unsigned long long)i));
+        float u = ((float)(h >> 40) + 0.5f) * (1.0f / 16777216.0f);  // (0,1)
+        out[i] = u - 0.5f;
+    }
+}
+__global__ void seed_advance_kernel(unsigned long long* seed_dev) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) *seed_dev = splitmix64(*seed_dev + 0x9E3779B97F4A7C15ull);
+}
+
 // ---------------------------------------------------------------- reductions
 __device__ __forceinline__ float block_sum(float v, float* red) {
     red[threadIdx.x] = v;
@@ -430,6 +445,17 @@ int hyres_uniform_noise(float* out, long long n, unsigned long long seed, unsign
     HY_REQUIRE(out, HYRES_E_ARG, "uniform_noise: NULL");
     hipLaunchKernelGGL(uniform_noise_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(s), out, n, seed, offset);
     return HY_LAUNCH_CHECK("uniform_noise");
+}
+
+int hyres_uniform_noise_dev(float* out, long long n, unsigned long long* seed_dev, unsigned long long salt,
+                            hyres_stream_t s) {
+    HY_REQUIRE(out && seed_dev, HYRES_E_ARG, "uniform_noise_dev: NULL");
+    hipLaunchKernelGGL(uniform_noise_dev_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(s), out, n,
+                       (const unsigned long long*)seed_dev, salt);
+    int rc = HY_LAUNCH_CHECK("uniform_noise_dev");
+    if (rc) return rc;
+    hipLaunchKernelGGL(seed_advance_kernel, dim3(1), dim3(64), 0, as_stream(s), seed_dev);
+    return HY_LAUNCH_CHECK("seed_advance");
 }
 
 static int reduce2(void (*k)(const float*, long long, float*), const float* x, long long n, float* out, void* ws,

@@ -96,6 +96,7 @@ _SIGS = {
     "hyres_gdn_reparam_bwd": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _P]),
     "hyres_gdn_dnorm": (_I, [_P, _P, _P, _P, _LL, _I, _I, _P]),
     "hyres_uniform_noise": (_I, [_P, _LL, _ULL, _ULL, _P]),
+    "hyres_uniform_noise_dev": (_I, [_P, _LL, _P, _ULL, _P]),
     "hyres_quantize": (_I, [_P, _I, _P, _LL, _P]),
     "hyres_ckbd_anchor_fwd": (_I, [_P, _P, _I, _P, _P, _I, _I, _I, _I, _P]),
     "hyres_ckbd_nonanchor_gc_fwd": (_I, [_P, _P, _P, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P,

@@ -15,6 +15,9 @@ from . import _lib as L
 from .ops import Node, Tape, _empty, param_grad, _ws
 
 
+_SALT = {"z": 0x5A17, "y_anchor": 0xA7C4, "y_non_anchor": 0x70A4, "y": 0x6C59}
+
+
 class NoiseSource:
     """U(-0.5, 0.5) noise from the HIP counter-based RNG (replaces torch ``uniform_`` draws).
 
@@ -31,9 +34,23 @@ class NoiseSource:
             assert tuple(t.shape) == (like.B, like.H, like.W, like.C), (key, t.shape)
             return t.contiguous()
         out = _empty((like.B, like.H, like.W, like.C), like.device)
+        if torch.cuda.is_current_stream_capturing():
+            # inside a HIP graph capture a host seed would be baked into every replay: draw from the
+            # device-resident seed instead (advanced on device after each draw)
+            L.call("hyres_uniform_noise_dev", out.data_ptr(), out.numel(), self._device_seed(like.device).data_ptr(),
+                   _SALT[key], L.stream())
+            return out
         seed = int(torch.randint(0, 2 ** 62, (1,)).item())
         L.call("hyres_uniform_noise", out.data_ptr(), out.numel(), seed, 0, L.stream())
         return out
+
+    def _device_seed(self, device) -> torch.Tensor:
+        seeds = self.__dict__.setdefault("_seeds", {})
+        t = seeds.get(device.index)
+        if t is None:  # initialised (outside any capture) from torch's CPU generator: manual_seed reproducible
+            t = torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).to(device)
+            seeds[device.index] = t
+        return t
 
 
 def _eb_param_lists(eb):

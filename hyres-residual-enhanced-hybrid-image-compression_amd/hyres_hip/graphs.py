@@ -1,0 +1,100 @@
+"""HIP-graph capture of the device step.
+
+The eager step enqueues ~1,000 kernels through Python (ctypes) per training step and ~350 per eval
+forward; the host needs ~28 ms / ~13.5 ms for that at bs=16 256x256, which leaves the GPU idle between
+dependent launches (eval is entirely host-bound). Capturing the step once into a HIP graph
+(``torch.cuda.CUDAGraph`` = hipGraph on ROCm) and replaying it launches the whole DAG — main stream,
+the AttentionBlock / MultiScaleRefine branch streams and the weight-gradient side stream, with their
+event edges — in one call.
+
+What is captured and what stays eager:
+  * captured: ``forward_device`` (+ RateDistortionLoss + backward for training), i.e. every
+    libhyres_hip launch of the reference's forward/backward (models/hyres.py:23-77,
+    src/utils/engine.py:33-55);
+  * eager: the optimiser (FusedAdam's bias correction reads the host step count), the RCCL gradient
+    all-reduce and the aux (quantiles) step — 3-10 launches per step.
+Graph-safety of the captured region:
+  * weights: the conv weight re-layout cache (hyres_hip.ops._prepped) is invalidated before capture so
+    every re-layout kernel is recorded and re-runs on each replay (weights change every optimiser step),
+    and again after capture so eager calls never trust a buffer only the graph writes;
+  * noise: training draws (EntropyBottleneck z, GaussianConditional y) read a device-resident seed that
+    the graph advances (hyres_uniform_noise_dev), so each replay draws fresh U(-1/2, 1/2);
+  * inputs x / jpeg_decoded / jpeg_bpp are static device buffers: ``replay(x, jpeg, bpp)`` copies new
+    data into them (device-to-device) before launching.
+"""
+from __future__ import annotations
+
+from typing import Callable, Optional
+
+import torch
+
+from . import ops as O
+
+
+def _prepare_noise(net: torch.nn.Module, device: torch.device) -> None:
+    from .entropy_ops import NoiseSource
+    for m in net.modules():
+        ns = getattr(m, "noise", None)
+        if isinstance(ns, NoiseSource):
+            ns._device_seed(device)
+
+
+class CapturedStep:
+    """``forward_device`` (eval) or forward + RD loss + backward (train) of a ResidualJPEGCompression,
+    captured once and replayed.
+
+    ``criterion``: a RateDistortionLoss for training capture (None = eval forward under no_grad).
+    ``zero_grad``: called after the warm-up runs (their backward accumulated into the gradients).
+    """
+
+    def __init__(self, net: torch.nn.Module, x: torch.Tensor, jpeg_decoded: torch.Tensor, jpeg_bpp: float = 0.0,
+                 noisequant: bool = False, criterion: Optional[Callable] = None,
+                 zero_grad: Optional[Callable[[], None]] = None, warmup: int = 2):
+        assert x.is_cuda, "CapturedStep needs device tensors"
+        self.net = net
+        self.train = criterion is not None
+        dev = x.device
+        self.x = x.detach().clone()
+        self.jpeg = jpeg_decoded.detach().clone()
+        self.bpp = torch.full((), float(jpeg_bpp), dtype=torch.float32, device=dev)
+        self.noisequant = noisequant
+        self.criterion = criterion
+        _prepare_noise(net, dev)
+
+        def run():
+            if self.train:
+                out = net.forward_device(self.x, self.jpeg, self.bpp, noisequant)
+                c = criterion(out, self.x)
+                c["loss"].backward()
+                return out, c
+            with torch.no_grad():
+                return net.forward_device(self.x, self.jpeg, self.bpp, noisequant), None
+
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(warmup):
+                run()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        torch.cuda.synchronize(dev)
+        if zero_grad is not None:
+            zero_grad()
+        self.graph = torch.cuda.CUDAGraph()
+        O.bump_weight_epoch()  # record every weight re-layout inside the graph
+        with torch.cuda.graph(self.graph):
+            self.out, self.crit = run()
+        O.bump_weight_epoch()  # eager calls must not reuse buffers only the graph writes
+        torch.cuda.synchronize(dev)
+
+    def replay(self, x: Optional[torch.Tensor] = None, jpeg_decoded: Optional[torch.Tensor] = None,
+               jpeg_bpp: Optional[float] = None):
+        """Run the captured step on the current stream; returns (outputs, loss dict or None) — static
+        tensors overwritten by the next replay."""
+        if x is not None:
+            self.x.copy_(x, non_blocking=True)
+        if jpeg_decoded is not None:
+            self.jpeg.copy_(jpeg_decoded, non_blocking=True)
+        if jpeg_bpp is not None:
+            self.bpp.fill_(float(jpeg_bpp))
+        self.graph.replay()
+        return self.out, self.crit

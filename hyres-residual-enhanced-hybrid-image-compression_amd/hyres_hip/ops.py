@@ -273,9 +273,9 @@ def _filter_taps(g: L.ConvGeom, mask: Optional[torch.Tensor]) -> L.ConvGeom:
 
 
 class KernelTimer:
-    """Optional HIP-event timing of the dominant kernel (conv_fwd_kernel<2,2,2,2,0,false>: Co > 64,
-    Ci % 32 == 0, no square prologue, fused epilogue) with its algorithmic FLOPs/bytes, for bench.py's
-    roofline line."""
+    """Optional HIP-event timing of conv_fwd_kernel launches, grouped by template instantiation (the same
+    selection hyres_conv_forward makes), with their algorithmic FLOPs/bytes; ``summary`` reports the
+    instantiation with the largest total time (the dominant kernel of bench.py's roofline line)."""
 
     enabled = False
     all_convs = False  # record every conv launch (layer table), not only the dominant variant
@@ -290,12 +290,27 @@ class KernelTimer:
     @classmethod
     def summary(cls):
         torch.cuda.synchronize()
-        ms = sum(ev[0].elapsed_time(ev[1]) for ev in cls.events)
-        flops = sum(ev[2] for ev in cls.events)
-        nbytes = sum(ev[3] for ev in cls.events)
-        n = len(cls.events)
-        return {"launches": n, "total_ms": ms, "avg_us": 1000.0 * ms / max(n, 1), "flops": flops,
-                "flops_per_launch": flops / max(n, 1), "bytes_per_launch": nbytes / max(n, 1)}
+        groups = {}
+        for s0, s1, fl, by, var in cls.events:
+            e = groups.setdefault(var, [0.0, 0.0, 0.0, 0])
+            e[0] += s0.elapsed_time(s1)
+            e[1] += fl
+            e[2] += by
+            e[3] += 1
+        if not groups:
+            return {"kernel": None, "launches": 0, "total_ms": 0.0, "avg_us": 0.0, "flops": 0.0,
+                    "flops_per_launch": 0.0, "bytes_per_launch": 0.0}
+        var, (ms, flops, nbytes, n) = max(groups.items(), key=lambda kv: kv[1][0])
+        return {"kernel": var, "launches": n, "total_ms": ms, "avg_us": 1000.0 * ms / n, "flops": flops,
+                "flops_per_launch": flops / n, "bytes_per_launch": nbytes / n,
+                "by_variant_ms": {k: round(v[0], 3) for k, v in groups.items()}}
+
+
+def conv_variant(g: L.ConvGeom, e: L.Epilogue, splitk: bool) -> str:
+    """The conv_fwd_kernel<TM, TN, WAVES_M, WAVES_N, MODE, SPLITK> hyres_conv_forward launches."""
+    tile = "2, 2, 2, 2" if g.Co > 64 else ("2, 1, 2, 2" if g.Co > 32 else "1, 1, 4, 1")
+    mode = (1 if e.square_input else 0) if g.Ci % 32 == 0 else 2
+    return f"conv_fwd_kernel<{tile}, {mode}, {'true' if splitk else 'false'}>"
 
 
 def conv_flops(g: L.ConvGeom) -> float:
@@ -315,9 +330,7 @@ def conv_bytes(g: L.ConvGeom, e: L.Epilogue) -> float:
 
 def _launch_conv(g: L.ConvGeom, x_ptr: int, w2: torch.Tensor, ldw: int, y_ptr: int, e: L.Epilogue) -> None:
     nb = L.load().hyres_conv_workspace_bytes(ctypes.byref(g))  # > 0 iff the launch is split-K
-    # the roofline kernel: conv_fwd_kernel<2,2,2,2,0,false> (Co > 64, Ci % 32 == 0, fused epilogue)
-    dominant = g.Co > 64 and g.Ci % 32 == 0 and not e.square_input and nb == 0
-    timed = KernelTimer.enabled and (dominant or KernelTimer.all_convs)
+    timed = KernelTimer.enabled
     if timed:
         s0 = torch.cuda.Event(enable_timing=True)
         s1 = torch.cuda.Event(enable_timing=True)
@@ -327,8 +340,7 @@ def _launch_conv(g: L.ConvGeom, x_ptr: int, w2: torch.Tensor, ldw: int, y_ptr: i
            None if ws is None else ws.data_ptr(), 0 if ws is None else ws.numel(), L.stream())
     if timed:
         s1.record()
-        if dominant:
-            KernelTimer.events.append((s0, s1, conv_flops(g), conv_bytes(g, e)))
+        KernelTimer.events.append((s0, s1, conv_flops(g), conv_bytes(g, e), conv_variant(g, e, nb > 0)))
         if KernelTimer.all_convs:
             desc = (f"B{g.B} {g.Hi}x{g.Wi}x{g.Ci}->{g.Ho}x{g.Wo}x{g.Co} taps{g.ntaps} ph{g.nphase} "
                     f"s{g.ish} epi{e.kind}{'+acc' if e.accumulate else ''}{'+res' if e.res else ''}")

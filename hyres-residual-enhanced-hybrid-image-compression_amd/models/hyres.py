@@ -44,9 +44,10 @@ class ResidualJPEGCompression(CompressionModel):
         O.Trace.add("x_hat", x_hat)
         return x_hat, y_lik, z_lik, residual, residual_hat
 
-    def forward_device(self, x: torch.Tensor, jpeg_decoded: torch.Tensor, jpeg_bpp: float = 0.0,
+    def forward_device(self, x: torch.Tensor, jpeg_decoded: torch.Tensor, jpeg_bpp=0.0,
                        noisequant: bool = False):
-        """Device-only forward with the JPEG stage's outputs supplied (both on the GPU)."""
+        """Device-only forward with the JPEG stage's outputs supplied (both on the GPU); ``jpeg_bpp`` is a
+        float or a 0-dim device tensor (graph capture: hyres_hip.graphs.CapturedStep)."""
         training = self.training
         rm = self.residual_model
 
@@ -62,7 +63,8 @@ class ResidualJPEGCompression(CompressionModel):
         return {
             "x_hat": x_hat,
             "likelihoods": {"y": y_lik, "z": z_lik},
-            "jpeg_bpp_loss": torch.tensor(jpeg_bpp, device=x.device),
+            "jpeg_bpp_loss": (jpeg_bpp if isinstance(jpeg_bpp, torch.Tensor)
+                              else torch.tensor(jpeg_bpp, device=x.device)),
             "jpeg_decoded": jpeg_decoded,
             "residual": residual,
             "residual_hat": residual_hat,

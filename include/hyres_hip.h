@@ -202,6 +202,10 @@ int hyres_gdn_dnorm(const float* g, const float* y, const float* n, float* dn, l
  * models/utils/quantization.py:6-10 and compressai EntropyModel.quantize("noise") */
 int hyres_uniform_noise(float* out, long long n, unsigned long long seed, unsigned long long offset,
                         hyres_stream_t s);
+/* Same distribution with the seed in device memory: draws with seed = mix(*seed_dev ^ salt), then
+ * advances *seed_dev (stream-ordered), so a captured HIP graph draws fresh noise on every replay. */
+int hyres_uniform_noise_dev(float* out, long long n, unsigned long long* seed_dev, unsigned long long salt,
+                            hyres_stream_t s);
 /* Quantizer.quantize (models/utils/quantization.py:11-14): mode 0 = "ste" value round(x)-x+x,
  * mode 1 = round (half-to-even) */
 int hyres_quantize(const float* x, int mode, float* y, long long n, hyres_stream_t s);

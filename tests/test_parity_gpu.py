@@ -544,3 +544,72 @@ def test_c5_kodak_size_eval_parity():
     assert out["likelihoods"]["y"].shape == (1, 192, 64, 96)
     assert out["likelihoods"]["z"].shape == (1, 128, 16, 24)
     _check_against_oracle(out, [0], x, jpeg, float(jpeg_bpp))
+
+
+# ------------------------------------------------------------------------------------------------ graphs
+def test_captured_eval_matches_eager_and_reference():
+    """hyres_hip.graphs.CapturedStep (eval): the replayed HIP graph computes exactly what the eager
+    launches compute, for the captured input and for new inputs copied into the static buffers."""
+    from hyres_hip.graphs import CapturedStep
+    g = load_npz("hyres_eval_b2_64.npz")
+    net, _ = _hip_model()
+    net.eval()
+    D = dev()
+    x, j, bpp = g["x"].to(D), g["jpeg_decoded"].to(D), float(g["jpeg_bpp"])
+    with torch.no_grad():
+        eager = net.forward_device(x, j, bpp)["x_hat"].clone()
+    cap = CapturedStep(net, x, j, bpp)
+    out, _ = cap.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out["x_hat"], eager)
+    assert rel_err(out["x_hat"].cpu(), g["x_hat"]) < TOL
+    x2 = torch.flip(x, dims=[3]).contiguous()
+    j2 = torch.flip(j, dims=[3]).contiguous()
+    with torch.no_grad():
+        eager2 = net.forward_device(x2, j2, bpp)
+    out, _ = cap.replay(x2, j2, bpp)
+    torch.cuda.synchronize()
+    assert torch.equal(out["x_hat"], eager2["x_hat"])
+    assert torch.equal(out["likelihoods"]["y"], eager2["likelihoods"]["y"])
+
+
+def test_captured_train_step_matches_eager():
+    """CapturedStep (train, recorded noise injected): loss and every parameter gradient of a replay equal
+    the eager step's; without injection every replay draws fresh noise (device-resident seed)."""
+    from hyres_hip.graphs import CapturedStep
+    from hyres_hip.loss import RateDistortionLoss
+    g = load_npz("hyres_train_b2_64.npz")
+    net, _ = _hip_model()
+    net.train()
+    D = dev()
+    x, j = g["x"].to(D), g["jpeg_decoded"].to(D)
+    rm = net.residual_model
+    rm.noise.injected = {"z": g["noise_z"].permute(0, 2, 3, 1).contiguous().to(D),
+                         "y": g["noise_y"].permute(0, 2, 3, 1).contiguous().to(D)}
+    crit = RateDistortionLoss(lmbda=0.045, alpha=0)
+    params = [p for p in net.parameters() if p.requires_grad]
+
+    def zero():
+        for p in params:
+            if p.grad is not None:
+                p.grad.zero_()
+
+    zero()
+    c = crit(net.forward_device(x, j, 0.25), x)
+    c["loss"].backward()
+    torch.cuda.synchronize()
+    loss_e = float(c["loss"])
+    grads_e = [p.grad.detach().clone() for p in params]
+    zero()
+    cap = CapturedStep(net, x, j, 0.25, criterion=crit, zero_grad=zero)
+    _, cc = cap.replay()
+    torch.cuda.synchronize()
+    assert float(cc["loss"]) == loss_e
+    for p, ge in zip(params, grads_e):
+        assert torch.equal(p.grad, ge), p.shape
+    # fresh noise per replay when nothing is injected
+    rm.noise.injected = None
+    cap2 = CapturedStep(net, x, j, 0.25, criterion=crit, zero_grad=zero)
+    l1 = float(cap2.replay()[1]["loss"])
+    l2 = float(cap2.replay()[1]["loss"])
+    assert l1 != l2 and abs(l1 - l2) < 0.05 * abs(l1)
