@@ -139,7 +139,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = world > 1
+    dist = world > 1 or os.environ.get("HYRES_BENCH_FORCE_DIST") == "1"  # rehearse the RCCL path at N=1
     if dist:
         import torch.distributed as tdist
         torch.cuda.set_device(local)
@@ -155,14 +155,17 @@ def main():
     net = ResidualJPEGCompression(jpeg_quality=args.jpeg_quality)
     torch.nn.Module.load_state_dict(net, synthetic_state_dict(net.state_dict()), strict=True)
     net = net.to(dev).train()
+    main_names = [n for n, p in sorted(net.named_parameters()) if not n.endswith(".quantiles")]
     main_p = [p for n, p in sorted(net.named_parameters()) if not n.endswith(".quantiles")]
     aux_p = [p for n, p in sorted(net.named_parameters()) if n.endswith(".quantiles")]
     opt = FusedAdam(main_p, lr=3e-4, max_grad_norm=1.0)
     aux_opt = FusedAdam(aux_p, lr=3e-4)
     reducer = None
     if dist:
-        from hyres_hip.ddp import FlatGradReducer
-        reducer = FlatGradReducer(opt.flat, world)
+        # RCCL all-reduce of refine / g_s / hyperprior gradient segments launched from backward-progress
+        # markers (overlapped with the rest of backward), the remainder (g_a) after backward
+        from hyres_hip.ddp import FlatGradReducer, HYRES_SEGMENTS
+        reducer = FlatGradReducer(opt.flat, world, names=main_names, segments=HYRES_SEGMENTS).overlap()
     crit = RateDistortionLoss(lmbda=args.lmbda, alpha=0)
 
     B, S = args.batch, args.size
@@ -175,7 +178,7 @@ def main():
     jpeg = jpeg_cpu.to(dev)
 
     graphed = None
-    if not args.no_graph:
+    if not args.no_graph and not dist:
         # forward + RD loss + backward captured once as a HIP graph (hyres_hip.graphs); the optimiser,
         # the RCCL all-reduce and the aux step stay eager (a handful of launches)
         from hyres_hip.graphs import CapturedStep
@@ -271,7 +274,7 @@ def main():
                      "algorithmic_bytes_per_launch": ks["bytes_per_launch"],
                      "timing": "HIP events around each launch of one eager step after the timed region",
                      "ms_by_variant": ks.get("by_variant_ms")},
-        "graph": not args.no_graph,
+        "graph": graphed is not None,
         "eval": evals,
         "cpu_baseline": cpu,
         "jpeg_host_ms_per_image": round(jpeg_ms, 3),

@@ -175,6 +175,29 @@ class Tape:
         SideStream.join()  # side-stream weight gradients complete before anyone reads .grad
 
 
+class GradReady:
+    """Backward-progress markers for overlapping the gradient all-reduce with backward.
+
+    ``mark(tape, name)`` during forward pushes a closure; the tape replays closures in reverse, so in
+    backward it runs once every layer built after the mark has launched its gradients (weight gradients
+    are on the side stream). Listeners (hyres_hip.ddp.FlatGradReducer.on_marker) are called with
+    ``name``; with no listener registered the mark costs nothing."""
+
+    listeners: list = []
+
+    @classmethod
+    def mark(cls, tape: Optional["Tape"], name: str) -> None:
+        if tape is None or not cls.listeners:
+            return
+        ls = list(cls.listeners)
+
+        def fire():
+            for f in ls:
+                f(name)
+
+        tape.push(fire)
+
+
 class Trace:
     """Debug/parity hook: when ``Trace.nodes`` is a dict, named activations are kept (by reference) so
     tests can read their values (``value``) and, after backward, their gradients (``grad``)."""

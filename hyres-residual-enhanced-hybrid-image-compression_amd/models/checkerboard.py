@@ -64,6 +64,7 @@ class LightWeightCheckerboard(CompressionModel):
         M = self.M
         T = O.Trace
         y = self.g_a.hip(tape, x)
+        O.GradReady.mark(tape, "hyper")  # backward: h_a/h_s/entropy/context/param_aggregation done
         z = self.h_a.hip(tape, y)
         z_hat, z_lik = self.entropy_bottleneck.hip(tape, z, training, noisequant, self.noise)
         lc = Node.new(y.B, y.H, y.W, 4 * M, y.device)
@@ -76,6 +77,7 @@ class LightWeightCheckerboard(CompressionModel):
         params_na = self.param_aggregation.hip(tape, lc)
         y_hat, y_lik = E.checkerboard_nonanchor_gc(tape, y, ya_hat, params_a, params_na, training, noisequant,
                                                    self.noise)
+        O.GradReady.mark(tape, "g_s")
         x_hat = self.g_s.hip(tape, y_hat)
         for name, n in (("y", y), ("z", z), ("z_hat", z_hat), ("latent_params", latent), ("y_anchor_hat", ya_hat),
                         ("ctx_params", ctx), ("y_hat", y_hat), ("residual_hat", x_hat)):

@@ -38,6 +38,7 @@ class ResidualJPEGCompression(CompressionModel):
         residual = R.add(tape, x, jpeg, alpha=-1.0)                       # hyres.py:48
         residual_hat, y_lik, z_lik = self.residual_model.hip(tape, residual, training, noisequant)
         x0 = R.add(tape, jpeg, residual_hat)                              # hyres.py:62
+        O.GradReady.mark(tape, "refine")  # backward: refine's gradients complete past this point
         refined = self.refine.hip(tape, x0)                               # hyres.py:65
         x_hat = R.add_clamp01(tape, x0, refined)                          # hyres.py:66-67
         O.Trace.add("x_hat_initial", x0)

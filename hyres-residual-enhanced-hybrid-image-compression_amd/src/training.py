@@ -102,8 +102,9 @@ def main(argv):
 
     optimizer, aux_optimizer = configure_optimizers(net, args, max_grad_norm=args.clip_max_norm)
     if world > 1:
-        from hyres_hip.ddp import FlatGradReducer
-        reducer = FlatGradReducer(optimizer.flat, world)
+        from hyres_hip.ddp import FlatGradReducer, HYRES_SEGMENTS
+        names = sorted(n for n, p in net.named_parameters() if not n.endswith(".quantiles") and p.requires_grad)
+        reducer = FlatGradReducer(optimizer.flat, world, names=names, segments=HYRES_SEGMENTS).overlap()
     lr_scheduler = torch.optim.lr_scheduler.MultiStepLR(optimizer, milestones=[400], gamma=0.1)
     criterion = RateDistortionLoss(lmbda=args.lmbda, alpha=args.alpha)
 

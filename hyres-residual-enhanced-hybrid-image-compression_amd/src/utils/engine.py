@@ -50,6 +50,8 @@ def train_one_epoch(model, criterion, train_dataloader, optimizer, aux_optimizer
         loss = out_criterion["loss"]
         if gradient_accumulation_steps != 1:
             loss = loss / gradient_accumulation_steps
+        if reducer is not None:  # overlapped all-reduce only on the accumulation boundary (DDP no_sync)
+            reducer.armed = (i + 1) % gradient_accumulation_steps == 0
         loss.backward()
         pending.append(out_criterion)
         if (i + 1) % gradient_accumulation_steps == 0:

@@ -40,6 +40,7 @@ def main():
         step()
     torch.cuda.synchronize()
     O.SideStream.enabled = False  # time each launch alone (no overlap with the side stream)
+    O.BranchStreams.enabled = False
     O.KernelTimer.reset()
     O.KernelTimer.enabled = True
     O.KernelTimer.all_convs = True

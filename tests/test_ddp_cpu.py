@@ -119,3 +119,61 @@ def test_flat_grad_reducer_gloo_world2():
 
 def test_sharded_gradient_equals_global_batch_gloo_world2():
     mp.spawn(_sharded_worker, args=(2, _free_port()), nprocs=2, join=True)
+
+
+def _overlap_worker(rank, world, port):
+    """Segmented all-reduce launched from backward-progress markers (hyres_hip.ops.GradReady) during the
+    tape backward, the remainder after it: same mean as the plain bucketed reduce; not armed (gradient
+    accumulation micro-batch) -> markers launch nothing."""
+    _init(rank, world, port)
+    try:
+        from hyres_hip.ddp import FlatGradReducer, HYRES_SEGMENTS
+        from hyres_hip.ops import GradReady, Tape
+        from hyres_hip.optim import FlatParams
+        names = sorted(["refine.conv.weight", "refine.conv.bias", "residual_model.g_a.0.weight",
+                        "residual_model.g_s.0.weight", "residual_model.h_a.0.weight",
+                        "residual_model.param_aggregation.0.bias", "residual_model.g_s.1.beta"])
+        shapes = [(5, 3), (3,), (4, 4), (7,), (2, 9), (6,), (11,)]
+        params = [torch.nn.Parameter(torch.zeros(s)) for s in shapes]
+        flat = FlatParams(params)
+        red = FlatGradReducer(flat, world, bucket_bytes=24, names=names, segments=HYRES_SEGMENTS)
+        assert set(red.segments) == {"refine", "g_s", "hyper"}
+        GradReady.listeners = []
+        red.overlap()
+        fired = []
+        for armed in (True, False):
+            flat.grad.zero_()
+            red.armed = armed
+            tape = Tape()
+            # forward order: g_a, [hyper mark], h_a/param_agg, [g_s mark], g_s, [refine mark], refine
+            owner = {"hyper": ("residual_model.h_a.", "residual_model.param_aggregation."),
+                     "g_s": ("residual_model.g_s.",), "refine": ("refine.",)}
+
+            def writer(prefixes):
+                def w():
+                    for i, (n, p) in enumerate(zip(names, params)):
+                        if n.startswith(prefixes):
+                            p.grad.copy_(torch.full(p.shape, float((rank + 1) * (i + 1))))
+                return w
+
+            tape.push(writer(("residual_model.g_a.",)))
+            for mk in ("hyper", "g_s", "refine"):
+                GradReady.mark(tape, mk)
+                tape.push(writer(owner[mk]))
+            tape.backward()
+            fired.append(list(red.fired))
+            if not armed:
+                assert red.fired == [] and red.works == []
+                continue
+            assert red.fired == ["refine", "g_s", "hyper"] and len(red.works) > 0
+            red.all_reduce()
+            mean = sum(r + 1 for r in range(world)) / world
+            for i, p in enumerate(params):
+                assert torch.allclose(p.grad, torch.full(p.shape, mean * (i + 1))), names[i]
+        GradReady.listeners = []
+    finally:
+        dist.destroy_process_group()
+
+
+def test_overlapped_segment_reduce_gloo_world2():
+    mp.spawn(_overlap_worker, args=(2, _free_port()), nprocs=2, join=True)

@@ -613,3 +613,45 @@ def test_captured_train_step_matches_eager():
     l1 = float(cap2.replay()[1]["loss"])
     l2 = float(cap2.replay()[1]["loss"])
     assert l1 != l2 and abs(l1 - l2) < 0.05 * abs(l1)
+
+
+def test_overlapped_rccl_reducer_single_rank():
+    """The RCCL path of hyres_hip.ddp.FlatGradReducer with backward-overlapped segments, on a one-rank
+    nccl (= RCCL) group: markers fire during the real model's tape backward, collectives are enqueued
+    behind the weight-gradient side stream, and the reduced gradients equal the un-reduced ones."""
+    import os
+    import socket
+    import torch.distributed as tdist
+    from hyres_hip.ddp import FlatGradReducer, HYRES_SEGMENTS
+    from hyres_hip.loss import RateDistortionLoss
+    from hyres_hip.ops import GradReady
+    from hyres_hip.optim import FusedAdam
+    g = load_npz("hyres_train_b2_64.npz")
+    net, _ = _hip_model()
+    net.train()
+    D = dev()
+    x, j = g["x"].to(D), g["jpeg_decoded"].to(D)
+    names = [n for n, p in sorted(net.named_parameters()) if not n.endswith(".quantiles")]
+    opt = FusedAdam([p for n, p in sorted(net.named_parameters()) if not n.endswith(".quantiles")], lr=0.0)
+    crit = RateDistortionLoss(lmbda=0.045, alpha=0)
+    net.residual_model.noise.injected = {"z": g["noise_z"].permute(0, 2, 3, 1).contiguous().to(D),
+                                         "y": g["noise_y"].permute(0, 2, 3, 1).contiguous().to(D)}
+    opt.zero_grad()
+    crit(net.forward_device(x, j, 0.0), x)["loss"].backward()
+    ref = opt.flat.grad.clone()
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    tdist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        red = FlatGradReducer(opt.flat, 1, names=names, segments=HYRES_SEGMENTS).overlap()
+        opt.zero_grad()
+        crit(net.forward_device(x, j, 0.0), x)["loss"].backward()
+        assert red.fired == ["refine", "g_s", "hyper"]
+        red.all_reduce()
+        torch.cuda.synchronize()
+        assert torch.equal(opt.flat.grad, ref)
+    finally:
+        GradReady.listeners = []
+        tdist.destroy_process_group()
