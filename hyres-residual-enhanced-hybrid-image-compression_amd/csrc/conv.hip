@@ -14,6 +14,7 @@
 // Weight gradients use a second kernel (P^T Q over pixels, split-K slabs + deterministic reduce).
 #include "common.h"
 
+#include <cstring>
 #include <utility>
 
 namespace hyres {
@@ -206,14 +207,12 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const ConvArgs a) {
     const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(a.x + (long long)b0 * img), (short)0, (int)(xrem < 0x7FFFFFF0LL ? xrem : 0x7FFFFFF0LL), 0x00020000);
     const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)a.w2, (short)0, a.w_bytes, 0x00020000);
-    int a_base[MODE == 2 ? 1 : A_V];  // element offset of image row 0 of this row's image, rel. to b0
-    if constexpr (MODE != 2) {
+    int a_base[A_V];  // element offset of image row 0 of this row's image, rel. to b0
 #pragma unroll
-        for (int q = 0; q < A_V; ++q) {
-            a_base[q] = (int)((a_b[q] - b0) * img);
-            a_i[q] *= g.ish;
-            a_j[q] *= g.isw;
-        }
+    for (int q = 0; q < A_V; ++q) {
+        a_base[q] = (int)((a_b[q] - b0) * img);
+        a_i[q] *= g.ish;
+        a_j[q] *= g.isw;
     }
     // tap offsets of this phase in LDS (uniform broadcast reads instead of indexed kernarg loads)
     __shared__ int2 tapoff[HYRES_MAX_TAPS];
@@ -245,30 +244,26 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const ConvArgs a) {
             ld_c += KT;
             if (ld_c == Ci) { ld_c = 0; ++ld_t; }
         } else {
+            // generic K = ntap*Ci (small Ci): a thread's k is the same for all its rows (256 % KT == 0),
+            // so the (tap, channel) decode happens once per chunk; branch-free raw buffer loads
             const int K = ntap * Ci;
+            const int k = kc * KT + (tid % KT);
+            const bool kok = k < K;
+            const int t = kok ? k / Ci : 0;
+            const int ci = k - t * Ci;
+            const int2 o = tapoff[t];
 #pragma unroll
             for (int q = 0; q < A_V; ++q) {
-                int e = tid + 256 * q;
-                int k = kc * KT + (e % KT);
-                float v = 0.f;
-                if (a_ok[q] && k < K) {
-                    int t = k / Ci;
-                    int ci = k - t * Ci;
-                    int gt = tap0 + t;
-                    int ih = a_i[q] * g.ish + g.dh[gt], iw = a_j[q] * g.isw + g.dw[gt];
-                    if (ih >= 0 && ih < g.Hi && iw >= 0 && iw < g.Wi)
-                        v = a.x[((long long)(a_b[q] * g.Hi + ih) * g.Wi + iw) * g.ldx + ci];
-                }
-                sa[q] = v;
+                const int ih = a_i[q] + o.x, iw = a_j[q] + o.y;
+                const bool okq = kok && a_ok[q] && (unsigned)ih < (unsigned)g.Hi && (unsigned)iw < (unsigned)g.Wi;
+                const int off = okq ? (a_base[q] + (ih * g.Wi + iw) * g.ldx + ci) * 4 : (int)0x80000000;
+                sa[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, off, 0, 0));
             }
 #pragma unroll
             for (int q = 0; q < B_V; ++q) {
-                int e = tid + 256 * q;
-                int co = n0 + e / KT;
-                int k = kc * KT + (e % KT);
-                float v = 0.f;
-                if (co < g.Co && k < K) v = a.w2[(long long)co * a.ldw + (long long)tap0 * Ci + k];
-                sb[q] = v;
+                const int co = n0 + (tid + 256 * q) / KT;
+                const int off = (co < g.Co && kok) ? (co * a.ldw + tap0 * Ci + k) * 4 : (int)0x80000000;
+                sb[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(wr, off, 0, 0));
             }
         }
     };
@@ -514,6 +509,107 @@ __global__ __launch_bounds__(256) void conv_splitk_reduce4_kernel(const ConvArgs
         const long long pix = (long long)(b * g.Ho + i * g.osh + g.oph[phase]) * g.Wo + j * g.osw + g.opw[phase];
         epi_store4(a.e, a.y, g.ldy, pix, n, v, slope);
     }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Narrow output (Co <= 4: the 3-channel image-side layers — g_s's last deconv 128->3, MultiScaleRefine's
+// conv 64->3 and the input-gradient of its conv 3->64). A 32-wide MFMA column tile would be >90% padding,
+// so these run on the VALU. Each 16-lane group owns one output pixel: lane l reads channels
+// [64s + 4l, +4) of every tap (a wave reads 4 adjacent pixels = contiguous NHWC rows, coalesced), keeps
+// CO partial sums, and the group folds them with 4 xor-shuffles. The phase's weights are staged once per
+// block in LDS as [tap][co][Ci] (a lane's float4 reads are consecutive across the group: conflict-free).
+// HBM traffic = the input once (tap re-reads hit L1/L2) + CO outputs.
+// ------------------------------------------------------------------------------------------------
+constexpr int NARROW_PIX = 256;      // output pixels per block
+constexpr int NARROW_WLDS = 8192;    // floats of staged weights (ntap * CO * Ci)
+
+template <int CO, int S>
+__global__ __launch_bounds__(256) void conv_narrow_kernel(const ConvArgs a) {
+    __shared__ __attribute__((aligned(16))) float Ws[NARROW_WLDS];
+    __shared__ int2 tapoff[HYRES_MAX_TAPS];
+    const hyres_conv_geom& g = a.g;
+    const int tid = threadIdx.x;
+    const int phase = blockIdx.y;
+    const int ntap = g.ntap[phase], tap0 = g.tap0[phase];
+    constexpr int CI = 64 * S;
+    for (int idx = tid; idx < ntap * CO * (CI / 4); idx += 256) {
+        const int c4 = idx % (CI / 4);
+        const int r = idx / (CI / 4);
+        const int co = r % CO, t = r / CO;
+        *reinterpret_cast<float4*>(&Ws[4 * idx]) = ld4(a.w2 + (long long)co * a.ldw + (tap0 + t) * CI + 4 * c4);
+    }
+    for (int i = tid; i < ntap; i += 256) tapoff[i] = make_int2(g.dh[tap0 + i], g.dw[tap0 + i]);
+    __syncthreads();
+
+    const int HqWq = g.Hq * g.Wq;
+    const int b0 = (blockIdx.x * NARROW_PIX) / HqWq;
+    const long long img = (long long)g.Hi * g.Wi * g.ldx;
+    const long long xrem = ((long long)g.B - b0) * img * 4;
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(a.x + (long long)b0 * img), (short)0, (int)(xrem < 0x7FFFFFF0LL ? xrem : 0x7FFFFFF0LL), 0x00020000);
+    const int l16 = tid & 15, slot = tid >> 4;  // 16 pixel slots per block pass
+    for (int it = 0; it < NARROW_PIX / 16; ++it) {
+        const int m = blockIdx.x * NARROW_PIX + it * 16 + slot;
+        const bool ok = m < a.M;
+        const int mm = ok ? m : 0;
+        const int b = mm / HqWq;
+        const int r = mm - b * HqWq;
+        const int i = r / g.Wq, j = r - (r / g.Wq) * g.Wq;
+        const int base = (int)((b - b0) * img);
+        float acc[CO];
+#pragma unroll
+        for (int c = 0; c < CO; ++c) acc[c] = 0.f;
+        for (int t = 0; t < ntap; ++t) {
+            const int2 o = tapoff[t];
+            const int ih = i * g.ish + o.x, iw = j * g.isw + o.y;
+            const bool in = ok && (unsigned)ih < (unsigned)g.Hi && (unsigned)iw < (unsigned)g.Wi;
+            const int off = in ? (base + (ih * g.Wi + iw) * g.ldx + 4 * l16) * 4 : (int)0x80000000;
+            float4 xv[S];
+#pragma unroll
+            for (int s2 = 0; s2 < S; ++s2)
+                xv[s2] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                        xr, in ? off + 256 * s2 : off, 0, 0));
+#pragma unroll
+            for (int s2 = 0; s2 < S; ++s2)
+#pragma unroll
+                for (int co = 0; co < CO; ++co) {
+                    const float4 w = *reinterpret_cast<const float4*>(&Ws[(t * CO + co) * CI + 64 * s2 + 4 * l16]);
+                    acc[co] = fmaf(xv[s2].x, w.x, acc[co]);
+                    acc[co] = fmaf(xv[s2].y, w.y, acc[co]);
+                    acc[co] = fmaf(xv[s2].z, w.z, acc[co]);
+                    acc[co] = fmaf(xv[s2].w, w.w, acc[co]);
+                }
+        }
+#pragma unroll
+        for (int co = 0; co < CO; ++co) {
+            float v = acc[co];
+            v += __shfl_xor(v, 8);
+            v += __shfl_xor(v, 4);
+            v += __shfl_xor(v, 2);
+            v += __shfl_xor(v, 1);
+            acc[co] = v;
+        }
+        float v = acc[0];
+#pragma unroll
+        for (int co = 1; co < CO; ++co) v = l16 == co ? acc[co] : v;
+        if (ok && l16 < CO) {
+            const long long pix = (long long)(b * g.Ho + i * g.osh + g.oph[phase]) * g.Wo + j * g.osw + g.opw[phase];
+            epi_store(a.e, a.y, g.ldy, pix, l16, v, epi_channel(a.e, l16));
+        }
+    }
+}
+
+static bool narrow_ok(const hyres_conv_geom* g) {
+    if (g->Co > 4 || (g->Ci != 64 && g->Ci != 128)) return false;
+    int maxtap = 0;
+    for (int p = 0; p < g->nphase; ++p) maxtap = std::max(maxtap, g->ntap[p]);
+    return maxtap * g->Co * g->Ci <= NARROW_WLDS;
+}
+
+template <int CO>
+static void launch_narrow(const ConvArgs& a, dim3 grid, hipStream_t st) {
+    if (a.g.Ci == 64) hipLaunchKernelGGL((conv_narrow_kernel<CO, 1>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((conv_narrow_kernel<CO, 2>), grid, dim3(256), 0, st, a);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -835,6 +931,43 @@ struct PrepArgs {
     int kh[HYRES_MAX_TAPS], kw[HYRES_MAX_TAPS];
 };
 
+__device__ __forceinline__ float prep_value(const PrepArgs& a, long long idx) {
+    const int c = (int)(idx % a.cols);
+    const long long rt = idx / a.cols;
+    const int t = (int)(rt % a.ntaps);
+    const int r = (int)(rt / a.ntaps);
+    const int kh = a.kh[t], kw = a.kw[t];
+    long long src;
+    switch (a.mode) {
+        case HYRES_WPREP_CONV: src = (((long long)r * a.Ci + c) * a.KH + kh) * a.KW + kw; break;
+        case HYRES_WPREP_CONV_DGRAD: src = (((long long)c * a.Ci + r) * a.KH + kh) * a.KW + kw; break;
+        case HYRES_WPREP_DECONV: src = (((long long)c * a.Co + r) * a.KH + kh) * a.KW + kw; break;
+        default: src = (((long long)r * a.Co + c) * a.KH + kh) * a.KW + kw; break;
+    }
+    float v = a.w[src];
+    if (a.mask) v *= a.mask[src];
+    return v;
+}
+
+struct PrepDesc {
+    PrepArgs a;
+    long long begin, count;
+};
+
+// one grid over the concatenated outputs of n descriptors; a block finds its descriptor by binary search
+__global__ __launch_bounds__(256) void weight_prep_batch_kernel(const PrepDesc* d, int n, long long total) {
+    for (long long idx = blockIdx.x * 256LL + threadIdx.x; idx < total; idx += (long long)gridDim.x * 256) {
+        int lo = 0, hi = n - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (d[mid].begin <= idx) lo = mid; else hi = mid - 1;
+        }
+        const PrepDesc& e = d[lo];
+        const long long k = idx - e.begin;
+        if (k < e.count) e.a.w2[k] = prep_value(e.a, k);
+    }
+}
+
 __global__ void weight_prep_kernel(const PrepArgs a) {
     const long long total = (long long)a.rows * a.ntaps * a.cols;
     for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
@@ -1092,6 +1225,40 @@ int hyres_conv_weight_prep(const hyres_conv_geom* g, const float* w, float* w2, 
     return HY_LAUNCH_CHECK("weight_prep_kernel");
 }
 
+long long hyres_prep_desc_bytes(void) { return (long long)sizeof(PrepDesc); }
+
+int hyres_prep_desc_fill(void* desc, const hyres_conv_geom* g, const float* w, float* w2, int mode, int Ci, int Co,
+                         int KH, int KW, long long begin, long long* count) {
+    HY_REQUIRE(desc && g && w && w2 && count, HYRES_E_ARG, "prep_desc_fill: NULL");
+    PrepDesc d{};
+    PrepArgs& a = d.a;
+    a.w = w; a.w2 = w2; a.mask = nullptr; a.mode = mode; a.KH = KH; a.KW = KW; a.Ci = Ci; a.Co = Co;
+    a.ntaps = g->ntaps;
+    for (int t = 0; t < g->ntaps; ++t) {
+        HY_REQUIRE(g->kh[t] < KH && g->kw[t] < KW, HYRES_E_SHAPE, "prep_desc: tap %d outside %dx%d", t, KH, KW);
+        a.kh[t] = g->kh[t];
+        a.kw[t] = g->kw[t];
+    }
+    switch (mode) {
+        case HYRES_WPREP_CONV: case HYRES_WPREP_DECONV: a.rows = Co; a.cols = Ci; break;
+        case HYRES_WPREP_CONV_DGRAD: case HYRES_WPREP_DECONV_DGRAD: a.rows = Ci; a.cols = Co; break;
+        default: return set_error(HYRES_E_ARG, "prep_desc: bad mode %d", mode);
+    }
+    d.begin = begin;
+    d.count = (long long)a.rows * a.ntaps * a.cols;
+    *count = d.count;
+    memcpy(desc, &d, sizeof(d));
+    return ok();
+}
+
+int hyres_conv_weight_prep_batch(const void* descs, int n, long long total, hyres_stream_t s) {
+    HY_REQUIRE(descs && n > 0 && total > 0, HYRES_E_ARG, "prep_batch: empty");
+    const int blocks = (int)std::min<long long>((total + 255) / 256, 8192);
+    hipLaunchKernelGGL(weight_prep_batch_kernel, dim3(blocks), dim3(256), 0, as_stream(s), (const PrepDesc*)descs, n,
+                       total);
+    return HY_LAUNCH_CHECK("weight_prep_batch_kernel");
+}
+
 struct ConvPlan {
     int BM, BN, nsplit, cps;
 };
@@ -1118,7 +1285,7 @@ static ConvPlan conv_plan(const hyres_conv_geom* g) {
 }
 
 long long hyres_conv_workspace_bytes(const hyres_conv_geom* g) {
-    if (!g) return 0;
+    if (!g || narrow_ok(g)) return 0;
     ConvPlan p = conv_plan(g);
     if (p.nsplit <= 1) return 0;
     return (long long)p.nsplit * g->nphase * ((long long)g->B * g->Hq * g->Wq) * g->Co * 4;
@@ -1173,6 +1340,18 @@ int hyres_conv_forward(const hyres_conv_geom* g, const float* x, const float* w2
     if (e->act == HYRES_ACT_RELU_MASK)
         HY_REQUIRE(e->aux0 && e->kind == HYRES_EPI_BIAS, HYRES_E_ARG, "conv: ReLU mask needs aux0, BIAS epilogue");
     hipStream_t st = as_stream(s);
+    if (narrow_ok(g) && !e->square_input && e->kind == HYRES_EPI_BIAS && aligned16(x) &&
+        aligned16(w2) && g->ldx % 4 == 0 && ldw % 4 == 0) {
+        a.nsplit = 1;
+        dim3 grid(ceil_div(a.M, NARROW_PIX), g->nphase);
+        switch (g->Co) {
+            case 1: launch_narrow<1>(a, grid, st); break;
+            case 2: launch_narrow<2>(a, grid, st); break;
+            case 3: launch_narrow<3>(a, grid, st); break;
+            default: launch_narrow<4>(a, grid, st); break;
+        }
+        return HY_LAUNCH_CHECK("conv_narrow_kernel");
+    }
     int rc;
     if (g->Co > 64) rc = launch_fwd<2, 2, 2, 2>(a, mode, st);
     else if (g->Co > 32) rc = launch_fwd<2, 1, 2, 2>(a, mode, st);

@@ -68,6 +68,10 @@ _SIGS = {
     "hyres_geom_deconv2d_dgrad": (_I, [ctypes.POINTER(ConvGeom)] + [_I] * 9),
     "hyres_geom_filter_taps": (_I, [ctypes.POINTER(ConvGeom), ctypes.POINTER(ctypes.c_ubyte), _I]),
     "hyres_conv_weight_prep": (_I, [ctypes.POINTER(ConvGeom), _P, _P, _I, _I, _I, _I, _I, _I, _P, _P]),
+    "hyres_prep_desc_bytes": (_LL, []),
+    "hyres_prep_desc_fill": (_I, [_P, ctypes.POINTER(ConvGeom), _P, _P, _I, _I, _I, _I, _I, _LL,
+                                  ctypes.POINTER(_LL)]),
+    "hyres_conv_weight_prep_batch": (_I, [_P, _I, _LL, _P]),
     "hyres_conv_forward": (_I, [ctypes.POINTER(ConvGeom), _P, _P, _I, _P, ctypes.POINTER(Epilogue), _P, _LL,
                                 _P]),
     "hyres_conv_workspace_bytes": (_LL, [ctypes.POINTER(ConvGeom)]),

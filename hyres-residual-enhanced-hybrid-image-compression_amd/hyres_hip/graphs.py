@@ -80,6 +80,7 @@ class CapturedStep:
         if zero_grad is not None:
             zero_grad()
         self.graph = torch.cuda.CUDAGraph()
+        O.PrepBatch.prepare(dev)  # descriptor table uploaded now: the capture records ONE batched re-layout
         O.bump_weight_epoch()  # record every weight re-layout inside the graph
         with torch.cuda.graph(self.graph):
             self.out, self.crit = run()

@@ -15,6 +15,7 @@ CPU oracle (oracle/hyres_oracle.py) in tests/test_parity_gpu.py.
 from __future__ import annotations
 
 import ctypes
+import weakref
 from typing import Callable, List, Optional
 
 import torch
@@ -68,7 +69,8 @@ def zeros(shape, device) -> torch.Tensor:
 class Node:
     """NHWC activation [B,H,W,C]; ``v`` may be a channel slice of a wider buffer (pixel stride ld)."""
 
-    __slots__ = ("v", "B", "H", "W", "C", "ld", "rg", "parent", "c0", "_g", "gflag", "relu_out", "gmasked")
+    __slots__ = ("v", "B", "H", "W", "C", "ld", "rg", "parent", "c0", "_g", "gflag", "relu_out", "gmasked",
+                 "pending")
 
     def __init__(self, v: torch.Tensor, rg: bool = True, parent: "Node" = None, c0: int = 0):
         assert v.dim() == 4 and v.stride(3) == 1, "Node expects an NHWC tensor with unit channel stride"
@@ -86,6 +88,9 @@ class Node:
         # whose input-gradient epilogue applied it as the FIRST contribution; cleared by any later one).
         self.relu_out = False
         self.gmasked = False
+        # deferred residual gradient (tensor, pixel stride): added by the next input-gradient conv's
+        # epilogue (``grad_target_epi``) instead of a separate add pass, or materialised on first access
+        self.pending = None
 
     @staticmethod
     def new(B, H, W, C, device, rg=True) -> "Node":
@@ -112,6 +117,8 @@ class Node:
     # ---- gradients
     def grad(self) -> Optional[torch.Tensor]:
         """The accumulated gradient (same view structure as v) or None if nothing flowed here."""
+        if self.pending is not None:
+            self._materialize()
         if self.parent is not None:
             pg = self.parent.grad()
             return None if pg is None else pg[..., self.c0:self.c0 + self.C]
@@ -120,8 +127,38 @@ class Node:
     def grad_ld(self) -> int:
         return self.parent.grad_ld() if self.parent is not None else self.C
 
+    def defer_residual(self, g: torch.Tensor, ld: int) -> bool:
+        """Record the residual-branch gradient ``g`` (pixel stride ``ld``) as this node's first contribution,
+        to be added inside the next writer's epilogue (False: not deferrable, the caller adds it now)."""
+        if self.parent is not None or self.gflag or self.pending is not None:
+            return False
+        self.pending = (g, ld)
+        return True
+
+    def _materialize(self) -> None:
+        g, ld = self.pending
+        self.pending = None
+        tgt, acc = self.grad_target()
+        L.call("hyres_add2d", g.data_ptr(), ld, tgt.data_ptr(), self.C, self.P, self.C, acc, L.stream())
+
+    def grad_target_epi(self, e: "L.Epilogue"):
+        """``grad_target`` for an input-gradient conv: a deferred residual gradient is folded into its
+        epilogue as ``e.res`` (the ReLU mask, if the conv applies it, then covers both). Returns
+        (tensor, accumulate, keep-alive tensor or None)."""
+        if self.pending is not None and self.parent is None and not self.gflag:
+            g, ld = self.pending
+            self.pending = None
+            tgt, acc = self.grad_target()
+            e.res = g.data_ptr()
+            e.ldres = ld
+            return tgt, acc, g
+        tgt, acc = self.grad_target()
+        return tgt, acc, None
+
     def grad_target(self):
         """(tensor, accumulate) for a kernel that adds its contribution to this node's gradient."""
+        if self.pending is not None:
+            self._materialize()
         if self.parent is not None:
             pg, _ = self.parent._zeroed_grad()
             return pg[..., self.c0:self.c0 + self.C], 1
@@ -142,6 +179,8 @@ class Node:
             self.gmasked = True
 
     def _zeroed_grad(self):
+        if self.pending is not None:
+            self._materialize()
         self.gmasked = False  # the caller accumulates an unmasked contribution
         if self._g is None:
             self._g = zeros(self.v.shape, self.v.device)
@@ -254,11 +293,100 @@ def _prepped(weight: torch.Tensor, geom: L.ConvGeom, mode: int, Ci: int, Co: int
     ent = cache.get(key)
     if ent is not None and ent[0] == stamp:
         return ent[1]
+    if ent is not None and PrepBatch.run(weight.device):  # re-lays out every registered weight at once
+        ent = cache.get(key)
+        if ent[0] == stamp:
+            return ent[1]
     buf = ent[1] if ent is not None else _empty((rows, geom.ntaps * cols), weight.device)
     L.call("hyres_conv_weight_prep", ctypes.byref(geom), weight.data_ptr(), buf.data_ptr(), mode, Ci, Co,
            KH, KW, pad, None, L.stream())
     cache[key] = (stamp, buf)
+    PrepBatch.register(weight, key, geom, buf, mode, Ci, Co, KH, KW)
     return buf
+
+
+class PrepBatch:
+    """All cached conv-weight re-layouts of a device as ONE batched launch per weight epoch (i.e. per
+    optimiser step) instead of one small launch per layer and layout. Entries are registered on their first
+    individual prep; the device descriptor table is (re)built outside graph capture, and the batch is run
+    at the first cache miss of a new epoch, after which every registered entry is stamped fresh."""
+
+    _state = {}  # device index -> dict(entries, table, n, total, epoch, dirty)
+
+    @classmethod
+    def register(cls, weight, key, geom, buf, mode, Ci, Co, KH, KW) -> None:
+        if weight.device.type != "cuda":
+            return
+        st = cls._state.setdefault(weight.device.index, {"entries": {}, "table": None, "epoch": -1, "dirty": False,
+                                                         "order": []})
+        ek = (id(weight), key)
+        ent = st["entries"].get(ek)
+        if ent is None or ent[0]() is not weight or ent[3]() is not buf:
+            g = L.ConvGeom()
+            ctypes.memmove(ctypes.byref(g), ctypes.byref(geom), ctypes.sizeof(g))
+            st["entries"][ek] = (weakref.ref(weight), key, g, weakref.ref(buf), mode, Ci, Co, KH, KW,
+                                 weight.data_ptr(), buf.data_ptr())
+            st["dirty"] = True
+
+    @classmethod
+    def _build(cls, st, device) -> None:
+        lib = L.load()
+        dsz = int(lib.hyres_prep_desc_bytes())
+        live = {}
+        for ek, e in st["entries"].items():
+            w, buf = e[0](), e[3]()
+            if w is not None and buf is not None and w.data_ptr() == e[9] and buf.data_ptr() == e[10]:
+                live[ek] = e
+        st["entries"] = live
+        ents = [(e[0](), e[1], e[2], e[3](), *e[4:9]) for e in live.values()]
+        if not ents:
+            st.update(table=None, n=0, total=0, order=[], dirty=False)
+            return
+        host = (ctypes.c_ubyte * (dsz * len(ents)))()
+        begin = 0
+        for i, (w, key, g, buf, mode, Ci, Co, KH, KW) in enumerate(ents):
+            cnt = ctypes.c_longlong(0)
+            L.check(lib.hyres_prep_desc_fill(ctypes.addressof(host) + i * dsz, ctypes.byref(g), w.data_ptr(),
+                                             buf.data_ptr(), mode, Ci, Co, KH, KW, begin, ctypes.byref(cnt)),
+                    "hyres_prep_desc_fill")
+            begin += cnt.value
+        t = torch.frombuffer(bytearray(host), dtype=torch.uint8).to(device)
+        order = [(weakref.ref(e[0]), e[1], weakref.ref(e[3]), e[0].data_ptr(), e[3].data_ptr()) for e in ents]
+        st.update(table=t, n=len(ents), total=begin, order=order, dirty=False)
+
+    @staticmethod
+    def _stale(st) -> bool:
+        for wr, key, br, wp, bp in st["order"]:
+            w, b = wr(), br()
+            if w is None or b is None or w.data_ptr() != wp or b.data_ptr() != bp:
+                return True
+        return False
+
+    @classmethod
+    def prepare(cls, device) -> None:
+        """Build the descriptor table now (outside graph capture) so a capture can record the batch."""
+        st = cls._state.get(device.index) if device.type == "cuda" else None
+        if st is not None and (st["dirty"] or st["table"] is None or cls._stale(st)):
+            cls._build(st, device)
+
+    @classmethod
+    def run(cls, device) -> bool:
+        st = cls._state.get(device.index) if device.type == "cuda" else None
+        if st is None or st["epoch"] == _WEIGHT_EPOCH[0]:
+            return False
+        capturing = torch.cuda.is_current_stream_capturing()
+        if st["dirty"] or st["table"] is None or cls._stale(st):
+            if capturing:
+                return False  # the table upload is a host->device copy: prep individually this time
+            cls._build(st, device)
+            if st["table"] is None:
+                return False
+        st["epoch"] = _WEIGHT_EPOCH[0]
+        L.call("hyres_conv_weight_prep_batch", st["table"].data_ptr(), st["n"], st["total"], L.stream())
+        for wr, key, br, _, _ in st["order"]:
+            w = wr()
+            w._hyres_prep[key] = ((w.data_ptr(), w._version, _WEIGHT_EPOCH[0]), br())
+        return True
 
 
 def _ws(nbytes: int, device, slot=0) -> torch.Tensor:
@@ -513,7 +641,7 @@ def conv2d(tape: Optional[Tape], x: Node, weight: torch.Tensor, bias: Optional[t
             return
         gp, gpld = _act_backward(y, gy, y.grad_ld(), act, pre, slope)
         P = y.P
-        if res is not None and res.rg:
+        if res is not None and res.rg and not res.defer_residual(gp, gpld):
             tgt, acc = res.grad_target()
             L.call("hyres_add2d", gp.data_ptr(), gpld, tgt.data_ptr(), res.grad_ld(), P, Co, acc, L.stream())
         if wants_grad(bias) and not wants_grad(weight):
@@ -527,12 +655,12 @@ def conv2d(tape: Optional[Tape], x: Node, weight: torch.Tensor, bias: Optional[t
             _wgrad(d, gp.data_ptr(), x.ptr(), param_grad(weight), x.device,
                    param_grad(bias) if wants_grad(bias) else None, keep=(gp, x.v), side=True)
         if x.rg:
-            tgt, acc = x.grad_target()
+            ed = L.Epilogue()
+            ed.kind = L.EPI_BIAS
+            tgt, acc, _keep = x.grad_target_epi(ed)
             gd = _filter_taps(_geom("hyres_geom_conv2d_dgrad", B, H, W, Ci, x.grad_ld(), Co, gpld, KH, KW, stride,
                                     pad, dil), mask)
             w2d = _prepped(weight, gd, L.WPREP_CONV_DGRAD, Ci_w, Co, KH, KW, pad, mask)
-            ed = L.Epilogue()
-            ed.kind = L.EPI_BIAS
             ed.accumulate = acc
             x.relu_mask_epilogue(ed, acc)
             _launch_conv(gd, gp.data_ptr(), w2d, gd.ntaps * Co, tgt.data_ptr(), ed)
@@ -575,11 +703,11 @@ def deconv2d(tape: Optional[Tape], x: Node, weight: torch.Tensor, bias: Optional
             d.accumulate = 1
             _wgrad(d, x.ptr(), gp.data_ptr(), param_grad(weight), x.device, keep=(gp, x.v), side=True)
         if x.rg:
-            tgt, acc = x.grad_target()
-            gd = _geom("hyres_geom_deconv2d_dgrad", B, H, W, Ci, x.grad_ld(), Co, gpld, K, pad)
-            w2d = _prepped(weight, gd, L.WPREP_DECONV_DGRAD, Ci, Co, K, K, pad)
             ed = L.Epilogue()
             ed.kind = L.EPI_BIAS
+            tgt, acc, _keep = x.grad_target_epi(ed)
+            gd = _geom("hyres_geom_deconv2d_dgrad", B, H, W, Ci, x.grad_ld(), Co, gpld, K, pad)
+            w2d = _prepped(weight, gd, L.WPREP_DECONV_DGRAD, Ci, Co, K, K, pad)
             ed.accumulate = acc
             x.relu_mask_epilogue(ed, acc)
             _launch_conv(gd, gp.data_ptr(), w2d, gd.ntaps * Co, tgt.data_ptr(), ed)

@@ -81,6 +81,14 @@ int hyres_geom_deconv2d_dgrad(hyres_conv_geom* g, int B, int H, int W, int Ci, i
 #define HYRES_WPREP_DECONV_DGRAD 3/* ConvT dgrad:     rows = Ci(in), cols = Co(out) */
 int hyres_conv_weight_prep(const hyres_conv_geom* g, const float* w, float* w2, int mode, int Ci,
                            int Co, int KH, int KW, int pad, const float* mask, hyres_stream_t s);
+/* Batched re-layout: every conv weight of a model in ONE launch per optimiser step.
+ * hyres_prep_desc_fill writes one descriptor (hyres_prep_desc_bytes() bytes, host memory) for the same
+ * arguments as hyres_conv_weight_prep, covering output elements [begin, begin + rows*ntaps*cols);
+ * hyres_conv_weight_prep_batch runs n device-resident descriptors (sorted by begin, total elements). */
+long long hyres_prep_desc_bytes(void);
+int hyres_prep_desc_fill(void* desc, const hyres_conv_geom* g, const float* w, float* w2, int mode, int Ci, int Co,
+                         int KH, int KW, long long begin, long long* count);
+int hyres_conv_weight_prep_batch(const void* descs, int n, long long total, hyres_stream_t s);
 
 /* epilogue of the convolution GEMM */
 #define HYRES_EPI_BIAS 0      /* y = act(acc + bias + res) */

@@ -655,3 +655,41 @@ def test_overlapped_rccl_reducer_single_rank():
     finally:
         GradReady.listeners = []
         tdist.destroy_process_group()
+
+
+def test_batched_weight_relayout_matches_individual():
+    """hyres_hip.ops.PrepBatch: after an optimiser-style weight update (new epoch) every cached conv
+    re-layout is refreshed by ONE batched launch, bit-identical to the per-layer re-layout kernel."""
+    import ctypes
+    from hyres_hip import _lib as L
+    from hyres_hip import ops as O
+    g = load_npz("hyres_eval_b2_64.npz")
+    net, _ = _hip_model()
+    net.eval()
+    D = dev()
+    x, j = g["x"].to(D), g["jpeg_decoded"].to(D)
+    with torch.no_grad():
+        ref = net.forward_device(x, j, 0.0)["x_hat"].clone()
+        W = net.residual_model.g_a[4].weight
+        W.data.add_(0.01)
+        O.bump_weight_epoch()
+        out = net.forward_device(x, j, 0.0)["x_hat"].clone()
+    torch.cuda.synchronize()
+    st = O.PrepBatch._state[D.index]
+    assert st["epoch"] == O._WEIGHT_EPOCH[0] and st["n"] > 10, "batched re-layout did not run"
+    assert not torch.equal(out, ref)
+    for wr, key, br, _, _ in st["order"]:
+        w, buf = wr(), br()
+        ent = [e for e in st["entries"].values() if e[0]() is w and e[1] == key][0]
+        _, _, geom, _, mode, Ci, Co, KH, KW, _, _ = ent
+        one = torch.empty_like(buf)
+        L.call("hyres_conv_weight_prep", ctypes.byref(geom), w.data_ptr(), one.data_ptr(), mode, Ci, Co, KH, KW, 0,
+               None, L.stream())
+        torch.cuda.synchronize()
+        assert torch.equal(one, buf), key
+    with torch.no_grad():
+        W.data.sub_(0.01)
+        O.bump_weight_epoch()
+        back = net.forward_device(x, j, 0.0)["x_hat"]
+    torch.cuda.synchronize()
+    assert torch.equal(back, ref)
