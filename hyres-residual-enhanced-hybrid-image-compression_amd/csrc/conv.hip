@@ -649,8 +649,13 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgradArgs a) {
     constexpr int BM = 32 * TM * WAVES_M;
     constexpr int BN = 32 * TN * WAVES_N;
     constexpr int PP = BM + 4, PQ = BN + 4;
-    __shared__ __attribute__((aligned(16))) float Ps[KT * PP];
-    __shared__ __attribute__((aligned(16))) float Qs[KT * PQ];
+    // double-buffered P/Q chunks (one barrier per step) when both fit the 64 KB static LDS
+    constexpr bool DB = (BM + BN) <= 192;
+    constexpr int NBUF = DB ? 2 : 1;
+    __shared__ __attribute__((aligned(16))) float Psm[NBUF * KT * PP];
+    __shared__ __attribute__((aligned(16))) float Qsm[NBUF * KT * PQ];
+    float* Ps = Psm;
+    float* Qs = Qsm;
     const hyres_wgrad_desc& d = a.d;
     const int tid = threadIdx.x;
     // XCD-aware order: hardware block b runs on XCD b % 8; give each XCD a contiguous logical range
@@ -818,39 +823,96 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgradArgs a) {
         load_p(kc_begin);
         load_q(t0);
     }
-    for (int kc = kc_begin; kc < kc_end; ++kc) {
-        static_for<NT>([&](auto J) {
-            constexpr int j = decltype(J)::value;
-            __syncthreads();
-            if (j == 0) store_p();
+    if constexpr (DB) {
+        // prologue: first step's operands in buffer 0; then per step: prefetch the next step's operands
+        // into registers, MFMAs on the current buffers, store the prefetch into the other buffers, ONE barrier
+        if (kc_begin < kc_end) {
+            store_p();
             store_q();
-            __syncthreads();
-            if (j == 0 && do_bias && tid < BM) {
+        }
+        __syncthreads();
+        int pcur = 0, qcur = 0;
+        for (int kc = kc_begin; kc < kc_end; ++kc) {
+            static_for<NT>([&](auto J) {
+                constexpr int j = decltype(J)::value;
+                Ps = Psm + pcur * (KT * PP);
+                Qs = Qsm + qcur * (KT * PQ);
+                const bool next_tap = j + 1 < NT;
+                const bool next_chunk = !next_tap && kc + 1 < kc_end;
+                if (next_tap) {
+                    load_q(t0 + j + 1);
+                } else if (next_chunk) {
+                    step_rows();
+                    load_p(kc + 1);
+                    load_q(t0);
+                }
+                if (j == 0 && do_bias && tid < BM) {
 #pragma unroll 8
-                for (int k = 0; k < KT; ++k) bsum += Ps[k * PP + tid];
-            }
-            if (j + 1 < NT) {
-                load_q(t0 + j + 1);
-            } else if (kc + 1 < kc_end) {
-                step_rows();
-                load_p(kc + 1);
-                load_q(t0);
-            }
+                    for (int k = 0; k < KT; ++k) bsum += Ps[k * PP + tid];
+                }
 #pragma unroll
-            for (int s = 0; s < KT / 2; ++s) {
-                const int k = lh * (KT / 2) + s;
-                float af[TM], bf[TN];
+                for (int s = 0; s < KT / 2; ++s) {
+                    const int k = lh * (KT / 2) + s;
+                    float af[TM], bf[TN];
 #pragma unroll
-                for (int tm = 0; tm < TM; ++tm) af[tm] = Ps[k * PP + wm * TM * 32 + tm * 32 + lr];
+                    for (int tm = 0; tm < TM; ++tm) af[tm] = Ps[k * PP + wm * TM * 32 + tm * 32 + lr];
 #pragma unroll
-                for (int tn = 0; tn < TN; ++tn) bf[tn] = Qs[k * PQ + wn * TN * 32 + tn * 32 + lr];
+                    for (int tn = 0; tn < TN; ++tn) bf[tn] = Qs[k * PQ + wn * TN * 32 + tn * 32 + lr];
 #pragma unroll
-                for (int tm = 0; tm < TM; ++tm)
+                    for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
-                    for (int tn = 0; tn < TN; ++tn)
-                        acc[j][tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[tm], bf[tn], acc[j][tm][tn], 0, 0, 0);
-            }
-        });
+                        for (int tn = 0; tn < TN; ++tn)
+                            acc[j][tm][tn] =
+                                __builtin_amdgcn_mfma_f32_32x32x2f32(af[tm], bf[tn], acc[j][tm][tn], 0, 0, 0);
+                }
+                if (next_tap || next_chunk) {
+                    Qs = Qsm + (qcur ^ 1) * (KT * PQ);
+                    store_q();
+                    if (next_chunk) {
+                        Ps = Psm + (pcur ^ 1) * (KT * PP);
+                        store_p();
+                    }
+                }
+                __syncthreads();
+                qcur ^= 1;
+                if (!next_tap) pcur ^= 1;
+            });
+        }
+    } else {
+        for (int kc = kc_begin; kc < kc_end; ++kc) {
+            static_for<NT>([&](auto J) {
+                constexpr int j = decltype(J)::value;
+                __syncthreads();
+                if (j == 0) store_p();
+                store_q();
+                __syncthreads();
+                if (j == 0 && do_bias && tid < BM) {
+    #pragma unroll 8
+                    for (int k = 0; k < KT; ++k) bsum += Ps[k * PP + tid];
+                }
+                if (j + 1 < NT) {
+                    load_q(t0 + j + 1);
+                } else if (kc + 1 < kc_end) {
+                    step_rows();
+                    load_p(kc + 1);
+                    load_q(t0);
+                }
+    #pragma unroll
+                for (int s = 0; s < KT / 2; ++s) {
+                    const int k = lh * (KT / 2) + s;
+                    float af[TM], bf[TN];
+    #pragma unroll
+                    for (int tm = 0; tm < TM; ++tm) af[tm] = Ps[k * PP + wm * TM * 32 + tm * 32 + lr];
+    #pragma unroll
+                    for (int tn = 0; tn < TN; ++tn) bf[tn] = Qs[k * PQ + wn * TN * 32 + tn * 32 + lr];
+    #pragma unroll
+                    for (int tm = 0; tm < TM; ++tm)
+    #pragma unroll
+                        for (int tn = 0; tn < TN; ++tn)
+                            acc[j][tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[tm], bf[tn], acc[j][tm][tn], 0, 0, 0);
+                }
+            });
+        }
     }
     if (do_bias && tid < BM && m0 + tid < d.M) a.bias_slab[(long long)split * d.M + m0 + tid] = bsum;
     // slab store [split][t][M][N]
