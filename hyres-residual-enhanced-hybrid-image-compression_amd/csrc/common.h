@@ -27,6 +27,8 @@ inline int ceil_div(long long a, long long b) { return (int)((a + b - 1) / b); }
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
 
 }  // namespace hyres

@@ -37,7 +37,6 @@ struct ConvArgs {
     int w_bytes; // bytes of W2 (buffer-resource range)
 };
 
-__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 
 struct EpiChannel {
     float bias, slope;
@@ -938,12 +937,12 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgradArgs a) {
 }
 
 // deterministic split-K reduce: 16 float4 lanes x 16 split groups per block (64 outputs per block)
-__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* slab, int nsplit, int ntaps, int M, int N,
-                                                           float* dst, int sm, int sn, int st, int accumulate) {
+__device__ __forceinline__ void wgrad_reduce_body(int blk, const float* slab, int nsplit, int ntaps, int M, int N,
+                                                  float* dst, int sm, int sn, int st, int accumulate) {
     __shared__ float red[16][65];
     const long long total = (long long)ntaps * M * N;
     const int lx = threadIdx.x & 15, ly = threadIdx.x >> 4;
-    const long long base = (long long)blockIdx.x * 64 + 4 * lx;
+    const long long base = (long long)blk * 64 + 4 * lx;
     float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
     if ((total & 3) == 0) {
         if (base < total)
@@ -967,7 +966,7 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* slab, in
     red[ly][4 * lx + 3] = s.w;
     __syncthreads();
     if (threadIdx.x < 64) {
-        const long long idx = (long long)blockIdx.x * 64 + threadIdx.x;
+        const long long idx = (long long)blk * 64 + threadIdx.x;
         if (idx < total) {
             float v = 0.f;
 #pragma unroll
@@ -980,6 +979,21 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* slab, in
             *p = accumulate ? (*p + v) : v;
         }
     }
+}
+
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* slab, int nsplit, int ntaps, int M, int N,
+                                                           float* dst, int sm, int sn, int st, int accumulate) {
+    wgrad_reduce_body(blockIdx.x, slab, nsplit, ntaps, M, N, dst, sm, sn, st, accumulate);
+}
+
+// weight-gradient slab reduce and the bias-gradient partials ([nsplit][M]) in one launch
+__global__ __launch_bounds__(256) void wgrad_bias_reduce_kernel(const float* slab, int nsplit, int ntaps, int M, int N,
+                                                                float* dst, int sm, int sn, int st, int accumulate,
+                                                                int nb_w, const float* bslab, float* dbias) {
+    if ((int)blockIdx.x < nb_w)
+        wgrad_reduce_body(blockIdx.x, slab, nsplit, ntaps, M, N, dst, sm, sn, st, accumulate);
+    else
+        wgrad_reduce_body(blockIdx.x - nb_w, bslab, nsplit, 1, M, 1, dbias, 1, 0, 0, accumulate);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1016,17 +1030,26 @@ struct PrepDesc {
     long long begin, count;
 };
 
-// one grid over the concatenated outputs of n descriptors; a block finds its descriptor by binary search
+// grid (chunks, n descriptors): blockIdx.y picks the descriptor (block-uniform: its fields are scalar
+// loads), blocks stride over its outputs with 32-bit index math
 __global__ __launch_bounds__(256) void weight_prep_batch_kernel(const PrepDesc* d, int n, long long total) {
-    for (long long idx = blockIdx.x * 256LL + threadIdx.x; idx < total; idx += (long long)gridDim.x * 256) {
-        int lo = 0, hi = n - 1;
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (d[mid].begin <= idx) lo = mid; else hi = mid - 1;
+    const PrepArgs& a = d[blockIdx.y].a;
+    const int count = (int)d[blockIdx.y].count;
+    const int tc = a.ntaps * a.cols;
+    for (int idx = blockIdx.x * 256 + threadIdx.x; idx < count; idx += gridDim.x * 256) {
+        const int r = idx / tc;
+        const int rem = idx - r * tc;
+        const int t = rem / a.cols;
+        const int c = rem - t * a.cols;
+        const int kh = a.kh[t], kw = a.kw[t];
+        int src;
+        switch (a.mode) {
+            case HYRES_WPREP_CONV: src = ((r * a.Ci + c) * a.KH + kh) * a.KW + kw; break;
+            case HYRES_WPREP_CONV_DGRAD: src = ((c * a.Ci + r) * a.KH + kh) * a.KW + kw; break;
+            case HYRES_WPREP_DECONV: src = ((c * a.Co + r) * a.KH + kh) * a.KW + kw; break;
+            default: src = ((r * a.Co + c) * a.KH + kh) * a.KW + kw; break;
         }
-        const PrepDesc& e = d[lo];
-        const long long k = idx - e.begin;
-        if (k < e.count) e.a.w2[k] = prep_value(e.a, k);
+        a.w2[idx] = a.w[src];
     }
 }
 
@@ -1308,15 +1331,15 @@ int hyres_prep_desc_fill(void* desc, const hyres_conv_geom* g, const float* w, f
     }
     d.begin = begin;
     d.count = (long long)a.rows * a.ntaps * a.cols;
+    HY_REQUIRE(d.count < (1LL << 31), HYRES_E_SHAPE, "prep_desc: weight too large");
     *count = d.count;
     memcpy(desc, &d, sizeof(d));
     return ok();
 }
 
 int hyres_conv_weight_prep_batch(const void* descs, int n, long long total, hyres_stream_t s) {
-    HY_REQUIRE(descs && n > 0 && total > 0, HYRES_E_ARG, "prep_batch: empty");
-    const int blocks = (int)std::min<long long>((total + 255) / 256, 8192);
-    hipLaunchKernelGGL(weight_prep_batch_kernel, dim3(blocks), dim3(256), 0, as_stream(s), (const PrepDesc*)descs, n,
+    HY_REQUIRE(descs && n > 0 && n <= 65535 && total > 0, HYRES_E_ARG, "prep_batch: bad size");
+    hipLaunchKernelGGL(weight_prep_batch_kernel, dim3(64, n), dim3(256), 0, as_stream(s), (const PrepDesc*)descs, n,
                        total);
     return HY_LAUNCH_CHECK("weight_prep_batch_kernel");
 }
@@ -1581,6 +1604,13 @@ int hyres_conv_wgrad(const hyres_wgrad_desc* d0, const float* pp, const float* q
     int rc = HY_LAUNCH_CHECK("wgrad_kernel");
     if (rc) return rc;
     const long long total = (long long)d->ntaps * d->M * d->N;
+    if (dbias && !swap) {  // [nsplit][M] bias partials reduced by the same launch
+        const int nb_w = ceil_div(total, 64);
+        hipLaunchKernelGGL(wgrad_bias_reduce_kernel, dim3(nb_w + ceil_div(d->M, 64)), dim3(256), 0, st,
+                           (const float*)ws, p.nsplit, d->ntaps, d->M, d->N, dst, d->sm, d->sn, d->st, d->accumulate,
+                           nb_w, (const float*)bias_ws, dbias);
+        return HY_LAUNCH_CHECK("wgrad_bias_reduce_kernel");
+    }
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(ceil_div(total, 64)), dim3(256), 0, st, (const float*)ws, p.nsplit,
                        d->ntaps, d->M, d->N, dst, d->sm, d->sn, d->st, d->accumulate);
     rc = HY_LAUNCH_CHECK("wgrad_reduce_kernel");

@@ -24,43 +24,45 @@ __device__ __forceinline__ void src_index(float scale, int o, int in, int& i0, i
     l0 = 1.0f - l1;
 }
 
-// VEC channels per thread (4: float4 when C, ld % 4 == 0 and 16B-aligned pointers)
+// VEC channels per thread (4: float4 when C, ld % 4 == 0 and 16B-aligned pointers). One block row per
+// output row (blockIdx.y = b*Ho + oh: the vertical stencil is block-uniform), threads over (ow, channel
+// group) with 32-bit index math.
 template <int VEC>
-__global__ void bilinear_fwd_kernel(const float* x, int ldx, float* y, int ldy, int B, int Hi, int Wi, int Ho,
-                                    int Wo, int C, float sh, float sw, int acc) {
+__global__ __launch_bounds__(256) void bilinear_fwd_kernel(const float* x, int ldx, float* y, int ldy, int B, int Hi,
+                                                           int Wi, int Ho, int Wo, int C, float sh, float sw, int acc) {
     const int CG = C / VEC;
-    const long long n = (long long)B * Ho * Wo * CG;
-    GRID_STRIDE(i, n) {
-        const int c = (int)(i % CG) * VEC;
-        const long long p = i / CG;
-        const int ow = (int)(p % Wo);
-        const int oh = (int)((p / Wo) % Ho);
-        const int b = (int)(p / ((long long)Wo * Ho));
-        int h0, h1, w0, w1;
-        float lh0, lh1, lw0, lw1;
-        src_index(sh, oh, Hi, h0, h1, lh0, lh1);
+    const int row = blockIdx.y;
+    const int b = row / Ho, oh = row - b * Ho;
+    int h0, h1;
+    float lh0, lh1;
+    src_index(sh, oh, Hi, h0, h1, lh0, lh1);
+    const float* x0 = x + ((long long)b * Hi + h0) * Wi * ldx;
+    const float* x1 = x + ((long long)b * Hi + h1) * Wi * ldx;
+    float* yr = y + (long long)row * Wo * ldy;
+    const int n = Wo * CG;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+        const int ow = i / CG;
+        const int c = (i - ow * CG) * VEC;
+        int w0, w1;
+        float lw0, lw1;
         src_index(sw, ow, Wi, w0, w1, lw0, lw1);
-        const float* xb = x + (long long)b * Hi * Wi * ldx + c;
-        const float* p00 = xb + ((long long)h0 * Wi + w0) * ldx;
-        const float* p01 = xb + ((long long)h0 * Wi + w1) * ldx;
-        const float* p10 = xb + ((long long)h1 * Wi + w0) * ldx;
-        const float* p11 = xb + ((long long)h1 * Wi + w1) * ldx;
-        float* yp = y + p * ldy + c;
+        float* yp = yr + (long long)ow * ldy + c;
         if constexpr (VEC == 4) {
-            const float4 a = *reinterpret_cast<const float4*>(p00), bq = *reinterpret_cast<const float4*>(p01);
-            const float4 cq = *reinterpret_cast<const float4*>(p10), d = *reinterpret_cast<const float4*>(p11);
+            const float4 a = ld4(x0 + w0 * ldx + c), bq = ld4(x0 + w1 * ldx + c);
+            const float4 cq = ld4(x1 + w0 * ldx + c), d = ld4(x1 + w1 * ldx + c);
             float4 v;
             v.x = lh0 * (lw0 * a.x + lw1 * bq.x) + lh1 * (lw0 * cq.x + lw1 * d.x);
             v.y = lh0 * (lw0 * a.y + lw1 * bq.y) + lh1 * (lw0 * cq.y + lw1 * d.y);
             v.z = lh0 * (lw0 * a.z + lw1 * bq.z) + lh1 * (lw0 * cq.z + lw1 * d.z);
             v.w = lh0 * (lw0 * a.w + lw1 * bq.w) + lh1 * (lw0 * cq.w + lw1 * d.w);
             if (acc) {
-                const float4 o = *reinterpret_cast<const float4*>(yp);
+                const float4 o = ld4(yp);
                 v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
             }
             *reinterpret_cast<float4*>(yp) = v;
         } else {
-            const float v = lh0 * (lw0 * p00[0] + lw1 * p01[0]) + lh1 * (lw0 * p10[0] + lw1 * p11[0]);
+            const float v = lh0 * (lw0 * x0[w0 * ldx + c] + lw1 * x0[w1 * ldx + c]) +
+                            lh1 * (lw0 * x1[w0 * ldx + c] + lw1 * x1[w1 * ldx + c]);
             *yp = acc ? *yp + v : v;
         }
     }
@@ -77,39 +79,46 @@ __device__ __forceinline__ float bw_weight(float scale, int o, int in, int targe
     return w;
 }
 
+__device__ __forceinline__ void bw_range(float inv, int t, int in, int out, int& lo, int& hi) {
+    // outputs o with src(o) in [t-1, t+1] : o in [(t-0.5)/s - 0.5, (t+1.5)/s - 0.5]
+    lo = max(0, (int)floorf(((float)t - 0.5f) * inv - 0.5f) - 1);
+    hi = min(out - 1, (int)ceilf(((float)t + 1.5f) * inv - 0.5f) + 1);
+    if (t == 0) lo = 0;
+    if (t == in - 1) hi = out - 1;
+}
+
+// one block row per input row (blockIdx.y = b*Hi + h): the vertical output range and weights are
+// block-uniform; threads over (w, channel group)
 template <int VEC>
-__global__ void bilinear_bwd_kernel(const float* gy, int ldgy, float* gx, int ldgx, int B, int Hi, int Wi, int Ho,
-                                    int Wo, int C, float sh, float sw, int acc) {
+__global__ __launch_bounds__(256) void bilinear_bwd_kernel(const float* gy, int ldgy, float* gx, int ldgx, int B,
+                                                           int Hi, int Wi, int Ho, int Wo, int C, float sh, float sw,
+                                                           int acc) {
     const int CG = C / VEC;
-    const long long n = (long long)B * Hi * Wi * CG;
-    const float ish = 1.0f / sh, isw = 1.0f / sw;
-    GRID_STRIDE(i, n) {
-        const int c = (int)(i % CG) * VEC;
-        const long long p = i / CG;
-        const int w = (int)(p % Wi);
-        const int h = (int)((p / Wi) % Hi);
-        const int b = (int)(p / ((long long)Wi * Hi));
-        // outputs o with src(o) in [t-1, t+1] : o in [(t-0.5)/s - 0.5, (t+1.5)/s - 0.5]
-        int oh_lo = max(0, (int)floorf(((float)h - 0.5f) * ish - 0.5f) - 1);
-        int oh_hi = min(Ho - 1, (int)ceilf(((float)h + 1.5f) * ish - 0.5f) + 1);
-        int ow_lo = max(0, (int)floorf(((float)w - 0.5f) * isw - 0.5f) - 1);
-        int ow_hi = min(Wo - 1, (int)ceilf(((float)w + 1.5f) * isw - 0.5f) + 1);
-        if (h == 0) oh_lo = 0;
-        if (w == 0) ow_lo = 0;
-        if (h == Hi - 1) oh_hi = Ho - 1;
-        if (w == Wi - 1) ow_hi = Wo - 1;
+    const int row = blockIdx.y;
+    const int b = row / Hi, h = row - b * Hi;
+    int oh_lo, oh_hi;
+    bw_range(1.0f / sh, h, Hi, Ho, oh_lo, oh_hi);
+    const float isw = 1.0f / sw;
+    const float* gb = gy + (long long)b * Ho * Wo * ldgy;
+    float* gr = gx + (long long)row * Wi * ldgx;
+    const int n = Wi * CG;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+        const int w = i / CG;
+        const int c = (i - w * CG) * VEC;
+        int ow_lo, ow_hi;
+        bw_range(isw, w, Wi, Wo, ow_lo, ow_hi);
         float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-        const float* gb = gy + (long long)b * Ho * Wo * ldgy + c;
         for (int oh = oh_lo; oh <= oh_hi; ++oh) {
             const float wh = bw_weight(sh, oh, Hi, h);
             if (wh == 0.f) continue;
             float4 rs = make_float4(0.f, 0.f, 0.f, 0.f);
+            const float* gq = gb + (long long)oh * Wo * ldgy + c;
             for (int ow = ow_lo; ow <= ow_hi; ++ow) {
                 const float ww = bw_weight(sw, ow, Wi, w);
                 if (ww == 0.f) continue;
-                const float* q = gb + ((long long)oh * Wo + ow) * ldgy;
+                const float* q = gq + ow * ldgy;
                 if constexpr (VEC == 4) {
-                    const float4 v = *reinterpret_cast<const float4*>(q);
+                    const float4 v = ld4(q);
                     rs.x += ww * v.x; rs.y += ww * v.y; rs.z += ww * v.z; rs.w += ww * v.w;
                 } else {
                     rs.x += ww * q[0];
@@ -117,10 +126,10 @@ __global__ void bilinear_bwd_kernel(const float* gy, int ldgy, float* gx, int ld
             }
             s.x += wh * rs.x; s.y += wh * rs.y; s.z += wh * rs.z; s.w += wh * rs.w;
         }
-        float* gp = gx + p * ldgx + c;
+        float* gp = gr + (long long)w * ldgx + c;
         if constexpr (VEC == 4) {
             if (acc) {
-                const float4 o = *reinterpret_cast<const float4*>(gp);
+                const float4 o = ld4(gp);
                 s.x += o.x; s.y += o.y; s.z += o.z; s.w += o.w;
             }
             *reinterpret_cast<float4*>(gp) = s;
@@ -453,26 +462,28 @@ int hyres_bilinear_fwd(const float* x, int ldx, float* y, int ldy, int B, int Hi
                        float scale_h, float scale_w, int accumulate, hyres_stream_t s) {
     HY_REQUIRE(x && y && Hi > 0 && Wi > 0 && Ho > 0 && Wo > 0, HYRES_E_ARG, "bilinear_fwd: bad args");
     const bool vec = C % 4 == 0 && ldx % 4 == 0 && ldy % 4 == 0 && aligned16(x) && aligned16(y);
-    long long n = (long long)B * Ho * Wo * (vec ? C / 4 : C);
+    HY_REQUIRE((long long)B * Ho <= 65535 && (long long)Wo * C < (1LL << 30), HYRES_E_SHAPE, "bilinear_fwd: too large");
+    const dim3 grid(ceil_div((long long)Wo * (vec ? C / 4 : C), 256), B * Ho);
     if (vec)
-        hipLaunchKernelGGL(bilinear_fwd_kernel<4>, dim3(grid_for_r(n)), dim3(256), 0, as_stream(s), x, ldx, y, ldy, B,
-                           Hi, Wi, Ho, Wo, C, scale_h, scale_w, accumulate);
+        hipLaunchKernelGGL(bilinear_fwd_kernel<4>, grid, dim3(256), 0, as_stream(s), x, ldx, y, ldy, B, Hi, Wi, Ho, Wo,
+                           C, scale_h, scale_w, accumulate);
     else
-        hipLaunchKernelGGL(bilinear_fwd_kernel<1>, dim3(grid_for_r(n)), dim3(256), 0, as_stream(s), x, ldx, y, ldy, B,
-                           Hi, Wi, Ho, Wo, C, scale_h, scale_w, accumulate);
+        hipLaunchKernelGGL(bilinear_fwd_kernel<1>, grid, dim3(256), 0, as_stream(s), x, ldx, y, ldy, B, Hi, Wi, Ho, Wo,
+                           C, scale_h, scale_w, accumulate);
     return HY_LAUNCH_CHECK("bilinear_fwd");
 }
 int hyres_bilinear_bwd(const float* gy, int ldgy, float* gx, int ldgx, int B, int Hi, int Wi, int Ho, int Wo, int C,
                        float scale_h, float scale_w, int accumulate, hyres_stream_t s) {
     HY_REQUIRE(gy && gx, HYRES_E_ARG, "bilinear_bwd: NULL");
     const bool vec = C % 4 == 0 && ldgy % 4 == 0 && ldgx % 4 == 0 && aligned16(gy) && aligned16(gx);
-    long long n = (long long)B * Hi * Wi * (vec ? C / 4 : C);
+    HY_REQUIRE((long long)B * Hi <= 65535 && (long long)Wi * C < (1LL << 30), HYRES_E_SHAPE, "bilinear_bwd: too large");
+    const dim3 grid(ceil_div((long long)Wi * (vec ? C / 4 : C), 256), B * Hi);
     if (vec)
-        hipLaunchKernelGGL(bilinear_bwd_kernel<4>, dim3(grid_for_r(n)), dim3(256), 0, as_stream(s), gy, ldgy, gx, ldgx,
-                           B, Hi, Wi, Ho, Wo, C, scale_h, scale_w, accumulate);
+        hipLaunchKernelGGL(bilinear_bwd_kernel<4>, grid, dim3(256), 0, as_stream(s), gy, ldgy, gx, ldgx, B, Hi, Wi, Ho,
+                           Wo, C, scale_h, scale_w, accumulate);
     else
-        hipLaunchKernelGGL(bilinear_bwd_kernel<1>, dim3(grid_for_r(n)), dim3(256), 0, as_stream(s), gy, ldgy, gx, ldgx,
-                           B, Hi, Wi, Ho, Wo, C, scale_h, scale_w, accumulate);
+        hipLaunchKernelGGL(bilinear_bwd_kernel<1>, grid, dim3(256), 0, as_stream(s), gy, ldgy, gx, ldgx, B, Hi, Wi, Ho,
+                           Wo, C, scale_h, scale_w, accumulate);
     return HY_LAUNCH_CHECK("bilinear_bwd");
 }
 
