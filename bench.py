@@ -130,8 +130,42 @@ def eval_legs(net, x, jpeg, jpeg_bpp, args, reps=20):
         npx = xe.shape[0] * xe.shape[2] * xe.shape[3]
         res[tag] = {"ms": round(ms, 3), "mpix_s": round(npx / ms / 1e3, 3), "eager_ms": round(ems, 3)}
         del cap
+    res["analysis_synthesis_bs%d" % x.shape[0]] = analysis_synthesis(net, x, reps)
     net.train()
     return res
+
+
+def analysis_synthesis(net, x, reps):
+    """North-star target (BASELINE.json): the N=128/M=192 analysis + synthesis pass (g_a on the residual,
+    g_s on y_hat; models/checkerboard.py:35-58) at bs=16 256x256, forward, as a HIP graph. Fraction of the
+    HBM roofline = SURVEY §8d ledger bytes (1.836 GB per image: g_a 0.918 + g_s 0.918) / t / 8 TB/s;
+    FLOP rate from the same ledger (40.66 GFLOP per image)."""
+    from hyres_hip import ops as O
+    rm = net.residual_model
+    B, _, H, W = x.shape
+    with torch.no_grad():
+        xn = O.to_nhwc(x - 0.5, rg=False)
+        yh = O.Node.new(B, H // 8, W // 8, rm.M, x.device, rg=False)
+        yh.v.copy_(torch.randn(yh.v.shape, generator=torch.Generator().manual_seed(3)).to(x.device))
+        for _ in range(2):
+            rm.g_a.hip(None, xn)
+            rm.g_s.hip(None, yh)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            rm.g_a.hip(None, xn)
+            rm.g_s.hip(None, yh)
+        torch.cuda.synchronize()
+        t0 = time.time()
+        for _ in range(reps):
+            g.replay()
+        torch.cuda.synchronize()
+        ms = (time.time() - t0) * 1000 / reps
+    ledger = B * 1.836e9
+    return {"ms": round(ms, 3), "ledger_bytes": ledger, "hbm_frac": round(ledger / (ms * 1e-3) / 8e12, 4),
+            "tflops": round(B * 40.66e9 / (ms * 1e-3) / 1e12, 2),
+            "mfma_fp32_frac": round(B * 40.66e9 / (ms * 1e-3) / 1e12 / MI355X_FP32_PEAK_TFLOPS, 4),
+            "target": "north_star: >= 0.40 of the HBM roofline, i.e. <= 9.2 ms at bs=16"}
 
 
 def main():
