@@ -130,6 +130,21 @@ def eval_legs(net, x, jpeg, jpeg_bpp, args, reps=20):
         npx = xe.shape[0] * xe.shape[2] * xe.shape[3]
         res[tag] = {"ms": round(ms, 3), "mpix_s": round(npx / ms / 1e3, 3), "eager_ms": round(ems, 3)}
         del cap
+    # configs[4] precision: inference under torch.autocast(float16) -> fp16-operand f16 MFMA convs
+    with torch.autocast("cuda", dtype=torch.float16):
+        for tag, xe, je, be in (("kodak_1x768x512_autocast_f16", xk.to(dev), jk.to(dev), bk),
+                                ("bs%d_%dx%d_autocast_f16" % (x.shape[0], x.shape[2], x.shape[3]), x, jpeg,
+                                 jpeg_bpp)):
+            cap = CapturedStep(net, xe, je, be)
+            torch.cuda.synchronize()
+            t0 = time.time()
+            for _ in range(reps):
+                cap.replay()
+            torch.cuda.synchronize()
+            ms = (time.time() - t0) * 1000 / reps
+            npx = xe.shape[0] * xe.shape[2] * xe.shape[3]
+            res[tag] = {"ms": round(ms, 3), "mpix_s": round(npx / ms / 1e3, 3)}
+            del cap
     res["analysis_synthesis_bs%d" % x.shape[0]] = analysis_synthesis(net, x, reps)
     net.train()
     return res

@@ -150,15 +150,21 @@ __device__ __forceinline__ void epi_store4(const hyres_epilogue& e, float* y, in
     st4(yp, make_float4(o[0], o[1], o[2], o[3]));
 }
 
-template <int TM, int TN, int WAVES_M, int WAVES_N, int MODE, bool SPLITK>
+template <int TM, int TN, int WAVES_M, int WAVES_N, int MODE, bool SPLITK, bool F16 = false>
 __global__ __launch_bounds__(256) void conv_fwd_kernel(const ConvArgs a) {
     // MODE 0: Ci % 32 == 0 (float4 loads); 1: same + square A (GDN); 2: generic scalar (small Ci).
+    // F16: operands rounded to fp16 when staged into LDS ([row][32 halves], pitch PADH halves) and
+    // consumed by v_mfma_f32_32x32x16_f16 (lane r,h holds row r, k = 8h..8h+7), fp32 accumulation.
+    static_assert(!F16 || MODE != 2, "fp16 operands on the Ci % 32 == 0 paths only");
+    constexpr int PADH = 40;
     constexpr int BM = 32 * TM * WAVES_M;
     constexpr int BN = 32 * TN * WAVES_N;
     constexpr int SMEM = ((BM + BN) * PADK > BM * (32 * WAVES_N + 8)) ? (BM + BN) * PADK : BM * (32 * WAVES_N + 8);
     __shared__ __attribute__((aligned(16))) float smem[SMEM];
     float* const As = smem;
     float* const Bs = smem + BM * PADK;
+    _Float16* const Ah = reinterpret_cast<_Float16*>(smem);
+    _Float16* const Bh = Ah + BM * PADH;
 
     const hyres_conv_geom& g = a.g;
     const int tid = threadIdx.x;
@@ -267,7 +273,19 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const ConvArgs a) {
         }
     };
     auto store_chunk = [&]() {
-        if constexpr (MODE != 2) {
+        if constexpr (F16) {
+            typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+            for (int q = 0; q < A_V; ++q) {
+                const half4 h = {(_Float16)ra[q].x, (_Float16)ra[q].y, (_Float16)ra[q].z, (_Float16)ra[q].w};
+                *reinterpret_cast<half4*>(&Ah[(tid / 8 + 32 * q) * PADH + 4 * c4]) = h;
+            }
+#pragma unroll
+            for (int q = 0; q < B_V; ++q) {
+                const half4 h = {(_Float16)rb[q].x, (_Float16)rb[q].y, (_Float16)rb[q].z, (_Float16)rb[q].w};
+                *reinterpret_cast<half4*>(&Bh[(tid / 8 + 32 * q) * PADH + 4 * c4]) = h;
+            }
+        } else if constexpr (MODE != 2) {
 #pragma unroll
             for (int q = 0; q < A_V; ++q)
                 *reinterpret_cast<float4*>(&As[(tid / 8 + 32 * q) * PADK + 4 * c4]) = ra[q];
@@ -313,6 +331,27 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const ConvArgs a) {
         store_chunk();
         __syncthreads();
         if (kc + 1 < kend) load_chunk(kc + 1);
+        if constexpr (F16) {
+            typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+#pragma unroll
+            for (int s16 = 0; s16 < 2; ++s16) {
+                half8 af[TM], bf[TN];
+#pragma unroll
+                for (int tm = 0; tm < TM; ++tm)
+                    af[tm] = *reinterpret_cast<const half8*>(
+                        &Ah[(wm * TM * 32 + tm * 32 + lr) * PADH + 16 * s16 + 8 * lh]);
+#pragma unroll
+                for (int tn = 0; tn < TN; ++tn)
+                    bf[tn] = *reinterpret_cast<const half8*>(
+                        &Bh[(wn * TN * 32 + tn * 32 + lr) * PADH + 16 * s16 + 8 * lh]);
+#pragma unroll
+                for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                    for (int tn = 0; tn < TN; ++tn)
+                        acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[tm], bf[tn], acc[tm][tn], 0, 0, 0);
+            }
+            continue;
+        }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             float4 af[TM], bf[TN];
@@ -1146,6 +1185,16 @@ template <int TM, int TN, int WM_, int WN_>
 static int launch_fwd(const ConvArgs& a, int mode, hipStream_t st) {
     constexpr int BM = 32 * TM * WM_, BN = 32 * TN * WN_;
     dim3 grid(ceil_div(a.M, BM), ceil_div(a.g.Co, BN), a.g.nphase * a.nsplit);
+    if (a.e.f16_operands && mode != 2) {
+        if (a.nsplit > 1) {
+            if (mode == 0) hipLaunchKernelGGL((conv_fwd_kernel<TM, TN, WM_, WN_, 0, true, true>), grid, dim3(256), 0, st, a);
+            else hipLaunchKernelGGL((conv_fwd_kernel<TM, TN, WM_, WN_, 1, true, true>), grid, dim3(256), 0, st, a);
+        } else {
+            if (mode == 0) hipLaunchKernelGGL((conv_fwd_kernel<TM, TN, WM_, WN_, 0, false, true>), grid, dim3(256), 0, st, a);
+            else hipLaunchKernelGGL((conv_fwd_kernel<TM, TN, WM_, WN_, 1, false, true>), grid, dim3(256), 0, st, a);
+        }
+        return HY_LAUNCH_CHECK("conv_fwd_kernel(f16)");
+    }
     // split-K launches are a separate instantiation (partials to the slab, no epilogue)
     if (a.nsplit > 1) {
         if (mode == 0) hipLaunchKernelGGL((conv_fwd_kernel<TM, TN, WM_, WN_, 0, true>), grid, dim3(256), 0, st, a);

@@ -40,7 +40,7 @@ class Epilogue(ctypes.Structure):
                 ("aux0", ctypes.c_void_p), ("ld0", ctypes.c_int),
                 ("aux1", ctypes.c_void_p), ("ld1", ctypes.c_int),
                 ("aux2", ctypes.c_void_p), ("ld2", ctypes.c_int),
-                ("out2", ctypes.c_void_p), ("ldo2", ctypes.c_int)]
+                ("out2", ctypes.c_void_p), ("ldo2", ctypes.c_int), ("f16_operands", ctypes.c_int)]
 
 
 class WgradDesc(ctypes.Structure):

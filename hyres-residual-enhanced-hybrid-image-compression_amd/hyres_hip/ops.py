@@ -479,6 +479,13 @@ def conv_bytes(g: L.ConvGeom, e: L.Epilogue) -> float:
     return b
 
 
+def f16_convs() -> bool:
+    """Inference under ``torch.autocast("cuda", dtype=torch.float16)`` (the reference's AMP path,
+    src/utils/engine.py / BASELINE configs[4]): forward convolutions without a tape take fp16 operands on
+    the f16 MFMA (fp32 accumulation, fp32 activations in HBM); training and input-gradients stay fp32."""
+    return torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.float16
+
+
 def _launch_conv(g: L.ConvGeom, x_ptr: int, w2: torch.Tensor, ldw: int, y_ptr: int, e: L.Epilogue) -> None:
     nb = L.load().hyres_conv_workspace_bytes(ctypes.byref(g))  # > 0 iff the launch is split-K
     timed = KernelTimer.enabled
@@ -630,6 +637,7 @@ def conv2d(tape: Optional[Tape], x: Node, weight: torch.Tensor, bias: Optional[t
             pre = _empty((B, Ho, Wo, Co), x.device)
             e.out2 = pre.data_ptr()
             e.ldo2 = Co
+    e.f16_operands = int(tape is None and f16_convs())
     _launch_conv(g, x.ptr(), w2, ldw, y.ptr(), e)
     y.relu_out = act == L.ACT_RELU
     if tape is None:
@@ -685,6 +693,7 @@ def deconv2d(tape: Optional[Tape], x: Node, weight: torch.Tensor, bias: Optional
     e.kind = L.EPI_BIAS
     e.act = act
     e.bias = L.ptr(bias)
+    e.f16_operands = int(tape is None and f16_convs())
     _launch_conv(g, x.ptr(), w2, g.ntaps * Ci, y.ptr(), e)
     y.relu_out = act == L.ACT_RELU
     if tape is None:
@@ -739,6 +748,7 @@ def gdn(tape: Optional[Tape], x: Node, beta: torch.Tensor, gamma: torch.Tensor, 
     e.ld0 = x.ld
     e.out2 = nrm.data_ptr()
     e.ldo2 = C
+    e.f16_operands = int(tape is None and f16_convs())
     _launch_conv(g, x.ptr(), gp, C, y.ptr(), e)
     if tape is None:
         return y

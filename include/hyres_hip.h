@@ -112,6 +112,9 @@ typedef struct hyres_epilogue {
     const float* aux1; int ld1;
     const float* aux2; int ld2;
     float* out2; int ldo2;
+    int f16_operands;             /* 1: X and W2 rounded to fp16 in the LDS staging, v_mfma_f32_32x32x16_f16
+                                   * with fp32 accumulation and fp32 epilogue (autocast-fp16 inference,
+                                   * BASELINE configs[4]); ignored on the small-Ci and narrow paths */
 } hyres_epilogue;
 
 /* Y = conv(X, W2) with the epilogue — nn.Conv2d / nn.ConvTranspose2d / GDN forward and their

@@ -529,7 +529,7 @@ def test_c3_bs32_eval_gc_path_parity():
 
 def test_c5_kodak_size_eval_parity():
     """BASELINE config C5 shape: one 768x512 image (Kodak size, W != H; latents 96x64 / 24x16), eval,
-    MultiScaleRefine on the HIP path (fp32 activations: fp16 is out of scope)."""
+    MultiScaleRefine on the HIP path, fp32 (the fp16-operand variant: test_c5_fp16_autocast_eval)."""
     net, _ = _hip_model()
     net.eval()
     g = torch.Generator().manual_seed(7)
@@ -544,6 +544,63 @@ def test_c5_kodak_size_eval_parity():
     assert out["likelihoods"]["y"].shape == (1, 192, 64, 96)
     assert out["likelihoods"]["z"].shape == (1, 128, 16, 24)
     _check_against_oracle(out, [0], x, jpeg, float(jpeg_bpp))
+
+
+@pytest.mark.parametrize("case", [(2, 64, 64, 16, 16, 3, 1, 1, 1), (2, 128, 192, 16, 16, 5, 2, 2, 1),
+                                  (2, 192, 96, 8, 8, 1, 1, 0, 1), (2, 96, 96, 8, 8, 3, 1, 1, 1)])
+def test_conv2d_fp16_operands(case):
+    """Forward conv under torch.autocast(float16), no tape: fp16-rounded operands on the f16 MFMA with fp32
+    accumulation == torch fp32 conv of the fp16-rounded operands (2e-6: only the summation order
+    differs), and within 4e-3 of the fp32 conv (operand rounding 2^-11)."""
+    from hyres_hip import ops as O
+    B, Ci, Co, H, W, K, s, p, d = case
+    x = _rand((B, Ci, H, W), 11)
+    w = _rand((Co, Ci, K, K), 12, 1.0 / (Ci * K * K) ** 0.5)
+    b = _rand((Co,), 13, 0.1)
+    y32 = F.conv2d(x, w, b, stride=s, padding=p, dilation=d)
+    yh = F.conv2d(x.half().float(), w.half().float(), b, stride=s, padding=p, dilation=d)
+    D = dev()
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.float16):
+        yn = O.conv2d(None, O.to_nhwc(x.to(D)), w.to(D), b.to(D), stride=s, pad=p, dil=d)
+        y = O.to_nchw(yn).cpu()
+    assert y.dtype == torch.float32
+    assert rel_err(y, yh) < 2e-6
+    assert rel_err(y, y32) < 4e-3
+
+
+def test_c5_fp16_autocast_eval():
+    """BASELINE configs[4]: Kodak-size inference under torch.autocast("cuda", float16) — forward convs take
+    fp16 operands on v_mfma_f32_32x32x16_f16 (fp32 accumulation and activations). No fp16 golden exists
+    (the reference's AMP path needs CUDA): parity is unpinned against the reference's fp16 run and checked
+    against this build's fp32 path, which is pinned to the reference fixtures. Tolerances (fp16 operands,
+    2^-11 relative rounding, which also flips a few round() decisions of y_hat, each perturbing a local
+    window of x_hat): PSNR within 0.05 dB, bpp within 1 %, mean |x_hat diff| < 1e-2 (measured 6.7e-3)."""
+    import math
+    net, _ = _hip_model()
+    net.eval()
+    g = torch.Generator().manual_seed(7)
+    base = F.interpolate(torch.rand(1, 3, 16, 24, generator=g), size=(512, 768), mode="bilinear",
+                         align_corners=False)
+    x = ((base * 0.8 + 0.2 * torch.rand(1, 3, 512, 768, generator=g)) * 255).floor() / 255
+    jpeg, jpeg_bpp = net.jpeg(x)
+    with torch.no_grad():
+        o32 = net(x, jpeg=(jpeg, jpeg_bpp))
+        with torch.autocast("cuda", dtype=torch.float16):
+            o16 = net(x, jpeg=(jpeg, jpeg_bpp))
+    torch.cuda.synchronize()
+    assert o16["x_hat"].dtype == torch.float32 and o16["likelihoods"]["y"].shape == (1, 192, 64, 96)
+    assert not torch.equal(o16["x_hat"], o32["x_hat"]), "fp16 operand path did not engage"
+    xd = x.to(o32["x_hat"].device)
+
+    def psnr(a):
+        return 10 * math.log10(1.0 / float(F.mse_loss(a, xd)))
+
+    def bits(o):
+        return sum(float((-torch.log2(v)).sum()) for v in o["likelihoods"].values())
+
+    assert abs(psnr(o16["x_hat"]) - psnr(o32["x_hat"])) < 0.05
+    assert abs(bits(o16) - bits(o32)) < 0.01 * bits(o32)
+    assert float((o16["x_hat"] - o32["x_hat"]).abs().mean()) < 1e-2
 
 
 # ------------------------------------------------------------------------------------------------ graphs
