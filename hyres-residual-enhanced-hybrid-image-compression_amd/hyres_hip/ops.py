@@ -461,7 +461,8 @@ def conv_variant(g: L.ConvGeom, e: L.Epilogue, splitk: bool) -> str:
     """The conv_fwd_kernel<TM, TN, WAVES_M, WAVES_N, MODE, SPLITK> hyres_conv_forward launches."""
     tile = "2, 2, 2, 2" if g.Co > 64 else ("2, 1, 2, 2" if g.Co > 32 else "1, 1, 4, 1")
     mode = (1 if e.square_input else 0) if g.Ci % 32 == 0 else 2
-    return f"conv_fwd_kernel<{tile}, {mode}, {'true' if splitk else 'false'}>"
+    f16 = "true" if (e.f16_operands and mode != 2) else "false"
+    return f"conv_fwd_kernel<{tile}, {mode}, {'true' if splitk else 'false'}, {f16}>"
 
 
 def conv_flops(g: L.ConvGeom) -> float:

@@ -5,7 +5,7 @@ set -o pipefail
 tag=${1:-r1}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
-BENCH="bench.py --steps 5 --warmup 2 --no-cpu-baseline"
+BENCH="bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-eval"
 scripts/gpu_run.sh \
   "bench_full:420:python3 bench.py" \
   "stats:400:rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${tag}_stats -o run -- python3 $BENCH" \
@@ -14,7 +14,7 @@ scripts/gpu_run.sh \
 rc=$?
 [ $rc -ne 0 ] && exit $rc
 python3 scripts/pmc_traffic.py gpurun_out/${tag}_pmc_fetch gpurun_out/${tag}_pmc_write \
-  --kernel "conv_fwd_kernel<2, 1, 2, 2, 0, false>" --out gpurun_out/${tag}_pmc_traffic.json \
+  --kernel "conv_fwd_kernel<2, 1, 2, 2, 0, false, false>" --out gpurun_out/${tag}_pmc_traffic.json \
   --command "rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE --kernel-trace --output-format csv -- python3 $BENCH" \
   > gpurun_out/pmc_traffic.log 2>&1 && \
-python3 scripts/prof_summary.py gpurun_out/${tag}_stats/run_kernel_stats.csv 7 > gpurun_out/${tag}_summary.txt
+python3 scripts/prof_summary.py gpurun_out/${tag}_stats/run_kernel_stats.csv 10 > gpurun_out/${tag}_summary.txt
