@@ -277,6 +277,17 @@ def main():
     step(eager=True)
     torch.cuda.synchronize()
     O.KernelTimer.enabled = False
+    ks = O.KernelTimer.summary()
+    # the same kernel without the concurrent branches' contention (branch and side streams off):
+    # its intrinsic rate, reported next to the live one
+    O.KernelTimer.reset()
+    O.KernelTimer.enabled = True
+    O.BranchStreams.enabled = O.SideStream.enabled = False
+    step(eager=True)
+    torch.cuda.synchronize()
+    O.BranchStreams.enabled = O.SideStream.enabled = True
+    O.KernelTimer.enabled = False
+    ks_iso = O.KernelTimer.summary()
     if dist:
         t = torch.tensor([elapsed], device=dev)
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
@@ -284,8 +295,10 @@ def main():
     ms = elapsed * 1000 / args.steps
     value = world * B * S * S * args.steps / elapsed / 1e6
 
-    ks = O.KernelTimer.summary()
     achieved = ks["flops"] / (ks["total_ms"] * 1e-3) / 1e12 if ks["total_ms"] > 0 else 0.0
+    iso = None
+    if ks_iso["kernel"] == ks["kernel"] and ks_iso["total_ms"] > 0:
+        iso = ks_iso["flops"] / (ks_iso["total_ms"] * 1e-3) / 1e12
 
 
     if rank != 0:
@@ -322,6 +335,9 @@ def main():
                      "flops_per_launch": ks["flops_per_launch"],
                      "algorithmic_bytes_per_launch": ks["bytes_per_launch"],
                      "timing": "HIP events around each launch of one eager step after the timed region",
+                     "achieved_isolated": None if iso is None else round(iso, 3),
+                     "frac_isolated": None if iso is None else round(iso / MI355X_FP32_PEAK_TFLOPS, 4),
+                     "avg_launch_us_isolated": round(ks_iso["avg_us"], 2),
                      "ms_by_variant": ks.get("by_variant_ms")},
         "graph": graphed is not None,
         "eval": evals,

@@ -14,6 +14,7 @@
 // Weight gradients use a second kernel (P^T Q over pixels, split-K slabs + deterministic reduce).
 #include "common.h"
 
+#include <cstdlib>
 #include <cstring>
 #include <utility>
 
@@ -1393,6 +1394,11 @@ int hyres_conv_weight_prep_batch(const void* descs, int n, long long total, hyre
     return HY_LAUNCH_CHECK("weight_prep_batch_kernel");
 }
 
+static int env_int(const char* name, int dflt) {
+    const char* e = getenv(name);
+    return (e && *e) ? atoi(e) : dflt;
+}
+
 struct ConvPlan {
     int BM, BN, nsplit, cps;
 };
@@ -1408,10 +1414,12 @@ static ConvPlan conv_plan(const hyres_conv_geom* g) {
     const int nk = (g->Ci % KT == 0) ? maxtap * (g->Ci / KT) : ceil_div((long long)maxtap * g->Ci, KT);
     p.nsplit = 1;
     p.cps = nk;
-    if (blocks < 512 && nk >= 8) {
-        // split K so that ~512 blocks are in flight, at least 4 chunks per split
-        int want = (int)std::min<long long>(ceil_div(512, blocks), 64);
-        int ns = std::max(1, std::min(want, nk / 4));
+    static const int sb = env_int("HYRES_CONV_SPLIT_BLOCKS", 512);
+    static const int sc = env_int("HYRES_CONV_SPLIT_MINCHUNKS", 4);
+    if (blocks < sb && nk >= 2 * sc) {
+        // split K so that ~sb blocks are in flight, at least sc chunks per split
+        int want = (int)std::min<long long>(ceil_div(sb, blocks), 64);
+        int ns = std::max(1, std::min(want, nk / sc));
         p.cps = ceil_div(nk, ns);
         p.nsplit = ceil_div(nk, p.cps);
     }
@@ -1542,6 +1550,7 @@ int hyres_wgrad_desc_deconv2d(hyres_wgrad_desc* d, int B, int H, int W, int Ci, 
 
 namespace hyres {
 
+
 struct WgradPlan {
     int TMc, TNc, WMc, WNc, NT, BM, BN, mtiles, ntiles, ngroups, nchunks, nsplit, cps, tapn, nblocks;
 };
@@ -1568,10 +1577,15 @@ static WgradPlan wgrad_plan(const hyres_wgrad_desc* d) {
     const long long Q = (long long)d->B * d->Hq * d->Wq;
     p.nchunks = ceil_div(Q, KT);
     const long long tiles = (long long)p.mtiles * p.ntiles * p.ngroups;
-    // ~1024 blocks, >= 8 chunks (256 pixels) per split, <= 512 splits
-    const long long want = std::max<long long>(1, (1024 + tiles - 1) / tiles);
-    const long long maxsplit = std::max<long long>(1, p.nchunks / 8);
-    p.nsplit = (int)std::min<long long>(std::min<long long>(want, maxsplit), 512);
+    // ~2048 blocks (swept on MI355X: 1024 -> 2048 is -0.6 % step time; fewer splits hurt), >= 8 chunks
+    // (256 pixels) per split, <= 512 splits (tunable: HYRES_WGRAD_BLOCKS,
+    // HYRES_WGRAD_MINCHUNKS, HYRES_WGRAD_MAXSPLIT)
+    static const int tb = env_int("HYRES_WGRAD_BLOCKS", 2048);
+    static const int mc = env_int("HYRES_WGRAD_MINCHUNKS", 8);
+    static const int ms = env_int("HYRES_WGRAD_MAXSPLIT", 512);
+    const long long want = std::max<long long>(1, (tb + tiles - 1) / tiles);
+    const long long maxsplit = std::max<long long>(1, p.nchunks / mc);
+    p.nsplit = (int)std::min<long long>(std::min<long long>(want, maxsplit), ms);
     p.cps = ceil_div(p.nchunks, p.nsplit);
     p.nsplit = ceil_div(p.nchunks, p.cps);
     p.nblocks = (int)(tiles * p.nsplit);
