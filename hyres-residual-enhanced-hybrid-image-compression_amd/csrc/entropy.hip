@@ -413,6 +413,80 @@ __global__ void eb_aux_kernel(const float* packed, const float* quantiles, const
 
 }  // namespace hyres
 
+namespace hyres {
+
+// ---------------------------------------------------------------- entropy-coding symbolisation
+// (compress/decompress). Symbols and CDF indexes are produced in NCHW order per image —
+// compressai's per-image string order (symbols[i].reshape(-1)) — from the NHWC activations.
+__device__ __forceinline__ bool ckbd_keep(int parity, int h, int w) {
+    return parity < 0 || (((h + w) & 1) == parity);
+}
+
+// GaussianConditional: sym = round(y*keep - mean) (compressai quantize "symbols"), idx = build_indexes(
+// max(scale, 0.11)) = (nt-1) - #{k < nt-1 : scale <= table[k]}.  y == NULL: indexes only.
+__global__ void gc_symbols_kernel(const float* y, int ldy, const float* params, int ldp, int M, int B, int H, int W,
+                                  int parity, const float* table, int nt, int* sym, int* idx) {
+    const long long n = (long long)B * M * H * W;
+    GRID_STRIDE(i, n) {
+        const int w = (int)(i % W);
+        const long long r = i / W;
+        const int h = (int)(r % H);
+        const long long r2 = r / H;
+        const int c = (int)(r2 % M);
+        const int b = (int)(r2 / M);
+        const long long pix = ((long long)b * H + h) * W + w;
+        const float scale = fmaxf(params[pix * ldp + c], 0.11f);
+        int k = nt - 1;
+        for (int t = 0; t < nt - 1; ++t) k -= (scale <= table[t]) ? 1 : 0;
+        idx[i] = k;
+        if (y) {
+            const float mean = params[pix * ldp + M + c];
+            const float yv = ckbd_keep(parity, h, w) ? y[pix * ldy + c] : 0.f;
+            sym[i] = (int)rintf(yv - mean);
+        }
+    }
+}
+
+// y_hat (+)= sym + mean (compressai dequantize), NHWC out
+__global__ void gc_dequant_kernel(const int* sym, const float* params, int ldp, int M, int B, int H, int W,
+                                  float* out, int ldo, int acc) {
+    const long long n = (long long)B * M * H * W;
+    GRID_STRIDE(i, n) {
+        const int w = (int)(i % W);
+        const long long r = i / W;
+        const int h = (int)(r % H);
+        const long long r2 = r / H;
+        const int c = (int)(r2 % M);
+        const int b = (int)(r2 / M);
+        const long long pix = ((long long)b * H + h) * W + w;
+        const float v = (float)sym[i] + params[pix * ldp + M + c];
+        float* o = out + pix * ldo + c;
+        *o = acc ? *o + v : v;
+    }
+}
+
+// EntropyBottleneck: sym = round(z - median_c) (dequant: sym + median_c), NCHW symbols, NHWC tensors
+__global__ void eb_symbols_kernel(const float* z, int ldz, const float* med, int B, int H, int W, int C, int* sym,
+                                  float* zhat, int ldo, int dequant) {
+    const long long n = (long long)B * C * H * W;
+    GRID_STRIDE(i, n) {
+        const int w = (int)(i % W);
+        const long long r = i / W;
+        const int h = (int)(r % H);
+        const long long r2 = r / H;
+        const int c = (int)(r2 % C);
+        const int b = (int)(r2 / C);
+        const long long pix = ((long long)b * H + h) * W + w;
+        if (dequant) {
+            zhat[pix * ldo + c] = (float)sym[i] + med[c];
+        } else {
+            sym[i] = (int)rintf(z[pix * ldz + c] - med[c]);
+        }
+    }
+}
+
+}  // namespace hyres
+
 using namespace hyres;
 
 extern "C" {
@@ -517,6 +591,34 @@ int hyres_eb_aux_loss(const float* packed, const float* quantiles, const float* 
     hipLaunchKernelGGL(eb_aux_kernel, dim3(1), dim3(512), 0, as_stream(s), packed, quantiles, target, loss,
                        g_quantiles, C);
     return HY_LAUNCH_CHECK("eb_aux_loss");
+}
+
+
+int hyres_gc_symbols(const float* y, int ldy, const float* params, int ldp, int M, int B, int H, int W, int parity,
+                     const float* scale_table, int nt, int* sym, int* idx, hyres_stream_t s) {
+    HY_REQUIRE(params && scale_table && idx && nt >= 1 && (!y || sym), HYRES_E_ARG, "gc_symbols: bad args");
+    const long long n = (long long)B * M * H * W;
+    hipLaunchKernelGGL(gc_symbols_kernel, dim3(grid_for_e(n)), dim3(256), 0, as_stream(s), y, ldy, params, ldp, M, B,
+                       H, W, parity, scale_table, nt, sym, idx);
+    return HY_LAUNCH_CHECK("gc_symbols");
+}
+
+int hyres_gc_dequant(const int* sym, const float* params, int ldp, int M, int B, int H, int W, float* out, int ldo,
+                     int accumulate, hyres_stream_t s) {
+    HY_REQUIRE(sym && params && out, HYRES_E_ARG, "gc_dequant: NULL");
+    const long long n = (long long)B * M * H * W;
+    hipLaunchKernelGGL(gc_dequant_kernel, dim3(grid_for_e(n)), dim3(256), 0, as_stream(s), sym, params, ldp, M, B, H,
+                       W, out, ldo, accumulate);
+    return HY_LAUNCH_CHECK("gc_dequant");
+}
+
+int hyres_eb_symbols(const float* z, int ldz, const float* medians, int B, int H, int W, int C, int* sym,
+                     float* zhat, int ldo, int dequant, hyres_stream_t s) {
+    HY_REQUIRE(medians && sym && (dequant ? zhat != nullptr : z != nullptr), HYRES_E_ARG, "eb_symbols: NULL");
+    const long long n = (long long)B * C * H * W;
+    hipLaunchKernelGGL(eb_symbols_kernel, dim3(grid_for_e(n)), dim3(256), 0, as_stream(s), z, ldz, medians, B, H, W, C,
+                       sym, zhat, ldo, dequant);
+    return HY_LAUNCH_CHECK("eb_symbols");
 }
 
 }  // extern "C"

@@ -102,6 +102,12 @@ _SIGS = {
     "hyres_uniform_noise": (_I, [_P, _LL, _ULL, _ULL, _P]),
     "hyres_uniform_noise_dev": (_I, [_P, _LL, _P, _ULL, _P]),
     "hyres_quantize": (_I, [_P, _I, _P, _LL, _P]),
+    "hyres_gc_symbols": (_I, [_P, _I, _P, _I, _I, _I, _I, _I, _I, _P, _I, _P, _P, _P]),
+    "hyres_gc_dequant": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _I, _I, _P]),
+    "hyres_eb_symbols": (_I, [_P, _I, _P, _I, _I, _I, _I, _P, _P, _I, _I, _P]),
+    "hyres_pmf_to_quantized_cdf": (_I, [_P, _I, _I, _P]),
+    "hyres_rans_encode_with_indexes": (_I, [_P, _P, _LL, _P, _I, _P, _P, _I, _P, _LL, ctypes.POINTER(_LL)]),
+    "hyres_rans_decode_with_indexes": (_I, [_P, _LL, _P, _LL, _P, _I, _P, _P, _I, _P]),
     "hyres_ckbd_anchor_fwd": (_I, [_P, _P, _I, _P, _P, _I, _I, _I, _I, _P]),
     "hyres_ckbd_nonanchor_gc_fwd": (_I, [_P, _P, _P, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P,
                                          _I, _I, _I, _I, _P]),

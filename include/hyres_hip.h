@@ -321,6 +321,35 @@ int hyres_adam_step(float* param, const float* grad, float* exp_avg, float* exp_
                     float lr, float beta1, float beta2, float eps, int step, const float* sumsq,
                     float max_norm, hyres_stream_t s);
 
+/* ------------------------------------------------------------------------------------------ */
+/* entropy coding (compress / decompress): compressai 1.2.6 semantics            */
+/* ------------------------------------------------------------------------------------------ */
+/* GaussianConditional.build_indexes(scales) + quantize(y, "symbols", means) of one checkerboard pass
+ * (models/checkerboard.py:159-161): params NHWC [B,H,W,ldp] with scales in channels [0,M) and means in
+ * [M,2M); y NHWC masked by parity (0 anchor, 1 non-anchor, -1 none); sym/idx int32 NCHW. y == NULL:
+ * indexes only (decoder side). */
+int hyres_gc_symbols(const float* y, int ldy, const float* params, int ldp, int M, int B, int H, int W, int parity,
+                     const float* scale_table, int nt, int* sym, int* idx, hyres_stream_t s);
+/* GaussianConditional.decompress's dequantize: out[NHWC] (+)= sym + means (checkerboard.py:162-164) */
+int hyres_gc_dequant(const int* sym, const float* params, int ldp, int M, int B, int H, int W, float* out, int ldo,
+                     int accumulate, hyres_stream_t s);
+/* EntropyBottleneck.compress/decompress symbolisation around the channel medians (checkerboard.py:170-171):
+ * dequant = 0: sym = round(z - med); 1: zhat = sym + med */
+int hyres_eb_symbols(const float* z, int ldz, const float* medians, int B, int H, int W, int C, int* sym,
+                     float* zhat, int ldo, int dequant, hyres_stream_t s);
+/* compressai pmf_to_quantized_cdf (cpp_exts/ops/ops.cpp): n probabilities -> n+1 CDF entries summing to
+ * 2^precision with every symbol frequency >= 1 (host) */
+int hyres_pmf_to_quantized_cdf(const float* pmf, int n, int precision, int* cdf_out);
+/* compressai RansEncoder.encode_with_indexes / RansDecoder.decode_with_indexes (cpp_exts/rans): 64-bit
+ * rANS, 16-bit CDFs [ncdf][cdf_stride], bypass escape for out-of-range symbols (host). out == NULL:
+ * *out_len = the string length only. */
+int hyres_rans_encode_with_indexes(const int* symbols, const int* indexes, long long n, const int* cdfs,
+                                   int cdf_stride, const int* cdf_sizes, const int* offsets, int ncdf,
+                                   unsigned char* out, long long out_cap, long long* out_len);
+int hyres_rans_decode_with_indexes(const unsigned char* in, long long in_len, const int* indexes, long long n,
+                                   const int* cdfs, int cdf_stride, const int* cdf_sizes, const int* offsets,
+                                   int ncdf, int* symbols_out);
+
 #ifdef __cplusplus
 }
 #endif

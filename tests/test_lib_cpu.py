@@ -56,3 +56,70 @@ def test_product_path_has_no_oracle_imports():
                 if re.search(r"^\s*(from|import)\s+oracle", txt, flags=re.M):
                     offenders.append(os.path.join(root, f))
     assert not offenders, offenders
+
+
+# ------------------------------------------------------------------ entropy coding (host side of f1)
+def _cdf_call(pmf):
+    import ctypes
+    import numpy as np
+    from hyres_hip import _lib as L
+    p = np.ascontiguousarray(pmf, dtype=np.float32)
+    out = np.zeros(len(p) + 1, dtype=np.int32)
+    L.check(L.load().hyres_pmf_to_quantized_cdf(p.ctypes.data, len(p), 16, out.ctypes.data), "cdf")
+    return out.tolist()
+
+
+def test_pmf_to_quantized_cdf_matches_restatement():
+    """hyres_pmf_to_quantized_cdf == compressai's pmf_to_quantized_cdf (oracle/entropy_coding.py), incl.
+    zero-probability symbols that must steal a frequency unit; the result is a valid 16-bit CDF."""
+    import numpy as np
+    from oracle.entropy_coding import gc_tables, pmf_to_quantized_cdf
+    rng = np.random.default_rng(5)
+    cases = [rng.random(n).astype(np.float32) for n in (2, 7, 40)]
+    cases.append(np.array([0.5, 0.0, 0.0, 0.5, 1e-9], np.float32))
+    z = rng.random(30).astype(np.float32)
+    z[::3] = 0
+    cases.append(z)
+    for p in cases:
+        p = p / p.sum()
+        got = _cdf_call(p)
+        assert got == pmf_to_quantized_cdf(p)
+        assert got[0] == 0 and got[-1] == 65536 and all(b > a for a, b in zip(got, got[1:]))
+    cdf, lengths, offsets = gc_tables([0.11, 1.0, 17.3, 256.0])
+    assert list(lengths) == [2 * (-o) + 3 for o in offsets] and cdf[:, 0].tolist() == [0] * 4
+
+
+def test_rans_roundtrip_and_bitstream_matches_restatement():
+    """hyres_rans_encode/decode_with_indexes: decode(encode(s)) == s, including symbols outside every CDF's
+    range (bypass escape), and the byte string equals the rans64 restatement's."""
+    import ctypes
+    import numpy as np
+    from hyres_hip import _lib as L
+    from oracle.entropy_coding import gc_tables, rans_decode, rans_encode
+    lib = L.load()
+    cdf, lengths, offsets = gc_tables(np.exp(np.linspace(np.log(0.11), np.log(256), 64)).astype(np.float32))
+    rng = np.random.default_rng(11)
+    n = 3000
+    idx = rng.integers(0, 64, n).astype(np.int32)
+    sym = np.round(rng.normal(0, 1, n) * np.exp(np.linspace(np.log(0.11), np.log(256), 64))[idx]).astype(np.int32)
+    sym[::97] = np.int32(5000)   # far outside: bypass
+    sym[5::131] = np.int32(-777)
+    cdf = np.ascontiguousarray(cdf, np.int32)
+    lengths = np.ascontiguousarray(lengths, np.int32)
+    offsets = np.ascontiguousarray(offsets, np.int32)
+    ln = ctypes.c_longlong(0)
+    L.check(lib.hyres_rans_encode_with_indexes(sym.ctypes.data, idx.ctypes.data, n, cdf.ctypes.data, cdf.shape[1],
+                                               lengths.ctypes.data, offsets.ctypes.data, 64, None, 0,
+                                               ctypes.byref(ln)), "enc")
+    buf = np.zeros(ln.value, np.uint8)
+    L.check(lib.hyres_rans_encode_with_indexes(sym.ctypes.data, idx.ctypes.data, n, cdf.ctypes.data, cdf.shape[1],
+                                               lengths.ctypes.data, offsets.ctypes.data, 64, buf.ctypes.data,
+                                               buf.size, ctypes.byref(ln)), "enc")
+    ref = rans_encode(sym.tolist(), idx.tolist(), cdf.tolist(), lengths.tolist(), offsets.tolist())
+    assert buf.tobytes() == ref
+    dec = np.zeros(n, np.int32)
+    L.check(lib.hyres_rans_decode_with_indexes(buf.ctypes.data, buf.size, idx.ctypes.data, n, cdf.ctypes.data,
+                                               cdf.shape[1], lengths.ctypes.data, offsets.ctypes.data, 64,
+                                               dec.ctypes.data), "dec")
+    assert np.array_equal(dec, sym)
+    assert rans_decode(ref, idx.tolist(), cdf.tolist(), lengths.tolist(), offsets.tolist()) == sym.tolist()
