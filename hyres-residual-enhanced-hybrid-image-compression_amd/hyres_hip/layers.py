@@ -246,6 +246,11 @@ class EntropyBottleneck(EntropyModel):
     def hip(self, tape, z: Node, training: bool, noisequant: bool, noise: E.NoiseSource):
         return E.entropy_bottleneck(tape, self, z, training, noisequant, noise)
 
+    def update(self, force: bool = False) -> bool:
+        """compressai EntropyBottleneck.update: quantized CDF tables for rANS coding."""
+        from . import entropy_coding as EC
+        return EC.eb_update(self, force=force)
+
 
 class GaussianConditional(EntropyModel):
     """compressai GaussianConditional(scale_table) — buffers only; the likelihood is fused into the
@@ -262,9 +267,12 @@ class GaussianConditional(EntropyModel):
         self.lower_bound_scale = LowerBound(scale_bound)
 
     def update_scale_table(self, scale_table, force: bool = False) -> bool:
+        """compressai GaussianConditional.update_scale_table (+ update): CDF tables per scale."""
         if self._offset.numel() > 0 and not force:
             return False
+        from . import entropy_coding as EC
         self.scale_table = torch.Tensor(tuple(float(s) for s in scale_table)).to(self.scale_bound.device)
+        EC.gc_update(self)
         return True
 
 
@@ -284,5 +292,15 @@ class CompressionModel(nn.Module):
         return out
 
     def update(self, scale_table=None, force=False):
-        """CDF tables for rANS coding are out of scope for this build."""
-        return False
+        """compressai CompressionModel.update: CDF tables of every EntropyBottleneck and
+        GaussianConditional (rANS coding for compress/decompress)."""
+        from . import entropy_coding as EC
+        if scale_table is None:
+            scale_table = EC.get_scale_table()
+        updated = False
+        for _, module in self.named_modules():
+            if isinstance(module, EntropyBottleneck):
+                updated |= module.update(force=force)
+            if isinstance(module, GaussianConditional):
+                updated |= module.update_scale_table(scale_table, force=force)
+        return updated

@@ -11,11 +11,14 @@ the first 2M input channels of param_aggregation.0 (the zero half contributes no
 from __future__ import annotations
 
 import math
+import time
 from typing import Optional
 
 import torch
 import torch.nn as nn
 
+from hyres_hip import _lib as L
+from hyres_hip import entropy_coding as EC
 from hyres_hip import entropy_ops as E
 from hyres_hip import ops as O
 from hyres_hip import runtime
@@ -35,6 +38,10 @@ def get_scale_table(min=SCALES_MIN, max=SCALES_MAX, levels=SCALES_LEVELS):
 
 
 class LightWeightCheckerboard(CompressionModel):
+    # True: obtain z_hat / y_anchor_hat inside compress by decoding the just-written strings, literally as
+    # the reference does; False (default): dequantise the encoded symbols on the device (identical values)
+    decode_in_compress = False
+
     def __init__(self, N=128, M=192):
         super().__init__()
         self.N, self.M = N, M
@@ -105,18 +112,87 @@ class LightWeightCheckerboard(CompressionModel):
         keep = anchor if mode == "anchor" else ~anchor
         return x * keep.to(x.dtype)
 
-    def compress(self, x):
-        raise NotImplementedError("rANS entropy coding (compress/decompress) is out of scope for this build: "
-                                  "SURVEY.md §8f row f1")
+    # ------------------------------------------------------------------ entropy coding (§8f f1)
+    def _hyper(self, z_hat: Node, H: int, W: int):
+        """h_s(z_hat) into cat-buffer [latent | ctx] and the anchor parameters (checkerboard.py:172-180)."""
+        M = self.M
+        lc = Node.new(z_hat.B, H, W, 4 * M, z_hat.device, rg=False)
+        latent = lc.slice(0, 2 * M)
+        self.h_s.hip(None, z_hat, out=latent)
+        params_a = self.param_aggregation.hip(None, latent)  # cat([latent, 0]): zero half skipped
+        return lc, params_a
 
+    @torch.no_grad()
+    def compress(self, x):
+        """models/checkerboard.py:167-201: strings [[anchor, non_anchor], z] (one string per image each).
+        The reference decodes its own anchor / z strings to obtain y_anchor_hat / z_hat; the symbols round
+        trip exactly, so here they are dequantised on the device from the encoded symbols instead."""
+        start_time = time.time()
+        dev = next(self.parameters()).device
+        M = self.M
+        gc, eb = self.gaussian_conditional, self.entropy_bottleneck
+        xn = O.to_nhwc(x.to(dev).float().contiguous(), rg=False)
+        y = self.g_a.hip(None, xn)
+        z = self.h_a.hip(None, y)
+        z_strings = EC.eb_compress(eb, z)
+        z_hat = EC.eb_decompress(eb, z_strings, z.H, z.W, dev) if self.decode_in_compress else None
+        if z_hat is None:
+            z_hat = Node.new(z.B, z.H, z.W, z.C, dev, rg=False)
+            sym = torch.empty(z.B * z.C * z.H * z.W, dtype=torch.int32, device=dev)
+            L.call("hyres_eb_symbols", z.ptr(), z.ld, EC._medians(eb).data_ptr(), z.B, z.H, z.W, z.C, sym.data_ptr(),
+                   None, 0, 0, L.stream())
+            L.call("hyres_eb_symbols", None, 0, EC._medians(eb).data_ptr(), z.B, z.H, z.W, z.C, sym.data_ptr(),
+                   z_hat.ptr(), z_hat.ld, 1, L.stream())
+        lc, params_a = self._hyper(z_hat, y.H, y.W)
+        anchor_strings = EC.gc_compress(gc, y, params_a, M, parity=0)
+        ya_hat = Node.new(y.B, y.H, y.W, M, dev, rg=False)
+        if self.decode_in_compress:
+            EC.gc_decompress(gc, anchor_strings, params_a, M, ya_hat)
+        else:
+            sym, _ = EC._gc_indexes(gc, params_a, M, y, 0)
+            L.call("hyres_gc_dequant", sym.data_ptr(), params_a.ptr(), params_a.ld, M, y.B, y.H, y.W, ya_hat.ptr(),
+                   ya_hat.ld, 0, L.stream())
+        self.context_prediction.hip(None, ya_hat, out=lc.slice(2 * M, 4 * M))
+        params_na = self.param_aggregation.hip(None, lc)
+        non_anchor_strings = EC.gc_compress(gc, y, params_na, M, parity=1)
+        return {
+            "strings": [[anchor_strings, non_anchor_strings], z_strings],
+            "shape": torch.Size([z.H, z.W]),
+            "time": time.time() - start_time,
+        }
+
+    @torch.no_grad()
     def decompress(self, strings, shape):
-        raise NotImplementedError("rANS entropy coding (compress/decompress) is out of scope for this build: "
-                                  "SURVEY.md §8f row f1")
+        """models/checkerboard.py:203-240 (including its ``g_s(y_hat).clamp_(0, 1)``)."""
+        start_time = time.time()
+        dev = next(self.parameters()).device
+        M = self.M
+        gc, eb = self.gaussian_conditional, self.entropy_bottleneck
+        h, w = int(shape[0]), int(shape[1])
+        z_hat = EC.eb_decompress(eb, strings[1], h, w, dev)
+        H, W = h * 4, w * 4
+        lc, params_a = self._hyper(z_hat, H, W)
+        y_hat = Node.new(z_hat.B, H, W, M, dev, rg=False)
+        EC.gc_decompress(gc, strings[0][0], params_a, M, y_hat)          # y_anchor_hat
+        self.context_prediction.hip(None, y_hat, out=lc.slice(2 * M, 4 * M))
+        params_na = self.param_aggregation.hip(None, lc)
+        EC.gc_decompress(gc, strings[0][1], params_na, M, y_hat, accumulate=True)  # + y_non_anchor_hat
+        x_hat = O.to_nchw(self.g_s.hip(None, y_hat)).clamp_(0, 1)
+        return {"x_hat": x_hat, "time": time.time() - start_time}
+
+    def inference(self, x):
+        """models/checkerboard.py:242-259."""
+        c = self.compress(x)
+        d = self.decompress(c["strings"], c["shape"])
+        return {"x_hat": d["x_hat"], "time": {"compression": c["time"], "decompression": d["time"],
+                                             "total": c["time"] + d["time"]}}
 
     def update(self, scale_table=None, force=False, **kwargs):
+        """models/checkerboard.py:261-267."""
         if scale_table is None:
             scale_table = get_scale_table()
         updated = self.gaussian_conditional.update_scale_table(scale_table, force=force)
+        updated |= super().update(force=force)
         return updated
 
     def load_state_dict(self, state_dict, strict: bool = True, **kwargs):

@@ -84,13 +84,29 @@ class ResidualJPEGCompression(CompressionModel):
         x_dev = x.to(device)
         return self.forward_device(x_dev, jpeg_decoded, float(jpeg_bpp), noisequant)
 
+    @torch.no_grad()
     def compress(self, x):
-        raise NotImplementedError("rANS entropy coding (compress/decompress) is out of scope for this build: "
-                                  "SURVEY.md §8f row f1")
+        """models/hyres.py:78-98: JPEG buffers (host) + the residual model's rANS strings."""
+        device = next(self.parameters()).device
+        x_cpu = x.detach().cpu() if x.device.type != "cpu" else x
+        jpeg_buffers = self.jpeg.compress(x_cpu)
+        jpeg_decoded = self.jpeg.decompress(jpeg_buffers, device)
+        residual = x.to(device) - jpeg_decoded
+        residual_compressed = self.residual_model.compress(residual)
+        residual_compressed["jpeg_buffers"] = jpeg_buffers
+        return residual_compressed
 
+    @torch.no_grad()
     def decompress(self, compressed_data):
-        raise NotImplementedError("rANS entropy coding (compress/decompress) is out of scope for this build: "
-                                  "SURVEY.md §8f row f1")
+        """models/hyres.py:100-131: JPEG decode + residual decode (clamped to [0, 1] by the reference's
+        LightWeightCheckerboard.decompress) + MultiScaleRefine + clamp."""
+        device = next(self.parameters()).device
+        jpeg_decoded = self.jpeg.decompress(compressed_data["jpeg_buffers"], device)
+        decompress_result = self.residual_model.decompress(compressed_data["strings"], compressed_data["shape"])
+        x_hat_initial = jpeg_decoded + decompress_result["x_hat"]
+        refined = self.refine(x_hat_initial)
+        decompress_result["x_hat"] = torch.clamp(x_hat_initial + refined, 0, 1)
+        return decompress_result
 
     def load_state_dict(self, state_dict, strict: bool = True, **kwargs):
         """models/hyres.py:136-167 with the refine-prefix bug fixed (keys are stripped per sub-module)."""

@@ -750,3 +750,49 @@ def test_batched_weight_relayout_matches_individual():
         back = net.forward_device(x, j, 0.0)["x_hat"]
     torch.cuda.synchronize()
     assert torch.equal(back, ref)
+
+
+# ------------------------------------------------------------------------------------------------ entropy coding
+def test_compress_decompress_roundtrip():
+    """update() -> compress -> decompress. The decoded residual equals the eval forward's
+    residual_hat (clamped as the reference's LightWeightCheckerboard.decompress does) to 1e-6 — the
+    checkerboard two-pass decode reproduces y_hat exactly — the final x_hat equals the reference formula on
+    it, the strings' length is in the range of the forward's ideal code length, and decoding inside compress
+    (the reference's literal order) writes the same strings. Bitstream parity with compressai itself is
+    unpinned (not installed); the coder is bit-exact to the restatement (tests/test_lib_cpu.py)."""
+    import math
+    g = load_npz("kodim01_crop64_eval.npz")
+    net, _ = _hip_model()
+    net.eval()
+    D = dev()
+    assert net.update(force=True)
+    rm = net.residual_model
+    assert rm.gaussian_conditional._quantized_cdf.shape[0] == 64 and rm.entropy_bottleneck._offset.numel() == 128
+    x = g["x"]
+    with torch.no_grad():
+        fwd = net(x)
+        c = net.compress(x)
+        d = net.decompress(c)
+        dres = rm.decompress(c["strings"], c["shape"])
+    torch.cuda.synchronize()
+    assert tuple(c["shape"]) == (x.shape[2] // 32, x.shape[3] // 32)
+    res_ref = fwd["residual_hat"].clamp(0, 1)
+    assert float((dres["x_hat"] - res_ref).abs().max()) <= 1e-6
+    x0 = fwd["jpeg_decoded"].to(D) + dres["x_hat"]
+    want = torch.clamp(x0 + net.refine(x0), 0, 1)
+    assert float((d["x_hat"] - want).abs().max()) <= 1e-6
+    nbytes = sum(len(s) for part in (c["strings"][0][0], c["strings"][0][1], c["strings"][1]) for s in part)
+    nstr = sum(len(part) for part in (c["strings"][0][0], c["strings"][0][1], c["strings"][1]))
+    ideal = sum(float((-torch.log2(v)).sum()) for v in fwd["likelihoods"].values()) / 8
+    # the reference codes BOTH checkerboard passes over all positions (anchor pass: y*mask_a with the anchor
+    # parameters, non-anchor pass likewise), while the forward's likelihood uses the combined y_hat with
+    # summed scales/means (models/checkerboard.py:136-142), so the two lengths agree only loosely
+    assert 0.5 * ideal <= nbytes <= 2.0 * ideal + 8 * nstr, (nbytes, ideal)
+    rm.decode_in_compress = True
+    try:
+        with torch.no_grad():
+            c2 = net.compress(x)
+    finally:
+        rm.decode_in_compress = False
+    assert c2["strings"] == c["strings"]
+    assert math.isfinite(c["time"]) and math.isfinite(d["time"])
