@@ -1,14 +1,9 @@
-"""Inference CLI (src/inference.py:18-253) — same flags; HIP forward path.
+"""Inference CLI (src/inference.py:18-253) — same flags; HIP forward path, rANS compress/decompress.
 
-The reference calls model.compress()/decompress() (rANS entropy coding, out of scope for this build —
-SURVEY.md §8f row f1).  This CLI runs the deterministic eval forward (the same quantisation decisions the
-coder would make) and reports
-  * y/z bpp as the ideal code length  -sum(log2 likelihood) / num_pixels  (what rANS approaches),
-  * JPEG bpp from the real JPEG bytes,
-  * PSNR = 10*log10(1/mse)  — the reference's formula at :123-125, ``-10*log10(mse*255^2)``, is wrong
-    (it would report a large negative number); fixed here and documented in DESIGN.md,
-  * enc/dec time = device forward time of the codec (synchronised), JPEG excluded, like the reference's
-    self-timers (checkerboard.py:169-239).
+Per image (as the reference, :53-150): ``model.compress(x)`` -> ``model.decompress(...)``; y/z bpp from
+the rANS string lengths, JPEG bpp from the real JPEG bytes, enc/dec time from the models' own timers.
+PSNR = 10*log10(1/mse) — the reference's formula at :123-125, ``-10*log10(mse*255^2)``, is wrong (it
+would report a large negative number); fixed here and documented in DESIGN.md.
 CSV columns are the reference's (:232-246)."""
 import argparse
 import csv
@@ -51,38 +46,42 @@ def _save(t, path):
 
 
 def process_image(model, img_path, output_dir, device, save_components=False):
+    """src/inference.py:53-150: compress -> decompress, bpp from the real strings (rANS + JPEG bytes)."""
     x = _load_image(img_path)
     H, W = x.shape[-2:]
     if H % 32 or W % 32:
         raise ValueError(f"{img_path}: H and W must be multiples of 32 (g_a /8 then h_a /4)")
     num_pixels = x.size(0) * H * W
-    with torch.no_grad():
-        jpeg_dec, jpeg_bpp = model.jpeg(x)
-        torch.cuda.synchronize()
-        t0 = time.time()
-        out = model(x, jpeg=(jpeg_dec, jpeg_bpp))
-        torch.cuda.synchronize()
-        t = time.time() - t0
-    y_bits = -torch.log2(out["likelihoods"]["y"].double()).sum().item()
-    z_bits = -torch.log2(out["likelihoods"]["z"].double()).sum().item()
-    y_bpp, z_bpp = y_bits / num_pixels, z_bits / num_pixels
-    total_bpp = jpeg_bpp + y_bpp + z_bpp
-    mse = torch.nn.functional.mse_loss(x.to(device), out["x_hat"]).item()
-    psnr = 10 * math.log10(1.0 / max(mse, 1e-12))
+    x = x.to(device)
+    out_enc = model.compress(x)
+    torch.cuda.synchronize()
+    enc_time = out_enc["time"]
+    out_dec = model.decompress(out_enc)
+    torch.cuda.synchronize()
+    dec_time = out_dec["time"]
     base, ext = os.path.splitext(os.path.basename(img_path))
-    _save(out["x_hat"], os.path.join(output_dir, f"{base}_recon{ext}"))
+    _save(out_dec["x_hat"], os.path.join(output_dir, f"{base}_recon{ext}"))
+    with torch.no_grad():
+        out_net = model(x)
     if save_components:
         _save(x, os.path.join(output_dir, f"{base}_original{ext}"))
-        _save(out["jpeg_decoded"], os.path.join(output_dir, f"{base}_jpeg{ext}"))
-        _save(out["residual"] * 0.5 + 0.5, os.path.join(output_dir, f"{base}_residual{ext}"))
-        _save(out["residual_hat"] * 0.5 + 0.5, os.path.join(output_dir, f"{base}_residual_hat{ext}"))
+        _save(out_net["jpeg_decoded"], os.path.join(output_dir, f"{base}_jpeg{ext}"))
+        _save(out_net["residual"] * 0.5 + 0.5, os.path.join(output_dir, f"{base}_residual{ext}"))
+        _save(out_net["residual_hat"] * 0.5 + 0.5, os.path.join(output_dir, f"{base}_residual_hat{ext}"))
+    y_bpp = sum(len(s) * 8 for part in out_enc["strings"][0] for s in part) / num_pixels
+    z_bpp = sum(len(s) * 8 for s in out_enc["strings"][1]) / num_pixels
+    jpeg_bpp = float(out_net["jpeg_bpp_loss"])
+    total_bpp = jpeg_bpp + y_bpp + z_bpp
+    mse = torch.nn.functional.mse_loss(x, out_dec["x_hat"]).item()
+    psnr = 10 * math.log10(1.0 / max(mse, 1e-12))
     print(f"Processed {img_path}")
     print(f"Total bpp: {total_bpp:.4f} (JPEG: {jpeg_bpp:.4f}, Y: {y_bpp:.5f}, Z: {z_bpp:.5f})")
     print(f"MSE: {mse * 255 ** 2:.4f})")
     print(f"PSNR: {psnr:.2f} dB, MS-SSIM: 0.0000")
-    print(f"Forward time: {t:.4f}s")
+    print(f"Encoding time: {enc_time:.4f}s, Decoding time: {dec_time:.4f}s")
     return {"filename": os.path.basename(img_path), "total_bpp": total_bpp, "jpeg_bpp": jpeg_bpp, "y_bpp": y_bpp,
-            "z_bpp": z_bpp, "mse": mse * 255 ** 2, "psnr": psnr, "ms_ssim": 0.0, "enc_time": t, "dec_time": 0.0}
+            "z_bpp": z_bpp, "mse": mse * 255 ** 2, "psnr": psnr, "ms_ssim": 0.0, "enc_time": enc_time,
+            "dec_time": dec_time}
 
 
 def main(argv):
@@ -99,6 +98,7 @@ def main(argv):
                                     jpeg_quality=args.jpeg_quality)
     model.load_state_dict(state_dict)
     model = model.to(device).eval()
+    model.update()  # CDF tables (no-op for a checkpoint saved after update(), src/updata.py)
     inp = Path(args.input).resolve()
     if inp.is_file():
         paths = [inp]

@@ -796,3 +796,28 @@ def test_compress_decompress_roundtrip():
         rm.decode_in_compress = False
     assert c2["strings"] == c["strings"]
     assert math.isfinite(c["time"]) and math.isfinite(d["time"])
+
+
+def test_inference_cli_compress_decompress(tmp_path):
+    """src/inference.py end to end on one 64x64 PNG: checkpoint load (weights_only), update(), compress ->
+    decompress, the reference's metrics.csv columns with bpp from the real strings and JPEG bytes."""
+    import csv
+    import numpy as np
+    from PIL import Image
+    from src.inference import main as infer_main
+    g = load_npz("kodim01_crop64_eval.npz")
+    net, sd = _hip_model()
+    ck = tmp_path / "ckpt.pth.tar"
+    torch.save({"state_dict": {k: v.cpu() for k, v in net.state_dict().items()}}, ck)
+    img = (g["x"][0].permute(1, 2, 0).numpy() * 255).round().astype(np.uint8)
+    Image.fromarray(img).save(tmp_path / "img.png")
+    out = tmp_path / "out"
+    infer_main(["--checkpoint", str(ck), "--input", str(tmp_path / "img.png"), "--output", str(out),
+                "--jpeg-quality", "50", "--save-components"])
+    rows = list(csv.DictReader(open(out / "metrics.csv")))
+    assert len(rows) == 1 and rows[0]["filename"] == "img.png"
+    r = rows[0]
+    assert float(r["y_bpp"]) > 0 and float(r["z_bpp"]) > 0 and float(r["jpeg_bpp"]) > 0
+    assert abs(float(r["total_bpp"]) - (float(r["jpeg_bpp"]) + float(r["y_bpp"]) + float(r["z_bpp"]))) < 1e-9
+    assert 5.0 < float(r["psnr"]) < 80.0
+    assert (out / "img_recon.png").exists() and (out / "img_residual_hat.png").exists()
