@@ -146,8 +146,31 @@ def eval_legs(net, x, jpeg, jpeg_bpp, args, reps=20):
             res[tag] = {"ms": round(ms, 3), "mpix_s": round(npx / ms / 1e3, 3)}
             del cap
     res["analysis_synthesis_bs%d" % x.shape[0]] = analysis_synthesis(net, x, reps)
+    res["kodak_codec"] = codec_leg(net, xk.to(dev), jk.to(dev))
     net.train()
     return res
+
+
+def codec_leg(net, xk, jk, reps=3):
+    """configs[4] / BASELINE.md §1: LightWeightCheckerboard.compress / decompress self-timers (transforms +
+    rANS, JPEG and MultiScaleRefine excluded — the span of the README's 0.476 s / 0.286 s) on one Kodak-size
+    768x512 residual, best of ``reps``; bpp from the strings. Synthetic image and recipe weights: the bpp is
+    not comparable with a trained model's."""
+    rm = net.residual_model
+    net.update(force=True)
+    residual = (xk - jk).contiguous()
+    enc, dec = [], []
+    for _ in range(reps):
+        c = rm.compress(residual)
+        d = rm.decompress(c["strings"], c["shape"])
+        torch.cuda.synchronize()
+        enc.append(c["time"])
+        dec.append(d["time"])
+    nbits = 8 * sum(len(s) for part in (c["strings"][0][0], c["strings"][0][1], c["strings"][1]) for s in part)
+    e, dd = min(enc) * 1000, min(dec) * 1000
+    return {"encode_ms": round(e, 2), "decode_ms": round(dd, 2), "residual_bpp": round(nbits / (512 * 768), 4),
+            "readme_encode_ms": 476.0, "readme_decode_ms": 286.0,
+            "speedup_vs_readme": round((476.0 + 286.0) / (e + dd), 2)}
 
 
 def analysis_synthesis(net, x, reps):
