@@ -110,8 +110,11 @@ class FlatGradReducer:
         if g.is_cuda:
             from .ops import SideStream
             main = torch.cuda.current_stream(g.device)
-            side = SideStream.get(g.device)
+            sides = SideStream.all(g.device)
+            side = sides[0]
             side.wait_stream(main)  # gradients of this segment: main-stream (dgrad-side) writes + side wgrads
+            for other in sides[1:]:
+                side.wait_stream(other)
             with torch.cuda.stream(side):
                 self._launch(ranges)
         else:

@@ -15,6 +15,7 @@ CPU oracle (oracle/hyres_oracle.py) in tests/test_parity_gpu.py.
 from __future__ import annotations
 
 import ctypes
+import os
 import weakref
 from typing import Callable, List, Optional
 
@@ -519,24 +520,34 @@ class SideStream:
     the side stream owns workspace slot 2."""
 
     enabled = True
+    count = max(1, int(os.environ.get("HYRES_SIDE_STREAMS", "1")))  # weight-gradient streams (round robin)
     _streams = {}
+    _rr = 0
     used = False
 
     @classmethod
-    def get(cls, device: torch.device) -> torch.cuda.Stream:
-        st = cls._streams.get(device.index)
-        if st is None:
-            st = torch.cuda.Stream(device=device)
-            cls._streams[device.index] = st
-        return st
+    def get(cls, device: torch.device, rotate: bool = False) -> torch.cuda.Stream:
+        sts = cls._streams.get(device.index)
+        if sts is None:
+            sts = [torch.cuda.Stream(device=device) for _ in range(cls.count)]
+            cls._streams[device.index] = sts
+        if rotate:
+            cls._rr = (cls._rr + 1) % len(sts)
+        return sts[cls._rr % len(sts)]
+
+    @classmethod
+    def all(cls, device: torch.device) -> list:
+        cls.get(device)
+        return list(cls._streams[device.index])
 
     @classmethod
     def join(cls) -> None:
         """Make the current stream wait for all side-stream work (end of backward)."""
         if not cls.used:
             return
-        for idx, st in cls._streams.items():
-            torch.cuda.current_stream(torch.device("cuda", idx)).wait_stream(st)
+        for idx, sts in cls._streams.items():
+            for st in sts:
+                torch.cuda.current_stream(torch.device("cuda", idx)).wait_stream(st)
         cls.used = False
 
 
@@ -547,7 +558,7 @@ def _wgrad(desc: L.WgradDesc, p_ptr: int, q_ptr: int, dst: torch.Tensor, device,
     side = side and SideStream.enabled and device.type == "cuda"
     if side:
         main = torch.cuda.current_stream(device)
-        st = SideStream.get(device)
+        st = SideStream.get(device, rotate=True)
         st.wait_stream(main)
         for t in tuple(keep) + (dst,) + ((dbias,) if dbias is not None else ()):
             t.record_stream(st)
