@@ -197,8 +197,15 @@ int hyres_rans_decode_with_indexes(const unsigned char* in, long long in_len, co
         const int* cdf = cdfs + (long long)ci * cdf_stride;
         const int max_value = cdf_sizes[ci] - 2;
         const uint32_t cum = dec.get(rans::PRECISION);
-        int s = 0;
-        while (s + 1 <= max_value + 1 && (uint32_t)cdf[s + 1] <= cum) ++s;  // cdf[s] <= cum < cdf[s+1]
+        // s with cdf[s] <= cum < cdf[s+1] (compressai scans linearly; the CDF is strictly increasing, so a
+        // binary search finds the same s in O(log L) — wide scales have L in the thousands)
+        int lo = 0, hi = max_value;  // cdf[max_value + 1] = 2^16 > cum
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if ((uint32_t)cdf[mid] <= cum) lo = mid;
+            else hi = mid - 1;
+        }
+        const int s = lo;
         dec.advance((uint32_t)cdf[s], (uint32_t)(cdf[s + 1] - cdf[s]), rans::PRECISION);
         int value = s;
         if (value == max_value) {

@@ -130,21 +130,53 @@ def _encode(model, sym: np.ndarray, idx: np.ndarray) -> bytes:
     ln = ctypes.c_longlong(0)
     args = (sym.ctypes.data, idx.ctypes.data, n, cdf.ctypes.data, cdf.shape[1], lengths.ctypes.data,
             offsets.ctypes.data, len(lengths))
-    L.check(lib.hyres_rans_encode_with_indexes(*args, None, 0, ctypes.byref(ln)), "rans_encode")
-    buf = np.empty(ln.value, dtype=np.uint8)
-    L.check(lib.hyres_rans_encode_with_indexes(*args, buf.ctypes.data, buf.size, ctypes.byref(ln)), "rans_encode")
-    return buf.tobytes()
+    buf = np.empty(8 * n + 64, dtype=np.uint8)  # 2 words per symbol: enough unless many bypass escapes
+    if lib.hyres_rans_encode_with_indexes(*args, buf.ctypes.data, buf.size, ctypes.byref(ln)) != 0:
+        buf = np.empty(ln.value, dtype=np.uint8)  # the failed call reported the exact length
+        L.check(lib.hyres_rans_encode_with_indexes(*args, buf.ctypes.data, buf.size, ctypes.byref(ln)),
+                "rans_encode")
+    return buf[:ln.value].tobytes()
 
 
-def _decode(model, data: bytes, idx: np.ndarray) -> np.ndarray:
+def _decode(model, data: bytes, idx: np.ndarray, out: np.ndarray = None) -> np.ndarray:
     cdf, lengths, offsets = _tables(model)
     src = np.frombuffer(data, dtype=np.uint8)
-    out = np.empty(idx.size, dtype=np.int32)
+    if out is None:
+        out = np.empty(idx.size, dtype=np.int32)
+    assert out.dtype == np.int32 and out.flags.c_contiguous and out.size == idx.size
     L.check(L.load().hyres_rans_decode_with_indexes(src.ctypes.data, src.size, idx.ctypes.data, int(idx.size),
                                                     cdf.ctypes.data, cdf.shape[1], lengths.ctypes.data,
                                                     offsets.ctypes.data, len(lengths), out.ctypes.data),
             "rans_decode")
     return out
+
+
+_POOL = None
+
+
+def _pool():
+    """Host threads for the rANS coder: strings are independent (per image, per pass), and the ctypes
+    calls release the GIL, so anchor / non-anchor / z strings (and the images of a batch) code in parallel
+    and overlap the GPU work that follows them in compress."""
+    global _POOL
+    if _POOL is None:
+        from concurrent.futures import ThreadPoolExecutor
+        _POOL = ThreadPoolExecutor(max_workers=8, thread_name_prefix="hyres-rans")
+    return _POOL
+
+
+def _map(fn, items):
+    items = list(items)
+    if len(items) <= 1:  # one image: decode on the calling thread
+        return [fn(it) for it in items]
+    return list(_pool().map(fn, items))
+
+
+def resolve(strings):
+    """Futures -> bytes (lists of per-image strings, possibly nested)."""
+    if isinstance(strings, list):
+        return [resolve(v) for v in strings]
+    return strings.result() if hasattr(strings, "result") else strings
 
 
 def _medians(eb) -> torch.Tensor:
@@ -155,23 +187,29 @@ def _eb_indexes(C: int, H: int, W: int) -> np.ndarray:
     return np.ascontiguousarray(np.repeat(np.arange(C, dtype=np.int32), H * W))
 
 
-def eb_compress(eb, z: Node) -> List[bytes]:
-    """EntropyBottleneck.compress(z): one string per image."""
+def eb_compress(eb, z: Node) -> list:
+    """EntropyBottleneck.compress(z): one string per image (futures; ``resolve`` -> bytes)."""
     B, H, W, C = z.B, z.H, z.W, z.C
     sym = torch.empty(B * C * H * W, dtype=torch.int32, device=z.device)
     L.call("hyres_eb_symbols", z.ptr(), z.ld, _medians(eb).data_ptr(), B, H, W, C, sym.data_ptr(), None, 0, 0,
            L.stream())
     sym_h = sym.cpu().numpy().reshape(B, -1)
     idx = _eb_indexes(C, H, W)
-    return [_encode(eb, np.ascontiguousarray(sym_h[b]), idx) for b in range(B)]
+    _tables(eb)
+    return [_pool().submit(_encode, eb, np.ascontiguousarray(sym_h[b]), idx) for b in range(B)]
 
 
 def eb_decompress(eb, strings: List[bytes], H: int, W: int, device) -> Node:
     """EntropyBottleneck.decompress(strings, (H, W)) -> z_hat (NHWC Node)."""
     B, C = len(strings), eb.channels
     idx = _eb_indexes(C, H, W)
-    sym = np.stack([_decode(eb, s, idx) for s in strings])
-    sym_d = torch.from_numpy(sym).to(device)
+    _tables(eb)
+    # decoded straight into pinned host memory: a pageable host->device copy of the symbols costs tens of
+    # ms on this platform (measured: 4.7 MB in 21-28 ms), a pinned one well under 1 ms
+    sym = torch.empty((B, C * H * W), dtype=torch.int32, pin_memory=True)
+    sym_np = sym.numpy()
+    _map(lambda bs: _decode(eb, bs[1], idx, sym_np[bs[0]]), enumerate(resolve(list(strings))))
+    sym_d = sym.to(device, non_blocking=True)
     z_hat = Node.new(B, H, W, C, device, rg=False)
     L.call("hyres_eb_symbols", None, 0, _medians(eb).data_ptr(), B, H, W, C, sym_d.data_ptr(), z_hat.ptr(),
            z_hat.ld, 1, L.stream())
@@ -189,14 +227,16 @@ def _gc_indexes(gc, params: Node, M: int, y: Node = None, parity: int = -1):
     return sym, idx
 
 
-def gc_compress(gc, y: Node, params: Node, M: int, parity: int) -> List[bytes]:
+def gc_compress(gc, y: Node, params: Node, M: int, parity: int) -> list:
     """GaussianConditional.compress(y * mask(parity), build_indexes(scales), means) per image
     (models/checkerboard.py:159-161); params = [.., scales(M) | means(M)]."""
     sym, idx = _gc_indexes(gc, params, M, y, parity)
     B = params.B
     sym_h = sym.cpu().numpy().reshape(B, -1)
     idx_h = idx.cpu().numpy().reshape(B, -1)
-    return [_encode(gc, np.ascontiguousarray(sym_h[b]), np.ascontiguousarray(idx_h[b])) for b in range(B)]
+    _tables(gc)
+    return [_pool().submit(_encode, gc, np.ascontiguousarray(sym_h[b]), np.ascontiguousarray(idx_h[b]))
+            for b in range(B)]
 
 
 def gc_decompress(gc, strings: List[bytes], params: Node, M: int, out: Node, accumulate: bool = False) -> Node:
@@ -204,8 +244,12 @@ def gc_decompress(gc, strings: List[bytes], params: Node, M: int, out: Node, acc
     _, idx = _gc_indexes(gc, params, M)
     B = params.B
     idx_h = idx.cpu().numpy().reshape(B, -1)
-    sym = np.stack([_decode(gc, s, np.ascontiguousarray(idx_h[b])) for b, s in enumerate(strings)])
-    sym_d = torch.from_numpy(sym).to(params.device)
+    _tables(gc)
+    sym = torch.empty(idx_h.shape, dtype=torch.int32, pin_memory=True)  # pinned: see eb_decompress
+    sym_np = sym.numpy()
+    _map(lambda bs: _decode(gc, bs[1], np.ascontiguousarray(idx_h[bs[0]]), sym_np[bs[0]]),
+         enumerate(resolve(list(strings))))
+    sym_d = sym.to(params.device, non_blocking=True)
     L.call("hyres_gc_dequant", sym_d.data_ptr(), params.ptr(), params.ld, M, B, params.H, params.W, out.ptr(), out.ld,
            int(accumulate), L.stream())
     return out

@@ -155,8 +155,9 @@ class LightWeightCheckerboard(CompressionModel):
         self.context_prediction.hip(None, ya_hat, out=lc.slice(2 * M, 4 * M))
         params_na = self.param_aggregation.hip(None, lc)
         non_anchor_strings = EC.gc_compress(gc, y, params_na, M, parity=1)
+        strings = EC.resolve([[anchor_strings, non_anchor_strings], z_strings])  # host rANS threads join
         return {
-            "strings": [[anchor_strings, non_anchor_strings], z_strings],
+            "strings": strings,
             "shape": torch.Size([z.H, z.W]),
             "time": time.time() - start_time,
         }
