@@ -17,4 +17,4 @@ python3 scripts/pmc_traffic.py gpurun_out/${tag}_pmc_fetch gpurun_out/${tag}_pmc
   --kernel "conv_fwd_kernel<2, 1, 2, 2, 0, false, false>" --out gpurun_out/${tag}_pmc_traffic.json \
   --command "rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE --kernel-trace --output-format csv -- python3 $BENCH" \
   > gpurun_out/pmc_traffic.log 2>&1 && \
-python3 scripts/prof_summary.py gpurun_out/${tag}_stats/run_kernel_stats.csv 10 > gpurun_out/${tag}_summary.txt
+python3 scripts/prof_summary.py gpurun_out/${tag}_stats/run_kernel_stats.csv 11 > gpurun_out/${tag}_summary.txt
