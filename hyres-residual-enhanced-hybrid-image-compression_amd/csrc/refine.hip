@@ -284,28 +284,32 @@ __global__ void se_bwd_x_kernel(const float* gy, const float* sgate, const float
 // ---------------------------------------------------------------- SpatialAttention
 // One wave per pixel (C <= 256, C % 4 == 0: float4 per lane): channel mean, max and the first-occurrence
 // argmax (torch.max(dim=1) on CPU keeps the first maximal index; the backward routes g_max there).
-__global__ void sa_pool_kernel(const float* x, float* pooled2, int* amax, long long P, int C) {
-    const int lane = threadIdx.x & 63;
-    const long long p = (long long)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
-    if (p >= P) return;
-    const float* xp = x + p * C;
+// channel mean / max (+ first argmax, torch.max semantics) per pixel: 16 lanes per pixel (4 pixels per wave,
+// each lane a float4 stride over the channels), folded with 4 xor-shuffles
+__global__ __launch_bounds__(256) void sa_pool_kernel(const float* x, float* pooled2, int* amax, long long P, int C) {
+    const int l16 = threadIdx.x & 15;
+    const long long p = (long long)blockIdx.x * 16 + (threadIdx.x >> 4);
+    const bool ok = p < P;
+    const float* xp = x + (ok ? p : 0) * C;
     float s = 0.f, m = -INFINITY;
     int mi = 0x7fffffff;
-    for (int c = 4 * lane; c < C; c += 256) {
-        const float4 v = *reinterpret_cast<const float4*>(xp + c);
-        s += (v.x + v.y) + (v.z + v.w);
-        if (v.x > m) { m = v.x; mi = c; }
-        if (v.y > m) { m = v.y; mi = c + 1; }
-        if (v.z > m) { m = v.z; mi = c + 2; }
-        if (v.w > m) { m = v.w; mi = c + 3; }
+    if (ok) {
+        for (int c = 4 * l16; c < C; c += 64) {
+            const float4 v = *reinterpret_cast<const float4*>(xp + c);
+            s += (v.x + v.y) + (v.z + v.w);
+            if (v.x > m) { m = v.x; mi = c; }
+            if (v.y > m) { m = v.y; mi = c + 1; }
+            if (v.z > m) { m = v.z; mi = c + 2; }
+            if (v.w > m) { m = v.w; mi = c + 3; }
+        }
     }
-    for (int off = 32; off > 0; off >>= 1) {
+    for (int off = 8; off > 0; off >>= 1) {
         s += __shfl_xor(s, off);
         const float om = __shfl_xor(m, off);
         const int oi = __shfl_xor(mi, off);
         if (om > m || (om == m && oi < mi)) { m = om; mi = oi; }
     }
-    if (lane == 0) {
+    if (ok && l16 == 0) {
         pooled2[p * 2 + 0] = s / (float)C;
         pooled2[p * 2 + 1] = m;
         amax[p] = mi;
@@ -542,9 +546,13 @@ int hyres_se_bwd(const float* x, const float* gy, const float* w1, const float* 
     return HY_LAUNCH_CHECK("se_bwd_x");
 }
 
+static int sa_bwd_blocks(long long n) {  // >= 4 pixels per thread: the 98-tap weight fold is amortised
+    return (int)std::max<long long>(1, std::min<long long>((n + 255) / 256, 1024));
+}
+
 long long hyres_spatial_attn_workspace_bytes(int B, int H, int W) {
     long long n = (long long)B * H * W;
-    int nb = grid_for_r(n);
+    int nb = sa_bwd_blocks(n);
     return (long long)nb * 98 * 4 + n * 4 + n * 2 * 4 + 1024;
 }
 
@@ -555,7 +563,8 @@ int hyres_spatial_attn_fwd(const float* x, const float* w, float* pooled2, int* 
                "spatial_attn: C %% 4 == 0 and 16B-aligned x/y required");
     long long P = (long long)B * H * W;
     hipStream_t st = as_stream(s);
-    hipLaunchKernelGGL(sa_pool_kernel, dim3((unsigned)((P + 3) / 4)), dim3(256), 0, st, x, pooled2, argmax, P, C);
+    HY_REQUIRE(C % 4 == 0 && aligned16(x), HYRES_E_ALIGN, "spatial_attn_fwd: C %% 4 and 16B-aligned x needed");
+    hipLaunchKernelGGL(sa_pool_kernel, dim3((unsigned)((P + 15) / 16)), dim3(256), 0, st, x, pooled2, argmax, P, C);
     int rc = HY_LAUNCH_CHECK("sa_pool");
     if (rc) return rc;
     hipLaunchKernelGGL(sa_conv_kernel, dim3(grid_for_r(P)), dim3(256), 0, st, (const float*)pooled2, w, attn, B, H, W);
@@ -581,7 +590,7 @@ int hyres_spatial_attn_bwd(const float* x, const float* w, const float* pooled2,
     hipLaunchKernelGGL(sa_bwd_logit_kernel, dim3((unsigned)((P + 3) / 4)), dim3(256), 0, st, x, gy, attn, glogit, P, C);
     int rc = HY_LAUNCH_CHECK("sa_bwd_logit");
     if (rc) return rc;
-    int nb = grid_for_r(P);
+    int nb = sa_bwd_blocks(P);
     hipLaunchKernelGGL(sa_bwd_conv_kernel, dim3(nb), dim3(256), 0, st, (const float*)glogit, pooled2, w, gp2, wpart, B,
                        H, W);
     rc = HY_LAUNCH_CHECK("sa_bwd_conv");
