@@ -141,6 +141,67 @@ __global__ void add2d_kernel(const float* x, int ldx, float* y, int ldy, long lo
         *yp = acc ? *yp + v : v;
     }
 }
+// float4 variants of the [P][C]-strided elementwise passes (C, every ld % 4 == 0, 16B-aligned, P*C < 2^31):
+// 32-bit index math, 16 B per lane
+__global__ __launch_bounds__(256) void add2d4_kernel(const float* x, int ldx, float* y, int ldy, int P, int C4,
+                                                     int acc) {
+    const int n = P * C4;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+        const int p = i / C4, c = 4 * (i - (i / C4) * C4);
+        float4 v = *reinterpret_cast<const float4*>(x + (long long)p * ldx + c);
+        float4* yp = reinterpret_cast<float4*>(y + (long long)p * ldy + c);
+        if (acc) {
+            const float4 o = *yp;
+            v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+        }
+        *yp = v;
+    }
+}
+__global__ __launch_bounds__(256) void relu_bwd_2d4_kernel(const float* y, int ldy, const float* g, int ldg,
+                                                           float* gx, int ldgx, int P, int C4) {
+    const int n = P * C4;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+        const int p = i / C4, c = 4 * (i - (i / C4) * C4);
+        const float4 yv = *reinterpret_cast<const float4*>(y + (long long)p * ldy + c);
+        const float4 gv = *reinterpret_cast<const float4*>(g + (long long)p * ldg + c);
+        *reinterpret_cast<float4*>(gx + (long long)p * ldgx + c) =
+            make_float4(yv.x > 0.f ? gv.x : 0.f, yv.y > 0.f ? gv.y : 0.f, yv.z > 0.f ? gv.z : 0.f,
+                        yv.w > 0.f ? gv.w : 0.f);
+    }
+}
+__global__ __launch_bounds__(256) void prelu_bwd4_kernel(const float* x, int ldx, const float* g, int ldg, float* gx,
+                                                         int ldgx, int P, int C4, const float* slope, float* part) {
+    const float a = slope[0];
+    const int n = P * C4;
+    float s = 0.f;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+        const int p = i / C4, c = 4 * (i - (i / C4) * C4);
+        const float4 xv = *reinterpret_cast<const float4*>(x + (long long)p * ldx + c);
+        const float4 gv = *reinterpret_cast<const float4*>(g + (long long)p * ldg + c);
+        *reinterpret_cast<float4*>(gx + (long long)p * ldgx + c) =
+            make_float4(xv.x > 0.f ? gv.x : a * gv.x, xv.y > 0.f ? gv.y : a * gv.y, xv.z > 0.f ? gv.z : a * gv.z,
+                        xv.w > 0.f ? gv.w : a * gv.w);
+        if (!(xv.x > 0.f)) s += xv.x * gv.x;
+        if (!(xv.y > 0.f)) s += xv.y * gv.y;
+        if (!(xv.z > 0.f)) s += xv.z * gv.z;
+        if (!(xv.w > 0.f)) s += xv.w * gv.w;
+    }
+    __shared__ float red[256];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int k = 128; k > 0; k >>= 1) {
+        if (threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+
+static inline bool vec4_2d(long long P, int C, const void* a, int lda, const void* b, int ldb, const void* c, int ldc) {
+    auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; };
+    return C % 4 == 0 && lda % 4 == 0 && ldb % 4 == 0 && ldc % 4 == 0 && al(a) && al(b) && al(c) &&
+           P * (long long)C < (1LL << 31);
+}
+
 __global__ void mul_kernel(const float* a, const float* b, float* y, long long n) {
     GRID_STRIDE(i, n) y[i] = a[i] * b[i];
 }
@@ -367,6 +428,11 @@ int hyres_relu_bwd(const float* y, const float* g, float* gx, long long n, hyres
 int hyres_relu_bwd_2d(const float* y, int ldy, const float* g, int ldg, float* gx, int ldgx, long long P, int C,
                       hyres_stream_t s) {
     HY_REQUIRE(y && g && gx, HYRES_E_ARG, "relu_bwd_2d: NULL");
+    if (vec4_2d(P, C, y, ldy, g, ldg, gx, ldgx)) {
+        hipLaunchKernelGGL(relu_bwd_2d4_kernel, dim3(grid_for(P * C / 4)), dim3(256), 0, as_stream(s), y, ldy, g, ldg,
+                           gx, ldgx, (int)P, C / 4);
+        return HY_LAUNCH_CHECK("relu_bwd_2d4");
+    }
     hipLaunchKernelGGL(relu_bwd_2d_kernel, dim3(grid_for(P * C)), dim3(256), 0, as_stream(s), y, ldy, g, ldg, gx,
                        ldgx, P, C);
     return HY_LAUNCH_CHECK("relu_bwd_2d");
@@ -378,8 +444,12 @@ int hyres_prelu_bwd(const float* x, int ldx, const float* g, int ldg, float* gx,
     HY_REQUIRE(x && g && gx && slope && dslope, HYRES_E_ARG, "prelu_bwd: NULL");
     int nb = grid_for(P * C, 4);
     HY_REQUIRE(ws && ws_bytes >= (long long)nb * 4, HYRES_E_WORKSPACE, "prelu_bwd: workspace");
-    hipLaunchKernelGGL(prelu_bwd_kernel, dim3(nb), dim3(256), 0, as_stream(s), x, ldx, g, ldg, gx, ldgx, P, C, slope,
-                       (float*)ws);
+    if (vec4_2d(P, C, x, ldx, g, ldg, gx, ldgx))
+        hipLaunchKernelGGL(prelu_bwd4_kernel, dim3(nb), dim3(256), 0, as_stream(s), x, ldx, g, ldg, gx, ldgx, (int)P,
+                           C / 4, slope, (float*)ws);
+    else
+        hipLaunchKernelGGL(prelu_bwd_kernel, dim3(nb), dim3(256), 0, as_stream(s), x, ldx, g, ldg, gx, ldgx, P, C,
+                           slope, (float*)ws);
     int rc = HY_LAUNCH_CHECK("prelu_bwd");
     if (rc) return rc;
     hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(256), 0, as_stream(s), (const float*)ws, nb, dslope, 1);
@@ -404,6 +474,11 @@ int hyres_accumulate(const float* x, float* y, long long n, hyres_stream_t s) {
 int hyres_add2d(const float* x, int ldx, float* y, int ldy, long long P, int C, int accumulate,
                 hyres_stream_t s) {
     HY_REQUIRE(x && y, HYRES_E_ARG, "add2d: NULL");
+    if (vec4_2d(P, C, x, ldx, y, ldy, y, ldy)) {
+        hipLaunchKernelGGL(add2d4_kernel, dim3(grid_for(P * C / 4)), dim3(256), 0, as_stream(s), x, ldx, y, ldy, (int)P,
+                           C / 4, accumulate);
+        return HY_LAUNCH_CHECK("add2d4");
+    }
     hipLaunchKernelGGL(add2d_kernel, dim3(grid_for(P * C)), dim3(256), 0, as_stream(s), x, ldx, y, ldy, P, C,
                        accumulate);
     return HY_LAUNCH_CHECK("add2d");

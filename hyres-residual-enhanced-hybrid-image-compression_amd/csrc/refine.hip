@@ -354,17 +354,20 @@ __global__ void sa_mul_kernel(const float* x, const float* attn, float* y, long 
 // bwd 1: g_logit[p] = (sum_c gy*x) * a*(1-a)
 __global__ void sa_bwd_logit_kernel(const float* x, const float* gy, const float* attn, float* glogit, long long P,
                                     int C) {
-    const int lane = threadIdx.x & 63;
-    const long long p = (long long)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
-    if (p >= P) return;
+    // 16 lanes per pixel (4 pixels per wave), 4 xor-shuffles
+    const int l16 = threadIdx.x & 15;
+    const long long p = (long long)blockIdx.x * 16 + (threadIdx.x >> 4);
+    const bool ok = p < P;
     float s = 0.f;
-    for (int c = 4 * lane; c < C; c += 256) {
-        const float4 g = *reinterpret_cast<const float4*>(gy + p * C + c);
-        const float4 v = *reinterpret_cast<const float4*>(x + p * C + c);
-        s += (g.x * v.x + g.y * v.y) + (g.z * v.z + g.w * v.w);
+    if (ok) {
+        for (int c = 4 * l16; c < C; c += 64) {
+            const float4 g = *reinterpret_cast<const float4*>(gy + p * C + c);
+            const float4 v = *reinterpret_cast<const float4*>(x + p * C + c);
+            s += (g.x * v.x + g.y * v.y) + (g.z * v.z + g.w * v.w);
+        }
     }
-    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
-    if (lane == 0) {
+    for (int off = 8; off > 0; off >>= 1) s += __shfl_xor(s, off);
+    if (ok && l16 == 0) {
         float a = attn[p];
         glogit[p] = s * a * (1.0f - a);
     }
@@ -587,7 +590,8 @@ int hyres_spatial_attn_bwd(const float* x, const float* w, const float* pooled2,
     float* gp2 = glogit + P;
     float* wpart = gp2 + 2 * P;
     hipStream_t st = as_stream(s);
-    hipLaunchKernelGGL(sa_bwd_logit_kernel, dim3((unsigned)((P + 3) / 4)), dim3(256), 0, st, x, gy, attn, glogit, P, C);
+    hipLaunchKernelGGL(sa_bwd_logit_kernel, dim3((unsigned)((P + 15) / 16)), dim3(256), 0, st, x, gy, attn, glogit, P,
+                       C);
     int rc = HY_LAUNCH_CHECK("sa_bwd_logit");
     if (rc) return rc;
     int nb = sa_bwd_blocks(P);
