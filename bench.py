@@ -233,11 +233,21 @@ def main():
     opt = FusedAdam(main_p, lr=3e-4, max_grad_norm=1.0)
     aux_opt = FusedAdam(aux_p, lr=3e-4)
     reducer = None
+    # N > 1: the captured forward/backward graph replays, then the flat gradients are all-reduced in two
+    # 32 MB RCCL buckets (measured at N=1: 44.5 ms graph vs 49 ms for the eager step whose all-reduce
+    # overlaps backward — the eager host enqueue costs more than an unoverlapped 41.5 MB all-reduce over
+    # xGMI). HYRES_DIST_OVERLAP=1 (or --no-graph) selects the eager overlapped path.
+    dist_mode = None
+    if dist:
+        overlap = args.no_graph or os.environ.get("HYRES_DIST_OVERLAP") == "1"
+        dist_mode = "eager-overlap" if overlap else "graph+allreduce"
     if dist:
         # RCCL all-reduce of refine / g_s / hyperprior gradient segments launched from backward-progress
         # markers (overlapped with the rest of backward), the remainder (g_a) after backward
         from hyres_hip.ddp import FlatGradReducer, HYRES_SEGMENTS
-        reducer = FlatGradReducer(opt.flat, world, names=main_names, segments=HYRES_SEGMENTS).overlap()
+        reducer = FlatGradReducer(opt.flat, world, names=main_names, segments=HYRES_SEGMENTS)
+        if dist_mode == "eager-overlap":
+            reducer.overlap()
     crit = RateDistortionLoss(lmbda=args.lmbda, alpha=0)
 
     B, S = args.batch, args.size
@@ -250,11 +260,12 @@ def main():
     jpeg = jpeg_cpu.to(dev)
 
     graphed = None
-    if not args.no_graph and not dist:
+    if not args.no_graph and dist_mode != "eager-overlap":
         # forward + RD loss + backward captured once as a HIP graph (hyres_hip.graphs); the optimiser,
         # the RCCL all-reduce and the aux step stay eager (a handful of launches)
         from hyres_hip.graphs import CapturedStep
-        graphed = CapturedStep(net, x, jpeg, jpeg_bpp, noisequant=False, criterion=crit, zero_grad=opt.zero_grad)
+        graphed = CapturedStep(net, x, jpeg, jpeg_bpp, noisequant=False, criterion=crit, zero_grad=opt.zero_grad,
+                               capture_error_mode="thread_local" if dist else "global")
 
     def fwd_bwd(eager=False):
         if graphed is not None and not eager:
@@ -363,6 +374,7 @@ def main():
                      "avg_launch_us_isolated": round(ks_iso["avg_us"], 2),
                      "ms_by_variant": ks.get("by_variant_ms")},
         "graph": graphed is not None,
+        "dist_mode": dist_mode,
         "eval": evals,
         "cpu_baseline": cpu,
         "jpeg_host_ms_per_image": round(jpeg_ms, 3),

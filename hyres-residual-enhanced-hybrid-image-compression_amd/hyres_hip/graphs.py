@@ -12,7 +12,8 @@ What is captured and what stays eager:
     libhyres_hip launch of the reference's forward/backward (models/hyres.py:23-77,
     src/utils/engine.py:33-55);
   * eager: the optimiser (FusedAdam's bias correction reads the host step count), the RCCL gradient
-    all-reduce and the aux (quantiles) step — 3-10 launches per step.
+    all-reduce (two 32 MB buckets after the replay: the graph holds no collective) and the aux
+    (quantiles) step — 3-10 launches per step.
 Graph-safety of the captured region:
   * weights: the conv weight re-layout cache (hyres_hip.ops._prepped) is invalidated before capture so
     every re-layout kernel is recorded and re-runs on each replay (weights change every optimiser step),
@@ -49,7 +50,8 @@ class CapturedStep:
 
     def __init__(self, net: torch.nn.Module, x: torch.Tensor, jpeg_decoded: torch.Tensor, jpeg_bpp: float = 0.0,
                  noisequant: bool = False, criterion: Optional[Callable] = None,
-                 zero_grad: Optional[Callable[[], None]] = None, warmup: int = 2):
+                 zero_grad: Optional[Callable[[], None]] = None, warmup: int = 2,
+                 capture_error_mode: str = "global"):
         assert x.is_cuda, "CapturedStep needs device tensors"
         self.net = net
         self.train = criterion is not None
@@ -82,7 +84,9 @@ class CapturedStep:
         self.graph = torch.cuda.CUDAGraph()
         O.PrepBatch.prepare(dev)  # descriptor table uploaded now: the capture records ONE batched re-layout
         O.bump_weight_epoch()  # record every weight re-layout inside the graph
-        with torch.cuda.graph(self.graph):
+        # "thread_local" when an RCCL process group exists: its watchdog thread polls events while the
+        # main thread captures (no collective is ever inside the graph)
+        with torch.cuda.graph(self.graph, capture_error_mode=capture_error_mode):
             self.out, self.crit = run()
         O.bump_weight_epoch()  # eager calls must not reuse buffers only the graph writes
         torch.cuda.synchronize(dev)

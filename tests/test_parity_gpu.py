@@ -714,6 +714,53 @@ def test_overlapped_rccl_reducer_single_rank():
         tdist.destroy_process_group()
 
 
+def test_captured_step_with_rccl_group_single_rank():
+    """The N > 1 bench path: the train step captured (capture_error_mode thread_local) while an RCCL
+    process group is live, replayed, then the flat gradients all-reduced in buckets after the replay;
+    the reduced gradients equal the eager step's."""
+    import os
+    import socket
+    import torch.distributed as tdist
+    from hyres_hip.ddp import FlatGradReducer, HYRES_SEGMENTS
+    from hyres_hip.graphs import CapturedStep
+    from hyres_hip.loss import RateDistortionLoss
+    from hyres_hip.optim import FusedAdam
+    g = load_npz("hyres_train_b2_64.npz")
+    net, _ = _hip_model()
+    net.train()
+    D = dev()
+    x, j = g["x"].to(D), g["jpeg_decoded"].to(D)
+    names = [n for n, p in sorted(net.named_parameters()) if not n.endswith(".quantiles")]
+    opt = FusedAdam([p for n, p in sorted(net.named_parameters()) if not n.endswith(".quantiles")], lr=0.0)
+    crit = RateDistortionLoss(lmbda=0.045, alpha=0)
+    net.residual_model.noise.injected = {"z": g["noise_z"].permute(0, 2, 3, 1).contiguous().to(D),
+                                         "y": g["noise_y"].permute(0, 2, 3, 1).contiguous().to(D)}
+    opt.zero_grad()
+    crit(net.forward_device(x, j, 0.0), x)["loss"].backward()
+    torch.cuda.synchronize()
+    ref = opt.flat.grad.clone()
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    tdist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        red = FlatGradReducer(opt.flat, 1, names=names, segments=HYRES_SEGMENTS)
+        red.all_reduce()  # a completed collective before the capture (the watchdog has work to poll)
+        opt.zero_grad()
+        cap = CapturedStep(net, x, j, 0.0, criterion=crit, zero_grad=opt.zero_grad,
+                           capture_error_mode="thread_local")
+        for _ in range(2):
+            opt.zero_grad()
+            cap.replay()
+            red.all_reduce()
+            torch.cuda.synchronize()
+            assert red.fired == []
+            assert torch.equal(opt.flat.grad, ref)
+    finally:
+        tdist.destroy_process_group()
+
+
 def test_batched_weight_relayout_matches_individual():
     """hyres_hip.ops.PrepBatch: after an optimiser-style weight update (new epoch) every cached conv
     re-layout is refreshed by ONE batched launch, bit-identical to the per-layer re-layout kernel."""
