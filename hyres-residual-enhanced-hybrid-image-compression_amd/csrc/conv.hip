@@ -16,6 +16,7 @@
 
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 #include <utility>
 
 namespace hyres {
@@ -976,23 +977,27 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgradArgs a) {
     });
 }
 
-// deterministic split-K reduce: 16 float4 lanes x 16 split groups per block (64 outputs per block)
+// deterministic split-K reduce: LX float4 lanes x (256 / LX) split groups per block (4*LX outputs per
+// block). Few outputs with many splits (1x1 / small weights over a whole batch: nsplit up to 512) take
+// LX = 4, so each thread walks nsplit/64 partial rows instead of nsplit/16 and 4x as many blocks run.
+template <int LX>
 __device__ __forceinline__ void wgrad_reduce_body(int blk, const float* slab, int nsplit, int ntaps, int M, int N,
                                                   float* dst, int sm, int sn, int st, int accumulate) {
-    __shared__ float red[16][65];
+    constexpr int G = 256 / LX, OUT = 4 * LX;
+    __shared__ float red[G][OUT + 1];
     const long long total = (long long)ntaps * M * N;
-    const int lx = threadIdx.x & 15, ly = threadIdx.x >> 4;
-    const long long base = (long long)blk * 64 + 4 * lx;
+    const int lx = threadIdx.x % LX, ly = threadIdx.x / LX;
+    const long long base = (long long)blk * OUT + 4 * lx;
     float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
     if ((total & 3) == 0) {
         if (base < total)
 #pragma unroll 4
-            for (int k = ly; k < nsplit; k += 16) {
+            for (int k = ly; k < nsplit; k += G) {
                 const float4 v = ld4(slab + k * total + base);
                 s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
             }
     } else {
-        for (int k = ly; k < nsplit; k += 16) {
+        for (int k = ly; k < nsplit; k += G) {
             const float* p = slab + k * total + base;
             if (base + 0 < total) s.x += p[0];
             if (base + 1 < total) s.y += p[1];
@@ -1005,12 +1010,12 @@ __device__ __forceinline__ void wgrad_reduce_body(int blk, const float* slab, in
     red[ly][4 * lx + 2] = s.z;
     red[ly][4 * lx + 3] = s.w;
     __syncthreads();
-    if (threadIdx.x < 64) {
-        const long long idx = (long long)blk * 64 + threadIdx.x;
+    if (threadIdx.x < OUT) {
+        const long long idx = (long long)blk * OUT + threadIdx.x;
         if (idx < total) {
             float v = 0.f;
-#pragma unroll
-            for (int g = 0; g < 16; ++g) v += red[g][threadIdx.x];
+#pragma unroll 16
+            for (int g = 0; g < G; ++g) v += red[g][threadIdx.x];
             const int n = (int)(idx % N);
             const long long r = idx / N;
             const int m = (int)(r % M);
@@ -1021,19 +1026,28 @@ __device__ __forceinline__ void wgrad_reduce_body(int blk, const float* slab, in
     }
 }
 
+template <int LX>
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* slab, int nsplit, int ntaps, int M, int N,
                                                            float* dst, int sm, int sn, int st, int accumulate) {
-    wgrad_reduce_body(blockIdx.x, slab, nsplit, ntaps, M, N, dst, sm, sn, st, accumulate);
+    wgrad_reduce_body<LX>(blockIdx.x, slab, nsplit, ntaps, M, N, dst, sm, sn, st, accumulate);
 }
 
 // weight-gradient slab reduce and the bias-gradient partials ([nsplit][M]) in one launch
+template <int LX>
 __global__ __launch_bounds__(256) void wgrad_bias_reduce_kernel(const float* slab, int nsplit, int ntaps, int M, int N,
                                                                 float* dst, int sm, int sn, int st, int accumulate,
                                                                 int nb_w, const float* bslab, float* dbias) {
     if ((int)blockIdx.x < nb_w)
-        wgrad_reduce_body(blockIdx.x, slab, nsplit, ntaps, M, N, dst, sm, sn, st, accumulate);
+        wgrad_reduce_body<LX>(blockIdx.x, slab, nsplit, ntaps, M, N, dst, sm, sn, st, accumulate);
     else
-        wgrad_reduce_body(blockIdx.x - nb_w, bslab, nsplit, 1, M, 1, dbias, 1, 0, 0, accumulate);
+        wgrad_reduce_body<LX>(blockIdx.x - nb_w, bslab, nsplit, 1, M, 1, dbias, 1, 0, 0, accumulate);
+}
+
+// lanes per block row for the reduce: keep ~>= 1024 blocks when the split count is large
+static int reduce_lx(long long total, int nsplit) {
+    if (nsplit <= 64 || (total + 63) / 64 >= 1024) return 16;
+    if ((total + 31) / 32 >= 1024) return 8;
+    return 4;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1495,7 +1509,13 @@ int hyres_conv_forward(const hyres_conv_geom* g, const float* x, const float* w2
         return HY_LAUNCH_CHECK("conv_narrow_kernel");
     }
     int rc;
-    if (g->Co > 64) rc = launch_fwd<2, 2, 2, 2>(a, mode, st);
+    // short-K layers (1x1 convs, <= 4 K chunks): the main loop is too short to hide the operand and
+    // epilogue latencies, so half-height tiles put twice as many blocks in flight
+    static const int shortk = env_int("HYRES_CONV_SHORTK", 1);
+    const bool short_k = shortk && a.nsplit == 1 && mode != 2 && g->nphase == 1 && g->ntaps == 1 && g->Ci <= 4 * KT;
+    if (short_k && g->Co > 64) rc = launch_fwd<1, 2, 2, 2>(a, mode, st);
+    else if (short_k && g->Co > 32) rc = launch_fwd<1, 1, 2, 2>(a, mode, st);
+    else if (g->Co > 64) rc = launch_fwd<2, 2, 2, 2>(a, mode, st);
     else if (g->Co > 32) rc = launch_fwd<2, 1, 2, 2>(a, mode, st);
     else rc = launch_fwd<1, 1, 4, 1>(a, mode, st);
     if (rc || a.nsplit == 1) return rc;
@@ -1667,26 +1687,36 @@ int hyres_conv_wgrad(const hyres_wgrad_desc* d0, const float* pp, const float* q
     int rc = HY_LAUNCH_CHECK("wgrad_kernel");
     if (rc) return rc;
     const long long total = (long long)d->ntaps * d->M * d->N;
-    if (dbias && !swap) {  // [nsplit][M] bias partials reduced by the same launch
-        const int nb_w = ceil_div(total, 64);
-        hipLaunchKernelGGL(wgrad_bias_reduce_kernel, dim3(nb_w + ceil_div(d->M, 64)), dim3(256), 0, st,
-                           (const float*)ws, p.nsplit, d->ntaps, d->M, d->N, dst, d->sm, d->sn, d->st, d->accumulate,
-                           nb_w, (const float*)bias_ws, dbias);
-        return HY_LAUNCH_CHECK("wgrad_bias_reduce_kernel");
-    }
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(ceil_div(total, 64)), dim3(256), 0, st, (const float*)ws, p.nsplit,
-                       d->ntaps, d->M, d->N, dst, d->sm, d->sn, d->st, d->accumulate);
-    rc = HY_LAUNCH_CHECK("wgrad_reduce_kernel");
-    if (rc || !dbias) return rc;
+    const int lx = reduce_lx(total, p.nsplit);
+    const int outb = 4 * lx;
+    auto reduce = [&](auto lxc) {
+        constexpr int LX = decltype(lxc)::value;
+        if (dbias && !swap) {  // [nsplit][M] bias partials reduced by the same launch
+            const int nb_w = (int)ceil_div(total, outb);
+            hipLaunchKernelGGL(wgrad_bias_reduce_kernel<LX>, dim3(nb_w + ceil_div(d->M, outb)), dim3(256), 0, st,
+                               (const float*)ws, p.nsplit, d->ntaps, d->M, d->N, dst, d->sm, d->sn, d->st,
+                               d->accumulate, nb_w, (const float*)bias_ws, dbias);
+            return HY_LAUNCH_CHECK("wgrad_bias_reduce_kernel");
+        }
+        hipLaunchKernelGGL(wgrad_reduce_kernel<LX>, dim3(ceil_div(total, outb)), dim3(256), 0, st, (const float*)ws,
+                           p.nsplit, d->ntaps, d->M, d->N, dst, d->sm, d->sn, d->st, d->accumulate);
+        int r = HY_LAUNCH_CHECK("wgrad_reduce_kernel");
+        if (r || !dbias || swap) return r;
+        // [nsplit][M] partials = a [nsplit][1][M][1] slab: the same parallel deterministic reduce
+        hipLaunchKernelGGL(wgrad_reduce_kernel<LX>, dim3(ceil_div(d->M, outb)), dim3(256), 0, st,
+                           (const float*)bias_ws, p.nsplit, 1, d->M, 1, dbias, 1, 0, 0, d->accumulate);
+        return HY_LAUNCH_CHECK("wgrad_reduce_kernel(bias)");
+    };
+    if (lx == 16) rc = reduce(std::integral_constant<int, 16>{});
+    else if (lx == 8) rc = reduce(std::integral_constant<int, 8>{});
+    else rc = reduce(std::integral_constant<int, 4>{});
+    if (rc || !dbias || !swap) return rc;
     if (swap) {  // P (= dY) is the tap-folded side here: plain column sums
         const int P = d0->B * d0->Hq * d0->Wq;
         return hyres_colsum(p_orig, P, d0->M, d0->ldp, dbias, d0->accumulate, bias_ws,
                             hyres_colsum_workspace_bytes(P, d0->M), s);
     }
-    // [nsplit][M] partials = a [nsplit][1][M][1] slab: the same parallel deterministic reduce
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(ceil_div(d->M, 64)), dim3(256), 0, st, (const float*)bias_ws, p.nsplit,
-                       1, d->M, 1, dbias, 1, 0, 0, d->accumulate);
-    return HY_LAUNCH_CHECK("wgrad_reduce_kernel(bias)");
+    return 0;
 }
 
 static int colsum_blocks(int P) {
