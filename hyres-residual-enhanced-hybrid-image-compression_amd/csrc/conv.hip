@@ -37,6 +37,7 @@ struct ConvArgs {
     float* slab; // [nsplit][nphase][M][Co] partials when nsplit > 1
     int vec4;    // every epilogue operand 16B aligned with ld % 4 == 0 and Co % 4 == 0
     int w_bytes; // bytes of W2 (buffer-resource range)
+    int xcd;     // 1: grid.x = M tiles x N tiles in XCD-aware order (grid.y = 1)
 };
 
 
@@ -173,8 +174,22 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const ConvArgs a) {
     const int nsplit = SPLITK ? a.nsplit : 1;
     const int phase = blockIdx.z / nsplit;
     const int split = blockIdx.z - phase * nsplit;
-    const int m0 = blockIdx.x * BM;
-    const int n0 = blockIdx.y * BN;
+    // XCD-aware tile order (a.xcd): hardware block b runs on XCD b % 8, so XCD x gets the contiguous
+    // logical range [x*q + min(x, r), ...) of the nb = q*8 + r tiles (a bijection for any nb); within
+    // it the N tiles of one M tile are adjacent. Neighbouring pixel tiles (the 3x3/5x5 halo rows) and
+    // the N tiles sharing an A tile then hit one L2 instead of being spread over all eight.
+    int m0, n0;
+    if (a.xcd) {
+        const int nb = gridDim.x, hw = blockIdx.x;
+        const int q = nb >> 3, r = nb & 7, x = hw & 7;
+        const int l = x * q + min(x, r) + (hw >> 3);
+        const int ntn = (g.Co + BN - 1) / BN;
+        m0 = (l / ntn) * BM;
+        n0 = (l - (l / ntn) * ntn) * BN;
+    } else {
+        m0 = blockIdx.x * BM;
+        n0 = blockIdx.y * BN;
+    }
     const int HqWq = g.Hq * g.Wq;
     const int ntap = g.ntap[phase];
     const int tap0 = g.tap0[phase];
@@ -1200,6 +1215,7 @@ template <int TM, int TN, int WM_, int WN_>
 static int launch_fwd(const ConvArgs& a, int mode, hipStream_t st) {
     constexpr int BM = 32 * TM * WM_, BN = 32 * TN * WN_;
     dim3 grid(ceil_div(a.M, BM), ceil_div(a.g.Co, BN), a.g.nphase * a.nsplit);
+    if (a.xcd) grid = dim3(grid.x * grid.y, 1, grid.z);
     if (a.e.f16_operands && mode != 2) {
         if (a.nsplit > 1) {
             if (mode == 0) hipLaunchKernelGGL((conv_fwd_kernel<TM, TN, WM_, WN_, 0, true, true>), grid, dim3(256), 0, st, a);
@@ -1455,6 +1471,8 @@ int hyres_conv_forward(const hyres_conv_geom* g, const float* x, const float* w2
     ConvArgs a;
     a.g = *g; a.x = x; a.w2 = w2; a.ldw = ldw; a.y = y; a.e = *e;
     a.M = g->B * g->Hq * g->Wq;
+    static const int xcd_order = env_int("HYRES_CONV_XCD", 1);
+    a.xcd = xcd_order;
     ConvPlan plan = conv_plan(g);
     a.nsplit = 1;
     a.cps = 0;
