@@ -1456,6 +1456,29 @@ static ConvPlan conv_plan(const hyres_conv_geom* g) {
     return p;
 }
 
+// Kernel choice of hyres_conv_forward, shared with hyres_conv_kernel_name (the profiler's label).
+// tile: 0 = <2,2,2,2> (128x128), 1 = <2,1,2,2> (128x64), 2 = <1,1,4,1> (128x32), 3 = <1,2,2,2> and
+// 4 = <1,1,2,2> (half-height tiles for short-K 1x1 layers: the <= 4-chunk main loop cannot hide the
+// operand and epilogue latencies, so twice as many blocks go in flight)
+struct ConvChoice {
+    bool narrow;
+    int tile, mode;
+};
+
+static ConvChoice choose_conv(const hyres_conv_geom* g, const hyres_epilogue* e, bool split, bool aligned) {
+    ConvChoice c{};
+    c.mode = (g->Ci % KT == 0) ? (e->square_input ? 1 : 0) : 2;
+    c.narrow = narrow_ok(g) && !e->square_input && e->kind == HYRES_EPI_BIAS && aligned;
+    static const int shortk = env_int("HYRES_CONV_SHORTK", 1);
+    const bool short_k = shortk && !split && c.mode != 2 && g->nphase == 1 && g->ntaps == 1 && g->Ci <= 4 * KT;
+    if (short_k && g->Co > 64) c.tile = 3;
+    else if (short_k && g->Co > 32) c.tile = 4;
+    else if (g->Co > 64) c.tile = 0;
+    else if (g->Co > 32) c.tile = 1;
+    else c.tile = 2;
+    return c;
+}
+
 long long hyres_conv_workspace_bytes(const hyres_conv_geom* g) {
     if (!g || narrow_ok(g)) return 0;
     ConvPlan p = conv_plan(g);
@@ -1514,8 +1537,9 @@ int hyres_conv_forward(const hyres_conv_geom* g, const float* x, const float* w2
     if (e->act == HYRES_ACT_RELU_MASK)
         HY_REQUIRE(e->aux0 && e->kind == HYRES_EPI_BIAS, HYRES_E_ARG, "conv: ReLU mask needs aux0, BIAS epilogue");
     hipStream_t st = as_stream(s);
-    if (narrow_ok(g) && !e->square_input && e->kind == HYRES_EPI_BIAS && aligned16(x) &&
-        aligned16(w2) && g->ldx % 4 == 0 && ldw % 4 == 0) {
+    const ConvChoice ch = choose_conv(g, e, a.nsplit > 1,
+                                      aligned16(x) && aligned16(w2) && g->ldx % 4 == 0 && ldw % 4 == 0);
+    if (ch.narrow) {
         a.nsplit = 1;
         dim3 grid(ceil_div(a.M, NARROW_PIX), g->nphase);
         switch (g->Co) {
@@ -1527,15 +1551,13 @@ int hyres_conv_forward(const hyres_conv_geom* g, const float* x, const float* w2
         return HY_LAUNCH_CHECK("conv_narrow_kernel");
     }
     int rc;
-    // short-K layers (1x1 convs, <= 4 K chunks): the main loop is too short to hide the operand and
-    // epilogue latencies, so half-height tiles put twice as many blocks in flight
-    static const int shortk = env_int("HYRES_CONV_SHORTK", 1);
-    const bool short_k = shortk && a.nsplit == 1 && mode != 2 && g->nphase == 1 && g->ntaps == 1 && g->Ci <= 4 * KT;
-    if (short_k && g->Co > 64) rc = launch_fwd<1, 2, 2, 2>(a, mode, st);
-    else if (short_k && g->Co > 32) rc = launch_fwd<1, 1, 2, 2>(a, mode, st);
-    else if (g->Co > 64) rc = launch_fwd<2, 2, 2, 2>(a, mode, st);
-    else if (g->Co > 32) rc = launch_fwd<2, 1, 2, 2>(a, mode, st);
-    else rc = launch_fwd<1, 1, 4, 1>(a, mode, st);
+    switch (ch.tile) {
+        case 0: rc = launch_fwd<2, 2, 2, 2>(a, mode, st); break;
+        case 1: rc = launch_fwd<2, 1, 2, 2>(a, mode, st); break;
+        case 3: rc = launch_fwd<1, 2, 2, 2>(a, mode, st); break;
+        case 4: rc = launch_fwd<1, 1, 2, 2>(a, mode, st); break;
+        default: rc = launch_fwd<1, 1, 4, 1>(a, mode, st); break;
+    }
     if (rc || a.nsplit == 1) return rc;
     long long total = (long long)a.M * g->Co * g->nphase;
     if (a.vec4) {
@@ -1546,6 +1568,20 @@ int hyres_conv_forward(const hyres_conv_geom* g, const float* x, const float* w2
     int blocks = (int)std::min<long long>((total + 255) / 256, 8192);
     hipLaunchKernelGGL(conv_splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, a);
     return HY_LAUNCH_CHECK("conv_splitk_reduce_kernel");
+}
+
+int hyres_conv_kernel_name(const hyres_conv_geom* g, const hyres_epilogue* e, int split, char* buf, int n) {
+    HY_REQUIRE(g && e && buf && n > 0, HYRES_E_ARG, "conv_kernel_name: bad args");
+    const ConvChoice ch = choose_conv(g, e, split != 0, true);
+    if (ch.narrow) {
+        snprintf(buf, n, "conv_narrow_kernel<%d, %d>", std::min(g->Co, 4), g->Ci == 64 ? 1 : 2);
+        return 0;
+    }
+    static const char* tiles[5] = {"2, 2, 2, 2", "2, 1, 2, 2", "1, 1, 4, 1", "1, 2, 2, 2", "1, 1, 2, 2"};
+    const bool f16 = e->f16_operands && ch.mode != 2;
+    snprintf(buf, n, "conv_fwd_kernel<%s, %d, %s, %s>", tiles[ch.tile], ch.mode, split ? "true" : "false",
+             f16 ? "true" : "false");
+    return 0;
 }
 
 int hyres_wgrad_desc_conv2d(hyres_wgrad_desc* d, int B, int H, int W, int Ci, int ldx, int Co, int ldy,

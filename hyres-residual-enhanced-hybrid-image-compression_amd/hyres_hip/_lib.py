@@ -75,6 +75,7 @@ _SIGS = {
     "hyres_conv_forward": (_I, [ctypes.POINTER(ConvGeom), _P, _P, _I, _P, ctypes.POINTER(Epilogue), _P, _LL,
                                 _P]),
     "hyres_conv_workspace_bytes": (_LL, [ctypes.POINTER(ConvGeom)]),
+    "hyres_conv_kernel_name": (_I, [ctypes.POINTER(ConvGeom), ctypes.POINTER(Epilogue), _I, ctypes.c_char_p, _I]),
     "hyres_wgrad_desc_conv2d": (_I, [ctypes.POINTER(WgradDesc)] + [_I] * 12),
     "hyres_wgrad_desc_deconv2d": (_I, [ctypes.POINTER(WgradDesc)] + [_I] * 9),
     "hyres_wgrad_workspace_bytes": (_LL, [ctypes.POINTER(WgradDesc)]),

@@ -459,17 +459,11 @@ class KernelTimer:
 
 
 def conv_variant(g: L.ConvGeom, e: L.Epilogue, splitk: bool) -> str:
-    """The conv_fwd_kernel<TM, TN, WAVES_M, WAVES_N, MODE, SPLITK> hyres_conv_forward launches."""
-    mode = (1 if e.square_input else 0) if g.Ci % 32 == 0 else 2
-    # short-K 1x1 layers take half-height tiles (conv.hip, HYRES_CONV_SHORTK, default on)
-    short_k = (os.environ.get("HYRES_CONV_SHORTK", "1") not in ("", "0") and not splitk and mode != 2
-               and g.nphase == 1 and g.ntaps == 1 and g.Ci <= 128 and g.Co > 32)
-    if short_k:
-        tile = "1, 2, 2, 2" if g.Co > 64 else "1, 1, 2, 2"
-    else:
-        tile = "2, 2, 2, 2" if g.Co > 64 else ("2, 1, 2, 2" if g.Co > 32 else "1, 1, 4, 1")
-    f16 = "true" if (e.f16_operands and mode != 2) else "false"
-    return f"conv_fwd_kernel<{tile}, {mode}, {'true' if splitk else 'false'}, {f16}>"
+    """The kernel hyres_conv_forward launches for (g, e), named by the launcher itself
+    (hyres_conv_kernel_name: the same choice function, so the label cannot drift from the routing)."""
+    buf = ctypes.create_string_buffer(96)
+    L.call("hyres_conv_kernel_name", ctypes.byref(g), ctypes.byref(e), int(bool(splitk)), buf, len(buf))
+    return buf.value.decode()
 
 
 def conv_flops(g: L.ConvGeom) -> float:

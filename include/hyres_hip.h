@@ -126,6 +126,11 @@ int hyres_conv_forward(const hyres_conv_geom* g, const float* x, const float* w2
 /* Scratch for split-K on small-M layers (0 = none needed).  Passing a NULL / short workspace is
  * valid: the launch then runs unsplit (same result, fewer blocks in flight). */
 long long hyres_conv_workspace_bytes(const hyres_conv_geom* g);
+/* Name of the kernel hyres_conv_forward launches for (g, e) — split != 0 when a workspace of
+ * hyres_conv_workspace_bytes(g) is passed — as rocprof prints it, e.g.
+ * "conv_fwd_kernel<2, 1, 2, 2, 0, false, false>" (16B-aligned operands assumed).  Host-only, no
+ * launch: the profiling label of bench.py's roofline line comes from the launcher's own choice. */
+int hyres_conv_kernel_name(const hyres_conv_geom* g, const hyres_epilogue* e, int split, char* buf, int n);
 
 /* Weight gradient:  dW[t][m][n] = sum_q P[q][m] * Q[shift_t(q)][n]  over a base grid q (B,Hq,Wq).
  * Conv2d: P = dY (output grid), Q = X;  ConvTranspose2d: P = X (input grid), Q = dY.

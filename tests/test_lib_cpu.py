@@ -123,3 +123,32 @@ def test_rans_roundtrip_and_bitstream_matches_restatement():
                                                dec.ctypes.data), "dec")
     assert np.array_equal(dec, sym)
     assert rans_decode(ref, idx.tolist(), cdf.tolist(), lengths.tolist(), offsets.tolist()) == sym.tolist()
+
+
+def test_conv_kernel_name_follows_the_launch_routing():
+    """hyres_conv_kernel_name (the profiler label bench.py's roofline line uses) reports the launcher's
+    own tile choice: 128x64 tiles for 3x3 64-channel layers, half-height tiles for short-K 1x1 layers,
+    the VALU narrow kernel for <= 4 output channels, split-K / fp16 / GDN-square flags."""
+    from hyres_hip import _lib as L
+    from hyres_hip.ops import _geom, conv_variant
+    e = L.Epilogue()
+    e.kind = L.EPI_BIAS
+    g3 = _geom("hyres_geom_conv2d", 16, 128, 128, 64, 64, 64, 64, 3, 3, 1, 1, 1)
+    assert conv_variant(g3, e, False) == "conv_fwd_kernel<2, 1, 2, 2, 0, false, false>"
+    assert conv_variant(g3, e, True) == "conv_fwd_kernel<2, 1, 2, 2, 0, true, false>"
+    g1 = _geom("hyres_geom_conv2d", 16, 128, 128, 64, 64, 128, 128, 1, 1, 1, 0, 1)
+    assert conv_variant(g1, e, False) == "conv_fwd_kernel<1, 2, 2, 2, 0, false, false>"
+    g1b = _geom("hyres_geom_conv2d", 16, 256, 256, 192, 192, 64, 64, 1, 1, 1, 0, 1)  # K = 192: not short
+    assert conv_variant(g1b, e, False) == "conv_fwd_kernel<2, 1, 2, 2, 0, false, false>"
+    g1c = _geom("hyres_geom_conv2d", 16, 128, 128, 128, 128, 64, 64, 1, 1, 1, 0, 1)
+    assert conv_variant(g1c, e, False) == "conv_fwd_kernel<1, 1, 2, 2, 0, false, false>"
+    gn = _geom("hyres_geom_conv2d", 16, 256, 256, 64, 64, 3, 3, 3, 3, 1, 1, 1)
+    assert conv_variant(gn, e, False) == "conv_narrow_kernel<3, 1>"
+    gs = _geom("hyres_geom_conv2d", 16, 256, 256, 3, 3, 64, 64, 3, 3, 1, 1, 1)  # Ci = 3: scalar path
+    assert conv_variant(gs, e, False) == "conv_fwd_kernel<2, 1, 2, 2, 2, false, false>"
+    e.square_input = 1
+    g2 = _geom("hyres_geom_conv2d", 16, 128, 128, 128, 128, 128, 128, 1, 1, 1, 0, 1)
+    assert conv_variant(g2, e, False) == "conv_fwd_kernel<1, 2, 2, 2, 1, false, false>"
+    e.square_input = 0
+    e.f16_operands = 1
+    assert conv_variant(g3, e, False) == "conv_fwd_kernel<2, 1, 2, 2, 0, false, true>"
