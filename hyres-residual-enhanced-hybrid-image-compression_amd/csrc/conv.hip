@@ -597,14 +597,21 @@ __global__ __launch_bounds__(256) void conv_narrow_kernel(const ConvArgs a) {
     __syncthreads();
 
     const int HqWq = g.Hq * g.Wq;
-    const int b0 = (blockIdx.x * NARROW_PIX) / HqWq;
+    // XCD-aware pixel-tile order (as conv_fwd_kernel): neighbouring rows' tiles, which share the 3x3
+    // halo, run on one XCD's L2
+    int bx = blockIdx.x;
+    if (a.xcd) {
+        const int nb = gridDim.x, q = nb >> 3, r = nb & 7, x = bx & 7;
+        bx = x * q + min(x, r) + (bx >> 3);
+    }
+    const int b0 = (bx * NARROW_PIX) / HqWq;
     const long long img = (long long)g.Hi * g.Wi * g.ldx;
     const long long xrem = ((long long)g.B - b0) * img * 4;
     const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(a.x + (long long)b0 * img), (short)0, (int)(xrem < 0x7FFFFFF0LL ? xrem : 0x7FFFFFF0LL), 0x00020000);
     const int l16 = tid & 15, slot = tid >> 4;  // 16 pixel slots per block pass
     for (int it = 0; it < NARROW_PIX / 16; ++it) {
-        const int m = blockIdx.x * NARROW_PIX + it * 16 + slot;
+        const int m = bx * NARROW_PIX + it * 16 + slot;
         const bool ok = m < a.M;
         const int mm = ok ? m : 0;
         const int b = mm / HqWq;
