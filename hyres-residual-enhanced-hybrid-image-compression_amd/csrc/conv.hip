@@ -38,6 +38,7 @@ struct ConvArgs {
     int vec4;    // every epilogue operand 16B aligned with ld % 4 == 0 and Co % 4 == 0
     int w_bytes; // bytes of W2 (buffer-resource range)
     int xcd;     // 1: grid.x = M tiles x N tiles in XCD-aware order (grid.y = 1)
+    int prio;    // 1: raise the wave priority while it issues its MFMA cluster (s_setprio)
 };
 
 
@@ -369,6 +370,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const ConvArgs a) {
             }
             continue;
         }
+        if (a.prio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             float4 af[TM], bf[TN];
@@ -391,6 +393,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const ConvArgs a) {
                         acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[tm][tn], 0, 0, 0);
                     }
         }
+        if (a.prio) __builtin_amdgcn_s_setprio(0);
     }
 
     // ---- epilogue: stage the accumulators through LDS one TN column slice at a time (static register
@@ -1502,7 +1505,9 @@ int hyres_conv_forward(const hyres_conv_geom* g, const float* x, const float* w2
     a.g = *g; a.x = x; a.w2 = w2; a.ldw = ldw; a.y = y; a.e = *e;
     a.M = g->B * g->Hq * g->Wq;
     static const int xcd_order = env_int("HYRES_CONV_XCD", 1);
+    static const int mfma_prio = env_int("HYRES_CONV_PRIO", 1);
     a.xcd = xcd_order;
+    a.prio = mfma_prio;
     ConvPlan plan = conv_plan(g);
     a.nsplit = 1;
     a.cps = 0;
