@@ -351,6 +351,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const ConvArgs a) {
         if (kc + 1 < kend) load_chunk(kc + 1);
         if constexpr (F16) {
             typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+            if (a.prio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
             for (int s16 = 0; s16 < 2; ++s16) {
                 half8 af[TM], bf[TN];
@@ -368,6 +369,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const ConvArgs a) {
                     for (int tn = 0; tn < TN; ++tn)
                         acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[tm], bf[tn], acc[tm][tn], 0, 0, 0);
             }
+            if (a.prio) __builtin_amdgcn_s_setprio(0);
             continue;
         }
         if (a.prio) __builtin_amdgcn_s_setprio(1);
