@@ -361,25 +361,76 @@ __global__ void rd_bwd_coef_kernel(const float* g0, const float* g1, const float
 }
 
 // ---------------------------------------------------------------- Adam (torch.optim.Adam, foreach math)
-__global__ void adam_kernel(float* p, const float* g, float* m, float* v, long long n, float lr, float b1,
-                            float b2, float eps, float bc1, float bc2_sqrt, const float* sumsq, float max_norm) {
+// torch computes 1-beta, the bias corrections, step_size and sqrt(bc2) in Python double precision and
+// hands them to the fp32 foreach kernels as scalars; the same is done here per thread (the step count
+// lives on the device so that a skipped step — GradScaler found_inf — needs no host round trip).
+struct AdamHyper {
+    double lr, beta1, beta2, eps, max_norm;
+    float omb1, omb2, epsf;  // (float)(1 - beta) computed in double, (float)eps
+};
+
+// skip: 0 never; 1 when sumsq is not finite (GradScaler found_inf); 2 when sumsq is NaN
+__device__ __forceinline__ bool adam_skip(const float* sumsq, int skip) {
+    if (!skip || !sumsq) return false;
+    const float v = sumsq[0];
+    return skip == 1 ? !isfinite(v) : isnan(v);
+}
+
+__global__ void adam_kernel(float* p, const float* g, float* m, float* v, long long n, AdamHyper h,
+                            const float* step_dev, const float* sumsq, const float* gscale, int skip) {
+    if (adam_skip(sumsq, skip)) return;
+    const double t = (double)step_dev[0] + 1.0;
+    const double bc1 = 1.0 - pow(h.beta1, t);
+    const double bc2 = 1.0 - pow(h.beta2, t);
+    const float step_size = (float)(h.lr / bc1);
+    const float bc2_sqrt = (float)sqrt(bc2);
+    const float gs = gscale ? gscale[0] : 1.0f;  // GradScaler unscale_: grad * inv_scale
     float clip = 1.0f;
-    if (sumsq) {
-        float total = sqrtf(sumsq[0]);
-        float coef = max_norm / (total + 1e-6f);
+    if (sumsq && h.max_norm > 0.0) {
+        // clip_grad_norm_ on the unscaled gradient: total = ||g * gs|| = sqrt(sumsq) * gs
+        const float total = sqrtf(sumsq[0]) * gs;
+        const float coef = (float)h.max_norm / (total + 1e-6f);
         clip = fminf(coef, 1.0f);
     }
-    const float step_size = lr / bc1;
     GRID_STRIDE(i, n) {
-        float gv = g[i] * clip;
+        float gv = g[i];
+        if (gscale) gv = gv * gs;
+        gv = gv * clip;
         float mv = m[i];
-        mv = mv + (1.0f - b1) * (gv - mv);  // lerp_(grad, 1-beta1)
-        float vv = v[i] * b2 + (1.0f - b2) * gv * gv;
+        mv = mv + h.omb1 * (gv - mv);                             // exp_avg.lerp_(grad, 1-beta1)
+        const float vv = v[i] * (float)h.beta2 + h.omb2 * (gv * gv);  // mul_(beta2).addcmul_(g, g, 1-beta2)
         m[i] = mv;
         v[i] = vv;
-        float denom = sqrtf(vv) / bc2_sqrt + eps;
+        const float denom = sqrtf(vv) / bc2_sqrt + h.epsf;
         p[i] = p[i] - step_size * (mv / denom);
     }
+}
+
+__global__ void adam_finish_kernel(float* step_dev, const float* sumsq, int skip) {
+    if (threadIdx.x == 0 && !adam_skip(sumsq, skip)) step_dev[0] = step_dev[0] + 1.0f;
+}
+
+// torch.amp.GradScaler.update (aten _amp_update_scale_): found_inf = !isfinite(sumsq of the scaled grads)
+__global__ void grad_scaler_update_kernel(const float* sumsq, float* scale, float* inv_scale, int* tracker,
+                                          float growth, float backoff, int interval) {
+    if (threadIdx.x != 0) return;
+    const bool found_inf = !isfinite(sumsq[0]);
+    float s = scale[0];
+    if (found_inf) {
+        s = s * backoff;
+        tracker[0] = 0;
+    } else {
+        const int succ = tracker[0] + 1;
+        if (succ == interval) {
+            const float ns = s * growth;
+            if (isfinite(ns)) s = ns;
+            tracker[0] = 0;
+        } else {
+            tracker[0] = succ;
+        }
+    }
+    scale[0] = s;
+    inv_scale[0] = (float)(1.0 / (double)s);  // scale.double().reciprocal().float()
 }
 
 }  // namespace hyres
@@ -598,15 +649,34 @@ int hyres_rd_bwd_coef(const float* g0, const float* g1, const float* g2, const f
                        (float)npx, (float)nel, coef);
     return HY_LAUNCH_CHECK("rd_bwd_coef");
 }
-int hyres_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, long long n, float lr,
-                    float beta1, float beta2, float eps, int step, const float* sumsq, float max_norm,
-                    hyres_stream_t s) {
-    HY_REQUIRE(param && grad && exp_avg && exp_avg_sq && step >= 1, HYRES_E_ARG, "adam: bad args");
-    double bc1 = 1.0 - std::pow((double)beta1, step);
-    double bc2 = 1.0 - std::pow((double)beta2, step);
+int hyres_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, long long n, double lr,
+                    double beta1, double beta2, double eps, float* step_dev, const float* sumsq, double max_norm,
+                    const float* gscale, int skip, hyres_stream_t s) {
+    HY_REQUIRE(param && grad && exp_avg && exp_avg_sq && step_dev, HYRES_E_ARG, "adam: NULL");
+    HY_REQUIRE(skip >= 0 && skip <= 2 && (skip == 0 || sumsq), HYRES_E_ARG, "adam: skip mode %d needs sumsq", skip);
+    AdamHyper h;
+    h.lr = lr;
+    h.beta1 = beta1;
+    h.beta2 = beta2;
+    h.eps = eps;
+    h.max_norm = max_norm;
+    h.omb1 = (float)(1.0 - beta1);
+    h.omb2 = (float)(1.0 - beta2);
+    h.epsf = (float)eps;
     hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n, 4)), dim3(256), 0, as_stream(s), param, grad, exp_avg,
-                       exp_avg_sq, n, lr, beta1, beta2, eps, (float)bc1, (float)std::sqrt(bc2), sumsq, max_norm);
-    return HY_LAUNCH_CHECK("adam");
+                       exp_avg_sq, n, h, (const float*)step_dev, sumsq, gscale, skip);
+    int rc = HY_LAUNCH_CHECK("adam");
+    if (rc) return rc;
+    hipLaunchKernelGGL(adam_finish_kernel, dim3(1), dim3(64), 0, as_stream(s), step_dev, sumsq, skip);
+    return HY_LAUNCH_CHECK("adam_finish");
+}
+int hyres_grad_scaler_update(const float* sumsq, float* scale, float* inv_scale, int* growth_tracker,
+                             double growth_factor, double backoff_factor, int growth_interval, hyres_stream_t s) {
+    HY_REQUIRE(sumsq && scale && inv_scale && growth_tracker && growth_interval > 0, HYRES_E_ARG,
+               "grad_scaler_update: bad args");
+    hipLaunchKernelGGL(grad_scaler_update_kernel, dim3(1), dim3(64), 0, as_stream(s), sumsq, scale, inv_scale,
+                       growth_tracker, (float)growth_factor, (float)backoff_factor, growth_interval);
+    return HY_LAUNCH_CHECK("grad_scaler_update");
 }
 
 }  // extern "C"

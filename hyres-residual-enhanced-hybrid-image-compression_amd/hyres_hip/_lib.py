@@ -55,6 +55,7 @@ _P = ctypes.c_void_p
 _I = ctypes.c_int
 _LL = ctypes.c_longlong
 _F = ctypes.c_float
+_D = ctypes.c_double
 _ULL = ctypes.c_ulonglong
 _PP = ctypes.POINTER(ctypes.c_void_p)
 
@@ -136,7 +137,8 @@ _SIGS = {
     "hyres_sumsq": (_I, [_P, _LL, _P, _P, _LL, _P]),
     "hyres_rd_finalize": (_I, [_P, _P, _F, _LL, _LL, _PP, _P]),
     "hyres_rd_bwd_coef": (_I, [_P, _P, _P, _P, _P, _P, _F, _LL, _LL, _P, _P]),
-    "hyres_adam_step": (_I, [_P, _P, _P, _P, _LL, _F, _F, _F, _F, _I, _P, _F, _P]),
+    "hyres_adam_step": (_I, [_P, _P, _P, _P, _LL, _D, _D, _D, _D, _P, _P, _D, _P, _I, _P]),
+    "hyres_grad_scaler_update": (_I, [_P, _P, _P, _P, _D, _D, _I, _P]),
 }
 
 _lib: Optional[ctypes.CDLL] = None

@@ -45,27 +45,29 @@ def _pmf_to_cdf(pmf: torch.Tensor, tail_mass: torch.Tensor, pmf_length: torch.Te
 def _logits_cumulative(eb, inputs: torch.Tensor) -> torch.Tensor:
     logits = inputs
     for i in range(len(eb.filters) + 1):
-        matrix = torch.nn.functional.softplus(getattr(eb, f"_matrix{i:d}").detach())
+        matrix = torch.nn.functional.softplus(getattr(eb, f"_matrix{i:d}").detach().cpu())
         logits = torch.matmul(matrix, logits)
-        logits = logits + getattr(eb, f"_bias{i:d}").detach()
+        logits = logits + getattr(eb, f"_bias{i:d}").detach().cpu()
         if i < len(eb.filters):
-            logits = logits + torch.tanh(getattr(eb, f"_factor{i:d}").detach()) * torch.tanh(logits)
+            logits = logits + torch.tanh(getattr(eb, f"_factor{i:d}").detach().cpu()) * torch.tanh(logits)
     return logits
 
 
 @torch.no_grad()
 def eb_update(eb, force: bool = False) -> bool:
-    """compressai EntropyBottleneck.update (1.2.6)."""
+    """compressai EntropyBottleneck.update (1.2.6).  Evaluated on the host in fp32, as the reference runs it
+    (src/updata.py:50-53 updates a CPU-loaded model): the CDF tables are then bit-identical to the
+    reference's for the same parameters, whatever device the model lives on."""
     if eb._offset.numel() > 0 and not force:
         return False
-    q = eb.quantiles.detach()
+    q = eb.quantiles.detach().cpu()
     medians = q[:, 0, 1]
     minima = torch.clamp(torch.ceil(medians - q[:, 0, 0]).int(), min=0)
     maxima = torch.clamp(torch.ceil(q[:, 0, 2] - medians).int(), min=0)
     pmf_start = medians - minima
     pmf_length = maxima + minima + 1
     max_length = int(pmf_length.max().item())
-    samples = torch.arange(max_length, device=q.device)[None, :] + pmf_start[:, None, None]
+    samples = torch.arange(max_length)[None, :] + pmf_start[:, None, None]
     lower = _logits_cumulative(eb, samples - 0.5)
     upper = _logits_cumulative(eb, samples + 0.5)
     sign = -torch.sign(lower + upper)

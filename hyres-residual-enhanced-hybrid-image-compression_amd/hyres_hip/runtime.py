@@ -62,7 +62,12 @@ class TapeFunction(torch.autograd.Function):
                 in_grads.append(None)
             else:
                 in_grads.append(O.to_nchw_grad(node))
+        # drop every reference to the step's activations: a loss tensor kept alive by the caller (metrics)
+        # must not pin the tape's NHWC buffers and their gradients
         ctx.tape = None
+        ctx.in_nodes = None
+        ctx.out_nodes = None
+        ctx.spec = None
         return (None, None) + tuple(in_grads) + (None,) * ctx.n_params
 
 

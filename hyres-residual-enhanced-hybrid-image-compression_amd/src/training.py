@@ -8,6 +8,7 @@ import argparse
 import os
 import random
 import sys
+import warnings
 
 import torch
 from torch.utils.data import DataLoader
@@ -60,6 +61,11 @@ class _NullWriter:
 
 def main(argv):
     args = parse_args(argv)
+    if args.alpha != 0:
+        # RateDistortionLoss's VGG16 term (src/losses/vgg16.py) needs torchvision's ImageNet weights, which
+        # are not available offline; train.sh runs with --alpha 0.  Fail before any data is touched.
+        raise SystemExit(f"--alpha {args.alpha}: the VGG perceptual term is not available in this build "
+                         f"(pass --alpha 0, as train.sh does)")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -145,10 +151,12 @@ def main(argv):
         writer.add_scalar("Test/loss", loss, epoch)
         writer.add_scalar("Test/mse", mse, epoch)
         writer.add_scalar("Test/bpp", bpp, epoch)
-        if isinstance(lr_scheduler, torch.optim.lr_scheduler.ReduceLROnPlateau):
+        # src/training.py:265 calls lr_scheduler.step(loss) for BOTH schedulers; on MultiStepLR that is the
+        # deprecated step(epoch=loss) whose closed form gives lr = base * 0.1 ** bisect([400], loss): with a
+        # loss of O(1) the learning rate never decays.  Mirrored (drop-in training schedule), not fixed.
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore", UserWarning)
             lr_scheduler.step(loss)
-        else:
-            lr_scheduler.step()
         is_best = loss < best_loss
         if args.save and rank == 0:
             state = {"epoch": epoch, "state_dict": net.state_dict(), "loss": loss,

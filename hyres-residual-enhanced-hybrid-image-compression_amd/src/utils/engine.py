@@ -5,11 +5,18 @@ Differences from the reference, by design:
     read back only when printing (every ``log_every`` steps) — the step itself never syncs;
   * clip_grad_norm_ + Adam are one fused HIP launch (hyres_hip.optim.FusedAdam(max_grad_norm=...));
   * with data parallelism the flat gradient is all-reduced over RCCL before the step (hyres_hip.ddp);
-  * ``mixed_precision`` is accepted for CLI compatibility; the HIP kernels compute in fp32 (the
-    reference's numerics), so autocast/GradScaler are not used.
+  * ``mixed_precision`` (train.sh:19) keeps the reference's semantics — the forward runs under
+    ``torch.autocast("cuda", float16)`` (the HIP convolutions then take fp16 operands on the f16 MFMA with
+    fp32 accumulation), the loss is scaled by a GradScaler (init 2^16, growth 2 / 2000 steps, backoff 0.5,
+    one per epoch as engine.py:23 creates it), gradients are unscaled before clipping, a step with
+    non-finite gradients is skipped and backs the scale off, and a NaN gradient also skips the aux step
+    (engine.py:60-74) — with the scaler state, the skip decision and the step count all on the device
+    (hyres_hip.optim.DeviceGradScaler), so there is still no per-step host sync.  The reference's NaN
+    warning is printed when the metrics are drained.
 """
 import os
 import time
+from contextlib import nullcontext
 
 import torch
 
@@ -20,14 +27,23 @@ __all__ = ["train_one_epoch", "test_epoch"]
 _KEYS = ("loss", "bpp_loss", "residual_bpp_loss", "y_bpp_loss", "z_bpp_loss", "mse_loss")
 
 
-def _drain(pending, meters):
-    if not pending:
-        return
-    vals = torch.stack([torch.stack([c[k].detach().reshape(()) for k in _KEYS]) for c in pending]).cpu()
-    for row in vals:
-        for k, v in zip(_KEYS, row.tolist()):
-            meters[k].update(v)
-    pending.clear()
+def _metrics(out_criterion):
+    """Detached device scalars of one step (keeps no reference to the step's autograd graph)."""
+    return torch.stack([out_criterion[k].detach().reshape(()).float() for k in _KEYS])
+
+
+def _drain(pending, meters, nan_flags=None):
+    if pending:
+        vals = torch.stack(pending).cpu()
+        for row in vals:
+            for k, v in zip(_KEYS, row.tolist()):
+                meters[k].update(v)
+        pending.clear()
+    if nan_flags:
+        for f in torch.cat(nan_flags).cpu().tolist():
+            if f != f:  # sum of squares NaN <=> a NaN gradient (engine.py:62-70)
+                print("Warning: NaN gradients detected, skipping update step")
+        nan_flags.clear()
 
 
 def train_one_epoch(model, criterion, train_dataloader, optimizer, aux_optimizer, epoch, clip_max_norm,
@@ -37,36 +53,54 @@ def train_one_epoch(model, criterion, train_dataloader, optimizer, aux_optimizer
     if hasattr(optimizer, "max_grad_norm"):
         optimizer.max_grad_norm = float(clip_max_norm)
     meters = {k: AverageMeter() for k in _KEYS}
-    pending = []
+    pending, nan_flags = [], []
     start = time.time()
+    device = next(model.parameters()).device
+    scaler = None
+    if mixed_precision:
+        from hyres_hip.optim import DeviceGradScaler
+        scaler = DeviceGradScaler(device)  # a fresh scaler per epoch, as engine.py:23
     optimizer.zero_grad()
     aux_optimizer.zero_grad()
     aux_loss = None
-    device = next(model.parameters()).device
+    amp = (lambda: torch.autocast("cuda", dtype=torch.float16)) if mixed_precision else nullcontext
     for i, d in enumerate(train_dataloader):
-        out_net = model(d, noisequant)
-        d = d.to(device)
-        out_criterion = criterion(out_net, d)
-        loss = out_criterion["loss"]
-        if gradient_accumulation_steps != 1:
-            loss = loss / gradient_accumulation_steps
+        with amp():
+            out_net = model(d, noisequant)
+            d = d.to(device)
+            out_criterion = criterion(out_net, d)
+            loss = out_criterion["loss"]
+            if gradient_accumulation_steps != 1:
+                loss = loss / gradient_accumulation_steps
         if reducer is not None:  # overlapped all-reduce only on the accumulation boundary (DDP no_sync)
             reducer.armed = (i + 1) % gradient_accumulation_steps == 0
-        loss.backward()
-        pending.append(out_criterion)
+        pending.append(_metrics(out_criterion))
+        if scaler is not None:
+            scaler.scale_loss(loss).backward()
+        else:
+            loss.backward()
+        del out_net, out_criterion, loss
         if (i + 1) % gradient_accumulation_steps == 0:
             if reducer is not None:
                 reducer.all_reduce()
+            nan_src = None
             if not hasattr(optimizer, "max_grad_norm") and clip_max_norm > 0:
                 torch.nn.utils.clip_grad_norm_(model.parameters(), clip_max_norm)
-            optimizer.step()
+            if scaler is not None:
+                optimizer.step(grad_scaler=scaler)  # unscale_ + clip + skip on inf/NaN (engine.py:57-80)
+                scaler.update(optimizer.sumsq)
+                if clip_max_norm > 0:
+                    nan_src = optimizer.sumsq.clone()
+                    nan_flags.append(nan_src)
+            else:
+                optimizer.step()
             optimizer.zero_grad()
             aux_loss = model.aux_loss()
             aux_loss.backward()
-            aux_optimizer.step()
+            aux_optimizer.step(skip_if_nan=nan_src)  # the reference's ``continue`` skips it on NaN
             aux_optimizer.zero_grad()
         if i % log_every == 0:
-            _drain(pending, meters)
+            _drain(pending, meters, nan_flags)
             print(f"Train epoch {epoch}: [{i * len(d)}/{len(train_dataloader.dataset)} "
                   f"({100. * i / max(len(train_dataloader), 1):.0f}%)]"
                   f"\tLoss: {meters['loss'].val:.3f} |\tBpp loss: {meters['bpp_loss'].val:.3f} |"
@@ -74,7 +108,7 @@ def train_one_epoch(model, criterion, train_dataloader, optimizer, aux_optimizer
                   f"\ty_Bpp loss: {meters['y_bpp_loss'].val:.4f} |\tz_Bpp loss: {meters['z_bpp_loss'].val:.4f} |"
                   f"\tMSE loss: {meters['mse_loss'].val:.3f} |"
                   f"\tAux loss: {float(aux_loss) if aux_loss is not None else 0.0:.2f}")
-    _drain(pending, meters)
+    _drain(pending, meters, nan_flags)
     print(f"Train epoch {epoch}: Average losses:\tLoss: {meters['loss'].avg:.3f} |"
           f"\tBpp loss: {meters['bpp_loss'].avg:.4f} |\tResidual Bpp: {meters['residual_bpp_loss'].avg:.4f} |"
           f"\ty_Bpp loss: {meters['y_bpp_loss'].avg:.5f} |\tz_Bpp loss: {meters['z_bpp_loss'].avg:.5f} |"
@@ -92,7 +126,7 @@ def test_epoch(epoch, test_dataloader, model, criterion, save_images=False, save
         for i, d in enumerate(test_dataloader):
             out_net = model(d)
             d = d.to(device)
-            pending.append(criterion(out_net, d))
+            pending.append(_metrics(criterion(out_net, d)))
             aux_meter.update(float(model.aux_loss()))
             if save_images and i < 6 and savepath:
                 _save_components(out_net, d, os.path.join(savepath, "best_recon"), i)

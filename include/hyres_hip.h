@@ -319,12 +319,24 @@ int hyres_rd_bwd_coef(const float* g0, const float* g1, const float* g2, const f
                       float* coef, hyres_stream_t s);
 /* global L2 norm of a flat buffer -> out[0] = sum sq ; clip factor computed on device */
 int hyres_sumsq(const float* x, long long n, float* out, void* ws, long long ws_bytes, hyres_stream_t s);
-/* fused Adam over a flat parameter buffer (torch.optim.Adam semantics, amsgrad=False,
- * weight_decay=0) with the clip_grad_norm_ factor min(1, max_norm/(sqrt(sumsq)+1e-6)) applied
- * to the gradient on the fly when sumsq != NULL. step is the 1-based step count. */
+/* fused Adam over a flat parameter buffer: torch.optim.Adam (foreach, amsgrad=False, weight_decay=0)
+ * replacing src/utils/engine.py:68-82 (clip_grad_norm_ -> [GradScaler] -> Adam.step). Hyper-parameters
+ * are doubles: 1-beta, the bias corrections, step_size and sqrt(bc2) are formed in double precision as
+ * torch does in Python, then used as fp32 scalars. step_dev: device float = completed steps (incremented
+ * on device unless the step is skipped). sumsq (device, may be NULL): sum of squares of ``grad``;
+ * with max_norm > 0 the clip_grad_norm_ factor min(1, max_norm/(||g*gscale||+1e-6)) is applied on the
+ * fly. gscale (device, may be NULL): GradScaler unscale factor 1/scale. skip: 0 never, 1 skip when
+ * sumsq is not finite (GradScaler.step's found_inf), 2 skip when sumsq is NaN (engine.py:60-74). */
 int hyres_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, long long n,
-                    float lr, float beta1, float beta2, float eps, int step, const float* sumsq,
-                    float max_norm, hyres_stream_t s);
+                    double lr, double beta1, double beta2, double eps, float* step_dev,
+                    const float* sumsq, double max_norm, const float* gscale, int skip,
+                    hyres_stream_t s);
+/* torch GradScaler.update on the device (engine.py:73,80): found_inf = !isfinite(sumsq[0]) of the
+ * scaled gradients; scale *= backoff on inf, *= growth after growth_interval clean steps;
+ * inv_scale = 1/scale. */
+int hyres_grad_scaler_update(const float* sumsq, float* scale, float* inv_scale, int* growth_tracker,
+                             double growth_factor, double backoff_factor, int growth_interval,
+                             hyres_stream_t s);
 
 /* ------------------------------------------------------------------------------------------ */
 /* entropy coding (compress / decompress): compressai 1.2.6 semantics            */

@@ -155,27 +155,110 @@ def rans_decode(data: bytes, indexes, cdfs, cdf_sizes, offsets) -> List[int]:
 
 
 def standardized_cumulative(x):
-    from scipy.special import erfc
-    return 0.5 * erfc(-(2 ** -0.5) * np.asarray(x, dtype=np.float64))
+    """compressai GaussianConditional._standardized_cumulative: 0.5 * erfc(-(2^-0.5) x), torch fp32."""
+    import torch
+    return 0.5 * torch.erfc(-(2 ** -0.5) * torch.as_tensor(np.asarray(x, dtype=np.float32)))
 
 
 def gc_tables(scale_table: Sequence[float], tail_mass: float = 1e-9):
-    """GaussianConditional.update (compressai 1.2.6): (quantized_cdf [n, L+2], cdf_length, offset)."""
+    """GaussianConditional.update (compressai 1.2.6): (quantized_cdf [n, L+2], cdf_length, offset).
+    compressai evaluates the pmf with torch in fp32 (the multiplier with scipy's norm.ppf)."""
+    import torch
     from scipy.stats import norm
-    st = np.asarray(scale_table, dtype=np.float32)
-    multiplier = -norm.ppf(tail_mass / 2)
-    pmf_center = np.ceil(st * np.float32(multiplier)).astype(np.int32)
+    st = torch.as_tensor(np.asarray(scale_table, dtype=np.float32))
+    multiplier = -float(norm.ppf(tail_mass / 2))
+    pmf_center = torch.ceil(st * multiplier).int()
     pmf_length = 2 * pmf_center + 1
     max_length = int(pmf_length.max())
-    samples = np.abs(np.arange(max_length, dtype=np.int32)[None, :] - pmf_center[:, None]).astype(np.float32)
-    scale = st[:, None]
-    upper = standardized_cumulative((np.float32(0.5) - samples) / scale).astype(np.float32)
-    lower = standardized_cumulative((np.float32(-0.5) - samples) / scale).astype(np.float32)
-    pmf = upper - lower
-    tail = 2 * lower[:, :1]
-    cdf = np.zeros((len(st), max_length + 2), dtype=np.int32)
-    for i in range(len(st)):
-        prob = np.concatenate([pmf[i, :pmf_length[i]], tail[i]])
-        c = pmf_to_quantized_cdf(prob)
+    samples = torch.abs(torch.arange(max_length).int() - pmf_center[:, None]).float()
+    scale = st.unsqueeze(1).float()
+    upper = standardized_cumulative((0.5 - samples) / scale)
+    lower = standardized_cumulative((-0.5 - samples) / scale)
+    pmf = (upper - lower).numpy()
+    tail = (2 * lower[:, :1]).numpy()
+    return _pmf_table(pmf, tail, pmf_length.numpy(), max_length), (pmf_length + 2).numpy(), (-pmf_center).numpy()
+
+
+def _pmf_table(pmf, tail, lengths, max_length):
+    """compressai EntropyModel._pmf_to_cdf."""
+    cdf = np.zeros((len(lengths), max_length + 2), dtype=np.int32)
+    for i, n in enumerate(lengths):
+        c = pmf_to_quantized_cdf(np.concatenate([pmf[i, :n], tail[i, :1]]))
         cdf[i, :len(c)] = c
-    return cdf, pmf_length + 2, -pmf_center
+    return cdf
+
+
+def eb_tables(quantiles, logits_cumulative):
+    """EntropyBottleneck.update (compressai 1.2.6) on the host: ``quantiles`` [C,1,3] fp32,
+    ``logits_cumulative(v [C,1,L]) -> [C,1,L]`` the factorized density's cumulative logits."""
+    import torch
+    q = quantiles.detach().float()
+    medians = q[:, 0, 1]
+    minima = torch.clamp(torch.ceil(medians - q[:, 0, 0]).int(), min=0)
+    maxima = torch.clamp(torch.ceil(q[:, 0, 2] - medians).int(), min=0)
+    pmf_start = medians - minima
+    pmf_length = maxima + minima + 1
+    max_length = int(pmf_length.max())
+    samples = torch.arange(max_length)[None, :] + pmf_start[:, None, None]
+    with torch.no_grad():
+        lower = logits_cumulative(samples - 0.5)
+        upper = logits_cumulative(samples + 0.5)
+    sign = -torch.sign(lower + upper)
+    pmf = torch.abs(torch.sigmoid(sign * upper) - torch.sigmoid(sign * lower))[:, 0, :]
+    tail = torch.sigmoid(lower[:, 0, :1]) + torch.sigmoid(-upper[:, 0, -1:])
+    return (_pmf_table(pmf.numpy(), tail.numpy(), pmf_length.numpy(), max_length), (pmf_length + 2).numpy(),
+            (-minima).numpy())
+
+
+def build_indexes(scales, scale_table):
+    """GaussianConditional.build_indexes: LowerBound(0.11) on the scales, then
+    index = len(table) - 1 - #{s in table[:-1] : scales <= s}."""
+    scales = np.maximum(np.asarray(scales, dtype=np.float32), np.float32(0.11))
+    table = np.asarray(scale_table, dtype=np.float32)
+    idx = np.full(scales.shape, len(table) - 1, dtype=np.int32)
+    for s in table[:-1]:
+        idx -= (scales <= s).astype(np.int32)
+    return idx
+
+
+def reference_compress(orc, residual, scale_table):
+    """LightWeightCheckerboard.compress (models/checkerboard.py:167-198) on the functional oracle
+    (oracle/hyres_oracle.py), with compressai 1.2.6's EntropyBottleneck / GaussianConditional compress:
+    symbols = round(v - means) (int), one rANS string per image over the NCHW-flattened symbols,
+    y_anchor_hat / z_hat obtained by decoding (= symbols + means).  Returns
+    ([[anchor_strings, non_anchor_strings], z_strings], intermediates)."""
+    import torch
+    with torch.no_grad():
+        y = orc.g_a(residual)
+        z = orc.h_a(y)
+        k = orc.rp + "entropy_bottleneck."
+        eb_cdf, eb_len, eb_off = eb_tables(orc.p(k + "quantiles"), orc.eb_logits_cumulative)
+        med = orc.eb_medians().reshape(1, -1, 1, 1)
+        z_sym = torch.round(z - med).int()
+        C = z.shape[1]
+        z_idx = np.repeat(np.arange(C, dtype=np.int32), z.shape[2] * z.shape[3])
+        z_strings = [rans_encode(z_sym[b].reshape(-1).tolist(), z_idx.tolist(), eb_cdf.tolist(), eb_len.tolist(),
+                                 eb_off.tolist()) for b in range(z.shape[0])]
+        z_hat = z_sym.float() + med
+        latent = orc.h_s(z_hat)
+        gc_cdf, gc_len, gc_off = gc_tables(scale_table)
+        tables = (gc_cdf.tolist(), gc_len.tolist(), gc_off.tolist())
+        H, W = y.shape[-2:]
+        am = orc.anchor_mask(H, W).to(y.dtype)
+
+        def code(v, scales, means):
+            sym = torch.round(v - means).int()
+            idx = build_indexes(scales.numpy(), scale_table)
+            strings = [rans_encode(sym[b].reshape(-1).tolist(), idx[b].reshape(-1).tolist(), *tables)
+                       for b in range(v.shape[0])]
+            return strings, sym, idx
+
+        s_a, m_a = orc.param_aggregation(torch.cat([latent, torch.zeros_like(latent)], 1)).chunk(2, 1)
+        a_strings, a_sym, a_idx = code(y * am, s_a, m_a)
+        y_anchor_hat = a_sym.float() + m_a
+        ctx = orc.context_prediction(y_anchor_hat)
+        s_n, m_n = orc.param_aggregation(torch.cat([latent, ctx], 1)).chunk(2, 1)
+        n_strings, n_sym, n_idx = code(y * (1 - am), s_n, m_n)
+    inter = {"y": y, "z": z, "z_sym": z_sym, "anchor_sym": a_sym, "anchor_idx": a_idx, "non_anchor_sym": n_sym,
+             "non_anchor_idx": n_idx, "eb_tables": (eb_cdf, eb_len, eb_off), "gc_tables": (gc_cdf, gc_len, gc_off)}
+    return [[a_strings, n_strings], z_strings], inter

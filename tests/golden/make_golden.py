@@ -13,7 +13,9 @@ How the reference is executed:
     BGR, 4:2:2 subsampling — PyTurboJPEG defaults, models/utils/turbo_jpeg_compression.py:35).
 Weights come from the name-keyed recipe in ``hyres_hip/weights.py``; no checkpoint is used.
 
-Outputs (small, committed):  tests/golden/hyres_eval_b2_64.npz, hyres_train_b2_64.npz, meta.json
+Outputs (small, committed):  tests/golden/hyres_eval_b2_64.npz, hyres_train_b2_64.npz,
+  hyres_train_nq_b2_64.{npz,json} (noisequant=True), checkerboard_sets.npz, kodim01_crop64_eval.npz, meta.json
+(``--only-noisequant`` regenerates just the noisequant train step)
 """
 from __future__ import annotations
 
@@ -105,16 +107,82 @@ def grad_summary(net):
     return out
 
 
-def main():
-    torch.set_num_threads(8)
-    hyres_mod, quant_mod = install_reference()
-    q = 50
-    B, H, W = 2, 64, 64
+def synthetic_input(B=2, H=64, W=64):
     g = torch.Generator().manual_seed(1926)
     x = torch.randint(0, 256, (B, 3, H, W), generator=g).float() / 255.0
     # smooth the synthetic image a little so JPEG + residual look like natural content
     x = torch.nn.functional.avg_pool2d(x, 3, 1, 1, count_include_pad=False)
-    x = (x * 255).round() / 255.0
+    return (x * 255).round() / 255.0
+
+
+def train_step_noisequant(hyres_mod, quant_mod, x, q=50, lmbda=0.045):
+    """Train step with ``noisequant=True`` (the reference's default for epochs <= 400, src/training.py:238-243):
+    every U(-.5,.5) draw is recorded in the reference's order EB(z) -> Quantizer(anchor) ->
+    Quantizer(non_anchor) -> GC(y) (models/checkerboard.py:96,121-122,132-133,142)."""
+    from oracle import compressai_restated as cr
+    net, sd = build_reference(hyres_mod, q)
+    net.train()
+    log = []
+    orig_em = cr.EntropyModel.quantize
+    orig_q = quant_mod.Quantizer.quantize
+
+    def rec_em(self, inputs, mode, means=None):
+        if mode == "noise":
+            n = torch.empty_like(inputs).uniform_(-0.5, 0.5)
+            log.append((type(self).__name__, n.clone()))
+            return inputs + n
+        return orig_em(self, inputs, mode, means)
+
+    def rec_q(self, inputs, quantize_type="noise"):
+        if quantize_type == "noise":
+            n = torch.empty_like(inputs).uniform_(-0.5, 0.5)
+            log.append(("Quantizer", n.clone()))
+            return inputs + n
+        return orig_q(self, inputs, quantize_type)
+
+    cr.EntropyModel.quantize = rec_em
+    quant_mod.Quantizer.quantize = rec_q
+    try:
+        torch.manual_seed(4321)
+        out = net(x, noisequant=True)
+    finally:
+        cr.EntropyModel.quantize = orig_em
+        quant_mod.Quantizer.quantize = orig_q
+    names = [n for n, _ in log]
+    assert names == ["EntropyBottleneck", "Quantizer", "Quantizer", "GaussianConditional"], names
+    B, _, H, W = x.shape
+    C = net.residual_model.N
+    nz = log[0][1].reshape(C, B, H // 32, W // 32).permute(1, 0, 2, 3).contiguous()
+    npx = B * H * W
+    y_bpp = torch.log(out["likelihoods"]["y"]).sum() / (-math.log(2) * npx)
+    z_bpp = torch.log(out["likelihoods"]["z"]).sum() / (-math.log(2) * npx)
+    mse = torch.nn.functional.mse_loss(out["x_hat"], x) * 255 ** 2
+    loss = lmbda * mse + y_bpp + z_bpp + out["jpeg_bpp_loss"]
+    loss.backward()
+    aux = net.aux_loss()
+    tr = {"x": x, "jpeg_decoded": out["jpeg_decoded"], "noise_z": nz, "noise_y_anchor": log[1][1],
+          "noise_y_non_anchor": log[2][1], "noise_y": log[3][1], "x_hat": out["x_hat"].detach(),
+          "residual_hat": out["residual_hat"].detach(),
+          "y_likelihoods": out["likelihoods"]["y"].detach(), "z_likelihoods": out["likelihoods"]["z"].detach(),
+          "loss": loss.detach(), "mse_loss": mse.detach(), "y_bpp": y_bpp.detach(), "z_bpp": z_bpp.detach(),
+          "jpeg_bpp": out["jpeg_bpp_loss"].detach().float(), "aux_loss": aux.detach()}
+    np.savez_compressed(os.path.join(OUT, "hyres_train_nq_b2_64.npz"),
+                        **{k: v.numpy().astype(np.float32) for k, v in tr.items()})
+    with open(os.path.join(OUT, "hyres_train_nq_b2_64.json"), "w") as f:
+        json.dump({"lambda": lmbda, "noisequant": True, "torch_seed": 4321, "train_grads": grad_summary(net)},
+                  f, indent=1)
+    print("noisequant train loss", float(loss), "aux", float(aux))
+
+
+def main():
+    torch.set_num_threads(8)
+    hyres_mod, quant_mod = install_reference()
+    if "--only-noisequant" in sys.argv:
+        train_step_noisequant(hyres_mod, quant_mod, synthetic_input())
+        return
+    q = 50
+    B, H, W = 2, 64, 64
+    x = synthetic_input(B, H, W)
     meta = {"jpeg_quality": q, "B": B, "H": H, "W": W, "weights": "hyres_hip.weights recipe, seed 1926",
             "reference": "/root/reference models/hyres.py + models/checkerboard.py (executed)",
             "compressai": "oracle/compressai_restated.py (1.2.6 restatement)"}
@@ -216,6 +284,8 @@ def main():
           "z_likelihoods": out["likelihoods"]["z"], "jpeg_bpp": torch.tensor(float(out["jpeg_bpp_loss"]))}
     np.savez_compressed(os.path.join(OUT, "kodim01_crop64_eval.npz"),
                         **{k: v.numpy().astype(np.float32) for k, v in kd.items()})
+
+    train_step_noisequant(hyres_mod, quant_mod, x, q)
 
     with open(os.path.join(OUT, "meta.json"), "w") as f:
         json.dump(meta, f, indent=1)

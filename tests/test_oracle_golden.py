@@ -92,3 +92,84 @@ def test_oracle_matches_reference_train_step():
         if abs(ss - summ["sumsq"]) > 1e-4 * max(summ["sumsq"], 1e-30):
             bad.append((k, ss, summ["sumsq"]))
     assert not bad, bad[:5]
+
+
+def _nq_noise(g):
+    return {"z": g["noise_z"], "y_anchor": g["noise_y_anchor"], "y_non_anchor": g["noise_y_non_anchor"],
+            "y": g["noise_y"]}
+
+
+def test_oracle_matches_reference_train_step_noisequant():
+    """noisequant=True train step (the reference's default for epochs <= 400, src/training.py:238-243):
+    EB noise on z feeds h_s directly (no STE), Quantizer "noise" on the anchor and non-anchor halves
+    (models/checkerboard.py:121-122,132-133, noise added at EVERY position), GC noise on y."""
+    import json
+    import os
+    from conftest import GOLDEN
+    torch.set_num_threads(8)
+    g = load_npz("hyres_train_nq_b2_64.npz")
+    with open(os.path.join(GOLDEN, "hyres_train_nq_b2_64.json")) as f:
+        meta = json.load(f)
+    orc, sd2 = oracle_from(recipe_state_dict(), requires_grad=True)
+    from oracle import rd_loss
+    out = orc.forward(g["x"], g["jpeg_decoded"], float(g["jpeg_bpp"]), training=True, noisequant=True,
+                      noise=_nq_noise(g))
+    crit = rd_loss(out, g["x"], meta["lambda"])
+    for k, r in (("mse_loss", "mse_loss"), ("y_bpp_loss", "y_bpp"), ("z_bpp_loss", "z_bpp"), ("loss", "loss")):
+        assert abs(float(crit[k].detach()) - float(g[r])) <= 1e-5 * abs(float(g[r])), k
+    assert rel_err(out["likelihoods"]["y"].detach(), g["y_likelihoods"]) < 1e-5
+    assert rel_err(out["likelihoods"]["z"].detach(), g["z_likelihoods"]) < 1e-5
+    assert rel_err(out["x_hat"].detach(), g["x_hat"]) < 1e-5
+    crit["loss"].backward()
+    aux = orc.eb_aux_loss()
+    assert abs(float(aux) - float(g["aux_loss"])) <= 1e-5 * abs(float(g["aux_loss"]))
+    bad = []
+    for k, summ in meta["train_grads"].items():
+        t = sd2[k]
+        if summ is None:
+            assert t.grad is None or float(t.grad.abs().max()) == 0.0, k
+            continue
+        gd = t.grad.double()
+        ss = float((gd * gd).sum())
+        if abs(ss - summ["sumsq"]) > 1e-4 * max(summ["sumsq"], 1e-30):
+            bad.append((k, ss, summ["sumsq"]))
+    assert not bad, bad[:5]
+
+
+def test_entropy_coder_tables_match_restatement():
+    """update() (models/checkerboard.py:261-267 -> compressai EntropyBottleneck.update /
+    GaussianConditional.update_scale_table, run on the host as src/updata.py does) builds CDF tables identical
+    to the compressai-1.2.6 restatement in oracle/entropy_coding.py, entry for entry."""
+    from oracle.entropy_coding import eb_tables, gc_tables
+    net, sd = build_model()
+    rm = net.residual_model
+    assert rm.update(force=True)
+    orc, _ = oracle_from(sd)
+    cdf, ln, off = eb_tables(sd["residual_model.entropy_bottleneck.quantiles"], orc.eb_logits_cumulative)
+    eb = rm.entropy_bottleneck
+    assert np.array_equal(eb._quantized_cdf.numpy(), cdf)
+    assert np.array_equal(eb._cdf_length.numpy(), ln) and np.array_equal(eb._offset.numpy(), off)
+    gc = rm.gaussian_conditional
+    cdf, ln, off = gc_tables(gc.scale_table.numpy())
+    assert np.array_equal(gc._quantized_cdf.numpy(), cdf)
+    assert np.array_equal(gc._cdf_length.numpy(), ln) and np.array_equal(gc._offset.numpy(), off)
+
+
+def test_reference_compress_restatement_roundtrips():
+    """The oracle's LightWeightCheckerboard.compress restatement decodes back to its own symbols (so the
+    byte-equality test of the HIP compress() against it is meaningful)."""
+    from oracle.entropy_coding import rans_decode, reference_compress
+    from models.checkerboard import get_scale_table
+    torch.set_num_threads(8)
+    g = load_npz("kodim01_crop64_eval.npz")
+    orc, _ = oracle_from(recipe_state_dict())
+    table = get_scale_table().numpy().astype(np.float32)
+    strings, it = reference_compress(orc, g["x"] - g["jpeg_decoded"], table)
+    cdf, ln, off = it["gc_tables"]
+    dec = rans_decode(strings[0][1][0], it["non_anchor_idx"][0].reshape(-1).tolist(), cdf.tolist(), ln.tolist(),
+                      off.tolist())
+    assert dec == it["non_anchor_sym"][0].reshape(-1).tolist()
+    cdf, ln, off = it["eb_tables"]
+    C, h, w = it["z_sym"].shape[1:]
+    dec = rans_decode(strings[1][0], np.repeat(np.arange(C), h * w).tolist(), cdf.tolist(), ln.tolist(), off.tolist())
+    assert dec == it["z_sym"][0].reshape(-1).tolist()
