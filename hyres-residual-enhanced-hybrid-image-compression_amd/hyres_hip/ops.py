@@ -243,11 +243,31 @@ class Trace:
     tests can read their values (``value``) and, after backward, their gradients (``grad``)."""
 
     nodes = None
+    # (kind, output node, pre-activation tensor or None) of every ReLU / PReLU fused into a conv epilogue,
+    # in forward order (tests read the branch decisions to make the oracle follow them at the kink)
+    acts = None
 
     @classmethod
     def add(cls, name: str, node: "Node") -> None:
         if cls.nodes is not None:
             cls.nodes[name] = node
+
+    @classmethod
+    def act(cls, node: "Node", act: int, pre: Optional[torch.Tensor]) -> None:
+        if cls.acts is not None and act in (L.ACT_RELU, L.ACT_PRELU):
+            cls.acts.append(("relu" if act == L.ACT_RELU else "prelu", node, pre))
+
+    @classmethod
+    def decisions(cls):
+        """{"relu": [...], "prelu": [...]} NCHW bool masks (pre-activation > 0) in forward order."""
+        out = {"relu": [], "prelu": []}
+        for kind, node, pre in cls.acts or []:
+            if pre is not None:
+                d = pre.view(node.B, node.H, node.W, node.C).permute(0, 3, 1, 2) > 0
+            else:
+                d = to_nchw(node) > 0
+            out[kind].append(d.cpu())
+        return out
 
     @classmethod
     def value(cls, name: str) -> torch.Tensor:
@@ -652,6 +672,7 @@ def conv2d(tape: Optional[Tape], x: Node, weight: torch.Tensor, bias: Optional[t
     e.f16_operands = int(tape is None and f16_convs())
     _launch_conv(g, x.ptr(), w2, ldw, y.ptr(), e)
     y.relu_out = act == L.ACT_RELU
+    Trace.act(y, act, pre)
     if tape is None:
         return y
 
@@ -708,6 +729,7 @@ def deconv2d(tape: Optional[Tape], x: Node, weight: torch.Tensor, bias: Optional
     e.f16_operands = int(tape is None and f16_convs())
     _launch_conv(g, x.ptr(), w2, g.ntaps * Ci, y.ptr(), e)
     y.relu_out = act == L.ACT_RELU
+    Trace.act(y, act, None)
     if tape is None:
         return y
 

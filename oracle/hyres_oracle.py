@@ -76,18 +76,18 @@ class Oracle:
 
     def rbb(self, x, key):
         """compressai ResidualBottleneckBlock(N, N): 1x1 -> ReLU -> 3x3 -> ReLU -> 1x1, + x."""
-        out = F.relu(self.conv(x, key + ".conv1"))
-        out = F.relu(self.conv(out, key + ".conv2", padding=1))
+        out = self.relu(self.conv(x, key + ".conv1"))
+        out = self.relu(self.conv(out, key + ".conv2", padding=1))
         out = self.conv(out, key + ".conv3")
         return out + x
 
     def res_unit(self, x, key):
         """models/layers/attention.py:18-30."""
-        out = F.relu(self.conv(x, key + ".conv.0"))
-        out = F.relu(self.conv(out, key + ".conv.2", padding=1))
+        out = self.relu(self.conv(x, key + ".conv.0"))
+        out = self.relu(self.conv(out, key + ".conv.2", padding=1))
         out = self.conv(out, key + ".conv.4")
         out = out + x
-        return F.relu(out)
+        return self.relu(out)
 
     def attention(self, x, key):
         """models/layers/attention.py:41-47: out = a*sigmoid(b) + x."""
@@ -132,22 +132,22 @@ class Oracle:
     def h_a(self, y):
         """models/checkerboard.py:61-67."""
         k = self.rp + "h_a."
-        z = F.relu(self.conv(y, k + "0", padding=1))
-        z = F.relu(self.conv(z, k + "2", stride=2, padding=2))
+        z = self.relu(self.conv(y, k + "0", padding=1))
+        z = self.relu(self.conv(z, k + "2", stride=2, padding=2))
         return self.conv(z, k + "4", stride=2, padding=2)
 
     def h_s(self, z_hat):
         """models/checkerboard.py:69-75."""
         k = self.rp + "h_s."
-        t = F.relu(self.deconv(z_hat, k + "0"))
-        t = F.relu(self.deconv(t, k + "2"))
+        t = self.relu(self.deconv(z_hat, k + "0"))
+        t = self.relu(self.deconv(t, k + "2"))
         return self.conv(t, k + "4", padding=1)
 
     def param_aggregation(self, t):
         """models/checkerboard.py:82-88 (three 1x1 convs 768->640->512->384)."""
         k = self.rp + "param_aggregation."
-        t = F.relu(self.conv(t, k + "0"))
-        t = F.relu(self.conv(t, k + "2"))
+        t = self.relu(self.conv(t, k + "0"))
+        t = self.relu(self.conv(t, k + "2"))
         return self.conv(t, k + "4")
 
     def context_prediction(self, y_anchor_hat):
@@ -223,6 +223,12 @@ class Oracle:
         """models/utils/quantization.py:11-12: round(t) - t.detach() + t (op order kept)."""
         return torch.round(t) - t.detach() + t
 
+    def quant_ste(self, v, m, key):
+        """``Quantizer.quantize(v - m, "ste") + m`` / ``quantize_ste(v - m) + m``; ``key`` names the decision
+        site ("z", "y_anchor", "y_non_anchor") so a test can make the round() follow another run's choice
+        at a half-integer tie."""
+        return self.ste(v - m) + m
+
     @staticmethod
     def anchor_mask(h, w):
         """models/checkerboard.py:109-110: anchor = (h+w) even."""
@@ -241,7 +247,7 @@ class Oracle:
         z_hat, z_lik = self.entropy_bottleneck(z, training, noise["z"] if training else None)
         if not noisequant:
             med = self.eb_medians().reshape(1, -1, 1, 1)
-            z_hat = self.ste(z - med) + med  # quantize_ste(z - m) + m, checkerboard.py:98-101
+            z_hat = self.quant_ste(z, med, "z")  # quantize_ste(z - m) + m, checkerboard.py:98-101
         T["z_hat"] = z_hat
         T["z_likelihoods"] = z_lik
         latent = self.h_s(z_hat)
@@ -256,7 +262,7 @@ class Oracle:
         if noisequant:
             y_anchor_hat = y_anchor + noise["y_anchor"]
         else:
-            y_anchor_hat = self.ste(y_anchor - m_a) + m_a
+            y_anchor_hat = self.quant_ste(y_anchor, m_a, "y_anchor")
         T["y_anchor_hat"] = y_anchor_hat
         ctx = self.context_prediction(y_anchor_hat)
         T["ctx_params"] = ctx
@@ -266,7 +272,7 @@ class Oracle:
         if noisequant:
             y_non_anchor_hat = y_non_anchor + noise["y_non_anchor"]
         else:
-            y_non_anchor_hat = self.ste(y_non_anchor - m_na) + m_na
+            y_non_anchor_hat = self.quant_ste(y_non_anchor, m_na, "y_non_anchor")
         T["y_non_anchor_hat"] = y_non_anchor_hat
         y_hat = y_anchor_hat + y_non_anchor_hat
         T["y_hat"] = y_hat
@@ -285,10 +291,18 @@ class Oracle:
         T["residual_hat"] = x_hat
         return {"x_hat": x_hat, "likelihoods": {"y": y_lik, "z": z_lik}}
 
-    # ---------------------------------------------------------------- MultiScaleRefine
+    # ---------------------------------------------------------------- activations (kink hooks)
+    # every ReLU / PReLU of the network goes through these two methods, so a test can detect inputs within
+    # rounding distance of the kink and evaluate the other branch (tests/test_parity_gpu.py)
+    @staticmethod
+    def relu(x):
+        return F.relu(x)
+
     @staticmethod
     def prelu(x, a):
         return F.prelu(x, a)
+
+    # ---------------------------------------------------------------- MultiScaleRefine
 
     def refine(self, x, trace=None):
         """models/layers/enhancement.py:85-112."""
