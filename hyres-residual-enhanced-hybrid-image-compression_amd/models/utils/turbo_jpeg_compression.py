@@ -8,8 +8,10 @@ Semantics kept from the reference:
 Backends: PyTurboJPEG if importable (bit-identical to the reference), else Pillow's bundled
 libjpeg-turbo with the same effective settings (channel order reversed in/out, subsampling=1 = 4:2:2).
 The hard-coded ``lib_path`` of the reference (:12) is replaced by the library's default lookup or
-``HYRES_TURBOJPEG_LIB``.  Images are coded by a thread pool (libjpeg-turbo releases the GIL), which is the
-host-side half of the multi-GPU scaling story.
+``HYRES_TURBOJPEG_LIB``.  Images are coded by worker processes when ``hyres_hip.jpeg_host.start()`` ran before the GPU was touched
+(Pillow's coder holds the GIL, so threads do not scale), else by a thread pool (PyTurboJPEG releases the
+GIL); ``prefetch`` overlaps the next batch's JPEG with the device step.  This is the host-side half of the
+multi-GPU scaling story.
 """
 from __future__ import annotations
 
@@ -22,17 +24,21 @@ import numpy as np
 import torch
 from torch import nn
 
+from hyres_hip import jpeg_host
+
 try:  # pragma: no cover - not installed in this image
     from turbojpeg import TurboJPEG as _TurboJPEG  # type: ignore
 except Exception:  # noqa: BLE001
     _TurboJPEG = None
 
 
-def _to_uint8_hwc(img: torch.Tensor) -> np.ndarray:
-    t = torch.clamp(img, 0, 1)
-    if t.size(0) == 1:
-        t = t.repeat(3, 1, 1)
-    return (t.permute(1, 2, 0) * 255).byte().numpy()
+def _to_uint8_batch(x: torch.Tensor) -> np.ndarray:
+    """[N,C,H,W] float -> [N,H,W,3] uint8: (clamp(x, 0, 1) * 255).byte() (truncation, :25,32), grey
+    images repeated to 3 channels (:26-28); one vectorised pass over the batch."""
+    t = torch.clamp(x, 0, 1)
+    if t.size(1) == 1:
+        t = t.repeat(1, 3, 1, 1)
+    return (t * 255).byte().permute(0, 2, 3, 1).contiguous().numpy()
 
 
 class _PillowTurbo:
@@ -48,10 +54,21 @@ class _PillowTurbo:
     def decode(self, data: bytes) -> np.ndarray:
         from PIL import Image
         im = Image.open(io.BytesIO(data)).convert("RGB")
-        return np.ascontiguousarray(np.asarray(im)[..., ::-1])
+        return np.asarray(im)[..., ::-1]
+
+
+class _Prefetched:
+    __slots__ = ("key", "future")
+
+    def __init__(self, key, future):
+        self.key, self.future = key, future
 
 
 class TurboJPEGCompression(nn.Module):
+    """Host JPEG stage.  Each image's encode -> decode round trip is ONE task on a thread pool (libjpeg-turbo
+    releases the GIL); ``prefetch(x)`` starts the next batch's round trip in the background so a training
+    loop overlaps the host JPEG stage with the device step (src/utils/engine.py does this)."""
+
     def __init__(self, quality=25, lib_path: Optional[str] = None, workers: Optional[int] = None):
         super().__init__()
         self.quality = quality
@@ -62,36 +79,82 @@ class TurboJPEGCompression(nn.Module):
         else:
             self.jpeg = _PillowTurbo()
             self.backend = "pillow-libjpeg-turbo"
-        self.workers = workers or min(16, os.cpu_count() or 1)
+        self.workers = workers or int(os.environ.get("HYRES_JPEG_WORKERS", min(16, os.cpu_count() or 1)))
         self._pool: Optional[ThreadPoolExecutor] = None
+        self._bg: Optional[ThreadPoolExecutor] = None
+        self._pending: Optional[_Prefetched] = None
 
     def _map(self, fn, items):
         if len(items) <= 1 or self.workers <= 1:
             return [fn(i) for i in items]
         if self._pool is None:
-            self._pool = ThreadPoolExecutor(max_workers=self.workers)
+            self._pool = ThreadPoolExecutor(max_workers=self.workers, thread_name_prefix="hyres-jpeg")
         return list(self._pool.map(fn, items))
 
     def compress(self, x: torch.Tensor) -> List[io.BytesIO]:
-        x_cpu = x.detach().cpu() if x.device.type != "cpu" else x.detach()
-        imgs = [_to_uint8_hwc(x_cpu[i]) for i in range(x_cpu.size(0))]
-        datas = self._map(lambda im: self.jpeg.encode(im, quality=self.quality), imgs)
+        imgs = _to_uint8_batch(x.detach().cpu())
+        datas = self._map(lambda im: self.jpeg.encode(im, quality=self.quality), list(imgs))
         return [io.BytesIO(d) for d in datas]
 
     def decompress(self, compressed_buffers, device) -> torch.Tensor:
         arrs = self._map(lambda b: self.jpeg.decode(b.getvalue()), list(compressed_buffers))
-        imgs = [torch.from_numpy(a).float().permute(2, 0, 1) / 255.0 for a in arrs]
-        return torch.stack(imgs, dim=0).to(device)
+        return self._stack(arrs).to(device)
+
+    @staticmethod
+    def _stack(arrs) -> torch.Tensor:
+        # torch.from_numpy(a).float().permute(2, 0, 1) / 255.0 per image (:55-58), batched
+        return torch.from_numpy(np.stack(arrs)).permute(0, 3, 1, 2).float() / 255.0
+
+    def _roundtrip(self, x: torch.Tensor):
+        imgs = _to_uint8_batch(x)
+        procs_pool, nprocs = jpeg_host.pool()
+        if procs_pool is not None and self.backend == "pillow-libjpeg-turbo" and imgs.shape[0] > 1:
+            # worker processes (Pillow's coder holds the GIL): contiguous chunks, results in order
+            k = -(-imgs.shape[0] // nprocs)
+            futs = [procs_pool.submit(jpeg_host.roundtrip_pillow, imgs[i:i + k], self.quality)
+                    for i in range(0, imgs.shape[0], k)]
+            sizes, arrs = [], []
+            for f in futs:
+                s_, a_ = f.result()
+                sizes += s_
+                arrs.append(a_)
+            N, _, H, W = x.size()
+            dec = torch.from_numpy(np.concatenate(arrs)).permute(0, 3, 1, 2).float() / 255.0
+            return dec, sum(n * 8 for n in sizes) / (N * H * W)
+
+        def one(im):
+            data = self.jpeg.encode(im, quality=self.quality)
+            return len(data), self.jpeg.decode(data)
+
+        res = self._map(one, list(imgs))
+        N, _, H, W = x.size()
+        bits = sum(n * 8 for n, _ in res)
+        return self._stack([a for _, a in res]), bits / (N * H * W)
+
+    @staticmethod
+    def _key(x: torch.Tensor):
+        return (id(x), x.data_ptr(), x._version, tuple(x.shape))
+
+    def prefetch(self, x: torch.Tensor) -> None:
+        """Start ``forward(x)``'s host work for a CPU batch in the background (one batch in flight)."""
+        if x.device.type != "cpu":
+            return
+        if self._bg is None:
+            self._bg = ThreadPoolExecutor(max_workers=1, thread_name_prefix="hyres-jpeg-prefetch")
+        self._pending = _Prefetched(self._key(x), self._bg.submit(self._roundtrip, x.detach()))
 
     def forward(self, x: torch.Tensor):
+        """(decoded [N,3,H,W] on x.device, jpeg_bpp = total bytes * 8 / (N*H*W))  (:62-77)."""
         device = x.device
-        buffers = self.compress(x)
-        N, _, H, W = x.size()
-        bits = sum(len(b.getvalue()) * 8 for b in buffers)
-        jpeg_bpp = bits / (N * H * W)
-        return self.decompress(buffers, device), jpeg_bpp
+        p = self._pending
+        if p is not None and x.device.type == "cpu" and p.key == self._key(x):
+            self._pending = None
+            decoded, bpp = p.future.result()
+        else:
+            decoded, bpp = self._roundtrip(x.detach().cpu())
+        return decoded.to(device), bpp
 
     def __getstate__(self):
         st = self.__dict__.copy()
-        st["_pool"] = None
+        st["_pool"] = st["_bg"] = st["_pending"] = None
         return st

@@ -66,6 +66,9 @@ def main(argv):
         # are not available offline; train.sh runs with --alpha 0.  Fail before any data is touched.
         raise SystemExit(f"--alpha {args.alpha}: the VGG perceptual term is not available in this build "
                          f"(pass --alpha 0, as train.sh does)")
+    # host JPEG worker processes, spawned before this process touches the GPU (hyres_hip.jpeg_host)
+    from hyres_hip import jpeg_host
+    jpeg_host.start()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

@@ -12,7 +12,9 @@ Differences from the reference, by design:
     non-finite gradients is skipped and backs the scale off, and a NaN gradient also skips the aux step
     (engine.py:60-74) — with the scaler state, the skip decision and the step count all on the device
     (hyres_hip.optim.DeviceGradScaler), so there is still no per-step host sync.  The reference's NaN
-    warning is printed when the metrics are drained.
+    warning is printed when the metrics are drained;
+  * the next batch's host JPEG round trip is started in the background before the current step
+    (TurboJPEGCompression.prefetch), so the host JPEG stage overlaps the device step.
 """
 import os
 import time
@@ -46,6 +48,16 @@ def _drain(pending, meters, nan_flags=None):
         nan_flags.clear()
 
 
+def _lookahead(loader):
+    """(batch, next batch or None) pairs."""
+    it = iter(loader)
+    cur = next(it, None)
+    while cur is not None:
+        nxt = next(it, None)
+        yield cur, nxt
+        cur = nxt
+
+
 def train_one_epoch(model, criterion, train_dataloader, optimizer, aux_optimizer, epoch, clip_max_norm,
                     noisequant=True, mixed_precision=False, gradient_accumulation_steps=1, reducer=None,
                     log_every=100):
@@ -64,7 +76,10 @@ def train_one_epoch(model, criterion, train_dataloader, optimizer, aux_optimizer
     aux_optimizer.zero_grad()
     aux_loss = None
     amp = (lambda: torch.autocast("cuda", dtype=torch.float16)) if mixed_precision else nullcontext
-    for i, d in enumerate(train_dataloader):
+    jpeg = getattr(model, "jpeg", None)
+    for i, (d, d_next) in enumerate(_lookahead(train_dataloader)):
+        if d_next is not None and hasattr(jpeg, "prefetch"):
+            jpeg.prefetch(d_next)  # the next batch's host JPEG overlaps this step's device work
         with amp():
             out_net = model(d, noisequant)
             d = d.to(device)
