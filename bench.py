@@ -44,6 +44,7 @@ def parse():
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of HIP-graph replay")
     ap.add_argument("--no-eval", action="store_true", help="skip the encode+decode (eval) legs")
     ap.add_argument("--no-host-jpeg", action="store_true", help="skip the with-host-JPEG legs")
+    ap.add_argument("--no-amp", action="store_true", help="skip the f16-amp (train.sh --mixed-precision) leg")
     ap.add_argument("--jpeg-procs", type=int, default=None, help="JPEG worker processes (default min(8, cpus))")
     return ap.parse_args()
 
@@ -164,6 +165,67 @@ def eval_legs(net, x, jpeg, jpeg_bpp, args, reps=20):
     res["kodak_codec"] = codec_leg(net, xk.to(dev), jk.to(dev))
     net.train()
     return res
+
+
+MI355X_F16_PEAK_TFLOPS = 2500.0  # dense f16 MFMA (MI355X_MICROARCH.md), no sparsity
+
+
+def amp_leg(net, opt, aux_opt, crit, x, jpeg, jpeg_bpp, args):
+    """train.sh's actual configuration (--mixed-precision, src/utils/engine.py:23-82): the C2 step under
+    torch.autocast(float16) — every conv / deconv / GDN contraction and its input-gradient on the f16 MFMA
+    (v_mfma_f32_32x32x16_f16, fp16 operands, fp32 accumulation and fp32 activations/gradients in HBM) —
+    with the device GradScaler (scaled loss, unscale-before-clip, skip on inf/NaN, backoff/growth), as a HIP
+    graph.  Reported beside the fp32 headline; dtype "f16-amp"."""
+    from hyres_hip.graphs import CapturedStep
+    from hyres_hip.optim import DeviceGradScaler
+    from hyres_hip import ops as O
+    dev = x.device
+    scaler = DeviceGradScaler(dev)
+    cap = CapturedStep(net, x, jpeg, jpeg_bpp, noisequant=False, criterion=crit, zero_grad=opt.zero_grad, amp=True,
+                       loss_scale=scaler.scale)
+
+    def step():
+        c = cap.replay()[1]
+        opt.step(grad_scaler=scaler)
+        scaler.update(opt.sumsq)
+        nan = opt.sumsq.clone()
+        opt.zero_grad()
+        aux = net.aux_loss()
+        aux.backward()
+        aux_opt.step(skip_if_nan=nan)
+        aux_opt.zero_grad()
+        return c
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.time()
+    for _ in range(args.steps):
+        c = step()
+    torch.cuda.synchronize()
+    ms = (time.time() - t0) * 1000 / args.steps
+    loss = float(c["loss"].detach())
+    B, _, H, W = x.shape
+    # dominant f16 kernel, live (one eager AMP step, HIP events per launch, as for the fp32 line)
+    O.KernelTimer.reset()
+    O.KernelTimer.enabled = True
+    with torch.autocast("cuda", dtype=torch.float16):
+        out = net.forward_device(x, jpeg, jpeg_bpp, noisequant=False)
+        cc = crit(out, x)
+    (cc["loss"] * scaler.scale.reshape(())).backward()
+    torch.cuda.synchronize()
+    O.KernelTimer.enabled = False
+    ks = O.KernelTimer.summary()
+    opt.zero_grad()
+    ach = ks["flops"] / (ks["total_ms"] * 1e-3) / 1e12 if ks["total_ms"] > 0 else 0.0
+    del cap
+    return {"dtype": "f16-amp", "value": round(B * H * W / ms / 1e3, 4), "unit": "Mpixels/s", "ms_per_step": round(ms, 3),
+            "loss": loss, "loss_scale": scaler.get_scale(),
+            "roofline": {"bound": "mfma", "kernel": ks["kernel"], "achieved": round(ach, 3),
+                         "peak": MI355X_F16_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(ach / MI355X_F16_PEAK_TFLOPS, 4),
+                         "avg_launch_us": round(ks["avg_us"], 2), "launches_per_step": ks["launches"]},
+            "note": "fp16 operands / fp32 accumulation on the f16 MFMA; weight gradients "
+                    + ("f16" if os.environ.get("HYRES_AMP_WGRAD_F16", "1") == "1" else "fp32")}
 
 
 def host_jpeg_legs(net, step_eager_cpu, x_cpu, reps=5):
@@ -414,6 +476,9 @@ def main():
     evals = None
     if world == 1 and not args.no_eval:
         evals = eval_legs(net, x, jpeg, jpeg_bpp, args)
+    amp = None
+    if world == 1 and not args.no_amp:
+        amp = amp_leg(net, opt, aux_opt, crit, x, jpeg, jpeg_bpp, args)
     host = None
     if world == 1 and not args.no_host_jpeg:
         host = host_jpeg_legs(net, step_eager_cpu, x_cpu)
@@ -459,6 +524,7 @@ def main():
         "cpu_baseline": cpu,
         "jpeg_host_ms_per_image": round(jpeg_ms, 3),
         "host_jpeg": host,
+        "amp": amp,
         "loss": loss_val,
     }
     print(json.dumps(line))

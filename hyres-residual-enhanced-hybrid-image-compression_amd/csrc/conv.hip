@@ -1004,6 +1004,231 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgradArgs a) {
     });
 }
 
+
+// ------------------------------------------------------------------------------------------------
+// AMP weight gradient (train.sh --mixed-precision): the same GEMM dW[t][m][n] = sum_q P[q][m] Q_t[q][n]
+// with P and Q rounded to fp16 when staged and consumed by v_mfma_f32_32x32x16_f16 (fp32 accumulation,
+// fp32 bias sums from the unrounded P).  Chunks of KTH = 64 pixels are staged exactly as they arrive
+// from HBM — [k][channel] rows, 4 channels (8 bytes) per ds_write_b64 — and read back transposed with
+// ds_read_b64_tr_b16, which hands each lane the 8 consecutive k of its row/column the MFMA wants.  Row
+// pitch = BM + 32 halves: the four rows of one transposed read land on disjoint banks.  Double-buffered
+// (one barrier per tap step).  Requires the vector path (M, N, ldp, ldq % 4 == 0) and no tap folding.
+// ------------------------------------------------------------------------------------------------
+constexpr int KTH = 64;
+typedef __fp16 fp16x4_t __attribute__((ext_vector_type(4)));
+typedef _Float16 halfx4_t __attribute__((ext_vector_type(4)));
+typedef _Float16 halfx8_t __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ halfx4_t lds_tr4(const _Float16* p) {
+    fp16x4_t v = __builtin_amdgcn_ds_read_tr16_b64_v4f16((__attribute__((address_space(3))) fp16x4_t*)(p));
+    return __builtin_bit_cast(halfx4_t, v);
+}
+
+template <int TM, int TN, int WAVES_M, int WAVES_N, int NT, bool SQ>
+__global__ __launch_bounds__(256) void wgrad_f16_kernel(const WgradArgs a) {
+    constexpr int BM = 32 * TM * WAVES_M;
+    constexpr int BN = 32 * TN * WAVES_N;
+    constexpr int PP = BM + 32, PQ = BN + 32;  // halves
+    __shared__ __attribute__((aligned(16))) _Float16 Psm[2 * KTH * PP];
+    __shared__ __attribute__((aligned(16))) _Float16 Qsm[2 * KTH * PQ];
+    const hyres_wgrad_desc& d = a.d;
+    const int tid = threadIdx.x;
+    const int bid = blockIdx.x;
+    const int lb = (bid & 7) * (gridDim.x >> 3) + (bid >> 3);
+    if (lb >= a.nblocks) return;
+    int rr = lb;
+    const int mt = rr % a.mtiles; rr /= a.mtiles;
+    const int nt = rr % a.ntiles; rr /= a.ntiles;
+    const int grp = rr % a.ngroups;
+    const int split = rr / a.ngroups;
+    const int m0 = mt * BM, n0 = nt * BN;
+    const int t0 = grp * NT;
+    const int HqWq = d.Hq * d.Wq;
+    const long long Qtot = (long long)d.B * HqWq;
+
+    constexpr int P_V = KTH * BM / 4 / 256, Q_V = KTH * BN / 4 / 256;
+    static_assert(P_V >= 1 && Q_V >= 1, "tile too small");
+    float4 rp[P_V], rq[Q_V];
+    // fixed per-thread channel quad (256 % (B/4) == 0): rows are tid/(B/4) + i*256/(B/4)
+    const int pc = (tid % (BM / 4)) * 4, prow0 = tid / (BM / 4);
+    const int qc = (tid % (BN / 4)) * 4, qrow0 = tid / (BN / 4);
+    constexpr int PRS = 256 / (BM / 4), QRS = 256 / (BN / 4);
+    int q_b[Q_V], q_i[Q_V], q_j[Q_V];
+    auto decode_rows = [&](int kc) {
+#pragma unroll
+        for (int i = 0; i < Q_V; ++i) {
+            const long long qq = (long long)kc * KTH + qrow0 + i * QRS;
+            if (qq < Qtot) {
+                q_b[i] = (int)(qq / HqWq);
+                const int r = (int)(qq - (long long)q_b[i] * HqWq);
+                q_i[i] = r / d.Wq;
+                q_j[i] = r - q_i[i] * d.Wq;
+            } else {
+                q_b[i] = -1; q_i[i] = 0; q_j[i] = 0;
+            }
+        }
+    };
+    auto step_rows = [&]() {
+#pragma unroll
+        for (int i = 0; i < Q_V; ++i) {
+            if (q_b[i] < 0) continue;
+            int j = q_j[i] + KTH, ii = q_i[i], b = q_b[i];
+            while (j >= d.Wq) { j -= d.Wq; ++ii; }
+            while (ii >= d.Hq) { ii -= d.Hq; ++b; }
+            q_j[i] = j; q_i[i] = ii; q_b[i] = b < d.B ? b : -1;
+        }
+    };
+    const bool do_bias = a.bias_slab != nullptr && nt == 0 && grp == 0;
+    float4 bsum = make_float4(0.f, 0.f, 0.f, 0.f);
+    auto load_p = [&](int kc) {
+        const long long k0 = (long long)kc * KTH;
+#pragma unroll
+        for (int i = 0; i < P_V; ++i) {
+            const long long qq = k0 + prow0 + i * PRS;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (qq < Qtot && m0 + pc < d.M) v = ld4(a.p + qq * d.ldp + m0 + pc);
+            rp[i] = v;
+        }
+    };
+    auto load_q = [&](int t) {
+#pragma unroll
+        for (int i = 0; i < Q_V; ++i) {
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (q_b[i] >= 0 && n0 + qc < d.N && t < d.ntaps) {
+                const int ih = q_i[i] * d.sq + d.dh[t], iw = q_j[i] * d.sq + d.dw[t];
+                if (ih >= 0 && ih < d.Hqq && iw >= 0 && iw < d.Wqq)
+                    v = ld4(a.q + ((long long)(q_b[i] * d.Hqq + ih) * d.Wqq + iw) * d.ldq + n0 + qc);
+            }
+            if constexpr (SQ) { v.x *= v.x; v.y *= v.y; v.z *= v.z; v.w *= v.w; }
+            rq[i] = v;
+        }
+    };
+    auto store_p = [&](_Float16* Ps) {
+#pragma unroll
+        for (int i = 0; i < P_V; ++i) {
+            if (do_bias) { bsum.x += rp[i].x; bsum.y += rp[i].y; bsum.z += rp[i].z; bsum.w += rp[i].w; }
+            const halfx4_t h = {(_Float16)rp[i].x, (_Float16)rp[i].y, (_Float16)rp[i].z, (_Float16)rp[i].w};
+            *reinterpret_cast<halfx4_t*>(&Ps[(prow0 + i * PRS) * PP + pc]) = h;
+        }
+    };
+    auto store_q = [&](_Float16* Qs) {
+#pragma unroll
+        for (int i = 0; i < Q_V; ++i) {
+            const halfx4_t h = {(_Float16)rq[i].x, (_Float16)rq[i].y, (_Float16)rq[i].z, (_Float16)rq[i].w};
+            *reinterpret_cast<halfx4_t*>(&Qs[(qrow0 + i * QRS) * PQ + qc]) = h;
+        }
+    };
+
+    const int lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+    // transposed-read address of this lane: half h = lane>>5 takes k rows 8h..8h+7 of each 16-k step; in
+    // its 16-lane group g, lane 4q+p supplies row (.. + q), columns 16g + 4p .. +3
+    const int lh = lane >> 5, lg = (lane >> 4) & 1, lq = (lane >> 2) & 3, lp = lane & 3;
+    const int tr_row = 8 * lh + lq, tr_col = 16 * lg + 4 * lp;
+    floatx16 acc[NT][TM][TN];
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int k = 0; k < TN; ++k)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[j][i][k][r] = 0.f;
+
+    const int kc_begin = split * a.chunks_per_split;
+    const int kc_end = min(a.nchunks, kc_begin + a.chunks_per_split);
+    if (kc_begin < kc_end) {
+        decode_rows(kc_begin);
+        load_p(kc_begin);
+        load_q(t0);
+        store_p(Psm);
+        store_q(Qsm);
+    }
+    __syncthreads();
+    int pcur = 0, qcur = 0;
+    for (int kc = kc_begin; kc < kc_end; ++kc) {
+        static_for<NT>([&](auto J) {
+            constexpr int j = decltype(J)::value;
+            const _Float16* Ps = Psm + pcur * (KTH * PP);
+            const _Float16* Qs = Qsm + qcur * (KTH * PQ);
+            const bool next_tap = j + 1 < NT;
+            const bool next_chunk = !next_tap && kc + 1 < kc_end;
+            if (next_tap) {
+                load_q(t0 + j + 1);
+            } else if (next_chunk) {
+                step_rows();
+                load_p(kc + 1);
+                load_q(t0);
+            }
+#pragma unroll
+            for (int s = 0; s < KTH / 16; ++s) {
+                halfx8_t af[TM], bf[TN];
+#pragma unroll
+                for (int tm = 0; tm < TM; ++tm) {
+                    const _Float16* src = Ps + (16 * s + tr_row) * PP + wm * TM * 32 + tm * 32 + tr_col;
+                    const halfx4_t lo = lds_tr4(src), hi = lds_tr4(src + 4 * PP);
+                    af[tm] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+                }
+#pragma unroll
+                for (int tn = 0; tn < TN; ++tn) {
+                    const _Float16* src = Qs + (16 * s + tr_row) * PQ + wn * TN * 32 + tn * 32 + tr_col;
+                    const halfx4_t lo = lds_tr4(src), hi = lds_tr4(src + 4 * PQ);
+                    bf[tn] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+                }
+#pragma unroll
+                for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                    for (int tn = 0; tn < TN; ++tn)
+                        acc[j][tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[tm], bf[tn], acc[j][tm][tn], 0, 0, 0);
+            }
+            if (next_tap || next_chunk) {
+                store_q(Qsm + (qcur ^ 1) * (KTH * PQ));
+                if (next_chunk) store_p(Psm + (pcur ^ 1) * (KTH * PP));
+            }
+            __syncthreads();
+            qcur ^= 1;
+            if (!next_tap) pcur ^= 1;
+        });
+    }
+    if (do_bias) {
+        // fp32 column sums of this thread's rows -> reduce the PRS threads that share a channel quad
+        float4* red = reinterpret_cast<float4*>(Psm);  // the loop ended with a barrier
+        red[tid] = bsum;
+        __syncthreads();
+        if (tid < BM / 4) {
+            float4 s4 = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int r = 0; r < PRS; ++r) {
+                const float4 v = red[tid + r * (BM / 4)];
+                s4.x += v.x; s4.y += v.y; s4.z += v.z; s4.w += v.w;
+            }
+            float* dst = a.bias_slab + (long long)split * d.M + m0 + 4 * tid;
+            const float sv[4] = {s4.x, s4.y, s4.z, s4.w};
+            for (int c = 0; c < 4; ++c)
+                if (m0 + 4 * tid + c < d.M) dst[c] = sv[c];
+        }
+    }
+    // slab store [split][t][M][N] (accumulator layout of v_mfma_f32_32x32x16_f16 = the 32x32x2 f32 one)
+    const int lr = lane & 31;
+    const long long MN = (long long)d.M * d.N;
+    static_for<NT>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) {
+            const int n = n0 + wn * TN * 32 + tn * 32 + lr;
+            const int t = t0 + j;
+            if (n >= d.N || t >= d.ntaps) continue;
+            float* out = a.slab + ((long long)split * d.ntaps + t) * MN + n;
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int m = m0 + wm * TM * 32 + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                    if (m < d.M) out[(long long)m * d.N] = acc[j][tm][tn][r];
+                }
+        }
+    });
+}
+
 // deterministic split-K reduce: LX float4 lanes x (256 / LX) split groups per block (4*LX outputs per
 // block). Few outputs with many splits (1x1 / small weights over a whole batch: nsplit up to 512) take
 // LX = 4, so each thread walks nsplit/64 partial rows instead of nsplit/16 and 4x as many blocks run.
@@ -1643,9 +1868,12 @@ struct WgradPlan {
     int TMc, TNc, WMc, WNc, NT, BM, BN, mtiles, ntiles, ngroups, nchunks, nsplit, cps, tapn, nblocks;
 };
 
+static bool wgrad_f16_ok(const hyres_wgrad_desc* d);
+
 static WgradPlan wgrad_plan(const hyres_wgrad_desc* d) {
     WgradPlan p{};
     p.NT = 1;
+    const int kt = wgrad_f16_ok(d) ? KTH : KT;
     p.tapn = (d->N <= 16 && d->ntaps > 1 && !d->square_q) ? 1 : 0;
     const int ncols = p.tapn ? d->ntaps * d->N : d->N;
     if (p.tapn) {
@@ -1663,13 +1891,13 @@ static WgradPlan wgrad_plan(const hyres_wgrad_desc* d) {
     p.mtiles = ceil_div(d->M, p.BM); p.ntiles = ceil_div(ncols, p.BN);
     p.ngroups = p.tapn ? 1 : ceil_div(d->ntaps, p.NT);
     const long long Q = (long long)d->B * d->Hq * d->Wq;
-    p.nchunks = ceil_div(Q, KT);
+    p.nchunks = ceil_div(Q, kt);
     const long long tiles = (long long)p.mtiles * p.ntiles * p.ngroups;
     // ~2048 blocks (swept on MI355X: 1024 -> 2048 is -0.6 % step time; fewer splits hurt), >= 8 chunks
-    // (256 pixels) per split, <= 512 splits (tunable: HYRES_WGRAD_BLOCKS,
+    // (256 pixels; f16: 4 chunks of 64) per split, <= 512 splits (tunable: HYRES_WGRAD_BLOCKS,
     // HYRES_WGRAD_MINCHUNKS, HYRES_WGRAD_MAXSPLIT)
     static const int tb = env_int("HYRES_WGRAD_BLOCKS", 2048);
-    static const int mc = env_int("HYRES_WGRAD_MINCHUNKS", 8);
+    const int mc = env_int("HYRES_WGRAD_MINCHUNKS", 8) * KT / kt;
     static const int ms = env_int("HYRES_WGRAD_MAXSPLIT", 512);
     const long long want = std::max<long long>(1, (tb + tiles - 1) / tiles);
     const long long maxsplit = std::max<long long>(1, p.nchunks / mc);
@@ -1678,6 +1906,13 @@ static WgradPlan wgrad_plan(const hyres_wgrad_desc* d) {
     p.nsplit = ceil_div(p.nchunks, p.cps);
     p.nblocks = (int)(tiles * p.nsplit);
     return p;
+}
+
+// f16 operands only on the vector path without tap folding (the 3-channel layers stay fp32)
+static bool wgrad_f16_ok(const hyres_wgrad_desc* d) {
+    const bool tapn = d->N <= 16 && d->ntaps > 1 && !d->square_q;
+    return d->f16_operands && !tapn && d->M % 4 == 0 && d->N % 4 == 0 && d->ldp % 4 == 0 && d->ldq % 4 == 0 &&
+           d->M >= 32 && d->N >= 32;
 }
 
 // Small-M stride-1 gradients are computed transposed with negated shifts so that the 3-channel
@@ -1738,6 +1973,8 @@ int hyres_conv_wgrad(const hyres_wgrad_desc* d0, const float* pp, const float* q
     const bool vp = (d->M % 4 == 0) && (d->ldp % 4 == 0) && aligned16(pp);
     const bool vq = !p.tapn && (d->N % 4 == 0) && (d->ldq % 4 == 0) && aligned16(qq);
     HY_REQUIRE(!d->square_q || (vp && vq), HYRES_E_SHAPE, "wgrad: square_q needs the vector path");
+    // the plan (chunk size, split count, workspace) assumed the f16 kernel: its operands must be aligned
+    HY_REQUIRE(!wgrad_f16_ok(d) || (vp && vq), HYRES_E_ALIGN, "wgrad(f16): P/Q must be 16-byte aligned");
     WgradArgs a;
     a.d = *d; a.p = pp; a.q = qq; a.slab = (float*)ws; a.chunks_per_split = p.cps; a.nchunks = p.nchunks;
     a.mtiles = p.mtiles; a.ntiles = p.ntiles; a.ngroups = p.ngroups; a.nblocks = p.nblocks; a.tapn = p.tapn;
@@ -1745,7 +1982,24 @@ int hyres_conv_wgrad(const hyres_wgrad_desc* d0, const float* pp, const float* q
     dim3 grid(ceil_div(p.nblocks, 8) * 8);
     hipStream_t st = as_stream(s);
     const bool sqr = d->square_q != 0;
-    if (p.TMc == 2 && p.TNc == 2) launch_wgrad<2, 2, 2, 2, 1>(a, vp, vq, sqr, grid, st);
+    if (wgrad_f16_ok(d)) {
+        auto f16 = [&](auto tm, auto tn, auto wm_, auto wn_, auto ntc) {
+            constexpr int TM_ = decltype(tm)::value, TN_ = decltype(tn)::value;
+            constexpr int WM2 = decltype(wm_)::value, WN2 = decltype(wn_)::value, NT_ = decltype(ntc)::value;
+            if (sqr) hipLaunchKernelGGL((wgrad_f16_kernel<TM_, TN_, WM2, WN2, NT_, true>), grid, dim3(256), 0, st, a);
+            else hipLaunchKernelGGL((wgrad_f16_kernel<TM_, TN_, WM2, WN2, NT_, false>), grid, dim3(256), 0, st, a);
+        };
+        using I1 = std::integral_constant<int, 1>;
+        using I2 = std::integral_constant<int, 2>;
+        using I4 = std::integral_constant<int, 4>;
+        if (p.TMc == 2 && p.TNc == 2) f16(I2{}, I2{}, I2{}, I2{}, I1{});
+        else if (p.TMc == 2) f16(I2{}, I1{}, I2{}, I2{}, I1{});
+        else if (p.WMc == 1) f16(I1{}, I1{}, I1{}, I4{}, I1{});
+        else if (p.WNc == 1) f16(I1{}, I1{}, I4{}, I1{}, I1{});
+        else if (p.NT == 9) f16(I1{}, I1{}, I2{}, I2{}, std::integral_constant<int, 9>{});
+        else if (p.NT == 5) f16(I1{}, I1{}, I2{}, I2{}, std::integral_constant<int, 5>{});
+        else f16(I1{}, I1{}, I2{}, I2{}, I1{});
+    } else if (p.TMc == 2 && p.TNc == 2) launch_wgrad<2, 2, 2, 2, 1>(a, vp, vq, sqr, grid, st);
     else if (p.TMc == 2) launch_wgrad<2, 1, 2, 2, 1>(a, vp, vq, sqr, grid, st);
     else if (p.WMc == 1) launch_wgrad<1, 1, 1, 4, 1>(a, vp, vq, sqr, grid, st);
     else if (p.WNc == 1) launch_wgrad<1, 1, 4, 1, 1>(a, vp, vq, sqr, grid, st);

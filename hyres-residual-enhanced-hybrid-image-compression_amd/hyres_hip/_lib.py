@@ -48,7 +48,7 @@ class WgradDesc(ctypes.Structure):
                 ("B", "Hq", "Wq", "M", "ldp", "N", "ldq", "Hqq", "Wqq", "sq", "ntaps")] + [
         ("dh", ctypes.c_int * MAX_TAPS), ("dw", ctypes.c_int * MAX_TAPS),
         ("sm", ctypes.c_int), ("sn", ctypes.c_int), ("st", ctypes.c_int),
-        ("square_q", ctypes.c_int), ("accumulate", ctypes.c_int)]
+        ("square_q", ctypes.c_int), ("accumulate", ctypes.c_int), ("f16_operands", ctypes.c_int)]
 
 
 _P = ctypes.c_void_p

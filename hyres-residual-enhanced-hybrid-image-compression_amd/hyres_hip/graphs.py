@@ -25,6 +25,7 @@ Graph-safety of the captured region:
 """
 from __future__ import annotations
 
+import contextlib
 from typing import Callable, Optional
 
 import torch
@@ -51,7 +52,8 @@ class CapturedStep:
     def __init__(self, net: torch.nn.Module, x: torch.Tensor, jpeg_decoded: torch.Tensor, jpeg_bpp: float = 0.0,
                  noisequant: bool = False, criterion: Optional[Callable] = None,
                  zero_grad: Optional[Callable[[], None]] = None, warmup: int = 2,
-                 capture_error_mode: str = "global"):
+                 capture_error_mode: str = "global", amp: bool = False,
+                 loss_scale: Optional[torch.Tensor] = None):
         assert x.is_cuda, "CapturedStep needs device tensors"
         self.net = net
         self.train = criterion is not None
@@ -64,12 +66,17 @@ class CapturedStep:
         _prepare_noise(net, dev)
 
         def run():
+            # amp: the forward under torch.autocast(float16) (engine.py:32) -> fp16-operand convolutions;
+            # loss_scale: the GradScaler's device scale multiplies the loss before backward (engine.py:51)
+            ctx = torch.autocast("cuda", dtype=torch.float16) if amp else contextlib.nullcontext()
             if self.train:
-                out = net.forward_device(self.x, self.jpeg, self.bpp, noisequant)
-                c = criterion(out, self.x)
-                c["loss"].backward()
+                with ctx:
+                    out = net.forward_device(self.x, self.jpeg, self.bpp, noisequant)
+                    c = criterion(out, self.x)
+                loss = c["loss"] if loss_scale is None else c["loss"] * loss_scale.reshape(())
+                loss.backward()
                 return out, c
-            with torch.no_grad():
+            with torch.no_grad(), ctx:
                 return net.forward_device(self.x, self.jpeg, self.bpp, noisequant), None
 
         side = torch.cuda.Stream(device=dev)

@@ -501,10 +501,15 @@ def conv_bytes(g: L.ConvGeom, e: L.Epilogue) -> float:
     return b
 
 
+AMP_WGRAD_F16 = int(os.environ.get("HYRES_AMP_WGRAD_F16", "1") == "1")
+
+
 def f16_convs() -> bool:
-    """Inference under ``torch.autocast("cuda", dtype=torch.float16)`` (the reference's AMP path,
-    src/utils/engine.py / BASELINE configs[4]): forward convolutions without a tape take fp16 operands on
-    the f16 MFMA (fp32 accumulation, fp32 activations in HBM); training and input-gradients stay fp32."""
+    """``torch.autocast("cuda", dtype=torch.float16)`` is active (the reference's AMP path, train.sh
+    --mixed-precision -> src/utils/engine.py:32, BASELINE configs[4]): convolutions started now take fp16
+    operands on the f16 MFMA (fp32 accumulation, fp32 activations in HBM) — the forward conv and, decided
+    at forward time like autocast's fp16 conv backward, its input-gradient and weight-gradient GEMMs
+    (HYRES_AMP_WGRAD_F16=0 keeps the weight gradients in fp32)."""
     return torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.float16
 
 
@@ -669,7 +674,8 @@ def conv2d(tape: Optional[Tape], x: Node, weight: torch.Tensor, bias: Optional[t
             pre = _empty((B, Ho, Wo, Co), x.device)
             e.out2 = pre.data_ptr()
             e.ldo2 = Co
-    e.f16_operands = int(tape is None and f16_convs())
+    f16 = int(f16_convs())
+    e.f16_operands = f16
     _launch_conv(g, x.ptr(), w2, ldw, y.ptr(), e)
     y.relu_out = act == L.ACT_RELU
     Trace.act(y, act, pre)
@@ -693,6 +699,7 @@ def conv2d(tape: Optional[Tape], x: Node, weight: torch.Tensor, bias: Optional[t
                    pad, dil)
             d.sm = Ci_w * KH * KW
             d.accumulate = 1
+            d.f16_operands = f16 * AMP_WGRAD_F16
             _wgrad(d, gp.data_ptr(), x.ptr(), param_grad(weight), x.device,
                    param_grad(bias) if wants_grad(bias) else None, keep=(gp, x.v), side=True)
         if x.rg:
@@ -703,6 +710,7 @@ def conv2d(tape: Optional[Tape], x: Node, weight: torch.Tensor, bias: Optional[t
                                     pad, dil), mask)
             w2d = _prepped(weight, gd, L.WPREP_CONV_DGRAD, Ci_w, Co, KH, KW, pad, mask)
             ed.accumulate = acc
+            ed.f16_operands = f16
             x.relu_mask_epilogue(ed, acc)
             _launch_conv(gd, gp.data_ptr(), w2d, gd.ntaps * Co, tgt.data_ptr(), ed)
 
@@ -726,7 +734,8 @@ def deconv2d(tape: Optional[Tape], x: Node, weight: torch.Tensor, bias: Optional
     e.kind = L.EPI_BIAS
     e.act = act
     e.bias = L.ptr(bias)
-    e.f16_operands = int(tape is None and f16_convs())
+    f16 = int(f16_convs())
+    e.f16_operands = f16
     _launch_conv(g, x.ptr(), w2, g.ntaps * Ci, y.ptr(), e)
     y.relu_out = act == L.ACT_RELU
     Trace.act(y, act, None)
@@ -744,6 +753,7 @@ def deconv2d(tape: Optional[Tape], x: Node, weight: torch.Tensor, bias: Optional
             d = L.WgradDesc()
             L.call("hyres_wgrad_desc_deconv2d", ctypes.byref(d), B, H, W, Ci, x.ld, Co, gpld, K, pad)
             d.accumulate = 1
+            d.f16_operands = f16 * AMP_WGRAD_F16
             _wgrad(d, x.ptr(), gp.data_ptr(), param_grad(weight), x.device, keep=(gp, x.v), side=True)
         if x.rg:
             ed = L.Epilogue()
@@ -752,6 +762,7 @@ def deconv2d(tape: Optional[Tape], x: Node, weight: torch.Tensor, bias: Optional
             gd = _geom("hyres_geom_deconv2d_dgrad", B, H, W, Ci, x.grad_ld(), Co, gpld, K, pad)
             w2d = _prepped(weight, gd, L.WPREP_DECONV_DGRAD, Ci, Co, K, K, pad)
             ed.accumulate = acc
+            ed.f16_operands = f16
             x.relu_mask_epilogue(ed, acc)
             _launch_conv(gd, gp.data_ptr(), w2d, gd.ntaps * Co, tgt.data_ptr(), ed)
 
@@ -782,7 +793,8 @@ def gdn(tape: Optional[Tape], x: Node, beta: torch.Tensor, gamma: torch.Tensor, 
     e.ld0 = x.ld
     e.out2 = nrm.data_ptr()
     e.ldo2 = C
-    e.f16_operands = int(tape is None and f16_convs())
+    f16 = int(f16_convs())
+    e.f16_operands = f16
     _launch_conv(g, x.ptr(), gp, C, y.ptr(), e)
     if tape is None:
         return y
@@ -805,6 +817,7 @@ def gdn(tape: Optional[Tape], x: Node, beta: torch.Tensor, gamma: torch.Tensor, 
             L.call("hyres_wgrad_desc_conv2d", ctypes.byref(d), x.B, x.H, x.W, C, x.ld, C, C, 1, 1, 1, 0, 1)
             d.square_q = 1
             d.accumulate = 0
+            d.f16_operands = f16 * AMP_WGRAD_F16
             _wgrad(d, dn.data_ptr(), x.ptr(), dgp, dev)
             dbp = _empty((C,), dev)
             _colsum_into(dn, y.P, C, C, dbp, acc=0)
@@ -823,6 +836,7 @@ def gdn(tape: Optional[Tape], x: Node, beta: torch.Tensor, gamma: torch.Tensor, 
             ed.ld1 = C
             ed.aux2 = nrm.data_ptr()
             ed.ld2 = C
+            ed.f16_operands = f16
             _launch_conv(gd, dn.data_ptr(), w2d, C, tgt.data_ptr(), ed)
 
     tape.push(bwd)

@@ -145,6 +145,7 @@ typedef struct hyres_wgrad_desc {
     int sm, sn, st;              /* destination strides (floats) */
     int square_q;                /* Q -> Q*Q (GDN gamma gradient) */
     int accumulate;
+    int f16_operands;            /* AMP: P, Q rounded to fp16 on the f16 MFMA, fp32 accumulation */
 } hyres_wgrad_desc;
 int hyres_wgrad_desc_conv2d(hyres_wgrad_desc* d, int B, int H, int W, int Ci, int ldx, int Co,
                             int ldy, int KH, int KW, int stride, int pad, int dil);

@@ -192,7 +192,7 @@ def test_grad_scaler_skip_and_backoff_gpu():
         if kind == "inf":
             grads[2][0, 1] = float("inf")
         if kind == "nan":
-            grads[4][7] = float("nan")
+            grads[3][7] = float("nan")
         for p, gr in zip(ref, grads):
             p.grad = gr.clone()
         fopt.zero_grad()

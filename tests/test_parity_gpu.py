@@ -1058,3 +1058,116 @@ def test_compress_bitstream_matches_oracle():
         for i, (sa, sb) in enumerate(zip(a, b)):
             assert sa == sb, (name, i, len(sa), len(sb))
     assert np.array_equal(rm.gaussian_conditional._quantized_cdf.cpu().numpy(), inter["gc_tables"][0])
+
+
+# ------------------------------------------------------------------------------------------------ AMP
+AMP_CASES = [(2, 64, 64, 16, 16, 3, 1, 1, 1), (2, 128, 192, 16, 16, 5, 2, 2, 1), (2, 192, 96, 8, 8, 1, 1, 0, 1),
+             (2, 64, 64, 16, 16, 3, 1, 2, 2), (2, 128, 128, 32, 32, 1, 1, 0, 1), (2, 192, 384, 8, 8, 5, 1, 2, 1)]
+
+
+@pytest.mark.parametrize("case", AMP_CASES)
+def test_conv2d_amp_fwd_bwd(case):
+    """train.sh --mixed-precision: a conv recorded on the tape under torch.autocast(float16) takes fp16
+    operands on the f16 MFMA for the forward, the input gradient AND the weight gradient (fp32 accumulation,
+    fp32 bias sums).  Against torch fp32 on the fp16-rounded operands: y = conv(x_h, w_h) + b,
+    dx = conv^T(gy_h, w_h), dw = sum gy_h x_h, db = sum gy (only the summation order differs: 1e-5)."""
+    from hyres_hip import ops as O
+    B, Ci, Co, H, W, K, s, p, d = case
+    x = _rand((B, Ci, H, W), 41)
+    w = _rand((Co, Ci, K, K), 42, 1.0 / (Ci * K * K) ** 0.5)
+    b = _rand((Co,), 43, 0.1)
+    xh, wh = x.half().float(), w.half().float()
+    yr = F.conv2d(xh, wh, b, stride=s, padding=p, dilation=d)
+    gy = _rand(yr.shape, 44)
+    gyh = gy.half().float()
+    xr, wr = xh.clone().requires_grad_(), wh.clone().requires_grad_()
+    F.conv2d(xr, wr, None, stride=s, padding=p, dilation=d).backward(gyh)
+    D = dev()
+    wd = torch.nn.Parameter(w.to(D))
+    bd = torch.nn.Parameter(b.to(D))
+    tape = O.Tape()
+    xn = O.to_nhwc(x.to(D), rg=True)
+    with torch.autocast("cuda", dtype=torch.float16):
+        yn = O.conv2d(tape, xn, wd, bd, stride=s, pad=p, dil=d)
+    y = O.to_nchw(yn)
+    yn.set_grad(O.nchw_grad_to_nhwc(gy.to(D)))
+    tape.backward()
+    torch.cuda.synchronize()
+    assert rel_err(y.cpu(), yr) < 1e-5
+    assert rel_err(O.to_nchw_grad(xn).cpu(), xr.grad) < 1e-5
+    assert rel_err(wd.grad.cpu(), wr.grad) < 1e-5
+    assert rel_err(bd.grad.cpu(), gy.sum((0, 2, 3))) < 1e-5
+
+
+def test_deconv2d_amp_fwd_bwd():
+    """Transposed conv (compressai deconv, 4 sub-pixel phases) under autocast: f16 forward, dgrad, wgrad."""
+    from hyres_hip import ops as O
+    B, Ci, Co, H, W = 2, 128, 128, 8, 8
+    x = _rand((B, Ci, H, W), 45)
+    w = _rand((Ci, Co, 5, 5), 46, 1.0 / (Ci * 25 / 4) ** 0.5)
+    b = _rand((Co,), 47, 0.1)
+    xh, wh = x.half().float(), w.half().float()
+    yr = F.conv_transpose2d(xh, wh, b, stride=2, padding=2, output_padding=1)
+    gy = _rand(yr.shape, 48)
+    xr, wr = xh.clone().requires_grad_(), wh.clone().requires_grad_()
+    F.conv_transpose2d(xr, wr, None, stride=2, padding=2, output_padding=1).backward(gy.half().float())
+    D = dev()
+    wd, bd = torch.nn.Parameter(w.to(D)), torch.nn.Parameter(b.to(D))
+    tape = O.Tape()
+    xn = O.to_nhwc(x.to(D), rg=True)
+    with torch.autocast("cuda", dtype=torch.float16):
+        yn = O.deconv2d(tape, xn, wd, bd)
+    yn.set_grad(O.nchw_grad_to_nhwc(gy.to(D)))
+    tape.backward()
+    torch.cuda.synchronize()
+    assert rel_err(O.to_nchw(yn).cpu(), yr) < 1e-5
+    assert rel_err(O.to_nchw_grad(xn).cpu(), xr.grad) < 1e-5
+    assert rel_err(wd.grad.cpu(), wr.grad) < 1e-5
+
+
+def test_amp_train_step_vs_fp32():
+    """The whole train step under autocast (noisequant=True fixture: no round() decisions to flip) against
+    this build's fp32 HIP step, which is pinned to the reference: the reference's own AMP run needs CUDA, so
+    parity with it is unpinned.  fp16 operands (2^-11 relative rounding) through ~150 convolutions, loss
+    scaled by 2^16 as the GradScaler does: loss within 1e-3 relative, every weight / bias gradient within
+    5e-2 in relative Frobenius norm of the fp32 one (PReLU slopes, sums of cancelling g*x, excluded), x_hat
+    PSNR within 0.05 dB."""
+    import json
+    import math
+    import os
+    from conftest import GOLDEN
+    g = load_npz("hyres_train_nq_b2_64.npz")
+    with open(os.path.join(GOLDEN, "hyres_train_nq_b2_64.json")) as f:
+        meta = json.load(f)
+    D = dev()
+    from hyres_hip.loss import RateDistortionLoss
+    res = {}
+    for amp in (False, True):
+        net, _ = _hip_model()
+        net.train()
+        net.residual_model.noise.injected = _nhwc_noise(g, NQ_KEYS, D)
+        ctx = torch.autocast("cuda", dtype=torch.float16) if amp else torch.autocast("cuda", enabled=False)
+        with ctx:
+            out = net(g["x"], noisequant=True, jpeg=(g["jpeg_decoded"], float(g["jpeg_bpp"])))
+            crit = RateDistortionLoss(lmbda=meta["lambda"], alpha=0)(out, g["x"].to(D))
+        S = 65536.0 if amp else 1.0  # the GradScaler's initial scale (engine.py:23)
+        (crit["loss"] * S).backward()
+        torch.cuda.synchronize()
+        grads = {k: p.grad.detach().double().cpu() / S for k, p in net.named_parameters() if p.grad is not None}
+        res[amp] = (float(crit["loss"]), out["x_hat"].detach().cpu(), grads)
+    l32, x32, g32 = res[False]
+    l16, x16, g16 = res[True]
+    assert abs(l16 - l32) <= 1e-3 * abs(l32), (l16, l32)
+    psnr = lambda a: 10 * math.log10(1.0 / float(F.mse_loss(a.double(), g["x"].double())))  # noqa: E731
+    assert abs(psnr(x16) - psnr(x32)) < 0.05
+    worst, fro = [], []
+    for k, r in g32.items():
+        sc = float(r.abs().max())
+        if sc > 0 and not k.endswith(("act_in.weight", ".1.weight", ".3.weight")):  # PReLU slopes: cancelled sums
+            worst.append((float((g16[k] - r).abs().max()) / sc, k))
+            fro.append((float((g16[k] - r).norm() / r.norm()), k))
+    worst.sort(reverse=True)
+    fro.sort(reverse=True)
+    print("AMP vs fp32: loss", l16, l32, "worst max-norm", worst[:4], "worst frobenius", fro[:4])
+    assert fro[0][0] < 5e-2, fro[:4]
+    assert not torch.equal(x16, x32), "fp16 operand path did not engage"
