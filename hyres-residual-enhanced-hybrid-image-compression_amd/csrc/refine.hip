@@ -139,92 +139,6 @@ __global__ __launch_bounds__(256) void bilinear_bwd_kernel(const float* gy, int 
     }
 }
 
-
-// Table-driven form of the same gather (identical arithmetic and summation order): per block (one input
-// row) the non-zero (output column, weight) pairs of every input column are built once in LDS and the
-// block-uniform (output row, weight) pairs once per thread, so the inner loop has no index math, no
-// zero-weight iterations and no branches.  Resampling ratios up to 4x give at most 8 pairs per axis.
-constexpr int BW_MAXT = 8;
-// grid.x * 256 >= Wi * C / VEC (no grid stride): a block's 256 elements span at most 256 input columns
-template <int VEC>
-__global__ __launch_bounds__(256) void bilinear_bwd_tab_kernel(const float* gy, int ldgy, float* gx, int ldgx, int B,
-                                                               int Hi, int Wi, int Ho, int Wo, int C, float sh,
-                                                               float sw, int acc) {
-    __shared__ short t_ow[256][BW_MAXT];
-    __shared__ float t_w[256][BW_MAXT];
-    __shared__ unsigned char t_n[256];
-    const int CG = C / VEC;
-    const int row = blockIdx.y;
-    const int b = row / Hi, h = row - b * Hi;
-    const int n = Wi * CG;
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    const int w_lo = (blockIdx.x * 256) / CG;
-    const int w_hi = min(Wi - 1, (blockIdx.x * 256 + 255) / CG);
-    const float isw = 1.0f / sw;
-    for (int w = w_lo + threadIdx.x; w <= w_hi; w += 256) {
-        int lo, hi;
-        bw_range(isw, w, Wi, Wo, lo, hi);
-        int k = 0;
-        for (int ow = lo; ow <= hi && k < BW_MAXT; ++ow) {
-            const float ww = bw_weight(sw, ow, Wi, w);
-            if (ww == 0.f) continue;
-            t_ow[w - w_lo][k] = (short)ow;
-            t_w[w - w_lo][k] = ww;
-            ++k;
-        }
-        t_n[w - w_lo] = (unsigned char)k;
-    }
-    int r_oh[BW_MAXT];
-    float r_w[BW_MAXT];
-    int nr = 0;
-    {
-        int lo, hi;
-        bw_range(1.0f / sh, h, Hi, Ho, lo, hi);
-        for (int oh = lo; oh <= hi; ++oh) {
-            const float wh = bw_weight(sh, oh, Hi, h);
-            if (wh == 0.f || nr >= BW_MAXT) continue;
-            r_oh[nr] = oh;
-            r_w[nr] = wh;
-            ++nr;
-        }
-    }
-    __syncthreads();
-    if (i >= n) return;
-    const float* gb = gy + (long long)b * Ho * Wo * ldgy;
-    float* gr = gx + (long long)row * Wi * ldgx;
-    const int w = i / CG;
-    const int c = (i - w * CG) * VEC;
-    const int tw = w - w_lo;
-    const int nc = t_n[tw];
-    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int r = 0; r < nr; ++r) {
-        const float* gq = gb + (long long)r_oh[r] * Wo * ldgy + c;
-        float4 rs = make_float4(0.f, 0.f, 0.f, 0.f);
-        for (int e = 0; e < nc; ++e) {
-            const float ww = t_w[tw][e];
-            const float* q = gq + (int)t_ow[tw][e] * ldgy;
-            if constexpr (VEC == 4) {
-                const float4 v = ld4(q);
-                rs.x += ww * v.x; rs.y += ww * v.y; rs.z += ww * v.z; rs.w += ww * v.w;
-            } else {
-                rs.x += ww * q[0];
-            }
-        }
-        const float wh = r_w[r];
-        s.x += wh * rs.x; s.y += wh * rs.y; s.z += wh * rs.z; s.w += wh * rs.w;
-    }
-    float* gp = gr + (long long)w * ldgx + c;
-    if constexpr (VEC == 4) {
-        if (acc) {
-            const float4 o = ld4(gp);
-            s.x += o.x; s.y += o.y; s.z += o.z; s.w += o.w;
-        }
-        *reinterpret_cast<float4*>(gp) = s;
-    } else {
-        *gp = acc ? *gp + s.x : s.x;
-    }
-}
-
 // ---------------------------------------------------------------- SEBlock
 // pool partial: grid (B, nchunk), block 256: thread handles channels c = tid % C-ish
 __global__ void se_pool_kernel(const float* x, int HW, int C, int per, float* part) {
@@ -571,15 +485,7 @@ int hyres_bilinear_bwd(const float* gy, int ldgy, float* gx, int ldgx, int B, in
     const bool vec = C % 4 == 0 && ldgy % 4 == 0 && ldgx % 4 == 0 && aligned16(gy) && aligned16(gx);
     HY_REQUIRE((long long)B * Hi <= 65535 && (long long)Wi * C < (1LL << 30), HYRES_E_SHAPE, "bilinear_bwd: too large");
     const dim3 grid(ceil_div((long long)Wi * (vec ? C / 4 : C), 256), B * Hi);
-    // table-driven kernel for resampling ratios up to 4x (<= 8 taps per axis), the loop form otherwise
-    const bool tab = Ho <= 4 * Hi && Wo <= 4 * Wi && Hi <= 4 * Ho && Wi <= 4 * Wo;
-    if (tab && vec)
-        hipLaunchKernelGGL(bilinear_bwd_tab_kernel<4>, grid, dim3(256), 0, as_stream(s), gy, ldgy, gx, ldgx, B, Hi, Wi,
-                           Ho, Wo, C, scale_h, scale_w, accumulate);
-    else if (tab)
-        hipLaunchKernelGGL(bilinear_bwd_tab_kernel<1>, grid, dim3(256), 0, as_stream(s), gy, ldgy, gx, ldgx, B, Hi, Wi,
-                           Ho, Wo, C, scale_h, scale_w, accumulate);
-    else if (vec)
+    if (vec)
         hipLaunchKernelGGL(bilinear_bwd_kernel<4>, grid, dim3(256), 0, as_stream(s), gy, ldgy, gx, ldgx, B, Hi, Wi, Ho,
                            Wo, C, scale_h, scale_w, accumulate);
     else
