@@ -538,14 +538,17 @@ def _colsum_into(g: torch.Tensor, P: int, C: int, ld: int, dst: torch.Tensor, ac
 
 
 class SideStream:
-    """Weight gradients are independent of the input-gradient chain: conv/deconv wgrads run on a side
-    HIP stream (forked from the main stream at the point their operands are ready, joined at the end of
-    the tape backward), filling CUs the latency-bound dgrad chain and small-grid layers leave idle.
+    """Weight gradients are independent of the input-gradient chain: with HYRES_SIDE_STREAM=1 conv/deconv
+    wgrads run on a side HIP stream (forked from the main stream at the point their operands are ready,
+    joined at the end of the tape backward).  Off by default since round 2: under graph replay the
+    concurrent wgrads cost more in contention with the big dgrad convs than they fill (C2 step 44.4 ->
+    43.0 ms fp32, 28.8 -> 28.2 ms AMP with it off; scripts/stream_policy.sh, profiles/r2_stream_policy.txt).
     Operand tensors are ``record_stream``-ed so the caching allocator does not recycle them early;
     the side stream owns workspace slot 2."""
 
-    enabled = True
+    enabled = os.environ.get("HYRES_SIDE_STREAM", "0") == "1"
     count = max(1, int(os.environ.get("HYRES_SIDE_STREAMS", "1")))  # weight-gradient streams (round robin)
+    priority = int(os.environ.get("HYRES_SIDE_PRIORITY", "0"))
     _streams = {}
     _rr = 0
     used = False
@@ -554,7 +557,7 @@ class SideStream:
     def get(cls, device: torch.device, rotate: bool = False) -> torch.cuda.Stream:
         sts = cls._streams.get(device.index)
         if sts is None:
-            sts = [torch.cuda.Stream(device=device) for _ in range(cls.count)]
+            sts = [torch.cuda.Stream(device=device, priority=cls.priority) for _ in range(cls.count)]
             cls._streams[device.index] = sts
         if rotate:
             cls._rr = (cls._rr + 1) % len(sts)
@@ -875,6 +878,10 @@ class BranchStreams:
     scales): a branch's kernels run concurrently with the other branches' in forward and backward."""
 
     enabled = True
+    # branches run concurrently only when the shared input has at most this many pixels (B*H*W);
+    # HYRES_BRANCH_MAX_PIXELS, default: always.  HYRES_BRANCH_PRIORITY: stream priority of branch k > 0
+    max_pixels = int(os.environ.get("HYRES_BRANCH_MAX_PIXELS", str(1 << 40)))
+    priority = int(os.environ.get("HYRES_BRANCH_PRIORITY", "0"))
     _streams = {}
 
     @classmethod
@@ -882,7 +889,7 @@ class BranchStreams:
         key = (device.index, k)
         st = cls._streams.get(key)
         if st is None:
-            st = torch.cuda.Stream(device=device)
+            st = torch.cuda.Stream(device=device, priority=cls.priority)
             cls._streams[key] = st
         return st
 
@@ -894,7 +901,7 @@ def run_branches(tape: Optional[Tape], x: Node, fns) -> list:
     closures are enqueued on their streams (so their kernels overlap), and a join closure (pushed first,
     so it runs last) makes the current stream wait for them and adds the proxies' gradients into x's.
     Forward ends with the current stream waiting for every branch."""
-    if not BranchStreams.enabled or x.device.type != "cuda" or len(fns) < 2:
+    if not BranchStreams.enabled or x.device.type != "cuda" or len(fns) < 2 or x.P > BranchStreams.max_pixels:
         return [fn(tape, x) for fn in fns]
     dev = x.device
     main = torch.cuda.current_stream(dev)

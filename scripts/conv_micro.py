@@ -22,6 +22,8 @@ def main():
     ap.add_argument("--stride", type=int, default=1)
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--relu", action="store_true")
+    ap.add_argument("--res", action="store_true", help="fused residual add (RU / RBB tail)")
+    ap.add_argument("--f16", action="store_true", help="fp16 operands (autocast)")
     a = ap.parse_args()
     from hyres_hip import _lib as L
     from hyres_hip import ops as O
@@ -30,21 +32,24 @@ def main():
     w = torch.randn(a.Co, a.Ci, a.K, a.K, device=dev) / (a.Ci * a.K * a.K) ** 0.5
     b = torch.randn(a.Co, device=dev)
     act = L.ACT_RELU if a.relu else L.ACT_NONE
-    for _ in range(3):
-        y = O.conv2d(None, x, w, b, stride=a.stride, pad=a.K // 2, act=act)
-    torch.cuda.synchronize()
-    e0 = torch.cuda.Event(enable_timing=True)
-    e1 = torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(a.iters):
-        y = O.conv2d(None, x, w, b, stride=a.stride, pad=a.K // 2, act=act, out=y)
-    e1.record()
+    res = O.Node(torch.randn(a.B, a.H // a.stride, a.H // a.stride, a.Co, device=dev), rg=False) if a.res else None
+    ctx = torch.autocast("cuda", dtype=torch.float16) if a.f16 else torch.autocast("cuda", enabled=False)
+    with ctx:
+        for _ in range(3):
+            y = O.conv2d(None, x, w, b, stride=a.stride, pad=a.K // 2, act=act, res=res)
+        torch.cuda.synchronize()
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(a.iters):
+            y = O.conv2d(None, x, w, b, stride=a.stride, pad=a.K // 2, act=act, res=res, out=y)
+        e1.record()
     torch.cuda.synchronize()
     us = 1000 * e0.elapsed_time(e1) / a.iters
     Ho = y.H
     flops = 2.0 * a.B * Ho * Ho * a.K * a.K * a.Ci * a.Co
-    byts = 4.0 * (a.B * a.H * a.H * a.Ci + a.B * Ho * Ho * a.Co + a.K * a.K * a.Ci * a.Co)
-    print(f"conv B{a.B} {a.H}x{a.H}x{a.Ci} -> {Ho}x{Ho}x{a.Co} K{a.K} s{a.stride}: {us:.1f} us, "
+    byts = 4.0 * (a.B * a.H * a.H * a.Ci + a.B * Ho * Ho * a.Co * (2 if a.res else 1) + a.K * a.K * a.Ci * a.Co)
+    print(f"conv B{a.B} {a.H}x{a.H}x{a.Ci} -> {Ho}x{Ho}x{a.Co} K{a.K} s{a.stride}{' +res' if a.res else ''}{' f16' if a.f16 else ''}: {us:.1f} us, "
           f"{flops / us / 1e6:.1f} TFLOP/s, {byts / us / 1e3:.0f} GB/s")
 
 
