@@ -139,6 +139,14 @@ _SIGS = {
     "hyres_rd_bwd_coef": (_I, [_P, _P, _P, _P, _P, _P, _F, _LL, _LL, _P, _P]),
     "hyres_adam_step": (_I, [_P, _P, _P, _P, _LL, _D, _D, _D, _D, _P, _P, _D, _P, _I, _P]),
     "hyres_grad_scaler_update": (_I, [_P, _P, _P, _P, _D, _D, _I, _P]),
+    "hyres_normalize_fwd": (_I, [_P, _P, _LL, _I, _P, _P, _P]),
+    "hyres_normalize_bwd": (_I, [_P, _P, _LL, _I, _P, _P, _I, _P]),
+    "hyres_relu_fwd": (_I, [_P, _P, _LL, _P]),
+    "hyres_maxpool2_fwd": (_I, [_P, _P, _P, _I, _I, _I, _I, _P]),
+    "hyres_maxpool2_bwd": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _P]),
+    "hyres_absdiff_workspace_bytes": (_LL, [_LL]),
+    "hyres_absdiff_mean": (_I, [_P, _P, _LL, _P, _I, _P, _LL, _P]),
+    "hyres_absdiff_bwd": (_I, [_P, _P, _P, _LL, _P, _I, _P]),
 }
 
 _lib: Optional[ctypes.CDLL] = None

@@ -1,8 +1,10 @@
 """RateDistortionLoss (src/losses/rd_loss.py:18-44) with HIP reductions.
 
 The bpp log-sums and the MSE are deterministic two-pass block reductions; the six scalars are
-finalised on device (no host sync).  The VGG perceptual term is out of scope (train.sh:14 uses
-alpha = 0 and the pretrained VGG16 weights cannot be fetched offline): alpha != 0 raises."""
+finalised on device (no host sync).  The VGG16 perceptual term (rd_loss.py:40, alpha * vgg * 255^2) runs
+on the HIP path (hyres_hip.vgg.VGGLoss) when alpha != 0; its ImageNet weights must be available locally
+(HYRES_VGG16_WEIGHTS).  With alpha = 0 (train.sh:14) it is not evaluated — the reference computes it and
+multiplies it by zero."""
 from __future__ import annotations
 
 import torch
@@ -65,18 +67,23 @@ class _RDLossFn(torch.autograd.Function):
 class RateDistortionLoss(nn.Module):
     """Custom rate distortion loss with a Lagrangian parameter (src/losses/rd_loss.py)."""
 
-    def __init__(self, lmbda=0.004, alpha=0.001):
+    def __init__(self, lmbda=0.004, alpha=0.001, vgg=None):
         super().__init__()
         self.lmbda = lmbda
         self.alpha = alpha
+        if alpha != 0 and vgg is None:
+            from .vgg import VGGLoss
+            vgg = VGGLoss()  # ImageNet weights from HYRES_VGG16_WEIGHTS (raises when absent)
+        self.vgg = vgg
 
     def forward(self, output, target):
-        if self.alpha != 0:
-            raise NotImplementedError("VGG perceptual loss (alpha != 0) is out of scope: pretrained VGG16 "
-                                      "weights are unavailable offline; train.sh uses --alpha 0")
         lik = output["likelihoods"]
         loss, bpp, res, yb, zb, mse = _RDLossFn.apply(lik["y"], lik["z"], output["x_hat"], target,
                                                       output.get("jpeg_bpp_loss"), self.lmbda)
-        zero = torch.zeros((), device=target.device)
+        if self.alpha != 0:
+            vgg = self.vgg(output["x_hat"], target) * 255 ** 2  # rd_loss.py:40
+            loss = loss + self.alpha * vgg                      # rd_loss.py:42
+        else:
+            vgg = torch.zeros((), device=target.device)
         return {"loss": loss, "bpp_loss": bpp, "residual_bpp_loss": res, "y_bpp_loss": yb, "z_bpp_loss": zb,
-                "mse_loss": mse, "vgg_loss": zero}
+                "mse_loss": mse, "vgg_loss": vgg}

@@ -63,9 +63,11 @@ def main(argv):
     args = parse_args(argv)
     if args.alpha != 0:
         # RateDistortionLoss's VGG16 term (src/losses/vgg16.py) needs torchvision's ImageNet weights, which
-        # are not available offline; train.sh runs with --alpha 0.  Fail before any data is touched.
-        raise SystemExit(f"--alpha {args.alpha}: the VGG perceptual term is not available in this build "
-                         f"(pass --alpha 0, as train.sh does)")
+        # cannot be downloaded here: fail before any data is touched unless a local copy is configured
+        from hyres_hip.vgg import _default_weights_path
+        if _default_weights_path() is None:
+            raise SystemExit(f"--alpha {args.alpha}: the VGG perceptual term needs VGG16 ImageNet weights; set "
+                             f"HYRES_VGG16_WEIGHTS to a local vgg16-397923af.pth (or pass --alpha 0, as train.sh does)")
     # host JPEG worker processes, spawned before this process touches the GPU (hyres_hip.jpeg_host)
     from hyres_hip import jpeg_host
     jpeg_host.start()

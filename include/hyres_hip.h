@@ -340,6 +340,29 @@ int hyres_grad_scaler_update(const float* sumsq, float* scale, float* inv_scale,
                              hyres_stream_t s);
 
 /* ------------------------------------------------------------------------------------------ */
+/* VGG16 perceptual loss (src/losses/vgg16.py, rd_loss.py:40), NHWC           */
+/* ------------------------------------------------------------------------------------------ */
+/* torchvision Normalize: y = (x - mean[c]) / std[c], C <= 4; mean / stdv are HOST arrays
+ * (vgg16.py:35-38, 50-51) */
+int hyres_normalize_fwd(const float* x, float* y, long long P, int C, const float* mean, const float* stdv,
+                        hyres_stream_t s);
+int hyres_normalize_bwd(const float* g, float* gx, long long P, int C, const float* mean, const float* stdv,
+                        int accumulate, hyres_stream_t s);
+/* y = max(x, 0) (nn.ReLU at a slice boundary, vgg16.py:29-33) */
+int hyres_relu_fwd(const float* x, float* y, long long n, hyres_stream_t s);
+/* nn.MaxPool2d(2, 2): argmax in {0..3} ((0,0),(0,1),(1,0),(1,1)), first maximum wins, NaN propagates */
+int hyres_maxpool2_fwd(const float* x, float* y, unsigned char* argmax, int B, int H, int W, int C, hyres_stream_t s);
+int hyres_maxpool2_bwd(const float* g, const unsigned char* argmax, float* gx, int B, int H, int W, int C,
+                       int accumulate, hyres_stream_t s);
+/* out[0] (+)= mean |a - b| (two-pass deterministic), its backward ga (+)= coef[0] * sign(a - b) / n
+ * (vgg16.py:58 torch.abs(x - y).mean()) */
+long long hyres_absdiff_workspace_bytes(long long n);
+int hyres_absdiff_mean(const float* a, const float* b, long long n, float* out, int accumulate, void* ws,
+                       long long ws_bytes, hyres_stream_t s);
+int hyres_absdiff_bwd(const float* a, const float* b, const float* coef, long long n, float* ga, int accumulate,
+                      hyres_stream_t s);
+
+/* ------------------------------------------------------------------------------------------ */
 /* entropy coding (compress / decompress): compressai 1.2.6 semantics            */
 /* ------------------------------------------------------------------------------------------ */
 /* GaussianConditional.build_indexes(scales) + quantize(y, "symbols", means) of one checkerboard pass

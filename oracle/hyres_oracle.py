@@ -381,3 +381,33 @@ def rd_loss(output, target, lmbda):
     out["mse_loss"] = F.mse_loss(output["x_hat"], target) * 255 ** 2
     out["loss"] = lmbda * out["mse_loss"] + out["bpp_loss"]
     return out
+
+
+def vgg_loss(features_sd, x, y, layer_ids=(2, 7, 14, 21, 28)):
+    """src/losses/vgg16.py:41-61 (VGGLoss.forward) on torchvision vgg16().features weights
+    ``features_sd`` ({"N.weight", "N.bias"}): Normalize(ImageNet mean/std) both inputs, then for each slice
+    [previous id + 1 .. id] the convs (3x3, pad 1) / ReLU / MaxPool2d(2, 2) of VGG16, and the sum over slices
+    of mean |f(x) - f(y)|."""
+    cfg = [64, 64, "M", 128, 128, "M", 256, 256, 256, "M", 512, 512, 512, "M", 512, 512, 512, "M"]
+    layers = []
+    for v in cfg:
+        layers += ["M"] if v == "M" else ["C", "R"]
+    mean = torch.tensor([0.485, 0.456, 0.406], dtype=x.dtype).view(1, 3, 1, 1)
+    std = torch.tensor([0.229, 0.224, 0.225], dtype=x.dtype).view(1, 3, 1, 1)
+    x = (x - mean) / std
+    y = (y - mean) / std
+    loss = 0
+    start = 0
+    for lid in layer_ids:
+        for i in range(start, lid + 1):
+            kind = layers[i]
+            if kind == "C":
+                w, b = features_sd[f"{i}.weight"].to(x.dtype), features_sd[f"{i}.bias"].to(x.dtype)
+                x, y = F.conv2d(x, w, b, padding=1), F.conv2d(y, w, b, padding=1)
+            elif kind == "R":
+                x, y = F.relu(x), F.relu(y)
+            else:
+                x, y = F.max_pool2d(x, 2, 2), F.max_pool2d(y, 2, 2)
+        start = lid + 1
+        loss = loss + torch.abs(x - y).mean()
+    return loss
