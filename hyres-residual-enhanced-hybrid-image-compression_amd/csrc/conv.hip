@@ -1666,23 +1666,66 @@ static int env_int(const char* name, int dflt) {
     return (e && *e) ? atoi(e) : dflt;
 }
 
+// Kernel choice of hyres_conv_forward, shared with hyres_conv_kernel_name / hyres_conv_plan (the profiler's
+// label). tile: 0 = <2,2,2,2> (128x128), 1 = <2,1,2,2> (128x64), 2 = <1,1,4,1> (128x32), 3 = <1,2,2,2>
+// (64x128), 4 = <1,1,2,2> (64x64).
+//   * short-K 1x1 layers (<= 4 K chunks): half-height tiles — the short main loop cannot hide the operand
+//     and epilogue latencies, so twice as many blocks go in flight;
+//   * small grids (<= 65536 output pixels: the 64^2 and 32^2 regions at bs 16): 64-row tiles, 64 wide up to
+//     192 channels (fp32) / below 192 (f16), else 64x128 (fp32) / 128x128 (f16); measured per geometry
+//     over every tile and split-K target (scripts/tile_sweep.py, profiles/r2_tile_sweep_*.txt);
+//   * otherwise 128-row tiles as wide as Co allows.
+// Split-K engages only when the chosen tile leaves fewer than 512 blocks and K has >= 8 chunks.
+struct ConvChoice {
+    bool narrow;
+    int tile, mode;
+};
+static const int TILE_BM[5] = {128, 128, 128, 64, 64};
+static const int TILE_BN[5] = {128, 64, 32, 128, 64};
+
+// Tile / split-K overrides set through hyres_conv_tuning (tuning sweeps; -1 = the heuristics below)
+// keys: HYRES_TUNE_TILE, _SPLIT_BLOCKS, _SPLIT_MINCHUNKS, _WGRAD_BLOCKS, _WGRAD_MINCHUNKS, _WGRAD_NT
+static int g_tune[6] = {-1, -1, -1, -1, -1, -1};
+
+static ConvChoice choose_conv(const hyres_conv_geom* g, const hyres_epilogue* e, bool aligned) {
+    ConvChoice c{};
+    c.mode = (g->Ci % KT == 0) ? (e->square_input ? 1 : 0) : 2;
+    c.narrow = narrow_ok(g) && !e->square_input && e->kind == HYRES_EPI_BIAS && aligned;
+    static const int shortk = env_int("HYRES_CONV_SHORTK", 1);
+    static const long long small_px = env_int("HYRES_CONV_SMALL_PIXELS", 65536);
+    const bool f16 = e->f16_operands && c.mode != 2;
+    const bool short_k = shortk && c.mode != 2 && g->nphase == 1 && g->ntaps == 1 && g->Ci <= 4 * KT;
+    const long long mtot = (long long)g->B * g->Hq * g->Wq * g->nphase;
+    if (short_k && g->Co > 64) c.tile = 3;
+    else if (short_k && g->Co > 32) c.tile = 4;
+    else if (c.mode != 2 && g->Co > 32 && mtot <= small_px) {
+        if (f16) c.tile = g->Co >= 192 ? 0 : 4;
+        else c.tile = g->Co > 192 ? 3 : 4;
+    }
+    else if (g->Co > 64) c.tile = 0;
+    else if (g->Co > 32) c.tile = 1;
+    else c.tile = 2;
+    if (g_tune[0] >= 0 && g_tune[0] <= 4) c.tile = g_tune[0];
+    return c;
+}
+
 struct ConvPlan {
-    int BM, BN, nsplit, cps;
+    int nsplit, cps;
 };
 
-static ConvPlan conv_plan(const hyres_conv_geom* g) {
+static ConvPlan conv_plan(const hyres_conv_geom* g, int tile) {
     ConvPlan p{};
-    p.BM = 128;
-    p.BN = g->Co > 64 ? 128 : (g->Co > 32 ? 64 : 32);
     const long long M = (long long)g->B * g->Hq * g->Wq;
-    long long blocks = (long long)ceil_div(M, p.BM) * ceil_div(g->Co, p.BN) * g->nphase;
+    long long blocks = (long long)ceil_div(M, TILE_BM[tile]) * ceil_div(g->Co, TILE_BN[tile]) * g->nphase;
     int maxtap = 0;
     for (int ph = 0; ph < g->nphase; ++ph) maxtap = std::max(maxtap, g->ntap[ph]);
     const int nk = (g->Ci % KT == 0) ? maxtap * (g->Ci / KT) : ceil_div((long long)maxtap * g->Ci, KT);
     p.nsplit = 1;
     p.cps = nk;
-    static const int sb = env_int("HYRES_CONV_SPLIT_BLOCKS", 512);
-    static const int sc = env_int("HYRES_CONV_SPLIT_MINCHUNKS", 4);
+    static const int sb_env = env_int("HYRES_CONV_SPLIT_BLOCKS", 512);
+    static const int sc_env = env_int("HYRES_CONV_SPLIT_MINCHUNKS", 4);
+    const int sb = g_tune[1] >= 0 ? g_tune[1] : sb_env;
+    const int sc = g_tune[2] > 0 ? g_tune[2] : sc_env;
     if (blocks < sb && nk >= 2 * sc) {
         // split K so that ~sb blocks are in flight, at least sc chunks per split
         int want = (int)std::min<long long>(ceil_div(sb, blocks), 64);
@@ -1693,34 +1736,38 @@ static ConvPlan conv_plan(const hyres_conv_geom* g) {
     return p;
 }
 
-// Kernel choice of hyres_conv_forward, shared with hyres_conv_kernel_name (the profiler's label).
-// tile: 0 = <2,2,2,2> (128x128), 1 = <2,1,2,2> (128x64), 2 = <1,1,4,1> (128x32), 3 = <1,2,2,2> and
-// 4 = <1,1,2,2> (half-height tiles for short-K 1x1 layers: the <= 4-chunk main loop cannot hide the
-// operand and epilogue latencies, so twice as many blocks go in flight)
-struct ConvChoice {
-    bool narrow;
-    int tile, mode;
-};
+static long long plan_ws_bytes(const hyres_conv_geom* g, const ConvPlan& p) {
+    if (p.nsplit <= 1) return 0;
+    return (long long)p.nsplit * g->nphase * ((long long)g->B * g->Hq * g->Wq) * g->Co * 4;
+}
 
-static ConvChoice choose_conv(const hyres_conv_geom* g, const hyres_epilogue* e, bool split, bool aligned) {
-    ConvChoice c{};
-    c.mode = (g->Ci % KT == 0) ? (e->square_input ? 1 : 0) : 2;
-    c.narrow = narrow_ok(g) && !e->square_input && e->kind == HYRES_EPI_BIAS && aligned;
-    static const int shortk = env_int("HYRES_CONV_SHORTK", 1);
-    const bool short_k = shortk && !split && c.mode != 2 && g->nphase == 1 && g->ntaps == 1 && g->Ci <= 4 * KT;
-    if (short_k && g->Co > 64) c.tile = 3;
-    else if (short_k && g->Co > 32) c.tile = 4;
-    else if (g->Co > 64) c.tile = 0;
-    else if (g->Co > 32) c.tile = 1;
-    else c.tile = 2;
-    return c;
+int hyres_conv_tuning(int key, int value, int* old) {
+    HY_REQUIRE(key >= 0 && key < 6, HYRES_E_ARG, "conv_tuning: key %d", key);
+    if (old) *old = g_tune[key];
+    g_tune[key] = value;
+    return ok();
 }
 
 long long hyres_conv_workspace_bytes(const hyres_conv_geom* g) {
+    // the larger of the fp32 and fp16-operand plans (the tile, hence the split, depends on the dtype)
     if (!g || narrow_ok(g)) return 0;
-    ConvPlan p = conv_plan(g);
-    if (p.nsplit <= 1) return 0;
-    return (long long)p.nsplit * g->nphase * ((long long)g->B * g->Hq * g->Wq) * g->Co * 4;
+    long long need = 0;
+    for (int f16 = 0; f16 < 2; ++f16) {
+        hyres_epilogue e{};
+        e.kind = HYRES_EPI_BIAS;
+        e.f16_operands = f16;
+        need = std::max(need, plan_ws_bytes(g, conv_plan(g, choose_conv(g, &e, true).tile)));
+    }
+    return need;
+}
+
+int hyres_conv_plan(const hyres_conv_geom* g, const hyres_epilogue* e, int* tile, int* nsplit) {
+    HY_REQUIRE(g && e, HYRES_E_ARG, "conv_plan: NULL argument");
+    const ConvChoice ch = choose_conv(g, e, true);
+    const ConvPlan p = ch.narrow ? ConvPlan{1, 0} : conv_plan(g, ch.tile);
+    if (tile) *tile = ch.narrow ? -1 : ch.tile;
+    if (nsplit) *nsplit = p.nsplit;
+    return ok();
 }
 
 int hyres_conv_forward(const hyres_conv_geom* g, const float* x, const float* w2, int ldw, float* y,
@@ -1735,7 +1782,8 @@ int hyres_conv_forward(const hyres_conv_geom* g, const float* x, const float* w2
     static const int mfma_prio = env_int("HYRES_CONV_PRIO", 1);
     a.xcd = xcd_order;
     a.prio = mfma_prio;
-    ConvPlan plan = conv_plan(g);
+    const ConvChoice ch = choose_conv(g, e, aligned16(x) && aligned16(w2) && g->ldx % 4 == 0 && ldw % 4 == 0);
+    ConvPlan plan = conv_plan(g, ch.tile);
     a.nsplit = 1;
     a.cps = 0;
     a.slab = nullptr;
@@ -1744,8 +1792,8 @@ int hyres_conv_forward(const hyres_conv_geom* g, const float* x, const float* w2
         a.vec4 = g->Co % 4 == 0 && al(y, g->ldy) && al(e->bias, 4) && al(e->res, e->ldres) && al(e->out2, e->ldo2) &&
                  al(e->aux0, e->ld0) && al(e->aux1, e->ld1) && al(e->aux2, e->ld2);
     }
-    const long long need = hyres_conv_workspace_bytes(g);
-    if (plan.nsplit > 1 && ws && ws_bytes >= need) {  // without workspace: single pass (correct, slower)
+    const long long need = plan_ws_bytes(g, plan);
+    if (!ch.narrow && plan.nsplit > 1 && ws && ws_bytes >= need) {  // without workspace: single pass (correct, slower)
         a.nsplit = plan.nsplit;
         a.cps = plan.cps;
         a.slab = (float*)ws;
@@ -1776,8 +1824,6 @@ int hyres_conv_forward(const hyres_conv_geom* g, const float* x, const float* w2
     if (e->act == HYRES_ACT_RELU_MASK)
         HY_REQUIRE(e->aux0 && e->kind == HYRES_EPI_BIAS, HYRES_E_ARG, "conv: ReLU mask needs aux0, BIAS epilogue");
     hipStream_t st = as_stream(s);
-    const ConvChoice ch = choose_conv(g, e, a.nsplit > 1,
-                                      aligned16(x) && aligned16(w2) && g->ldx % 4 == 0 && ldw % 4 == 0);
     if (ch.narrow) {
         a.nsplit = 1;
         dim3 grid(ceil_div(a.M, NARROW_PIX), g->nphase);
@@ -1811,7 +1857,7 @@ int hyres_conv_forward(const hyres_conv_geom* g, const float* x, const float* w2
 
 int hyres_conv_kernel_name(const hyres_conv_geom* g, const hyres_epilogue* e, int split, char* buf, int n) {
     HY_REQUIRE(g && e && buf && n > 0, HYRES_E_ARG, "conv_kernel_name: bad args");
-    const ConvChoice ch = choose_conv(g, e, split != 0, true);
+    const ConvChoice ch = choose_conv(g, e, true);
     if (ch.narrow) {
         snprintf(buf, n, "conv_narrow_kernel<%d, %d>", std::min(g->Co, 4), g->Ci == 64 ? 1 : 2);
         return 0;
@@ -1885,21 +1931,32 @@ static WgradPlan wgrad_plan(const hyres_wgrad_desc* d) {
     else if (d->N <= 32) { p.TMc = 1; p.TNc = 1; p.WMc = 4; p.WNc = 1; }
     else {
         p.TMc = 1; p.TNc = 1; p.WMc = 2; p.WNc = 2;
+        // fp32: group 9 / 5 taps per block (operand reuse); f16: one tap per block column group (measured
+        // faster on every f16 geometry of the step: the f16 main loop is short, more blocks hide it better)
         p.NT = (d->ntaps % 9 == 0) ? 9 : (d->ntaps % 5 == 0) ? 5 : 1;
+        if (kt == KTH || g_tune[5] == 1) p.NT = 1;
     }
     p.BM = 32 * p.TMc * p.WMc; p.BN = 32 * p.TNc * p.WNc;
     p.mtiles = ceil_div(d->M, p.BM); p.ntiles = ceil_div(ncols, p.BN);
     p.ngroups = p.tapn ? 1 : ceil_div(d->ntaps, p.NT);
-    const long long Q = (long long)d->B * d->Hq * d->Wq;
-    p.nchunks = ceil_div(Q, kt);
+    p.nchunks = ceil_div((long long)d->B * d->Hq * d->Wq, kt);
     const long long tiles = (long long)p.mtiles * p.ntiles * p.ngroups;
     // ~2048 blocks (swept on MI355X: 1024 -> 2048 is -0.6 % step time; fewer splits hurt), >= 8 chunks
     // (256 pixels; f16: 4 chunks of 64) per split, <= 512 splits (tunable: HYRES_WGRAD_BLOCKS,
-    // HYRES_WGRAD_MINCHUNKS, HYRES_WGRAD_MAXSPLIT)
-    static const int tb = env_int("HYRES_WGRAD_BLOCKS", 2048);
-    const int mc = env_int("HYRES_WGRAD_MINCHUNKS", 8) * KT / kt;
+    // HYRES_WGRAD_MINCHUNKS, HYRES_WGRAD_MAXSPLIT). Small grids (<= 16384 pixels, the 32^2 region at
+    // bs 16): ~4096 blocks, fp32 multi-tap splits down to 4 chunks. The split count is capped so that the partial
+    // slab stays <= 16 M floats (64 MB): for the wide 1x1 layers (M x N ~ 0.5 M) the slab write + reduce
+    // otherwise costs more than the parallelism buys (scripts/tile_sweep.py --wgrad)
+    const long long Q = (long long)d->B * d->Hq * d->Wq;
+    const bool small = Q <= 16384;
+    static const int tb_env = env_int("HYRES_WGRAD_BLOCKS", 2048);
+    static const int mc_env = env_int("HYRES_WGRAD_MINCHUNKS", 8);
+    const int tb = g_tune[3] > 0 ? g_tune[3] : (small ? 2 * tb_env : tb_env);
+    const int mc0 = g_tune[4] > 0 ? g_tune[4] : ((small && kt == KT && d->ntaps > 1) ? mc_env / 2 : mc_env);
+    const int mc = std::max(1, mc0 * KT / kt);
     static const int ms = env_int("HYRES_WGRAD_MAXSPLIT", 512);
-    const long long want = std::max<long long>(1, (tb + tiles - 1) / tiles);
+    const long long slab_cap = std::max<long long>(4, (16LL << 20) / ((long long)d->ntaps * d->M * d->N));
+    const long long want = std::min<long long>(std::max<long long>(1, (tb + tiles - 1) / tiles), slab_cap);
     const long long maxsplit = std::max<long long>(1, p.nchunks / mc);
     p.nsplit = (int)std::min<long long>(std::min<long long>(want, maxsplit), ms);
     p.cps = ceil_div(p.nchunks, p.nsplit);

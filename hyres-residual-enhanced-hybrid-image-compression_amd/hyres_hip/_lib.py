@@ -77,6 +77,8 @@ _SIGS = {
                                 _P]),
     "hyres_conv_workspace_bytes": (_LL, [ctypes.POINTER(ConvGeom)]),
     "hyres_conv_kernel_name": (_I, [ctypes.POINTER(ConvGeom), ctypes.POINTER(Epilogue), _I, ctypes.c_char_p, _I]),
+    "hyres_conv_tuning": (_I, [_I, _I, _P]),
+    "hyres_conv_plan": (_I, [ctypes.POINTER(ConvGeom), ctypes.POINTER(Epilogue), _P, _P]),
     "hyres_wgrad_desc_conv2d": (_I, [ctypes.POINTER(WgradDesc)] + [_I] * 12),
     "hyres_wgrad_desc_deconv2d": (_I, [ctypes.POINTER(WgradDesc)] + [_I] * 9),
     "hyres_wgrad_workspace_bytes": (_LL, [ctypes.POINTER(WgradDesc)]),

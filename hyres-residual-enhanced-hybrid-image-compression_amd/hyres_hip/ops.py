@@ -486,6 +486,13 @@ def conv_variant(g: L.ConvGeom, e: L.Epilogue, splitk: bool) -> str:
     return buf.value.decode()
 
 
+def conv_split(g: L.ConvGeom, e: L.Epilogue) -> int:
+    """The split-K factor hyres_conv_forward will use for (g, e) (1 = fused epilogue)."""
+    tile, ns = ctypes.c_int(0), ctypes.c_int(1)
+    L.call("hyres_conv_plan", ctypes.byref(g), ctypes.byref(e), ctypes.byref(tile), ctypes.byref(ns))
+    return ns.value
+
+
 def conv_flops(g: L.ConvGeom) -> float:
     taps = sum(g.ntap[p] for p in range(g.nphase))
     return 2.0 * g.B * g.Hq * g.Wq * taps * g.Ci * g.Co
@@ -514,7 +521,7 @@ def f16_convs() -> bool:
 
 
 def _launch_conv(g: L.ConvGeom, x_ptr: int, w2: torch.Tensor, ldw: int, y_ptr: int, e: L.Epilogue) -> None:
-    nb = L.load().hyres_conv_workspace_bytes(ctypes.byref(g))  # > 0 iff the launch is split-K
+    nb = L.load().hyres_conv_workspace_bytes(ctypes.byref(g))  # > 0 iff a split-K plan exists
     timed = KernelTimer.enabled
     if timed:
         s0 = torch.cuda.Event(enable_timing=True)
@@ -525,7 +532,7 @@ def _launch_conv(g: L.ConvGeom, x_ptr: int, w2: torch.Tensor, ldw: int, y_ptr: i
            None if ws is None else ws.data_ptr(), 0 if ws is None else ws.numel(), L.stream())
     if timed:
         s1.record()
-        KernelTimer.events.append((s0, s1, conv_flops(g), conv_bytes(g, e), conv_variant(g, e, nb > 0)))
+        KernelTimer.events.append((s0, s1, conv_flops(g), conv_bytes(g, e), conv_variant(g, e, conv_split(g, e) > 1)))
         if KernelTimer.all_convs:
             desc = (f"B{g.B} {g.Hi}x{g.Wi}x{g.Ci}->{g.Ho}x{g.Wo}x{g.Co} taps{g.ntaps} ph{g.nphase} "
                     f"s{g.ish} epi{e.kind}{'+acc' if e.accumulate else ''}{'+res' if e.res else ''}")

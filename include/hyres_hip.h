@@ -131,6 +131,20 @@ long long hyres_conv_workspace_bytes(const hyres_conv_geom* g);
  * "conv_fwd_kernel<2, 1, 2, 2, 0, false, false>" (16B-aligned operands assumed).  Host-only, no
  * launch: the profiling label of bench.py's roofline line comes from the launcher's own choice. */
 int hyres_conv_kernel_name(const hyres_conv_geom* g, const hyres_epilogue* e, int split, char* buf, int n);
+/* Tuning override of the conv planners (sweeps only; not used by the product path). key 0: tile
+ * (0 = 128x128, 1 = 128x64, 2 = 128x32, 3 = 64x128, 4 = 64x64), 1: split-K target block count,
+ * 2: minimum K chunks per split; value -1 restores the built-in heuristic. *old (may be NULL) gets the
+ * previous value. Not thread-safe against concurrent launches. */
+/* The launcher's choice for (g, e): *tile = 0..4 as above (-1: the narrow VALU kernel), *nsplit = split-K
+ * factor (1 = fused epilogue). Pure host function. */
+int hyres_conv_plan(const hyres_conv_geom* g, const hyres_epilogue* e, int* tile, int* nsplit);
+#define HYRES_TUNE_TILE 0
+#define HYRES_TUNE_SPLIT_BLOCKS 1
+#define HYRES_TUNE_SPLIT_MINCHUNKS 2
+#define HYRES_TUNE_WGRAD_BLOCKS 3     /* weight gradients: split-K target block count */
+#define HYRES_TUNE_WGRAD_MINCHUNKS 4  /* minimum 32-pixel chunks per split */
+#define HYRES_TUNE_WGRAD_NT 5         /* 1: no tap grouping (one tap per block column group) */
+int hyres_conv_tuning(int key, int value, int* old);
 
 /* Weight gradient:  dW[t][m][n] = sum_q P[q][m] * Q[shift_t(q)][n]  over a base grid q (B,Hq,Wq).
  * Conv2d: P = dY (output grid), Q = X;  ConvTranspose2d: P = X (input grid), Q = dY.

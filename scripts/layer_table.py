@@ -19,6 +19,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=16)
     ap.add_argument("--size", type=int, default=256)
+    ap.add_argument("--amp", action="store_true", help="fp16-operand convs (autocast), as the AMP training mode")
     args = ap.parse_args()
     from hyres_hip.weights import synthetic_state_dict
     from hyres_hip.loss import RateDistortionLoss
@@ -33,8 +34,10 @@ def main():
     crit = RateDistortionLoss(lmbda=0.045, alpha=0)
 
     def step():
-        out = net.forward_device(x, x, 0.0)
-        crit(out, x)["loss"].backward()
+        with torch.autocast("cuda", dtype=torch.float16, enabled=args.amp):
+            out = net.forward_device(x, x, 0.0)
+            loss = crit(out, x)["loss"]
+        loss.backward()
 
     for _ in range(2):
         step()
@@ -59,6 +62,13 @@ def main():
     for d, (n, ms, fl, by) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
         us = 1000 * ms / n
         print(f"{ms:7.3f} {n:3d} {us:9.1f} {fl / us / 1e6:7.1f} {by / us / 1e3:7.0f}  {d}")
+    # by region: the larger of the two resolutions a launch touches (WGRAD rows: P / Q sides)
+    region = collections.Counter()
+    for d, (n, ms, fl, by) in agg.items():
+        sizes = [int(t.split("x")[0]) for t in d.replace("->", " ").split() if "x" in t and t[0].isdigit()]
+        region[max(sizes)] += ms
+    print("by resolution (max side touched): " +
+          ", ".join(f"{r}^2 {ms:.2f} ms" for r, ms in sorted(region.items(), reverse=True)))
 
 
 if __name__ == "__main__":

@@ -152,3 +152,36 @@ def test_conv_kernel_name_follows_the_launch_routing():
     e.square_input = 0
     e.f16_operands = 1
     assert conv_variant(g3, e, False) == "conv_fwd_kernel<2, 1, 2, 2, 0, false, true>"
+    # small grids (<= 65536 output pixels): 64-row tiles; f16 takes 128x128 from 192 channels up
+    e.f16_operands = 0
+    s3 = _geom("hyres_geom_conv2d", 16, 32, 32, 96, 96, 96, 96, 3, 3, 1, 1, 1)
+    assert conv_variant(s3, e, False) == "conv_fwd_kernel<1, 1, 2, 2, 0, false, false>"
+    s5 = _geom("hyres_geom_conv2d", 16, 32, 32, 512, 512, 384, 384, 1, 1, 1, 0, 1)
+    assert conv_variant(s5, e, False) == "conv_fwd_kernel<1, 2, 2, 2, 0, false, false>"
+    e.f16_operands = 1
+    assert conv_variant(s5, e, False) == "conv_fwd_kernel<2, 2, 2, 2, 0, false, true>"
+    assert conv_variant(s3, e, False) == "conv_fwd_kernel<1, 1, 2, 2, 0, false, true>"
+
+
+def test_conv_plan_split_follows_the_tile():
+    """Split-K engages only when the chosen tile leaves < 512 blocks and K has >= 8 chunks; the workspace
+    query covers the larger of the fp32 / f16 plans."""
+    import ctypes
+    from hyres_hip import _lib as L
+    from hyres_hip.ops import _geom
+    lib = L.load()
+    e = L.Epilogue()
+    e.kind = L.EPI_BIAS
+
+    def plan(g):
+        t, n = ctypes.c_int(), ctypes.c_int()
+        L.check(lib.hyres_conv_plan(ctypes.byref(g), ctypes.byref(e), ctypes.byref(t), ctypes.byref(n)), "plan")
+        return t.value, n.value
+    s3 = _geom("hyres_geom_conv2d", 16, 32, 32, 96, 96, 96, 96, 3, 3, 1, 1, 1)     # 256 x 2 = 512 blocks
+    assert plan(s3) == (4, 1) and lib.hyres_conv_workspace_bytes(ctypes.byref(s3)) == 0
+    h = _geom("hyres_geom_conv2d", 16, 32, 32, 128, 128, 128, 128, 5, 5, 2, 2, 1)  # 16^2 out: 64 x 2 blocks
+    t, ns = plan(h)
+    assert t == 4 and ns == 4
+    assert lib.hyres_conv_workspace_bytes(ctypes.byref(h)) >= ns * 16 * 16 * 16 * 128 * 4
+    big = _geom("hyres_geom_conv2d", 16, 128, 128, 64, 64, 64, 64, 3, 3, 1, 1, 1)
+    assert plan(big) == (1, 1)
