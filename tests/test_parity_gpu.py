@@ -1063,7 +1063,7 @@ def test_compress_bitstream_matches_oracle():
 # ------------------------------------------------------------------------------------------------ AMP
 AMP_CASES = [(2, 64, 64, 16, 16, 3, 1, 1, 1), (2, 128, 192, 16, 16, 5, 2, 2, 1), (2, 192, 96, 8, 8, 1, 1, 0, 1),
              (2, 64, 64, 16, 16, 3, 1, 2, 2), (2, 128, 128, 32, 32, 1, 1, 0, 1), (2, 192, 384, 8, 8, 5, 1, 2, 1),
-             # halo-tile kernel: 32-channel chunks, partial 16x16 tiles, Co not a multiple of 64
+             # odd spatial sizes, Co a multiple of 32 but not of 64 (partial N tiles in fwd and dgrad)
              (2, 96, 96, 20, 20, 3, 1, 1, 1), (3, 64, 96, 36, 12, 3, 1, 1, 1), (1, 128, 128, 48, 40, 3, 1, 2, 2)]
 
 
