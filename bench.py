@@ -332,10 +332,14 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1 or os.environ.get("HYRES_BENCH_FORCE_DIST") == "1"  # rehearse the RCCL path at N=1
+    # rehearsal knobs for the N>1 path on a one-GPU box: HYRES_BENCH_ONE_GPU=1 puts every rank on device 0,
+    # HYRES_BENCH_BACKEND=gloo replaces RCCL (which refuses two ranks on one device); defaults = the real run
+    if os.environ.get("HYRES_BENCH_ONE_GPU") == "1":
+        local = 0
     if dist:
         import torch.distributed as tdist
         torch.cuda.set_device(local)
-        tdist.init_process_group("nccl")
+        tdist.init_process_group(os.environ.get("HYRES_BENCH_BACKEND", "nccl"))
     dev = torch.device("cuda", local)
 
     from hyres_hip.weights import synthetic_state_dict
@@ -435,7 +439,7 @@ def main():
         tdist.barrier()
     torch.cuda.synchronize()
     elapsed = time.time() - t0
-    loss_val = float(c["loss"])
+    loss_val = float(c["loss"].detach())
     # dominant-kernel roofline, measured live with HIP events (on the stream each conv launch goes to:
     # torch's current stream, also inside the branch streams) around every conv_fwd_kernel launch of one
     # eager step of the same workload right after the timed region (a graph replay cannot carry
