@@ -626,26 +626,39 @@ __global__ __launch_bounds__(256) void conv_narrow_kernel(const ConvArgs a) {
         float acc[CO];
 #pragma unroll
         for (int c = 0; c < CO; ++c) acc[c] = 0.f;
-        for (int t = 0; t < ntap; ++t) {
-            const int2 o = tapoff[t];
-            const int ih = i * g.ish + o.x, iw = j * g.isw + o.y;
-            const bool in = ok && (unsigned)ih < (unsigned)g.Hi && (unsigned)iw < (unsigned)g.Wi;
-            const int off = in ? (base + (ih * g.Wi + iw) * g.ldx + 4 * l16) * 4 : (int)0x80000000;
-            float4 xv[S];
+        // taps in groups of TG: all TG input rows are requested before the first FMA (a loop of one load
+        // then its FMAs serialised ~9 memory latencies per output pixel: 254 us -> see DESIGN §4)
+        constexpr int TG = 9;
+        for (int t0 = 0; t0 < ntap; t0 += TG) {
+            float4 xv[TG][S];
 #pragma unroll
-            for (int s2 = 0; s2 < S; ++s2)
-                xv[s2] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                        xr, in ? off + 256 * s2 : off, 0, 0));
+            for (int u = 0; u < TG; ++u) {
+                const int t = t0 + u;
+                const int2 o = tapoff[t < ntap ? t : 0];
+                const int ih = i * g.ish + o.x, iw = j * g.isw + o.y;
+                const bool in = ok && t < ntap && (unsigned)ih < (unsigned)g.Hi && (unsigned)iw < (unsigned)g.Wi;
+                const int off = in ? (base + (ih * g.Wi + iw) * g.ldx + 4 * l16) * 4 : (int)0x80000000;
 #pragma unroll
-            for (int s2 = 0; s2 < S; ++s2)
+                for (int s2 = 0; s2 < S; ++s2)
+                    xv[u][s2] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                              xr, in ? off + 256 * s2 : off, 0, 0));
+            }
 #pragma unroll
-                for (int co = 0; co < CO; ++co) {
-                    const float4 w = *reinterpret_cast<const float4*>(&Ws[(t * CO + co) * CI + 64 * s2 + 4 * l16]);
-                    acc[co] = fmaf(xv[s2].x, w.x, acc[co]);
-                    acc[co] = fmaf(xv[s2].y, w.y, acc[co]);
-                    acc[co] = fmaf(xv[s2].z, w.z, acc[co]);
-                    acc[co] = fmaf(xv[s2].w, w.w, acc[co]);
-                }
+            for (int u = 0; u < TG; ++u) {
+                const int t = t0 + u;
+                if (t >= ntap) break;
+#pragma unroll
+                for (int s2 = 0; s2 < S; ++s2)
+#pragma unroll
+                    for (int co = 0; co < CO; ++co) {
+                        const float4 w =
+                            *reinterpret_cast<const float4*>(&Ws[(t * CO + co) * CI + 64 * s2 + 4 * l16]);
+                        acc[co] = fmaf(xv[u][s2].x, w.x, acc[co]);
+                        acc[co] = fmaf(xv[u][s2].y, w.y, acc[co]);
+                        acc[co] = fmaf(xv[u][s2].z, w.z, acc[co]);
+                        acc[co] = fmaf(xv[u][s2].w, w.w, acc[co]);
+                    }
+            }
         }
 #pragma unroll
         for (int co = 0; co < CO; ++co) {
@@ -1229,6 +1242,174 @@ __global__ __launch_bounds__(256) void wgrad_f16_kernel(const WgradArgs a) {
     });
 }
 
+// ------------------------------------------------------------------------------------------------
+// Thin-operand weight gradient: dW[t][m][n] = sum_q P[q][m] * Q[shift_t(q)][n] with N <= 4 (the 3-channel
+// image side: refine conv 3->64 / 64->3 at 256^2 (the latter through the swapped descriptor), g_a's 5x5 s2
+// conv 3->128, g_s's deconv 128->3) and M = 64*MW wide channels. An MFMA tile would be >90 % padding and
+// the tap-folded MFMA path gathers Q with scalar loads (13-15 TF/s, ~1 TB/s, 240-280 us per layer); here
+// the work is VALU FMAs at the HBM rate of P:
+//   * a block owns ``rpb`` consecutive base-grid rows (b, i) and one group of TG taps (grid.y);
+//   * per row, the Q rows the group's taps touch (<= THIN_ROWS rows x (Wq-1)*sq + tap span columns) are
+//     staged once in LDS as float4 (n padded to 4), zero outside the image;
+//   * wave w walks pixels j = w, w+4, ...: lane l holds P[q][l + 64*mw] (coalesced rows, the next pixel's
+//     row prefetched before this pixel's FMAs), the tap's Q values are one broadcast ds_read_b128;
+//   * per-lane accumulators [MW][TG][NC] (+ the P column sums = the bias gradient) are reduced over the
+//     block's 4 waves through LDS into the split slab [block][t][m][n]; the deterministic slab reduce of
+//     the generic path finishes it.
+// ------------------------------------------------------------------------------------------------
+constexpr int THIN_ROWS = 5, THIN_SPAN = 264;  // staged window: rows x columns (host check: ncol <= SPAN)
+constexpr int THIN_COLS = THIN_SPAN;
+constexpr int THIN_STAGE = (THIN_ROWS * THIN_COLS + 255) / 256;  // staged window entries per thread
+
+template <int MW, int NC, int TG, int SQ>
+__global__ __launch_bounds__(256) void wgrad_thin_kernel(const WgradArgs a, int rpb, int dhmin, int dwmin, int nrow,
+                                                         int ncol) {
+    constexpr int PCH = 64 / MW;            // pixels per P chunk (PCH x 64*MW floats = 16 KB)
+    constexpr int PV = PCH * 16 * MW / 256;  // float4 per thread per chunk
+    constexpr int PPW = PCH / 4;             // pixels per wave per chunk
+    __shared__ __attribute__((aligned(16))) float Qs[THIN_ROWS * THIN_COLS * 4];
+    __shared__ __attribute__((aligned(16))) float Ps[PCH * 64 * MW];
+    const hyres_wgrad_desc& d = a.d;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int blk = blockIdx.x, grp = blockIdx.y;
+    const int t0 = grp * TG;
+    const int ntg = min(TG, d.ntaps - t0);
+    const int R = d.B * d.Hq;
+    const int r0 = blk * rpb, r1 = min(R, r0 + rpb);
+    const bool do_bias = a.bias_slab != nullptr && grp == 0;
+    const int nst = nrow * THIN_COLS;
+    // per-tap window offsets through LDS (an indexed read of the by-value descriptor's tap arrays would
+    // copy them to scratch); taps past ntg read any slot: their accumulators are never stored
+    __shared__ int toff_s[TG];
+    if (tid < TG)
+        toff_s[tid] = tid < ntg ? ((d.dh[t0 + tid] - dhmin) * THIN_COLS + (d.dw[t0 + tid] - dwmin)) * 4 : 0;
+    __syncthreads();
+    int toff[TG];
+#pragma unroll
+    for (int u = 0; u < TG; ++u) toff[u] = toff_s[u];
+    // accumulators as float4 (thin channels in .xyzw): an array of MW*TG vectors stays in registers where
+    // a [MW][TG][4] float array (> 32 elements) is demoted to scratch
+    float4 acc[MW][TG];
+    float bsum[MW];
+#pragma unroll
+    for (int w = 0; w < MW; ++w) {
+        bsum[w] = 0.f;
+#pragma unroll
+        for (int u = 0; u < TG; ++u) acc[w][u] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    float4 pr4[PV];
+    for (int r = r0; r < r1; ++r) {
+        const int b = r / d.Hq, i = r - (r / d.Hq) * d.Hq;
+        const float* prow = a.p + (long long)r * d.Wq * d.ldp;
+        auto load_chunk = [&](int c0) {
+#pragma unroll
+            for (int k = 0; k < PV; ++k) {
+                const int idx = tid + 256 * k;
+                const int px = idx / (16 * MW), c4 = idx - (idx / (16 * MW)) * (16 * MW);
+                pr4[k] = c0 + px < d.Wq ? ld4(prow + (long long)(c0 + px) * d.ldp + 4 * c4)
+                                        : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+        };
+        load_chunk(0);
+        __syncthreads();  // the previous row's readers of Qs / Ps are done
+        // this row's Q window (zero outside the image, past N channels and past column ncol): every load of
+        // the window is issued before the first LDS store (a rolled loop serialised one latency per entry)
+        {
+            float4 qv[THIN_STAGE];
+#pragma unroll
+            for (int k = 0; k < THIN_STAGE; ++k) {
+                const int idx = tid + 256 * k;
+                const int rr = idx / THIN_COLS, cc = idx - (idx / THIN_COLS) * THIN_COLS;
+                const int ih = i * SQ + dhmin + rr, iw = dwmin + cc;
+                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (idx < nst && cc < ncol && (unsigned)ih < (unsigned)d.Hqq && (unsigned)iw < (unsigned)d.Wqq) {
+                    const float* qp = a.q + ((long long)(b * d.Hqq + ih) * d.Wqq + iw) * d.ldq;
+                    v.x = qp[0];
+                    if (NC > 1 && d.N > 1) v.y = qp[1];
+                    if (NC > 2 && d.N > 2) v.z = qp[2];
+                    if (NC > 3 && d.N > 3) v.w = qp[3];
+                }
+                qv[k] = v;
+            }
+#pragma unroll
+            for (int k = 0; k < THIN_STAGE; ++k)
+                if (tid + 256 * k < nst) *reinterpret_cast<float4*>(&Qs[(tid + 256 * k) * 4]) = qv[k];
+        }
+        for (int c0 = 0; c0 < d.Wq; c0 += PCH) {
+            if (c0) __syncthreads();  // the previous chunk's readers of Ps are done
+#pragma unroll
+            for (int k = 0; k < PV; ++k) *reinterpret_cast<float4*>(&Ps[4 * (tid + 256 * k)]) = pr4[k];
+            __syncthreads();
+            if (c0 + PCH < d.Wq) load_chunk(c0 + PCH);  // next chunk in flight during this chunk's FMAs
+#pragma unroll 2
+            for (int uu = 0; uu < PPW; ++uu) {
+                const int pl = wave * PPW + uu;
+                const int j = c0 + pl;
+                if (j >= d.Wq) break;  // wave-uniform
+                float pv[MW];
+#pragma unroll
+                for (int w = 0; w < MW; ++w) pv[w] = Ps[pl * 64 * MW + 64 * w + lane];
+                const float* qg = Qs + j * SQ * 4;
+#pragma unroll
+                for (int v = 0; v < TG; ++v) {
+                    const float4 q = *reinterpret_cast<const float4*>(qg + toff[v]);
+#pragma unroll
+                    for (int w = 0; w < MW; ++w) {
+                        acc[w][v].x = fmaf(pv[w], q.x, acc[w][v].x);
+                        if (NC > 1) acc[w][v].y = fmaf(pv[w], q.y, acc[w][v].y);
+                        if (NC > 2) acc[w][v].z = fmaf(pv[w], q.z, acc[w][v].z);
+                        if (NC > 3) acc[w][v].w = fmaf(pv[w], q.w, acc[w][v].w);
+                    }
+                }
+#pragma unroll
+                for (int w = 0; w < MW; ++w) bsum[w] += pv[w];
+            }
+        }
+    }
+    float* red = Qs;
+    // reduce the 4 waves' partials: one tap at a time through LDS ([wave][MW*NC][64]), wave 0 writes
+    const long long MN = (long long)d.M * d.N;
+    static_for<TG>([&](auto U) {  // compile-time tap index: acc stays in registers
+        constexpr int u = decltype(U)::value;
+        if (u < ntg) {
+            __syncthreads();
+#pragma unroll
+            for (int w = 0; w < MW; ++w) {
+                const float av[4] = {acc[w][u].x, acc[w][u].y, acc[w][u].z, acc[w][u].w};
+#pragma unroll
+                for (int n = 0; n < NC; ++n) red[(wave * MW * NC + w * NC + n) * 64 + lane] = av[n];
+            }
+            __syncthreads();
+            if (wave == 0) {
+                float* out = a.slab + ((long long)blk * d.ntaps + t0 + u) * MN;
+#pragma unroll
+                for (int w = 0; w < MW; ++w)
+#pragma unroll
+                    for (int n = 0; n < NC; ++n) {
+                        if (n >= d.N) continue;
+                        const int kk = (w * NC + n) * 64 + lane;
+                        const float v = red[kk] + red[MW * NC * 64 + kk] + red[2 * MW * NC * 64 + kk] +
+                                        red[3 * MW * NC * 64 + kk];
+                        out[(long long)(lane + 64 * w) * d.N + n] = v;
+                    }
+            }
+        }
+    });
+    if (do_bias) {
+        __syncthreads();
+#pragma unroll
+        for (int w = 0; w < MW; ++w) red[(wave * MW + w) * 64 + lane] = bsum[w];
+        __syncthreads();
+        if (wave == 0)
+#pragma unroll
+            for (int w = 0; w < MW; ++w) {
+                const int k = w * 64 + lane;
+                a.bias_slab[(long long)blk * d.M + lane + 64 * w] =
+                    red[k] + red[MW * 64 + k] + red[2 * MW * 64 + k] + red[3 * MW * 64 + k];
+            }
+    }
+}
+
 // deterministic split-K reduce: LX float4 lanes x (256 / LX) split groups per block (4*LX outputs per
 // block). Few outputs with many splits (1x1 / small weights over a whole batch: nsplit up to 512) take
 // LX = 4, so each thread walks nsplit/64 partial rows instead of nsplit/16 and 4x as many blocks run.
@@ -1674,6 +1855,7 @@ static int env_int(const char* name, int dflt) {
 //   * small grids (<= 65536 output pixels: the 64^2 and 32^2 regions at bs 16): 64-row tiles, 64 wide up to
 //     192 channels (fp32) / below 192 (f16), else 64x128 (fp32) / 128x128 (f16); measured per geometry
 //     over every tile and split-K target (scripts/tile_sweep.py, profiles/r2_tile_sweep_*.txt);
+//   * the scalar-load path (Ci % 32 != 0: the 3-channel image side) 64-row tiles (3->64 at 256^2: 198 -> 140 us);
 //   * otherwise 128-row tiles as wide as Co allows.
 // Split-K engages only when the chosen tile leaves fewer than 512 blocks and K has >= 8 chunks.
 struct ConvChoice {
@@ -1685,7 +1867,7 @@ static const int TILE_BN[5] = {128, 64, 32, 128, 64};
 
 // Tile / split-K overrides set through hyres_conv_tuning (tuning sweeps; -1 = the heuristics below)
 // keys: HYRES_TUNE_TILE, _SPLIT_BLOCKS, _SPLIT_MINCHUNKS, _WGRAD_BLOCKS, _WGRAD_MINCHUNKS, _WGRAD_NT
-static int g_tune[6] = {-1, -1, -1, -1, -1, -1};
+static int g_tune[7] = {-1, -1, -1, -1, -1, -1, -1};  // + _WGRAD_MAXSPLIT
 
 static ConvChoice choose_conv(const hyres_conv_geom* g, const hyres_epilogue* e, bool aligned) {
     ConvChoice c{};
@@ -1702,6 +1884,7 @@ static ConvChoice choose_conv(const hyres_conv_geom* g, const hyres_epilogue* e,
         if (f16) c.tile = g->Co >= 192 ? 0 : 4;
         else c.tile = g->Co > 192 ? 3 : 4;
     }
+    else if (c.mode == 2 && g->Co > 32) c.tile = g->Co > 64 ? 3 : 4;  // scalar-load path: 64-row tiles
     else if (g->Co > 64) c.tile = 0;
     else if (g->Co > 32) c.tile = 1;
     else c.tile = 2;
@@ -1742,7 +1925,7 @@ static long long plan_ws_bytes(const hyres_conv_geom* g, const ConvPlan& p) {
 }
 
 int hyres_conv_tuning(int key, int value, int* old) {
-    HY_REQUIRE(key >= 0 && key < 6, HYRES_E_ARG, "conv_tuning: key %d", key);
+    HY_REQUIRE(key >= 0 && key < 7, HYRES_E_ARG, "conv_tuning: key %d", key);
     if (old) *old = g_tune[key];
     g_tune[key] = value;
     return ok();
@@ -1954,7 +2137,8 @@ static WgradPlan wgrad_plan(const hyres_wgrad_desc* d) {
     const int tb = g_tune[3] > 0 ? g_tune[3] : (small ? 2 * tb_env : tb_env);
     const int mc0 = g_tune[4] > 0 ? g_tune[4] : ((small && kt == KT && d->ntaps > 1) ? mc_env / 2 : mc_env);
     const int mc = std::max(1, mc0 * KT / kt);
-    static const int ms = env_int("HYRES_WGRAD_MAXSPLIT", 512);
+    static const int ms_env = env_int("HYRES_WGRAD_MAXSPLIT", 512);
+    const int ms = g_tune[6] > 0 ? g_tune[6] : ms_env;
     const long long slab_cap = std::max<long long>(4, (16LL << 20) / ((long long)d->ntaps * d->M * d->N));
     const long long want = std::min<long long>(std::max<long long>(1, (tb + tiles - 1) / tiles), slab_cap);
     const long long maxsplit = std::max<long long>(1, p.nchunks / mc);
@@ -1988,6 +2172,65 @@ static hyres_wgrad_desc wgrad_swapped(const hyres_wgrad_desc* d) {
     return e;
 }
 
+// thin-operand weight-gradient plan (wgrad_thin_kernel): N <= 4, M in {64, 128}, the staged Q window fits
+struct ThinPlan {
+    int mw, nc, tg, ngroups, rpb, nblk, dhmin, dwmin, nrow, ncol, sq;
+};
+
+static bool thin_plan(const hyres_wgrad_desc* d, ThinPlan* tp) {
+    static const int on = env_int("HYRES_WGRAD_THIN", 1);
+    if (!on || d->N > 4 || (d->M != 64 && d->M != 128) || d->square_q || d->ntaps < 1 || d->ntaps > 25)
+        return false;
+    int hmin = 1 << 30, hmax = -(1 << 30), wmin = 1 << 30, wmax = -(1 << 30);
+    for (int t = 0; t < d->ntaps; ++t) {
+        hmin = std::min(hmin, d->dh[t]); hmax = std::max(hmax, d->dh[t]);
+        wmin = std::min(wmin, d->dw[t]); wmax = std::max(wmax, d->dw[t]);
+    }
+    ThinPlan p{};
+    p.dhmin = hmin; p.dwmin = wmin;
+    p.nrow = hmax - hmin + 1;
+    p.ncol = (d->Wq - 1) * d->sq + (wmax - wmin) + 1;
+    if (p.nrow > THIN_ROWS || p.ncol > THIN_SPAN || (d->sq != 1 && d->sq != 2)) return false;
+    if (d->ldp % 4 != 0) return false;  // P chunks staged as float4
+    p.mw = d->M / 64;
+    p.nc = d->N == 3 ? 3 : 4;
+    p.sq = d->sq;
+    p.tg = d->ntaps <= 9 ? 9 : (p.mw == 1 ? 25 : 13);
+    p.ngroups = ceil_div(d->ntaps, p.tg);
+    const int R = d->B * d->Hq;
+    p.rpb = std::max(1, ceil_div(R * p.ngroups, 1024));  // ~1024 blocks (4 per CU)
+    p.nblk = ceil_div(R, p.rpb);
+    *tp = p;
+    return true;
+}
+
+static void launch_thin(const WgradArgs& a, const ThinPlan& p, hipStream_t st) {
+    const dim3 grid(p.nblk, p.ngroups);
+    auto go = [&](auto mw, auto nc, auto tg) {
+        constexpr int MW_ = decltype(mw)::value, NC_ = decltype(nc)::value, TG_ = decltype(tg)::value;
+        if (p.sq == 1)
+            hipLaunchKernelGGL((wgrad_thin_kernel<MW_, NC_, TG_, 1>), grid, dim3(256), 0, st, a, p.rpb, p.dhmin,
+                               p.dwmin, p.nrow, p.ncol);
+        else
+            hipLaunchKernelGGL((wgrad_thin_kernel<MW_, NC_, TG_, 2>), grid, dim3(256), 0, st, a, p.rpb, p.dhmin,
+                               p.dwmin, p.nrow, p.ncol);
+    };
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using I3 = std::integral_constant<int, 3>;
+    using I4 = std::integral_constant<int, 4>;
+    using I9 = std::integral_constant<int, 9>;
+    using I13 = std::integral_constant<int, 13>;
+    using I25 = std::integral_constant<int, 25>;
+    if (p.mw == 1) {
+        if (p.nc == 3) { if (p.tg == 9) go(I1{}, I3{}, I9{}); else go(I1{}, I3{}, I25{}); }
+        else { if (p.tg == 9) go(I1{}, I4{}, I9{}); else go(I1{}, I4{}, I25{}); }
+    } else {
+        if (p.nc == 3) { if (p.tg == 9) go(I2{}, I3{}, I9{}); else go(I2{}, I3{}, I13{}); }
+        else { if (p.tg == 9) go(I2{}, I4{}, I9{}); else go(I2{}, I4{}, I13{}); }
+    }
+}
+
 template <int TM, int TN, int WM_, int WN_, int NT>
 static void launch_wgrad(const WgradArgs& a, bool vp, bool vq, bool sqr, dim3 grid, hipStream_t st) {
     if (vp && vq && sqr) hipLaunchKernelGGL((wgrad_kernel<TM, TN, WM_, WN_, NT, true, true, true>), grid, dim3(256), 0, st, a);
@@ -2010,9 +2253,19 @@ long long hyres_wgrad_workspace_bytes(const hyres_wgrad_desc* d) {
     hyres_wgrad_desc e = swap ? wgrad_swapped(d) : *d;
     WgradPlan p = wgrad_plan(&e);
     // + the bias-gradient partials: [nsplit][M] in the kernel, or colsum partials when swapped
-    const long long bias = swap ? hyres_colsum_workspace_bytes(d->B * d->Hq * d->Wq, d->M) / 4 + 4
-                                : (long long)p.nsplit * e.M + 4;
-    return (wgrad_slab_floats(&e, p) + bias) * 4;
+    auto need = [&](const WgradPlan& q) {
+        const long long bias = swap ? hyres_colsum_workspace_bytes(d->B * d->Hq * d->Wq, d->M) / 4 + 4
+                                    : (long long)q.nsplit * e.M + 4;
+        return (wgrad_slab_floats(&e, q) + bias) * 4;
+    };
+    long long bytes = need(p);
+    ThinPlan tp;
+    if (thin_plan(&e, &tp)) {  // one slab row per thin block (the launch may still take the generic path
+        WgradPlan q = p;       // when P is not 16-byte aligned: cover both)
+        q.nsplit = tp.nblk;
+        bytes = std::max(bytes, need(q));
+    }
+    return bytes;
 }
 
 int hyres_conv_wgrad(const hyres_wgrad_desc* d0, const float* pp, const float* qq, float* dst, float* dbias,
@@ -2026,6 +2279,9 @@ int hyres_conv_wgrad(const hyres_wgrad_desc* d0, const float* pp, const float* q
     const hyres_wgrad_desc* d = &dd;
     if (swap) std::swap(pp, qq);
     WgradPlan p = wgrad_plan(d);
+    ThinPlan tp;
+    const bool thin = thin_plan(d, &tp) && aligned16(pp);
+    if (thin) p.nsplit = tp.nblk;
     float* bias_ws = (float*)ws + wgrad_slab_floats(d, p);
     const bool vp = (d->M % 4 == 0) && (d->ldp % 4 == 0) && aligned16(pp);
     const bool vq = !p.tapn && (d->N % 4 == 0) && (d->ldq % 4 == 0) && aligned16(qq);
@@ -2039,7 +2295,9 @@ int hyres_conv_wgrad(const hyres_wgrad_desc* d0, const float* pp, const float* q
     dim3 grid(ceil_div(p.nblocks, 8) * 8);
     hipStream_t st = as_stream(s);
     const bool sqr = d->square_q != 0;
-    if (wgrad_f16_ok(d)) {
+    if (thin) {
+        launch_thin(a, tp, st);
+    } else if (wgrad_f16_ok(d)) {
         auto f16 = [&](auto tm, auto tn, auto wm_, auto wn_, auto ntc) {
             constexpr int TM_ = decltype(tm)::value, TN_ = decltype(tn)::value;
             constexpr int WM2 = decltype(wm_)::value, WN2 = decltype(wn_)::value, NT_ = decltype(ntc)::value;

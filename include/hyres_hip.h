@@ -144,6 +144,7 @@ int hyres_conv_plan(const hyres_conv_geom* g, const hyres_epilogue* e, int* tile
 #define HYRES_TUNE_WGRAD_BLOCKS 3     /* weight gradients: split-K target block count */
 #define HYRES_TUNE_WGRAD_MINCHUNKS 4  /* minimum 32-pixel chunks per split */
 #define HYRES_TUNE_WGRAD_NT 5         /* 1: no tap grouping (one tap per block column group) */
+#define HYRES_TUNE_WGRAD_MAXSPLIT 6   /* maximum split count */
 int hyres_conv_tuning(int key, int value, int* old);
 
 /* Weight gradient:  dW[t][m][n] = sum_q P[q][m] * Q[shift_t(q)][n]  over a base grid q (B,Hq,Wq).

@@ -34,11 +34,13 @@ GEOMS = [
     (128, 128, 64, 1, 1, False),
     (128, 64, 128, 1, 1, True),
 ]
-# weight gradients (H, Ci, Co, K): P = dY [.., Co], Q = X [.., Ci]
+# weight gradients (H, Ci, Co, K[, stride]): P = dY [.., Co], Q = X [.., Ci]
 WGEOMS = [
     (32, 96, 96, 3), (32, 96, 192, 1), (32, 192, 96, 1), (32, 192, 384, 5), (32, 192, 384, 3),
     (32, 768, 640, 1), (32, 512, 384, 1), (64, 64, 64, 3), (64, 128, 64, 1), (128, 64, 64, 3),
 ]
+# the image-side 3-channel layers (refine conv 3->64 / 64->3 at 256^2, g_a's 5x5 s2 3->128)
+WGEOMS3 = [(256, 3, 64, 3, 1), (256, 64, 3, 3, 1), (256, 3, 128, 5, 2)]
 TILES = [0, 1, 2, 3, 4]
 SPLITS = [0, 512, 1024, 2048]
 
@@ -49,6 +51,7 @@ def main():
     ap.add_argument("--f16", action="store_true")
     ap.add_argument("--B", type=int, default=16)
     ap.add_argument("--wgrad", action="store_true")
+    ap.add_argument("--three", action="store_true", help="--wgrad over the 3-channel layers, incl. max split")
     a = ap.parse_args()
     if a.wgrad:
         return sweep_wgrad(a)
@@ -76,7 +79,8 @@ def main():
         torch.cuda.synchronize()
         return 1000 * e0.elapsed_time(e1) / a.iters
 
-    for H, Ci, Co, K, s, r in GEOMS:
+    geoms = [(256, 3, 64, 3, 1, False), (256, 3, 128, 5, 2, False)] if a.three else GEOMS
+    for H, Ci, Co, K, s, r in geoms:
         x = O.Node(torch.randn(a.B, H, H, Ci, device=dev), rg=False)
         w = torch.randn(Co, Ci, K, K, device=dev) / (Ci * K * K) ** 0.5
         b = torch.randn(Co, device=dev)
@@ -108,11 +112,14 @@ def sweep_wgrad(a):
     def tune(k, v):
         L.check(lib.hyres_conv_tuning(k, v, None), "tuning")
 
-    for H, Ci, Co, K in WGEOMS:
+    for geom in (WGEOMS3 if a.three else WGEOMS):
+        H, Ci, Co, K = geom[:4]
+        st = geom[4] if len(geom) > 4 else 1
         d = L.WgradDesc()
-        L.check(lib.hyres_wgrad_desc_conv2d(ctypes.byref(d), a.B, H, H, Ci, Ci, Co, Co, K, K, 1, K // 2, 1), "desc")
+        L.check(lib.hyres_wgrad_desc_conv2d(ctypes.byref(d), a.B, H, H, Ci, Ci, Co, Co, K, K, st, K // 2, 1), "desc")
         d.f16_operands = int(a.f16)
-        P = torch.randn(a.B, H, H, Co, device=dev)
+        Ho = (H + 2 * (K // 2) - K) // st + 1
+        P = torch.randn(a.B, Ho, Ho, Co, device=dev)
         Q = torch.randn(a.B, H, H, Ci, device=dev)
         dst = torch.zeros(Co, Ci, K, K, device=dev)
         db = torch.zeros(Co, device=dev)
@@ -134,22 +141,29 @@ def sweep_wgrad(a):
             torch.cuda.synchronize()
             return 1000 * e0.elapsed_time(e1) / a.iters
 
-        for k in (3, 4, 5):
+        for k in (3, 4, 5, 6):
             tune(k, -1)
         base = timeit()
         rows = []
-        for tb in (1024, 2048, 4096):
-            for mc in (2, 4, 8):
-                for nt in (-1, 1):
-                    tune(3, tb), tune(4, mc), tune(5, nt)
-                    rows.append((timeit(), tb, mc, nt))
-        for k in (3, 4, 5):
+        if a.three:
+            for tb in (2048, 8192, 32768):
+                for mc in (2, 4, 8):
+                    for msx in (512, 2048, 8192):
+                        tune(3, tb), tune(4, mc), tune(6, msx)
+                        rows.append((timeit(), tb, mc, msx))
+        else:
+            for tb in (1024, 2048, 4096):
+                for mc in (2, 4, 8):
+                    for nt in (-1, 1):
+                        tune(3, tb), tune(4, mc), tune(5, nt)
+                        rows.append((timeit(), tb, mc, nt))
+        for k in (3, 4, 5, 6):
             tune(k, -1)
         rows.sort()
-        flops = 2.0 * a.B * H * H * K * K * Ci * Co
+        flops = 2.0 * a.B * Ho * Ho * K * K * Ci * Co
         us, tb, mc, nt = rows[0]
         print(f"WGRAD B{a.B} {H}x{H} {Ci}->{Co} K{K}{' f16' if a.f16 else ''}: heuristic {base:.1f} us "
-              f"({flops / base / 1e6:.1f} TF/s) | best blocks {tb} minchunks {mc} nt {nt}: {us:.1f} us "
+              f"({flops / base / 1e6:.1f} TF/s) | best blocks {tb} minchunks {mc} {'maxsplit' if a.three else 'nt'} {nt}: {us:.1f} us "
               f"({flops / us / 1e6:.1f} TF/s) | top3 " +
               " ".join(f"b{b}/c{c}/n{n}:{u:.1f}" for u, b, c, n in rows[:3]), flush=True)
 

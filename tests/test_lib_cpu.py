@@ -145,7 +145,7 @@ def test_conv_kernel_name_follows_the_launch_routing():
     gn = _geom("hyres_geom_conv2d", 16, 256, 256, 64, 64, 3, 3, 3, 3, 1, 1, 1)
     assert conv_variant(gn, e, False) == "conv_narrow_kernel<3, 1>"
     gs = _geom("hyres_geom_conv2d", 16, 256, 256, 3, 3, 64, 64, 3, 3, 1, 1, 1)  # Ci = 3: scalar path
-    assert conv_variant(gs, e, False) == "conv_fwd_kernel<2, 1, 2, 2, 2, false, false>"
+    assert conv_variant(gs, e, False) == "conv_fwd_kernel<1, 1, 2, 2, 2, false, false>"
     e.square_input = 1
     g2 = _geom("hyres_geom_conv2d", 16, 128, 128, 128, 128, 128, 128, 1, 1, 1, 0, 1)
     assert conv_variant(g2, e, False) == "conv_fwd_kernel<1, 2, 2, 2, 1, false, false>"

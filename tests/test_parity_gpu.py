@@ -48,6 +48,12 @@ CONV_CASES = [
     (2, 64, 96, 16, 16, 5, 1, 2, 1),   # wgrad: 5 fused taps per block
     (2, 5, 48, 12, 12, 3, 1, 1, 1),    # wgrad: taps folded into N (N=5)
     (2, 48, 5, 12, 12, 3, 1, 1, 1),    # wgrad: small-M swap (M=5)
+    # thin-operand weight gradient (wgrad_thin_kernel): N <= 4, M in {64, 128}
+    (2, 1, 64, 20, 36, 3, 1, 1, 1),    # N = 1 (4-channel accumulator variant)
+    (2, 64, 2, 20, 36, 3, 1, 1, 1),    # swapped (M = 2 -> wide 64, thin 2)
+    (1, 3, 64, 6, 256, 3, 1, 2, 2),    # 256-wide row window, dilation 2
+    (1, 3, 64, 4, 300, 3, 1, 1, 1),    # window wider than the LDS stage: generic tap-folded path
+    (2, 3, 128, 16, 40, 5, 2, 2, 1),   # two tap groups, stride 2
 ]
 
 
