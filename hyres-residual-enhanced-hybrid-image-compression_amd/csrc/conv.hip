@@ -1019,6 +1019,135 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgradArgs a) {
 
 
 // ------------------------------------------------------------------------------------------------
+// Halo-staged weight gradient for stride-1 KxK convolutions (K = 3: one block does all 9 taps; K = 5: one
+// kernel row of 5 taps per block) whose rows are a multiple of 32 pixels, so a 32-pixel K chunk is one row
+// segment (b, i, j0..j0+31). Per chunk the block stages P (32 px x 64 m) and ONE Q halo tile (KR rows x
+// (32 + K - 1) px x 64 n) in LDS, double-buffered, and every tap reads its B operand from the halo at
+// its (dh, dw) shift. The generic kernel instead gathers a shifted 32-px Q chunk per tap (9 global loads
+// and 9 barriers per chunk, the latency of each exposed at 2 blocks per CU); here it is one load of
+// 3 x 34 px per chunk and one barrier per 9 x 16 MFMAs. 64 x 64 tiles, 4 waves of 32 x 32.
+// ------------------------------------------------------------------------------------------------
+template <int KR, int KW>
+__global__ __launch_bounds__(256, 2) void wgrad_halo_kernel(const WgradArgs a, int dhg, int dwg) {
+    constexpr int BM = 64, BN = 64, NT = KR * KW, HC = 32 + KW - 1;
+    constexpr int PP = BM + 4, PQ = BN + 4;
+    constexpr int PSZ = KT * PP, HSZ = KR * HC * PQ;
+    constexpr int P_V = KT * BM / 4 / 256;
+    constexpr int H_E = KR * HC * (BN / 4);
+    constexpr int H_V = (H_E + 255) / 256;
+    __shared__ __attribute__((aligned(16))) float smem[2 * (PSZ + HSZ)];
+    const hyres_wgrad_desc& d = a.d;
+    const int tid = threadIdx.x;
+    const int bid = blockIdx.x;
+    const int lb = (bid & 7) * (gridDim.x >> 3) + (bid >> 3);  // XCD-aware order, as wgrad_kernel
+    if (lb >= a.nblocks) return;
+    int rr = lb;
+    const int mt = rr % a.mtiles; rr /= a.mtiles;
+    const int nt = rr % a.ntiles; rr /= a.ntiles;
+    const int grp = rr % a.ngroups;
+    const int split = rr / a.ngroups;
+    const int m0 = mt * BM, n0 = nt * BN;
+    const int t0 = grp * NT;
+    const int dh0 = dhg + grp * KR;  // the group's first kernel row offset, first column offset dwg
+    const int cpr = d.Wq / 32;
+    float4 rp[P_V], rh[H_V];
+    auto load = [&](int kc) {
+        const int b = kc / (d.Hq * cpr);
+        const int rem = kc - b * d.Hq * cpr;
+        const int i = rem / cpr;
+        const int j0 = (rem - i * cpr) * 32;
+        const long long q0 = (long long)kc * 32;
+#pragma unroll
+        for (int q = 0; q < P_V; ++q) {
+            const int e = tid + 256 * q;
+            const int row = e / (BM / 4), c = (e % (BM / 4)) * 4;
+            rp[q] = m0 + c < d.M ? ld4(a.p + (q0 + row) * d.ldp + m0 + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int q = 0; q < H_V; ++q) {
+            const int e = tid + 256 * q;
+            const int pix = e / (BN / 4), c = (e % (BN / 4)) * 4;
+            const int hr = pix / HC, hc = pix - (pix / HC) * HC;
+            const int ih = i + dh0 + hr, iw = j0 + dwg + hc;
+            const bool ok = e < H_E && (unsigned)ih < (unsigned)d.Hqq && (unsigned)iw < (unsigned)d.Wqq && n0 + c < d.N;
+            rh[q] = ok ? ld4(a.q + ((long long)(b * d.Hqq + ih) * d.Wqq + iw) * d.ldq + n0 + c)
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    auto store = [&](int buf) {
+        float* Ps = smem + buf * (PSZ + HSZ);
+        float* Hs = Ps + PSZ;
+#pragma unroll
+        for (int q = 0; q < P_V; ++q) {
+            const int e = tid + 256 * q;
+            *reinterpret_cast<float4*>(&Ps[(e / (BM / 4)) * PP + (e % (BM / 4)) * 4]) = rp[q];
+        }
+#pragma unroll
+        for (int q = 0; q < H_V; ++q) {
+            const int e = tid + 256 * q;
+            if (e < H_E) *reinterpret_cast<float4*>(&Hs[(e / (BN / 4)) * PQ + (e % (BN / 4)) * 4]) = rh[q];
+        }
+    };
+
+    const int lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int lr = lane & 31, lh = lane >> 5;
+    floatx16 acc[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+    const bool do_bias = a.bias_slab != nullptr && nt == 0 && grp == 0;
+    float bsum = 0.f;
+    const int kb = split * a.chunks_per_split;
+    const int ke = min(a.nchunks, kb + a.chunks_per_split);
+    if (kb < ke) {
+        load(kb);
+        store(0);
+    }
+    __syncthreads();
+    int cur = 0;
+    for (int kc = kb; kc < ke; ++kc) {
+        if (kc + 1 < ke) load(kc + 1);  // next chunk in flight during this chunk's NT x 16 MFMAs
+        const float* Ps = smem + cur * (PSZ + HSZ);
+        const float* Hs = Ps + PSZ;
+        if (do_bias && tid < BM) {
+#pragma unroll 8
+            for (int k = 0; k < KT; ++k) bsum += Ps[k * PP + tid];
+        }
+        static_for<NT>([&](auto J) {
+            constexpr int t = decltype(J)::value;
+            constexpr int hr = t / KW, hc = t % KW;
+#pragma unroll
+            for (int s2 = 0; s2 < KT / 2; ++s2) {
+                const int k = lh * (KT / 2) + s2;
+                const float af = Ps[k * PP + wm * 32 + lr];
+                const float bf = Hs[(hr * HC + k + hc) * PQ + wn * 32 + lr];
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(af, bf, acc[t], 0, 0, 0);
+            }
+        });
+        if (kc + 1 < ke) store(cur ^ 1);
+        __syncthreads();
+        cur ^= 1;
+    }
+    if (do_bias && tid < BM && m0 + tid < d.M) a.bias_slab[(long long)split * d.M + m0 + tid] = bsum;
+    const long long MN = (long long)d.M * d.N;
+    static_for<NT>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        const int n = n0 + wn * 32 + lr;
+        if (n < d.N) {
+            float* out = a.slab + ((long long)split * d.ntaps + t0 + j) * MN + n;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                if (m < d.M) out[(long long)m * d.N] = acc[j][r];
+            }
+        }
+    });
+}
+
+
+// ------------------------------------------------------------------------------------------------
 // AMP weight gradient (train.sh --mixed-precision): the same GEMM dW[t][m][n] = sum_q P[q][m] Q_t[q][n]
 // with P and Q rounded to fp16 when staged and consumed by v_mfma_f32_32x32x16_f16 (fp32 accumulation,
 // fp32 bias sums from the unrounded P).  Chunks of KTH = 64 pixels are staged exactly as they arrive
@@ -2095,7 +2224,22 @@ namespace hyres {
 
 struct WgradPlan {
     int TMc, TNc, WMc, WNc, NT, BM, BN, mtiles, ntiles, ngroups, nchunks, nsplit, cps, tapn, nblocks;
+    int halo, hk, hdh, hdw;  // wgrad_halo_kernel: K, first tap's (dh, dw)
 };
+
+// wgrad_halo_kernel applies: fp32, stride-1 dense KxK taps (K = 3 or 5, dilation 1) on rows of a multiple of
+// 32 pixels, both operands >= 32 channels on the float4 path
+static bool halo_ok(const hyres_wgrad_desc* d, int* K) {
+    static const int on = env_int("HYRES_WGRAD_HALO", 1);
+    if (!on || d->f16_operands || d->square_q || d->sq != 1 || d->Hqq != d->Hq || d->Wqq != d->Wq) return false;
+    if (d->Wq % 32 != 0 || d->M < 32 || d->N < 32 || d->M % 4 || d->N % 4 || d->ldp % 4 || d->ldq % 4) return false;
+    const int k = d->ntaps == 9 ? 3 : d->ntaps == 25 ? 5 : 0;
+    if (!k) return false;
+    for (int t = 0; t < d->ntaps; ++t)
+        if (d->dh[t] != d->dh[0] + t / k || d->dw[t] != d->dw[0] + t % k) return false;
+    *K = k;
+    return true;
+}
 
 static bool wgrad_f16_ok(const hyres_wgrad_desc* d);
 
@@ -2123,6 +2267,17 @@ static WgradPlan wgrad_plan(const hyres_wgrad_desc* d) {
     p.mtiles = ceil_div(d->M, p.BM); p.ntiles = ceil_div(ncols, p.BN);
     p.ngroups = p.tapn ? 1 : ceil_div(d->ntaps, p.NT);
     p.nchunks = ceil_div((long long)d->B * d->Hq * d->Wq, kt);
+    if (kt == KT && halo_ok(d, &p.hk)) {
+        p.halo = 1;
+        p.hdh = d->dh[0];
+        p.hdw = d->dw[0];
+        p.tapn = 0;
+        p.TMc = p.TNc = 1; p.WMc = p.WNc = 2;
+        p.BM = p.BN = 64;
+        p.mtiles = ceil_div(d->M, 64); p.ntiles = ceil_div(d->N, 64);
+        p.NT = p.hk == 3 ? 9 : 5;
+        p.ngroups = d->ntaps / p.NT;
+    }
     const long long tiles = (long long)p.mtiles * p.ntiles * p.ngroups;
     // ~2048 blocks (swept on MI355X: 1024 -> 2048 is -0.6 % step time; fewer splits hurt), >= 8 chunks
     // (256 pixels; f16: 4 chunks of 64) per split, <= 512 splits (tunable: HYRES_WGRAD_BLOCKS,
@@ -2288,6 +2443,7 @@ int hyres_conv_wgrad(const hyres_wgrad_desc* d0, const float* pp, const float* q
     HY_REQUIRE(!d->square_q || (vp && vq), HYRES_E_SHAPE, "wgrad: square_q needs the vector path");
     // the plan (chunk size, split count, workspace) assumed the f16 kernel: its operands must be aligned
     HY_REQUIRE(!wgrad_f16_ok(d) || (vp && vq), HYRES_E_ALIGN, "wgrad(f16): P/Q must be 16-byte aligned");
+    HY_REQUIRE(!p.halo || (vp && vq), HYRES_E_ALIGN, "wgrad(halo): P/Q must be 16-byte aligned");
     WgradArgs a;
     a.d = *d; a.p = pp; a.q = qq; a.slab = (float*)ws; a.chunks_per_split = p.cps; a.nchunks = p.nchunks;
     a.mtiles = p.mtiles; a.ntiles = p.ntiles; a.ngroups = p.ngroups; a.nblocks = p.nblocks; a.tapn = p.tapn;
@@ -2297,6 +2453,9 @@ int hyres_conv_wgrad(const hyres_wgrad_desc* d0, const float* pp, const float* q
     const bool sqr = d->square_q != 0;
     if (thin) {
         launch_thin(a, tp, st);
+    } else if (p.halo) {
+        if (p.hk == 3) hipLaunchKernelGGL((wgrad_halo_kernel<3, 3>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
+        else hipLaunchKernelGGL((wgrad_halo_kernel<1, 5>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
     } else if (wgrad_f16_ok(d)) {
         auto f16 = [&](auto tm, auto tn, auto wm_, auto wn_, auto ntc) {
             constexpr int TM_ = decltype(tm)::value, TN_ = decltype(tn)::value;

@@ -37,7 +37,7 @@ GEOMS = [
 # weight gradients (H, Ci, Co, K[, stride]): P = dY [.., Co], Q = X [.., Ci]
 WGEOMS = [
     (32, 96, 96, 3), (32, 96, 192, 1), (32, 192, 96, 1), (32, 192, 384, 5), (32, 192, 384, 3),
-    (32, 768, 640, 1), (32, 512, 384, 1), (64, 64, 64, 3), (64, 128, 64, 1), (128, 64, 64, 3),
+    (32, 768, 640, 1), (32, 512, 384, 1), (64, 64, 64, 3), (64, 128, 64, 1), (128, 64, 64, 3), (256, 64, 64, 3),
 ]
 # the image-side 3-channel layers (refine conv 3->64 / 64->3 at 256^2, g_a's 5x5 s2 3->128)
 WGEOMS3 = [(256, 3, 64, 3, 1), (256, 64, 3, 3, 1), (256, 3, 128, 5, 2)]
