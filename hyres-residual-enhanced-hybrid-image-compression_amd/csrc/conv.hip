@@ -1019,17 +1019,17 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgradArgs a) {
 
 
 // ------------------------------------------------------------------------------------------------
-// Halo-staged weight gradient for stride-1 KxK convolutions (K = 3: one block does all 9 taps; K = 5: one
-// kernel row of 5 taps per block) whose rows are a multiple of 32 pixels, so a 32-pixel K chunk is one row
-// segment (b, i, j0..j0+31). Per chunk the block stages P (32 px x 64 m) and ONE Q halo tile (KR rows x
-// (32 + K - 1) px x 64 n) in LDS, double-buffered, and every tap reads its B operand from the halo at
-// its (dh, dw) shift. The generic kernel instead gathers a shifted 32-px Q chunk per tap (9 global loads
+// Halo-staged weight gradient for KxK convolutions / transposed convolutions at Q stride SQ = 1 or 2 (K = 3:
+// one block does all 9 taps; K = 5: one kernel row of 5 taps per block) whose base rows are a multiple of
+// 32 pixels, so a 32-pixel K chunk is one row segment (b, i, j0..j0+31). Per chunk the block stages P
+// (32 px x 64 m) and ONE Q halo tile (KR rows x (31*SQ + K) px x 64 n) in LDS, double-buffered, and every
+// tap reads its B operand from the halo at its (dh, dw) shift (pixel k at column k*SQ + dw). The generic kernel instead gathers a shifted 32-px Q chunk per tap (9 global loads
 // and 9 barriers per chunk, the latency of each exposed at 2 blocks per CU); here it is one load of
 // 3 x 34 px per chunk and one barrier per 9 x 16 MFMAs. 64 x 64 tiles, 4 waves of 32 x 32.
 // ------------------------------------------------------------------------------------------------
-template <int KR, int KW>
+template <int KR, int KW, int SQ>
 __global__ __launch_bounds__(256, 2) void wgrad_halo_kernel(const WgradArgs a, int dhg, int dwg) {
-    constexpr int BM = 64, BN = 64, NT = KR * KW, HC = 32 + KW - 1;
+    constexpr int BM = 64, BN = 64, NT = KR * KW, HC = 31 * SQ + KW;  // halo columns of a 32-px chunk
     constexpr int PP = BM + 4, PQ = BN + 4;
     constexpr int PSZ = KT * PP, HSZ = KR * HC * PQ;
     constexpr int P_V = KT * BM / 4 / 256;
@@ -1068,7 +1068,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo_kernel(const WgradArgs a, i
             const int e = tid + 256 * q;
             const int pix = e / (BN / 4), c = (e % (BN / 4)) * 4;
             const int hr = pix / HC, hc = pix - (pix / HC) * HC;
-            const int ih = i + dh0 + hr, iw = j0 + dwg + hc;
+            const int ih = i * SQ + dh0 + hr, iw = j0 * SQ + dwg + hc;
             const bool ok = e < H_E && (unsigned)ih < (unsigned)d.Hqq && (unsigned)iw < (unsigned)d.Wqq && n0 + c < d.N;
             rh[q] = ok ? ld4(a.q + ((long long)(b * d.Hqq + ih) * d.Wqq + iw) * d.ldq + n0 + c)
                        : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1122,7 +1122,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo_kernel(const WgradArgs a, i
             for (int s2 = 0; s2 < KT / 2; ++s2) {
                 const int k = lh * (KT / 2) + s2;
                 const float af = Ps[k * PP + wm * 32 + lr];
-                const float bf = Hs[(hr * HC + k + hc) * PQ + wn * 32 + lr];
+                const float bf = Hs[(hr * HC + k * SQ + hc) * PQ + wn * 32 + lr];
                 acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(af, bf, acc[t], 0, 0, 0);
             }
         });
@@ -2227,14 +2227,14 @@ struct WgradPlan {
     int halo, hk, hdh, hdw;  // wgrad_halo_kernel: K, first tap's (dh, dw)
 };
 
-// wgrad_halo_kernel applies: fp32, stride-1 dense KxK taps (K = 3 or 5, dilation 1) on rows of a multiple of
-// 32 pixels, both operands >= 32 channels on the float4 path
+// wgrad_halo_kernel applies: fp32, dense KxK taps (K = 3 or 5, dilation 1), Q stride 1 or 2, base rows of a
+// multiple of 32 pixels, both operands >= 32 channels on the float4 path
 static bool halo_ok(const hyres_wgrad_desc* d, int* K) {
     static const int on = env_int("HYRES_WGRAD_HALO", 1);
-    if (!on || d->f16_operands || d->square_q || d->sq != 1 || d->Hqq != d->Hq || d->Wqq != d->Wq) return false;
+    if (!on || d->f16_operands || d->square_q || (d->sq != 1 && d->sq != 2)) return false;
     if (d->Wq % 32 != 0 || d->M < 32 || d->N < 32 || d->M % 4 || d->N % 4 || d->ldp % 4 || d->ldq % 4) return false;
     const int k = d->ntaps == 9 ? 3 : d->ntaps == 25 ? 5 : 0;
-    if (!k) return false;
+    if (!k || (d->sq == 2 && k != 5)) return false;  // stride 2 only for the 5x5 (de)convs (3x3 s2: 123 KB LDS)
     for (int t = 0; t < d->ntaps; ++t)
         if (d->dh[t] != d->dh[0] + t / k || d->dw[t] != d->dw[0] + t % k) return false;
     *K = k;
@@ -2298,6 +2298,14 @@ static WgradPlan wgrad_plan(const hyres_wgrad_desc* d) {
     const long long want = std::min<long long>(std::max<long long>(1, (tb + tiles - 1) / tiles), slab_cap);
     const long long maxsplit = std::max<long long>(1, p.nchunks / mc);
     p.nsplit = (int)std::min<long long>(std::min<long long>(want, maxsplit), ms);
+    if (p.halo) {
+        // whole rounds only: the halo kernel runs 2 blocks per CU (3 for 5x5 stride 1); a partial last round
+        // of long split-K blocks costs as much as a full one, so drop it (e.g. 800 -> 500 blocks)
+        const long long cap = 256LL * ((p.hk == 5 && d->sq == 1) ? 3 : 2);
+        if (tiles * p.nsplit > cap) p.nsplit = (int)std::max<long long>(1, (tiles * p.nsplit / cap) * cap / tiles);
+        // and fill a partial single round when that grows the slab by <= 25 % (128^2 3x3: 455 -> 512)
+        else if (cap / tiles <= maxsplit && 4 * (cap / tiles) <= 5LL * p.nsplit) p.nsplit = (int)(cap / tiles);
+    }
     p.cps = ceil_div(p.nchunks, p.nsplit);
     p.nsplit = ceil_div(p.nchunks, p.cps);
     p.nblocks = (int)(tiles * p.nsplit);
@@ -2454,8 +2462,9 @@ int hyres_conv_wgrad(const hyres_wgrad_desc* d0, const float* pp, const float* q
     if (thin) {
         launch_thin(a, tp, st);
     } else if (p.halo) {
-        if (p.hk == 3) hipLaunchKernelGGL((wgrad_halo_kernel<3, 3>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
-        else hipLaunchKernelGGL((wgrad_halo_kernel<1, 5>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
+        if (p.hk == 3) hipLaunchKernelGGL((wgrad_halo_kernel<3, 3, 1>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
+        else if (d->sq == 1) hipLaunchKernelGGL((wgrad_halo_kernel<1, 5, 1>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
+        else hipLaunchKernelGGL((wgrad_halo_kernel<1, 5, 2>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
     } else if (wgrad_f16_ok(d)) {
         auto f16 = [&](auto tm, auto tn, auto wm_, auto wn_, auto ntc) {
             constexpr int TM_ = decltype(tm)::value, TN_ = decltype(tn)::value;

@@ -54,6 +54,11 @@ CONV_CASES = [
     (1, 3, 64, 6, 256, 3, 1, 2, 2),    # 256-wide row window, dilation 2
     (1, 3, 64, 4, 300, 3, 1, 1, 1),    # window wider than the LDS stage: generic tap-folded path
     (2, 3, 128, 16, 40, 5, 2, 2, 1),   # two tap groups, stride 2
+    # halo-staged weight gradient (wgrad_halo_kernel): base rows a multiple of 32 pixels
+    (2, 64, 64, 32, 32, 3, 1, 1, 1),   # 3x3, all 9 taps per block
+    (1, 96, 64, 8, 64, 3, 1, 1, 1),    # partial N tile (Ci = 96), two 32-px chunks per row
+    (2, 64, 64, 64, 64, 5, 2, 2, 1),   # 5x5 stride 2 (Q stride 2), one kernel row per block
+    (2, 64, 128, 32, 64, 5, 1, 2, 1),  # 5x5 stride 1, two M tiles
 ]
 
 
@@ -86,7 +91,7 @@ def test_conv2d_fwd_bwd(case):
 
 
 @pytest.mark.parametrize("case", [(2, 192, 128, 4, 4), (2, 128, 128, 8, 8), (2, 128, 3, 16, 16),
-                                  (2, 128, 192, 4, 4)])
+                                  (2, 128, 192, 4, 4), (2, 64, 64, 32, 32)])  # last: halo wgrad, Q stride 2
 def test_deconv2d_fwd_bwd(case):
     from hyres_hip import ops as O
     B, Ci, Co, H, W = case
