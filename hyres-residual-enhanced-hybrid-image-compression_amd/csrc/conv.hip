@@ -39,6 +39,7 @@ struct ConvArgs {
     int w_bytes; // bytes of W2 (buffer-resource range)
     int xcd;     // 1: grid.x = M tiles x N tiles in XCD-aware order (grid.y = 1)
     int prio;    // 1: raise the wave priority while it issues its MFMA cluster (s_setprio)
+    int x_bytes; // conv1x1_stream_kernel: bytes of X (buffer-resource range)
 };
 
 
@@ -516,6 +517,98 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const ConvArgs a) {
                     if (n + c < g.Co) epi_store(a.e, a.y, g.ldy, pix, n + c, vv[c], epi_channel(a.e, n + c));
             }
         }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Streaming 1x1 conv (K = Ci <= 128, Co = 32*NT): the K-short pointwise layers of the ResidualUnits /
+// RBBs at 64^2..256^2 sit at the fp32 ridge (64-128 FLOP per output element against 8-12 bytes), and the
+// tiled kernel above runs them as lock-stepped blocks (load, then MFMA, then epilogue), so their MFMA and
+// HBM phases add instead of overlapping. Here each WAVE streams its own 32-pixel tiles with no block
+// barrier after the one-time weight staging:
+//   * W [Co][K] sits in LDS for the whole (persistent) block, pitch K+4 (conflict-free ds_read_b128);
+//   * the wave's A operand goes HBM -> registers directly in the MFMA layout: lane (r, h) holds pixel
+//     p0+r, channels 8j+4h..8j+4h+3 (j < K/8), so a float4 feeds 4 MFMA k-steps; each float4 is reloaded
+//     for the wave's next tile right after its last MFMA (rolling prefetch);
+//   * the product is formed transposed (C^T = W X^T), so each lane's accumulator holds 4 consecutive
+//     channels of one pixel per register quad: the results are stored as float4 straight from the
+//     accumulator layout — no LDS round trip.
+// Exact fp32 (v_mfma_f32_32x32x2f32), epilogue bias + ReLU / PReLU (+ pre-activation copy). Layers whose
+// epilogue streams a second operand (residual, ReLU mask, old y) stay on the tiled kernel: prefetching
+// that operand per wave tile doubles the registers (2 waves/SIMD) and measured slower than the tiles
+// (128^2 64->128 +res 95 vs 92 us, 64^2 27 vs 24 us; profiles/r2_micro_1x1_stream.txt).
+template <int NT, int KC>
+__global__ __launch_bounds__(256, 2) void conv1x1_stream_kernel(const ConvArgs a) {
+    constexpr int K = 8 * KC, KP = K + 4, CO = 32 * NT;
+    __shared__ __attribute__((aligned(16))) float Ws[CO * KP];
+    const hyres_conv_geom& g = a.g;
+    const hyres_epilogue& e = a.e;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int lr = lane & 31, lh = lane >> 5;
+    for (int i = tid; i < CO * (K / 4); i += 256) {
+        const int co = i / (K / 4), k4 = i - co * (K / 4);
+        *reinterpret_cast<float4*>(&Ws[co * KP + 4 * k4]) = ld4(a.w2 + (long long)co * a.ldw + 4 * k4);
+    }
+    __shared__ __attribute__((aligned(16))) float bs[CO];
+    for (int i = tid; i < CO; i += 256) bs[i] = e.bias ? e.bias[i] : 0.f;
+    const float slope = (e.act == HYRES_ACT_PRELU) ? e.slope[0] : 0.f;
+    __syncthreads();
+
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, a.x_bytes, 0x00020000);
+    const int ntile = (a.M + 31) / 32;
+    const int gw = blockIdx.x * 4 + wave, nw = gridDim.x * 4;
+    auto load_a = [&](int tile, int j) -> float4 {
+        const int p = tile * 32 + lr;
+        const int off = (tile < ntile && p < a.M) ? (p * g.ldx + 8 * j + 4 * lh) * 4 : (int)0x80000000;
+        return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
+    };
+    float4 av[KC];
+#pragma unroll
+    for (int j = 0; j < KC; ++j) av[j] = load_a(gw, j);
+    // GEMM as C^T = W X^T (MFMA A operand = weights, B operand = pixels): lane (r, h) ends up holding
+    // pixel p0+r, channels 32t + 8q + 4h .. +3 in acc[t][4q .. 4q+3] -> one float4 per (t, q)
+    for (int tile = gw; tile < ntile; tile += nw) {
+        const int p = tile * 32 + lr;
+        const bool pok = p < a.M;
+        floatx16 acc[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+        if (a.prio) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int j = 0; j < KC; ++j) {
+            float4 bv[NT];
+#pragma unroll
+            for (int t = 0; t < NT; ++t) bv[t] = *reinterpret_cast<const float4*>(&Ws[(32 * t + lr) * KP + 8 * j + 4 * lh]);
+            const float4 x = av[j];
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(bv[t].x, x.x, acc[t], 0, 0, 0);
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(bv[t].y, x.y, acc[t], 0, 0, 0);
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(bv[t].z, x.z, acc[t], 0, 0, 0);
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(bv[t].w, x.w, acc[t], 0, 0, 0);
+            }
+            av[j] = load_a(tile + nw, j);  // rolling prefetch of the wave's next tile
+        }
+        if (a.prio) __builtin_amdgcn_s_setprio(0);
+        if (!pok) continue;
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int n = 32 * t + 8 * q + 4 * lh;
+                const float4 b4 = *reinterpret_cast<const float4*>(&bs[n]);
+                float o[4] = {acc[t][4 * q] + b4.x, acc[t][4 * q + 1] + b4.y, acc[t][4 * q + 2] + b4.z,
+                              acc[t][4 * q + 3] + b4.w};
+                if (e.out2) st4(e.out2 + (long long)p * e.ldo2 + n, make_float4(o[0], o[1], o[2], o[3]));
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    if (e.act == HYRES_ACT_RELU) o[c] = fmaxf(o[c], 0.f);
+                    else if (e.act == HYRES_ACT_PRELU) o[c] = o[c] >= 0.f ? o[c] : slope * o[c];
+                }
+                st4(a.y + (long long)p * g.ldy + n, make_float4(o[0], o[1], o[2], o[3]));
+            }
     }
 }
 
@@ -1786,6 +1879,34 @@ static int launch_fwd(const ConvArgs& a, int mode, hipStream_t st) {
     return HY_LAUNCH_CHECK("conv_fwd_kernel");
 }
 
+// persistent grid: as many blocks as fit on the chip at once (occupancy query, cached per instantiation),
+// capped by blocks_per_cu (<= 0: no cap) and by the 32-pixel tiles available (4 per block)
+template <int NT, int KC>
+static int launch_stream_one(const ConvArgs& a, int blocks_per_cu, hipStream_t st) {
+    static int occ = -1;
+    if (occ < 0) {
+        int n = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, conv1x1_stream_kernel<NT, KC>, 256, 0) != hipSuccess || n < 1)
+            n = 1;
+        occ = n;
+    }
+    const int per_cu = blocks_per_cu > 0 ? std::min(occ, blocks_per_cu) : occ;
+    const int blocks = std::max(1, std::min(ceil_div(ceil_div(a.M, 32), 4), 256 * per_cu));
+    hipLaunchKernelGGL((conv1x1_stream_kernel<NT, KC>), dim3(blocks), dim3(256), 0, st, a);
+    return HY_LAUNCH_CHECK("conv1x1_stream_kernel");
+}
+
+static int launch_stream(const ConvArgs& a, int nt, int kc, int blocks_per_cu, hipStream_t st) {
+#define HY_STREAM(NT, KC) \
+    if (nt == NT && kc == KC) return launch_stream_one<NT, KC>(a, blocks_per_cu, st);
+    HY_STREAM(2, 8) HY_STREAM(2, 12) HY_STREAM(2, 16)
+    HY_STREAM(3, 8) HY_STREAM(3, 12) HY_STREAM(3, 16)
+    HY_STREAM(4, 8) HY_STREAM(4, 12) HY_STREAM(4, 16)
+    HY_STREAM(6, 8)
+#undef HY_STREAM
+    return set_error(HYRES_E_ARG, "conv1x1_stream: no instantiation for NT=%d KC=%d", nt, kc);
+}
+
 static void fill_taps(hyres_conv_geom* g, int p, int* tapcount, int K, int pad, int ph, int pw) {
     // sub-pixel phase (ph, pw) of a stride-2 transposed structure: taps kh with (ph+pad-kh) even
     g->tap0[p] = *tapcount;
@@ -1991,6 +2112,23 @@ struct ConvChoice {
     bool narrow;
     int tile, mode;
 };
+// conv1x1_stream_kernel eligibility: single-tap stride-1 fp32 1x1 with K = Ci in {64, 96, 128}, Co in
+// {64, 96, 128} (or 192 with K = 64), BIAS epilogue with no streamed operand (residual / ReLU mask /
+// old y), grids >= HYRES_CONV_STREAM_PIXELS output pixels (default 65536). Returns NT (Co / 32) or 0.
+static int stream_nt(const hyres_conv_geom* g, const hyres_epilogue* e) {
+    static const int on = env_int("HYRES_CONV_STREAM1X1", 1);
+    static const long long min_px = env_int("HYRES_CONV_STREAM_PIXELS", 65536);
+    if (!on || e->f16_operands || e->square_input || e->kind != HYRES_EPI_BIAS) return 0;
+    if (g->nphase != 1 || g->ntaps != 1 || g->ish != 1 || g->isw != 1 || g->dh[0] != 0 || g->dw[0] != 0) return 0;
+    if (g->Hi != g->Hq || g->Wi != g->Wq || g->Ho != g->Hq || g->Wo != g->Wq) return 0;
+    if ((long long)g->B * g->Hq * g->Wq < min_px) return 0;
+    if (g->Ci != 64 && g->Ci != 96 && g->Ci != 128) return 0;
+    if (e->res || e->act == HYRES_ACT_RELU_MASK || e->accumulate) return 0;
+    if (g->Co == 64 || g->Co == 96 || g->Co == 128) return g->Co / 32;
+    if (g->Co == 192 && g->Ci == 64) return 6;
+    return 0;
+}
+
 static const int TILE_BM[5] = {128, 128, 128, 64, 64};
 static const int TILE_BN[5] = {128, 64, 32, 128, 64};
 
@@ -2147,6 +2285,16 @@ int hyres_conv_forward(const hyres_conv_geom* g, const float* x, const float* w2
         }
         return HY_LAUNCH_CHECK("conv_narrow_kernel");
     }
+    {
+        const int nt = stream_nt(g, e);
+        const long long xb = (long long)a.M * g->ldx * 4;
+        if (nt && mode == 0 && a.vec4 && xb < 0x7FFFFFF0LL && aligned16(x) && aligned16(w2) && ldw % 4 == 0) {
+            a.x_bytes = (int)xb;
+            a.nsplit = 1;
+            static const int per_cu = env_int("HYRES_CONV_STREAM_BLOCKS_PER_CU", 0);
+            return launch_stream(a, nt, g->Ci / 8, per_cu, st);
+        }
+    }
     int rc;
     switch (ch.tile) {
         case 0: rc = launch_fwd<2, 2, 2, 2>(a, mode, st); break;
@@ -2173,6 +2321,13 @@ int hyres_conv_kernel_name(const hyres_conv_geom* g, const hyres_epilogue* e, in
     if (ch.narrow) {
         snprintf(buf, n, "conv_narrow_kernel<%d, %d>", std::min(g->Co, 4), g->Ci == 64 ? 1 : 2);
         return 0;
+    }
+    {
+        const int nt = stream_nt(g, e);
+        if (nt && ch.mode == 0) {
+            snprintf(buf, n, "conv1x1_stream_kernel<%d, %d>", nt, g->Ci / 8);
+            return 0;
+        }
     }
     static const char* tiles[5] = {"2, 2, 2, 2", "2, 1, 2, 2", "1, 1, 4, 1", "1, 2, 2, 2", "1, 1, 2, 2"};
     const bool f16 = e->f16_operands && ch.mode != 2;

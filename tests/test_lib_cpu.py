@@ -137,11 +137,11 @@ def test_conv_kernel_name_follows_the_launch_routing():
     assert conv_variant(g3, e, False) == "conv_fwd_kernel<2, 1, 2, 2, 0, false, false>"
     assert conv_variant(g3, e, True) == "conv_fwd_kernel<2, 1, 2, 2, 0, true, false>"
     g1 = _geom("hyres_geom_conv2d", 16, 128, 128, 64, 64, 128, 128, 1, 1, 1, 0, 1)
-    assert conv_variant(g1, e, False) == "conv_fwd_kernel<1, 2, 2, 2, 0, false, false>"
+    assert conv_variant(g1, e, False) == "conv1x1_stream_kernel<4, 8>"  # K <= 128 1x1, >= 64k pixels
     g1b = _geom("hyres_geom_conv2d", 16, 256, 256, 192, 192, 64, 64, 1, 1, 1, 0, 1)  # K = 192: not short
     assert conv_variant(g1b, e, False) == "conv_fwd_kernel<2, 1, 2, 2, 0, false, false>"
     g1c = _geom("hyres_geom_conv2d", 16, 128, 128, 128, 128, 64, 64, 1, 1, 1, 0, 1)
-    assert conv_variant(g1c, e, False) == "conv_fwd_kernel<1, 1, 2, 2, 0, false, false>"
+    assert conv_variant(g1c, e, False) == "conv1x1_stream_kernel<2, 16>"
     gn = _geom("hyres_geom_conv2d", 16, 256, 256, 64, 64, 3, 3, 3, 3, 1, 1, 1)
     assert conv_variant(gn, e, False) == "conv_narrow_kernel<3, 1>"
     gs = _geom("hyres_geom_conv2d", 16, 256, 256, 3, 3, 64, 64, 3, 3, 1, 1, 1)  # Ci = 3: scalar path
