@@ -163,6 +163,9 @@ def eval_legs(net, x, jpeg, jpeg_bpp, args, reps=20):
             del cap
     res["analysis_synthesis_bs%d" % x.shape[0]] = analysis_synthesis(net, x, reps)
     res["kodak_codec"] = codec_leg(net, xk.to(dev), jk.to(dev))
+    # configs[4]: the same codec under autocast (fp16 MFMA operands, fp16 activations above the latent)
+    with torch.autocast("cuda", dtype=torch.float16):
+        res["kodak_codec_autocast_f16"] = codec_leg(net, xk.to(dev), jk.to(dev))
     net.train()
     return res
 

@@ -54,24 +54,26 @@ __device__ __forceinline__ EpiChannel epi_channel(const hyres_epilogue& e, int n
     return c;
 }
 
-// Apply the epilogue to one GEMM result v for output pixel ``pix`` / channel n and store it.
+// Apply the epilogue to one GEMM result v for output pixel ``pix`` / channel n and store it
+// (H: y and the activation operands res / aux0 / out2 are fp16 in HBM).
+template <bool H = false>
 __device__ __forceinline__ void epi_store(const hyres_epilogue& e, float* y, int ldy, long long pix, int n, float v,
                                           const EpiChannel& c) {
     switch (e.kind) {
         case HYRES_EPI_BIAS: {
             v += c.bias;
-            if (e.res) v += e.res[pix * e.ldres + n];
-            if (e.out2) e.out2[pix * e.ldo2 + n] = v;  // pre-activation (PReLU backward)
+            if (e.res) v += ldv<H>(e.res, pix * e.ldres + n);
+            if (e.out2) stv<H>(e.out2, pix * e.ldo2 + n, v);  // pre-activation (PReLU backward)
             if (e.act == HYRES_ACT_RELU) v = fmaxf(v, 0.f);
             else if (e.act == HYRES_ACT_PRELU) v = v >= 0.f ? v : c.slope * v;
-            else if (e.act == HYRES_ACT_RELU_MASK) v = e.aux0[pix * e.ld0 + n] > 0.f ? v : 0.f;
+            else if (e.act == HYRES_ACT_RELU_MASK) v = ldv<H>(e.aux0, pix * e.ld0 + n) > 0.f ? v : 0.f;
             break;
         }
         case HYRES_EPI_GDN:
         case HYRES_EPI_IGDN: {
             const float nv = v + c.bias;
-            const float xv = e.aux0[pix * e.ld0 + n];
-            e.out2[pix * e.ldo2 + n] = nv;
+            const float xv = ldv<H>(e.aux0, pix * e.ld0 + n);
+            stv<H>(e.out2, pix * e.ldo2 + n, nv);
             v = (e.kind == HYRES_EPI_GDN) ? xv * (1.0f / sqrtf(nv)) : xv * sqrtf(nv);
             break;
         }
@@ -86,14 +88,19 @@ __device__ __forceinline__ void epi_store(const hyres_epilogue& e, float* y, int
         }
         default: break;
     }
-    float* yp = y + pix * ldy + n;
-    if (e.accumulate) v += *yp;
-    *yp = v;
+    if constexpr (H) {
+        stv<true>(y, pix * ldy + n, v);  // host: no accumulate with fp16 output
+    } else {
+        float* yp = y + pix * ldy + n;
+        if (e.accumulate) v += *yp;
+        *yp = v;
+    }
 }
 
 __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
 
 // float4 variant of epi_store for channels n..n+3 (all operands 16B aligned).
+template <bool H = false>
 __device__ __forceinline__ void epi_store4(const hyres_epilogue& e, float* y, int ldy, long long pix, int n, float4 v,
                                            float slope) {
     float o[4] = {v.x, v.y, v.z, v.w};
@@ -101,10 +108,10 @@ __device__ __forceinline__ void epi_store4(const hyres_epilogue& e, float* y, in
         case HYRES_EPI_BIAS: {
             if (e.bias) { const float4 b = ld4(e.bias + n); o[0] += b.x; o[1] += b.y; o[2] += b.z; o[3] += b.w; }
             if (e.res) {
-                const float4 r = ld4(e.res + pix * e.ldres + n);
+                const float4 r = ldv4<H>(e.res, pix * e.ldres + n);
                 o[0] += r.x; o[1] += r.y; o[2] += r.z; o[3] += r.w;
             }
-            if (e.out2) st4(e.out2 + pix * e.ldo2 + n, make_float4(o[0], o[1], o[2], o[3]));
+            if (e.out2) stv4<H>(e.out2, pix * e.ldo2 + n, make_float4(o[0], o[1], o[2], o[3]));
             if (e.act == HYRES_ACT_RELU) {
 #pragma unroll
                 for (int c = 0; c < 4; ++c) o[c] = fmaxf(o[c], 0.f);
@@ -112,7 +119,7 @@ __device__ __forceinline__ void epi_store4(const hyres_epilogue& e, float* y, in
 #pragma unroll
                 for (int c = 0; c < 4; ++c) o[c] = o[c] >= 0.f ? o[c] : slope * o[c];
             } else if (e.act == HYRES_ACT_RELU_MASK) {
-                const float4 y = ld4(e.aux0 + pix * e.ld0 + n);
+                const float4 y = ldv4<H>(e.aux0, pix * e.ld0 + n);
                 o[0] = y.x > 0.f ? o[0] : 0.f;
                 o[1] = y.y > 0.f ? o[1] : 0.f;
                 o[2] = y.z > 0.f ? o[2] : 0.f;
@@ -123,10 +130,10 @@ __device__ __forceinline__ void epi_store4(const hyres_epilogue& e, float* y, in
         case HYRES_EPI_GDN:
         case HYRES_EPI_IGDN: {
             const float4 b = e.bias ? ld4(e.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
-            const float4 x = ld4(e.aux0 + pix * e.ld0 + n);
+            const float4 x = ldv4<H>(e.aux0, pix * e.ld0 + n);
             const float nv[4] = {o[0] + b.x, o[1] + b.y, o[2] + b.z, o[3] + b.w};
             const float xv[4] = {x.x, x.y, x.z, x.w};
-            st4(e.out2 + pix * e.ldo2 + n, make_float4(nv[0], nv[1], nv[2], nv[3]));
+            stv4<H>(e.out2, pix * e.ldo2 + n, make_float4(nv[0], nv[1], nv[2], nv[3]));
 #pragma unroll
             for (int c = 0; c < 4; ++c)
                 o[c] = (e.kind == HYRES_EPI_GDN) ? xv[c] * (1.0f / sqrtf(nv[c])) : xv[c] * sqrtf(nv[c]);
@@ -147,20 +154,29 @@ __device__ __forceinline__ void epi_store4(const hyres_epilogue& e, float* y, in
         }
         default: break;
     }
-    float* yp = y + pix * ldy + n;
-    if (e.accumulate) {
-        const float4 p = ld4(yp);
-        o[0] += p.x; o[1] += p.y; o[2] += p.z; o[3] += p.w;
+    if constexpr (H) {
+        stv4<true>(y, pix * ldy + n, make_float4(o[0], o[1], o[2], o[3]));
+    } else {
+        float* yp = y + pix * ldy + n;
+        if (e.accumulate) {
+            const float4 p = ld4(yp);
+            o[0] += p.x; o[1] += p.y; o[2] += p.z; o[3] += p.w;
+        }
+        st4(yp, make_float4(o[0], o[1], o[2], o[3]));
     }
-    st4(yp, make_float4(o[0], o[1], o[2], o[3]));
 }
 
-template <int TM, int TN, int WAVES_M, int WAVES_N, int MODE, bool SPLITK, bool F16 = false>
-__global__ __launch_bounds__(256) void conv_fwd_kernel(const ConvArgs a) {
+template <int TM, int TN, int WAVES_M, int WAVES_N, int MODE, bool SPLITK, bool F16, int IO>
+__device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
     // MODE 0: Ci % 32 == 0 (float4 loads); 1: same + square A (GDN); 2: generic scalar (small Ci).
     // F16: operands rounded to fp16 when staged into LDS ([row][32 halves], pitch PADH halves) and
     // consumed by v_mfma_f32_32x32x16_f16 (lane r,h holds row r, k = 8h..8h+7), fp32 accumulation.
+    // IO (fp16 activations in HBM, autocast inference): bit 0 X is fp16 (8-byte loads of 4 channels),
+    // bit 1 Y / res / aux0 / out2 are fp16; arithmetic stays fp32 (F16: fp16 MFMA operands as before).
     static_assert(!F16 || MODE != 2, "fp16 operands on the Ci % 32 == 0 paths only");
+    static_assert(!(IO & 1) || MODE != 2, "fp16 X on the Ci % 32 == 0 paths only");
+    constexpr bool XH = (IO & 1) != 0, YH = (IO & 2) != 0;
+    constexpr int XES = XH ? 2 : 4;  // X element bytes
     constexpr int PADH = 40;
     constexpr int BM = 32 * TM * WAVES_M;
     constexpr int BN = 32 * TN * WAVES_N;
@@ -227,9 +243,10 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const ConvArgs a) {
     // the block's first image so 32-bit byte offsets suffice (host checks 3 images < 2 GB).
     const int b0 = m0 / HqWq;
     const long long img = (long long)g.Hi * g.Wi * g.ldx;
-    const long long xrem = ((long long)g.B - b0) * img * 4;
+    const long long xrem = ((long long)g.B - b0) * img * XES;
     const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(a.x + (long long)b0 * img), (short)0, (int)(xrem < 0x7FFFFFF0LL ? xrem : 0x7FFFFFF0LL), 0x00020000);
+        (void*)(reinterpret_cast<const char*>(a.x) + (long long)b0 * img * XES), (short)0,
+        (int)(xrem < 0x7FFFFFF0LL ? xrem : 0x7FFFFFF0LL), 0x00020000);
     const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)a.w2, (short)0, a.w_bytes, 0x00020000);
     int a_base[A_V];  // element offset of image row 0 of this row's image, rel. to b0
 #pragma unroll
@@ -254,8 +271,14 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const ConvArgs a) {
             for (int q = 0; q < A_V; ++q) {
                 const int ih = a_i[q] + o.x, iw = a_j[q] + o.y;
                 const bool ok = a_ok[q] && (unsigned)ih < (unsigned)g.Hi && (unsigned)iw < (unsigned)g.Wi;
-                const int off = ok ? (a_base[q] + (ih * g.Wi + iw) * g.ldx + c0) * 4 : (int)0x80000000;
-                float4 v = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
+                const int off = ok ? (a_base[q] + (ih * g.Wi + iw) * g.ldx + c0) * XES : (int)0x80000000;
+                float4 v;
+                if constexpr (XH) {
+                    const half4_t h = __builtin_bit_cast(half4_t, __builtin_amdgcn_raw_buffer_load_b64(xr, off, 0, 0));
+                    v = make_float4((float)h.x, (float)h.y, (float)h.z, (float)h.w);
+                } else {
+                    v = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
+                }
                 if constexpr (MODE == 1) { v.x *= v.x; v.y *= v.y; v.z *= v.z; v.w *= v.w; }
                 ra[q] = v;
             }
@@ -452,16 +475,16 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const ConvArgs a) {
                         px[u] = pix;
                         const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
                         bs[u] = (ok[u] && e.bias) ? ld4(e.bias + n) : z4;
-                        rs[u] = (ok[u] && e.res) ? ld4(e.res + pix * e.ldres + n) : z4;
-                        yo[u] = (ok[u] && e.accumulate) ? ld4(a.y + pix * g.ldy + n) : z4;
-                        mk[u] = (ok[u] && e.act == HYRES_ACT_RELU_MASK) ? ld4(e.aux0 + pix * e.ld0 + n) : z4;
+                        rs[u] = (ok[u] && e.res) ? ldv4<YH>(e.res, pix * e.ldres + n) : z4;
+                        yo[u] = (!YH && ok[u] && e.accumulate) ? ld4(a.y + pix * g.ldy + n) : z4;
+                        mk[u] = (ok[u] && e.act == HYRES_ACT_RELU_MASK) ? ldv4<YH>(e.aux0, pix * e.ld0 + n) : z4;
                     }
 #pragma unroll
                     for (int u = 0; u < U; ++u) {
                         if (!ok[u]) continue;
                         float o[4] = {v[u].x + bs[u].x + rs[u].x, v[u].y + bs[u].y + rs[u].y,
                                       v[u].z + bs[u].z + rs[u].z, v[u].w + bs[u].w + rs[u].w};
-                        if (e.out2) st4(e.out2 + px[u] * e.ldo2 + nn[u], make_float4(o[0], o[1], o[2], o[3]));
+                        if (e.out2) stv4<YH>(e.out2, px[u] * e.ldo2 + nn[u], make_float4(o[0], o[1], o[2], o[3]));
                         if (e.act == HYRES_ACT_RELU) {
 #pragma unroll
                             for (int c = 0; c < 4; ++c) o[c] = fmaxf(o[c], 0.f);
@@ -474,8 +497,8 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const ConvArgs a) {
                             o[2] = mk[u].z > 0.f ? o[2] : 0.f;
                             o[3] = mk[u].w > 0.f ? o[3] : 0.f;
                         }
-                        st4(a.y + px[u] * g.ldy + nn[u],
-                            make_float4(o[0] + yo[u].x, o[1] + yo[u].y, o[2] + yo[u].z, o[3] + yo[u].w));
+                        stv4<YH>(a.y, px[u] * g.ldy + nn[u],
+                                 make_float4(o[0] + yo[u].x, o[1] + yo[u].y, o[2] + yo[u].z, o[3] + yo[u].w));
                     }
                 }
                 continue;
@@ -509,15 +532,27 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const ConvArgs a) {
                 pix = (long long)(b * g.Ho + i * g.osh + oph) * g.Wo + j * g.osw + opw;
             }
             if (a.vec4) {
-                epi_store4(a.e, a.y, g.ldy, pix, n, v, slope);
+                epi_store4<YH>(a.e, a.y, g.ldy, pix, n, v, slope);
             } else {
                 const float vv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
                 for (int c = 0; c < 4; ++c)
-                    if (n + c < g.Co) epi_store(a.e, a.y, g.ldy, pix, n + c, vv[c], epi_channel(a.e, n + c));
+                    if (n + c < g.Co) epi_store<YH>(a.e, a.y, g.ldy, pix, n + c, vv[c], epi_channel(a.e, n + c));
             }
         }
     }
+}
+
+template <int TM, int TN, int WAVES_M, int WAVES_N, int MODE, bool SPLITK, bool F16 = false>
+__global__ __launch_bounds__(256) void conv_fwd_kernel(const ConvArgs a) {
+    conv_fwd_body<TM, TN, WAVES_M, WAVES_N, MODE, SPLITK, F16, 0>(a);
+}
+
+// fp16 activations in HBM (IO = 1: X fp16, 2: Y fp16, 3: both); fp16 MFMA operands except on the
+// small-Ci scalar path (MODE 2: the fp32 image in, fp16 features out)
+template <int TM, int TN, int WAVES_M, int WAVES_N, int MODE, bool SPLITK, int IO>
+__global__ __launch_bounds__(256) void conv_fwd_h_kernel(const ConvArgs a) {
+    conv_fwd_body<TM, TN, WAVES_M, WAVES_N, MODE, SPLITK, MODE != 2, IO>(a);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -613,6 +648,7 @@ __global__ __launch_bounds__(256, 2) void conv1x1_stream_kernel(const ConvArgs a
 }
 
 // split-K reduction + epilogue: one thread per (phase, m, n)
+template <bool H>
 __global__ void conv_splitk_reduce_kernel(const ConvArgs a) {
     const hyres_conv_geom& g = a.g;
     const long long per_phase = (long long)a.M * g.Co;
@@ -630,11 +666,12 @@ __global__ void conv_splitk_reduce_kernel(const ConvArgs a) {
         const int rr = m - b * HqWq;
         const int i = rr / g.Wq, j = rr - (rr / g.Wq) * g.Wq;
         const long long pix = (long long)(b * g.Ho + i * g.osh + g.oph[phase]) * g.Wo + j * g.osw + g.opw[phase];
-        epi_store(a.e, a.y, g.ldy, pix, n, v, epi_channel(a.e, n));
+        epi_store<H>(a.e, a.y, g.ldy, pix, n, v, epi_channel(a.e, n));
     }
 }
 
 // float4 variant (vec4 launches): 4 channels per thread, split loads unrolled, float4 epilogue
+template <bool H>
 __global__ __launch_bounds__(256) void conv_splitk_reduce4_kernel(const ConvArgs a) {
     const hyres_conv_geom& g = a.g;
     const int C4 = g.Co >> 2;
@@ -660,7 +697,7 @@ __global__ __launch_bounds__(256) void conv_splitk_reduce4_kernel(const ConvArgs
         const int rr = m - b * HqWq;
         const int i = rr / g.Wq, j = rr - (rr / g.Wq) * g.Wq;
         const long long pix = (long long)(b * g.Ho + i * g.osh + g.oph[phase]) * g.Wo + j * g.osw + g.opw[phase];
-        epi_store4(a.e, a.y, g.ldy, pix, n, v, slope);
+        epi_store4<H>(a.e, a.y, g.ldy, pix, n, v, slope);
     }
 }
 
@@ -676,7 +713,7 @@ __global__ __launch_bounds__(256) void conv_splitk_reduce4_kernel(const ConvArgs
 constexpr int NARROW_PIX = 256;      // output pixels per block
 constexpr int NARROW_WLDS = 8192;    // floats of staged weights (ntap * CO * Ci)
 
-template <int CO, int S>
+template <int CO, int S, bool XH = false>
 __global__ __launch_bounds__(256) void conv_narrow_kernel(const ConvArgs a) {
     __shared__ __attribute__((aligned(16))) float Ws[NARROW_WLDS];
     __shared__ int2 tapoff[HYRES_MAX_TAPS];
@@ -703,10 +740,12 @@ __global__ __launch_bounds__(256) void conv_narrow_kernel(const ConvArgs a) {
         bx = x * q + min(x, r) + (bx >> 3);
     }
     const int b0 = (bx * NARROW_PIX) / HqWq;
+    constexpr int XES = XH ? 2 : 4;  // X element bytes (XH: fp16 activations, autocast inference)
     const long long img = (long long)g.Hi * g.Wi * g.ldx;
-    const long long xrem = ((long long)g.B - b0) * img * 4;
+    const long long xrem = ((long long)g.B - b0) * img * XES;
     const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(a.x + (long long)b0 * img), (short)0, (int)(xrem < 0x7FFFFFF0LL ? xrem : 0x7FFFFFF0LL), 0x00020000);
+        (void*)(reinterpret_cast<const char*>(a.x) + (long long)b0 * img * XES), (short)0,
+        (int)(xrem < 0x7FFFFFF0LL ? xrem : 0x7FFFFFF0LL), 0x00020000);
     const int l16 = tid & 15, slot = tid >> 4;  // 16 pixel slots per block pass
     for (int it = 0; it < NARROW_PIX / 16; ++it) {
         const int m = bx * NARROW_PIX + it * 16 + slot;
@@ -730,11 +769,18 @@ __global__ __launch_bounds__(256) void conv_narrow_kernel(const ConvArgs a) {
                 const int2 o = tapoff[t < ntap ? t : 0];
                 const int ih = i * g.ish + o.x, iw = j * g.isw + o.y;
                 const bool in = ok && t < ntap && (unsigned)ih < (unsigned)g.Hi && (unsigned)iw < (unsigned)g.Wi;
-                const int off = in ? (base + (ih * g.Wi + iw) * g.ldx + 4 * l16) * 4 : (int)0x80000000;
+                const int off = in ? (base + (ih * g.Wi + iw) * g.ldx + 4 * l16) * XES : (int)0x80000000;
 #pragma unroll
-                for (int s2 = 0; s2 < S; ++s2)
-                    xv[u][s2] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                              xr, in ? off + 256 * s2 : off, 0, 0));
+                for (int s2 = 0; s2 < S; ++s2) {
+                    if constexpr (XH) {
+                        const half4_t h = __builtin_bit_cast(
+                            half4_t, __builtin_amdgcn_raw_buffer_load_b64(xr, in ? off + 128 * s2 : off, 0, 0));
+                        xv[u][s2] = make_float4((float)h.x, (float)h.y, (float)h.z, (float)h.w);
+                    } else {
+                        xv[u][s2] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                                  xr, in ? off + 256 * s2 : off, 0, 0));
+                    }
+                }
             }
 #pragma unroll
             for (int u = 0; u < TG; ++u) {
@@ -781,6 +827,11 @@ static bool narrow_ok(const hyres_conv_geom* g) {
 
 template <int CO>
 static void launch_narrow(const ConvArgs& a, dim3 grid, hipStream_t st) {
+    if (a.e.io_f16 & 1) {
+        if (a.g.Ci == 64) hipLaunchKernelGGL((conv_narrow_kernel<CO, 1, true>), grid, dim3(256), 0, st, a);
+        else hipLaunchKernelGGL((conv_narrow_kernel<CO, 2, true>), grid, dim3(256), 0, st, a);
+        return;
+    }
     if (a.g.Ci == 64) hipLaunchKernelGGL((conv_narrow_kernel<CO, 1>), grid, dim3(256), 0, st, a);
     else hipLaunchKernelGGL((conv_narrow_kernel<CO, 2>), grid, dim3(256), 0, st, a);
 }
@@ -1856,6 +1907,25 @@ static int launch_fwd(const ConvArgs& a, int mode, hipStream_t st) {
     constexpr int BM = 32 * TM * WM_, BN = 32 * TN * WN_;
     dim3 grid(ceil_div(a.M, BM), ceil_div(a.g.Co, BN), a.g.nphase * a.nsplit);
     if (a.xcd) grid = dim3(grid.x * grid.y, 1, grid.z);
+    if (a.e.io_f16) {
+        const int io = a.e.io_f16;
+#define HY_H(MODE_, SPLIT_)                                                                                       \
+    {                                                                                                            \
+        if (io == 1) hipLaunchKernelGGL((conv_fwd_h_kernel<TM, TN, WM_, WN_, MODE_, SPLIT_, 1>), grid, dim3(256), 0, st, a); \
+        else if (io == 2) hipLaunchKernelGGL((conv_fwd_h_kernel<TM, TN, WM_, WN_, MODE_, SPLIT_, 2>), grid, dim3(256), 0, st, a); \
+        else hipLaunchKernelGGL((conv_fwd_h_kernel<TM, TN, WM_, WN_, MODE_, SPLIT_, 3>), grid, dim3(256), 0, st, a); \
+    }
+        if (mode == 2) {
+            if (a.nsplit > 1) hipLaunchKernelGGL((conv_fwd_h_kernel<TM, TN, WM_, WN_, 2, true, 2>), grid, dim3(256), 0, st, a);
+            else hipLaunchKernelGGL((conv_fwd_h_kernel<TM, TN, WM_, WN_, 2, false, 2>), grid, dim3(256), 0, st, a);
+        } else if (a.nsplit > 1) {
+            if (mode == 0) HY_H(0, true) else HY_H(1, true)
+        } else {
+            if (mode == 0) HY_H(0, false) else HY_H(1, false)
+        }
+#undef HY_H
+        return HY_LAUNCH_CHECK("conv_fwd_h_kernel");
+    }
     if (a.e.f16_operands && mode != 2) {
         if (a.nsplit > 1) {
             if (mode == 0) hipLaunchKernelGGL((conv_fwd_kernel<TM, TN, WM_, WN_, 0, true, true>), grid, dim3(256), 0, st, a);
@@ -2118,7 +2188,7 @@ struct ConvChoice {
 static int stream_nt(const hyres_conv_geom* g, const hyres_epilogue* e) {
     static const int on = env_int("HYRES_CONV_STREAM1X1", 1);
     static const long long min_px = env_int("HYRES_CONV_STREAM_PIXELS", 65536);
-    if (!on || e->f16_operands || e->square_input || e->kind != HYRES_EPI_BIAS) return 0;
+    if (!on || e->f16_operands || e->io_f16 || e->square_input || e->kind != HYRES_EPI_BIAS) return 0;
     if (g->nphase != 1 || g->ntaps != 1 || g->ish != 1 || g->isw != 1 || g->dh[0] != 0 || g->dw[0] != 0) return 0;
     if (g->Hi != g->Hq || g->Wi != g->Wq || g->Ho != g->Hq || g->Wo != g->Wq) return 0;
     if ((long long)g->B * g->Hq * g->Wq < min_px) return 0;
@@ -2271,6 +2341,13 @@ int hyres_conv_forward(const hyres_conv_geom* g, const float* x, const float* w2
     if (e->kind == HYRES_EPI_GDN_BWD || e->kind == HYRES_EPI_IGDN_BWD)
         HY_REQUIRE(e->aux0 && e->aux1 && e->aux2, HYRES_E_ARG, "conv: GDN bwd epilogue needs aux0..2");
     if (e->act == HYRES_ACT_PRELU) HY_REQUIRE(e->slope, HYRES_E_ARG, "conv: PReLU needs slope");
+    if (e->io_f16) {
+        HY_REQUIRE(e->io_f16 >= 1 && e->io_f16 <= 3 && !e->accumulate &&
+                       (e->kind == HYRES_EPI_BIAS || e->kind == HYRES_EPI_GDN || e->kind == HYRES_EPI_IGDN),
+                   HYRES_E_ARG, "conv: fp16 activations are forward-only (no accumulate / GDN backward)");
+        HY_REQUIRE(!(e->io_f16 & 1) || mode != 2, HYRES_E_ARG, "conv: fp16 X needs Ci %% 32 == 0");
+        HY_REQUIRE(!ch.narrow || !(e->io_f16 & 2), HYRES_E_ARG, "conv: the Co <= 4 kernel writes fp32 only");
+    }
     if (e->act == HYRES_ACT_RELU_MASK)
         HY_REQUIRE(e->aux0 && e->kind == HYRES_EPI_BIAS, HYRES_E_ARG, "conv: ReLU mask needs aux0, BIAS epilogue");
     hipStream_t st = as_stream(s);
@@ -2305,13 +2382,16 @@ int hyres_conv_forward(const hyres_conv_geom* g, const float* x, const float* w2
     }
     if (rc || a.nsplit == 1) return rc;
     long long total = (long long)a.M * g->Co * g->nphase;
+    const bool yh = (e->io_f16 & 2) != 0;
     if (a.vec4) {
         int blocks = (int)std::min<long long>((total / 4 + 255) / 256, 8192);
-        hipLaunchKernelGGL(conv_splitk_reduce4_kernel, dim3(blocks), dim3(256), 0, st, a);
+        if (yh) hipLaunchKernelGGL(conv_splitk_reduce4_kernel<true>, dim3(blocks), dim3(256), 0, st, a);
+        else hipLaunchKernelGGL(conv_splitk_reduce4_kernel<false>, dim3(blocks), dim3(256), 0, st, a);
         return HY_LAUNCH_CHECK("conv_splitk_reduce4_kernel");
     }
     int blocks = (int)std::min<long long>((total + 255) / 256, 8192);
-    hipLaunchKernelGGL(conv_splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, a);
+    if (yh) hipLaunchKernelGGL(conv_splitk_reduce_kernel<true>, dim3(blocks), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(conv_splitk_reduce_kernel<false>, dim3(blocks), dim3(256), 0, st, a);
     return HY_LAUNCH_CHECK("conv_splitk_reduce_kernel");
 }
 
@@ -2331,6 +2411,11 @@ int hyres_conv_kernel_name(const hyres_conv_geom* g, const hyres_epilogue* e, in
     }
     static const char* tiles[5] = {"2, 2, 2, 2", "2, 1, 2, 2", "1, 1, 4, 1", "1, 2, 2, 2", "1, 1, 2, 2"};
     const bool f16 = e->f16_operands && ch.mode != 2;
+    if (e->io_f16) {
+        snprintf(buf, n, "conv_fwd_h_kernel<%s, %d, %s, %d>", tiles[ch.tile], ch.mode, split ? "true" : "false",
+                 e->io_f16);
+        return 0;
+    }
     snprintf(buf, n, "conv_fwd_kernel<%s, %d, %s, %s>", tiles[ch.tile], ch.mode, split ? "true" : "false",
              f16 ? "true" : "false");
     return 0;

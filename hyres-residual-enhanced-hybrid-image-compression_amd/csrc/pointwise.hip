@@ -119,6 +119,15 @@ __global__ void attn_gate_fwd_kernel(const float* a, const float* b, const float
         out[i] = a[i] * s + x[i];
     }
 }
+// fp16 activations (autocast inference): a, b, x, out fp16, 4 elements per thread, fp32 arithmetic
+__global__ void attn_gate_fwd4h_kernel(const float* a, const float* b, const float* x, float* out, long long n4) {
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+        const float4 av = ldv4<true>(a, 4 * i), bv = ldv4<true>(b, 4 * i), xv = ldv4<true>(x, 4 * i);
+        const float4 s = make_float4(1.0f / (1.0f + expf(-bv.x)), 1.0f / (1.0f + expf(-bv.y)),
+                                     1.0f / (1.0f + expf(-bv.z)), 1.0f / (1.0f + expf(-bv.w)));
+        stv4<true>(out, 4 * i, make_float4(av.x * s.x + xv.x, av.y * s.y + xv.y, av.z * s.z + xv.z, av.w * s.w + xv.w));
+    }
+}
 __global__ void attn_gate_bwd_kernel(const float* a, const float* b, const float* g, float* ga, float* gb,
                                      long long n) {
     GRID_STRIDE(i, n) {
@@ -510,6 +519,12 @@ int hyres_attn_gate_fwd(const float* a, const float* b, const float* x, float* o
     HY_REQUIRE(a && b && x && out, HYRES_E_ARG, "attn_gate_fwd: NULL");
     hipLaunchKernelGGL(attn_gate_fwd_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(s), a, b, x, out, n);
     return HY_LAUNCH_CHECK("attn_gate_fwd");
+}
+int hyres_attn_gate_fwd_f16(const void* a, const void* b, const void* x, void* out, long long n, hyres_stream_t s) {
+    HY_REQUIRE(a && b && x && out && n % 4 == 0, HYRES_E_ARG, "attn_gate_fwd_f16: NULL or n %% 4 != 0");
+    hipLaunchKernelGGL(attn_gate_fwd4h_kernel, dim3(grid_for(n / 4)), dim3(256), 0, as_stream(s), (const float*)a,
+                       (const float*)b, (const float*)x, (float*)out, n / 4);
+    return HY_LAUNCH_CHECK("attn_gate_fwd_f16");
 }
 int hyres_attn_gate_bwd(const float* a, const float* b, const float* g, float* ga, float* gb, long long n,
                         hyres_stream_t s) {

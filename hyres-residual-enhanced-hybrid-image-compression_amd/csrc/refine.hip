@@ -27,18 +27,19 @@ __device__ __forceinline__ void src_index(float scale, int o, int in, int& i0, i
 // VEC channels per thread (4: float4 when C, ld % 4 == 0 and 16B-aligned pointers). One block row per
 // output row (blockIdx.y = b*Ho + oh: the vertical stencil is block-uniform), threads over (ow, channel
 // group) with 32-bit index math.
-template <int VEC>
+template <int VEC, bool H = false>
 __global__ __launch_bounds__(256) void bilinear_fwd_kernel(const float* x, int ldx, float* y, int ldy, int B, int Hi,
                                                            int Wi, int Ho, int Wo, int C, float sh, float sw, int acc) {
+    // H: x and y fp16 in HBM (autocast inference), fp32 arithmetic, no accumulate
     const int CG = C / VEC;
     const int row = blockIdx.y;
     const int b = row / Ho, oh = row - b * Ho;
     int h0, h1;
     float lh0, lh1;
     src_index(sh, oh, Hi, h0, h1, lh0, lh1);
-    const float* x0 = x + ((long long)b * Hi + h0) * Wi * ldx;
-    const float* x1 = x + ((long long)b * Hi + h1) * Wi * ldx;
-    float* yr = y + (long long)row * Wo * ldy;
+    const long long x0 = ((long long)b * Hi + h0) * Wi * ldx;  // element offsets of the two source rows
+    const long long x1 = ((long long)b * Hi + h1) * Wi * ldx;
+    const long long yr = (long long)row * Wo * ldy;
     const int n = Wo * CG;
     for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
         const int ow = i / CG;
@@ -46,23 +47,30 @@ __global__ __launch_bounds__(256) void bilinear_fwd_kernel(const float* x, int l
         int w0, w1;
         float lw0, lw1;
         src_index(sw, ow, Wi, w0, w1, lw0, lw1);
-        float* yp = yr + (long long)ow * ldy + c;
+        float* yp = y + yr + (long long)ow * ldy + c;
         if constexpr (VEC == 4) {
-            const float4 a = ld4(x0 + w0 * ldx + c), bq = ld4(x0 + w1 * ldx + c);
-            const float4 cq = ld4(x1 + w0 * ldx + c), d = ld4(x1 + w1 * ldx + c);
+            const float4 a = ldv4<H>(x, x0 + w0 * ldx + c), bq = ldv4<H>(x, x0 + w1 * ldx + c);
+            const float4 cq = ldv4<H>(x, x1 + w0 * ldx + c), d = ldv4<H>(x, x1 + w1 * ldx + c);
             float4 v;
             v.x = lh0 * (lw0 * a.x + lw1 * bq.x) + lh1 * (lw0 * cq.x + lw1 * d.x);
             v.y = lh0 * (lw0 * a.y + lw1 * bq.y) + lh1 * (lw0 * cq.y + lw1 * d.y);
             v.z = lh0 * (lw0 * a.z + lw1 * bq.z) + lh1 * (lw0 * cq.z + lw1 * d.z);
             v.w = lh0 * (lw0 * a.w + lw1 * bq.w) + lh1 * (lw0 * cq.w + lw1 * d.w);
-            if (acc) {
-                const float4 o = ld4(yp);
-                v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+            if constexpr (H) {
+                stv4<true>(y, yr + (long long)ow * ldy + c, v);
+            } else {
+                if (acc) {
+                    const float4 o = ld4(yp);
+                    v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+                }
+                *reinterpret_cast<float4*>(yp) = v;
             }
-            *reinterpret_cast<float4*>(yp) = v;
         } else {
-            const float v = lh0 * (lw0 * x0[w0 * ldx + c] + lw1 * x0[w1 * ldx + c]) +
-                            lh1 * (lw0 * x1[w0 * ldx + c] + lw1 * x1[w1 * ldx + c]);
+            static_assert(!H, "fp16 resampling on the float4 path only");
+            const float* x0p = x + x0;
+            const float* x1p = x + x1;
+            const float v = lh0 * (lw0 * x0p[w0 * ldx + c] + lw1 * x0p[w1 * ldx + c]) +
+                            lh1 * (lw0 * x1p[w0 * ldx + c] + lw1 * x1p[w1 * ldx + c]);
             *yp = acc ? *yp + v : v;
         }
     }
@@ -178,6 +186,18 @@ __global__ void se_fc_kernel(const float* part, int nch, const float* w1, const 
         sgate[b * C + c] = 1.0f / (1.0f + expf(-s));
     }
 }
+// fp16 activations (autocast inference): x, y fp16, 4 channels per thread
+__global__ void se_scale4h_kernel(const float* x, const float* sgate, float* y, int B, int HW, int C) {
+    const int C4 = C >> 2;
+    const long long n = (long long)B * HW * C4;
+    GRID_STRIDE(i, n) {
+        const int c = 4 * (int)(i % C4);
+        const int b = (int)(i / ((long long)HW * C4));
+        const float4 v = ldv4<true>(x, 4 * i);
+        const float4 gt = ld4(sgate + b * C + c);
+        stv4<true>(y, 4 * i, make_float4(v.x * gt.x, v.y * gt.y, v.z * gt.z, v.w * gt.w));
+    }
+}
 __global__ void se_scale_kernel(const float* x, const float* sgate, float* y, int B, int HW, int C) {
     const long long n = (long long)B * HW * C;
     GRID_STRIDE(i, n) {
@@ -188,7 +208,7 @@ __global__ void se_scale_kernel(const float* x, const float* sgate, float* y, in
 }
 // float4 variants (C % 4 == 0, 256 % (C/4) == 0): 256 threads = (C/4 channel groups) x (pixel lanes),
 // every thread busy, deterministic LDS fold over the pixel lanes. SQ: sum of gy*x (backward) instead of x.
-template <bool PROD>
+template <bool PROD, bool H = false>
 __global__ __launch_bounds__(256) void se_pool4_kernel(const float* x, const float* gy, int HW, int C, int per,
                                                        float* part) {
     __shared__ float4 red[256];
@@ -199,7 +219,7 @@ __global__ __launch_bounds__(256) void se_pool4_kernel(const float* x, const flo
     float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int p = p0 + lane; p < p1; p += PL) {
         const long long i = ((long long)b * HW + p) * C + 4 * g;
-        float4 v = *reinterpret_cast<const float4*>(x + i);
+        float4 v = ldv4<H>(x, i);
         if constexpr (PROD) {
             const float4 q = *reinterpret_cast<const float4*>(gy + i);
             v.x *= q.x; v.y *= q.y; v.z *= q.z; v.w *= q.w;
@@ -286,16 +306,17 @@ __global__ void se_bwd_x_kernel(const float* gy, const float* sgate, const float
 // argmax (torch.max(dim=1) on CPU keeps the first maximal index; the backward routes g_max there).
 // channel mean / max (+ first argmax, torch.max semantics) per pixel: 16 lanes per pixel (4 pixels per wave,
 // each lane a float4 stride over the channels), folded with 4 xor-shuffles
+template <bool H = false>
 __global__ __launch_bounds__(256) void sa_pool_kernel(const float* x, float* pooled2, int* amax, long long P, int C) {
     const int l16 = threadIdx.x & 15;
     const long long p = (long long)blockIdx.x * 16 + (threadIdx.x >> 4);
     const bool ok = p < P;
-    const float* xp = x + (ok ? p : 0) * C;
+    const long long xp = (ok ? p : 0) * C;
     float s = 0.f, m = -INFINITY;
     int mi = 0x7fffffff;
     if (ok) {
         for (int c = 4 * l16; c < C; c += 64) {
-            const float4 v = *reinterpret_cast<const float4*>(xp + c);
+            const float4 v = ldv4<H>(x, xp + c);
             s += (v.x + v.y) + (v.z + v.w);
             if (v.x > m) { m = v.x; mi = c; }
             if (v.y > m) { m = v.y; mi = c + 1; }
@@ -340,15 +361,16 @@ __global__ void sa_conv_kernel(const float* pooled2, const float* w, float* attn
     }
 }
 // y = x * attn[p], float4 over channels (C % 4 == 0)
+template <bool H = false>
 __global__ void sa_mul_kernel(const float* x, const float* attn, float* y, long long P, int C) {
     const int C4 = C >> 2;
     const long long n = P * C4;
     GRID_STRIDE(i, n) {
         const long long p = i / C4;
         const float a = attn[p];
-        float4 v = reinterpret_cast<const float4*>(x)[i];
+        float4 v = ldv4<H>(x, 4 * i);
         v.x *= a; v.y *= a; v.z *= a; v.w *= a;
-        reinterpret_cast<float4*>(y)[i] = v;
+        stv4<H>(y, 4 * i, v);
     }
 }
 // bwd 1: g_logit[p] = (sum_c gy*x) * a*(1-a)
@@ -479,6 +501,18 @@ int hyres_bilinear_fwd(const float* x, int ldx, float* y, int ldy, int B, int Hi
                            C, scale_h, scale_w, accumulate);
     return HY_LAUNCH_CHECK("bilinear_fwd");
 }
+int hyres_bilinear_fwd_f16(const void* x, int ldx, void* y, int ldy, int B, int Hi, int Wi, int Ho, int Wo, int C,
+                           float scale_h, float scale_w, hyres_stream_t s) {
+    HY_REQUIRE(x && y && Hi > 0 && Wi > 0 && Ho > 0 && Wo > 0, HYRES_E_ARG, "bilinear_fwd_f16: bad args");
+    HY_REQUIRE(C % 4 == 0 && ldx % 4 == 0 && ldy % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 7) == 0 &&
+                   (reinterpret_cast<uintptr_t>(y) & 7) == 0,
+               HYRES_E_ALIGN, "bilinear_fwd_f16: C, ld %% 4 == 0 and 8B-aligned x/y required");
+    HY_REQUIRE((long long)B * Ho <= 65535 && (long long)Wo * C < (1LL << 30), HYRES_E_SHAPE, "bilinear_fwd_f16: too large");
+    const dim3 grid(ceil_div((long long)Wo * (C / 4), 256), B * Ho);
+    hipLaunchKernelGGL((bilinear_fwd_kernel<4, true>), grid, dim3(256), 0, as_stream(s), (const float*)x, ldx, (float*)y,
+                       ldy, B, Hi, Wi, Ho, Wo, C, scale_h, scale_w, 0);
+    return HY_LAUNCH_CHECK("bilinear_fwd_f16");
+}
 int hyres_bilinear_bwd(const float* gy, int ldgy, float* gx, int ldgx, int B, int Hi, int Wi, int Ho, int Wo, int C,
                        float scale_h, float scale_w, int accumulate, hyres_stream_t s) {
     HY_REQUIRE(gy && gx, HYRES_E_ARG, "bilinear_bwd: NULL");
@@ -519,6 +553,30 @@ int hyres_se_fwd(const float* x, const float* w1, const float* w2, float* y, flo
     long long n = (long long)B * HW * C;
     hipLaunchKernelGGL(se_scale_kernel, dim3(grid_for_r(n)), dim3(256), 0, st, x, (const float*)sgate, y, B, HW, C);
     return HY_LAUNCH_CHECK("se_scale");
+}
+
+int hyres_se_fwd_f16(const void* x, const float* w1, const float* w2, void* y, float* pooled, float* hidden,
+                     float* sgate, int B, int HW, int C, int Cr, void* ws, long long ws_bytes, hyres_stream_t s) {
+    HY_REQUIRE(x && w1 && w2 && y && pooled && hidden && sgate, HYRES_E_ARG, "se_fwd_f16: NULL");
+    HY_REQUIRE(C % 4 == 0 && C <= 1024 && 256 % (C / 4) == 0 && (reinterpret_cast<uintptr_t>(x) & 7) == 0 &&
+                   (reinterpret_cast<uintptr_t>(y) & 7) == 0,
+               HYRES_E_ALIGN, "se_fwd_f16: C %% 4 == 0, 256 %% (C/4) == 0, 8B-aligned x/y required");
+    const int nch = se_chunks(HW);
+    HY_REQUIRE(ws && ws_bytes >= (long long)B * nch * C * 4, HYRES_E_WORKSPACE, "se_fwd_f16: workspace");
+    const int per = (HW + nch - 1) / nch;
+    hipStream_t st = as_stream(s);
+    hipLaunchKernelGGL((se_pool4_kernel<false, true>), dim3(B, nch), dim3(256), 0, st, (const float*)x,
+                       (const float*)nullptr, HW, C, per, (float*)ws);
+    int rc = HY_LAUNCH_CHECK("se_pool_f16");
+    if (rc) return rc;
+    hipLaunchKernelGGL(se_fc_kernel, dim3(B), dim3(256), (C + Cr) * 4, st, (const float*)ws, nch, w1, w2, pooled,
+                       hidden, sgate, HW, C, Cr);
+    rc = HY_LAUNCH_CHECK("se_fc");
+    if (rc) return rc;
+    const long long n = (long long)B * HW * C / 4;
+    hipLaunchKernelGGL(se_scale4h_kernel, dim3(grid_for_r(n)), dim3(256), 0, st, (const float*)x, (const float*)sgate,
+                       (float*)y, B, HW, C);
+    return HY_LAUNCH_CHECK("se_scale_f16");
 }
 
 int hyres_se_bwd(const float* x, const float* gy, const float* w1, const float* w2, const float* pooled,
@@ -567,14 +625,34 @@ int hyres_spatial_attn_fwd(const float* x, const float* w, float* pooled2, int* 
     long long P = (long long)B * H * W;
     hipStream_t st = as_stream(s);
     HY_REQUIRE(C % 4 == 0 && aligned16(x), HYRES_E_ALIGN, "spatial_attn_fwd: C %% 4 and 16B-aligned x needed");
-    hipLaunchKernelGGL(sa_pool_kernel, dim3((unsigned)((P + 15) / 16)), dim3(256), 0, st, x, pooled2, argmax, P, C);
+    hipLaunchKernelGGL(sa_pool_kernel<false>, dim3((unsigned)((P + 15) / 16)), dim3(256), 0, st, x, pooled2, argmax, P, C);
     int rc = HY_LAUNCH_CHECK("sa_pool");
     if (rc) return rc;
     hipLaunchKernelGGL(sa_conv_kernel, dim3(grid_for_r(P)), dim3(256), 0, st, (const float*)pooled2, w, attn, B, H, W);
     rc = HY_LAUNCH_CHECK("sa_conv");
     if (rc) return rc;
-    hipLaunchKernelGGL(sa_mul_kernel, dim3(grid_for_r(P * C / 4)), dim3(256), 0, st, x, (const float*)attn, y, P, C);
+    hipLaunchKernelGGL(sa_mul_kernel<false>, dim3(grid_for_r(P * C / 4)), dim3(256), 0, st, x, (const float*)attn, y, P, C);
     return HY_LAUNCH_CHECK("sa_mul");
+}
+
+int hyres_spatial_attn_fwd_f16(const void* x, const float* w, float* pooled2, int* argmax, float* attn, void* y, int B,
+                               int H, int W, int C, hyres_stream_t s) {
+    HY_REQUIRE(x && w && pooled2 && argmax && attn && y, HYRES_E_ARG, "spatial_attn_fwd_f16: NULL");
+    HY_REQUIRE(C % 4 == 0 && C <= 1024 && (reinterpret_cast<uintptr_t>(x) & 7) == 0 &&
+                   (reinterpret_cast<uintptr_t>(y) & 7) == 0,
+               HYRES_E_ALIGN, "spatial_attn_fwd_f16: C %% 4 == 0 and 8B-aligned x/y required");
+    const long long P = (long long)B * H * W;
+    hipStream_t st = as_stream(s);
+    hipLaunchKernelGGL(sa_pool_kernel<true>, dim3((unsigned)((P + 15) / 16)), dim3(256), 0, st, (const float*)x, pooled2,
+                       argmax, P, C);
+    int rc = HY_LAUNCH_CHECK("sa_pool_f16");
+    if (rc) return rc;
+    hipLaunchKernelGGL(sa_conv_kernel, dim3(grid_for_r(P)), dim3(256), 0, st, (const float*)pooled2, w, attn, B, H, W);
+    rc = HY_LAUNCH_CHECK("sa_conv");
+    if (rc) return rc;
+    hipLaunchKernelGGL(sa_mul_kernel<true>, dim3(grid_for_r(P * C / 4)), dim3(256), 0, st, (const float*)x,
+                       (const float*)attn, (float*)y, P, C);
+    return HY_LAUNCH_CHECK("sa_mul_f16");
 }
 
 int hyres_spatial_attn_bwd(const float* x, const float* w, const float* pooled2, const int* argmax, const float* attn,

@@ -40,7 +40,8 @@ class Epilogue(ctypes.Structure):
                 ("aux0", ctypes.c_void_p), ("ld0", ctypes.c_int),
                 ("aux1", ctypes.c_void_p), ("ld1", ctypes.c_int),
                 ("aux2", ctypes.c_void_p), ("ld2", ctypes.c_int),
-                ("out2", ctypes.c_void_p), ("ldo2", ctypes.c_int), ("f16_operands", ctypes.c_int)]
+                ("out2", ctypes.c_void_p), ("ldo2", ctypes.c_int), ("f16_operands", ctypes.c_int),
+                ("io_f16", ctypes.c_int)]
 
 
 class WgradDesc(ctypes.Structure):
@@ -94,6 +95,7 @@ _SIGS = {
     "hyres_relu_bwd_2d": (_I, [_P, _I, _P, _I, _P, _I, _LL, _I, _P]),
     "hyres_prelu_bwd": (_I, [_P, _I, _P, _I, _P, _I, _LL, _I, _P, _P, _P, _LL, _P]),
     "hyres_attn_gate_fwd": (_I, [_P, _P, _P, _P, _LL, _P]),
+    "hyres_attn_gate_fwd_f16": (_I, [_P, _P, _P, _P, _LL, _P]),
     "hyres_attn_gate_bwd": (_I, [_P, _P, _P, _P, _P, _LL, _P]),
     "hyres_accumulate": (_I, [_P, _P, _LL, _P]),
     "hyres_scale": (_I, [_P, _P, _F, _P, _LL, _I, _P]),
@@ -129,6 +131,9 @@ _SIGS = {
     "hyres_se_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _LL, _P]),
     "hyres_se_workspace_bytes": (_LL, [_I, _I, _I]),
     "hyres_spatial_attn_fwd": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P]),
+    "hyres_bilinear_fwd_f16": (_I, [_P, _I, _P, _I, _I, _I, _I, _I, _I, _I, _F, _F, _P]),
+    "hyres_se_fwd_f16": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _LL, _P]),
+    "hyres_spatial_attn_fwd_f16": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P]),
     "hyres_spatial_attn_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _LL, _P]),
     "hyres_spatial_attn_workspace_bytes": (_LL, [_I, _I, _I]),
     "hyres_sum_log": (_I, [_P, _LL, _P, _P, _LL, _P]),

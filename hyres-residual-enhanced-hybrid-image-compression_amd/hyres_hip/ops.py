@@ -14,6 +14,7 @@ CPU oracle (oracle/hyres_oracle.py) in tests/test_parity_gpu.py.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 import weakref
@@ -54,8 +55,8 @@ class Workspace:
         return buf
 
 
-def _empty(shape, device) -> torch.Tensor:
-    return torch.empty(shape, dtype=torch.float32, device=device)
+def _empty(shape, device, dtype=torch.float32) -> torch.Tensor:
+    return torch.empty(shape, dtype=dtype, device=device)
 
 
 def zero_(t: torch.Tensor) -> torch.Tensor:
@@ -94,8 +95,13 @@ class Node:
         self.pending = None
 
     @staticmethod
-    def new(B, H, W, C, device, rg=True) -> "Node":
-        return Node(_empty((B, H, W, C), device), rg)
+    def new(B, H, W, C, device, rg=True, dtype=torch.float32) -> "Node":
+        return Node(_empty((B, H, W, C), device, dtype), rg)
+
+    @property
+    def half(self) -> bool:
+        """fp16 storage (autocast inference with fp16 activations, see ``act_f16``)."""
+        return self.v.dtype == torch.float16
 
     def slice(self, c0: int, c1: int, rg: Optional[bool] = None) -> "Node":
         return Node(self.v[..., c0:c1], self.rg if rg is None else rg, parent=self, c0=c0)
@@ -520,6 +526,36 @@ def f16_convs() -> bool:
     return torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.float16
 
 
+F16_ACT = os.environ.get("HYRES_F16_ACT", "1") == "1"
+_F16_REGION = [0]
+
+
+@contextlib.contextmanager
+def f16_region():
+    """Marks the sub-graphs whose activations may live as fp16 in HBM: g_a above the latent resolution,
+    g_s after its latent AttentionBlock, MultiScaleRefine (models/checkerboard.py, models/hyres.py)."""
+    _F16_REGION[0] += 1
+    try:
+        yield
+    finally:
+        _F16_REGION[0] -= 1
+
+
+def act_f16(tape: Optional["Tape"], H: int, W: int) -> bool:
+    """Store this activation as fp16 in HBM: inference (no tape) under ``torch.autocast(float16)`` — the
+    reference's C5 configuration ("fp16 activations": autocast makes every conv output fp16) — inside an
+    ``f16_region``. The latent-resolution entropy path (y, h_a, h_s, context, param_aggregation, the
+    likelihoods, the rANS symbols) stays fp32, so encoder and decoder index the same CDFs at any image size.
+    Arithmetic stays fp32 inside every kernel; HYRES_F16_ACT=0 keeps fp32 activations (fp16 operands only)."""
+    return tape is None and _F16_REGION[0] > 0 and F16_ACT and f16_convs()
+
+
+def _io_flags(x: "Node", y: "Node", tape: Optional["Tape"]) -> int:
+    io = (1 if x.half else 0) | (2 if y.half else 0)
+    assert io == 0 or tape is None, "fp16 activations are inference-only"
+    return io
+
+
 def _launch_conv(g: L.ConvGeom, x_ptr: int, w2: torch.Tensor, ldw: int, y_ptr: int, e: L.Epilogue) -> None:
     nb = L.load().hyres_conv_workspace_bytes(ctypes.byref(g))  # > 0 iff a split-K plan exists
     timed = KernelTimer.enabled
@@ -662,7 +698,8 @@ def conv2d(tape: Optional[Tape], x: Node, weight: torch.Tensor, bias: Optional[t
     B, H, W = x.B, x.H, x.W
     Ho = (H + 2 * pad - dil * (KH - 1) - 1) // stride + 1
     Wo = (W + 2 * pad - dil * (KW - 1) - 1) // stride + 1
-    y = out if out is not None else Node.new(B, Ho, Wo, Co, x.device)
+    ydt = torch.float16 if Co > 4 and act_f16(tape, Ho, Wo) else torch.float32
+    y = out if out is not None else Node.new(B, Ho, Wo, Co, x.device, dtype=ydt)
     assert (y.B, y.H, y.W, y.C) == (B, Ho, Wo, Co), ((y.B, y.H, y.W, y.C), (B, Ho, Wo, Co))
     g = _filter_taps(_geom("hyres_geom_conv2d", B, H, W, Ci, x.ld, Co, y.ld, KH, KW, stride, pad, dil), mask)
     if KH == 1 and KW == 1 and mask is None:
@@ -674,9 +711,10 @@ def conv2d(tape: Optional[Tape], x: Node, weight: torch.Tensor, bias: Optional[t
     e.act = act
     e.bias = L.ptr(bias)
     if res is not None:
-        assert (res.B, res.H, res.W, res.C) == (B, Ho, Wo, Co)
+        assert (res.B, res.H, res.W, res.C) == (B, Ho, Wo, Co) and res.half == y.half
         e.res = res.ptr()
         e.ldres = res.ld
+    e.io_f16 = _io_flags(x, y, tape)
     pre = None
     if act == L.ACT_PRELU:
         e.slope = slope.data_ptr()
@@ -737,13 +775,15 @@ def deconv2d(tape: Optional[Tape], x: Node, weight: torch.Tensor, bias: Optional
     assert Ci == x.C
     pad = K // 2
     B, H, W = x.B, x.H, x.W
-    y = out if out is not None else Node.new(B, 2 * H, 2 * W, Co, x.device)
+    ydt = torch.float16 if Co > 4 and act_f16(tape, 2 * H, 2 * W) else torch.float32
+    y = out if out is not None else Node.new(B, 2 * H, 2 * W, Co, x.device, dtype=ydt)
     g = _geom("hyres_geom_deconv2d", B, H, W, Ci, x.ld, Co, y.ld, K, pad)
     w2 = _prepped(weight, g, L.WPREP_DECONV, Ci, Co, K, K, pad)
     e = L.Epilogue()
     e.kind = L.EPI_BIAS
     e.act = act
     e.bias = L.ptr(bias)
+    e.io_f16 = _io_flags(x, y, tape)
     f16 = int(f16_convs())
     e.f16_operands = f16
     _launch_conv(g, x.ptr(), w2, g.ntaps * Ci, y.ptr(), e)
@@ -792,11 +832,12 @@ def gdn(tape: Optional[Tape], x: Node, beta: torch.Tensor, gamma: torch.Tensor, 
     bp = _empty((C,), dev)
     gp = _empty((C, C), dev)
     L.call("hyres_gdn_reparam_fwd", beta.data_ptr(), gamma.data_ptr(), bp.data_ptr(), gp.data_ptr(), C, L.stream())
-    y = Node.new(x.B, x.H, x.W, C, dev)
-    nrm = _empty((x.B, x.H, x.W, C), dev)
+    y = Node.new(x.B, x.H, x.W, C, dev, dtype=x.v.dtype)  # fp16 in -> fp16 out (autocast inference)
+    nrm = _empty((x.B, x.H, x.W, C), dev, x.v.dtype)
     g = _geom("hyres_geom_conv2d", x.B, x.H, x.W, C, x.ld, C, C, 1, 1, 1, 0, 1)
     e = L.Epilogue()
     e.kind = L.EPI_IGDN if inverse else L.EPI_GDN
+    e.io_f16 = _io_flags(x, y, tape)
     e.square_input = 1
     e.bias = bp.data_ptr()
     e.aux0 = x.ptr()
@@ -857,7 +898,11 @@ def attn_gate(tape: Optional[Tape], a: Node, b: Node, x: Node) -> Node:
     """AttentionBlock combine (models/layers/attention.py:44-47): out = a * sigmoid(b) + x."""
     assert a.contiguous and b.contiguous and x.contiguous
     n = a.P * a.C
-    out = Node.new(a.B, a.H, a.W, a.C, a.device)
+    out = Node.new(a.B, a.H, a.W, a.C, a.device, dtype=a.v.dtype)
+    if a.half:
+        assert b.half and x.half and tape is None
+        L.call("hyres_attn_gate_fwd_f16", a.ptr(), b.ptr(), x.ptr(), out.ptr(), n, L.stream())
+        return out
     L.call("hyres_attn_gate_fwd", a.ptr(), b.ptr(), x.ptr(), out.ptr(), n, L.stream())
     if tape is None:
         return out
@@ -970,6 +1015,8 @@ def to_nhwc(x: torch.Tensor, rg: bool = False) -> Node:
 
 
 def to_nchw(x: Node) -> torch.Tensor:
+    if x.half:  # fp16 activation (autocast inference): returned as fp32 NCHW
+        return x.v.permute(0, 3, 1, 2).float().contiguous()
     out = _empty((x.B, x.C, x.H, x.W), x.device)
     L.call("hyres_nhwc_to_nchw", x.ptr(), x.ld, out.data_ptr(), x.B, x.C, x.H, x.W, L.stream())
     return out

@@ -17,7 +17,12 @@ def bilinear(tape: Optional[Tape], x: Node, Ho: int, Wo: int, scale_h: float, sc
     """F.interpolate(mode='bilinear', align_corners=False).  ``scale_*`` is torch's source-index scale:
     1/scale_factor when a scale_factor is given (enhancement.py:96,101), in/out for ``size=``
     (enhancement.py:98,103)."""
-    y = out if out is not None else Node.new(x.B, Ho, Wo, x.C, x.device)
+    y = out if out is not None else Node.new(x.B, Ho, Wo, x.C, x.device, dtype=x.v.dtype)
+    if x.half:  # fp16 activations (autocast inference)
+        assert y.half and tape is None
+        L.call("hyres_bilinear_fwd_f16", x.ptr(), x.ld, y.ptr(), y.ld, x.B, x.H, x.W, Ho, Wo, x.C, float(scale_h),
+               float(scale_w), L.stream())
+        return y
     L.call("hyres_bilinear_fwd", x.ptr(), x.ld, y.ptr(), y.ld, x.B, x.H, x.W, Ho, Wo, x.C, float(scale_h),
            float(scale_w), 0, L.stream())
     if tape is None:
@@ -41,13 +46,15 @@ def se_block(tape: Optional[Tape], x: Node, w1: torch.Tensor, w2: torch.Tensor) 
     B, HW, C = x.B, x.H * x.W, x.C
     Cr = w1.shape[0]
     dev = x.device
-    y = Node.new(x.B, x.H, x.W, C, dev)
+    y = Node.new(x.B, x.H, x.W, C, dev, dtype=x.v.dtype)
     pooled = _empty((B, C), dev)
     hidden = _empty((B, Cr), dev)
     sgate = _empty((B, C), dev)
     wsb = L.load().hyres_se_workspace_bytes(B, HW, C)
     ws = _ws(wsb + B * C * 4, dev, slot=1)
-    L.call("hyres_se_fwd", x.ptr(), w1.data_ptr(), w2.data_ptr(), y.ptr(), pooled.data_ptr(), hidden.data_ptr(),
+    fn = "hyres_se_fwd_f16" if x.half else "hyres_se_fwd"
+    assert not x.half or tape is None
+    L.call(fn, x.ptr(), w1.data_ptr(), w2.data_ptr(), y.ptr(), pooled.data_ptr(), hidden.data_ptr(),
            sgate.data_ptr(), B, HW, C, Cr, ws.data_ptr(), ws.numel(), L.stream())
     if tape is None:
         return y
@@ -80,9 +87,11 @@ def spatial_attention_mul(tape: Optional[Tape], x: Node, w: torch.Tensor) -> Nod
     pooled2 = _empty((B, H, W, 2), dev)
     argmax = torch.empty((B, H, W), dtype=torch.int32, device=dev)
     attn = _empty((B, H, W), dev)
-    y = Node.new(B, H, W, C, dev)
-    L.call("hyres_spatial_attn_fwd", x.ptr(), w.data_ptr(), pooled2.data_ptr(), argmax.data_ptr(), attn.data_ptr(),
-           y.ptr(), B, H, W, C, L.stream())
+    y = Node.new(B, H, W, C, dev, dtype=x.v.dtype)
+    fn = "hyres_spatial_attn_fwd_f16" if x.half else "hyres_spatial_attn_fwd"
+    assert not x.half or tape is None
+    L.call(fn, x.ptr(), w.data_ptr(), pooled2.data_ptr(), argmax.data_ptr(), attn.data_ptr(), y.ptr(), B, H, W, C,
+           L.stream())
     if tape is None:
         return y
 

@@ -67,10 +67,23 @@ class LightWeightCheckerboard(CompressionModel):
             conv1x1(4 * M, 640), ReLU(inplace=True), conv1x1(640, 512), ReLU(inplace=True), conv1x1(512, 2 * M))
 
     # ------------------------------------------------------------------ HIP graph
+    def _g_a(self, tape, x: Node) -> Node:
+        """g_a; under autocast inference its layers above the latent resolution keep fp16 activations in
+        HBM (O.f16_region), conv(N, M) writes the latent y in fp32."""
+        with O.f16_region():
+            t = self.g_a[:7].hip(tape, x)
+        return self.g_a[7:].hip(tape, t)
+
+    def _g_s(self, tape, y_hat: Node) -> Node:
+        """g_s; the latent AttentionBlock(M) in fp32, the rest in the fp16 region (autocast inference)."""
+        t = self.g_s[:1].hip(tape, y_hat)
+        with O.f16_region():
+            return self.g_s[1:].hip(tape, t)
+
     def hip(self, tape, x: Node, training: bool, noisequant: bool):
         M = self.M
         T = O.Trace
-        y = self.g_a.hip(tape, x)
+        y = self._g_a(tape, x)
         O.GradReady.mark(tape, "hyper")  # backward: h_a/h_s/entropy/context/param_aggregation done
         z = self.h_a.hip(tape, y)
         z_hat, z_lik = self.entropy_bottleneck.hip(tape, z, training, noisequant, self.noise)
@@ -85,7 +98,7 @@ class LightWeightCheckerboard(CompressionModel):
         y_hat, y_lik = E.checkerboard_nonanchor_gc(tape, y, ya_hat, params_a, params_na, training, noisequant,
                                                    self.noise)
         O.GradReady.mark(tape, "g_s")
-        x_hat = self.g_s.hip(tape, y_hat)
+        x_hat = self._g_s(tape, y_hat)
         for name, n in (("y", y), ("z", z), ("z_hat", z_hat), ("latent_params", latent), ("y_anchor_hat", ya_hat),
                         ("ctx_params", ctx), ("y_hat", y_hat), ("residual_hat", x_hat)):
             T.add(name, n)
@@ -132,7 +145,7 @@ class LightWeightCheckerboard(CompressionModel):
         M = self.M
         gc, eb = self.gaussian_conditional, self.entropy_bottleneck
         xn = O.to_nhwc(x.to(dev).float().contiguous(), rg=False)
-        y = self.g_a.hip(None, xn)
+        y = self._g_a(None, xn)
         z = self.h_a.hip(None, y)
         z_strings = EC.eb_compress(eb, z)
         z_hat = EC.eb_decompress(eb, z_strings, z.H, z.W, dev) if self.decode_in_compress else None
@@ -178,7 +191,7 @@ class LightWeightCheckerboard(CompressionModel):
         self.context_prediction.hip(None, y_hat, out=lc.slice(2 * M, 4 * M))
         params_na = self.param_aggregation.hip(None, lc)
         EC.gc_decompress(gc, strings[0][1], params_na, M, y_hat, accumulate=True)  # + y_non_anchor_hat
-        x_hat = O.to_nchw(self.g_s.hip(None, y_hat)).clamp_(0, 1)
+        x_hat = O.to_nchw(self._g_s(None, y_hat)).clamp_(0, 1)
         return {"x_hat": x_hat, "time": time.time() - start_time}
 
     def inference(self, x):

@@ -39,7 +39,8 @@ class ResidualJPEGCompression(CompressionModel):
         residual_hat, y_lik, z_lik = self.residual_model.hip(tape, residual, training, noisequant)
         x0 = R.add(tape, jpeg, residual_hat)                              # hyres.py:62
         O.GradReady.mark(tape, "refine")  # backward: refine's gradients complete past this point
-        refined = self.refine.hip(tape, x0)                               # hyres.py:65
+        with O.f16_region():  # fp16 activations under autocast inference (configs[4])
+            refined = self.refine.hip(tape, x0)                           # hyres.py:65
         x_hat = R.add_clamp01(tape, x0, refined)                          # hyres.py:66-67
         O.Trace.add("x_hat_initial", x0)
         O.Trace.add("x_hat", x_hat)
@@ -104,7 +105,8 @@ class ResidualJPEGCompression(CompressionModel):
         jpeg_decoded = self.jpeg.decompress(compressed_data["jpeg_buffers"], device)
         decompress_result = self.residual_model.decompress(compressed_data["strings"], compressed_data["shape"])
         x_hat_initial = jpeg_decoded + decompress_result["x_hat"]
-        refined = self.refine(x_hat_initial)
+        with O.f16_region():  # fp16 activations under autocast (configs[4])
+            refined = self.refine(x_hat_initial)
         decompress_result["x_hat"] = torch.clamp(x_hat_initial + refined, 0, 1)
         return decompress_result
 

@@ -104,7 +104,7 @@ class MultiScaleRefine(HipModule):
         feat = self.se_block.hip(tape, feat)
         B, H, W = feat.B, feat.H, feat.W
         assert H % 4 == 0 and W % 4 == 0, "MultiScaleRefine needs H, W divisible by 4"
-        multi = Node.new(B, H, W, 3 * mid, feat.device)
+        multi = Node.new(B, H, W, 3 * mid, feat.device, dtype=feat.v.dtype)  # fp16 under autocast inference
 
         def scale1(tape, f):  # scale 1 (orig), written into multi[..., 0:mid]
             self.scale1.hip(tape, f, out=multi.slice(0, mid))

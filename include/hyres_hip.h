@@ -115,6 +115,11 @@ typedef struct hyres_epilogue {
     int f16_operands;             /* 1: X and W2 rounded to fp16 in the LDS staging, v_mfma_f32_32x32x16_f16
                                    * with fp32 accumulation and fp32 epilogue (autocast-fp16 inference,
                                    * BASELINE configs[4]); ignored on the small-Ci and narrow paths */
+    int io_f16;                   /* fp16 activations in HBM (autocast inference, configs[4]): bit 0 = X is
+                                   * fp16, bit 1 = Y and the epilogue's activation operands (res, aux0,
+                                   * out2) are fp16 (bias/slope stay fp32). Forward only: no accumulate,
+                                   * no GDN-backward kinds. X-fp16 needs Ci % 32 == 0 (or the narrow
+                                   * Co <= 4 kernel, whose Y stays fp32). */
 } hyres_epilogue;
 
 /* Y = conv(X, W2) with the epilogue — nn.Conv2d / nn.ConvTranspose2d / GDN forward and their
@@ -201,6 +206,8 @@ int hyres_prelu_bwd(const float* x, int ldx, const float* g, int ldg, float* gx,
 /* AttentionBlock gate (models/layers/attention.py:44-47): out = a*sigmoid(b) + x */
 int hyres_attn_gate_fwd(const float* a, const float* b, const float* x, float* out, long long n,
                         hyres_stream_t s);
+/* fp16 activations (autocast inference): a, b, x, out fp16 in HBM, n % 4 == 0, 8B-aligned. */
+int hyres_attn_gate_fwd_f16(const void* a, const void* b, const void* x, void* out, long long n, hyres_stream_t s);
 int hyres_attn_gate_bwd(const float* a, const float* b, const float* g, float* ga, float* gb,
                         long long n, hyres_stream_t s);
 /* y (+)= x  (gradient fan-in) */
@@ -309,6 +316,15 @@ int hyres_spatial_attn_bwd(const float* x, const float* w, const float* pooled2,
                            const float* attn, const float* gy, float* gx, float* gw, int B, int H, int W,
                            int C, void* ws, long long ws_bytes, hyres_stream_t s);
 long long hyres_spatial_attn_workspace_bytes(int B, int H, int W);
+/* fp16-activation forwards (x and y fp16 in HBM, fp32 arithmetic; autocast inference, BASELINE
+ * configs[4] "fp16 activations"): same semantics as the fp32 forwards above (bilinear without
+ * accumulate; C % 4 == 0, ld % 4 == 0, 8B-aligned x/y). pooled / hidden / sgate / pooled2 / attn fp32. */
+int hyres_bilinear_fwd_f16(const void* x, int ldx, void* y, int ldy, int B, int Hi, int Wi, int Ho, int Wo,
+                           int C, float scale_h, float scale_w, hyres_stream_t s);
+int hyres_se_fwd_f16(const void* x, const float* w1, const float* w2, void* y, float* pooled, float* hidden,
+                     float* sgate, int B, int HW, int C, int Cr, void* ws, long long ws_bytes, hyres_stream_t s);
+int hyres_spatial_attn_fwd_f16(const void* x, const float* w, float* pooled2, int* argmax, float* attn,
+                               void* y, int B, int H, int W, int C, hyres_stream_t s);
 
 /* ------------------------------------------------------------------------------------------ */
 /* losses and optimiser (src/losses/rd_loss.py:18-44, src/utils/engine.py:56-90)              */
