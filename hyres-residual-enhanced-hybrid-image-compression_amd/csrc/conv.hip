@@ -1938,7 +1938,7 @@ __global__ __launch_bounds__(256) void colsum_final_kernel(const float* part, in
 // conv_fwd_pf2_kernel: 64-row tiles on small grids (<= 65536 output pixels: few blocks per CU, K loops
 // latency-bound) with >= 4 K chunks per block; HYRES_CONV_PF2=0 disables
 static bool use_pf2_geom(const hyres_conv_geom& g, int mode, bool io, int tile_bm, int cps) {
-    static const int on = [] { const char* v = getenv("HYRES_CONV_PF2"); return (v && *v) ? atoi(v) : 1; }();
+    static const int on = [] { const char* v = getenv("HYRES_CONV_PF2"); return (v && *v) ? atoi(v) : 0; }();
     if (!on || io || mode == 2 || tile_bm != 64) return false;
     return (long long)g.B * g.Hq * g.Wq * g.nphase <= 65536 && cps >= 4;
 }
