@@ -161,6 +161,13 @@ def test_conv_kernel_name_follows_the_launch_routing():
     e.f16_operands = 1
     assert conv_variant(s5, e, False) == "conv_fwd_kernel<2, 2, 2, 2, 0, false, true>"
     assert conv_variant(s3, e, False) == "conv_fwd_kernel<1, 1, 2, 2, 0, false, true>"
+    # fp16 activations (autocast inference): conv_fwd_h_kernel<tile, mode, split, io>
+    e.io_f16 = 3
+    assert conv_variant(g3, e, False) == "conv_fwd_h_kernel<2, 1, 2, 2, 0, false, 3>"
+    assert conv_variant(g1, e, False) == "conv_fwd_h_kernel<1, 2, 2, 2, 0, false, 3>"  # not the fp32 stream kernel
+    e.io_f16 = 2
+    e.f16_operands = 0
+    assert conv_variant(gs, e, False) == "conv_fwd_h_kernel<1, 1, 2, 2, 2, false, 2>"  # fp32 image in, fp16 out
 
 
 def test_conv_plan_split_follows_the_tile():
