@@ -40,7 +40,6 @@ struct ConvArgs {
     int xcd;     // 1: grid.x = M tiles x N tiles in XCD-aware order (grid.y = 1)
     int prio;    // 1: raise the wave priority while it issues its MFMA cluster (s_setprio)
     int x_bytes; // conv1x1_stream_kernel: bytes of X (buffer-resource range)
-    int tile_bm; // rows of the chosen tile (host-side routing)
 };
 
 
@@ -167,7 +166,7 @@ __device__ __forceinline__ void epi_store4(const hyres_epilogue& e, float* y, in
     }
 }
 
-template <int TM, int TN, int WAVES_M, int WAVES_N, int MODE, bool SPLITK, bool F16, int IO, int PF = 1>
+template <int TM, int TN, int WAVES_M, int WAVES_N, int MODE, bool SPLITK, bool F16, int IO>
 __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
     // MODE 0: Ci % 32 == 0 (float4 loads); 1: same + square A (GDN); 2: generic scalar (small Ci).
     // F16: operands rounded to fp16 when staged into LDS ([row][32 halves], pitch PADH halves) and
@@ -176,9 +175,6 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
     // bit 1 Y / res / aux0 / out2 are fp16; arithmetic stays fp32 (F16: fp16 MFMA operands as before).
     static_assert(!F16 || MODE != 2, "fp16 operands on the Ci % 32 == 0 paths only");
     static_assert(!(IO & 1) || MODE != 2, "fp16 X on the Ci % 32 == 0 paths only");
-    // PF = 2 (small-grid layers, few blocks per CU): two register sets, so each chunk's global loads are
-    // issued two chunks ahead of its LDS store instead of one (latency-bound K loops)
-    static_assert(PF == 1 || (PF == 2 && MODE != 2), "prefetch distance 2 on the vector paths only");
     constexpr bool XH = (IO & 1) != 0, YH = (IO & 2) != 0;
     constexpr int XES = XH ? 2 : 4;  // X element bytes
     constexpr int PADH = 40;
@@ -240,7 +236,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
     if constexpr (MODE == 2) nk = (ntap * Ci + KT - 1) / KT;
     else nk = ntap * (Ci / KT);
 
-    float4 ra[PF][MODE == 2 ? 1 : A_V], rb[PF][MODE == 2 ? 1 : B_V];
+    float4 ra[MODE == 2 ? 1 : A_V], rb[MODE == 2 ? 1 : B_V];
     float sa[MODE == 2 ? A_V : 1], sb[MODE == 2 ? B_V : 1];
 
     // vector path: raw buffer loads (out-of-range offset -> 0, no branches). The X resource starts at
@@ -266,7 +262,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
     // (tap, channel) of the next chunk to load, advanced incrementally (no division per chunk)
     int ld_t = 0, ld_c = 0;
 
-    auto load_chunk = [&](int kc, int sl) {
+    auto load_chunk = [&](int kc) {
         if constexpr (MODE != 2) {
             const int2 o = tapoff[ld_t];
             const int c0 = ld_c + 4 * c4;
@@ -284,13 +280,13 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
                     v = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
                 }
                 if constexpr (MODE == 1) { v.x *= v.x; v.y *= v.y; v.z *= v.z; v.w *= v.w; }
-                ra[sl][q] = v;
+                ra[q] = v;
             }
 #pragma unroll
             for (int q = 0; q < B_V; ++q) {
                 const int co = n0 + tid / 8 + 32 * q;
                 const int off = co < g.Co ? (co * a.ldw + gt * Ci + c0) * 4 : (int)0x80000000;
-                rb[sl][q] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(wr, off, 0, 0));
+                rb[q] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(wr, off, 0, 0));
             }
             ld_c += KT;
             if (ld_c == Ci) { ld_c = 0; ++ld_t; }
@@ -318,28 +314,26 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
             }
         }
     };
-    auto store_chunk = [&](int sl) {
+    auto store_chunk = [&]() {
         if constexpr (F16) {
             typedef _Float16 half4 __attribute__((ext_vector_type(4)));
 #pragma unroll
             for (int q = 0; q < A_V; ++q) {
-                const float4 v = ra[sl][q];
-                const half4 h = {(_Float16)v.x, (_Float16)v.y, (_Float16)v.z, (_Float16)v.w};
+                const half4 h = {(_Float16)ra[q].x, (_Float16)ra[q].y, (_Float16)ra[q].z, (_Float16)ra[q].w};
                 *reinterpret_cast<half4*>(&Ah[(tid / 8 + 32 * q) * PADH + 4 * c4]) = h;
             }
 #pragma unroll
             for (int q = 0; q < B_V; ++q) {
-                const float4 v = rb[sl][q];
-                const half4 h = {(_Float16)v.x, (_Float16)v.y, (_Float16)v.z, (_Float16)v.w};
+                const half4 h = {(_Float16)rb[q].x, (_Float16)rb[q].y, (_Float16)rb[q].z, (_Float16)rb[q].w};
                 *reinterpret_cast<half4*>(&Bh[(tid / 8 + 32 * q) * PADH + 4 * c4]) = h;
             }
         } else if constexpr (MODE != 2) {
 #pragma unroll
             for (int q = 0; q < A_V; ++q)
-                *reinterpret_cast<float4*>(&As[(tid / 8 + 32 * q) * PADK + 4 * c4]) = ra[sl][q];
+                *reinterpret_cast<float4*>(&As[(tid / 8 + 32 * q) * PADK + 4 * c4]) = ra[q];
 #pragma unroll
             for (int q = 0; q < B_V; ++q)
-                *reinterpret_cast<float4*>(&Bs[(tid / 8 + 32 * q) * PADK + 4 * c4]) = rb[sl][q];
+                *reinterpret_cast<float4*>(&Bs[(tid / 8 + 32 * q) * PADK + 4 * c4]) = rb[q];
         } else {
 #pragma unroll
             for (int q = 0; q < A_V; ++q) {
@@ -373,7 +367,12 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
         ld_t = kbeg / cpt;
         ld_c = (kbeg - ld_t * cpt) * KT;
     }
-    auto mfma_chunk = [&]() {
+    if (kbeg < kend) load_chunk(kbeg);
+    for (int kc = kbeg; kc < kend; ++kc) {
+        __syncthreads();
+        store_chunk();
+        __syncthreads();
+        if (kc + 1 < kend) load_chunk(kc + 1);
         if constexpr (F16) {
             typedef _Float16 half8 __attribute__((ext_vector_type(8)));
             if (a.prio) __builtin_amdgcn_s_setprio(1);
@@ -395,58 +394,32 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
                         acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[tm], bf[tn], acc[tm][tn], 0, 0, 0);
             }
             if (a.prio) __builtin_amdgcn_s_setprio(0);
-        } else {
-            if (a.prio) __builtin_amdgcn_s_setprio(1);
+            continue;
+        }
+        if (a.prio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                float4 af[TM], bf[TN];
+        for (int u = 0; u < 4; ++u) {
+            float4 af[TM], bf[TN];
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm)
+                af[tm] = *reinterpret_cast<const float4*>(
+                    &As[(wm * TM * 32 + tm * 32 + lr) * PADK + lh * 16 + 4 * u]);
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn)
+                bf[tn] = *reinterpret_cast<const float4*>(
+                    &Bs[(wn * TN * 32 + tn * 32 + lr) * PADK + lh * 16 + 4 * u]);
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
 #pragma unroll
                 for (int tm = 0; tm < TM; ++tm)
-                    af[tm] = *reinterpret_cast<const float4*>(
-                        &As[(wm * TM * 32 + tm * 32 + lr) * PADK + lh * 16 + 4 * u]);
 #pragma unroll
-                for (int tn = 0; tn < TN; ++tn)
-                    bf[tn] = *reinterpret_cast<const float4*>(
-                        &Bs[(wn * TN * 32 + tn * 32 + lr) * PADK + lh * 16 + 4 * u]);
-#pragma unroll
-                for (int e = 0; e < 4; ++e)
-#pragma unroll
-                    for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-                        for (int tn = 0; tn < TN; ++tn) {
-                            float av = e == 0 ? af[tm].x : e == 1 ? af[tm].y : e == 2 ? af[tm].z : af[tm].w;
-                            float bv = e == 0 ? bf[tn].x : e == 1 ? bf[tn].y : e == 2 ? bf[tn].z : bf[tn].w;
-                            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[tm][tn], 0, 0, 0);
-                        }
-            }
-            if (a.prio) __builtin_amdgcn_s_setprio(0);
+                    for (int tn = 0; tn < TN; ++tn) {
+                        float av = e == 0 ? af[tm].x : e == 1 ? af[tm].y : e == 2 ? af[tm].z : af[tm].w;
+                        float bv = e == 0 ? bf[tn].x : e == 1 ? bf[tn].y : e == 2 ? bf[tn].z : bf[tn].w;
+                        acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[tm][tn], 0, 0, 0);
+                    }
         }
-    };
-    if constexpr (PF == 1) {
-        if (kbeg < kend) load_chunk(kbeg, 0);
-        for (int kc = kbeg; kc < kend; ++kc) {
-            __syncthreads();
-            store_chunk(0);
-            __syncthreads();
-            if (kc + 1 < kend) load_chunk(kc + 1, 0);
-            mfma_chunk();
-        }
-    } else {
-        if (kbeg < kend) load_chunk(kbeg, 0);
-        if (kbeg + 1 < kend) load_chunk(kbeg + 1, 1);
-        for (int kc = kbeg; kc < kend; kc += 2) {
-            __syncthreads();
-            store_chunk(0);
-            __syncthreads();
-            if (kc + 2 < kend) load_chunk(kc + 2, 0);
-            mfma_chunk();
-            if (kc + 1 >= kend) break;
-            __syncthreads();
-            store_chunk(1);
-            __syncthreads();
-            if (kc + 3 < kend) load_chunk(kc + 3, 1);
-            mfma_chunk();
-        }
+        if (a.prio) __builtin_amdgcn_s_setprio(0);
     }
 
     // ---- epilogue: stage the accumulators through LDS one TN column slice at a time (static register
@@ -573,12 +546,6 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
 template <int TM, int TN, int WAVES_M, int WAVES_N, int MODE, bool SPLITK, bool F16 = false>
 __global__ __launch_bounds__(256) void conv_fwd_kernel(const ConvArgs a) {
     conv_fwd_body<TM, TN, WAVES_M, WAVES_N, MODE, SPLITK, F16, 0>(a);
-}
-
-// small grids (the 64-row tiles of the 64^2 / 32^2 layers): prefetch distance 2 in the K loop
-template <int TM, int TN, int WAVES_M, int WAVES_N, int MODE, bool SPLITK, bool F16>
-__global__ __launch_bounds__(256) void conv_fwd_pf2_kernel(const ConvArgs a) {
-    conv_fwd_body<TM, TN, WAVES_M, WAVES_N, MODE, SPLITK, F16, 0, 2>(a);
 }
 
 // fp16 activations in HBM (IO = 1: X fp16, 2: Y fp16, 3: both); fp16 MFMA operands except on the
@@ -1154,17 +1121,17 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgradArgs a) {
                     load_p(kc + 1);
                     load_q(t0);
                 }
-#pragma unroll
+    #pragma unroll
                 for (int s = 0; s < KT / 2; ++s) {
                     const int k = lh * (KT / 2) + s;
                     float af[TM], bf[TN];
-#pragma unroll
+    #pragma unroll
                     for (int tm = 0; tm < TM; ++tm) af[tm] = Ps[k * PP + wm * TM * 32 + tm * 32 + lr];
-#pragma unroll
+    #pragma unroll
                     for (int tn = 0; tn < TN; ++tn) bf[tn] = Qs[k * PQ + wn * TN * 32 + tn * 32 + lr];
-#pragma unroll
+    #pragma unroll
                     for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
+    #pragma unroll
                         for (int tn = 0; tn < TN; ++tn)
                             acc[j][tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[tm], bf[tn], acc[j][tm][tn], 0, 0, 0);
                 }
@@ -1935,20 +1902,6 @@ __global__ __launch_bounds__(256) void colsum_final_kernel(const float* part, in
 // ------------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------------
-// conv_fwd_pf2_kernel: 64-row tiles on small grids (<= 65536 output pixels: few blocks per CU, K loops
-// latency-bound) with >= 4 K chunks per block; HYRES_CONV_PF2=0 disables
-static bool use_pf2_geom(const hyres_conv_geom& g, int mode, bool io, int tile_bm, int cps) {
-    static const int on = [] { const char* v = getenv("HYRES_CONV_PF2"); return (v && *v) ? atoi(v) : 0; }();
-    if (!on || io || mode == 2 || tile_bm != 64) return false;
-    return (long long)g.B * g.Hq * g.Wq * g.nphase <= 65536 && cps >= 4;
-}
-static bool use_pf2(const ConvArgs& a, int mode) {
-    int maxtap = 0;
-    for (int ph = 0; ph < a.g.nphase; ++ph) maxtap = std::max(maxtap, a.g.ntap[ph]);
-    const int nk = maxtap * (a.g.Ci / KT);
-    return use_pf2_geom(a.g, mode, a.e.io_f16 != 0, a.tile_bm, a.nsplit > 1 ? a.cps : nk);
-}
-
 template <int TM, int TN, int WM_, int WN_>
 static int launch_fwd(const ConvArgs& a, int mode, hipStream_t st) {
     constexpr int BM = 32 * TM * WM_, BN = 32 * TN * WN_;
@@ -1972,21 +1925,6 @@ static int launch_fwd(const ConvArgs& a, int mode, hipStream_t st) {
         }
 #undef HY_H
         return HY_LAUNCH_CHECK("conv_fwd_h_kernel");
-    }
-    if (use_pf2(a, mode)) {
-        const bool f16 = a.e.f16_operands != 0;
-#define HY_PF(MODE_, SPLIT_)                                                                                    \
-    {                                                                                                          \
-        if (f16) hipLaunchKernelGGL((conv_fwd_pf2_kernel<TM, TN, WM_, WN_, MODE_, SPLIT_, true>), grid, dim3(256), 0, st, a); \
-        else hipLaunchKernelGGL((conv_fwd_pf2_kernel<TM, TN, WM_, WN_, MODE_, SPLIT_, false>), grid, dim3(256), 0, st, a); \
-    }
-        if (a.nsplit > 1) {
-            if (mode == 0) HY_PF(0, true) else HY_PF(1, true)
-        } else {
-            if (mode == 0) HY_PF(0, false) else HY_PF(1, false)
-        }
-#undef HY_PF
-        return HY_LAUNCH_CHECK("conv_fwd_pf2_kernel");
     }
     if (a.e.f16_operands && mode != 2) {
         if (a.nsplit > 1) {
@@ -2434,7 +2372,6 @@ int hyres_conv_forward(const hyres_conv_geom* g, const float* x, const float* w2
             return launch_stream(a, nt, g->Ci / 8, per_cu, st);
         }
     }
-    a.tile_bm = TILE_BM[ch.tile];
     int rc;
     switch (ch.tile) {
         case 0: rc = launch_fwd<2, 2, 2, 2>(a, mode, st); break;
@@ -2478,17 +2415,6 @@ int hyres_conv_kernel_name(const hyres_conv_geom* g, const hyres_epilogue* e, in
         snprintf(buf, n, "conv_fwd_h_kernel<%s, %d, %s, %d>", tiles[ch.tile], ch.mode, split ? "true" : "false",
                  e->io_f16);
         return 0;
-    }
-    {
-        int maxtap = 0;
-        for (int ph = 0; ph < g->nphase; ++ph) maxtap = std::max(maxtap, g->ntap[ph]);
-        const ConvPlan p = conv_plan(g, ch.tile);
-        const int nk = ch.mode == 2 ? 0 : maxtap * (g->Ci / KT);
-        if (use_pf2_geom(*g, ch.mode, false, TILE_BM[ch.tile], split && p.nsplit > 1 ? p.cps : nk)) {
-            snprintf(buf, n, "conv_fwd_pf2_kernel<%s, %d, %s, %s>", tiles[ch.tile], ch.mode, split ? "true" : "false",
-                     f16 ? "true" : "false");
-            return 0;
-        }
     }
     snprintf(buf, n, "conv_fwd_kernel<%s, %d, %s, %s>", tiles[ch.tile], ch.mode, split ? "true" : "false",
              f16 ? "true" : "false");
