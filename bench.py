@@ -199,6 +199,19 @@ def amp_leg(net, opt, aux_opt, crit, x, jpeg, jpeg_bpp, args):
         aux_opt.zero_grad()
         return c
 
+    def step_graph_cpu(xc, x_next):
+        """The drop-in loop's graphed step (src/utils/engine.py _GraphedStep): JPEG on the host for a CPU
+        batch (the next one prefetched), H2D, replay, optimiser."""
+        net.jpeg.prefetch(x_next)
+        dec, bpp = net.jpeg(xc)
+        graphed.replay(xc.to(dev), dec.to(dev), float(bpp))
+        opt.step()
+        opt.zero_grad()
+        aux = net.aux_loss()
+        aux.backward()
+        aux_opt.step()
+        aux_opt.zero_grad()
+
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -231,7 +244,7 @@ def amp_leg(net, opt, aux_opt, crit, x, jpeg, jpeg_bpp, args):
                     + ("f16" if os.environ.get("HYRES_AMP_WGRAD_F16", "1") == "1" else "fp32")}
 
 
-def host_jpeg_legs(net, step_eager_cpu, x_cpu, reps=5):
+def host_jpeg_legs(net, step_eager_cpu, x_cpu, reps=5, step_graph_cpu=None):
     """SURVEY §8d "reported twice" / §8f f2: the host JPEG stage alone (1 thread, a thread pool, worker
     processes) and the C2 train step WITH the host JPEG stage inline, eager, as train.sh runs it
     (``model(d)`` on a CPU batch: JPEG round trip on the host, H2D copy, device step), then the same with
@@ -268,6 +281,17 @@ def host_jpeg_legs(net, step_eager_cpu, x_cpu, reps=5):
         torch.cuda.synchronize()
         ms = (time.time() - t0) * 1000 / reps
         res[tag] = {"ms_per_step": round(ms, 3), "mpix_s": round(B * x_cpu.shape[2] * x_cpu.shape[3] / ms / 1e3, 3)}
+    if step_graph_cpu is not None:
+        # src/utils/engine.py's default: host JPEG (prefetched) + H2D + the replayed forward/loss/backward graph
+        step_graph_cpu(xs[0], xs[1])
+        torch.cuda.synchronize()
+        t0 = time.time()
+        for i in range(reps):
+            step_graph_cpu(xs[i % 2], xs[(i + 1) % 2])
+        torch.cuda.synchronize()
+        ms = (time.time() - t0) * 1000 / reps
+        res["with_host_jpeg_prefetch_graph"] = {"ms_per_step": round(ms, 3),
+                                                "mpix_s": round(B * x_cpu.shape[2] * x_cpu.shape[3] / ms / 1e3, 3)}
     return res
 
 
@@ -428,6 +452,19 @@ def main():
         aux_opt.step()
         aux_opt.zero_grad()
 
+    def step_graph_cpu(xc, x_next):
+        """The drop-in loop's graphed step (src/utils/engine.py _GraphedStep): JPEG on the host for a CPU
+        batch (the next one prefetched), H2D, replay, optimiser."""
+        net.jpeg.prefetch(x_next)
+        dec, bpp = net.jpeg(xc)
+        graphed.replay(xc.to(dev), dec.to(dev), float(bpp))
+        opt.step()
+        opt.zero_grad()
+        aux = net.aux_loss()
+        aux.backward()
+        aux_opt.step()
+        aux_opt.zero_grad()
+
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -488,7 +525,7 @@ def main():
         amp = amp_leg(net, opt, aux_opt, crit, x, jpeg, jpeg_bpp, args)
     host = None
     if world == 1 and not args.no_host_jpeg:
-        host = host_jpeg_legs(net, step_eager_cpu, x_cpu)
+        host = host_jpeg_legs(net, step_eager_cpu, x_cpu, step_graph_cpu=step_graph_cpu if graphed is not None else None)
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, args.cpu_baseline_seconds)

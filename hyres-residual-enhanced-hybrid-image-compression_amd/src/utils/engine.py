@@ -14,7 +14,11 @@ Differences from the reference, by design:
     (hyres_hip.optim.DeviceGradScaler), so there is still no per-step host sync.  The reference's NaN
     warning is printed when the metrics are drained;
   * the next batch's host JPEG round trip is started in the background before the current step
-    (TurboJPEGCompression.prefetch), so the host JPEG stage overlaps the device step.
+    (TurboJPEGCompression.prefetch), so the host JPEG stage overlaps the device step;
+  * forward + RD loss + backward replay as a HIP graph (hyres_hip.graphs.CapturedStep, one capture per
+    batch shape / noisequant / precision, taken on an accumulation boundary); the host JPEG stage, the
+    H2D copies, the gradient all-reduce (after the replay, as bench.py's N > 1 default), the optimiser and
+    the aux step stay eager. HYRES_TRAIN_GRAPH=0 runs every step eagerly (the reference's structure).
 """
 import os
 import time
@@ -48,6 +52,51 @@ def _drain(pending, meters, nan_flags=None):
         nan_flags.clear()
 
 
+class _GraphedStep:
+    """The drop-in training step's forward + loss + backward as replayed HIP graphs."""
+
+    def __init__(self, model, criterion, device, mixed_precision, accumulation, scaler, zero_grad):
+        self.model, self.criterion, self.device = model, criterion, device
+        self.amp, self.accum, self.scaler, self.zero_grad = mixed_precision, accumulation, scaler, zero_grad
+        self.caps = {}
+        # loss multiplier inside the graph: 1/accumulation (x the GradScaler's device scale under AMP)
+        self.ls = torch.full((1,), 1.0 / accumulation, dtype=torch.float32, device=device)
+        self.enabled = os.environ.get("HYRES_TRAIN_GRAPH", "1") == "1" and device.type == "cuda"
+
+    def __call__(self, d, noisequant, boundary_start, reducer):
+        """Returns the static loss dict of the replayed step, or None (run this step eagerly)."""
+        if not self.enabled or d.device.type != "cpu" or not hasattr(self.model, "forward_device"):
+            return None
+        key = (tuple(d.shape), bool(noisequant), bool(self.amp))
+        cap = self.caps.get(key)
+        if cap is None and not boundary_start:
+            return None  # capturing zeroes the gradients: only where no partial accumulation exists
+        dec, bpp = self.model.jpeg(d)  # host JPEG round trip (prefetched in the background)
+        x = d.to(self.device)
+        jd = dec.to(self.device)
+        if self.scaler is not None:
+            torch.mul(self.scaler.scale, 1.0 / self.accum, out=self.ls)
+        if cap is None:
+            from hyres_hip.graphs import CapturedStep
+            armed = reducer.armed if reducer is not None else None
+            if reducer is not None:
+                reducer.armed = False  # no collective inside warm-up or capture
+            try:
+                cap = CapturedStep(self.model, x, jd, float(bpp), noisequant=noisequant, criterion=self.criterion,
+                                   zero_grad=self.zero_grad, amp=self.amp, loss_scale=self.ls,
+                                   capture_error_mode="thread_local" if reducer is not None else "global")
+            except Exception as exc:  # noqa: BLE001 - any capture failure: stay correct, run eagerly
+                print(f"HIP graph capture failed ({exc!r}); training steps run eagerly")
+                self.enabled = False
+                self.zero_grad()
+                return None
+            finally:
+                if reducer is not None:
+                    reducer.armed = armed
+            self.caps[key] = cap
+        return cap.replay(x, jd, float(bpp))[1]
+
+
 def _lookahead(loader):
     """(batch, next batch or None) pairs."""
     it = iter(loader)
@@ -77,24 +126,32 @@ def train_one_epoch(model, criterion, train_dataloader, optimizer, aux_optimizer
     aux_loss = None
     amp = (lambda: torch.autocast("cuda", dtype=torch.float16)) if mixed_precision else nullcontext
     jpeg = getattr(model, "jpeg", None)
+    graphed = _GraphedStep(model, criterion, device, mixed_precision, gradient_accumulation_steps, scaler,
+                           optimizer.zero_grad)
     for i, (d, d_next) in enumerate(_lookahead(train_dataloader)):
         if d_next is not None and hasattr(jpeg, "prefetch"):
             jpeg.prefetch(d_next)  # the next batch's host JPEG overlaps this step's device work
-        with amp():
-            out_net = model(d, noisequant)
-            d = d.to(device)
-            out_criterion = criterion(out_net, d)
-            loss = out_criterion["loss"]
-            if gradient_accumulation_steps != 1:
-                loss = loss / gradient_accumulation_steps
-        if reducer is not None:  # overlapped all-reduce only on the accumulation boundary (DDP no_sync)
-            reducer.armed = (i + 1) % gradient_accumulation_steps == 0
-        pending.append(_metrics(out_criterion))
-        if scaler is not None:
-            scaler.scale_loss(loss).backward()
+        crit = graphed(d, noisequant, i % gradient_accumulation_steps == 0, reducer)
+        if crit is not None:
+            pending.append(_metrics(crit))
+            n_img = len(d)
         else:
-            loss.backward()
-        del out_net, out_criterion, loss
+            with amp():
+                out_net = model(d, noisequant)
+                d = d.to(device)
+                out_criterion = criterion(out_net, d)
+                loss = out_criterion["loss"]
+                if gradient_accumulation_steps != 1:
+                    loss = loss / gradient_accumulation_steps
+            if reducer is not None:  # overlapped all-reduce only on the accumulation boundary (DDP no_sync)
+                reducer.armed = (i + 1) % gradient_accumulation_steps == 0
+            pending.append(_metrics(out_criterion))
+            if scaler is not None:
+                scaler.scale_loss(loss).backward()
+            else:
+                loss.backward()
+            n_img = len(d)
+            del out_net, out_criterion, loss
         if (i + 1) % gradient_accumulation_steps == 0:
             if reducer is not None:
                 reducer.all_reduce()
@@ -116,7 +173,7 @@ def train_one_epoch(model, criterion, train_dataloader, optimizer, aux_optimizer
             aux_optimizer.zero_grad()
         if i % log_every == 0:
             _drain(pending, meters, nan_flags)
-            print(f"Train epoch {epoch}: [{i * len(d)}/{len(train_dataloader.dataset)} "
+            print(f"Train epoch {epoch}: [{i * n_img}/{len(train_dataloader.dataset)} "
                   f"({100. * i / max(len(train_dataloader), 1):.0f}%)]"
                   f"\tLoss: {meters['loss'].val:.3f} |\tBpp loss: {meters['bpp_loss'].val:.3f} |"
                   f"\tResidual Bpp: {meters['residual_bpp_loss'].val:.3f} |"
