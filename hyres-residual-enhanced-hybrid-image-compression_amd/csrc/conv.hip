@@ -1171,9 +1171,11 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgradArgs a) {
 // and 9 barriers per chunk, the latency of each exposed at 2 blocks per CU); here it is one load of
 // 3 x 34 px per chunk and one barrier per 9 x 16 MFMAs. 64 x 64 tiles, 4 waves of 32 x 32.
 // ------------------------------------------------------------------------------------------------
-template <int KR, int KW, int SQ>
+template <int KR, int KW, int SQ, int DIL = 1>
 __global__ __launch_bounds__(256, 2) void wgrad_halo_kernel(const WgradArgs a, int dhg, int dwg) {
-    constexpr int BM = 64, BN = 64, NT = KR * KW, HC = 31 * SQ + KW;  // halo columns of a 32-px chunk
+    // DIL: tap spacing (2: MultiScaleRefine's dilated 3x3, enhancement.py:44-51): the KR halo rows are DIL
+    // rows apart, the halo columns span 31*SQ + DIL*(KW-1) + 1 pixels
+    constexpr int BM = 64, BN = 64, NT = KR * KW, HC = 31 * SQ + DIL * (KW - 1) + 1;  // halo columns of a 32-px chunk
     constexpr int PP = BM + 4, PQ = BN + 4;
     constexpr int PSZ = KT * PP, HSZ = KR * HC * PQ;
     constexpr int P_V = KT * BM / 4 / 256;
@@ -1192,7 +1194,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo_kernel(const WgradArgs a, i
     const int split = rr / a.ngroups;
     const int m0 = mt * BM, n0 = nt * BN;
     const int t0 = grp * NT;
-    const int dh0 = dhg + grp * KR;  // the group's first kernel row offset, first column offset dwg
+    const int dh0 = dhg + grp * KR * DIL;  // the group's first kernel row offset, first column offset dwg
     const int cpr = d.Wq / 32;
     float4 rp[P_V], rh[H_V];
     auto load = [&](int kc) {
@@ -1212,7 +1214,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo_kernel(const WgradArgs a, i
             const int e = tid + 256 * q;
             const int pix = e / (BN / 4), c = (e % (BN / 4)) * 4;
             const int hr = pix / HC, hc = pix - (pix / HC) * HC;
-            const int ih = i * SQ + dh0 + hr, iw = j0 * SQ + dwg + hc;
+            const int ih = i * SQ + dh0 + DIL * hr, iw = j0 * SQ + dwg + hc;
             const bool ok = e < H_E && (unsigned)ih < (unsigned)d.Hqq && (unsigned)iw < (unsigned)d.Wqq && n0 + c < d.N;
             rh[q] = ok ? ld4(a.q + ((long long)(b * d.Hqq + ih) * d.Wqq + iw) * d.ldq + n0 + c)
                        : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1266,7 +1268,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo_kernel(const WgradArgs a, i
             for (int s2 = 0; s2 < KT / 2; ++s2) {
                 const int k = lh * (KT / 2) + s2;
                 const float af = Ps[k * PP + wm * 32 + lr];
-                const float bf = Hs[(hr * HC + k * SQ + hc) * PQ + wn * 32 + lr];
+                const float bf = Hs[(hr * HC + k * SQ + DIL * hc) * PQ + wn * 32 + lr];
                 acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(af, bf, acc[t], 0, 0, 0);
             }
         });
@@ -2464,20 +2466,25 @@ namespace hyres {
 
 struct WgradPlan {
     int TMc, TNc, WMc, WNc, NT, BM, BN, mtiles, ntiles, ngroups, nchunks, nsplit, cps, tapn, nblocks;
-    int halo, hk, hdh, hdw;  // wgrad_halo_kernel: K, first tap's (dh, dw)
+    int halo, hk, hdh, hdw, hdil;  // wgrad_halo_kernel: K, first tap's (dh, dw), tap spacing
 };
 
-// wgrad_halo_kernel applies: fp32, dense KxK taps (K = 3 or 5, dilation 1), Q stride 1 or 2, base rows of a
-// multiple of 32 pixels, both operands >= 32 channels on the float4 path
-static bool halo_ok(const hyres_wgrad_desc* d, int* K) {
+// wgrad_halo_kernel applies: fp32, dense KxK taps (K = 3 or 5, dilation 1; K = 3 with dilation 2), Q stride
+// 1 or 2 (5x5 only), base rows of a multiple of 32 pixels, both operands >= 32 channels on the float4 path.
+// *dil = the tap spacing.
+static bool halo_ok(const hyres_wgrad_desc* d, int* K, int* dil) {
     static const int on = env_int("HYRES_WGRAD_HALO", 1);
     if (!on || d->f16_operands || d->square_q || (d->sq != 1 && d->sq != 2)) return false;
     if (d->Wq % 32 != 0 || d->M < 32 || d->N < 32 || d->M % 4 || d->N % 4 || d->ldp % 4 || d->ldq % 4) return false;
     const int k = d->ntaps == 9 ? 3 : d->ntaps == 25 ? 5 : 0;
     if (!k || (d->sq == 2 && k != 5)) return false;  // stride 2 only for the 5x5 (de)convs (3x3 s2: 123 KB LDS)
+    static const int dil_on = env_int("HYRES_WGRAD_HALO_DIL", 1);
+    const int D = d->dw[1] - d->dw[0];
+    if (D != 1 && !(dil_on && D == 2 && k == 3 && d->sq == 1)) return false;
     for (int t = 0; t < d->ntaps; ++t)
-        if (d->dh[t] != d->dh[0] + t / k || d->dw[t] != d->dw[0] + t % k) return false;
+        if (d->dh[t] != d->dh[0] + D * (t / k) || d->dw[t] != d->dw[0] + D * (t % k)) return false;
     *K = k;
+    *dil = D;
     return true;
 }
 
@@ -2507,7 +2514,7 @@ static WgradPlan wgrad_plan(const hyres_wgrad_desc* d) {
     p.mtiles = ceil_div(d->M, p.BM); p.ntiles = ceil_div(ncols, p.BN);
     p.ngroups = p.tapn ? 1 : ceil_div(d->ntaps, p.NT);
     p.nchunks = ceil_div((long long)d->B * d->Hq * d->Wq, kt);
-    if (kt == KT && halo_ok(d, &p.hk)) {
+    if (kt == KT && halo_ok(d, &p.hk, &p.hdil)) {
         p.halo = 1;
         p.hdh = d->dh[0];
         p.hdw = d->dw[0];
@@ -2702,7 +2709,9 @@ int hyres_conv_wgrad(const hyres_wgrad_desc* d0, const float* pp, const float* q
     if (thin) {
         launch_thin(a, tp, st);
     } else if (p.halo) {
-        if (p.hk == 3) hipLaunchKernelGGL((wgrad_halo_kernel<3, 3, 1>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
+        if (p.hk == 3 && p.hdil == 2)
+            hipLaunchKernelGGL((wgrad_halo_kernel<3, 3, 1, 2>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
+        else if (p.hk == 3) hipLaunchKernelGGL((wgrad_halo_kernel<3, 3, 1>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
         else if (d->sq == 1) hipLaunchKernelGGL((wgrad_halo_kernel<1, 5, 1>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
         else hipLaunchKernelGGL((wgrad_halo_kernel<1, 5, 2>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
     } else if (wgrad_f16_ok(d)) {

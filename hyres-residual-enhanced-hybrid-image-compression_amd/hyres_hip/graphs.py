@@ -26,6 +26,7 @@ Graph-safety of the captured region:
 from __future__ import annotations
 
 import contextlib
+import os
 from typing import Callable, Optional
 
 import torch
@@ -93,7 +94,11 @@ class CapturedStep:
         O.bump_weight_epoch()  # record every weight re-layout inside the graph
         # "thread_local" when an RCCL process group exists: its watchdog thread polls events while the
         # main thread captures (no collective is ever inside the graph)
-        with torch.cuda.graph(self.graph, capture_error_mode=capture_error_mode):
+        # HYRES_MAIN_PRIORITY: stream priority of the captured main stream (the graph's kernels keep it;
+        # the branch streams' is HYRES_BRANCH_PRIORITY)
+        prio = int(os.environ.get("HYRES_MAIN_PRIORITY", "0"))
+        cap_stream = torch.cuda.Stream(device=dev, priority=prio) if prio else None
+        with torch.cuda.graph(self.graph, stream=cap_stream, capture_error_mode=capture_error_mode):
             self.out, self.crit = run()
         O.bump_weight_epoch()  # eager calls must not reuse buffers only the graph writes
         torch.cuda.synchronize(dev)

@@ -56,6 +56,8 @@ CONV_CASES = [
     (2, 3, 128, 16, 40, 5, 2, 2, 1),   # two tap groups, stride 2
     # halo-staged weight gradient (wgrad_halo_kernel): base rows a multiple of 32 pixels
     (2, 64, 64, 32, 32, 3, 1, 1, 1),   # 3x3, all 9 taps per block
+    (2, 64, 64, 20, 64, 3, 1, 2, 2),   # dilated 3x3 (MultiScaleRefine): halo rows 2 apart
+    (1, 96, 64, 32, 32, 3, 1, 2, 2),
     (1, 96, 64, 8, 64, 3, 1, 1, 1),    # partial N tile (Ci = 96), two 32-px chunks per row
     (2, 64, 64, 64, 64, 5, 2, 2, 1),   # 5x5 stride 2 (Q stride 2), one kernel row per block
     (2, 64, 128, 32, 64, 5, 1, 2, 1),  # 5x5 stride 1, two M tiles
