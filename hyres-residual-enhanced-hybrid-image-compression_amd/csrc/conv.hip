@@ -1171,6 +1171,135 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgradArgs a) {
 // and 9 barriers per chunk, the latency of each exposed at 2 blocks per CU); here it is one load of
 // 3 x 34 px per chunk and one barrier per 9 x 16 MFMAs. 64 x 64 tiles, 4 waves of 32 x 32.
 // ------------------------------------------------------------------------------------------------
+// 1x1 weight gradient (stride 1, fp32, 16B-aligned P/Q): dW[m][n] = sum_p P[p][m] Q[p][n] over the split's
+// pixel range. P and Q rows of one 32-pixel chunk are the same pixels, so both load as contiguous float4
+// rows (no tap shift / pixel decode); double-buffered [pixel][channel] LDS tiles, one barrier per chunk;
+// the bias gradient (column sums of P) rides on the A operand already in registers (one VALU add per
+// MFMA step in the wn == 0 waves) instead of a serial LDS pass per chunk.
+template <int TM, int TN, int WAVES_M, int WAVES_N>
+__global__ __launch_bounds__(256) void wgrad1x1_kernel(const WgradArgs a) {
+    constexpr int BM = 32 * TM * WAVES_M, BN = 32 * TN * WAVES_N;
+    constexpr int PP = BM + 4, PQ = BN + 4;
+    constexpr int P_V = KT * BM / 4 / 256, Q_V = KT * BN / 4 / 256;
+    static_assert(P_V >= 1 && Q_V >= 1, "tile too small");
+    __shared__ __attribute__((aligned(16))) float Psm[2 * KT * PP];
+    __shared__ __attribute__((aligned(16))) float Qsm[2 * KT * PQ];
+    const hyres_wgrad_desc& d = a.d;
+    const int tid = threadIdx.x;
+    const int bid = blockIdx.x;
+    const int lb = (bid & 7) * (gridDim.x >> 3) + (bid >> 3);  // XCD-aware order, as wgrad_kernel
+    if (lb >= a.nblocks) return;
+    int rr = lb;
+    const int mt = rr % a.mtiles; rr /= a.mtiles;
+    const int nt = rr % a.ntiles; rr /= a.ntiles;
+    const int split = rr;
+    const int m0 = mt * BM, n0 = nt * BN;
+    const long long Qtot = (long long)d.B * d.Hq * d.Wq;
+    float4 rp[P_V], rq[Q_V];
+    auto load = [&](int kc) {
+        const long long k0 = (long long)kc * KT;
+#pragma unroll
+        for (int i = 0; i < P_V; ++i) {
+            const int e = tid + 256 * i;
+            const int row = e / (BM / 4), c = (e % (BM / 4)) * 4;
+            rp[i] = (k0 + row < Qtot && m0 + c < d.M) ? ld4(a.p + (k0 + row) * d.ldp + m0 + c)
+                                                        : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int i = 0; i < Q_V; ++i) {
+            const int e = tid + 256 * i;
+            const int row = e / (BN / 4), c = (e % (BN / 4)) * 4;
+            rq[i] = (k0 + row < Qtot && n0 + c < d.N) ? ld4(a.q + (k0 + row) * d.ldq + n0 + c)
+                                                        : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    auto store = [&](int buf) {
+        float* Ps = Psm + buf * (KT * PP);
+        float* Qs = Qsm + buf * (KT * PQ);
+#pragma unroll
+        for (int i = 0; i < P_V; ++i) {
+            const int e = tid + 256 * i;
+            *reinterpret_cast<float4*>(&Ps[(e / (BM / 4)) * PP + (e % (BM / 4)) * 4]) = rp[i];
+        }
+#pragma unroll
+        for (int i = 0; i < Q_V; ++i) {
+            const int e = tid + 256 * i;
+            *reinterpret_cast<float4*>(&Qs[(e / (BN / 4)) * PQ + (e % (BN / 4)) * 4]) = rq[i];
+        }
+    };
+    const int lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+    const int lr = lane & 31, lh = lane >> 5;
+    floatx16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    const bool do_bias = a.bias_slab != nullptr && nt == 0 && wn == 0;
+    float bsum[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) bsum[i] = 0.f;
+    const int kb = split * a.chunks_per_split;
+    const int ke = min(a.nchunks, kb + a.chunks_per_split);
+    if (kb < ke) {
+        load(kb);
+        store(0);
+    }
+    __syncthreads();
+    int cur = 0;
+    for (int kc = kb; kc < ke; ++kc) {
+        const bool next = kc + 1 < ke;
+        if (next) load(kc + 1);  // in flight during this chunk's MFMAs
+        const float* Ps = Psm + cur * (KT * PP);
+        const float* Qs = Qsm + cur * (KT * PQ);
+#pragma unroll
+        for (int s2 = 0; s2 < KT / 2; ++s2) {
+            const int k = 2 * s2 + lh;
+            float av[TM], bv[TN];
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm) av[tm] = Ps[k * PP + wm * TM * 32 + tm * 32 + lr];
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn) bv[tn] = Qs[k * PQ + wn * TN * 32 + tn * 32 + lr];
+            if (do_bias) {
+#pragma unroll
+                for (int tm = 0; tm < TM; ++tm) bsum[tm] += av[tm];
+            }
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                for (int tn = 0; tn < TN; ++tn)
+                    acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[tm], bv[tn], acc[tm][tn], 0, 0, 0);
+        }
+        if (next) store(cur ^ 1);
+        __syncthreads();
+        cur ^= 1;
+    }
+    if (do_bias) {
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm) {
+            const float t = bsum[tm] + __shfl_xor(bsum[tm], 32);  // the two lane halves cover even / odd pixels
+            const int m = m0 + wm * TM * 32 + tm * 32 + lr;
+            if (lh == 0 && m < d.M) a.bias_slab[(long long)split * d.M + m] = t;
+        }
+    }
+    const long long MN = (long long)d.M * d.N;
+    float* out = a.slab + (long long)split * MN;
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) {
+            const int n = n0 + wn * TN * 32 + tn * 32 + lr;
+            if (n >= d.N) continue;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + wm * TM * 32 + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                if (m < d.M) out[(long long)m * d.N + n] = acc[tm][tn][r];
+            }
+        }
+}
+
 template <int KR, int KW, int SQ, int DIL = 1>
 __global__ __launch_bounds__(256, 2) void wgrad_halo_kernel(const WgradArgs a, int dhg, int dwg) {
     // DIL: tap spacing (2: MultiScaleRefine's dilated 3x3, enhancement.py:44-51): the KR halo rows are DIL
@@ -2706,7 +2835,17 @@ int hyres_conv_wgrad(const hyres_wgrad_desc* d0, const float* pp, const float* q
     dim3 grid(ceil_div(p.nblocks, 8) * 8);
     hipStream_t st = as_stream(s);
     const bool sqr = d->square_q != 0;
-    if (thin) {
+    static const int w1x1 = env_int("HYRES_WGRAD_1X1", 1);
+    const bool one = w1x1 && !thin && !p.halo && !wgrad_f16_ok(d) && !sqr && !p.tapn && vp && vq &&
+                     d->ntaps == 1 && d->dh[0] == 0 && d->dw[0] == 0 && d->sq == 1 && d->Hqq == d->Hq &&
+                     d->Wqq == d->Wq && p.ngroups == 1;
+    if (one) {
+        if (p.TMc == 2 && p.TNc == 2) hipLaunchKernelGGL((wgrad1x1_kernel<2, 2, 2, 2>), grid, dim3(256), 0, st, a);
+        else if (p.TMc == 2) hipLaunchKernelGGL((wgrad1x1_kernel<2, 1, 2, 2>), grid, dim3(256), 0, st, a);
+        else if (p.WMc == 1) hipLaunchKernelGGL((wgrad1x1_kernel<1, 1, 1, 4>), grid, dim3(256), 0, st, a);
+        else if (p.WNc == 1) hipLaunchKernelGGL((wgrad1x1_kernel<1, 1, 4, 1>), grid, dim3(256), 0, st, a);
+        else hipLaunchKernelGGL((wgrad1x1_kernel<1, 1, 2, 2>), grid, dim3(256), 0, st, a);
+    } else if (thin) {
         launch_thin(a, tp, st);
     } else if (p.halo) {
         if (p.hk == 3 && p.hdil == 2)

@@ -1,0 +1,58 @@
+"""Microbenchmark one conv weight gradient (hyres_conv_wgrad: kernel + split reduce) with HIP events,
+with and without the fused bias gradient.
+
+    python scripts/wgrad_micro.py [--B 16 --H 128 --Ci 64 --Co 128 --K 1 --iters 30]
+"""
+import argparse
+import ctypes
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "hyres-residual-enhanced-hybrid-image-compression_amd"))
+
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--B", type=int, default=16)
+    ap.add_argument("--H", type=int, default=128)
+    ap.add_argument("--Ci", type=int, default=64)
+    ap.add_argument("--Co", type=int, default=128)
+    ap.add_argument("--K", type=int, default=1)
+    ap.add_argument("--iters", type=int, default=30)
+    a = ap.parse_args()
+    from hyres_hip import _lib as L
+    dev = torch.device("cuda:0")
+    x = torch.randn(a.B, a.H, a.H, a.Ci, device=dev)
+    gy = torch.randn(a.B, a.H, a.H, a.Co, device=dev)
+    dw = torch.zeros(a.Co, a.Ci, a.K, a.K, device=dev)
+    db = torch.zeros(a.Co, device=dev)
+    d = L.WgradDesc()
+    L.call("hyres_wgrad_desc_conv2d", ctypes.byref(d), a.B, a.H, a.H, a.Ci, a.Ci, a.Co, a.Co, a.K, a.K, 1, a.K // 2, 1)
+    d.sm = a.Ci * a.K * a.K
+    nb = L.load().hyres_wgrad_workspace_bytes(ctypes.byref(d))
+    ws = torch.empty(nb // 4 + 16, device=dev)
+    for bias in (True, False):
+        def run():
+            L.call("hyres_conv_wgrad", ctypes.byref(d), gy.data_ptr(), x.data_ptr(), dw.data_ptr(),
+                   db.data_ptr() if bias else None, ws.data_ptr(), nb, L.stream())
+        for _ in range(3):
+            run()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(a.iters):
+            run()
+        e1.record()
+        torch.cuda.synchronize()
+        us = 1000 * e0.elapsed_time(e1) / a.iters
+        flops = 2.0 * a.B * a.H * a.H * a.K * a.K * a.Ci * a.Co
+        byts = 4.0 * a.B * a.H * a.H * (a.Ci + a.Co)
+        print(f"wgrad B{a.B} {a.H}^2 {a.Ci}->{a.Co} K{a.K} bias={int(bias)}: {us:.1f} us, {flops / us / 1e6:.1f} TFLOP/s, "
+              f"{byts / us / 1e3:.0f} GB/s")
+
+
+if __name__ == "__main__":
+    main()
