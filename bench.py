@@ -97,7 +97,7 @@ def cpu_baseline(args, budget_s):
                       f"itself cannot run here (compressai absent)"}
 
 
-PMC_TRAFFIC = os.path.join(REPO, "profiles", "r2_v2_pmc_traffic.json")  # scripts/profile_round.sh r2v2
+PMC_TRAFFIC = os.path.join(REPO, "profiles", "r2_v3_pmc_traffic.json")  # scripts/profile_round.sh r2v3
 
 
 def traffic_bytes_per_launch(kernel):
