@@ -3,6 +3,8 @@
 // Activations are NHWC; every kernel streams HBM with the channel index on the fastest lanes.
 #include "common.h"
 
+#include <cstdlib>
+
 namespace hyres {
 
 #define GRID_STRIDE(i, n) \
@@ -144,6 +146,43 @@ __global__ __launch_bounds__(256) void bilinear_bwd_kernel(const float* gy, int 
         } else {
             *gp = acc ? *gp + s.x : s.x;
         }
+    }
+}
+
+// backward of an exact integer down-sampling (enhancement.py:96,101: F.interpolate(scale_factor=1/S),
+// S = 2 or 4, H_in = S*H_out): with align_corners=False every output o averages input pixels
+// S*o + (S-2)/2 and the next one with weights 1/2 (src = S*(o+0.5)-0.5 is exact in fp32), so each
+// input-gradient element receives exactly one 0.25*gy term or nothing — a streaming kernel instead of
+// the general gather (which evaluates every candidate stencil weight per element); the same fp32 result
+// (0.5 * (0.5 * g) == 0.25 * g).
+template <int S>
+__global__ __launch_bounds__(256) void bilinear_down_bwd_kernel(const float* gy, int ldgy, float* gx, int ldgx, int Hi,
+                                                                int Wi, int Ho, int Wo, int C, int acc) {
+    constexpr int A0 = (S - 2) / 2;
+    const int CG = C / 4;
+    const int row = blockIdx.y;
+    const int b = row / Hi, h = row - b * Hi;
+    const int dh = h - A0;
+    const bool hok = dh >= 0 && (dh % S) < 2;
+    const long long gyr = ((long long)b * Ho + (hok ? dh / S : 0)) * Wo;
+    float* gr = gx + (long long)row * Wi * ldgx;
+    const int n = Wi * CG;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+        const int w = i / CG;
+        const int c = (i - w * CG) * 4;
+        const int dw = w - A0;
+        const bool ok = hok && dw >= 0 && (dw % S) < 2;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (ok) {
+            const float4 g = ld4(gy + (gyr + dw / S) * ldgy + c);
+            v = make_float4(0.25f * g.x, 0.25f * g.y, 0.25f * g.z, 0.25f * g.w);
+        }
+        float* gp = gr + (long long)w * ldgx + c;
+        if (acc) {
+            const float4 o = ld4(gp);
+            v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+        }
+        *reinterpret_cast<float4*>(gp) = v;
     }
 }
 
@@ -519,6 +558,17 @@ int hyres_bilinear_bwd(const float* gy, int ldgy, float* gx, int ldgx, int B, in
     const bool vec = C % 4 == 0 && ldgy % 4 == 0 && ldgx % 4 == 0 && aligned16(gy) && aligned16(gx);
     HY_REQUIRE((long long)B * Hi <= 65535 && (long long)Wi * C < (1LL << 30), HYRES_E_SHAPE, "bilinear_bwd: too large");
     const dim3 grid(ceil_div((long long)Wi * (vec ? C / 4 : C), 256), B * Hi);
+    static const int down_on = [] { const char* v = getenv("HYRES_BILINEAR_DOWN_BWD"); return (v && *v) ? atoi(v) : 1; }();
+    for (int S = 2; S <= 4 && vec && down_on; S += 2) {
+        if (scale_h != (float)S || scale_w != (float)S || Hi != S * Ho || Wi != S * Wo) continue;
+        if (S == 2)
+            hipLaunchKernelGGL(bilinear_down_bwd_kernel<2>, grid, dim3(256), 0, as_stream(s), gy, ldgy, gx, ldgx, Hi,
+                               Wi, Ho, Wo, C, accumulate);
+        else
+            hipLaunchKernelGGL(bilinear_down_bwd_kernel<4>, grid, dim3(256), 0, as_stream(s), gy, ldgy, gx, ldgx, Hi,
+                               Wi, Ho, Wo, C, accumulate);
+        return HY_LAUNCH_CHECK("bilinear_down_bwd");
+    }
     if (vec)
         hipLaunchKernelGGL(bilinear_bwd_kernel<4>, grid, dim3(256), 0, as_stream(s), gy, ldgy, gx, ldgx, B, Hi, Wi, Ho,
                            Wo, C, scale_h, scale_w, accumulate);
