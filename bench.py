@@ -352,10 +352,12 @@ def analysis_synthesis(net, x, reps):
 
 def main():
     args = parse()
-    # host JPEG worker processes: spawned before this process touches the GPU (hyres_hip.jpeg_host)
-    from hyres_hip import jpeg_host
-    jpeg_host.start(args.jpeg_procs)
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    # host JPEG worker processes: spawned before this process touches the GPU (hyres_hip.jpeg_host); only
+    # the N = 1 run times the host JPEG legs, so N > 1 ranks code their one setup batch in-process (no
+    # 8 workers per rank on a full node)
+    from hyres_hip import jpeg_host
+    jpeg_host.start(args.jpeg_procs if world == 1 else 0)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1 or os.environ.get("HYRES_BENCH_FORCE_DIST") == "1"  # rehearse the RCCL path at N=1
