@@ -80,6 +80,10 @@ class CapturedStep:
             with torch.no_grad(), ctx:
                 return net.forward_device(self.x, self.jpeg, self.bpp, noisequant), None
 
+        # warm-up and capture run on side streams while the parameters' AccumulateGrad nodes were made on
+        # the default stream; the stream waits above/below order them, so torch's mismatch warning is noise
+        if self.train and hasattr(torch.autograd.graph, "set_warn_on_accumulate_grad_stream_mismatch"):
+            torch.autograd.graph.set_warn_on_accumulate_grad_stream_mismatch(False)
         side = torch.cuda.Stream(device=dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):

@@ -179,7 +179,7 @@ def train_one_epoch(model, criterion, train_dataloader, optimizer, aux_optimizer
                   f"\tResidual Bpp: {meters['residual_bpp_loss'].val:.3f} |"
                   f"\ty_Bpp loss: {meters['y_bpp_loss'].val:.4f} |\tz_Bpp loss: {meters['z_bpp_loss'].val:.4f} |"
                   f"\tMSE loss: {meters['mse_loss'].val:.3f} |"
-                  f"\tAux loss: {float(aux_loss) if aux_loss is not None else 0.0:.2f}")
+                  f"\tAux loss: {float(aux_loss.detach()) if aux_loss is not None else 0.0:.2f}")
     _drain(pending, meters, nan_flags)
     print(f"Train epoch {epoch}: Average losses:\tLoss: {meters['loss'].avg:.3f} |"
           f"\tBpp loss: {meters['bpp_loss'].avg:.4f} |\tResidual Bpp: {meters['residual_bpp_loss'].avg:.4f} |"
