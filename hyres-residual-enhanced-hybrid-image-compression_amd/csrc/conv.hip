@@ -1647,6 +1647,156 @@ __global__ __launch_bounds__(256) void wgrad_f16_kernel(const WgradArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// AMP halo-staged weight gradient: wgrad_halo_kernel's schedule (one 32-pixel row segment of P and ONE
+// Q halo tile of KR rows x HC columns per chunk, all KR x KW taps of the group read from the halo at their
+// (dh, dw) shift, one barrier per chunk) with wgrad_f16_kernel's operands: both tiles rounded to fp16 when
+// staged ([pixel][channel] rows, pitch 64 + 32 halves) and read back transposed with ds_read_b64_tr_b16
+// into v_mfma_f32_32x32x16_f16 (fp32 accumulation). The generic f16 kernel gathers a shifted Q chunk per
+// tap (one tap per block, 9x the Q loads); here a 3x3 group costs one 3 x 34-pixel halo load per chunk.
+// The tap's B rows are halo rows base + k*SQ: the transposed read takes per-lane addresses, so the stride
+// is just a pitch of SQ*PQ. Bias gradient = fp32 column sums of the unrounded P (as wgrad_f16_kernel).
+// ------------------------------------------------------------------------------------------------
+template <int KR, int KW, int SQ, int DIL = 1>
+__global__ __launch_bounds__(256, 2) void wgrad_halo_f16_kernel(const WgradArgs a, int dhg, int dwg) {
+    constexpr int BM = 64, BN = 64, NT = KR * KW, HC = 31 * SQ + DIL * (KW - 1) + 1;
+    constexpr int PP = BM + 32, PQ = BN + 32;  // halves
+    constexpr int PSZ = KT * PP, HSZ = KR * HC * PQ;
+    constexpr int P_V = KT * BM / 4 / 256;  // 2 float4 of P per thread and chunk
+    constexpr int H_E = KR * HC * (BN / 4);
+    constexpr int H_V = (H_E + 255) / 256;
+    static_assert((PSZ + HSZ) % 4 == 0, "8-byte aligned buffers for the transposed reads");
+    __shared__ __attribute__((aligned(16))) _Float16 smem[2 * (PSZ + HSZ)];
+    const hyres_wgrad_desc& d = a.d;
+    const int tid = threadIdx.x;
+    const int bid = blockIdx.x;
+    const int lb = (bid & 7) * (gridDim.x >> 3) + (bid >> 3);  // XCD-aware order, as wgrad_kernel
+    if (lb >= a.nblocks) return;
+    int rr = lb;
+    const int mt = rr % a.mtiles; rr /= a.mtiles;
+    const int nt = rr % a.ntiles; rr /= a.ntiles;
+    const int grp = rr % a.ngroups;
+    const int split = rr / a.ngroups;
+    const int m0 = mt * BM, n0 = nt * BN;
+    const int t0 = grp * NT;
+    const int dh0 = dhg + grp * KR * DIL;
+    const int cpr = d.Wq / 32;
+    // this thread's fixed channel quad of P (256 % (BM/4) == 0): rows tid/16 + 16*q
+    const int pc = (tid % (BM / 4)) * 4, prow0 = tid / (BM / 4);
+    float4 rp[P_V], rh[H_V];
+    auto load = [&](int kc) {
+        const int b = kc / (d.Hq * cpr);
+        const int rem = kc - b * d.Hq * cpr;
+        const int i = rem / cpr;
+        const int j0 = (rem - i * cpr) * 32;
+        const long long q0 = (long long)kc * 32;
+#pragma unroll
+        for (int q = 0; q < P_V; ++q)
+            rp[q] = m0 + pc < d.M ? ld4(a.p + (q0 + prow0 + 16 * q) * d.ldp + m0 + pc) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int q = 0; q < H_V; ++q) {
+            const int e = tid + 256 * q;
+            const int pix = e / (BN / 4), c = (e % (BN / 4)) * 4;
+            const int hr = pix / HC, hc = pix - (pix / HC) * HC;
+            const int ih = i * SQ + dh0 + DIL * hr, iw = j0 * SQ + dwg + hc;
+            const bool ok = e < H_E && (unsigned)ih < (unsigned)d.Hqq && (unsigned)iw < (unsigned)d.Wqq && n0 + c < d.N;
+            rh[q] = ok ? ld4(a.q + ((long long)(b * d.Hqq + ih) * d.Wqq + iw) * d.ldq + n0 + c)
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    const bool do_bias = a.bias_slab != nullptr && nt == 0 && grp == 0;
+    float4 bsum = make_float4(0.f, 0.f, 0.f, 0.f);
+    auto store = [&](int buf) {
+        _Float16* Ps = smem + buf * (PSZ + HSZ);
+        _Float16* Hs = Ps + PSZ;
+#pragma unroll
+        for (int q = 0; q < P_V; ++q) {
+            if (do_bias) { bsum.x += rp[q].x; bsum.y += rp[q].y; bsum.z += rp[q].z; bsum.w += rp[q].w; }
+            const halfx4_t h = {(_Float16)rp[q].x, (_Float16)rp[q].y, (_Float16)rp[q].z, (_Float16)rp[q].w};
+            *reinterpret_cast<halfx4_t*>(&Ps[(prow0 + 16 * q) * PP + pc]) = h;
+        }
+#pragma unroll
+        for (int q = 0; q < H_V; ++q) {
+            const int e = tid + 256 * q;
+            if (e < H_E) {
+                const halfx4_t h = {(_Float16)rh[q].x, (_Float16)rh[q].y, (_Float16)rh[q].z, (_Float16)rh[q].w};
+                *reinterpret_cast<halfx4_t*>(&Hs[(e / (BN / 4)) * PQ + (e % (BN / 4)) * 4]) = h;
+            }
+        }
+    };
+
+    const int lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    // transposed-read lane address (wgrad_f16_kernel): half lh takes k rows 8lh..8lh+7 of a 16-k step
+    const int lh = lane >> 5, lg = (lane >> 4) & 1, lq = (lane >> 2) & 3, lp = lane & 3;
+    const int tr_row = 8 * lh + lq, tr_col = 16 * lg + 4 * lp;
+    floatx16 acc[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+    const int kb = split * a.chunks_per_split;
+    const int ke = min(a.nchunks, kb + a.chunks_per_split);
+    if (kb < ke) {
+        load(kb);
+        store(0);
+    }
+    __syncthreads();
+    int cur = 0;
+    for (int kc = kb; kc < ke; ++kc) {
+        if (kc + 1 < ke) load(kc + 1);  // next chunk in flight during this chunk's NT x 2 MFMAs per wave
+        const _Float16* Ps = smem + cur * (PSZ + HSZ);
+        const _Float16* Hs = Ps + PSZ;
+#pragma unroll
+        for (int s = 0; s < KT / 16; ++s) {
+            const _Float16* pa = Ps + (16 * s + tr_row) * PP + wm * 32 + tr_col;
+            const halfx4_t alo = lds_tr4(pa), ahi = lds_tr4(pa + 4 * PP);
+            const halfx8_t af = __builtin_shufflevector(alo, ahi, 0, 1, 2, 3, 4, 5, 6, 7);
+            static_for<NT>([&](auto J) {
+                constexpr int t = decltype(J)::value;
+                constexpr int hr = t / KW, hc = t % KW;
+                const _Float16* pb = Hs + (hr * HC + DIL * hc + SQ * (16 * s + tr_row)) * PQ + wn * 32 + tr_col;
+                const halfx4_t blo = lds_tr4(pb), bhi = lds_tr4(pb + 4 * SQ * PQ);
+                const halfx8_t bf = __builtin_shufflevector(blo, bhi, 0, 1, 2, 3, 4, 5, 6, 7);
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af, bf, acc[t], 0, 0, 0);
+            });
+        }
+        if (kc + 1 < ke) store(cur ^ 1);
+        __syncthreads();
+        cur ^= 1;
+    }
+    if (do_bias) {
+        float4* red = reinterpret_cast<float4*>(smem);  // the loop ended with a barrier
+        red[tid] = bsum;
+        __syncthreads();
+        if (tid < BM / 4) {
+            float4 s4 = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int r = 0; r < 256 / (BM / 4); ++r) {
+                const float4 v = red[tid + r * (BM / 4)];
+                s4.x += v.x; s4.y += v.y; s4.z += v.z; s4.w += v.w;
+            }
+            float* dst = a.bias_slab + (long long)split * d.M + m0 + 4 * tid;
+            const float sv[4] = {s4.x, s4.y, s4.z, s4.w};
+            for (int c = 0; c < 4; ++c)
+                if (m0 + 4 * tid + c < d.M) dst[c] = sv[c];
+        }
+    }
+    const int lr = lane & 31;
+    const long long MN = (long long)d.M * d.N;
+    static_for<NT>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        const int n = n0 + wn * 32 + lr;
+        if (n < d.N) {
+            float* out = a.slab + ((long long)split * d.ntaps + t0 + j) * MN + n;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                if (m < d.M) out[(long long)m * d.N] = acc[j][r];
+            }
+        }
+    });
+}
+
+// ------------------------------------------------------------------------------------------------
 // Thin-operand weight gradient: dW[t][m][n] = sum_q P[q][m] * Q[shift_t(q)][n] with N <= 4 (the 3-channel
 // image side: refine conv 3->64 / 64->3 at 256^2 (the latter through the swapped descriptor), g_a's 5x5 s2
 // conv 3->128, g_s's deconv 128->3) and M = 64*MW wide channels. An MFMA tile would be >90 % padding and
@@ -2603,7 +2753,8 @@ struct WgradPlan {
 // *dil = the tap spacing.
 static bool halo_ok(const hyres_wgrad_desc* d, int* K, int* dil) {
     static const int on = env_int("HYRES_WGRAD_HALO", 1);
-    if (!on || d->f16_operands || d->square_q || (d->sq != 1 && d->sq != 2)) return false;
+    static const int f16_on = env_int("HYRES_WGRAD_HALO_F16", 1);  // AMP: wgrad_halo_f16_kernel
+    if (!on || (d->f16_operands && !f16_on) || d->square_q || (d->sq != 1 && d->sq != 2)) return false;
     if (d->Wq % 32 != 0 || d->M < 32 || d->N < 32 || d->M % 4 || d->N % 4 || d->ldp % 4 || d->ldq % 4) return false;
     const int k = d->ntaps == 9 ? 3 : d->ntaps == 25 ? 5 : 0;
     if (!k || (d->sq == 2 && k != 5)) return false;  // stride 2 only for the 5x5 (de)convs (3x3 s2: 123 KB LDS)
@@ -2622,7 +2773,9 @@ static bool wgrad_f16_ok(const hyres_wgrad_desc* d);
 static WgradPlan wgrad_plan(const hyres_wgrad_desc* d) {
     WgradPlan p{};
     p.NT = 1;
-    const int kt = wgrad_f16_ok(d) ? KTH : KT;
+    int hk = 0, hdil = 1;
+    const bool halo = halo_ok(d, &hk, &hdil);  // fp32 or (AMP) f16 halo kernel: 32-pixel chunks either way
+    const int kt = (wgrad_f16_ok(d) && !halo) ? KTH : KT;
     p.tapn = (d->N <= 16 && d->ntaps > 1 && !d->square_q) ? 1 : 0;
     const int ncols = p.tapn ? d->ntaps * d->N : d->N;
     if (p.tapn) {
@@ -2643,8 +2796,10 @@ static WgradPlan wgrad_plan(const hyres_wgrad_desc* d) {
     p.mtiles = ceil_div(d->M, p.BM); p.ntiles = ceil_div(ncols, p.BN);
     p.ngroups = p.tapn ? 1 : ceil_div(d->ntaps, p.NT);
     p.nchunks = ceil_div((long long)d->B * d->Hq * d->Wq, kt);
-    if (kt == KT && halo_ok(d, &p.hk, &p.hdil)) {
+    if (halo) {
         p.halo = 1;
+        p.hk = hk;
+        p.hdil = hdil;
         p.hdh = d->dh[0];
         p.hdw = d->dw[0];
         p.tapn = 0;
@@ -2847,6 +3002,12 @@ int hyres_conv_wgrad(const hyres_wgrad_desc* d0, const float* pp, const float* q
         else hipLaunchKernelGGL((wgrad1x1_kernel<1, 1, 2, 2>), grid, dim3(256), 0, st, a);
     } else if (thin) {
         launch_thin(a, tp, st);
+    } else if (p.halo && wgrad_f16_ok(d)) {
+        if (p.hk == 3 && p.hdil == 2)
+            hipLaunchKernelGGL((wgrad_halo_f16_kernel<3, 3, 1, 2>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
+        else if (p.hk == 3) hipLaunchKernelGGL((wgrad_halo_f16_kernel<3, 3, 1>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
+        else if (d->sq == 1) hipLaunchKernelGGL((wgrad_halo_f16_kernel<1, 5, 1>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
+        else hipLaunchKernelGGL((wgrad_halo_f16_kernel<1, 5, 2>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
     } else if (p.halo) {
         if (p.hk == 3 && p.hdil == 2)
             hipLaunchKernelGGL((wgrad_halo_kernel<3, 3, 1, 2>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);

@@ -21,6 +21,8 @@ def main():
     ap.add_argument("--Ci", type=int, default=64)
     ap.add_argument("--Co", type=int, default=128)
     ap.add_argument("--K", type=int, default=1)
+    ap.add_argument("--dil", type=int, default=1)
+    ap.add_argument("--f16", action="store_true", help="AMP: fp16 operands (f16 MFMA)")
     ap.add_argument("--iters", type=int, default=30)
     a = ap.parse_args()
     from hyres_hip import _lib as L
@@ -30,7 +32,8 @@ def main():
     dw = torch.zeros(a.Co, a.Ci, a.K, a.K, device=dev)
     db = torch.zeros(a.Co, device=dev)
     d = L.WgradDesc()
-    L.call("hyres_wgrad_desc_conv2d", ctypes.byref(d), a.B, a.H, a.H, a.Ci, a.Ci, a.Co, a.Co, a.K, a.K, 1, a.K // 2, 1)
+    L.call("hyres_wgrad_desc_conv2d", ctypes.byref(d), a.B, a.H, a.H, a.Ci, a.Ci, a.Co, a.Co, a.K, a.K, 1, a.dil * (a.K // 2), a.dil)
+    d.f16_operands = int(a.f16)
     d.sm = a.Ci * a.K * a.K
     nb = L.load().hyres_wgrad_workspace_bytes(ctypes.byref(d))
     ws = torch.empty(nb // 4 + 16, device=dev)
@@ -50,7 +53,7 @@ def main():
         us = 1000 * e0.elapsed_time(e1) / a.iters
         flops = 2.0 * a.B * a.H * a.H * a.K * a.K * a.Ci * a.Co
         byts = 4.0 * a.B * a.H * a.H * (a.Ci + a.Co)
-        print(f"wgrad B{a.B} {a.H}^2 {a.Ci}->{a.Co} K{a.K} bias={int(bias)}: {us:.1f} us, {flops / us / 1e6:.1f} TFLOP/s, "
+        print(f"wgrad{' f16' if a.f16 else ''} B{a.B} {a.H}^2 {a.Ci}->{a.Co} K{a.K} d{a.dil} bias={int(bias)}: {us:.1f} us, {flops / us / 1e6:.1f} TFLOP/s, "
               f"{byts / us / 1e3:.0f} GB/s")
 
 

@@ -1227,7 +1227,10 @@ def test_compress_bitstream_matches_oracle():
 AMP_CASES = [(2, 64, 64, 16, 16, 3, 1, 1, 1), (2, 128, 192, 16, 16, 5, 2, 2, 1), (2, 192, 96, 8, 8, 1, 1, 0, 1),
              (2, 64, 64, 16, 16, 3, 1, 2, 2), (2, 128, 128, 32, 32, 1, 1, 0, 1), (2, 192, 384, 8, 8, 5, 1, 2, 1),
              # odd spatial sizes, Co a multiple of 32 but not of 64 (partial N tiles in fwd and dgrad)
-             (2, 96, 96, 20, 20, 3, 1, 1, 1), (3, 64, 96, 36, 12, 3, 1, 1, 1), (1, 128, 128, 48, 40, 3, 1, 2, 2)]
+             (2, 96, 96, 20, 20, 3, 1, 1, 1), (3, 64, 96, 36, 12, 3, 1, 1, 1), (1, 128, 128, 48, 40, 3, 1, 2, 2),
+             # rows a multiple of 32 pixels: the f16 halo-staged weight gradient (3x3, dilated 3x3, 5x5 s2;
+             # Co = 96: a partial second M tile)
+             (2, 64, 64, 32, 32, 3, 1, 1, 1), (2, 64, 96, 32, 64, 3, 1, 2, 2), (2, 64, 96, 64, 64, 5, 2, 2, 1)]
 
 
 @pytest.mark.parametrize("case", AMP_CASES)
@@ -1264,10 +1267,12 @@ def test_conv2d_amp_fwd_bwd(case):
     assert rel_err(bd.grad.cpu(), gy.sum((0, 2, 3))) < 1e-5
 
 
-def test_deconv2d_amp_fwd_bwd():
-    """Transposed conv (compressai deconv, 4 sub-pixel phases) under autocast: f16 forward, dgrad, wgrad."""
+@pytest.mark.parametrize("hw", [8, 32])
+def test_deconv2d_amp_fwd_bwd(hw):
+    """Transposed conv (compressai deconv, 4 sub-pixel phases) under autocast: f16 forward, dgrad, wgrad
+    (hw = 32: rows of 32 pixels, the f16 halo-staged weight gradient)."""
     from hyres_hip import ops as O
-    B, Ci, Co, H, W = 2, 128, 128, 8, 8
+    B, Ci, Co, H, W = 2, 128, 128, hw, hw
     x = _rand((B, Ci, H, W), 45)
     w = _rand((Ci, Co, 5, 5), 46, 1.0 / (Ci * 25 / 4) ** 0.5)
     b = _rand((Co,), 47, 0.1)
