@@ -1349,12 +1349,18 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo_kernel(const WgradArgs a, i
                        : make_float4(0.f, 0.f, 0.f, 0.f);
         }
     };
+    // bias gradient = column sums of P, accumulated from the staging registers (this thread's channel
+    // quad (tid % 16) * 4 is fixed) and reduced once at the end: a per-chunk LDS column pass in one wave
+    // held every barrier back by that wave's extra work (256^2 3x3: 676 vs 617 us without bias)
+    const bool do_bias = a.bias_slab != nullptr && nt == 0 && grp == 0;
+    float4 bsum = make_float4(0.f, 0.f, 0.f, 0.f);
     auto store = [&](int buf) {
         float* Ps = smem + buf * (PSZ + HSZ);
         float* Hs = Ps + PSZ;
 #pragma unroll
         for (int q = 0; q < P_V; ++q) {
             const int e = tid + 256 * q;
+            if (do_bias) { bsum.x += rp[q].x; bsum.y += rp[q].y; bsum.z += rp[q].z; bsum.w += rp[q].w; }
             *reinterpret_cast<float4*>(&Ps[(e / (BM / 4)) * PP + (e % (BM / 4)) * 4]) = rp[q];
         }
 #pragma unroll
@@ -1372,8 +1378,6 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo_kernel(const WgradArgs a, i
     for (int j = 0; j < NT; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
-    const bool do_bias = a.bias_slab != nullptr && nt == 0 && grp == 0;
-    float bsum = 0.f;
     const int kb = split * a.chunks_per_split;
     const int ke = min(a.nchunks, kb + a.chunks_per_split);
     if (kb < ke) {
@@ -1386,10 +1390,6 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo_kernel(const WgradArgs a, i
         if (kc + 1 < ke) load(kc + 1);  // next chunk in flight during this chunk's NT x 16 MFMAs
         const float* Ps = smem + cur * (PSZ + HSZ);
         const float* Hs = Ps + PSZ;
-        if (do_bias && tid < BM) {
-#pragma unroll 8
-            for (int k = 0; k < KT; ++k) bsum += Ps[k * PP + tid];
-        }
         static_for<NT>([&](auto J) {
             constexpr int t = decltype(J)::value;
             constexpr int hr = t / KW, hc = t % KW;
@@ -1405,7 +1405,22 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo_kernel(const WgradArgs a, i
         __syncthreads();
         cur ^= 1;
     }
-    if (do_bias && tid < BM && m0 + tid < d.M) a.bias_slab[(long long)split * d.M + m0 + tid] = bsum;
+    if (do_bias) {
+        float4* red = reinterpret_cast<float4*>(smem);  // the loop ended with a barrier
+        red[tid] = bsum;
+        __syncthreads();
+        if (tid < BM / 4) {
+            float4 s4 = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int r = 0; r < 256 / (BM / 4); ++r) {
+                const float4 v = red[tid + r * (BM / 4)];
+                s4.x += v.x; s4.y += v.y; s4.z += v.z; s4.w += v.w;
+            }
+            float* dst = a.bias_slab + (long long)split * d.M + m0 + 4 * tid;
+            const float sv[4] = {s4.x, s4.y, s4.z, s4.w};
+            for (int c = 0; c < 4; ++c)
+                if (m0 + 4 * tid + c < d.M) dst[c] = sv[c];
+        }
+    }
     const long long MN = (long long)d.M * d.N;
     static_for<NT>([&](auto J) {
         constexpr int j = decltype(J)::value;

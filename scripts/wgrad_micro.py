@@ -37,7 +37,7 @@ def main():
     d.sm = a.Ci * a.K * a.K
     nb = L.load().hyres_wgrad_workspace_bytes(ctypes.byref(d))
     ws = torch.empty(nb // 4 + 16, device=dev)
-    for bias in (True, False):
+    for bias in (False, True):
         def run():
             L.call("hyres_conv_wgrad", ctypes.byref(d), gy.data_ptr(), x.data_ptr(), dw.data_ptr(),
                    db.data_ptr() if bias else None, ws.data_ptr(), nb, L.stream())
