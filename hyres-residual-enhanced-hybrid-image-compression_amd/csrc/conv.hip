@@ -1456,7 +1456,8 @@ __device__ __forceinline__ halfx4_t lds_tr4(const _Float16* p) {
     return __builtin_bit_cast(halfx4_t, v);
 }
 
-template <int TM, int TN, int WAVES_M, int WAVES_N, int NT, bool SQ>
+// ONE: a 1x1 stride-1 gradient on the base grid (Q row = P row): Q rows load like P rows, no pixel decode
+template <int TM, int TN, int WAVES_M, int WAVES_N, int NT, bool SQ, bool ONE = false>
 __global__ __launch_bounds__(256) void wgrad_f16_kernel(const WgradArgs a) {
     constexpr int BM = 32 * TM * WAVES_M;
     constexpr int BN = 32 * TN * WAVES_N;
@@ -1487,6 +1488,7 @@ __global__ __launch_bounds__(256) void wgrad_f16_kernel(const WgradArgs a) {
     constexpr int PRS = 256 / (BM / 4), QRS = 256 / (BN / 4);
     int q_b[Q_V], q_i[Q_V], q_j[Q_V];
     auto decode_rows = [&](int kc) {
+        if constexpr (ONE) return;
 #pragma unroll
         for (int i = 0; i < Q_V; ++i) {
             const long long qq = (long long)kc * KTH + qrow0 + i * QRS;
@@ -1501,6 +1503,7 @@ __global__ __launch_bounds__(256) void wgrad_f16_kernel(const WgradArgs a) {
         }
     };
     auto step_rows = [&]() {
+        if constexpr (ONE) return;
 #pragma unroll
         for (int i = 0; i < Q_V; ++i) {
             if (q_b[i] < 0) continue;
@@ -1522,7 +1525,17 @@ __global__ __launch_bounds__(256) void wgrad_f16_kernel(const WgradArgs a) {
             rp[i] = v;
         }
     };
+    int cur_kc = 0;  // ONE: the chunk load_q fetches (Q rows = P rows)
     auto load_q = [&](int t) {
+        if constexpr (ONE) {
+            const long long k0 = (long long)cur_kc * KTH;
+#pragma unroll
+            for (int i = 0; i < Q_V; ++i) {
+                const long long qq = k0 + qrow0 + i * QRS;
+                rq[i] = (qq < Qtot && n0 + qc < d.N) ? ld4(a.q + qq * d.ldq + n0 + qc) : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+            return;
+        }
 #pragma unroll
         for (int i = 0; i < Q_V; ++i) {
             float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1572,6 +1585,7 @@ __global__ __launch_bounds__(256) void wgrad_f16_kernel(const WgradArgs a) {
     if (kc_begin < kc_end) {
         decode_rows(kc_begin);
         load_p(kc_begin);
+        cur_kc = kc_begin;
         load_q(t0);
         store_p(Psm);
         store_q(Qsm);
@@ -1590,6 +1604,7 @@ __global__ __launch_bounds__(256) void wgrad_f16_kernel(const WgradArgs a) {
             } else if (next_chunk) {
                 step_rows();
                 load_p(kc + 1);
+                cur_kc = kc + 1;
                 load_q(t0);
             }
 #pragma unroll
@@ -3030,10 +3045,15 @@ int hyres_conv_wgrad(const hyres_wgrad_desc* d0, const float* pp, const float* q
         else if (d->sq == 1) hipLaunchKernelGGL((wgrad_halo_kernel<1, 5, 1>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
         else hipLaunchKernelGGL((wgrad_halo_kernel<1, 5, 2>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
     } else if (wgrad_f16_ok(d)) {
+        static const int f16_one = env_int("HYRES_WGRAD_F16_1X1", 1);
+        const bool one16 = f16_one && !sqr && d->ntaps == 1 && d->dh[0] == 0 && d->dw[0] == 0 && d->sq == 1 &&
+                           d->Hqq == d->Hq && d->Wqq == d->Wq && p.ngroups == 1;
         auto f16 = [&](auto tm, auto tn, auto wm_, auto wn_, auto ntc) {
             constexpr int TM_ = decltype(tm)::value, TN_ = decltype(tn)::value;
             constexpr int WM2 = decltype(wm_)::value, WN2 = decltype(wn_)::value, NT_ = decltype(ntc)::value;
             if (sqr) hipLaunchKernelGGL((wgrad_f16_kernel<TM_, TN_, WM2, WN2, NT_, true>), grid, dim3(256), 0, st, a);
+            else if (NT_ == 1 && one16)
+                hipLaunchKernelGGL((wgrad_f16_kernel<TM_, TN_, WM2, WN2, 1, false, true>), grid, dim3(256), 0, st, a);
             else hipLaunchKernelGGL((wgrad_f16_kernel<TM_, TN_, WM2, WN2, NT_, false>), grid, dim3(256), 0, st, a);
         };
         using I1 = std::integral_constant<int, 1>;
