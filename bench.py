@@ -97,7 +97,7 @@ def cpu_baseline(args, budget_s):
                       f"itself cannot run here (compressai absent)"}
 
 
-PMC_TRAFFIC = os.path.join(REPO, "profiles", "r2_v4_pmc_traffic.json")  # scripts/profile_round.sh r2_v4
+PMC_TRAFFIC = os.path.join(REPO, "profiles", "r2_v5_pmc_traffic.json")  # scripts/profile_round.sh r2_v5
 EAGER_TIMED = 3  # eager steps behind the live per-launch roofline timing
 
 
