@@ -101,6 +101,18 @@ PMC_TRAFFIC = os.path.join(REPO, "profiles", "r2_v5_pmc_traffic.json")  # script
 EAGER_TIMED = 3  # eager steps behind the live per-launch roofline timing
 
 
+def kernel_label(kernel):
+    """What the dominant kernel is: the VALU narrow-output kernel (Co <= 4) and the streaming 1x1 kernel are
+    not the implicit-GEMM tile kernel."""
+    if kernel.startswith("conv_narrow"):
+        return "narrow-output conv (Co <= 4), fp32 VALU FMA — not MFMA; priced against the MFMA peak as an upper bound"
+    if kernel.startswith("conv1x1_stream"):
+        return "streaming 1x1 conv, fp32 MFMA, weights resident in LDS"
+    if "true>" in kernel.replace(" ", "").split(",")[-1]:
+        return "implicit-GEMM conv, f16 MFMA, fused epilogue"
+    return "implicit-GEMM conv, fp32 MFMA, fused epilogue"
+
+
 def traffic_bytes_per_launch(kernel):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC passes of this same
     command (scripts/pmc_traffic.py: 2 x FETCH_SIZE + WRITE_SIZE, separate passes, gfx950 FETCH_SIZE
@@ -393,8 +405,13 @@ def main():
     # xGMI). HYRES_DIST_OVERLAP=1 (or --no-graph) selects the eager overlapped path.
     dist_mode = None
     if dist:
+        # default "graph+overlap": the captured step records an external event at each backward-progress
+        # marker and each gradient segment's RCCL all-reduce starts on a communication stream as soon as
+        # its event fires inside the replay (hyres_hip.graphs / ddp.FlatGradReducer.reduce_graphed);
+        # HYRES_DIST_MODE=graph+allreduce reduces after the replay; eager-overlap = the eager step
         overlap = args.no_graph or os.environ.get("HYRES_DIST_OVERLAP") == "1"
-        dist_mode = "eager-overlap" if overlap else "graph+allreduce"
+        dist_mode = "eager-overlap" if overlap else os.environ.get("HYRES_DIST_MODE", "graph+overlap")
+        assert dist_mode in ("eager-overlap", "graph+overlap", "graph+allreduce"), dist_mode
     if dist:
         # RCCL all-reduce of refine / g_s / hyperprior gradient segments launched from backward-progress
         # markers (overlapped with the rest of backward), the remainder (g_a) after backward
@@ -419,7 +436,8 @@ def main():
         # the RCCL all-reduce and the aux step stay eager (a handful of launches)
         from hyres_hip.graphs import CapturedStep
         graphed = CapturedStep(net, x, jpeg, jpeg_bpp, noisequant=False, criterion=crit, zero_grad=opt.zero_grad,
-                               capture_error_mode="thread_local" if dist else "global")
+                               capture_error_mode="thread_local" if dist else "global",
+                               reducer=reducer if dist_mode == "graph+overlap" else None)
 
     def fwd_bwd(eager=False):
         if graphed is not None and not eager:
@@ -432,7 +450,10 @@ def main():
     def step(eager=False):
         c = fwd_bwd(eager)
         if reducer is not None:
-            reducer.all_reduce()
+            if graphed is not None and not eager:
+                reducer.reduce_graphed(graphed.marker_events)  # empty list -> after-replay buckets
+            else:
+                reducer.all_reduce()
         opt.step()
         opt.zero_grad()
         aux = net.aux_loss()
@@ -556,7 +577,7 @@ def main():
         "config": {"workload": "C2 train step (configs[1]): ResidualJPEGCompression N=128 M=192, fwd+bwd+"
                                "optimizer, lambda=0.045, noisequant=False, JPEG q50 precomputed on host",
                    "global_batch": B * world, "image": [S, S], "parallelism": f"dp{world}"},
-        "roofline": {"bound": "mfma", "kernel": f"{ks['kernel']} (implicit-GEMM conv, fp32 MFMA, fused epilogue)",
+        "roofline": {"bound": "mfma", "kernel": f"{ks['kernel']} ({kernel_label(ks['kernel'])})",
                      "achieved": round(achieved, 3), "peak": MI355X_FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved / MI355X_FP32_PEAK_TFLOPS, 4),
                      "traffic": traffic_bytes_per_launch(ks["kernel"]),

@@ -313,12 +313,36 @@ __global__ void sum_sqdiff_kernel(const float* a, const float* b, long long n, f
     float r = block_sum(s, red);
     if (threadIdx.x == 0) part[blockIdx.x] = r;
 }
-__global__ void sumsq_kernel(const float* x, long long n, float* part) {
-    __shared__ float red[256];
-    float s = 0.f;
-    GRID_STRIDE(i, n) s += x[i] * x[i];
-    float r = block_sum(s, red);
-    if (threadIdx.x == 0) part[blockIdx.x] = r;
+// Sum of squares for clip_grad_norm_ and GradScaler's found_inf, accumulated AND returned in fp64: a large
+// but finite gradient never overflows the sum (torch's found_inf is an element-wise !isfinite test, and its
+// clip norm is taken on the unscaled gradient), so the result is +inf only when an element is +-inf and NaN
+// only when an element is NaN.
+__global__ void sumsq_kernel(const float* x, long long n, double* part) {
+    __shared__ double red[256];
+    double s = 0.0;
+    GRID_STRIDE(i, n) {
+        const double v = (double)x[i];
+        s += v * v;
+    }
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int k = 128; k > 0; k >>= 1) {
+        if (threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+__global__ void sumsq_final_kernel(const double* part, int nb, double* out) {
+    __shared__ double red[256];
+    double s = 0.0;
+    for (int i = threadIdx.x; i < nb; i += 256) s += part[i];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int k = 128; k > 0; k >>= 1) {
+        if (threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[0] = red[0];
 }
 __global__ void scale_recip_kernel(const float* x, const float* coef, float scale, float* g, long long n) {
     const float c = coef[0] * scale;
@@ -379,14 +403,14 @@ struct AdamHyper {
 };
 
 // skip: 0 never; 1 when sumsq is not finite (GradScaler found_inf); 2 when sumsq is NaN
-__device__ __forceinline__ bool adam_skip(const float* sumsq, int skip) {
+__device__ __forceinline__ bool adam_skip(const double* sumsq, int skip) {
     if (!skip || !sumsq) return false;
-    const float v = sumsq[0];
+    const double v = sumsq[0];
     return skip == 1 ? !isfinite(v) : isnan(v);
 }
 
 __global__ void adam_kernel(float* p, const float* g, float* m, float* v, long long n, AdamHyper h,
-                            const float* step_dev, const float* sumsq, const float* gscale, int skip) {
+                            const float* step_dev, const double* sumsq, const float* gscale, int skip) {
     if (adam_skip(sumsq, skip)) return;
     const double t = (double)step_dev[0] + 1.0;
     const double bc1 = 1.0 - pow(h.beta1, t);
@@ -397,7 +421,7 @@ __global__ void adam_kernel(float* p, const float* g, float* m, float* v, long l
     float clip = 1.0f;
     if (sumsq && h.max_norm > 0.0) {
         // clip_grad_norm_ on the unscaled gradient: total = ||g * gs|| = sqrt(sumsq) * gs
-        const float total = sqrtf(sumsq[0]) * gs;
+        const float total = (float)(sqrt(sumsq[0]) * (double)gs);
         const float coef = (float)h.max_norm / (total + 1e-6f);
         clip = fminf(coef, 1.0f);
     }
@@ -415,12 +439,13 @@ __global__ void adam_kernel(float* p, const float* g, float* m, float* v, long l
     }
 }
 
-__global__ void adam_finish_kernel(float* step_dev, const float* sumsq, int skip) {
+__global__ void adam_finish_kernel(float* step_dev, const double* sumsq, int skip) {
     if (threadIdx.x == 0 && !adam_skip(sumsq, skip)) step_dev[0] = step_dev[0] + 1.0f;
 }
 
-// torch.amp.GradScaler.update (aten _amp_update_scale_): found_inf = !isfinite(sumsq of the scaled grads)
-__global__ void grad_scaler_update_kernel(const float* sumsq, float* scale, float* inv_scale, int* tracker,
+// torch.amp.GradScaler.update (aten _amp_update_scale_): found_inf = !isfinite(sumsq of the scaled grads), which
+// is exactly "some element is inf/NaN" because hyres_sumsq accumulates in fp64 (no overflow of finite sums)
+__global__ void grad_scaler_update_kernel(const double* sumsq, float* scale, float* inv_scale, int* tracker,
                                           float growth, float backoff, int interval) {
     if (threadIdx.x != 0) return;
     const bool found_inf = !isfinite(sumsq[0]);
@@ -450,6 +475,38 @@ extern "C" {
 
 int hyres_version(void) { return 10000; }
 const char* hyres_last_error_string(void) { return g_err.c_str(); }
+
+int hyres_event_create(void** ev) {
+    HY_REQUIRE(ev, HYRES_E_ARG, "event_create: NULL");
+    hipEvent_t e = nullptr;
+    hipError_t err = hipEventCreateWithFlags(&e, hipEventDisableTiming);
+    HY_REQUIRE(err == hipSuccess, (int)err, "hipEventCreateWithFlags: %s", hipGetErrorString(err));
+    *ev = (void*)e;
+    return 0;
+}
+int hyres_event_destroy(void* ev) {
+    HY_REQUIRE(ev, HYRES_E_ARG, "event_destroy: NULL");
+    hipError_t err = hipEventDestroy((hipEvent_t)ev);
+    HY_REQUIRE(err == hipSuccess, (int)err, "hipEventDestroy: %s", hipGetErrorString(err));
+    return 0;
+}
+int hyres_event_record_external(void* ev, hyres_stream_t s) {
+    HY_REQUIRE(ev, HYRES_E_ARG, "event_record_external: NULL");
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    hipError_t err = hipStreamIsCapturing(as_stream(s), &st);
+    HY_REQUIRE(err == hipSuccess, (int)err, "hipStreamIsCapturing: %s", hipGetErrorString(err));
+    err = st == hipStreamCaptureStatusActive
+              ? hipEventRecordWithFlags((hipEvent_t)ev, as_stream(s), hipEventRecordExternal)
+              : hipEventRecord((hipEvent_t)ev, as_stream(s));
+    HY_REQUIRE(err == hipSuccess, (int)err, "hipEventRecordWithFlags(external): %s", hipGetErrorString(err));
+    return 0;
+}
+int hyres_stream_wait_event(hyres_stream_t s, void* ev) {
+    HY_REQUIRE(ev, HYRES_E_ARG, "stream_wait_event: NULL");
+    hipError_t err = hipStreamWaitEvent(as_stream(s), (hipEvent_t)ev, 0);
+    HY_REQUIRE(err == hipSuccess, (int)err, "hipStreamWaitEvent: %s", hipGetErrorString(err));
+    return 0;
+}
 
 int hyres_nchw_to_nhwc(const float* x, float* y, int B, int C, int H, int W, int ldy, hyres_stream_t s) {
     HY_REQUIRE(x && y && ldy >= C, HYRES_E_ARG, "nchw_to_nhwc: bad args");
@@ -497,7 +554,7 @@ int hyres_relu_bwd_2d(const float* y, int ldy, const float* g, int ldg, float* g
                        ldgx, P, C);
     return HY_LAUNCH_CHECK("relu_bwd_2d");
 }
-long long hyres_reduce_workspace_bytes(long long n) { return (long long)grid_for(n, 4) * 4 + 256; }
+long long hyres_reduce_workspace_bytes(long long n) { return (long long)grid_for(n, 4) * 8 + 256; }  // fp64 partials
 
 int hyres_prelu_bwd(const float* x, int ldx, const float* g, int ldg, float* gx, int ldgx, long long P, int C,
                     const float* slope, float* dslope, void* ws, long long ws_bytes, hyres_stream_t s) {
@@ -613,9 +670,15 @@ int hyres_sum_log(const float* x, long long n, float* out, void* ws, long long w
     HY_REQUIRE(x && out, HYRES_E_ARG, "sum_log: NULL");
     return reduce2(sum_log_kernel, x, n, out, ws, ws_bytes, s, "sum_log");
 }
-int hyres_sumsq(const float* x, long long n, float* out, void* ws, long long ws_bytes, hyres_stream_t s) {
+int hyres_sumsq(const float* x, long long n, double* out, void* ws, long long ws_bytes, hyres_stream_t s) {
     HY_REQUIRE(x && out, HYRES_E_ARG, "sumsq: NULL");
-    return reduce2(sumsq_kernel, x, n, out, ws, ws_bytes, s, "sumsq");
+    int nb = grid_for(n, 4);
+    HY_REQUIRE(ws && ws_bytes >= (long long)nb * 8, HYRES_E_WORKSPACE, "sumsq: workspace");
+    hipLaunchKernelGGL(sumsq_kernel, dim3(nb), dim3(256), 0, as_stream(s), x, n, (double*)ws);
+    int rc = HY_LAUNCH_CHECK("sumsq");
+    if (rc) return rc;
+    hipLaunchKernelGGL(sumsq_final_kernel, dim3(1), dim3(256), 0, as_stream(s), (const double*)ws, nb, out);
+    return HY_LAUNCH_CHECK("sumsq");
 }
 int hyres_sum_sqdiff(const float* a, const float* b, long long n, float* out, void* ws, long long ws_bytes,
                      hyres_stream_t s) {
@@ -665,7 +728,7 @@ int hyres_rd_bwd_coef(const float* g0, const float* g1, const float* g2, const f
     return HY_LAUNCH_CHECK("rd_bwd_coef");
 }
 int hyres_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, long long n, double lr,
-                    double beta1, double beta2, double eps, float* step_dev, const float* sumsq, double max_norm,
+                    double beta1, double beta2, double eps, float* step_dev, const double* sumsq, double max_norm,
                     const float* gscale, int skip, hyres_stream_t s) {
     HY_REQUIRE(param && grad && exp_avg && exp_avg_sq && step_dev, HYRES_E_ARG, "adam: NULL");
     HY_REQUIRE(skip >= 0 && skip <= 2 && (skip == 0 || sumsq), HYRES_E_ARG, "adam: skip mode %d needs sumsq", skip);
@@ -685,7 +748,7 @@ int hyres_adam_step(float* param, const float* grad, float* exp_avg, float* exp_
     hipLaunchKernelGGL(adam_finish_kernel, dim3(1), dim3(64), 0, as_stream(s), step_dev, sumsq, skip);
     return HY_LAUNCH_CHECK("adam_finish");
 }
-int hyres_grad_scaler_update(const float* sumsq, float* scale, float* inv_scale, int* growth_tracker,
+int hyres_grad_scaler_update(const double* sumsq, float* scale, float* inv_scale, int* growth_tracker,
                              double growth_factor, double backoff_factor, int growth_interval, hyres_stream_t s) {
     HY_REQUIRE(sumsq && scale && inv_scale && growth_tracker && growth_interval > 0, HYRES_E_ARG,
                "grad_scaler_update: bad args");

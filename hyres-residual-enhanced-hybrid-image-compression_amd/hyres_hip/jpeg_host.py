@@ -25,13 +25,27 @@ def _noop(i):
     return i
 
 
+def default_procs(world: Optional[int] = None) -> int:
+    """Worker processes per rank: HYRES_JPEG_PROCS, else min(8, cpus // world) so that the ranks of one node
+    share the host cores instead of each starting 8 workers (64 processes at 8 ranks)."""
+    if "HYRES_JPEG_PROCS" in os.environ:
+        return int(os.environ["HYRES_JPEG_PROCS"])
+    if world is None:
+        world = int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1")))
+    try:
+        cpus = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        cpus = os.cpu_count() or 1
+    return max(0, min(8, cpus // max(world, 1)))
+
+
 def start(procs: Optional[int] = None) -> int:
-    """Start ``procs`` JPEG worker processes (default HYRES_JPEG_PROCS or min(8, cpus)); 0 disables."""
+    """Start ``procs`` JPEG worker processes (default ``default_procs()``); 0 or 1 disables."""
     global _POOL, _PROCS
     if _POOL is not None:
         return _PROCS
     if procs is None:
-        procs = int(os.environ.get("HYRES_JPEG_PROCS", min(8, os.cpu_count() or 1)))
+        procs = default_procs()
     if procs <= 1:
         return 0
     _POOL = ProcessPoolExecutor(max_workers=procs, mp_context=mp.get_context("spawn"))

@@ -87,7 +87,9 @@ class FusedAdam(torch.optim.Optimizer):
         self.exp_avg = _device_buffer(self.flat.numel, dev)
         self.exp_avg_sq = _device_buffer(self.flat.numel, dev)
         self.step_dev = _device_buffer(1, dev)  # completed steps (float, as torch's Adam ``step`` tensor)
-        self.sumsq = torch.zeros(1, dtype=torch.float32, device=dev)  # sum g^2 of the last step's gradient
+        # sum g^2 of the last step's gradient, fp64 (hyres_sumsq: no overflow of a finite sum, so a non-finite
+        # value means a non-finite element, as torch's element-wise found_inf)
+        self.sumsq = torch.zeros(1, dtype=torch.float64, device=dev)
 
     def compute_sumsq(self) -> torch.Tensor:
         """sum of squares of the flat gradient into ``self.sumsq`` (device; no sync)."""
@@ -117,6 +119,7 @@ class FusedAdam(torch.optim.Optimizer):
         elif skip_if_nan is not None:
             # the kernel reads one sum of squares for both clipping and the skip test
             assert self.max_grad_norm == 0, "skip_if_nan is for the unclipped aux optimiser"
+            assert skip_if_nan.dtype == torch.float64 and skip_if_nan.is_cuda, "skip_if_nan: a FusedAdam.sumsq"
             sumsq, skip = skip_if_nan.data_ptr(), 2
         L.call("hyres_adam_step", self.flat.data.data_ptr(), self.flat.grad.data_ptr(), self.exp_avg.data_ptr(),
                self.exp_avg_sq.data_ptr(), self.flat.numel, float(g["lr"]), float(b1), float(b2), float(g["eps"]),
@@ -132,7 +135,7 @@ class FusedAdam(torch.optim.Optimizer):
 
     def grad_norm(self) -> torch.Tensor:
         """||g||_2 (device scalar) of the flat gradient (what clip_grad_norm_ returns)."""
-        return self.compute_sumsq().clone().sqrt()
+        return self.compute_sumsq().sqrt().float()
 
     # ------------------------------------------------------------------ checkpoints (torch.optim.Adam layout)
     def state_dict(self):

@@ -17,6 +17,8 @@ from __future__ import annotations
 
 import io
 import os
+import weakref
+from collections import OrderedDict
 from concurrent.futures import ThreadPoolExecutor
 from typing import List, Optional
 
@@ -57,13 +59,6 @@ class _PillowTurbo:
         return np.asarray(im)[..., ::-1]
 
 
-class _Prefetched:
-    __slots__ = ("key", "future")
-
-    def __init__(self, key, future):
-        self.key, self.future = key, future
-
-
 class TurboJPEGCompression(nn.Module):
     """Host JPEG stage.  Each image's encode -> decode round trip is ONE task on a thread pool (libjpeg-turbo
     releases the GIL); ``prefetch(x)`` starts the next batch's round trip in the background so a training
@@ -82,7 +77,12 @@ class TurboJPEGCompression(nn.Module):
         self.workers = workers or int(os.environ.get("HYRES_JPEG_WORKERS", min(16, os.cpu_count() or 1)))
         self._pool: Optional[ThreadPoolExecutor] = None
         self._bg: Optional[ThreadPoolExecutor] = None
-        self._pending: Optional[_Prefetched] = None
+        # prefetched round trips keyed by _key(x): a loop that prefetches batch i+1 before it reads batch i
+        # (src/utils/engine.py) keeps both in flight; an entry is popped when its forward uses it
+        self._pending: "OrderedDict[tuple, object]" = OrderedDict()
+        self.max_pending = 4
+        self.prefetch_hits = 0
+        self.prefetch_misses = 0
 
     def _map(self, fn, items):
         if len(items) <= 1 or self.workers <= 1:
@@ -136,25 +136,36 @@ class TurboJPEGCompression(nn.Module):
         return (id(x), x.data_ptr(), x._version, tuple(x.shape))
 
     def prefetch(self, x: torch.Tensor) -> None:
-        """Start ``forward(x)``'s host work for a CPU batch in the background (one batch in flight)."""
+        """Start ``forward(x)``'s host work for a CPU batch in the background.  Up to ``max_pending`` batches
+        stay in flight (oldest dropped first); prefetching a batch that is already pending is a no-op."""
         if x.device.type != "cpu":
+            return
+        key = self._key(x)
+        if key in self._pending:
             return
         if self._bg is None:
             self._bg = ThreadPoolExecutor(max_workers=1, thread_name_prefix="hyres-jpeg-prefetch")
-        self._pending = _Prefetched(self._key(x), self._bg.submit(self._roundtrip, x.detach()))
+        while len(self._pending) >= self.max_pending:
+            _, (_, old) = self._pending.popitem(last=False)
+            old.cancel()
+        # the weak reference guards against a freed batch whose id/address a new tensor reuses
+        self._pending[key] = (weakref.ref(x), self._bg.submit(self._roundtrip, x.detach()))
 
     def forward(self, x: torch.Tensor):
         """(decoded [N,3,H,W] on x.device, jpeg_bpp = total bytes * 8 / (N*H*W))  (:62-77)."""
         device = x.device
-        p = self._pending
-        if p is not None and x.device.type == "cpu" and p.key == self._key(x):
-            self._pending = None
-            decoded, bpp = p.future.result()
+        ent = self._pending.pop(self._key(x), None) if x.device.type == "cpu" else None
+        fut = ent[1] if ent is not None and ent[0]() is x else None
+        if fut is not None:
+            self.prefetch_hits += 1
+            decoded, bpp = fut.result()
         else:
+            self.prefetch_misses += 1
             decoded, bpp = self._roundtrip(x.detach().cpu())
         return decoded.to(device), bpp
 
     def __getstate__(self):
         st = self.__dict__.copy()
-        st["_pool"] = st["_bg"] = st["_pending"] = None
+        st["_pool"] = st["_bg"] = None
+        st["_pending"] = OrderedDict()
         return st

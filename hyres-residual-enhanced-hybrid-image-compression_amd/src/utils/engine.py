@@ -17,8 +17,9 @@ Differences from the reference, by design:
     (TurboJPEGCompression.prefetch), so the host JPEG stage overlaps the device step;
   * forward + RD loss + backward replay as a HIP graph (hyres_hip.graphs.CapturedStep, one capture per
     batch shape / noisequant / precision, taken on an accumulation boundary); the host JPEG stage, the
-    H2D copies, the gradient all-reduce (after the replay, as bench.py's N > 1 default), the optimiser and
-    the aux step stay eager. HYRES_TRAIN_GRAPH=0 runs every step eagerly (the reference's structure).
+    H2D copies, the gradient all-reduce (each segment started from an event the replay records at its
+    backward-progress marker, as bench.py's N > 1 default), the optimiser and the aux step stay eager; a
+    capture failure on any rank makes every rank run eagerly. HYRES_TRAIN_GRAPH=0 runs every step eagerly (the reference's structure).
 """
 import os
 import time
@@ -62,6 +63,7 @@ class _GraphedStep:
         # loss multiplier inside the graph: 1/accumulation (x the GradScaler's device scale under AMP)
         self.ls = torch.full((1,), 1.0 / accumulation, dtype=torch.float32, device=device)
         self.enabled = os.environ.get("HYRES_TRAIN_GRAPH", "1") == "1" and device.type == "cuda"
+        self.last = None
 
     def __call__(self, d, noisequant, boundary_start, reducer):
         """Returns the static loss dict of the replayed step, or None (run this step eagerly)."""
@@ -81,20 +83,41 @@ class _GraphedStep:
             armed = reducer.armed if reducer is not None else None
             if reducer is not None:
                 reducer.armed = False  # no collective inside warm-up or capture
+            err = None
             try:
                 cap = CapturedStep(self.model, x, jd, float(bpp), noisequant=noisequant, criterion=self.criterion,
                                    zero_grad=self.zero_grad, amp=self.amp, loss_scale=self.ls,
-                                   capture_error_mode="thread_local" if reducer is not None else "global")
+                                   capture_error_mode="thread_local" if reducer is not None else "global",
+                                   reducer=reducer)
             except Exception as exc:  # noqa: BLE001 - any capture failure: stay correct, run eagerly
-                print(f"HIP graph capture failed ({exc!r}); training steps run eagerly")
-                self.enabled = False
-                self.zero_grad()
-                return None
+                err = exc
             finally:
                 if reducer is not None:
                     reducer.armed = armed
+            if not _all_ranks_ok(err is None, self.device):
+                # every rank falls back together: a graphed rank and an eager rank would issue different
+                # collectives (segment markers vs buckets) and hang or mix up the all-reduce
+                print(f"HIP graph capture failed ({err!r} on this rank); training steps run eagerly")
+                self.enabled = False
+                self.zero_grad()
+                return None
             self.caps[key] = cap
+        self.last = cap
         return cap.replay(x, jd, float(bpp))[1]
+
+    def reduce(self, reducer):
+        """The boundary all-reduce after a replayed step: each segment's collectives start on the external
+        event the capture recorded at its backward-progress marker (overlapping the rest of the replay)."""
+        reducer.reduce_graphed(self.last.marker_events)
+
+
+def _all_ranks_ok(ok: bool, device) -> bool:
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return ok
+    flag = torch.tensor([1.0 if ok else 0.0], device=device if dist.get_backend() == "nccl" else "cpu")
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    return bool(flag.item() == 1.0)
 
 
 def _lookahead(loader):
@@ -132,6 +155,7 @@ def train_one_epoch(model, criterion, train_dataloader, optimizer, aux_optimizer
         if d_next is not None and hasattr(jpeg, "prefetch"):
             jpeg.prefetch(d_next)  # the next batch's host JPEG overlaps this step's device work
         crit = graphed(d, noisequant, i % gradient_accumulation_steps == 0, reducer)
+        step_graphed = crit is not None
         if crit is not None:
             pending.append(_metrics(crit))
             n_img = len(d)
@@ -154,7 +178,10 @@ def train_one_epoch(model, criterion, train_dataloader, optimizer, aux_optimizer
             del out_net, out_criterion, loss
         if (i + 1) % gradient_accumulation_steps == 0:
             if reducer is not None:
-                reducer.all_reduce()
+                if step_graphed:
+                    graphed.reduce(reducer)
+                else:
+                    reducer.all_reduce()
             nan_src = None
             if not hasattr(optimizer, "max_grad_norm") and clip_max_norm > 0:
                 torch.nn.utils.clip_grad_norm_(model.parameters(), clip_max_norm)

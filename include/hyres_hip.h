@@ -34,6 +34,18 @@ typedef void* hyres_stream_t; /* hipStream_t */
 int hyres_version(void);
 const char* hyres_last_error_string(void);
 
+/* Graph-ordered events for the data-parallel gradient path (replaces the reference's nn.DataParallel
+ * gradient gather, src/training.py:211-212).  The only runtime objects the library creates: an event
+ * recorded with hipEventRecordExternal while a stream is being captured becomes an event-record NODE of
+ * the graph, so each replay records it when the backward reaches that point; a stream outside the graph
+ * waits on it (hyres_stream_wait_event) and starts that gradient segment's RCCL all-reduce while the rest
+ * of the replay computes (hyres_hip/ddp.py reduce_graphed).  Outside capture the record is a plain
+ * hipEventRecord. */
+int hyres_event_create(void** ev);                               /* hipEventDisableTiming */
+int hyres_event_destroy(void* ev);
+int hyres_event_record_external(void* ev, hyres_stream_t s);
+int hyres_stream_wait_event(hyres_stream_t s, void* ev);
+
 /* ------------------------------------------------------------------------------------------ */
 /* convolution geometry (implicit GEMM, NHWC).                                                */
 /* One launch computes Y[b, i*osh+oph[p], j*osw+opw[p], co] for every phase p < nphase and base */
@@ -349,8 +361,11 @@ int hyres_rd_finalize(const float* sums, const float* jpeg_bpp, float lmbda, lon
 int hyres_rd_bwd_coef(const float* g0, const float* g1, const float* g2, const float* g3,
                       const float* g4, const float* g5, float lmbda, long long npx, long long nel,
                       float* coef, hyres_stream_t s);
-/* global L2 norm of a flat buffer -> out[0] = sum sq ; clip factor computed on device */
-int hyres_sumsq(const float* x, long long n, float* out, void* ws, long long ws_bytes, hyres_stream_t s);
+/* sum of squares of a flat buffer, accumulated and returned in fp64 -> out[0] (device double): a finite
+ * gradient never overflows it, so !isfinite(out[0]) <=> some element is inf/NaN (GradScaler found_inf is
+ * element-wise, torch/amp/grad_scaler.py) and the clip norm of engine.py:76 stays exact; ws >= 8 bytes per
+ * block (hyres_reduce_workspace_bytes). */
+int hyres_sumsq(const float* x, long long n, double* out, void* ws, long long ws_bytes, hyres_stream_t s);
 /* fused Adam over a flat parameter buffer: torch.optim.Adam (foreach, amsgrad=False, weight_decay=0)
  * replacing src/utils/engine.py:68-82 (clip_grad_norm_ -> [GradScaler] -> Adam.step). Hyper-parameters
  * are doubles: 1-beta, the bias corrections, step_size and sqrt(bc2) are formed in double precision as
@@ -361,12 +376,12 @@ int hyres_sumsq(const float* x, long long n, float* out, void* ws, long long ws_
  * sumsq is not finite (GradScaler.step's found_inf), 2 skip when sumsq is NaN (engine.py:60-74). */
 int hyres_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, long long n,
                     double lr, double beta1, double beta2, double eps, float* step_dev,
-                    const float* sumsq, double max_norm, const float* gscale, int skip,
+                    const double* sumsq, double max_norm, const float* gscale, int skip,
                     hyres_stream_t s);
 /* torch GradScaler.update on the device (engine.py:73,80): found_inf = !isfinite(sumsq[0]) of the
  * scaled gradients; scale *= backoff on inf, *= growth after growth_interval clean steps;
  * inv_scale = 1/scale. */
-int hyres_grad_scaler_update(const float* sumsq, float* scale, float* inv_scale, int* growth_tracker,
+int hyres_grad_scaler_update(const double* sumsq, float* scale, float* inv_scale, int* growth_tracker,
                              double growth_factor, double backoff_factor, int growth_interval,
                              hyres_stream_t s);
 

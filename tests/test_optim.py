@@ -184,7 +184,9 @@ def test_grad_scaler_skip_and_backoff_gpu():
     tsc.scale(torch.ones((), device=D))  # torch's scaler allocates its state lazily on the first scale()
     aux = [torch.nn.Parameter(torch.ones(4, device=D))]
     faux = FusedAdam(aux, lr=1e-2)
-    plan = ["ok", "inf", "ok", "nan", "ok", "ok", "ok"]
+    # "big": a finite scaled gradient whose fp32 sum of squares would overflow — torch's found_inf is
+    # element-wise, so it must NOT skip the step or back the scale off (hyres_sumsq accumulates in fp64)
+    plan = ["ok", "inf", "ok", "big", "nan", "ok", "ok", "ok"]
     aux_steps = 0
     for k, kind in enumerate(plan):
         S = tsc.get_scale()
@@ -193,6 +195,8 @@ def test_grad_scaler_skip_and_backoff_gpu():
             grads[2][0, 1] = float("inf")
         if kind == "nan":
             grads[3][7] = float("nan")
+        if kind == "big":
+            grads[1].view(-1)[:4] = 1e15 * S
         for p, gr in zip(ref, grads):
             p.grad = gr.clone()
         fopt.zero_grad()
@@ -211,6 +215,7 @@ def test_grad_scaler_skip_and_backoff_gpu():
         faux.step(skip_if_nan=fopt.sumsq.clone())
         torch.cuda.synchronize()
         assert msc.get_scale() == tsc.get_scale(), (k, kind, msc.get_scale(), tsc.get_scale())
-    assert fopt.steps == 5 and faux.steps == aux_steps == 6
+    assert fopt.steps == sum(k in ("ok", "big") for k in plan)
+    assert faux.steps == aux_steps == sum(k != "nan" for k in plan)
     for p, q in zip(ref, mine):
         assert float((q.detach() - p.detach()).abs().max()) <= 2e-6 * float(p.detach().abs().max())
