@@ -556,6 +556,180 @@ __global__ __launch_bounds__(256) void conv_fwd_h_kernel(const ConvArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// Halo-staged f16 3x3 conv (autocast; the dominant AMP kernel).  The implicit-GEMM kernel above gathers the
+// A operand once per tap from L2: for a 3x3 64->64 layer at 128^2 that is ~1 GB of L2->CU traffic per launch
+// (PMC: TCC hits+misses ~7.9 M requests, 84 % hit) for 134 MB of HBM traffic, and its one-chunk register
+// prefetch cannot cover that latency with the 4 f16 MFMAs a 32-deep chunk gives each wave (SQ_WAIT_ANY 48 %
+// of wave-cycles).  Here a block computes a 4-row x 64-pixel x 64-channel output tile: the 6 x 66-pixel
+// input halo of one 32-channel chunk is staged ONCE in LDS as fp16 (2 buffers: the next chunk's halo loads
+// are issued in three parts between the taps of the current chunk), and all 9 taps read their A fragments
+// from it (ds_read_b128, 80-B pixel pitch: conflict-free); the B fragments (weights, fp32 W2 converted in
+// registers) come straight from L2 in MFMA layout, one tap ahead.  L2->CU bytes per output pixel drop from
+// ~3.4 KB to ~1.5 KB.  Taps: any 9 offsets within [-1, 1]^2 (the conv and its input-gradient), stride 1,
+// same-size output, Ci % 32 == 0, Co % 64 == 0, Wo % 64 == 0.  IO: bit 0 X fp16, bit 1 Y/res/aux fp16.
+constexpr int HALO_R = 4, HALO_TW = 64, HALO_HR = HALO_R + 2, HALO_HW = HALO_TW + 2;
+constexpr int HALO_NPX = HALO_HR * HALO_HW;  // 396 halo pixels
+constexpr int HALO_PH = 40;                   // halves per staged pixel (32 channels + 8 pad: 80-B pitch)
+constexpr int HALO_E = HALO_NPX * 8;          // float4 elements of one 32-channel halo chunk
+constexpr int HALO_PE = (HALO_E + 2) / 3;     // per staging part (3 parts per chunk)
+constexpr int HALO_PV = (HALO_PE + 255) / 256;
+
+template <int IO>
+__global__ __launch_bounds__(256, 2) void conv3x3_halo_f16_kernel(const ConvArgs a) {
+    constexpr bool XH = (IO & 1) != 0, YH = (IO & 2) != 0;
+    constexpr int XES = XH ? 2 : 4;
+    constexpr int HBUF = HALO_NPX * HALO_PH;  // halves per buffer
+    constexpr int CP = 64 + 4;                // epilogue staging pitch (floats)
+    static_assert(2 * 64 * CP * 4 <= 2 * HBUF * 2, "epilogue staging fits in the halo buffers");
+    __shared__ __attribute__((aligned(16))) _Float16 hal[2 * HBUF];
+    __shared__ int2 tapoff[9];
+    typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+
+    const hyres_conv_geom& g = a.g;
+    const int tid = threadIdx.x;
+    // tile decode, XCD-aware (conv_fwd_body): N tiles fastest, then row tiles (vertical neighbours share
+    // two of the six halo rows through one L2), column tiles, images
+    const int nnt = g.Co / 64, nrt = (g.Ho + HALO_R - 1) / HALO_R, nct = g.Wo / HALO_TW;
+    int l;
+    {
+        const int nb = gridDim.x, hw = blockIdx.x;
+        const int q = nb >> 3, r = nb & 7, x = hw & 7;
+        l = x * q + min(x, r) + (hw >> 3);
+    }
+    const int nt = l % nnt; l /= nnt;
+    const int rt = l % nrt; l /= nrt;
+    const int ct = l % nct;
+    const int b = l / nct;
+    const int n0 = nt * 64, i0 = rt * HALO_R, j0 = ct * HALO_TW;
+    const int Ci = g.Ci, nch = Ci / 32;
+    if (tid < 9) tapoff[tid] = make_int2(g.dh[tid], g.dw[tid]);
+
+    const long long img = (long long)g.Hi * g.Wi * g.ldx;
+    const long long xrem = img * XES;
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(reinterpret_cast<const char*>(a.x) + (long long)b * img * XES), (short)0,
+        (int)(xrem < 0x7FFFFFF0LL ? xrem : 0x7FFFFFF0LL), 0x00020000);
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)a.w2, (short)0, a.w_bytes, 0x00020000);
+
+    const int lane = tid & 63, wave = tid >> 6;
+    const int wm = wave & 1, wn = wave >> 1;  // rows 2wm, 2wm+1; channels n0 + 32wn ..
+    const int lr = lane & 31, lh = lane >> 5;
+
+    // ---- halo staging (part p of chunk c: elements [p*PE, (p+1)*PE) of the 396 px x 8 float4)
+    float4 hreg[HALO_PV];
+    auto hload = [&](int part, int c) {
+        const int ci0 = c * 32;
+#pragma unroll
+        for (int q = 0; q < HALO_PV; ++q) {
+            const int e = part * HALO_PE + tid + 256 * q;
+            const int px = e >> 3, c4 = e & 7;
+            const int hr = px / HALO_HW, hc = px - hr * HALO_HW;
+            const int ih = i0 - 1 + hr, iw = j0 - 1 + hc;
+            const bool ok = e < (part + 1) * HALO_PE && e < HALO_E && (unsigned)ih < (unsigned)g.Hi &&
+                            (unsigned)iw < (unsigned)g.Wi;
+            const int off = ok ? ((ih * g.Wi + iw) * g.ldx + ci0 + 4 * c4) * XES : (int)0x80000000;
+            if constexpr (XH) {
+                const half4_t h = __builtin_bit_cast(half4_t, __builtin_amdgcn_raw_buffer_load_b64(xr, off, 0, 0));
+                hreg[q] = make_float4((float)h.x, (float)h.y, (float)h.z, (float)h.w);
+            } else {
+                hreg[q] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
+            }
+        }
+    };
+    auto hstore = [&](int part, int buf) {
+#pragma unroll
+        for (int q = 0; q < HALO_PV; ++q) {
+            const int e = part * HALO_PE + tid + 256 * q;
+            if (e < (part + 1) * HALO_PE && e < HALO_E) {
+                const int px = e >> 3, c4 = e & 7;
+                const half4_t h = {(_Float16)hreg[q].x, (_Float16)hreg[q].y, (_Float16)hreg[q].z, (_Float16)hreg[q].w};
+                *reinterpret_cast<half4_t*>(&hal[buf * HBUF + px * HALO_PH + 4 * c4]) = h;
+            }
+        }
+    };
+    // ---- B fragments of one tap (both 16-deep k-steps of the chunk): W2[co][t][ci], fp32 -> fp16
+    const int co = n0 + wn * 32 + lr;
+    float4 bnx[4];
+    auto bload = [&](int t, int c) {
+        const int base = (co * a.ldw + t * Ci + c * 32 + 8 * lh) * 4;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            bnx[2 * ks] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(wr, base + 64 * ks, 0, 0));
+            bnx[2 * ks + 1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(wr, base + 64 * ks + 16, 0, 0));
+        }
+    };
+
+    floatx16 acc[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+
+#pragma unroll
+    for (int part = 0; part < 3; ++part) {
+        hload(part, 0);
+        hstore(part, 0);
+    }
+    bload(0, 0);
+    __syncthreads();
+    for (int c = 0; c < nch; ++c) {
+        const _Float16* H = hal + (c & 1) * HBUF;
+        const bool more = c + 1 < nch;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+            half8 bf[2];
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+                const float4 u = bnx[2 * ks], v = bnx[2 * ks + 1];
+                bf[ks] = half8{(_Float16)u.x, (_Float16)u.y, (_Float16)u.z, (_Float16)u.w,
+                               (_Float16)v.x, (_Float16)v.y, (_Float16)v.z, (_Float16)v.w};
+            }
+            if (t < 8) bload(t + 1, c);
+            else if (more) bload(0, c + 1);
+            if (more && t % 3 == 0) hload(t / 3, c + 1);
+            const int2 o = tapoff[t];
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+                for (int at = 0; at < 4; ++at) {
+                    const int orow = 2 * wm + (at >> 1);  // output row within the tile
+                    const int px = (orow + 1 + o.x) * HALO_HW + (at & 1) * 32 + lr + 1 + o.y;
+                    const half8 af = *reinterpret_cast<const half8*>(&H[px * HALO_PH + 16 * ks + 8 * lh]);
+                    acc[at] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af, bf[ks], acc[at], 0, 0, 0);
+                }
+            }
+            if (more && t % 3 == 2) hstore(t / 3, (c + 1) & 1);
+        }
+        __syncthreads();
+    }
+
+    // ---- epilogue in two passes of 2 output rows (rows p and 2 + p), staged through the halo buffers
+    float* Cs = reinterpret_cast<float*>(hal);
+    const float slope = (a.e.act == HYRES_ACT_PRELU) ? a.e.slope[0] : 0.f;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+        if (p) __syncthreads();
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                Cs[(wm * 64 + h * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh) * CP + wn * 32 + lr] = acc[2 * p + h][r];
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int idx = tid + 256 * k;
+            const int c4 = idx & 15, px = (idx >> 4) & 63, rr = idx >> 10;
+            const int i = i0 + 2 * rr + p, j = j0 + px;
+            if (i < g.Ho) {
+                const float4 v = *reinterpret_cast<const float4*>(&Cs[(rr * 64 + px) * CP + 4 * c4]);
+                const long long pix = ((long long)b * g.Ho + i) * g.Wo + j;
+                epi_store4<YH>(a.e, a.y, g.ldy, pix, n0 + 4 * c4, v, slope);
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
 // Streaming 1x1 conv (K = Ci <= 128, Co = 32*NT): the K-short pointwise layers of the ResidualUnits /
 // RBBs at 64^2..256^2 sit at the fp32 ridge (64-128 FLOP per output element against 8-12 bytes), and the
 // tiled kernel above runs them as lock-stepped blocks (load, then MFMA, then epilogue), so their MFMA and
@@ -2478,6 +2652,29 @@ static int env_int(const char* name, int dflt) {
     return (e && *e) ? atoi(e) : dflt;
 }
 
+// conv3x3_halo_f16_kernel applies (see above); HYRES_CONV_HALO16=0 turns it off
+static bool halo16_ok(const hyres_conv_geom* g, const hyres_epilogue* e) {
+    static const int on = env_int("HYRES_CONV_HALO16", 1);
+    if (!on || !e->f16_operands || g->nphase != 1 || g->ntaps != 9 || g->Ci % 32 != 0 || g->Co % 64 != 0) return false;
+    if (g->ish != 1 || g->isw != 1 || g->Hi != g->Ho || g->Wi != g->Wo || g->Hq != g->Ho || g->Wq != g->Wo) return false;
+    if (g->Wo % HALO_TW != 0 || e->square_input) return false;
+    for (int t = 0; t < 9; ++t)
+        if (g->dh[t] < -1 || g->dh[t] > 1 || g->dw[t] < -1 || g->dw[t] > 1) return false;
+    return true;
+}
+
+static int launch_halo16(const ConvArgs& a, hipStream_t st) {
+    const hyres_conv_geom& g = a.g;
+    const int blocks = g.B * ((g.Ho + HALO_R - 1) / HALO_R) * (g.Wo / HALO_TW) * (g.Co / 64);
+    switch (a.e.io_f16) {
+        case 0: hipLaunchKernelGGL(conv3x3_halo_f16_kernel<0>, dim3(blocks), dim3(256), 0, st, a); break;
+        case 1: hipLaunchKernelGGL(conv3x3_halo_f16_kernel<1>, dim3(blocks), dim3(256), 0, st, a); break;
+        case 2: hipLaunchKernelGGL(conv3x3_halo_f16_kernel<2>, dim3(blocks), dim3(256), 0, st, a); break;
+        default: hipLaunchKernelGGL(conv3x3_halo_f16_kernel<3>, dim3(blocks), dim3(256), 0, st, a); break;
+    }
+    return HY_LAUNCH_CHECK("conv3x3_halo_f16_kernel");
+}
+
 // Kernel choice of hyres_conv_forward, shared with hyres_conv_kernel_name / hyres_conv_plan (the profiler's
 // label). tile: 0 = <2,2,2,2> (128x128), 1 = <2,1,2,2> (128x64), 2 = <1,1,4,1> (128x32), 3 = <1,2,2,2>
 // (64x128), 4 = <1,1,2,2> (64x64).
@@ -2673,6 +2870,10 @@ int hyres_conv_forward(const hyres_conv_geom* g, const float* x, const float* w2
         }
         return HY_LAUNCH_CHECK("conv_narrow_kernel");
     }
+    if (mode == 0 && a.vec4 && halo16_ok(g, e)) {
+        a.nsplit = 1;
+        return launch_halo16(a, st);
+    }
     {
         const int nt = stream_nt(g, e);
         const long long xb = (long long)a.M * g->ldx * 4;
@@ -2711,6 +2912,10 @@ int hyres_conv_kernel_name(const hyres_conv_geom* g, const hyres_epilogue* e, in
     const ConvChoice ch = choose_conv(g, e, true);
     if (ch.narrow) {
         snprintf(buf, n, "conv_narrow_kernel<%d, %d>", std::min(g->Co, 4), g->Ci == 64 ? 1 : 2);
+        return 0;
+    }
+    if (ch.mode == 0 && halo16_ok(g, e)) {
+        snprintf(buf, n, "conv3x3_halo_f16_kernel<%d>", e->io_f16);
         return 0;
     }
     {

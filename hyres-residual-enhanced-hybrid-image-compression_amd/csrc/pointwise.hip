@@ -492,13 +492,32 @@ int hyres_event_destroy(void* ev) {
 }
 int hyres_event_record_external(void* ev, hyres_stream_t s) {
     HY_REQUIRE(ev, HYRES_E_ARG, "event_record_external: NULL");
-    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-    hipError_t err = hipStreamIsCapturing(as_stream(s), &st);
-    HY_REQUIRE(err == hipSuccess, (int)err, "hipStreamIsCapturing: %s", hipGetErrorString(err));
-    err = st == hipStreamCaptureStatusActive
-              ? hipEventRecordWithFlags((hipEvent_t)ev, as_stream(s), hipEventRecordExternal)
-              : hipEventRecord((hipEvent_t)ev, as_stream(s));
-    HY_REQUIRE(err == hipSuccess, (int)err, "hipEventRecordWithFlags(external): %s", hipGetErrorString(err));
+    hipStream_t st = as_stream(s);
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    unsigned long long id = 0;
+    hipGraph_t graph = nullptr;
+    const hipGraphNode_t* deps = nullptr;
+    size_t ndeps = 0;
+    hipError_t err = hipStreamGetCaptureInfo_v2(st, &cs, &id, &graph, &deps, &ndeps);
+    if (err != hipSuccess) {
+        (void)hipGetLastError();  // never leave a sticky error behind for the caller's runtime
+        return ::hyres::set_error((int)err, "hipStreamGetCaptureInfo_v2: %s", hipGetErrorString(err));
+    }
+    if (cs != hipStreamCaptureStatusActive) {
+        err = hipEventRecord((hipEvent_t)ev, st);
+    } else {
+        // hipEventRecordWithFlags(hipEventRecordExternal) is refused inside a capture on this runtime, so the
+        // event-record node is added to the captured graph by hand, after the stream's current frontier, and
+        // becomes the stream's new frontier (the captured work that follows is ordered after it)
+        hipGraphNode_t node = nullptr;
+        err = hipGraphAddEventRecordNode(&node, graph, deps, ndeps, (hipEvent_t)ev);
+        if (err == hipSuccess)
+            err = hipStreamUpdateCaptureDependencies(st, &node, 1, hipStreamSetCaptureDependencies);
+    }
+    if (err != hipSuccess) {
+        (void)hipGetLastError();
+        return ::hyres::set_error((int)err, "event record (capture %d): %s", (int)cs, hipGetErrorString(err));
+    }
     return 0;
 }
 int hyres_stream_wait_event(hyres_stream_t s, void* ev) {

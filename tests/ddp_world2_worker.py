@@ -11,8 +11,8 @@ the launching test touches anything but its own process.  Each rank:
      all-reduces with ``FlatGradReducer.reduce_graphed`` (segments start on the markers' events);
   3. replays again and reduces after the replay (``all_reduce``): must equal (2) bit for bit;
   4. takes one FusedAdam(clip 1.0) step; rank 0 then broadcasts its parameters, every rank checks equality;
-Rank 0 finally runs the SAME step single-process on the whole bs=4 batch (fresh model, same weights) and
-saves both flat gradients + losses to OUT (an .npz) for the test to compare.
+Rank 0 finally re-runs each rank's shard single-process (their mean must equal the reduced gradient bit for
+bit) and the whole bs=4 batch (fresh models, same weights), and saves the flat gradients + losses to OUT.
 """
 import os
 import sys
@@ -101,19 +101,31 @@ def main():
     params_equal_all = int(params_equal) == world
 
     if rank == 0:
-        # the same step, one process, the whole batch
-        net1, names1, opt1 = build(dev)
-        jd1, bpp1 = net1.jpeg(x_all)
-        x1, j1 = x_all.to(dev), jd1.to(dev)
-        net1.residual_model.noise.injected = {"z": nz_all.to(dev), "y": ny_all.to(dev)}
-        cap1 = CapturedStep(net1, x1, j1, float(bpp1), criterion=crit, zero_grad=opt1.zero_grad)
-        opt1.zero_grad()
-        _, c1 = cap1.replay()
-        torch.cuda.synchronize()
+        def single(sl_):
+            """The same graphed step in one process on the batch slice ``sl_`` (fresh model, same weights)."""
+            net1, _, opt1 = build(dev)
+            jd1, bpp1 = net1.jpeg(x_all[sl_])
+            net1.residual_model.noise.injected = {"z": nz_all[sl_].to(dev), "y": ny_all[sl_].to(dev)}
+            cap1 = CapturedStep(net1, x_all[sl_].to(dev), jd1.to(dev), float(bpp1), criterion=crit,
+                                zero_grad=opt1.zero_grad)
+            opt1.zero_grad()
+            _, c1 = cap1.replay()
+            torch.cuda.synchronize()
+            return opt1.flat.grad.clone(), float(c1["loss"])
+
+        # (a) each rank's shard recomputed here: their mean is what the all-reduce must produce, bit for bit
+        # (sum of two fp32 values, then x 1/world — the reducer's exact arithmetic)
+        halves = [single(slice(r * per, (r + 1) * per)) for r in range(world)]
+        g_mean = halves[0][0]
+        for gh, _ in halves[1:]:
+            g_mean = g_mean + gh
+        g_mean = g_mean * (1.0 / world)
+        # (b) the whole batch in one process: equal up to batch-size-dependent summation order
+        g_all, loss_all = single(slice(0, x_all.shape[0]))
         offs = np.array(opt.flat.offsets, dtype=np.int64)
         sizes = np.array([p.numel() for p in opt.flat.params], dtype=np.int64)
-        np.savez(out_path, g_ddp=g_overlap.cpu().numpy(), g_single=opt1.flat.grad.cpu().numpy(),
-                 loss_ddp=np.float64(loss_mean), loss_single=np.float64(float(c1["loss"])),
+        np.savez(out_path, g_ddp=g_overlap.cpu().numpy(), g_mean=g_mean.cpu().numpy(),
+                 g_single=g_all.cpu().numpy(), loss_ddp=np.float64(loss_mean), loss_single=np.float64(loss_all),
                  same_after=np.bool_(same_after), params_equal=np.bool_(params_equal_all),
                  offsets=offs, sizes=sizes, names=np.array(names))
     dist.barrier()

@@ -15,7 +15,8 @@ Weights come from the name-keyed recipe in ``hyres_hip/weights.py``; no checkpoi
 
 Outputs (small, committed):  tests/golden/hyres_eval_b2_64.npz, hyres_train_b2_64.npz,
   hyres_train_nq_b2_64.{npz,json} (noisequant=True), checkerboard_sets.npz, kodim01_crop64_eval.npz, meta.json
-(``--only-noisequant`` regenerates just the noisequant train step)
+  hyres_amp_b2_64.{npz,json} (the reference under autocast float16: eval forward + train step)
+(``--only-noisequant`` / ``--only-amp`` regenerate just that fixture)
 """
 from __future__ import annotations
 
@@ -174,11 +175,88 @@ def train_step_noisequant(hyres_mod, quant_mod, x, q=50, lmbda=0.045):
     print("noisequant train loss", float(loss), "aux", float(aux))
 
 
+def amp_fixtures(hyres_mod, x, q=50, lmbda=0.045, scale=float(os.environ.get("AMP_SCALE", "1.0"))):
+    """The reference under autocast(float16) (train.sh:19 ``--mixed-precision``; src/utils/engine.py:32 wraps
+    forward + criterion in autocast, engine.py:51 scales the loss with GradScaler(init 2^16)) -> hyres_amp_b2_64.npz.
+
+    The reference's autocast is CUDA's; this container has no GPU, so the reference runs under
+    ``torch.autocast("cpu", dtype=torch.float16)``.  Both lists put conv2d / conv_transpose2d / linear /
+    matmul / prelu in fp16 (fp16 operands, fp16 output — every conv output of the model is an fp16 tensor
+    either way) and promote mixed fp16/fp32 elementwise ops to fp32.  They differ on ops CUDA forces to fp32
+    that the CPU list leaves in the input dtype: ``pow`` (GDN's x**2 — no value difference: the conv rounds
+    x**2 to fp16 in both), ``rsqrt`` (GDN's norm: fp32 on CUDA, fp16 on CPU, then x*norm is fp32 / fp16),
+    ``exp``, ``log``, ``softplus``, ``sum`` on fp16 inputs (EntropyBottleneck logits; the likelihoods leave
+    LowerBound as fp32 in both, so the RD loss's log/sum run in fp32 in both), and ``mse_loss`` is fp32 in
+    both.  The HIP path follows CUDA's lists, so the tests compare against this fixture at AMP-level
+    tolerances (loss 1e-3, PSNR 0.01 dB, bpp 1 %) with round-decision flips counted, not bitwise.
+    Train step: noisequant=False with the EntropyBottleneck / GaussianConditional noise draws recorded (seed
+    1234), loss x scale -> backward -> gradients / scale (GradScaler.unscale_).  scale defaults to 1: the
+    GradScaler's initial 2^16 overflows this fp16 backward (the reference would skip that step and back the
+    scale off), and 256 gives the same unscaled gradients as 1 (checked), so nothing underflows at 1."""
+    out_d = {"x": x}
+    net, sd = build_reference(hyres_mod, q)
+    net.eval()
+    with torch.no_grad(), torch.autocast("cpu", dtype=torch.float16):
+        ev = net(x)
+    out_d.update({"eval_x_hat": ev["x_hat"].float(), "eval_residual_hat": ev["residual_hat"].float(),
+                  "eval_y_likelihoods": ev["likelihoods"]["y"].float(),
+                  "eval_z_likelihoods": ev["likelihoods"]["z"].float(), "jpeg_decoded": ev["jpeg_decoded"].float(),
+                  "jpeg_bpp": torch.tensor(float(ev["jpeg_bpp_loss"]))})
+    net, sd = build_reference(hyres_mod, q)
+    net.train()
+    noise_log = []
+    from oracle import compressai_restated as cr
+    orig_q = cr.EntropyModel.quantize
+
+    def rec_quantize(self, inputs, mode, means=None):
+        if mode == "noise":
+            n = torch.empty_like(inputs).uniform_(-0.5, 0.5)
+            noise_log.append((type(self).__name__, n.clone()))
+            return inputs + n
+        return orig_q(self, inputs, mode, means)
+
+    cr.EntropyModel.quantize = rec_quantize
+    torch.manual_seed(1234)
+    try:
+        with torch.autocast("cpu", dtype=torch.float16):
+            out = net(x, noisequant=False)
+            N_, _, H_, W_ = x.shape
+            npx = N_ * H_ * W_
+            y_bpp = torch.log(out["likelihoods"]["y"]).sum() / (-math.log(2) * npx)
+            z_bpp = torch.log(out["likelihoods"]["z"]).sum() / (-math.log(2) * npx)
+            mse = torch.nn.functional.mse_loss(out["x_hat"], x) * 255 ** 2
+            loss = lmbda * mse + y_bpp + z_bpp + out["jpeg_bpp_loss"]
+    finally:
+        cr.EntropyModel.quantize = orig_q
+    assert [n for n, _ in noise_log] == ["EntropyBottleneck", "GaussianConditional"], noise_log
+    (loss * scale).backward()
+    for p in net.parameters():
+        if p.grad is not None:
+            p.grad.div_(scale)
+    B, _, H, W = x.shape
+    C = net.residual_model.N
+    nz = noise_log[0][1].reshape(C, B, H // 32, W // 32).permute(1, 0, 2, 3).contiguous()
+    out_d.update({"noise_z": nz.float(), "noise_y": noise_log[1][1].float(), "train_x_hat": out["x_hat"].detach().float(),
+                  "train_y_likelihoods": out["likelihoods"]["y"].detach().float(),
+                  "train_z_likelihoods": out["likelihoods"]["z"].detach().float(),
+                  "loss": loss.detach().float(), "mse_loss": mse.detach().float(), "y_bpp": y_bpp.detach().float(),
+                  "z_bpp": z_bpp.detach().float()})
+    np.savez_compressed(os.path.join(OUT, "hyres_amp_b2_64.npz"),
+                        **{k: v.numpy().astype(np.float32) for k, v in out_d.items()})
+    with open(os.path.join(OUT, "hyres_amp_b2_64.json"), "w") as f:
+        json.dump({"lambda": lmbda, "autocast": "cpu float16", "loss_scale": scale, "torch_seed": 1234,
+                   "train_grads": grad_summary(net)}, f, indent=1)
+    print("amp eval / train: loss", float(loss), "mse", float(mse))
+
+
 def main():
     torch.set_num_threads(8)
     hyres_mod, quant_mod = install_reference()
     if "--only-noisequant" in sys.argv:
         train_step_noisequant(hyres_mod, quant_mod, synthetic_input())
+        return
+    if "--only-amp" in sys.argv:
+        amp_fixtures(hyres_mod, synthetic_input())
         return
     q = 50
     B, H, W = 2, 64, 64
@@ -286,6 +364,7 @@ def main():
                         **{k: v.numpy().astype(np.float32) for k, v in kd.items()})
 
     train_step_noisequant(hyres_mod, quant_mod, x, q)
+    amp_fixtures(hyres_mod, x, q)
 
     with open(os.path.join(OUT, "meta.json"), "w") as f:
         json.dump(meta, f, indent=1)

@@ -2,9 +2,9 @@
 
 Two ranks on device 0 over gloo (tests/ddp_world2_worker.py) run the graphed step on halves of a bs=4
 batch with the gradient all-reduce triggered from inside the replay (external events at the backward-progress
-markers, ``FlatGradReducer.reduce_graphed``); the averaged gradient must equal the single-process bs=4
-gradient, the after-replay reduction must give the same bits, and the ranks' parameters after the
-FusedAdam step must be identical (reference: src/training.py:211-212 data parallelism, engine.py:50-90).
+markers, ``FlatGradReducer.reduce_graphed``); the reduced gradient must equal the mean of the two shards'
+single-process gradients bit for bit and the single-process bs=4 gradient to 1e-3, the after-replay
+reduction must give the same bits, and the ranks' parameters after the FusedAdam step must be identical (reference: src/training.py:211-212 data parallelism, engine.py:50-90).
 """
 import os
 import socket
@@ -41,13 +41,17 @@ def test_world2_graphed_ddp_gradient_parity(tmp_path):
         d = {k: z[k] for k in z.files}
     assert bool(d["same_after"]), "graph-triggered reduction != after-replay reduction"
     assert bool(d["params_equal"]), "ranks diverged after the optimiser step"
+    # the reduced gradient IS the mean of the two shards' gradients, bit for bit (deterministic kernels,
+    # fp32 a + b then x 1/2 in both)
+    assert np.array_equal(d["g_ddp"], d["g_mean"]), float(np.abs(d["g_ddp"] - d["g_mean"]).max())
     gd, gs = d["g_ddp"].astype(np.float64), d["g_single"].astype(np.float64)
     # per-rank mean losses averaged == the global-batch loss
     assert abs(float(d["loss_ddp"]) - float(d["loss_single"])) <= 1e-5 * abs(float(d["loss_single"]))
-    # flat gradient: the mean of two bs=2 gradients vs one bs=4 gradient differs only by fp32 summation
-    # order (different tilings / split-K of the two batch sizes)
+    # vs ONE bs=4 step: the shards see different tilings / split-K factors than the whole batch, so fp32
+    # summation order differs, and where a round(y - mu) or ReLU input sits within that rounding of its
+    # decision point the branch flips (the decision-exact oracle tests, test_parity_gpu, cover that
+    # mechanism); normwise 1e-3 over the flat gradient
     flat = np.linalg.norm(gd - gs) / np.linalg.norm(gs)
-    assert flat < 1e-5, flat
     worst = []
     for name, o, n in zip(d["names"], d["offsets"], d["sizes"]):
         a, b = gd[o:o + n], gs[o:o + n]
@@ -56,7 +60,7 @@ def test_world2_graphed_ddp_gradient_parity(tmp_path):
             worst.append((np.linalg.norm(a - b) / nb, str(name)))
     worst.sort(reverse=True)
     print("flat", flat, "worst tensors", worst[:3])
-    assert worst[0][0] < 1e-4, worst[:3]
+    assert flat < 1e-3, (flat, worst[:3])
 
 
 def test_external_event_orders_host_work_after_graph_launch():
