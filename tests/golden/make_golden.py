@@ -16,7 +16,8 @@ Weights come from the name-keyed recipe in ``hyres_hip/weights.py``; no checkpoi
 Outputs (small, committed):  tests/golden/hyres_eval_b2_64.npz, hyres_train_b2_64.npz,
   hyres_train_nq_b2_64.{npz,json} (noisequant=True), checkerboard_sets.npz, kodim01_crop64_eval.npz, meta.json
   hyres_amp_b2_64.{npz,json} (the reference under autocast float16: eval forward + train step)
-(``--only-noisequant`` / ``--only-amp`` regenerate just that fixture)
+  vgg_b2_64.npz (the reference's VGGLoss on recipe VGG16 weights)
+(``--only-noisequant`` / ``--only-amp`` / ``--only-vgg`` regenerate just that fixture)
 """
 from __future__ import annotations
 
@@ -249,8 +250,80 @@ def amp_fixtures(hyres_mod, x, q=50, lmbda=0.045, scale=float(os.environ.get("AM
     print("amp eval / train: loss", float(loss), "mse", float(mse))
 
 
+def vgg_fixture(x, x_hat):
+    """The reference's own VGGLoss (src/losses/vgg16.py:7-61, rd_loss.py:40) -> vgg_b2_64.npz.
+
+    torchvision is absent: ``torchvision.models.vgg16(pretrained=True)`` is stubbed to return configuration
+    D's ``features`` (Conv 3x3 pad 1 / ReLU(inplace) / MaxPool2d(2, 2), torchvision's layer indices) holding
+    tests/helpers.vgg16_recipe_features() instead of ImageNet weights, and ``transforms.Normalize`` is
+    restated ((x - mean) / std per channel).  The reference module itself — its slicing at [2, 7, 14, 21, 28],
+    its normalisation call and its per-slice ``abs().mean()`` sum — runs unchanged.  Stores the loss of
+    VGGLoss()(x_hat, x) and d loss / d x_hat."""
+    import importlib.util
+    from torch import nn
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from helpers import vgg16_recipe_features
+    sd = vgg16_recipe_features()
+    cfg = [64, 64, "M", 128, 128, "M", 256, 256, 256, "M", 512, 512, 512, "M", 512, 512, 512, "M"]
+
+    def vgg16(pretrained=False, **kw):
+        layers, cin = [], 3
+        for v in cfg:
+            if v == "M":
+                layers.append(nn.MaxPool2d(kernel_size=2, stride=2))
+            else:
+                layers += [nn.Conv2d(cin, v, kernel_size=3, padding=1), nn.ReLU(inplace=True)]
+                cin = v
+        feats = nn.Sequential(*layers)
+        with torch.no_grad():
+            for k, t in sd.items():
+                i, name = k.split(".")
+                getattr(feats[int(i)], name).copy_(t)
+        return types.SimpleNamespace(features=feats)
+
+    class Normalize(nn.Module):
+        def __init__(self, mean, std):
+            super().__init__()
+            self.mean = torch.tensor(mean).view(1, -1, 1, 1)
+            self.std = torch.tensor(std).view(1, -1, 1, 1)
+
+        def forward(self, t):
+            return (t - self.mean) / self.std
+
+    tv = types.ModuleType("torchvision")
+    tvm = types.ModuleType("torchvision.models")
+    tvt = types.ModuleType("torchvision.transforms")
+    tvm.vgg16 = vgg16
+    tvt.Normalize = Normalize
+    tv.models, tv.transforms = tvm, tvt
+    saved = {k: sys.modules.get(k) for k in ("torchvision", "torchvision.models", "torchvision.transforms")}
+    sys.modules.update({"torchvision": tv, "torchvision.models": tvm, "torchvision.transforms": tvt})
+    try:
+        spec = importlib.util.spec_from_file_location("ref_vgg16", os.path.join(REF, "src/losses/vgg16.py"))
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        vgg = mod.VGGLoss()
+        xh = x_hat.detach().clone().requires_grad_(True)
+        loss = vgg(xh, x)
+        loss.backward()
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                sys.modules.pop(k, None)
+            else:
+                sys.modules[k] = v
+    np.savez_compressed(os.path.join(OUT, "vgg_b2_64.npz"), x=x.numpy().astype(np.float32),
+                        x_hat=x_hat.numpy().astype(np.float32), loss=np.float32(float(loss)),
+                        grad_x_hat=xh.grad.numpy().astype(np.float32))
+    print("reference VGGLoss", float(loss))
+
+
 def main():
     torch.set_num_threads(8)
+    if "--only-vgg" in sys.argv:
+        g = np.load(os.path.join(OUT, "hyres_eval_b2_64.npz"))
+        vgg_fixture(torch.from_numpy(g["x"]), torch.from_numpy(g["x_hat"]).clamp(0, 1))
+        return
     hyres_mod, quant_mod = install_reference()
     if "--only-noisequant" in sys.argv:
         train_step_noisequant(hyres_mod, quant_mod, synthetic_input())
@@ -365,6 +438,7 @@ def main():
 
     train_step_noisequant(hyres_mod, quant_mod, x, q)
     amp_fixtures(hyres_mod, x, q)
+    vgg_fixture(x, torch.from_numpy(np.load(os.path.join(OUT, "hyres_eval_b2_64.npz"))["x_hat"]).clamp(0, 1))
 
     with open(os.path.join(OUT, "meta.json"), "w") as f:
         json.dump(meta, f, indent=1)

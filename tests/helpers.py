@@ -60,3 +60,22 @@ def rel_err(a, b):
     a = a.double()
     b = b.double()
     return float((a - b).abs().max() / max(b.abs().max(), 1e-30))
+
+
+# torchvision vgg16().features (configuration D): conv layer index -> (Co, Ci)
+VGG16_CONVS = {0: (64, 3), 2: (64, 64), 5: (128, 64), 7: (128, 128), 10: (256, 128), 12: (256, 256), 14: (256, 256),
+               17: (512, 256), 19: (512, 512), 21: (512, 512), 24: (512, 512), 26: (512, 512), 28: (512, 512)}
+
+
+def vgg16_recipe_features(upto=28):
+    """Deterministic stand-in for VGG16's ImageNet features (not downloadable here): He-scaled normal
+    weights and small biases from one generator per layer, {"N.weight", "N.bias"} for conv layers <= upto.
+    tests/golden/make_golden.py feeds the same tensors to the reference's own VGGLoss (src/losses/vgg16.py)."""
+    sd = {}
+    for i, (co, ci) in VGG16_CONVS.items():
+        if i > upto:
+            continue
+        g = torch.Generator().manual_seed(1000 + i)
+        sd[f"{i}.weight"] = torch.randn(co, ci, 3, 3, generator=g) * (2.0 / (ci * 9)) ** 0.5
+        sd[f"{i}.bias"] = torch.randn(co, generator=g) * 0.01
+    return sd
