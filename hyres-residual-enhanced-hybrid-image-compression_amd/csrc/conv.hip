@@ -102,13 +102,13 @@ __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<floa
 // float4 variant of epi_store for channels n..n+3 (all operands 16B aligned).
 template <bool H = false>
 __device__ __forceinline__ void epi_store4(const hyres_epilogue& e, float* y, int ldy, long long pix, int n, float4 v,
-                                           float slope) {
+                                           float slope, const float4* rpre = nullptr) {
     float o[4] = {v.x, v.y, v.z, v.w};
     switch (e.kind) {
         case HYRES_EPI_BIAS: {
             if (e.bias) { const float4 b = ld4(e.bias + n); o[0] += b.x; o[1] += b.y; o[2] += b.z; o[3] += b.w; }
-            if (e.res) {
-                const float4 r = ldv4<H>(e.res, pix * e.ldres + n);
+            if (e.res) {  // rpre: the residual already loaded by the caller (same value, same order)
+                const float4 r = rpre ? *rpre : ldv4<H>(e.res, pix * e.ldres + n);
                 o[0] += r.x; o[1] += r.y; o[2] += r.z; o[3] += r.w;
             }
             if (e.out2) stv4<H>(e.out2, pix * e.ldo2 + n, make_float4(o[0], o[1], o[2], o[3]));
@@ -726,6 +726,229 @@ __global__ __launch_bounds__(256, 2) void conv3x3_halo_f16_kernel(const ConvArgs
                 epi_store4<YH>(a.e, a.y, g.ldy, pix, n0 + 4 * c4, v, slope);
             }
         }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Weight-resident persistent f16 3x3 conv, Ci = 64 (the 64-channel 3x3 convs of every ResidualUnit / RBB
+// / MultiScaleRefine scale at 64^2..256^2, forward and input-gradient).  conv3x3_halo_f16_kernel above still
+// re-reads the B operand (all 576 x 64 weights, fp32) from L2 once per wave and 256-pixel tile: 147 KB per
+// 32-channel chunk per block against 51 KB of halo, ~400 GB/s per CU of L2->CU traffic, 2-3x what a CU gets
+// from L2 (MI355X_MICROARCH.md "Indexed rows": 66-73 GB/s per CU from L2) — so it measured no faster than the
+// implicit-GEMM kernel.  Here one 512-thread block per CU converts the layer's weights of its 64-channel
+// output slice to fp16 ONCE into LDS (9 taps x 64 co x 64 ci, 80-B rows: 92 KB) and then walks its share of
+// the 4-row x 64-pixel tiles; per tile and 32-channel chunk only the 6 x 66-pixel halo moves (fp32 -> fp16,
+// 7 float4 per thread issued one chunk ahead, 2 LDS buffers: 63 KB), and every A and B fragment is a
+// conflict-free ds_read_b128.  Per CU that is ~22 B per cycle at the MFMA rate, below the L2 rate; the
+// epilogue is applied from the accumulators directly (per-lane scalar epi_store: the LDS is full).
+// 8 waves = 4 output rows x 2 co halves, 2 A tiles (64 px) each; tiles are walked XCD-contiguously.
+constexpr int WRES_LDS_B = 2 * 9 * 64 * HALO_PH;  // halves: [chunk][tap][co][40]
+constexpr int WRES_HV = (HALO_E + 511) / 512;     // halo float4 per thread per chunk (7)
+
+template <int IO, int V = 1>
+__global__ __launch_bounds__(512, 2) void conv3x3_wres_f16_kernel(const ConvArgs a, int ntiles, int groups) {
+    constexpr bool XH = (IO & 1) != 0, YH = (IO & 2) != 0;
+    constexpr int XES = XH ? 2 : 4;
+    constexpr int HBUF = HALO_NPX * HALO_PH;
+    __shared__ __attribute__((aligned(16))) _Float16 lds[WRES_LDS_B + 2 * HBUF];
+    __shared__ int2 tapoff[9];
+    typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+    _Float16* const Bs = lds;
+    _Float16* const Hs = lds + WRES_LDS_B;
+
+    const hyres_conv_geom& g = a.g;
+    const int tid = threadIdx.x;
+    const int nrt = (g.Ho + HALO_R - 1) / HALO_R, nct = g.Wo / HALO_TW;
+    // block -> (output-channel group, share of the tiles): the blocks of one XCD (b % 8) take one contiguous
+    // range of tiles, interleaved, so that vertically adjacent tiles (two shared halo rows) run together on it
+    const int nb = gridDim.x / groups;  // blocks per channel group
+    const int grp = blockIdx.x % groups, bg = blockIdx.x / groups;
+    const int n0 = grp * 64;
+    const int xcd = bg & 7, nx = (nb + 7 - xcd) >> 3, jx = bg >> 3;  // blocks of this XCD, index among them
+    const int q = ntiles >> 3, rr8 = ntiles & 7;
+    const int tbeg = xcd * q + min(xcd, rr8), tcnt = q + (xcd < rr8 ? 1 : 0);
+    const int mytiles = jx < tcnt ? (tcnt - 1 - jx) / nx + 1 : 0;
+    if (tid < 9) tapoff[tid] = make_int2(g.dh[tid], g.dw[tid]);
+    __shared__ __attribute__((aligned(16))) float bias_s[64];
+    if (tid < 64) bias_s[tid] = a.e.bias ? a.e.bias[n0 + tid] : 0.f;
+
+    // ---- the 64-channel weight slice, fp32 W2[co][t][ci] -> fp16 Bs[(c*9 + t)*64 + co][k] (ci = 32c + k)
+    for (int f = tid; f < 64 * 9 * 16; f += 512) {
+        const int co = f / 144, rem = f - co * 144, t = rem >> 4, ci = 4 * (rem & 15);
+        const float4 w = ld4(a.w2 + (long long)(n0 + co) * a.ldw + t * 64 + ci);
+        const half4_t h = {(_Float16)w.x, (_Float16)w.y, (_Float16)w.z, (_Float16)w.w};
+        *reinterpret_cast<half4_t*>(&Bs[(((ci >> 5) * 9 + t) * 64 + co) * HALO_PH + (ci & 31)]) = h;
+    }
+
+    const long long img = (long long)g.Hi * g.Wi * g.ldx;
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)a.x, (short)0, (int)std::min<long long>((long long)g.B * img * XES, 0x7FFFFFF0LL), 0x00020000);
+    const int lane = tid & 63, wave = tid >> 6;
+    const int orow = wave & 3, wn = wave >> 2;
+    const int lr = lane & 31, lh = lane >> 5;
+
+    auto tile_of = [&](int k, int& b, int& i0, int& j0) {
+        int l = tbeg + jx + k * nx;
+        const int rt = l % nrt; l /= nrt;
+        const int ct = l % nct;
+        b = l / nct;
+        i0 = rt * HALO_R;
+        j0 = ct * HALO_TW;
+    };
+    // halo chunks are prefetched TWO steps ahead (two register sets, alternating): one step of MFMA work
+    // (~2.3k cycles per SIMD) does not cover an HBM-bound 50 KB-per-CU chunk load
+    auto hload = [&](float4 (&h)[WRES_HV], int step) {
+        int b, i0, j0;
+        tile_of(step >> 1, b, i0, j0);
+        const int c = step & 1;
+        const int base = b * (int)img;  // element offset of image b (host checks the batch < 2 GB)
+#pragma unroll
+        for (int v = 0; v < WRES_HV; ++v) {
+            const int e = tid + 512 * v;
+            const int px = e >> 3, c4 = e & 7;
+            const int hr = px / HALO_HW, hc = px - hr * HALO_HW;
+            const int ih = i0 - 1 + hr, iw = j0 - 1 + hc;
+            const bool ok = e < HALO_E && (unsigned)ih < (unsigned)g.Hi && (unsigned)iw < (unsigned)g.Wi;
+            const int off = ok ? (base + (ih * g.Wi + iw) * g.ldx + 32 * c + 4 * c4) * XES : (int)0x80000000;
+            if constexpr (XH) {
+                const half4_t hh = __builtin_bit_cast(half4_t, __builtin_amdgcn_raw_buffer_load_b64(xr, off, 0, 0));
+                h[v] = make_float4((float)hh.x, (float)hh.y, (float)hh.z, (float)hh.w);
+            } else {
+                h[v] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
+            }
+        }
+    };
+    auto hstore = [&](const float4 (&h)[WRES_HV], int buf) {
+#pragma unroll
+        for (int v = 0; v < WRES_HV; ++v) {
+            const int e = tid + 512 * v;
+            if (e < HALO_E) {
+                const half4_t hh = {(_Float16)h[v].x, (_Float16)h[v].y, (_Float16)h[v].z, (_Float16)h[v].w};
+                *reinterpret_cast<half4_t*>(&Hs[buf * HBUF + (e >> 3) * HALO_PH + 4 * (e & 7)]) = hh;
+            }
+        }
+    };
+
+    // the product is formed transposed (C^T = W X^T, as conv1x1_stream_kernel): lane (lr, lh) of A tile `at`
+    // holds pixel j0 + 32 at + lr and, per register quad qd, the 4 consecutive channels n0 + 32 wn + 8 qd + 4 lh
+    // .. + 3 — the epilogue loads / stores float4 straight from the accumulators
+    floatx16 acc[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+    const float slope = (a.e.act == HYRES_ACT_PRELU) ? a.e.slope[0] : 0.f;
+    const bool pre_res = a.e.kind == HYRES_EPI_BIAS && a.e.res != nullptr;
+    float4 rres[2][4];  // the tile's residual operand, prefetched one step before the epilogue
+    const int steps = mytiles * 2;  // two 32-channel chunks per tile
+    auto tile_pix = [&](int k, int at, int& i, long long& pix) {
+        int b, i0, j0;
+        tile_of(k, b, i0, j0);
+        i = i0 + orow;
+        pix = ((long long)b * g.Ho + i) * g.Wo + j0 + 32 * at + lr;
+    };
+    auto body = [&](int s, float4 (&hl)[WRES_HV], const float4 (&hs)[WRES_HV]) {
+        const int k = s >> 1, c = s & 1;
+        // the epilogue's residual is loaded BEFORE the halo two steps ahead: vmcnt retires loads in issue
+        // order, so waiting for it then does not wait for that halo too (the bias comes from LDS for the same
+        // reason)
+        if (V == 0 && s + 2 < steps) hload(hl, s + 2);
+        if (c == 1 && pre_res) {
+#pragma unroll
+            for (int at = 0; at < 2; ++at) {
+                int i;
+                long long pix;
+                tile_pix(k, at, i, pix);
+#pragma unroll
+                for (int qd = 0; qd < 4; ++qd)
+                    rres[at][qd] = i < g.Ho ? ldv4<YH>(a.e.res, pix * a.e.ldres + n0 + 32 * wn + 8 * qd + 4 * lh)
+                                            : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+        }
+        if (V != 0 && s + 2 < steps) hload(hl, s + 2);
+        const _Float16* H = Hs + (s & 1) * HBUF;
+        const _Float16* Bc = Bs + c * 9 * 64 * HALO_PH;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+            const int2 o = tapoff[t];
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+                const half8 bf = *reinterpret_cast<const half8*>(&Bc[(t * 64 + wn * 32 + lr) * HALO_PH + 16 * ks + 8 * lh]);
+#pragma unroll
+                for (int at = 0; at < 2; ++at) {
+                    const int px = (orow + 1 + o.x) * HALO_HW + at * 32 + lr + 1 + o.y;
+                    const half8 af = *reinterpret_cast<const half8*>(&H[px * HALO_PH + 16 * ks + 8 * lh]);
+                    acc[at] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bf, af, acc[at], 0, 0, 0);
+                }
+            }
+        }
+        if (c == 1) {
+#pragma unroll
+            for (int at = 0; at < 2; ++at) {
+                int i;
+                long long pix;
+                tile_pix(k, at, i, pix);
+                if (i < g.Ho) {
+#pragma unroll
+                    for (int qd = 0; qd < 4; ++qd) {
+                        const int n = n0 + 32 * wn + 8 * qd + 4 * lh;
+                        const float4 v = make_float4(acc[at][4 * qd], acc[at][4 * qd + 1], acc[at][4 * qd + 2],
+                                                     acc[at][4 * qd + 3]);
+                        if (V < 2) {
+                            epi_store4<YH>(a.e, a.y, g.ldy, pix, n, v, slope, pre_res ? &rres[at][qd] : nullptr);
+                        } else if (a.e.kind == HYRES_EPI_BIAS) {
+                            const float4 bb = *reinterpret_cast<const float4*>(&bias_s[n - n0]);
+                            float o[4] = {v.x + bb.x, v.y + bb.y, v.z + bb.z, v.w + bb.w};
+                            if (a.e.res) {
+                                const float4 r = pre_res ? rres[at][qd] : ldv4<YH>(a.e.res, pix * a.e.ldres + n);
+                                o[0] += r.x; o[1] += r.y; o[2] += r.z; o[3] += r.w;
+                            }
+                            if (a.e.out2) stv4<YH>(a.e.out2, pix * a.e.ldo2 + n, make_float4(o[0], o[1], o[2], o[3]));
+                            if (a.e.act == HYRES_ACT_RELU) {
+#pragma unroll
+                                for (int cc = 0; cc < 4; ++cc) o[cc] = fmaxf(o[cc], 0.f);
+                            } else if (a.e.act == HYRES_ACT_PRELU) {
+#pragma unroll
+                                for (int cc = 0; cc < 4; ++cc) o[cc] = o[cc] >= 0.f ? o[cc] : slope * o[cc];
+                            } else if (a.e.act == HYRES_ACT_RELU_MASK) {
+                                const float4 m = ldv4<YH>(a.e.aux0, pix * a.e.ld0 + n);
+                                o[0] = m.x > 0.f ? o[0] : 0.f;
+                                o[1] = m.y > 0.f ? o[1] : 0.f;
+                                o[2] = m.z > 0.f ? o[2] : 0.f;
+                                o[3] = m.w > 0.f ? o[3] : 0.f;
+                            }
+                            if constexpr (!YH) {
+                                float* yp = a.y + pix * g.ldy + n;
+                                if (a.e.accumulate) {
+                                    const float4 p = ld4(yp);
+                                    o[0] += p.x; o[1] += p.y; o[2] += p.z; o[3] += p.w;
+                                }
+                                st4(yp, make_float4(o[0], o[1], o[2], o[3]));
+                            } else {
+                                stv4<true>(a.y, pix * g.ldy + n, make_float4(o[0], o[1], o[2], o[3]));
+                            }
+                        } else {
+                            epi_store4<YH>(a.e, a.y, g.ldy, pix, n, v, slope);
+                        }
+                    }
+                }
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[at][r] = 0.f;
+            }
+        }
+        if (s + 1 < steps) hstore(hs, (s + 1) & 1);
+        __syncthreads();
+    };
+    float4 hA[WRES_HV], hB[WRES_HV];
+    if (steps > 0) {
+        hload(hA, 0);
+        hstore(hA, 0);
+    }
+    if (steps > 1) hload(hB, 1);
+    __syncthreads();
+    for (int s = 0; s < steps; s += 2) {
+        body(s, hA, hB);
+        if (s + 1 < steps) body(s + 1, hB, hA);
     }
 }
 
@@ -2663,6 +2886,49 @@ static bool halo16_ok(const hyres_conv_geom* g, const hyres_epilogue* e) {
     return true;
 }
 
+// conv3x3_wres_f16_kernel: the halo16 geometry with Ci == 64, enough 256-pixel tiles per block to amortise
+// the one-time weight conversion (>= 2 per block); HYRES_CONV_WRES16=0 turns it off
+static int g_cus = 0;
+static int num_cus() {
+    if (!g_cus) {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                     hipSuccess || n < 1)
+            n = 256;
+        g_cus = n;
+    }
+    return g_cus;
+}
+
+static bool wres16_ok(const hyres_conv_geom* g) {
+    static const int on = env_int("HYRES_CONV_WRES16", 1);
+    if (!on || g->Ci != 64) return false;
+    const long long tiles = (long long)g->B * ((g->Ho + HALO_R - 1) / HALO_R) * (g->Wo / HALO_TW);
+    const int groups = g->Co / 64;
+    return tiles >= 2LL * std::max(1, num_cus() / groups) && (long long)g->B * g->Hi * g->Wi * g->ldx * 4 < 0x7FFFFFF0LL;
+}
+
+static int launch_wres16(const ConvArgs& a, hipStream_t st) {
+    const hyres_conv_geom& g = a.g;
+    const int ntiles = g.B * ((g.Ho + HALO_R - 1) / HALO_R) * (g.Wo / HALO_TW);
+    const int groups = g.Co / 64;
+    const int per = std::max(1, num_cus() / groups);
+    const dim3 grid(per * groups);
+    static const int variant = env_int("HYRES_WRES_VARIANT", 1);
+    if (a.e.io_f16 == 0 && variant != 1) {  // tuning variants (fp32 activations only)
+        if (variant == 0) hipLaunchKernelGGL((conv3x3_wres_f16_kernel<0, 0>), grid, dim3(512), 0, st, a, ntiles, groups);
+        else hipLaunchKernelGGL((conv3x3_wres_f16_kernel<0, 2>), grid, dim3(512), 0, st, a, ntiles, groups);
+        return HY_LAUNCH_CHECK("conv3x3_wres_f16_kernel");
+    }
+    switch (a.e.io_f16) {
+        case 0: hipLaunchKernelGGL(conv3x3_wres_f16_kernel<0>, grid, dim3(512), 0, st, a, ntiles, groups); break;
+        case 1: hipLaunchKernelGGL(conv3x3_wres_f16_kernel<1>, grid, dim3(512), 0, st, a, ntiles, groups); break;
+        case 2: hipLaunchKernelGGL(conv3x3_wres_f16_kernel<2>, grid, dim3(512), 0, st, a, ntiles, groups); break;
+        default: hipLaunchKernelGGL(conv3x3_wres_f16_kernel<3>, grid, dim3(512), 0, st, a, ntiles, groups); break;
+    }
+    return HY_LAUNCH_CHECK("conv3x3_wres_f16_kernel");
+}
+
 static int launch_halo16(const ConvArgs& a, hipStream_t st) {
     const hyres_conv_geom& g = a.g;
     const int blocks = g.B * ((g.Ho + HALO_R - 1) / HALO_R) * (g.Wo / HALO_TW) * (g.Co / 64);
@@ -2872,7 +3138,7 @@ int hyres_conv_forward(const hyres_conv_geom* g, const float* x, const float* w2
     }
     if (mode == 0 && a.vec4 && halo16_ok(g, e)) {
         a.nsplit = 1;
-        return launch_halo16(a, st);
+        return wres16_ok(g) ? launch_wres16(a, st) : launch_halo16(a, st);
     }
     {
         const int nt = stream_nt(g, e);
@@ -2915,7 +3181,7 @@ int hyres_conv_kernel_name(const hyres_conv_geom* g, const hyres_epilogue* e, in
         return 0;
     }
     if (ch.mode == 0 && halo16_ok(g, e)) {
-        snprintf(buf, n, "conv3x3_halo_f16_kernel<%d>", e->io_f16);
+        snprintf(buf, n, "%s<%d>", wres16_ok(g) ? "conv3x3_wres_f16_kernel" : "conv3x3_halo_f16_kernel", e->io_f16);
         return 0;
     }
     {

@@ -777,6 +777,13 @@ def test_fp16_activation_ops():
         yo64 = O.conv2d(None, x64, w, b, pad=1)
         assert not yo64.half
         assert rel_err(O.to_nchw(yo64).cpu(), O.to_nchw(O.conv2d(None, f32(x64), w, b, pad=1)).cpu()) < 1e-5
+        # enough tiles for the weight-resident persistent kernel (IO 3 and IO 1)
+        xw, rw = _nhwc16(_rand((4, 64, 128, 256), 9)), _nhwc16(_rand((4, 64, 128, 256), 10))
+        with O.f16_region():
+            yw = O.conv2d(None, xw, w, b, pad=1, act=L.ACT_RELU, res=rw)
+        chk(yw, O.conv2d(None, f32(xw), w, b, pad=1, act=L.ACT_RELU, res=f32(rw)), "wres conv res relu")
+        yow = O.conv2d(None, xw, w, b, pad=1)
+        assert rel_err(O.to_nchw(yow).cpu(), O.to_nchw(O.conv2d(None, f32(xw), w, b, pad=1)).cpu()) < 1e-5
         # image side: fp32 X (Ci=3, scalar path) -> fp16 Y; 5x5 s2
         xi = O.to_nhwc(_rand((2, 3, 32, 40), 5).to(D))
         wi = _rand((128, 3, 5, 5), 6, 1.0 / 75 ** 0.5).to(D)
@@ -1248,7 +1255,10 @@ AMP_CASES = [(2, 64, 64, 16, 16, 3, 1, 1, 1), (2, 128, 192, 16, 16, 5, 2, 2, 1),
              (2, 64, 64, 32, 32, 3, 1, 1, 1), (2, 64, 96, 32, 64, 3, 1, 2, 2), (2, 64, 96, 64, 64, 5, 2, 2, 1),
              # W a multiple of 64, Co of 64: the halo-staged f16 3x3 conv (conv3x3_halo_f16_kernel) in the forward
              # and (Ci = 64 / 128) the input gradient; H = 10 leaves a partial 4-row tile, Ci = 96 three chunks
-             (2, 64, 64, 16, 64, 3, 1, 1, 1), (1, 96, 128, 10, 128, 3, 1, 1, 1), (2, 128, 64, 8, 64, 3, 1, 1, 1)]
+             (2, 64, 64, 16, 64, 3, 1, 1, 1), (1, 96, 128, 10, 128, 3, 1, 1, 1), (2, 128, 64, 8, 64, 3, 1, 1, 1),
+             # Ci = 64 with >= 2 tiles per CU: the weight-resident persistent kernel (conv3x3_wres_f16_kernel), one
+             # and two 64-channel output groups, a partial last row tile
+             (4, 64, 64, 128, 256, 3, 1, 1, 1), (2, 64, 128, 128, 256, 3, 1, 1, 1), (4, 64, 64, 126, 256, 3, 1, 1, 1)]
 
 
 @pytest.mark.parametrize("case", AMP_CASES)
