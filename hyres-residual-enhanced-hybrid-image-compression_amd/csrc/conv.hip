@@ -969,7 +969,15 @@ __global__ __launch_bounds__(512, 2) void conv3x3_wres_f16_kernel(const ConvArgs
 // epilogue streams a second operand (residual, ReLU mask, old y) stay on the tiled kernel: prefetching
 // that operand per wave tile doubles the registers (2 waves/SIMD) and measured slower than the tiles
 // (128^2 64->128 +res 95 vs 92 us, 64^2 27 vs 24 us; profiles/r2_micro_1x1_stream.txt).
-template <int NT, int KC>
+// R16 (autocast, f16_operands): both operands are rounded to fp16 as they are loaded, and the products of
+// those fp16 values are formed exactly by the fp32 MFMA with fp32 accumulation — the same arithmetic as the
+// f16 MFMA (whose products of fp16 inputs are exact in fp32) up to the summation order. These layers are
+// HBM-bound (<= 128 FLOP per output element), so the f16 rate buys nothing and the streaming structure does.
+__device__ __forceinline__ float4 round_f16(float4 v) {
+    return make_float4((float)(_Float16)v.x, (float)(_Float16)v.y, (float)(_Float16)v.z, (float)(_Float16)v.w);
+}
+
+template <int NT, int KC, bool R16 = false>
 __global__ __launch_bounds__(256, 2) void conv1x1_stream_kernel(const ConvArgs a) {
     constexpr int K = 8 * KC, KP = K + 4, CO = 32 * NT;
     __shared__ __attribute__((aligned(16))) float Ws[CO * KP];
@@ -979,7 +987,9 @@ __global__ __launch_bounds__(256, 2) void conv1x1_stream_kernel(const ConvArgs a
     const int lr = lane & 31, lh = lane >> 5;
     for (int i = tid; i < CO * (K / 4); i += 256) {
         const int co = i / (K / 4), k4 = i - co * (K / 4);
-        *reinterpret_cast<float4*>(&Ws[co * KP + 4 * k4]) = ld4(a.w2 + (long long)co * a.ldw + 4 * k4);
+        float4 w = ld4(a.w2 + (long long)co * a.ldw + 4 * k4);
+        if constexpr (R16) w = round_f16(w);
+        *reinterpret_cast<float4*>(&Ws[co * KP + 4 * k4]) = w;
     }
     __shared__ __attribute__((aligned(16))) float bs[CO];
     for (int i = tid; i < CO; i += 256) bs[i] = e.bias ? e.bias[i] : 0.f;
@@ -1013,7 +1023,8 @@ __global__ __launch_bounds__(256, 2) void conv1x1_stream_kernel(const ConvArgs a
             float4 bv[NT];
 #pragma unroll
             for (int t = 0; t < NT; ++t) bv[t] = *reinterpret_cast<const float4*>(&Ws[(32 * t + lr) * KP + 8 * j + 4 * lh]);
-            const float4 x = av[j];
+            float4 x = av[j];
+            if constexpr (R16) x = round_f16(x);
 #pragma unroll
             for (int t = 0; t < NT; ++t) {
                 acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(bv[t].x, x.x, acc[t], 0, 0, 0);
@@ -2670,7 +2681,8 @@ static int launch_stream_one(const ConvArgs& a, int blocks_per_cu, hipStream_t s
     }
     const int per_cu = blocks_per_cu > 0 ? std::min(occ, blocks_per_cu) : occ;
     const int blocks = std::max(1, std::min(ceil_div(ceil_div(a.M, 32), 4), 256 * per_cu));
-    hipLaunchKernelGGL((conv1x1_stream_kernel<NT, KC>), dim3(blocks), dim3(256), 0, st, a);
+    if (a.e.f16_operands) hipLaunchKernelGGL((conv1x1_stream_kernel<NT, KC, true>), dim3(blocks), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((conv1x1_stream_kernel<NT, KC>), dim3(blocks), dim3(256), 0, st, a);
     return HY_LAUNCH_CHECK("conv1x1_stream_kernel");
 }
 
@@ -2961,8 +2973,9 @@ struct ConvChoice {
 // old y), grids >= HYRES_CONV_STREAM_PIXELS output pixels (default 65536). Returns NT (Co / 32) or 0.
 static int stream_nt(const hyres_conv_geom* g, const hyres_epilogue* e) {
     static const int on = env_int("HYRES_CONV_STREAM1X1", 1);
+    static const int on16 = env_int("HYRES_CONV_STREAM1X1_F16", 1);  // autocast: fp16-rounded operands
     static const long long min_px = env_int("HYRES_CONV_STREAM_PIXELS", 65536);
-    if (!on || e->f16_operands || e->io_f16 || e->square_input || e->kind != HYRES_EPI_BIAS) return 0;
+    if (!on || (e->f16_operands && !on16) || e->io_f16 || e->square_input || e->kind != HYRES_EPI_BIAS) return 0;
     if (g->nphase != 1 || g->ntaps != 1 || g->ish != 1 || g->isw != 1 || g->dh[0] != 0 || g->dw[0] != 0) return 0;
     if (g->Hi != g->Hq || g->Wi != g->Wq || g->Ho != g->Hq || g->Wo != g->Wq) return 0;
     if ((long long)g->B * g->Hq * g->Wq < min_px) return 0;
@@ -3187,7 +3200,7 @@ int hyres_conv_kernel_name(const hyres_conv_geom* g, const hyres_epilogue* e, in
     {
         const int nt = stream_nt(g, e);
         if (nt && ch.mode == 0) {
-            snprintf(buf, n, "conv1x1_stream_kernel<%d, %d>", nt, g->Ci / 8);
+            snprintf(buf, n, "conv1x1_stream_kernel<%d, %d%s>", nt, g->Ci / 8, e->f16_operands ? ", true" : "");
             return 0;
         }
     }

@@ -466,7 +466,8 @@ class KernelTimer:
         cls.table = []
 
     @classmethod
-    def summary(cls):
+    def groups(cls):
+        """{instantiation: [total ms, FLOPs, algorithmic bytes, launches]} of the recorded launches."""
         torch.cuda.synchronize()
         groups = {}
         for s0, s1, fl, by, var in cls.events:
@@ -475,10 +476,22 @@ class KernelTimer:
             e[1] += fl
             e[2] += by
             e[3] += 1
+        return groups
+
+    @classmethod
+    def summary(cls, pick=None):
+        """The instantiation with the largest total time (or the largest among those ``pick(name, group)``
+        accepts)."""
+        groups = cls.groups()
+        if pick is not None:
+            groups_all = groups
+            groups = {k: v for k, v in groups.items() if pick(k, v)}
         if not groups:
             return {"kernel": None, "launches": 0, "total_ms": 0.0, "avg_us": 0.0, "flops": 0.0,
                     "flops_per_launch": 0.0, "bytes_per_launch": 0.0}
         var, (ms, flops, nbytes, n) = max(groups.items(), key=lambda kv: kv[1][0])
+        if pick is not None:
+            groups = groups_all
         return {"kernel": var, "launches": n, "total_ms": ms, "avg_us": 1000.0 * ms / n, "flops": flops,
                 "flops_per_launch": flops / n, "bytes_per_launch": nbytes / n,
                 "by_variant_ms": {k: round(v[0], 3) for k, v in groups.items()}}

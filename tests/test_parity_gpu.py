@@ -1258,7 +1258,9 @@ AMP_CASES = [(2, 64, 64, 16, 16, 3, 1, 1, 1), (2, 128, 192, 16, 16, 5, 2, 2, 1),
              (2, 64, 64, 16, 64, 3, 1, 1, 1), (1, 96, 128, 10, 128, 3, 1, 1, 1), (2, 128, 64, 8, 64, 3, 1, 1, 1),
              # Ci = 64 with >= 2 tiles per CU: the weight-resident persistent kernel (conv3x3_wres_f16_kernel), one
              # and two 64-channel output groups, a partial last row tile
-             (4, 64, 64, 128, 256, 3, 1, 1, 1), (2, 64, 128, 128, 256, 3, 1, 1, 1), (4, 64, 64, 126, 256, 3, 1, 1, 1)]
+             (4, 64, 64, 128, 256, 3, 1, 1, 1), (2, 64, 128, 128, 256, 3, 1, 1, 1), (4, 64, 64, 126, 256, 3, 1, 1, 1),
+             # >= 65536 pixels, 1x1: the streaming 1x1 kernel on fp16-rounded operands
+             (4, 64, 128, 128, 128, 1, 1, 0, 1), (4, 128, 64, 128, 128, 1, 1, 0, 1)]
 
 
 @pytest.mark.parametrize("case", AMP_CASES)
