@@ -151,7 +151,17 @@ def test_conv_kernel_name_follows_the_launch_routing():
     assert conv_variant(g2, e, False) == "conv_fwd_kernel<1, 2, 2, 2, 1, false, false>"
     e.square_input = 0
     e.f16_operands = 1
-    assert conv_variant(g3, e, False) == "conv_fwd_kernel<2, 1, 2, 2, 0, false, true>"
+    # autocast 3x3, Ci = 64, >= 2 tiles of 4 x 64 pixels per CU: the weight-resident persistent kernel; fewer
+    # tiles or Ci != 64: the halo-staged kernel; W % 64 != 0: the implicit-GEMM tiles
+    assert conv_variant(g3, e, False) == "conv3x3_wres_f16_kernel<0>"
+    gh = _geom("hyres_geom_conv2d", 2, 64, 64, 64, 64, 64, 64, 3, 3, 1, 1, 1)
+    assert conv_variant(gh, e, False) == "conv3x3_halo_f16_kernel<0>"
+    gh2 = _geom("hyres_geom_conv2d", 16, 128, 128, 96, 96, 64, 64, 3, 3, 1, 1, 1)
+    assert conv_variant(gh2, e, False) == "conv3x3_halo_f16_kernel<0>"
+    gw = _geom("hyres_geom_conv2d", 16, 32, 32, 64, 64, 64, 64, 3, 3, 1, 1, 1)
+    assert conv_variant(gw, e, False) == "conv_fwd_kernel<1, 1, 2, 2, 0, false, true>"
+    # autocast 1x1 (K <= 128, >= 64k pixels): the streaming kernel on fp16-rounded operands
+    assert conv_variant(g1, e, False) == "conv1x1_stream_kernel<4, 8, true>"
     # small grids (<= 65536 output pixels): 64-row tiles; f16 takes 128x128 from 192 channels up
     e.f16_operands = 0
     s3 = _geom("hyres_geom_conv2d", 16, 32, 32, 96, 96, 96, 96, 3, 3, 1, 1, 1)
@@ -163,7 +173,8 @@ def test_conv_kernel_name_follows_the_launch_routing():
     assert conv_variant(s3, e, False) == "conv_fwd_kernel<1, 1, 2, 2, 0, false, true>"
     # fp16 activations (autocast inference): conv_fwd_h_kernel<tile, mode, split, io>
     e.io_f16 = 3
-    assert conv_variant(g3, e, False) == "conv_fwd_h_kernel<2, 1, 2, 2, 0, false, 3>"
+    assert conv_variant(g3, e, False) == "conv3x3_wres_f16_kernel<3>"
+    assert conv_variant(g1b, e, False) == "conv_fwd_h_kernel<2, 1, 2, 2, 0, false, 3>"
     assert conv_variant(g1, e, False) == "conv_fwd_h_kernel<1, 2, 2, 2, 0, false, 3>"  # not the fp32 stream kernel
     e.io_f16 = 2
     e.f16_operands = 0
