@@ -769,8 +769,6 @@ __global__ __launch_bounds__(512, 2) void conv3x3_wres_f16_kernel(const ConvArgs
     const int tbeg = xcd * q + min(xcd, rr8), tcnt = q + (xcd < rr8 ? 1 : 0);
     const int mytiles = jx < tcnt ? (tcnt - 1 - jx) / nx + 1 : 0;
     if (tid < 9) tapoff[tid] = make_int2(g.dh[tid], g.dw[tid]);
-    __shared__ __attribute__((aligned(16))) float bias_s[64];
-    if (tid < 64) bias_s[tid] = a.e.bias ? a.e.bias[n0 + tid] : 0.f;
 
     // ---- the 64-channel weight slice, fp32 W2[co][t][ci] -> fp16 Bs[(c*9 + t)*64 + co][k] (ci = 32c + k)
     for (int f = tid; f < 64 * 9 * 16; f += 512) {
@@ -894,42 +892,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3_wres_f16_kernel(const ConvArgs
                         const int n = n0 + 32 * wn + 8 * qd + 4 * lh;
                         const float4 v = make_float4(acc[at][4 * qd], acc[at][4 * qd + 1], acc[at][4 * qd + 2],
                                                      acc[at][4 * qd + 3]);
-                        if (V < 2) {
-                            epi_store4<YH>(a.e, a.y, g.ldy, pix, n, v, slope, pre_res ? &rres[at][qd] : nullptr);
-                        } else if (a.e.kind == HYRES_EPI_BIAS) {
-                            const float4 bb = *reinterpret_cast<const float4*>(&bias_s[n - n0]);
-                            float o[4] = {v.x + bb.x, v.y + bb.y, v.z + bb.z, v.w + bb.w};
-                            if (a.e.res) {
-                                const float4 r = pre_res ? rres[at][qd] : ldv4<YH>(a.e.res, pix * a.e.ldres + n);
-                                o[0] += r.x; o[1] += r.y; o[2] += r.z; o[3] += r.w;
-                            }
-                            if (a.e.out2) stv4<YH>(a.e.out2, pix * a.e.ldo2 + n, make_float4(o[0], o[1], o[2], o[3]));
-                            if (a.e.act == HYRES_ACT_RELU) {
-#pragma unroll
-                                for (int cc = 0; cc < 4; ++cc) o[cc] = fmaxf(o[cc], 0.f);
-                            } else if (a.e.act == HYRES_ACT_PRELU) {
-#pragma unroll
-                                for (int cc = 0; cc < 4; ++cc) o[cc] = o[cc] >= 0.f ? o[cc] : slope * o[cc];
-                            } else if (a.e.act == HYRES_ACT_RELU_MASK) {
-                                const float4 m = ldv4<YH>(a.e.aux0, pix * a.e.ld0 + n);
-                                o[0] = m.x > 0.f ? o[0] : 0.f;
-                                o[1] = m.y > 0.f ? o[1] : 0.f;
-                                o[2] = m.z > 0.f ? o[2] : 0.f;
-                                o[3] = m.w > 0.f ? o[3] : 0.f;
-                            }
-                            if constexpr (!YH) {
-                                float* yp = a.y + pix * g.ldy + n;
-                                if (a.e.accumulate) {
-                                    const float4 p = ld4(yp);
-                                    o[0] += p.x; o[1] += p.y; o[2] += p.z; o[3] += p.w;
-                                }
-                                st4(yp, make_float4(o[0], o[1], o[2], o[3]));
-                            } else {
-                                stv4<true>(a.y, pix * g.ldy + n, make_float4(o[0], o[1], o[2], o[3]));
-                            }
-                        } else {
-                            epi_store4<YH>(a.e, a.y, g.ldy, pix, n, v, slope);
-                        }
+                        epi_store4<YH>(a.e, a.y, g.ldy, pix, n, v, slope, pre_res ? &rres[at][qd] : nullptr);
                     }
                 }
 #pragma unroll
@@ -2927,9 +2890,8 @@ static int launch_wres16(const ConvArgs& a, hipStream_t st) {
     const int per = std::max(1, num_cus() / groups);
     const dim3 grid(per * groups);
     static const int variant = env_int("HYRES_WRES_VARIANT", 1);
-    if (a.e.io_f16 == 0 && variant != 1) {  // tuning variants (fp32 activations only)
-        if (variant == 0) hipLaunchKernelGGL((conv3x3_wres_f16_kernel<0, 0>), grid, dim3(512), 0, st, a, ntiles, groups);
-        else hipLaunchKernelGGL((conv3x3_wres_f16_kernel<0, 2>), grid, dim3(512), 0, st, a, ntiles, groups);
+    if (a.e.io_f16 == 0 && variant == 0) {  // A/B: halo prefetch issued before the residual loads
+        hipLaunchKernelGGL((conv3x3_wres_f16_kernel<0, 0>), grid, dim3(512), 0, st, a, ntiles, groups);
         return HY_LAUNCH_CHECK("conv3x3_wres_f16_kernel");
     }
     switch (a.e.io_f16) {
