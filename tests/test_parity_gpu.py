@@ -1454,3 +1454,36 @@ def test_amp_matches_reference_autocast_fixture():
     print(f"AMP train gradient norms vs reference AMP: global {glob:.3e}, median {med:.3e}, worst {rel[:3]}")
     assert eval_ok and all(terms)
     assert glob < 0.05 and med < 0.05
+
+
+@pytest.mark.parametrize("K,Ci,Co,H", [(3, 64, 64, 128), (1, 128, 64, 128), (1, 64, 128, 128)])
+def test_wgrad_many_split_reduce_deterministic(K, Ci, Co, H):
+    """Weight + bias gradients with >= 64 split-K slabs (bs 16: the two-pass row-streaming reduce,
+    wgrad_reduce_rows_kernel + wgrad_reduce_final_kernel) against torch fp32 (1e-5), and bit-identical
+    across two runs (the reduce sums in a fixed order: no atomics)."""
+    import ctypes
+    from hyres_hip import _lib as L
+    D = dev()
+    B = 16
+    x = _rand((B, H, H, Ci), 71).to(D)
+    gy = _rand((B, H, H, Co), 72).to(D)
+    d = L.WgradDesc()
+    L.call("hyres_wgrad_desc_conv2d", ctypes.byref(d), B, H, H, Ci, Ci, Co, Co, K, K, 1, K // 2, 1)
+    d.sm = Ci * K * K
+    nb = L.load().hyres_wgrad_workspace_bytes(ctypes.byref(d))
+    ws = torch.empty(nb // 4 + 16, device=D)
+    outs = []
+    for _ in range(2):
+        dw = torch.zeros(Co, Ci, K, K, device=D)
+        db = torch.zeros(Co, device=D)
+        L.call("hyres_conv_wgrad", ctypes.byref(d), gy.data_ptr(), x.data_ptr(), dw.data_ptr(), db.data_ptr(),
+               ws.data_ptr(), nb, L.stream())
+        torch.cuda.synchronize()
+        outs.append((dw.clone(), db.clone()))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    xr = x.cpu().permute(0, 3, 1, 2).contiguous().requires_grad_(False)
+    gyr = gy.cpu().permute(0, 3, 1, 2).contiguous()
+    wr = torch.zeros(Co, Ci, K, K, requires_grad=True)
+    F.conv2d(xr, wr, None, padding=K // 2).backward(gyr)
+    assert rel_err(outs[0][0].cpu(), wr.grad) < 1e-5
+    assert rel_err(outs[0][1].cpu(), gyr.sum((0, 2, 3))) < 1e-5
