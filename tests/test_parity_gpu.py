@@ -1458,9 +1458,9 @@ def test_amp_matches_reference_autocast_fixture():
 
 @pytest.mark.parametrize("K,Ci,Co,H", [(3, 64, 64, 128), (1, 128, 64, 128), (1, 64, 128, 128)])
 def test_wgrad_many_split_reduce_deterministic(K, Ci, Co, H):
-    """Weight + bias gradients with >= 64 split-K slabs (bs 16: the two-pass row-streaming reduce,
-    wgrad_reduce_rows_kernel + wgrad_reduce_final_kernel) against torch fp32 (1e-5), and bit-identical
-    across two runs (the reduce sums in a fixed order: no atomics)."""
+    """Weight + bias gradients at bs 16 (hundreds of split-K slabs and the fused bias partials, reduced by
+    wgrad_bias_reduce_kernel) against torch fp32 (1e-5), and bit-identical across two runs (the split reduce
+    sums in a fixed order: no atomics)."""
     import ctypes
     from hyres_hip import _lib as L
     D = dev()
