@@ -916,6 +916,143 @@ __global__ __launch_bounds__(512, 2) void conv3x3_wres_f16_kernel(const ConvArgs
 }
 
 // ------------------------------------------------------------------------------------------------
+// Weight-resident persistent fp32 3x3 conv, Ci = 64 (the fp32 headline path's dominant family: the 64-channel
+// 3x3 convs of the ResidualUnits / RBBs / MultiScaleRefine at 64^2..256^2 and their input-gradients, the
+// `conv_fwd_kernel<2, 1, 2, 2, 0, false, false>` population). That implicit-GEMM kernel is MFMA-bound at
+// ~0.6-0.7 of the fp32 peak isolated: each 32-deep K chunk costs two barriers, a register->LDS store of
+// 24 KB and a re-gather of the shifted A rows from L2, against 32 MFMAs per wave. Here one 512-thread block
+// per CU holds the fp32 weights of a 32-channel output slice in LDS (9 taps x 32 co x 64 ci, 36-float rows:
+// 83 KB) for the whole launch and walks 4-row x 64-pixel tiles; per tile and 32-channel chunk only the
+// 6 x 66-pixel fp32 halo moves (7 float4 per thread, loaded during the previous chunk's MFMAs), so a wave
+// issues 144 MFMAs (9 taps x 16 k-steps) per barrier pair. Fragments as in conv_fwd_body (k-permuted rows:
+// one ds_read_b128 feeds 4 MFMA steps, 36-float pitch conflict-free); the product is formed transposed
+// (C^T = W X^T) so the epilogue stores float4 from the accumulators. 8 waves = 4 output rows x 2 pixel
+// halves, one 32 x 32 accumulator each. Exact fp32 (v_mfma_f32_32x32x2f32), the same sums per output as
+// the implicit-GEMM kernel up to the K order.
+constexpr int WF_PK = 36;  // floats per staged row (32 + 4 pad)
+constexpr int WF_LDS_W = 2 * 9 * 32 * WF_PK;
+constexpr int WF_LDS_H = HALO_NPX * WF_PK;
+
+__global__ __launch_bounds__(512, 2) void conv3x3_wres_f32_kernel(const ConvArgs a, int ntiles, int groups) {
+    __shared__ __attribute__((aligned(16))) float lds[WF_LDS_W + WF_LDS_H];
+    __shared__ int2 tapoff[9];
+    float* const Ws = lds;
+    float* const Hs = lds + WF_LDS_W;
+    const hyres_conv_geom& g = a.g;
+    const int tid = threadIdx.x;
+    const int nrt = (g.Ho + HALO_R - 1) / HALO_R, nct = g.Wo / HALO_TW;
+    const int nb = gridDim.x / groups;
+    const int grp = blockIdx.x % groups, bg = blockIdx.x / groups;
+    const int n0 = grp * 32;
+    const int xcd = bg & 7, nx = (nb + 7 - xcd) >> 3, jx = bg >> 3;
+    const int q = ntiles >> 3, rr8 = ntiles & 7;
+    const int tbeg = xcd * q + min(xcd, rr8), tcnt = q + (xcd < rr8 ? 1 : 0);
+    const int mytiles = jx < tcnt ? (tcnt - 1 - jx) / nx + 1 : 0;
+    if (tid < 9) tapoff[tid] = make_int2(g.dh[tid], g.dw[tid]);
+    // weights W2[co][t][ci] -> Ws[((c*9 + t)*32 + co)*36 + k], ci = 32c + k
+    for (int f = tid; f < 32 * 9 * 16; f += 512) {
+        const int co = f / 144, rem = f - co * 144, t = rem >> 4, ci = 4 * (rem & 15);
+        *reinterpret_cast<float4*>(&Ws[(((ci >> 5) * 9 + t) * 32 + co) * WF_PK + (ci & 31)]) =
+            ld4(a.w2 + (long long)(n0 + co) * a.ldw + t * 64 + ci);
+    }
+    const long long img = (long long)g.Hi * g.Wi * g.ldx;
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)a.x, (short)0, (int)std::min<long long>((long long)g.B * img * 4, 0x7FFFFFF0LL), 0x00020000);
+    const int lane = tid & 63, wave = tid >> 6;
+    const int orow = wave & 3, ph = wave >> 2;  // output row in the tile, 32-pixel half
+    const int lr = lane & 31, lh = lane >> 5;
+
+    auto tile_of = [&](int k, int& b, int& i0, int& j0) {
+        int l = tbeg + jx + k * nx;
+        const int rt = l % nrt; l /= nrt;
+        const int ct = l % nct;
+        b = l / nct;
+        i0 = rt * HALO_R;
+        j0 = ct * HALO_TW;
+    };
+    float4 hreg[WRES_HV];
+    auto hload = [&](int step) {
+        int b, i0, j0;
+        tile_of(step >> 1, b, i0, j0);
+        const int c = step & 1;
+        const int base = b * (int)img;
+#pragma unroll
+        for (int v = 0; v < WRES_HV; ++v) {
+            const int e = tid + 512 * v;
+            const int px = e >> 3, c4 = e & 7;
+            const int hr = px / HALO_HW, hc = px - hr * HALO_HW;
+            const int ih = i0 - 1 + hr, iw = j0 - 1 + hc;
+            const bool ok = e < HALO_E && (unsigned)ih < (unsigned)g.Hi && (unsigned)iw < (unsigned)g.Wi;
+            const int off = ok ? (base + (ih * g.Wi + iw) * g.ldx + 32 * c + 4 * c4) * 4 : (int)0x80000000;
+            hreg[v] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
+        }
+    };
+    auto hstore = [&]() {
+#pragma unroll
+        for (int v = 0; v < WRES_HV; ++v) {
+            const int e = tid + 512 * v;
+            if (e < HALO_E) *reinterpret_cast<float4*>(&Hs[(e >> 3) * WF_PK + 4 * (e & 7)]) = hreg[v];
+        }
+    };
+    floatx16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    const float slope = (a.e.act == HYRES_ACT_PRELU) ? a.e.slope[0] : 0.f;
+    const bool pre_res = a.e.kind == HYRES_EPI_BIAS && a.e.res != nullptr;
+    float4 rres[4];
+    const int steps = mytiles * 2;
+    if (steps > 0) {
+        hload(0);
+        hstore();
+    }
+    __syncthreads();
+    for (int s = 0; s < steps; ++s) {
+        const int k = s >> 1, c = s & 1;
+        int b, i0, j0;
+        tile_of(k, b, i0, j0);
+        const int i = i0 + orow;
+        const long long pix = ((long long)b * g.Ho + i) * g.Wo + j0 + 32 * ph + lr;
+        if (c == 1 && pre_res) {  // the epilogue's residual, issued before the next halo (vmcnt order)
+#pragma unroll
+            for (int qd = 0; qd < 4; ++qd)
+                rres[qd] = i < g.Ho ? ld4(a.e.res + pix * a.e.ldres + n0 + 8 * qd + 4 * lh) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        if (s + 1 < steps) hload(s + 1);
+        const float* Wc = Ws + c * 9 * 32 * WF_PK;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+            const int2 o = tapoff[t];
+            const float* arow = &Hs[((orow + 1 + o.x) * HALO_HW + 32 * ph + lr + 1 + o.y) * WF_PK + lh * 16];
+            const float* brow = &Wc[(t * 32 + lr) * WF_PK + lh * 16];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const float4 av = *reinterpret_cast<const float4*>(arow + 4 * u);
+                const float4 bv = *reinterpret_cast<const float4*>(brow + 4 * u);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(bv.x, av.x, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(bv.y, av.y, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(bv.z, av.z, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(bv.w, av.w, acc, 0, 0, 0);
+            }
+        }
+        if (c == 1) {
+            if (i < g.Ho) {
+#pragma unroll
+                for (int qd = 0; qd < 4; ++qd) {
+                    const int n = n0 + 8 * qd + 4 * lh;
+                    const float4 v = make_float4(acc[4 * qd], acc[4 * qd + 1], acc[4 * qd + 2], acc[4 * qd + 3]);
+                    epi_store4<false>(a.e, a.y, g.ldy, pix, n, v, slope, pre_res ? &rres[qd] : nullptr);
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+        }
+        __syncthreads();  // every wave is done with this chunk's halo
+        if (s + 1 < steps) hstore();
+        __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
 // Streaming 1x1 conv (K = Ci <= 128, Co = 32*NT): the K-short pointwise layers of the ResidualUnits /
 // RBBs at 64^2..256^2 sit at the fp32 ridge (64-128 FLOP per output element against 8-12 bytes), and the
 // tiled kernel above runs them as lock-stepped blocks (load, then MFMA, then epilogue), so their MFMA and
@@ -2903,6 +3040,32 @@ static int launch_wres16(const ConvArgs& a, hipStream_t st) {
     return HY_LAUNCH_CHECK("conv3x3_wres_f16_kernel");
 }
 
+// conv3x3_wres_f32_kernel: fp32 operands, the halo16 geometry with Ci == 64 and Co % 32 == 0, >= 2 tiles per
+// block; HYRES_CONV_WRES32=0 turns it off
+static bool wres32_ok(const hyres_conv_geom* g, const hyres_epilogue* e) {
+    static const int on = env_int("HYRES_CONV_WRES32", 1);
+    if (!on || e->f16_operands || e->io_f16 || e->square_input || g->nphase != 1 || g->ntaps != 9 || g->Ci != 64 ||
+        g->Co % 32 != 0)
+        return false;
+    if (g->ish != 1 || g->isw != 1 || g->Hi != g->Ho || g->Wi != g->Wo || g->Hq != g->Ho || g->Wq != g->Wo ||
+        g->Wo % HALO_TW != 0)
+        return false;
+    for (int t = 0; t < 9; ++t)
+        if (g->dh[t] < -1 || g->dh[t] > 1 || g->dw[t] < -1 || g->dw[t] > 1) return false;
+    const long long tiles = (long long)g->B * ((g->Ho + HALO_R - 1) / HALO_R) * (g->Wo / HALO_TW);
+    const int groups = g->Co / 32;
+    return tiles >= 2LL * std::max(1, num_cus() / groups) && (long long)g->B * g->Hi * g->Wi * g->ldx * 4 < 0x7FFFFFF0LL;
+}
+
+static int launch_wres32(const ConvArgs& a, hipStream_t st) {
+    const hyres_conv_geom& g = a.g;
+    const int ntiles = g.B * ((g.Ho + HALO_R - 1) / HALO_R) * (g.Wo / HALO_TW);
+    const int groups = g.Co / 32;
+    const int per = std::max(1, num_cus() / groups);
+    hipLaunchKernelGGL(conv3x3_wres_f32_kernel, dim3(per * groups), dim3(512), 0, st, a, ntiles, groups);
+    return HY_LAUNCH_CHECK("conv3x3_wres_f32_kernel");
+}
+
 static int launch_halo16(const ConvArgs& a, hipStream_t st) {
     const hyres_conv_geom& g = a.g;
     const int blocks = g.B * ((g.Ho + HALO_R - 1) / HALO_R) * (g.Wo / HALO_TW) * (g.Co / 64);
@@ -3111,6 +3274,10 @@ int hyres_conv_forward(const hyres_conv_geom* g, const float* x, const float* w2
         }
         return HY_LAUNCH_CHECK("conv_narrow_kernel");
     }
+    if (mode == 0 && a.vec4 && wres32_ok(g, e)) {
+        a.nsplit = 1;
+        return launch_wres32(a, st);
+    }
     if (mode == 0 && a.vec4 && halo16_ok(g, e)) {
         a.nsplit = 1;
         return wres16_ok(g) ? launch_wres16(a, st) : launch_halo16(a, st);
@@ -3153,6 +3320,10 @@ int hyres_conv_kernel_name(const hyres_conv_geom* g, const hyres_epilogue* e, in
     const ConvChoice ch = choose_conv(g, e, true);
     if (ch.narrow) {
         snprintf(buf, n, "conv_narrow_kernel<%d, %d>", std::min(g->Co, 4), g->Ci == 64 ? 1 : 2);
+        return 0;
+    }
+    if (ch.mode == 0 && wres32_ok(g, e)) {
+        snprintf(buf, n, "conv3x3_wres_f32_kernel");
         return 0;
     }
     if (ch.mode == 0 && halo16_ok(g, e)) {

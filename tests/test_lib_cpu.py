@@ -134,8 +134,11 @@ def test_conv_kernel_name_follows_the_launch_routing():
     e = L.Epilogue()
     e.kind = L.EPI_BIAS
     g3 = _geom("hyres_geom_conv2d", 16, 128, 128, 64, 64, 64, 64, 3, 3, 1, 1, 1)
-    assert conv_variant(g3, e, False) == "conv_fwd_kernel<2, 1, 2, 2, 0, false, false>"
-    assert conv_variant(g3, e, True) == "conv_fwd_kernel<2, 1, 2, 2, 0, true, false>"
+    # fp32 3x3 with Ci = 64, W % 64 == 0 and >= 2 tiles per block: the weight-resident persistent kernel
+    assert conv_variant(g3, e, False) == "conv3x3_wres_f32_kernel"
+    g3b = _geom("hyres_geom_conv2d", 16, 128, 128, 96, 96, 64, 64, 3, 3, 1, 1, 1)  # Ci = 96: implicit GEMM
+    assert conv_variant(g3b, e, False) == "conv_fwd_kernel<2, 1, 2, 2, 0, false, false>"
+    assert conv_variant(g3b, e, True) == "conv_fwd_kernel<2, 1, 2, 2, 0, true, false>"
     g1 = _geom("hyres_geom_conv2d", 16, 128, 128, 64, 64, 128, 128, 1, 1, 1, 0, 1)
     assert conv_variant(g1, e, False) == "conv1x1_stream_kernel<4, 8>"  # K <= 128 1x1, >= 64k pixels
     g1b = _geom("hyres_geom_conv2d", 16, 256, 256, 192, 192, 64, 64, 1, 1, 1, 0, 1)  # K = 192: not short

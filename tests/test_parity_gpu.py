@@ -61,6 +61,11 @@ CONV_CASES = [
     (1, 96, 64, 8, 64, 3, 1, 1, 1),    # partial N tile (Ci = 96), two 32-px chunks per row
     (2, 64, 64, 64, 64, 5, 2, 2, 1),   # 5x5 stride 2 (Q stride 2), one kernel row per block
     (2, 64, 128, 32, 64, 5, 1, 2, 1),  # 5x5 stride 1, two M tiles
+    # weight-resident persistent fp32 3x3 (conv3x3_wres_f32_kernel): Ci = 64, >= 2 tiles of 4 x 64 pixels per
+    # block; forward and input-gradient; a partial last row tile; one 32-channel output slice (Co = 32)
+    (2, 64, 64, 128, 256, 3, 1, 1, 1),
+    (2, 64, 64, 126, 256, 3, 1, 1, 1),
+    (4, 64, 32, 128, 256, 3, 1, 1, 1),
 ]
 
 
