@@ -97,7 +97,7 @@ def cpu_baseline(args, budget_s):
                       f"itself cannot run here (compressai absent)"}
 
 
-PMC_TRAFFIC = os.path.join(REPO, "profiles", "r2_v5_pmc_traffic.json")  # scripts/profile_round.sh r2_v5
+PMC_TRAFFIC = os.path.join(REPO, "profiles", os.environ.get("HYRES_PMC_TRAFFIC", "r3_v2_pmc_traffic.json"))  # scripts/profile_round.sh r3_v2
 EAGER_TIMED = 3  # eager steps behind the live per-launch roofline timing
 
 
@@ -110,6 +110,8 @@ def kernel_label(kernel):
         if kernel.replace(" ", "").endswith(",true>"):
             return "streaming 1x1 conv, fp16-rounded operands on the fp32 MFMA (autocast), HBM-bound"
         return "streaming 1x1 conv, fp32 MFMA, weights resident in LDS"
+    if kernel.startswith("conv3x3_wres_f32"):
+        return "weight-resident persistent 3x3 conv, fp32 MFMA, fp32 weights in LDS, halo tiles"
     if kernel.startswith("conv3x3_wres_f16"):
         return "weight-resident persistent 3x3 conv, f16 MFMA, fp16 halo tiles in LDS"
     if kernel.startswith("conv3x3_halo_f16"):

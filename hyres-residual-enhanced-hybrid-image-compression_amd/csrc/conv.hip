@@ -3012,6 +3012,15 @@ static int num_cus() {
     return g_cus;
 }
 
+// blocks per output-channel group: one per CU (persistent), or HYRES_WRES_TPB tiles per block — under the
+// concurrent branch streams of the train step a persistent grid cannot move work off CUs that are busy with
+// another kernel, smaller blocks can
+static int wres_blocks(int ntiles, int groups) {
+    static const int tpb = env_int("HYRES_WRES_TPB", 0);
+    if (tpb > 0) return std::max(1, ceil_div(ntiles, tpb));
+    return std::max(1, num_cus() / groups);
+}
+
 static bool wres16_ok(const hyres_conv_geom* g) {
     static const int on = env_int("HYRES_CONV_WRES16", 1);
     if (!on || g->Ci != 64) return false;
@@ -3024,7 +3033,7 @@ static int launch_wres16(const ConvArgs& a, hipStream_t st) {
     const hyres_conv_geom& g = a.g;
     const int ntiles = g.B * ((g.Ho + HALO_R - 1) / HALO_R) * (g.Wo / HALO_TW);
     const int groups = g.Co / 64;
-    const int per = std::max(1, num_cus() / groups);
+    const int per = wres_blocks(ntiles, groups);
     const dim3 grid(per * groups);
     static const int variant = env_int("HYRES_WRES_VARIANT", 1);
     if (a.e.io_f16 == 0 && variant == 0) {  // A/B: halo prefetch issued before the residual loads
@@ -3061,7 +3070,7 @@ static int launch_wres32(const ConvArgs& a, hipStream_t st) {
     const hyres_conv_geom& g = a.g;
     const int ntiles = g.B * ((g.Ho + HALO_R - 1) / HALO_R) * (g.Wo / HALO_TW);
     const int groups = g.Co / 32;
-    const int per = std::max(1, num_cus() / groups);
+    const int per = wres_blocks(ntiles, groups);
     hipLaunchKernelGGL(conv3x3_wres_f32_kernel, dim3(per * groups), dim3(512), 0, st, a, ntiles, groups);
     return HY_LAUNCH_CHECK("conv3x3_wres_f32_kernel");
 }

@@ -13,8 +13,11 @@ scripts/gpu_run.sh \
   "pmc_write:500:rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/${tag}_pmc_write -o run -- python3 $BENCH"
 rc=$?
 [ $rc -ne 0 ] && exit $rc
+# the dominant kernel named by the bench line's roofline (label in parentheses stripped)
+KERNEL=$(grep '^{' gpurun_out/bench_full.log | python3 -c "import json,sys; print(json.loads(sys.stdin.read())['roofline']['kernel'].split(' (')[0])")
 python3 scripts/pmc_traffic.py gpurun_out/${tag}_pmc_fetch gpurun_out/${tag}_pmc_write \
-  --kernel "conv_fwd_kernel<2, 1, 2, 2, 0, false, false>" --out gpurun_out/${tag}_pmc_traffic.json \
+  --kernel "$KERNEL" --out gpurun_out/${tag}_pmc_traffic.json \
   --command "rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE --kernel-trace --output-format csv -- python3 $BENCH" \
   > gpurun_out/pmc_traffic.log 2>&1 && \
 python3 scripts/prof_summary.py gpurun_out/${tag}_stats/run_kernel_stats.csv 11 > gpurun_out/${tag}_summary.txt
+scripts/profile_steps.sh ${tag}
