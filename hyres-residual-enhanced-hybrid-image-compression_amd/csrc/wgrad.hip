@@ -1,0 +1,1670 @@
+// Weight gradients (and bias column sums) for every Conv2d / ConvTranspose2d / GDN of the HyRES hot path on
+// CDNA4 (gfx950): dW[t][m][n] = sum_q P[q][m] * Q[shift_t(q)][n] over the batch's pixels, split-K over pixel
+// ranges into [nsplit][ntaps][M][N] slabs reduced in a fixed order (deterministic, no atomics).
+#include "conv_common.h"
+
+namespace hyres {
+
+
+// ------------------------------------------------------------------------------------------------
+// weight gradient:  out[t][m][n] = sum_q P[q][m] * Q[shift_t(q)][n]      (K = pixels q)
+//   * a block owns one (m-tile, n-tile, group of NT taps, pixel split); the P chunk is staged once
+//     and reused by all NT taps, only the shifted Q chunk is re-gathered per tap (L1/L2-hot);
+//   * ``tapn``: taps folded into the column dimension (c = t*N + n) for N <= 16 (3-channel images),
+//     so a 32-wide MFMA column tile is not 90% padding;
+//   * blocks of one pixel split are consecutive in logical order and mapped onto one XCD so their
+//     shared P/Q rows hit that XCD's L2;
+//   * split-K partials go to a [nsplit][ntaps][M][N] slab, reduced deterministically.
+// ------------------------------------------------------------------------------------------------
+struct WgradArgs {
+    hyres_wgrad_desc d;
+    const float* p;
+    const float* q;
+    float* slab;  // [nsplit][ntaps][M][N]
+    int chunks_per_split;
+    int nchunks;
+    int mtiles, ntiles, ngroups;
+    int nblocks;  // logical blocks (grid padded to a multiple of 8 for the XCD remap)
+    int tapn;
+    float* bias_slab;  // [nsplit][M] column sums of P (the bias gradient) or NULL
+};
+
+template <typename F, int... Is>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, Is...>) {
+    (f(std::integral_constant<int, Is>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+    static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+template <int TM, int TN, int WAVES_M, int WAVES_N, int NT, bool VP, bool VQ, bool SQ>
+__global__ __launch_bounds__(256) void wgrad_kernel(const WgradArgs a) {
+    constexpr int BM = 32 * TM * WAVES_M;
+    constexpr int BN = 32 * TN * WAVES_N;
+    constexpr int PP = BM + 4, PQ = BN + 4;
+    // double-buffered P/Q chunks (one barrier per step) when both fit the 64 KB static LDS
+    constexpr bool DB = (BM + BN) <= 192;
+    constexpr int NBUF = DB ? 2 : 1;
+    __shared__ __attribute__((aligned(16))) float Psm[NBUF * KT * PP];
+    __shared__ __attribute__((aligned(16))) float Qsm[NBUF * KT * PQ];
+    float* Ps = Psm;
+    float* Qs = Qsm;
+    const hyres_wgrad_desc& d = a.d;
+    const int tid = threadIdx.x;
+    // XCD-aware order: hardware block b runs on XCD b % 8; give each XCD a contiguous logical range
+    const int bid = blockIdx.x;
+    const int lb = (bid & 7) * (gridDim.x >> 3) + (bid >> 3);
+    if (lb >= a.nblocks) return;
+    int rr = lb;
+    const int mt = rr % a.mtiles; rr /= a.mtiles;
+    const int nt = rr % a.ntiles; rr /= a.ntiles;
+    const int grp = rr % a.ngroups;
+    const int split = rr / a.ngroups;
+    const int m0 = mt * BM, n0 = nt * BN;
+    const int t0 = grp * NT;
+    const int HqWq = d.Hq * d.Wq;
+    const long long Qtot = (long long)d.B * HqWq;
+    const bool tapn = a.tapn != 0;
+
+    constexpr int P_V = VP ? (KT * BM / 4 / 256) : (KT * BM / 256);
+    constexpr int Q_V = VQ ? (KT * BN / 4 / 256) : (KT * BN / 256);
+    static_assert(P_V >= 1 && Q_V >= 1, "tile too small");
+    float4 rp[VP ? P_V : 1], rq[VQ ? Q_V : 1];
+    float sp[VP ? 1 : P_V], sq[VQ ? 1 : Q_V];
+
+    // per-thread Q rows/columns (fixed for the whole kernel) and the pixel decode of the current chunk
+    int q_row[Q_V], q_col[Q_V], q_tap[Q_V];
+#pragma unroll
+    for (int i = 0; i < Q_V; ++i) {
+        const int e = tid + 256 * i;
+        q_row[i] = VQ ? e / (BN / 4) : e / BN;
+        const int c = n0 + (VQ ? (e % (BN / 4)) * 4 : e % BN);
+        if (!VQ && tapn) {
+            q_tap[i] = c / d.N;
+            q_col[i] = c - q_tap[i] * d.N;
+        } else {
+            q_tap[i] = 0;
+            q_col[i] = c;
+        }
+    }
+    int q_b[Q_V], q_i[Q_V], q_j[Q_V];
+    // pixel decode of each thread's Q rows: divisions once (first chunk of the split), then stepped by KT
+    // pixels per chunk in raster order (q_b = -1 past the end)
+    auto decode_rows = [&](int kc) {
+#pragma unroll
+        for (int i = 0; i < Q_V; ++i) {
+            const long long qq = (long long)kc * KT + q_row[i];
+            if (qq < Qtot) {
+                q_b[i] = (int)(qq / HqWq);
+                const int r = (int)(qq - (long long)q_b[i] * HqWq);
+                q_i[i] = r / d.Wq;
+                q_j[i] = r - q_i[i] * d.Wq;
+            } else {
+                q_b[i] = -1; q_i[i] = 0; q_j[i] = 0;
+            }
+        }
+    };
+    auto step_rows = [&]() {
+#pragma unroll
+        for (int i = 0; i < Q_V; ++i) {
+            if (q_b[i] < 0) continue;
+            int j = q_j[i] + KT, ii = q_i[i], b = q_b[i];
+            while (j >= d.Wq) { j -= d.Wq; ++ii; }
+            while (ii >= d.Hq) { ii -= d.Hq; ++b; }
+            q_j[i] = j; q_i[i] = ii; q_b[i] = b < d.B ? b : -1;
+        }
+    };
+    auto load_p = [&](int kc) {
+        const long long k0 = (long long)kc * KT;
+        if constexpr (VP) {
+#pragma unroll
+            for (int i = 0; i < P_V; ++i) {
+                const int e = tid + 256 * i;
+                const int row = e / (BM / 4), c = (e % (BM / 4)) * 4;
+                const long long qq = k0 + row;
+                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (qq < Qtot && m0 + c < d.M) v = ld4(a.p + qq * d.ldp + m0 + c);
+                rp[i] = v;
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < P_V; ++i) {
+                const int e = tid + 256 * i;
+                const int row = e / BM, c = e % BM;
+                const long long qq = k0 + row;
+                float v = 0.f;
+                if (qq < Qtot && m0 + c < d.M) v = a.p[qq * d.ldp + m0 + c];
+                sp[i] = v;
+            }
+        }
+    };
+    auto load_q = [&](int t) {
+#pragma unroll
+        for (int i = 0; i < Q_V; ++i) {
+            const int tt = tapn ? q_tap[i] : t;
+            bool ok = q_b[i] >= 0 && q_col[i] < d.N && tt < d.ntaps;
+            long long off = 0;
+            if (ok) {
+                const int ih = q_i[i] * d.sq + d.dh[tt], iw = q_j[i] * d.sq + d.dw[tt];
+                ok = ih >= 0 && ih < d.Hqq && iw >= 0 && iw < d.Wqq;
+                off = ((long long)(q_b[i] * d.Hqq + ih) * d.Wqq + iw) * d.ldq + q_col[i];
+            }
+            if constexpr (VQ) {
+                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (ok) v = ld4(a.q + off);
+                if constexpr (SQ) { v.x *= v.x; v.y *= v.y; v.z *= v.z; v.w *= v.w; }
+                rq[i] = v;
+            } else {
+                float v = ok ? a.q[off] : 0.f;
+                if constexpr (SQ) v *= v;
+                sq[i] = v;
+            }
+        }
+    };
+    auto store_p = [&]() {
+        if constexpr (VP) {
+#pragma unroll
+            for (int i = 0; i < P_V; ++i) {
+                const int e = tid + 256 * i;
+                const int row = e / (BM / 4), c = (e % (BM / 4)) * 4;
+                *reinterpret_cast<float4*>(&Ps[row * PP + c]) = rp[i];
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < P_V; ++i) {
+                const int e = tid + 256 * i;
+                Ps[(e / BM) * PP + e % BM] = sp[i];
+            }
+        }
+    };
+    auto store_q = [&]() {
+        if constexpr (VQ) {
+#pragma unroll
+            for (int i = 0; i < Q_V; ++i) {
+                const int e = tid + 256 * i;
+                *reinterpret_cast<float4*>(&Qs[q_row[i] * PQ + (e % (BN / 4)) * 4]) = rq[i];
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < Q_V; ++i) {
+                const int e = tid + 256 * i;
+                Qs[q_row[i] * PQ + e % BN] = sq[i];
+            }
+        }
+    };
+
+    const int lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+    const int lr = lane & 31, lh = lane >> 5;
+    floatx16 acc[NT][TM][TN];
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int k = 0; k < TN; ++k)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[j][i][k][r] = 0.f;
+
+    // bias gradient = column sums of P over all pixels: one column tile / tap group per split does it
+    const bool do_bias = a.bias_slab != nullptr && nt == 0 && grp == 0;
+    float bsum = 0.f;
+    const int kc_begin = split * a.chunks_per_split;
+    const int kc_end = min(a.nchunks, kc_begin + a.chunks_per_split);
+    if (kc_begin < kc_end) {
+        decode_rows(kc_begin);
+        load_p(kc_begin);
+        load_q(t0);
+    }
+    if constexpr (DB) {
+        // prologue: first step's operands in buffer 0; then per step: prefetch the next step's operands
+        // into registers, MFMAs on the current buffers, store the prefetch into the other buffers, ONE barrier
+        if (kc_begin < kc_end) {
+            store_p();
+            store_q();
+        }
+        __syncthreads();
+        int pcur = 0, qcur = 0;
+        for (int kc = kc_begin; kc < kc_end; ++kc) {
+            static_for<NT>([&](auto J) {
+                constexpr int j = decltype(J)::value;
+                Ps = Psm + pcur * (KT * PP);
+                Qs = Qsm + qcur * (KT * PQ);
+                const bool next_tap = j + 1 < NT;
+                const bool next_chunk = !next_tap && kc + 1 < kc_end;
+                if (next_tap) {
+                    load_q(t0 + j + 1);
+                } else if (next_chunk) {
+                    step_rows();
+                    load_p(kc + 1);
+                    load_q(t0);
+                }
+                if (j == 0 && do_bias && tid < BM) {
+#pragma unroll 8
+                    for (int k = 0; k < KT; ++k) bsum += Ps[k * PP + tid];
+                }
+#pragma unroll
+                for (int s = 0; s < KT / 2; ++s) {
+                    const int k = lh * (KT / 2) + s;
+                    float af[TM], bf[TN];
+#pragma unroll
+                    for (int tm = 0; tm < TM; ++tm) af[tm] = Ps[k * PP + wm * TM * 32 + tm * 32 + lr];
+#pragma unroll
+                    for (int tn = 0; tn < TN; ++tn) bf[tn] = Qs[k * PQ + wn * TN * 32 + tn * 32 + lr];
+#pragma unroll
+                    for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                        for (int tn = 0; tn < TN; ++tn)
+                            acc[j][tm][tn] =
+                                __builtin_amdgcn_mfma_f32_32x32x2f32(af[tm], bf[tn], acc[j][tm][tn], 0, 0, 0);
+                }
+                if (next_tap || next_chunk) {
+                    Qs = Qsm + (qcur ^ 1) * (KT * PQ);
+                    store_q();
+                    if (next_chunk) {
+                        Ps = Psm + (pcur ^ 1) * (KT * PP);
+                        store_p();
+                    }
+                }
+                __syncthreads();
+                qcur ^= 1;
+                if (!next_tap) pcur ^= 1;
+            });
+        }
+    } else {
+        for (int kc = kc_begin; kc < kc_end; ++kc) {
+            static_for<NT>([&](auto J) {
+                constexpr int j = decltype(J)::value;
+                __syncthreads();
+                if (j == 0) store_p();
+                store_q();
+                __syncthreads();
+                if (j == 0 && do_bias && tid < BM) {
+    #pragma unroll 8
+                    for (int k = 0; k < KT; ++k) bsum += Ps[k * PP + tid];
+                }
+                if (j + 1 < NT) {
+                    load_q(t0 + j + 1);
+                } else if (kc + 1 < kc_end) {
+                    step_rows();
+                    load_p(kc + 1);
+                    load_q(t0);
+                }
+    #pragma unroll
+                for (int s = 0; s < KT / 2; ++s) {
+                    const int k = lh * (KT / 2) + s;
+                    float af[TM], bf[TN];
+    #pragma unroll
+                    for (int tm = 0; tm < TM; ++tm) af[tm] = Ps[k * PP + wm * TM * 32 + tm * 32 + lr];
+    #pragma unroll
+                    for (int tn = 0; tn < TN; ++tn) bf[tn] = Qs[k * PQ + wn * TN * 32 + tn * 32 + lr];
+    #pragma unroll
+                    for (int tm = 0; tm < TM; ++tm)
+    #pragma unroll
+                        for (int tn = 0; tn < TN; ++tn)
+                            acc[j][tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[tm], bf[tn], acc[j][tm][tn], 0, 0, 0);
+                }
+            });
+        }
+    }
+    if (do_bias && tid < BM && m0 + tid < d.M) a.bias_slab[(long long)split * d.M + m0 + tid] = bsum;
+    // slab store [split][t][M][N]
+    const long long MN = (long long)d.M * d.N;
+    static_for<NT>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) {
+            const int c = n0 + wn * TN * 32 + tn * 32 + lr;
+            int t = t0 + j, n = c;
+            if (tapn) { t = c / d.N; n = c - t * d.N; }
+            if (n >= d.N || t >= d.ntaps) continue;
+            float* out = a.slab + ((long long)split * d.ntaps + t) * MN + n;
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int m = m0 + wm * TM * 32 + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                    if (m < d.M) out[(long long)m * d.N] = acc[j][tm][tn][r];
+                }
+        }
+    });
+}
+
+
+// ------------------------------------------------------------------------------------------------
+// Halo-staged weight gradient for KxK convolutions / transposed convolutions at Q stride SQ = 1 or 2 (K = 3:
+// one block does all 9 taps; K = 5: one kernel row of 5 taps per block) whose base rows are a multiple of
+// 32 pixels, so a 32-pixel K chunk is one row segment (b, i, j0..j0+31). Per chunk the block stages P
+// (32 px x 64 m) and ONE Q halo tile (KR rows x (31*SQ + K) px x 64 n) in LDS, double-buffered, and every
+// tap reads its B operand from the halo at its (dh, dw) shift (pixel k at column k*SQ + dw). The generic kernel instead gathers a shifted 32-px Q chunk per tap (9 global loads
+// and 9 barriers per chunk, the latency of each exposed at 2 blocks per CU); here it is one load of
+// 3 x 34 px per chunk and one barrier per 9 x 16 MFMAs. 64 x 64 tiles, 4 waves of 32 x 32.
+// ------------------------------------------------------------------------------------------------
+// 1x1 weight gradient (stride 1, fp32, 16B-aligned P/Q): dW[m][n] = sum_p P[p][m] Q[p][n] over the split's
+// pixel range. P and Q rows of one 32-pixel chunk are the same pixels, so both load as contiguous float4
+// rows (no tap shift / pixel decode); double-buffered [pixel][channel] LDS tiles, one barrier per chunk;
+// the bias gradient (column sums of P) rides on the A operand already in registers (one VALU add per
+// MFMA step in the wn == 0 waves) instead of a serial LDS pass per chunk.
+template <int TM, int TN, int WAVES_M, int WAVES_N>
+__global__ __launch_bounds__(256) void wgrad1x1_kernel(const WgradArgs a) {
+    constexpr int BM = 32 * TM * WAVES_M, BN = 32 * TN * WAVES_N;
+    constexpr int PP = BM + 4, PQ = BN + 4;
+    constexpr int P_V = KT * BM / 4 / 256, Q_V = KT * BN / 4 / 256;
+    static_assert(P_V >= 1 && Q_V >= 1, "tile too small");
+    __shared__ __attribute__((aligned(16))) float Psm[2 * KT * PP];
+    __shared__ __attribute__((aligned(16))) float Qsm[2 * KT * PQ];
+    const hyres_wgrad_desc& d = a.d;
+    const int tid = threadIdx.x;
+    const int bid = blockIdx.x;
+    const int lb = (bid & 7) * (gridDim.x >> 3) + (bid >> 3);  // XCD-aware order, as wgrad_kernel
+    if (lb >= a.nblocks) return;
+    int rr = lb;
+    const int mt = rr % a.mtiles; rr /= a.mtiles;
+    const int nt = rr % a.ntiles; rr /= a.ntiles;
+    const int split = rr;
+    const int m0 = mt * BM, n0 = nt * BN;
+    const long long Qtot = (long long)d.B * d.Hq * d.Wq;
+    float4 rp[P_V], rq[Q_V];
+    auto load = [&](int kc) {
+        const long long k0 = (long long)kc * KT;
+#pragma unroll
+        for (int i = 0; i < P_V; ++i) {
+            const int e = tid + 256 * i;
+            const int row = e / (BM / 4), c = (e % (BM / 4)) * 4;
+            rp[i] = (k0 + row < Qtot && m0 + c < d.M) ? ld4(a.p + (k0 + row) * d.ldp + m0 + c)
+                                                        : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int i = 0; i < Q_V; ++i) {
+            const int e = tid + 256 * i;
+            const int row = e / (BN / 4), c = (e % (BN / 4)) * 4;
+            rq[i] = (k0 + row < Qtot && n0 + c < d.N) ? ld4(a.q + (k0 + row) * d.ldq + n0 + c)
+                                                        : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    auto store = [&](int buf) {
+        float* Ps = Psm + buf * (KT * PP);
+        float* Qs = Qsm + buf * (KT * PQ);
+#pragma unroll
+        for (int i = 0; i < P_V; ++i) {
+            const int e = tid + 256 * i;
+            *reinterpret_cast<float4*>(&Ps[(e / (BM / 4)) * PP + (e % (BM / 4)) * 4]) = rp[i];
+        }
+#pragma unroll
+        for (int i = 0; i < Q_V; ++i) {
+            const int e = tid + 256 * i;
+            *reinterpret_cast<float4*>(&Qs[(e / (BN / 4)) * PQ + (e % (BN / 4)) * 4]) = rq[i];
+        }
+    };
+    const int lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+    const int lr = lane & 31, lh = lane >> 5;
+    floatx16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    const bool do_bias = a.bias_slab != nullptr && nt == 0 && wn == 0;
+    float bsum[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) bsum[i] = 0.f;
+    const int kb = split * a.chunks_per_split;
+    const int ke = min(a.nchunks, kb + a.chunks_per_split);
+    if (kb < ke) {
+        load(kb);
+        store(0);
+    }
+    __syncthreads();
+    int cur = 0;
+    for (int kc = kb; kc < ke; ++kc) {
+        const bool next = kc + 1 < ke;
+        if (next) load(kc + 1);  // in flight during this chunk's MFMAs
+        const float* Ps = Psm + cur * (KT * PP);
+        const float* Qs = Qsm + cur * (KT * PQ);
+#pragma unroll
+        for (int s2 = 0; s2 < KT / 2; ++s2) {
+            const int k = 2 * s2 + lh;
+            float av[TM], bv[TN];
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm) av[tm] = Ps[k * PP + wm * TM * 32 + tm * 32 + lr];
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn) bv[tn] = Qs[k * PQ + wn * TN * 32 + tn * 32 + lr];
+            if (do_bias) {
+#pragma unroll
+                for (int tm = 0; tm < TM; ++tm) bsum[tm] += av[tm];
+            }
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                for (int tn = 0; tn < TN; ++tn)
+                    acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[tm], bv[tn], acc[tm][tn], 0, 0, 0);
+        }
+        if (next) store(cur ^ 1);
+        __syncthreads();
+        cur ^= 1;
+    }
+    if (do_bias) {
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm) {
+            const float t = bsum[tm] + __shfl_xor(bsum[tm], 32);  // the two lane halves cover even / odd pixels
+            const int m = m0 + wm * TM * 32 + tm * 32 + lr;
+            if (lh == 0 && m < d.M) a.bias_slab[(long long)split * d.M + m] = t;
+        }
+    }
+    const long long MN = (long long)d.M * d.N;
+    float* out = a.slab + (long long)split * MN;
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) {
+            const int n = n0 + wn * TN * 32 + tn * 32 + lr;
+            if (n >= d.N) continue;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + wm * TM * 32 + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                if (m < d.M) out[(long long)m * d.N + n] = acc[tm][tn][r];
+            }
+        }
+}
+
+template <int KR, int KW, int SQ, int DIL = 1>
+__global__ __launch_bounds__(256, 2) void wgrad_halo_kernel(const WgradArgs a, int dhg, int dwg) {
+    // DIL: tap spacing (2: MultiScaleRefine's dilated 3x3, enhancement.py:44-51): the KR halo rows are DIL
+    // rows apart, the halo columns span 31*SQ + DIL*(KW-1) + 1 pixels
+    constexpr int BM = 64, BN = 64, NT = KR * KW, HC = 31 * SQ + DIL * (KW - 1) + 1;  // halo columns of a 32-px chunk
+    constexpr int PP = BM + 4, PQ = BN + 4;
+    constexpr int PSZ = KT * PP, HSZ = KR * HC * PQ;
+    constexpr int P_V = KT * BM / 4 / 256;
+    constexpr int H_E = KR * HC * (BN / 4);
+    constexpr int H_V = (H_E + 255) / 256;
+    __shared__ __attribute__((aligned(16))) float smem[2 * (PSZ + HSZ)];
+    const hyres_wgrad_desc& d = a.d;
+    const int tid = threadIdx.x;
+    const int bid = blockIdx.x;
+    const int lb = (bid & 7) * (gridDim.x >> 3) + (bid >> 3);  // XCD-aware order, as wgrad_kernel
+    if (lb >= a.nblocks) return;
+    int rr = lb;
+    const int mt = rr % a.mtiles; rr /= a.mtiles;
+    const int nt = rr % a.ntiles; rr /= a.ntiles;
+    const int grp = rr % a.ngroups;
+    const int split = rr / a.ngroups;
+    const int m0 = mt * BM, n0 = nt * BN;
+    const int t0 = grp * NT;
+    const int dh0 = dhg + grp * KR * DIL;  // the group's first kernel row offset, first column offset dwg
+    const int cpr = d.Wq / 32;
+    float4 rp[P_V], rh[H_V];
+    auto load = [&](int kc) {
+        const int b = kc / (d.Hq * cpr);
+        const int rem = kc - b * d.Hq * cpr;
+        const int i = rem / cpr;
+        const int j0 = (rem - i * cpr) * 32;
+        const long long q0 = (long long)kc * 32;
+#pragma unroll
+        for (int q = 0; q < P_V; ++q) {
+            const int e = tid + 256 * q;
+            const int row = e / (BM / 4), c = (e % (BM / 4)) * 4;
+            rp[q] = m0 + c < d.M ? ld4(a.p + (q0 + row) * d.ldp + m0 + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int q = 0; q < H_V; ++q) {
+            const int e = tid + 256 * q;
+            const int pix = e / (BN / 4), c = (e % (BN / 4)) * 4;
+            const int hr = pix / HC, hc = pix - (pix / HC) * HC;
+            const int ih = i * SQ + dh0 + DIL * hr, iw = j0 * SQ + dwg + hc;
+            const bool ok = e < H_E && (unsigned)ih < (unsigned)d.Hqq && (unsigned)iw < (unsigned)d.Wqq && n0 + c < d.N;
+            rh[q] = ok ? ld4(a.q + ((long long)(b * d.Hqq + ih) * d.Wqq + iw) * d.ldq + n0 + c)
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    // bias gradient = column sums of P, accumulated from the staging registers (this thread's channel
+    // quad (tid % 16) * 4 is fixed) and reduced once at the end: a per-chunk LDS column pass in one wave
+    // held every barrier back by that wave's extra work (256^2 3x3: 676 vs 617 us without bias)
+    const bool do_bias = a.bias_slab != nullptr && nt == 0 && grp == 0;
+    float4 bsum = make_float4(0.f, 0.f, 0.f, 0.f);
+    auto store = [&](int buf) {
+        float* Ps = smem + buf * (PSZ + HSZ);
+        float* Hs = Ps + PSZ;
+#pragma unroll
+        for (int q = 0; q < P_V; ++q) {
+            const int e = tid + 256 * q;
+            if (do_bias) { bsum.x += rp[q].x; bsum.y += rp[q].y; bsum.z += rp[q].z; bsum.w += rp[q].w; }
+            *reinterpret_cast<float4*>(&Ps[(e / (BM / 4)) * PP + (e % (BM / 4)) * 4]) = rp[q];
+        }
+#pragma unroll
+        for (int q = 0; q < H_V; ++q) {
+            const int e = tid + 256 * q;
+            if (e < H_E) *reinterpret_cast<float4*>(&Hs[(e / (BN / 4)) * PQ + (e % (BN / 4)) * 4]) = rh[q];
+        }
+    };
+
+    const int lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int lr = lane & 31, lh = lane >> 5;
+    floatx16 acc[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+    const int kb = split * a.chunks_per_split;
+    const int ke = min(a.nchunks, kb + a.chunks_per_split);
+    if (kb < ke) {
+        load(kb);
+        store(0);
+    }
+    __syncthreads();
+    int cur = 0;
+    for (int kc = kb; kc < ke; ++kc) {
+        if (kc + 1 < ke) load(kc + 1);  // next chunk in flight during this chunk's NT x 16 MFMAs
+        const float* Ps = smem + cur * (PSZ + HSZ);
+        const float* Hs = Ps + PSZ;
+        static_for<NT>([&](auto J) {
+            constexpr int t = decltype(J)::value;
+            constexpr int hr = t / KW, hc = t % KW;
+#pragma unroll
+            for (int s2 = 0; s2 < KT / 2; ++s2) {
+                const int k = lh * (KT / 2) + s2;
+                const float af = Ps[k * PP + wm * 32 + lr];
+                const float bf = Hs[(hr * HC + k * SQ + DIL * hc) * PQ + wn * 32 + lr];
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(af, bf, acc[t], 0, 0, 0);
+            }
+        });
+        if (kc + 1 < ke) store(cur ^ 1);
+        __syncthreads();
+        cur ^= 1;
+    }
+    if (do_bias) {
+        float4* red = reinterpret_cast<float4*>(smem);  // the loop ended with a barrier
+        red[tid] = bsum;
+        __syncthreads();
+        if (tid < BM / 4) {
+            float4 s4 = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int r = 0; r < 256 / (BM / 4); ++r) {
+                const float4 v = red[tid + r * (BM / 4)];
+                s4.x += v.x; s4.y += v.y; s4.z += v.z; s4.w += v.w;
+            }
+            float* dst = a.bias_slab + (long long)split * d.M + m0 + 4 * tid;
+            const float sv[4] = {s4.x, s4.y, s4.z, s4.w};
+            for (int c = 0; c < 4; ++c)
+                if (m0 + 4 * tid + c < d.M) dst[c] = sv[c];
+        }
+    }
+    const long long MN = (long long)d.M * d.N;
+    static_for<NT>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        const int n = n0 + wn * 32 + lr;
+        if (n < d.N) {
+            float* out = a.slab + ((long long)split * d.ntaps + t0 + j) * MN + n;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                if (m < d.M) out[(long long)m * d.N] = acc[j][r];
+            }
+        }
+    });
+}
+
+
+// ------------------------------------------------------------------------------------------------
+// AMP weight gradient (train.sh --mixed-precision): the same GEMM dW[t][m][n] = sum_q P[q][m] Q_t[q][n]
+// with P and Q rounded to fp16 when staged and consumed by v_mfma_f32_32x32x16_f16 (fp32 accumulation,
+// fp32 bias sums from the unrounded P).  Chunks of KTH = 64 pixels are staged exactly as they arrive
+// from HBM — [k][channel] rows, 4 channels (8 bytes) per ds_write_b64 — and read back transposed with
+// ds_read_b64_tr_b16, which hands each lane the 8 consecutive k of its row/column the MFMA wants.  Row
+// pitch = BM + 32 halves: the four rows of one transposed read land on disjoint banks.  Double-buffered
+// (one barrier per tap step).  Requires the vector path (M, N, ldp, ldq % 4 == 0) and no tap folding.
+// ------------------------------------------------------------------------------------------------
+constexpr int KTH = 64;
+typedef __fp16 fp16x4_t __attribute__((ext_vector_type(4)));
+typedef _Float16 halfx4_t __attribute__((ext_vector_type(4)));
+typedef _Float16 halfx8_t __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ halfx4_t lds_tr4(const _Float16* p) {
+    fp16x4_t v = __builtin_amdgcn_ds_read_tr16_b64_v4f16((__attribute__((address_space(3))) fp16x4_t*)(p));
+    return __builtin_bit_cast(halfx4_t, v);
+}
+
+// ONE: a 1x1 stride-1 gradient on the base grid (Q row = P row): Q rows load like P rows, no pixel decode
+template <int TM, int TN, int WAVES_M, int WAVES_N, int NT, bool SQ, bool ONE = false>
+__global__ __launch_bounds__(256) void wgrad_f16_kernel(const WgradArgs a) {
+    constexpr int BM = 32 * TM * WAVES_M;
+    constexpr int BN = 32 * TN * WAVES_N;
+    constexpr int PP = BM + 32, PQ = BN + 32;  // halves
+    __shared__ __attribute__((aligned(16))) _Float16 Psm[2 * KTH * PP];
+    __shared__ __attribute__((aligned(16))) _Float16 Qsm[2 * KTH * PQ];
+    const hyres_wgrad_desc& d = a.d;
+    const int tid = threadIdx.x;
+    const int bid = blockIdx.x;
+    const int lb = (bid & 7) * (gridDim.x >> 3) + (bid >> 3);
+    if (lb >= a.nblocks) return;
+    int rr = lb;
+    const int mt = rr % a.mtiles; rr /= a.mtiles;
+    const int nt = rr % a.ntiles; rr /= a.ntiles;
+    const int grp = rr % a.ngroups;
+    const int split = rr / a.ngroups;
+    const int m0 = mt * BM, n0 = nt * BN;
+    const int t0 = grp * NT;
+    const int HqWq = d.Hq * d.Wq;
+    const long long Qtot = (long long)d.B * HqWq;
+
+    constexpr int P_V = KTH * BM / 4 / 256, Q_V = KTH * BN / 4 / 256;
+    static_assert(P_V >= 1 && Q_V >= 1, "tile too small");
+    float4 rp[P_V], rq[Q_V];
+    // fixed per-thread channel quad (256 % (B/4) == 0): rows are tid/(B/4) + i*256/(B/4)
+    const int pc = (tid % (BM / 4)) * 4, prow0 = tid / (BM / 4);
+    const int qc = (tid % (BN / 4)) * 4, qrow0 = tid / (BN / 4);
+    constexpr int PRS = 256 / (BM / 4), QRS = 256 / (BN / 4);
+    int q_b[Q_V], q_i[Q_V], q_j[Q_V];
+    auto decode_rows = [&](int kc) {
+        if constexpr (ONE) return;
+#pragma unroll
+        for (int i = 0; i < Q_V; ++i) {
+            const long long qq = (long long)kc * KTH + qrow0 + i * QRS;
+            if (qq < Qtot) {
+                q_b[i] = (int)(qq / HqWq);
+                const int r = (int)(qq - (long long)q_b[i] * HqWq);
+                q_i[i] = r / d.Wq;
+                q_j[i] = r - q_i[i] * d.Wq;
+            } else {
+                q_b[i] = -1; q_i[i] = 0; q_j[i] = 0;
+            }
+        }
+    };
+    auto step_rows = [&]() {
+        if constexpr (ONE) return;
+#pragma unroll
+        for (int i = 0; i < Q_V; ++i) {
+            if (q_b[i] < 0) continue;
+            int j = q_j[i] + KTH, ii = q_i[i], b = q_b[i];
+            while (j >= d.Wq) { j -= d.Wq; ++ii; }
+            while (ii >= d.Hq) { ii -= d.Hq; ++b; }
+            q_j[i] = j; q_i[i] = ii; q_b[i] = b < d.B ? b : -1;
+        }
+    };
+    const bool do_bias = a.bias_slab != nullptr && nt == 0 && grp == 0;
+    float4 bsum = make_float4(0.f, 0.f, 0.f, 0.f);
+    auto load_p = [&](int kc) {
+        const long long k0 = (long long)kc * KTH;
+#pragma unroll
+        for (int i = 0; i < P_V; ++i) {
+            const long long qq = k0 + prow0 + i * PRS;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (qq < Qtot && m0 + pc < d.M) v = ld4(a.p + qq * d.ldp + m0 + pc);
+            rp[i] = v;
+        }
+    };
+    int cur_kc = 0;  // ONE: the chunk load_q fetches (Q rows = P rows)
+    auto load_q = [&](int t) {
+        if constexpr (ONE) {
+            const long long k0 = (long long)cur_kc * KTH;
+#pragma unroll
+            for (int i = 0; i < Q_V; ++i) {
+                const long long qq = k0 + qrow0 + i * QRS;
+                rq[i] = (qq < Qtot && n0 + qc < d.N) ? ld4(a.q + qq * d.ldq + n0 + qc) : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+            return;
+        }
+#pragma unroll
+        for (int i = 0; i < Q_V; ++i) {
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (q_b[i] >= 0 && n0 + qc < d.N && t < d.ntaps) {
+                const int ih = q_i[i] * d.sq + d.dh[t], iw = q_j[i] * d.sq + d.dw[t];
+                if (ih >= 0 && ih < d.Hqq && iw >= 0 && iw < d.Wqq)
+                    v = ld4(a.q + ((long long)(q_b[i] * d.Hqq + ih) * d.Wqq + iw) * d.ldq + n0 + qc);
+            }
+            if constexpr (SQ) { v.x *= v.x; v.y *= v.y; v.z *= v.z; v.w *= v.w; }
+            rq[i] = v;
+        }
+    };
+    auto store_p = [&](_Float16* Ps) {
+#pragma unroll
+        for (int i = 0; i < P_V; ++i) {
+            if (do_bias) { bsum.x += rp[i].x; bsum.y += rp[i].y; bsum.z += rp[i].z; bsum.w += rp[i].w; }
+            const halfx4_t h = {(_Float16)rp[i].x, (_Float16)rp[i].y, (_Float16)rp[i].z, (_Float16)rp[i].w};
+            *reinterpret_cast<halfx4_t*>(&Ps[(prow0 + i * PRS) * PP + pc]) = h;
+        }
+    };
+    auto store_q = [&](_Float16* Qs) {
+#pragma unroll
+        for (int i = 0; i < Q_V; ++i) {
+            const halfx4_t h = {(_Float16)rq[i].x, (_Float16)rq[i].y, (_Float16)rq[i].z, (_Float16)rq[i].w};
+            *reinterpret_cast<halfx4_t*>(&Qs[(qrow0 + i * QRS) * PQ + qc]) = h;
+        }
+    };
+
+    const int lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+    // transposed-read address of this lane: half h = lane>>5 takes k rows 8h..8h+7 of each 16-k step; in
+    // its 16-lane group g, lane 4q+p supplies row (.. + q), columns 16g + 4p .. +3
+    const int lh = lane >> 5, lg = (lane >> 4) & 1, lq = (lane >> 2) & 3, lp = lane & 3;
+    const int tr_row = 8 * lh + lq, tr_col = 16 * lg + 4 * lp;
+    floatx16 acc[NT][TM][TN];
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int k = 0; k < TN; ++k)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[j][i][k][r] = 0.f;
+
+    const int kc_begin = split * a.chunks_per_split;
+    const int kc_end = min(a.nchunks, kc_begin + a.chunks_per_split);
+    if (kc_begin < kc_end) {
+        decode_rows(kc_begin);
+        load_p(kc_begin);
+        cur_kc = kc_begin;
+        load_q(t0);
+        store_p(Psm);
+        store_q(Qsm);
+    }
+    __syncthreads();
+    int pcur = 0, qcur = 0;
+    for (int kc = kc_begin; kc < kc_end; ++kc) {
+        static_for<NT>([&](auto J) {
+            constexpr int j = decltype(J)::value;
+            const _Float16* Ps = Psm + pcur * (KTH * PP);
+            const _Float16* Qs = Qsm + qcur * (KTH * PQ);
+            const bool next_tap = j + 1 < NT;
+            const bool next_chunk = !next_tap && kc + 1 < kc_end;
+            if (next_tap) {
+                load_q(t0 + j + 1);
+            } else if (next_chunk) {
+                step_rows();
+                load_p(kc + 1);
+                cur_kc = kc + 1;
+                load_q(t0);
+            }
+#pragma unroll
+            for (int s = 0; s < KTH / 16; ++s) {
+                halfx8_t af[TM], bf[TN];
+#pragma unroll
+                for (int tm = 0; tm < TM; ++tm) {
+                    const _Float16* src = Ps + (16 * s + tr_row) * PP + wm * TM * 32 + tm * 32 + tr_col;
+                    const halfx4_t lo = lds_tr4(src), hi = lds_tr4(src + 4 * PP);
+                    af[tm] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+                }
+#pragma unroll
+                for (int tn = 0; tn < TN; ++tn) {
+                    const _Float16* src = Qs + (16 * s + tr_row) * PQ + wn * TN * 32 + tn * 32 + tr_col;
+                    const halfx4_t lo = lds_tr4(src), hi = lds_tr4(src + 4 * PQ);
+                    bf[tn] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+                }
+#pragma unroll
+                for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                    for (int tn = 0; tn < TN; ++tn)
+                        acc[j][tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[tm], bf[tn], acc[j][tm][tn], 0, 0, 0);
+            }
+            if (next_tap || next_chunk) {
+                store_q(Qsm + (qcur ^ 1) * (KTH * PQ));
+                if (next_chunk) store_p(Psm + (pcur ^ 1) * (KTH * PP));
+            }
+            __syncthreads();
+            qcur ^= 1;
+            if (!next_tap) pcur ^= 1;
+        });
+    }
+    if (do_bias) {
+        // fp32 column sums of this thread's rows -> reduce the PRS threads that share a channel quad
+        float4* red = reinterpret_cast<float4*>(Psm);  // the loop ended with a barrier
+        red[tid] = bsum;
+        __syncthreads();
+        if (tid < BM / 4) {
+            float4 s4 = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int r = 0; r < PRS; ++r) {
+                const float4 v = red[tid + r * (BM / 4)];
+                s4.x += v.x; s4.y += v.y; s4.z += v.z; s4.w += v.w;
+            }
+            float* dst = a.bias_slab + (long long)split * d.M + m0 + 4 * tid;
+            const float sv[4] = {s4.x, s4.y, s4.z, s4.w};
+            for (int c = 0; c < 4; ++c)
+                if (m0 + 4 * tid + c < d.M) dst[c] = sv[c];
+        }
+    }
+    // slab store [split][t][M][N] (accumulator layout of v_mfma_f32_32x32x16_f16 = the 32x32x2 f32 one)
+    const int lr = lane & 31;
+    const long long MN = (long long)d.M * d.N;
+    static_for<NT>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) {
+            const int n = n0 + wn * TN * 32 + tn * 32 + lr;
+            const int t = t0 + j;
+            if (n >= d.N || t >= d.ntaps) continue;
+            float* out = a.slab + ((long long)split * d.ntaps + t) * MN + n;
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int m = m0 + wm * TM * 32 + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                    if (m < d.M) out[(long long)m * d.N] = acc[j][tm][tn][r];
+                }
+        }
+    });
+}
+
+// ------------------------------------------------------------------------------------------------
+// AMP halo-staged weight gradient: wgrad_halo_kernel's schedule (one 32-pixel row segment of P and ONE
+// Q halo tile of KR rows x HC columns per chunk, all KR x KW taps of the group read from the halo at their
+// (dh, dw) shift, one barrier per chunk) with wgrad_f16_kernel's operands: both tiles rounded to fp16 when
+// staged ([pixel][channel] rows, pitch 64 + 32 halves) and read back transposed with ds_read_b64_tr_b16
+// into v_mfma_f32_32x32x16_f16 (fp32 accumulation). The generic f16 kernel gathers a shifted Q chunk per
+// tap (one tap per block, 9x the Q loads); here a 3x3 group costs one 3 x 34-pixel halo load per chunk.
+// The tap's B rows are halo rows base + k*SQ: the transposed read takes per-lane addresses, so the stride
+// is just a pitch of SQ*PQ. Bias gradient = fp32 column sums of the unrounded P (as wgrad_f16_kernel).
+// ------------------------------------------------------------------------------------------------
+template <int KR, int KW, int SQ, int DIL = 1>
+__global__ __launch_bounds__(256, 2) void wgrad_halo_f16_kernel(const WgradArgs a, int dhg, int dwg) {
+    constexpr int BM = 64, BN = 64, NT = KR * KW, HC = 31 * SQ + DIL * (KW - 1) + 1;
+    constexpr int PP = BM + 32, PQ = BN + 32;  // halves
+    constexpr int PSZ = KT * PP, HSZ = KR * HC * PQ;
+    constexpr int P_V = KT * BM / 4 / 256;  // 2 float4 of P per thread and chunk
+    constexpr int H_E = KR * HC * (BN / 4);
+    constexpr int H_V = (H_E + 255) / 256;
+    static_assert((PSZ + HSZ) % 4 == 0, "8-byte aligned buffers for the transposed reads");
+    __shared__ __attribute__((aligned(16))) _Float16 smem[2 * (PSZ + HSZ)];
+    const hyres_wgrad_desc& d = a.d;
+    const int tid = threadIdx.x;
+    const int bid = blockIdx.x;
+    const int lb = (bid & 7) * (gridDim.x >> 3) + (bid >> 3);  // XCD-aware order, as wgrad_kernel
+    if (lb >= a.nblocks) return;
+    int rr = lb;
+    const int mt = rr % a.mtiles; rr /= a.mtiles;
+    const int nt = rr % a.ntiles; rr /= a.ntiles;
+    const int grp = rr % a.ngroups;
+    const int split = rr / a.ngroups;
+    const int m0 = mt * BM, n0 = nt * BN;
+    const int t0 = grp * NT;
+    const int dh0 = dhg + grp * KR * DIL;
+    const int cpr = d.Wq / 32;
+    // this thread's fixed channel quad of P (256 % (BM/4) == 0): rows tid/16 + 16*q
+    const int pc = (tid % (BM / 4)) * 4, prow0 = tid / (BM / 4);
+    float4 rp[P_V], rh[H_V];
+    auto load = [&](int kc) {
+        const int b = kc / (d.Hq * cpr);
+        const int rem = kc - b * d.Hq * cpr;
+        const int i = rem / cpr;
+        const int j0 = (rem - i * cpr) * 32;
+        const long long q0 = (long long)kc * 32;
+#pragma unroll
+        for (int q = 0; q < P_V; ++q)
+            rp[q] = m0 + pc < d.M ? ld4(a.p + (q0 + prow0 + 16 * q) * d.ldp + m0 + pc) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int q = 0; q < H_V; ++q) {
+            const int e = tid + 256 * q;
+            const int pix = e / (BN / 4), c = (e % (BN / 4)) * 4;
+            const int hr = pix / HC, hc = pix - (pix / HC) * HC;
+            const int ih = i * SQ + dh0 + DIL * hr, iw = j0 * SQ + dwg + hc;
+            const bool ok = e < H_E && (unsigned)ih < (unsigned)d.Hqq && (unsigned)iw < (unsigned)d.Wqq && n0 + c < d.N;
+            rh[q] = ok ? ld4(a.q + ((long long)(b * d.Hqq + ih) * d.Wqq + iw) * d.ldq + n0 + c)
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    const bool do_bias = a.bias_slab != nullptr && nt == 0 && grp == 0;
+    float4 bsum = make_float4(0.f, 0.f, 0.f, 0.f);
+    auto store = [&](int buf) {
+        _Float16* Ps = smem + buf * (PSZ + HSZ);
+        _Float16* Hs = Ps + PSZ;
+#pragma unroll
+        for (int q = 0; q < P_V; ++q) {
+            if (do_bias) { bsum.x += rp[q].x; bsum.y += rp[q].y; bsum.z += rp[q].z; bsum.w += rp[q].w; }
+            const halfx4_t h = {(_Float16)rp[q].x, (_Float16)rp[q].y, (_Float16)rp[q].z, (_Float16)rp[q].w};
+            *reinterpret_cast<halfx4_t*>(&Ps[(prow0 + 16 * q) * PP + pc]) = h;
+        }
+#pragma unroll
+        for (int q = 0; q < H_V; ++q) {
+            const int e = tid + 256 * q;
+            if (e < H_E) {
+                const halfx4_t h = {(_Float16)rh[q].x, (_Float16)rh[q].y, (_Float16)rh[q].z, (_Float16)rh[q].w};
+                *reinterpret_cast<halfx4_t*>(&Hs[(e / (BN / 4)) * PQ + (e % (BN / 4)) * 4]) = h;
+            }
+        }
+    };
+
+    const int lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    // transposed-read lane address (wgrad_f16_kernel): half lh takes k rows 8lh..8lh+7 of a 16-k step
+    const int lh = lane >> 5, lg = (lane >> 4) & 1, lq = (lane >> 2) & 3, lp = lane & 3;
+    const int tr_row = 8 * lh + lq, tr_col = 16 * lg + 4 * lp;
+    floatx16 acc[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+    const int kb = split * a.chunks_per_split;
+    const int ke = min(a.nchunks, kb + a.chunks_per_split);
+    if (kb < ke) {
+        load(kb);
+        store(0);
+    }
+    __syncthreads();
+    int cur = 0;
+    for (int kc = kb; kc < ke; ++kc) {
+        if (kc + 1 < ke) load(kc + 1);  // next chunk in flight during this chunk's NT x 2 MFMAs per wave
+        const _Float16* Ps = smem + cur * (PSZ + HSZ);
+        const _Float16* Hs = Ps + PSZ;
+#pragma unroll
+        for (int s = 0; s < KT / 16; ++s) {
+            const _Float16* pa = Ps + (16 * s + tr_row) * PP + wm * 32 + tr_col;
+            const halfx4_t alo = lds_tr4(pa), ahi = lds_tr4(pa + 4 * PP);
+            const halfx8_t af = __builtin_shufflevector(alo, ahi, 0, 1, 2, 3, 4, 5, 6, 7);
+            static_for<NT>([&](auto J) {
+                constexpr int t = decltype(J)::value;
+                constexpr int hr = t / KW, hc = t % KW;
+                const _Float16* pb = Hs + (hr * HC + DIL * hc + SQ * (16 * s + tr_row)) * PQ + wn * 32 + tr_col;
+                const halfx4_t blo = lds_tr4(pb), bhi = lds_tr4(pb + 4 * SQ * PQ);
+                const halfx8_t bf = __builtin_shufflevector(blo, bhi, 0, 1, 2, 3, 4, 5, 6, 7);
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af, bf, acc[t], 0, 0, 0);
+            });
+        }
+        if (kc + 1 < ke) store(cur ^ 1);
+        __syncthreads();
+        cur ^= 1;
+    }
+    if (do_bias) {
+        float4* red = reinterpret_cast<float4*>(smem);  // the loop ended with a barrier
+        red[tid] = bsum;
+        __syncthreads();
+        if (tid < BM / 4) {
+            float4 s4 = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int r = 0; r < 256 / (BM / 4); ++r) {
+                const float4 v = red[tid + r * (BM / 4)];
+                s4.x += v.x; s4.y += v.y; s4.z += v.z; s4.w += v.w;
+            }
+            float* dst = a.bias_slab + (long long)split * d.M + m0 + 4 * tid;
+            const float sv[4] = {s4.x, s4.y, s4.z, s4.w};
+            for (int c = 0; c < 4; ++c)
+                if (m0 + 4 * tid + c < d.M) dst[c] = sv[c];
+        }
+    }
+    const int lr = lane & 31;
+    const long long MN = (long long)d.M * d.N;
+    static_for<NT>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        const int n = n0 + wn * 32 + lr;
+        if (n < d.N) {
+            float* out = a.slab + ((long long)split * d.ntaps + t0 + j) * MN + n;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                if (m < d.M) out[(long long)m * d.N] = acc[j][r];
+            }
+        }
+    });
+}
+
+// ------------------------------------------------------------------------------------------------
+// Thin-operand weight gradient: dW[t][m][n] = sum_q P[q][m] * Q[shift_t(q)][n] with N <= 4 (the 3-channel
+// image side: refine conv 3->64 / 64->3 at 256^2 (the latter through the swapped descriptor), g_a's 5x5 s2
+// conv 3->128, g_s's deconv 128->3) and M = 64*MW wide channels. An MFMA tile would be >90 % padding and
+// the tap-folded MFMA path gathers Q with scalar loads (13-15 TF/s, ~1 TB/s, 240-280 us per layer); here
+// the work is VALU FMAs at the HBM rate of P:
+//   * a block owns ``rpb`` consecutive base-grid rows (b, i) and one group of TG taps (grid.y);
+//   * per row, the Q rows the group's taps touch (<= THIN_ROWS rows x (Wq-1)*sq + tap span columns) are
+//     staged once in LDS as float4 (n padded to 4), zero outside the image;
+//   * wave w walks pixels j = w, w+4, ...: lane l holds P[q][l + 64*mw] (coalesced rows, the next pixel's
+//     row prefetched before this pixel's FMAs), the tap's Q values are one broadcast ds_read_b128;
+//   * per-lane accumulators [MW][TG][NC] (+ the P column sums = the bias gradient) are reduced over the
+//     block's 4 waves through LDS into the split slab [block][t][m][n]; the deterministic slab reduce of
+//     the generic path finishes it.
+// ------------------------------------------------------------------------------------------------
+constexpr int THIN_ROWS = 5, THIN_SPAN = 264;  // staged window: rows x columns (host check: ncol <= SPAN)
+constexpr int THIN_COLS = THIN_SPAN;
+constexpr int THIN_STAGE = (THIN_ROWS * THIN_COLS + 255) / 256;  // staged window entries per thread
+
+template <int MW, int NC, int TG, int SQ>
+__global__ __launch_bounds__(256) void wgrad_thin_kernel(const WgradArgs a, int rpb, int dhmin, int dwmin, int nrow,
+                                                         int ncol) {
+    constexpr int PCH = 64 / MW;            // pixels per P chunk (PCH x 64*MW floats = 16 KB)
+    constexpr int PV = PCH * 16 * MW / 256;  // float4 per thread per chunk
+    constexpr int PPW = PCH / 4;             // pixels per wave per chunk
+    __shared__ __attribute__((aligned(16))) float Qs[THIN_ROWS * THIN_COLS * 4];
+    __shared__ __attribute__((aligned(16))) float Ps[PCH * 64 * MW];
+    const hyres_wgrad_desc& d = a.d;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int blk = blockIdx.x, grp = blockIdx.y;
+    const int t0 = grp * TG;
+    const int ntg = min(TG, d.ntaps - t0);
+    const int R = d.B * d.Hq;
+    const int r0 = blk * rpb, r1 = min(R, r0 + rpb);
+    const bool do_bias = a.bias_slab != nullptr && grp == 0;
+    const int nst = nrow * THIN_COLS;
+    // per-tap window offsets through LDS (an indexed read of the by-value descriptor's tap arrays would
+    // copy them to scratch); taps past ntg read any slot: their accumulators are never stored
+    __shared__ int toff_s[TG];
+    if (tid < TG)
+        toff_s[tid] = tid < ntg ? ((d.dh[t0 + tid] - dhmin) * THIN_COLS + (d.dw[t0 + tid] - dwmin)) * 4 : 0;
+    __syncthreads();
+    int toff[TG];
+#pragma unroll
+    for (int u = 0; u < TG; ++u) toff[u] = toff_s[u];
+    // accumulators as float4 (thin channels in .xyzw): an array of MW*TG vectors stays in registers where
+    // a [MW][TG][4] float array (> 32 elements) is demoted to scratch
+    float4 acc[MW][TG];
+    float bsum[MW];
+#pragma unroll
+    for (int w = 0; w < MW; ++w) {
+        bsum[w] = 0.f;
+#pragma unroll
+        for (int u = 0; u < TG; ++u) acc[w][u] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    float4 pr4[PV];
+    for (int r = r0; r < r1; ++r) {
+        const int b = r / d.Hq, i = r - (r / d.Hq) * d.Hq;
+        const float* prow = a.p + (long long)r * d.Wq * d.ldp;
+        auto load_chunk = [&](int c0) {
+#pragma unroll
+            for (int k = 0; k < PV; ++k) {
+                const int idx = tid + 256 * k;
+                const int px = idx / (16 * MW), c4 = idx - (idx / (16 * MW)) * (16 * MW);
+                pr4[k] = c0 + px < d.Wq ? ld4(prow + (long long)(c0 + px) * d.ldp + 4 * c4)
+                                        : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+        };
+        load_chunk(0);
+        __syncthreads();  // the previous row's readers of Qs / Ps are done
+        // this row's Q window (zero outside the image, past N channels and past column ncol): every load of
+        // the window is issued before the first LDS store (a rolled loop serialised one latency per entry)
+        {
+            float4 qv[THIN_STAGE];
+#pragma unroll
+            for (int k = 0; k < THIN_STAGE; ++k) {
+                const int idx = tid + 256 * k;
+                const int rr = idx / THIN_COLS, cc = idx - (idx / THIN_COLS) * THIN_COLS;
+                const int ih = i * SQ + dhmin + rr, iw = dwmin + cc;
+                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (idx < nst && cc < ncol && (unsigned)ih < (unsigned)d.Hqq && (unsigned)iw < (unsigned)d.Wqq) {
+                    const float* qp = a.q + ((long long)(b * d.Hqq + ih) * d.Wqq + iw) * d.ldq;
+                    v.x = qp[0];
+                    if (NC > 1 && d.N > 1) v.y = qp[1];
+                    if (NC > 2 && d.N > 2) v.z = qp[2];
+                    if (NC > 3 && d.N > 3) v.w = qp[3];
+                }
+                qv[k] = v;
+            }
+#pragma unroll
+            for (int k = 0; k < THIN_STAGE; ++k)
+                if (tid + 256 * k < nst) *reinterpret_cast<float4*>(&Qs[(tid + 256 * k) * 4]) = qv[k];
+        }
+        for (int c0 = 0; c0 < d.Wq; c0 += PCH) {
+            if (c0) __syncthreads();  // the previous chunk's readers of Ps are done
+#pragma unroll
+            for (int k = 0; k < PV; ++k) *reinterpret_cast<float4*>(&Ps[4 * (tid + 256 * k)]) = pr4[k];
+            __syncthreads();
+            if (c0 + PCH < d.Wq) load_chunk(c0 + PCH);  // next chunk in flight during this chunk's FMAs
+#pragma unroll 2
+            for (int uu = 0; uu < PPW; ++uu) {
+                const int pl = wave * PPW + uu;
+                const int j = c0 + pl;
+                if (j >= d.Wq) break;  // wave-uniform
+                float pv[MW];
+#pragma unroll
+                for (int w = 0; w < MW; ++w) pv[w] = Ps[pl * 64 * MW + 64 * w + lane];
+                const float* qg = Qs + j * SQ * 4;
+#pragma unroll
+                for (int v = 0; v < TG; ++v) {
+                    const float4 q = *reinterpret_cast<const float4*>(qg + toff[v]);
+#pragma unroll
+                    for (int w = 0; w < MW; ++w) {
+                        acc[w][v].x = fmaf(pv[w], q.x, acc[w][v].x);
+                        if (NC > 1) acc[w][v].y = fmaf(pv[w], q.y, acc[w][v].y);
+                        if (NC > 2) acc[w][v].z = fmaf(pv[w], q.z, acc[w][v].z);
+                        if (NC > 3) acc[w][v].w = fmaf(pv[w], q.w, acc[w][v].w);
+                    }
+                }
+#pragma unroll
+                for (int w = 0; w < MW; ++w) bsum[w] += pv[w];
+            }
+        }
+    }
+    float* red = Qs;
+    // reduce the 4 waves' partials: one tap at a time through LDS ([wave][MW*NC][64]), wave 0 writes
+    const long long MN = (long long)d.M * d.N;
+    static_for<TG>([&](auto U) {  // compile-time tap index: acc stays in registers
+        constexpr int u = decltype(U)::value;
+        if (u < ntg) {
+            __syncthreads();
+#pragma unroll
+            for (int w = 0; w < MW; ++w) {
+                const float av[4] = {acc[w][u].x, acc[w][u].y, acc[w][u].z, acc[w][u].w};
+#pragma unroll
+                for (int n = 0; n < NC; ++n) red[(wave * MW * NC + w * NC + n) * 64 + lane] = av[n];
+            }
+            __syncthreads();
+            if (wave == 0) {
+                float* out = a.slab + ((long long)blk * d.ntaps + t0 + u) * MN;
+#pragma unroll
+                for (int w = 0; w < MW; ++w)
+#pragma unroll
+                    for (int n = 0; n < NC; ++n) {
+                        if (n >= d.N) continue;
+                        const int kk = (w * NC + n) * 64 + lane;
+                        const float v = red[kk] + red[MW * NC * 64 + kk] + red[2 * MW * NC * 64 + kk] +
+                                        red[3 * MW * NC * 64 + kk];
+                        out[(long long)(lane + 64 * w) * d.N + n] = v;
+                    }
+            }
+        }
+    });
+    if (do_bias) {
+        __syncthreads();
+#pragma unroll
+        for (int w = 0; w < MW; ++w) red[(wave * MW + w) * 64 + lane] = bsum[w];
+        __syncthreads();
+        if (wave == 0)
+#pragma unroll
+            for (int w = 0; w < MW; ++w) {
+                const int k = w * 64 + lane;
+                a.bias_slab[(long long)blk * d.M + lane + 64 * w] =
+                    red[k] + red[MW * 64 + k] + red[2 * MW * 64 + k] + red[3 * MW * 64 + k];
+            }
+    }
+}
+
+// deterministic split-K reduce: LX float4 lanes x (256 / LX) split groups per block (4*LX outputs per
+// block). Few outputs with many splits (1x1 / small weights over a whole batch: nsplit up to 512) take
+// LX = 4, so each thread walks nsplit/64 partial rows instead of nsplit/16 and 4x as many blocks run.
+template <int LX>
+__device__ __forceinline__ void wgrad_reduce_body(int blk, const float* slab, int nsplit, int ntaps, int M, int N,
+                                                  float* dst, int sm, int sn, int st, int accumulate) {
+    constexpr int G = 256 / LX, OUT = 4 * LX;
+    __shared__ float red[G][OUT + 1];
+    const long long total = (long long)ntaps * M * N;
+    const int lx = threadIdx.x % LX, ly = threadIdx.x / LX;
+    const long long base = (long long)blk * OUT + 4 * lx;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    if ((total & 3) == 0) {
+        if (base < total)
+#pragma unroll 4
+            for (int k = ly; k < nsplit; k += G) {
+                const float4 v = ld4(slab + k * total + base);
+                s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+            }
+    } else {
+        for (int k = ly; k < nsplit; k += G) {
+            const float* p = slab + k * total + base;
+            if (base + 0 < total) s.x += p[0];
+            if (base + 1 < total) s.y += p[1];
+            if (base + 2 < total) s.z += p[2];
+            if (base + 3 < total) s.w += p[3];
+        }
+    }
+    red[ly][4 * lx + 0] = s.x;
+    red[ly][4 * lx + 1] = s.y;
+    red[ly][4 * lx + 2] = s.z;
+    red[ly][4 * lx + 3] = s.w;
+    __syncthreads();
+    if (threadIdx.x < OUT) {
+        const long long idx = (long long)blk * OUT + threadIdx.x;
+        if (idx < total) {
+            float v = 0.f;
+#pragma unroll 16
+            for (int g = 0; g < G; ++g) v += red[g][threadIdx.x];
+            const int n = (int)(idx % N);
+            const long long r = idx / N;
+            const int m = (int)(r % M);
+            const int t = (int)(r / M);
+            float* p = dst + (long long)m * sm + (long long)n * sn + (long long)t * st;
+            *p = accumulate ? (*p + v) : v;
+        }
+    }
+}
+
+template <int LX>
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* slab, int nsplit, int ntaps, int M, int N,
+                                                           float* dst, int sm, int sn, int st, int accumulate) {
+    wgrad_reduce_body<LX>(blockIdx.x, slab, nsplit, ntaps, M, N, dst, sm, sn, st, accumulate);
+}
+
+// weight-gradient slab reduce and the bias-gradient partials ([nsplit][M]) in one launch
+template <int LX>
+__global__ __launch_bounds__(256) void wgrad_bias_reduce_kernel(const float* slab, int nsplit, int ntaps, int M, int N,
+                                                                float* dst, int sm, int sn, int st, int accumulate,
+                                                                int nb_w, const float* bslab, float* dbias) {
+    if ((int)blockIdx.x < nb_w)
+        wgrad_reduce_body<LX>(blockIdx.x, slab, nsplit, ntaps, M, N, dst, sm, sn, st, accumulate);
+    else
+        wgrad_reduce_body<LX>(blockIdx.x - nb_w, bslab, nsplit, 1, M, 1, dbias, 1, 0, 0, accumulate);
+}
+
+// lanes per block row for the reduce: keep ~>= 1024 blocks when the split count is large
+static int reduce_lx(long long total, int nsplit) {
+    if (nsplit <= 64 || (total + 63) / 64 >= 1024) return 16;
+    if ((total + 31) / 32 >= 1024) return 8;
+    return 4;
+}
+
+// Column sums of a [P][C] (pixel stride ld) matrix, deterministic two-pass.
+// Pass 1: a block owns a row range; its 256 threads are laid out TR x TC over (rows, channel groups of
+// VEC floats) so every wave reads whole contiguous rows; the TR partial rows are folded through LDS.
+template <int VEC>
+__global__ __launch_bounds__(256) void colsum_partial_kernel(const float* x, int P, int C, int ld,
+                                                             int rows_per_block, float* part) {
+    __shared__ float red[256 * VEC];
+    const int groups = C / VEC;                       // channel groups
+    const int TC = groups < 256 ? groups : 256;        // threads across channels
+    const int TR = 256 / TC;                           // threads across rows
+    const int tc = threadIdx.x % TC, tr = threadIdx.x / TC;
+    const int r0 = blockIdx.x * rows_per_block;
+    const int r1 = min(P, r0 + rows_per_block);
+    for (int g0 = 0; g0 < groups; g0 += TC) {
+        const int gi = g0 + tc;
+        float acc[VEC];
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) acc[v] = 0.f;
+        if (tr < TR && gi < groups) {
+            for (int r = r0 + tr; r < r1; r += TR) {
+                const float* p = x + (long long)r * ld + gi * VEC;
+                if constexpr (VEC == 4) {
+                    float4 q = *reinterpret_cast<const float4*>(p);
+                    acc[0] += q.x; acc[1] += q.y; acc[2] += q.z; acc[3] += q.w;
+                } else {
+                    acc[0] += p[0];
+                }
+            }
+        }
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) red[threadIdx.x * VEC + v] = acc[v];
+        __syncthreads();
+        if (tr == 0 && gi < groups) {
+            for (int k = 1; k < TR; ++k)
+#pragma unroll
+                for (int v = 0; v < VEC; ++v) acc[v] += red[(k * TC + tc) * VEC + v];
+#pragma unroll
+            for (int v = 0; v < VEC; ++v) part[(long long)blockIdx.x * C + gi * VEC + v] = acc[v];
+        }
+        __syncthreads();
+    }
+}
+
+// Pass 2: block handles 64 columns; 4 thread rows split the partials, folded through LDS.
+__global__ __launch_bounds__(256) void colsum_final_kernel(const float* part, int nb, int C, float* dst,
+                                                           int accumulate) {
+    __shared__ float red[256];
+    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int q = threadIdx.x >> 6;
+    float s = 0.f;
+    if (c < C)
+        for (int b = q; b < nb; b += 4) s += part[(long long)b * C + c];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    if (q == 0 && c < C) {
+        s = red[threadIdx.x] + red[threadIdx.x + 64] + red[threadIdx.x + 128] + red[threadIdx.x + 192];
+        dst[c] = accumulate ? dst[c] + s : s;
+    }
+}
+
+}  // namespace hyres
+
+using namespace hyres;
+
+namespace hyres {
+
+
+struct WgradPlan {
+    int TMc, TNc, WMc, WNc, NT, BM, BN, mtiles, ntiles, ngroups, nchunks, nsplit, cps, tapn, nblocks;
+    int halo, hk, hdh, hdw, hdil;  // wgrad_halo_kernel: K, first tap's (dh, dw), tap spacing
+};
+
+// wgrad_halo_kernel applies: fp32, dense KxK taps (K = 3 or 5, dilation 1; K = 3 with dilation 2), Q stride
+// 1 or 2 (5x5 only), base rows of a multiple of 32 pixels, both operands >= 32 channels on the float4 path.
+// *dil = the tap spacing.
+static bool halo_ok(const hyres_wgrad_desc* d, int* K, int* dil) {
+    static const int on = env_int("HYRES_WGRAD_HALO", 1);
+    static const int f16_on = env_int("HYRES_WGRAD_HALO_F16", 1);  // AMP: wgrad_halo_f16_kernel
+    if (!on || (d->f16_operands && !f16_on) || d->square_q || (d->sq != 1 && d->sq != 2)) return false;
+    if (d->Wq % 32 != 0 || d->M < 32 || d->N < 32 || d->M % 4 || d->N % 4 || d->ldp % 4 || d->ldq % 4) return false;
+    const int k = d->ntaps == 9 ? 3 : d->ntaps == 25 ? 5 : 0;
+    if (!k || (d->sq == 2 && k != 5)) return false;  // stride 2 only for the 5x5 (de)convs (3x3 s2: 123 KB LDS)
+    static const int dil_on = env_int("HYRES_WGRAD_HALO_DIL", 1);
+    const int D = d->dw[1] - d->dw[0];
+    if (D != 1 && !(dil_on && D == 2 && k == 3 && d->sq == 1)) return false;
+    for (int t = 0; t < d->ntaps; ++t)
+        if (d->dh[t] != d->dh[0] + D * (t / k) || d->dw[t] != d->dw[0] + D * (t % k)) return false;
+    *K = k;
+    *dil = D;
+    return true;
+}
+
+static bool wgrad_f16_ok(const hyres_wgrad_desc* d);
+
+static WgradPlan wgrad_plan(const hyres_wgrad_desc* d) {
+    WgradPlan p{};
+    p.NT = 1;
+    int hk = 0, hdil = 1;
+    const bool halo = halo_ok(d, &hk, &hdil);  // fp32 or (AMP) f16 halo kernel: 32-pixel chunks either way
+    const int kt = (wgrad_f16_ok(d) && !halo) ? KTH : KT;
+    p.tapn = (d->N <= 16 && d->ntaps > 1 && !d->square_q) ? 1 : 0;
+    const int ncols = p.tapn ? d->ntaps * d->N : d->N;
+    if (p.tapn) {
+        if (ncols <= 32) { p.TMc = 1; p.TNc = 1; p.WMc = 4; p.WNc = 1; }
+        else { p.TMc = 1; p.TNc = 1; p.WMc = 2; p.WNc = 2; }
+    } else if (d->M >= 128 && d->N >= 128) { p.TMc = 2; p.TNc = 2; p.WMc = 2; p.WNc = 2; }
+    else if (d->M >= 128 && d->N >= 64 && d->ntaps == 1) { p.TMc = 2; p.TNc = 1; p.WMc = 2; p.WNc = 2; }
+    else if (d->M <= 32) { p.TMc = 1; p.TNc = 1; p.WMc = 1; p.WNc = 4; }
+    else if (d->N <= 32) { p.TMc = 1; p.TNc = 1; p.WMc = 4; p.WNc = 1; }
+    else {
+        p.TMc = 1; p.TNc = 1; p.WMc = 2; p.WNc = 2;
+        // fp32: group 9 / 5 taps per block (operand reuse); f16: one tap per block column group (measured
+        // faster on every f16 geometry of the step: the f16 main loop is short, more blocks hide it better)
+        p.NT = (d->ntaps % 9 == 0) ? 9 : (d->ntaps % 5 == 0) ? 5 : 1;
+        if (kt == KTH || g_tune[5] == 1) p.NT = 1;
+    }
+    p.BM = 32 * p.TMc * p.WMc; p.BN = 32 * p.TNc * p.WNc;
+    p.mtiles = ceil_div(d->M, p.BM); p.ntiles = ceil_div(ncols, p.BN);
+    p.ngroups = p.tapn ? 1 : ceil_div(d->ntaps, p.NT);
+    p.nchunks = ceil_div((long long)d->B * d->Hq * d->Wq, kt);
+    if (halo) {
+        p.halo = 1;
+        p.hk = hk;
+        p.hdil = hdil;
+        p.hdh = d->dh[0];
+        p.hdw = d->dw[0];
+        p.tapn = 0;
+        p.TMc = p.TNc = 1; p.WMc = p.WNc = 2;
+        p.BM = p.BN = 64;
+        p.mtiles = ceil_div(d->M, 64); p.ntiles = ceil_div(d->N, 64);
+        p.NT = p.hk == 3 ? 9 : 5;
+        p.ngroups = d->ntaps / p.NT;
+    }
+    const long long tiles = (long long)p.mtiles * p.ntiles * p.ngroups;
+    // ~2048 blocks (swept on MI355X: 1024 -> 2048 is -0.6 % step time; fewer splits hurt), >= 8 chunks
+    // (256 pixels; f16: 4 chunks of 64) per split, <= 512 splits (tunable: HYRES_WGRAD_BLOCKS,
+    // HYRES_WGRAD_MINCHUNKS, HYRES_WGRAD_MAXSPLIT). Small grids (<= 16384 pixels, the 32^2 region at
+    // bs 16): ~4096 blocks, fp32 multi-tap splits down to 4 chunks. The split count is capped so that the partial
+    // slab stays <= 16 M floats (64 MB): for the wide 1x1 layers (M x N ~ 0.5 M) the slab write + reduce
+    // otherwise costs more than the parallelism buys (scripts/tile_sweep.py --wgrad)
+    const long long Q = (long long)d->B * d->Hq * d->Wq;
+    const bool small = Q <= 16384;
+    static const int tb_env = env_int("HYRES_WGRAD_BLOCKS", 2048);
+    static const int mc_env = env_int("HYRES_WGRAD_MINCHUNKS", 8);
+    const int tb = g_tune[3] > 0 ? g_tune[3] : (small ? 2 * tb_env : tb_env);
+    const int mc0 = g_tune[4] > 0 ? g_tune[4] : ((small && kt == KT && d->ntaps > 1) ? mc_env / 2 : mc_env);
+    const int mc = std::max(1, mc0 * KT / kt);
+    static const int ms_env = env_int("HYRES_WGRAD_MAXSPLIT", 512);
+    const int ms = g_tune[6] > 0 ? g_tune[6] : ms_env;
+    const long long slab_cap = std::max<long long>(4, (16LL << 20) / ((long long)d->ntaps * d->M * d->N));
+    const long long want = std::min<long long>(std::max<long long>(1, (tb + tiles - 1) / tiles), slab_cap);
+    const long long maxsplit = std::max<long long>(1, p.nchunks / mc);
+    p.nsplit = (int)std::min<long long>(std::min<long long>(want, maxsplit), ms);
+    if (p.halo) {
+        // whole rounds only: the halo kernel runs 2 blocks per CU (3 for 5x5 stride 1); a partial last round
+        // of long split-K blocks costs as much as a full one, so drop it (e.g. 800 -> 500 blocks)
+        const long long cap = 256LL * ((p.hk == 5 && d->sq == 1) ? 3 : 2);
+        if (tiles * p.nsplit > cap) p.nsplit = (int)std::max<long long>(1, (tiles * p.nsplit / cap) * cap / tiles);
+        // and fill a partial single round when that grows the slab by <= 25 % (128^2 3x3: 455 -> 512)
+        else if (cap / tiles <= maxsplit && 4 * (cap / tiles) <= 5LL * p.nsplit) p.nsplit = (int)(cap / tiles);
+    }
+    p.cps = ceil_div(p.nchunks, p.nsplit);
+    p.nsplit = ceil_div(p.nchunks, p.cps);
+    p.nblocks = (int)(tiles * p.nsplit);
+    return p;
+}
+
+// f16 operands only on the vector path without tap folding (the 3-channel layers stay fp32)
+static bool wgrad_f16_ok(const hyres_wgrad_desc* d) {
+    const bool tapn = d->N <= 16 && d->ntaps > 1 && !d->square_q;
+    return d->f16_operands && !tapn && d->M % 4 == 0 && d->N % 4 == 0 && d->ldp % 4 == 0 && d->ldq % 4 == 0 &&
+           d->M >= 32 && d->N >= 32;
+}
+
+// Small-M stride-1 gradients are computed transposed with negated shifts so that the 3-channel
+// operand becomes the (tap-folded) column side:  out[t][m][n] = sum_q' Q[q'][n] * P[q' - shift_t][m].
+static bool wgrad_swap(const hyres_wgrad_desc* d) {
+    return d->M <= 16 && d->N > 16 && d->ntaps > 1 && d->sq == 1 && d->Hqq == d->Hq && d->Wqq == d->Wq &&
+           !d->square_q;
+}
+
+static hyres_wgrad_desc wgrad_swapped(const hyres_wgrad_desc* d) {
+    hyres_wgrad_desc e = *d;
+    e.M = d->N; e.ldp = d->ldq;
+    e.N = d->M; e.ldq = d->ldp;
+    for (int t = 0; t < d->ntaps; ++t) { e.dh[t] = -d->dh[t]; e.dw[t] = -d->dw[t]; }
+    e.sm = d->sn; e.sn = d->sm;
+    return e;
+}
+
+// thin-operand weight-gradient plan (wgrad_thin_kernel): N <= 4, M in {64, 128}, the staged Q window fits
+struct ThinPlan {
+    int mw, nc, tg, ngroups, rpb, nblk, dhmin, dwmin, nrow, ncol, sq;
+};
+
+static bool thin_plan(const hyres_wgrad_desc* d, ThinPlan* tp) {
+    static const int on = env_int("HYRES_WGRAD_THIN", 1);
+    if (!on || d->N > 4 || (d->M != 64 && d->M != 128) || d->square_q || d->ntaps < 1 || d->ntaps > 25)
+        return false;
+    int hmin = 1 << 30, hmax = -(1 << 30), wmin = 1 << 30, wmax = -(1 << 30);
+    for (int t = 0; t < d->ntaps; ++t) {
+        hmin = std::min(hmin, d->dh[t]); hmax = std::max(hmax, d->dh[t]);
+        wmin = std::min(wmin, d->dw[t]); wmax = std::max(wmax, d->dw[t]);
+    }
+    ThinPlan p{};
+    p.dhmin = hmin; p.dwmin = wmin;
+    p.nrow = hmax - hmin + 1;
+    p.ncol = (d->Wq - 1) * d->sq + (wmax - wmin) + 1;
+    if (p.nrow > THIN_ROWS || p.ncol > THIN_SPAN || (d->sq != 1 && d->sq != 2)) return false;
+    if (d->ldp % 4 != 0) return false;  // P chunks staged as float4
+    p.mw = d->M / 64;
+    p.nc = d->N == 3 ? 3 : 4;
+    p.sq = d->sq;
+    p.tg = d->ntaps <= 9 ? 9 : (p.mw == 1 ? 25 : 13);
+    p.ngroups = ceil_div(d->ntaps, p.tg);
+    const int R = d->B * d->Hq;
+    p.rpb = std::max(1, ceil_div(R * p.ngroups, 1024));  // ~1024 blocks (4 per CU)
+    p.nblk = ceil_div(R, p.rpb);
+    *tp = p;
+    return true;
+}
+
+static void launch_thin(const WgradArgs& a, const ThinPlan& p, hipStream_t st) {
+    const dim3 grid(p.nblk, p.ngroups);
+    auto go = [&](auto mw, auto nc, auto tg) {
+        constexpr int MW_ = decltype(mw)::value, NC_ = decltype(nc)::value, TG_ = decltype(tg)::value;
+        if (p.sq == 1)
+            hipLaunchKernelGGL((wgrad_thin_kernel<MW_, NC_, TG_, 1>), grid, dim3(256), 0, st, a, p.rpb, p.dhmin,
+                               p.dwmin, p.nrow, p.ncol);
+        else
+            hipLaunchKernelGGL((wgrad_thin_kernel<MW_, NC_, TG_, 2>), grid, dim3(256), 0, st, a, p.rpb, p.dhmin,
+                               p.dwmin, p.nrow, p.ncol);
+    };
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using I3 = std::integral_constant<int, 3>;
+    using I4 = std::integral_constant<int, 4>;
+    using I9 = std::integral_constant<int, 9>;
+    using I13 = std::integral_constant<int, 13>;
+    using I25 = std::integral_constant<int, 25>;
+    if (p.mw == 1) {
+        if (p.nc == 3) { if (p.tg == 9) go(I1{}, I3{}, I9{}); else go(I1{}, I3{}, I25{}); }
+        else { if (p.tg == 9) go(I1{}, I4{}, I9{}); else go(I1{}, I4{}, I25{}); }
+    } else {
+        if (p.nc == 3) { if (p.tg == 9) go(I2{}, I3{}, I9{}); else go(I2{}, I3{}, I13{}); }
+        else { if (p.tg == 9) go(I2{}, I4{}, I9{}); else go(I2{}, I4{}, I13{}); }
+    }
+}
+
+template <int TM, int TN, int WM_, int WN_, int NT>
+static void launch_wgrad(const WgradArgs& a, bool vp, bool vq, bool sqr, dim3 grid, hipStream_t st) {
+    if (vp && vq && sqr) hipLaunchKernelGGL((wgrad_kernel<TM, TN, WM_, WN_, NT, true, true, true>), grid, dim3(256), 0, st, a);
+    else if (vp && vq) hipLaunchKernelGGL((wgrad_kernel<TM, TN, WM_, WN_, NT, true, true, false>), grid, dim3(256), 0, st, a);
+    else if (vp) hipLaunchKernelGGL((wgrad_kernel<TM, TN, WM_, WN_, NT, true, false, false>), grid, dim3(256), 0, st, a);
+    else if (vq) hipLaunchKernelGGL((wgrad_kernel<TM, TN, WM_, WN_, NT, false, true, false>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((wgrad_kernel<TM, TN, WM_, WN_, NT, false, false, false>), grid, dim3(256), 0, st, a);
+}
+
+}  // namespace hyres
+
+extern "C" {
+
+static long long wgrad_slab_floats(const hyres_wgrad_desc* e, const WgradPlan& p) {
+    return (long long)p.nsplit * e->ntaps * (long long)e->M * e->N;
+}
+
+long long hyres_wgrad_workspace_bytes(const hyres_wgrad_desc* d) {
+    const bool swap = wgrad_swap(d);
+    hyres_wgrad_desc e = swap ? wgrad_swapped(d) : *d;
+    WgradPlan p = wgrad_plan(&e);
+    // + the bias-gradient partials: [nsplit][M] in the kernel, or colsum partials when swapped
+    auto need = [&](const WgradPlan& q) {
+        const long long bias = swap ? hyres_colsum_workspace_bytes(d->B * d->Hq * d->Wq, d->M) / 4 + 4
+                                    : (long long)q.nsplit * e.M + 4;
+        return (wgrad_slab_floats(&e, q) + bias) * 4;
+    };
+    long long bytes = need(p);
+    ThinPlan tp;
+    if (thin_plan(&e, &tp)) {  // one slab row per thin block (the launch may still take the generic path
+        WgradPlan q = p;       // when P is not 16-byte aligned: cover both)
+        q.nsplit = tp.nblk;
+        bytes = std::max(bytes, need(q));
+    }
+    return bytes;
+}
+
+int hyres_conv_wgrad(const hyres_wgrad_desc* d0, const float* pp, const float* qq, float* dst, float* dbias,
+                     void* ws, long long ws_bytes, hyres_stream_t s) {
+    HY_REQUIRE(d0 && pp && qq && dst, HYRES_E_ARG, "wgrad: NULL");
+    const long long need = hyres_wgrad_workspace_bytes(d0);
+    HY_REQUIRE(ws && ws_bytes >= need, HYRES_E_WORKSPACE, "wgrad: workspace %lld < %lld", ws_bytes, need);
+    const float* p_orig = pp;
+    const bool swap = wgrad_swap(d0);
+    const hyres_wgrad_desc dd = swap ? wgrad_swapped(d0) : *d0;
+    const hyres_wgrad_desc* d = &dd;
+    if (swap) std::swap(pp, qq);
+    WgradPlan p = wgrad_plan(d);
+    ThinPlan tp;
+    const bool thin = thin_plan(d, &tp) && aligned16(pp);
+    if (thin) p.nsplit = tp.nblk;
+    float* bias_ws = (float*)ws + wgrad_slab_floats(d, p);
+    const bool vp = (d->M % 4 == 0) && (d->ldp % 4 == 0) && aligned16(pp);
+    const bool vq = !p.tapn && (d->N % 4 == 0) && (d->ldq % 4 == 0) && aligned16(qq);
+    HY_REQUIRE(!d->square_q || (vp && vq), HYRES_E_SHAPE, "wgrad: square_q needs the vector path");
+    // the plan (chunk size, split count, workspace) assumed the f16 kernel: its operands must be aligned
+    HY_REQUIRE(!wgrad_f16_ok(d) || (vp && vq), HYRES_E_ALIGN, "wgrad(f16): P/Q must be 16-byte aligned");
+    HY_REQUIRE(!p.halo || (vp && vq), HYRES_E_ALIGN, "wgrad(halo): P/Q must be 16-byte aligned");
+    WgradArgs a;
+    a.d = *d; a.p = pp; a.q = qq; a.slab = (float*)ws; a.chunks_per_split = p.cps; a.nchunks = p.nchunks;
+    a.mtiles = p.mtiles; a.ntiles = p.ntiles; a.ngroups = p.ngroups; a.nblocks = p.nblocks; a.tapn = p.tapn;
+    a.bias_slab = (dbias && !swap) ? bias_ws : nullptr;
+    dim3 grid(ceil_div(p.nblocks, 8) * 8);
+    hipStream_t st = as_stream(s);
+    const bool sqr = d->square_q != 0;
+    static const int w1x1 = env_int("HYRES_WGRAD_1X1", 1);
+    const bool one = w1x1 && !thin && !p.halo && !wgrad_f16_ok(d) && !sqr && !p.tapn && vp && vq &&
+                     d->ntaps == 1 && d->dh[0] == 0 && d->dw[0] == 0 && d->sq == 1 && d->Hqq == d->Hq &&
+                     d->Wqq == d->Wq && p.ngroups == 1;
+    if (one) {
+        if (p.TMc == 2 && p.TNc == 2) hipLaunchKernelGGL((wgrad1x1_kernel<2, 2, 2, 2>), grid, dim3(256), 0, st, a);
+        else if (p.TMc == 2) hipLaunchKernelGGL((wgrad1x1_kernel<2, 1, 2, 2>), grid, dim3(256), 0, st, a);
+        else if (p.WMc == 1) hipLaunchKernelGGL((wgrad1x1_kernel<1, 1, 1, 4>), grid, dim3(256), 0, st, a);
+        else if (p.WNc == 1) hipLaunchKernelGGL((wgrad1x1_kernel<1, 1, 4, 1>), grid, dim3(256), 0, st, a);
+        else hipLaunchKernelGGL((wgrad1x1_kernel<1, 1, 2, 2>), grid, dim3(256), 0, st, a);
+    } else if (thin) {
+        launch_thin(a, tp, st);
+    } else if (p.halo && wgrad_f16_ok(d)) {
+        if (p.hk == 3 && p.hdil == 2)
+            hipLaunchKernelGGL((wgrad_halo_f16_kernel<3, 3, 1, 2>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
+        else if (p.hk == 3) hipLaunchKernelGGL((wgrad_halo_f16_kernel<3, 3, 1>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
+        else if (d->sq == 1) hipLaunchKernelGGL((wgrad_halo_f16_kernel<1, 5, 1>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
+        else hipLaunchKernelGGL((wgrad_halo_f16_kernel<1, 5, 2>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
+    } else if (p.halo) {
+        if (p.hk == 3 && p.hdil == 2)
+            hipLaunchKernelGGL((wgrad_halo_kernel<3, 3, 1, 2>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
+        else if (p.hk == 3) hipLaunchKernelGGL((wgrad_halo_kernel<3, 3, 1>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
+        else if (d->sq == 1) hipLaunchKernelGGL((wgrad_halo_kernel<1, 5, 1>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
+        else hipLaunchKernelGGL((wgrad_halo_kernel<1, 5, 2>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
+    } else if (wgrad_f16_ok(d)) {
+        static const int f16_one = env_int("HYRES_WGRAD_F16_1X1", 1);
+        const bool one16 = f16_one && !sqr && d->ntaps == 1 && d->dh[0] == 0 && d->dw[0] == 0 && d->sq == 1 &&
+                           d->Hqq == d->Hq && d->Wqq == d->Wq && p.ngroups == 1;
+        auto f16 = [&](auto tm, auto tn, auto wm_, auto wn_, auto ntc) {
+            constexpr int TM_ = decltype(tm)::value, TN_ = decltype(tn)::value;
+            constexpr int WM2 = decltype(wm_)::value, WN2 = decltype(wn_)::value, NT_ = decltype(ntc)::value;
+            if (sqr) hipLaunchKernelGGL((wgrad_f16_kernel<TM_, TN_, WM2, WN2, NT_, true>), grid, dim3(256), 0, st, a);
+            else if (NT_ == 1 && one16)
+                hipLaunchKernelGGL((wgrad_f16_kernel<TM_, TN_, WM2, WN2, 1, false, true>), grid, dim3(256), 0, st, a);
+            else hipLaunchKernelGGL((wgrad_f16_kernel<TM_, TN_, WM2, WN2, NT_, false>), grid, dim3(256), 0, st, a);
+        };
+        using I1 = std::integral_constant<int, 1>;
+        using I2 = std::integral_constant<int, 2>;
+        using I4 = std::integral_constant<int, 4>;
+        if (p.TMc == 2 && p.TNc == 2) f16(I2{}, I2{}, I2{}, I2{}, I1{});
+        else if (p.TMc == 2) f16(I2{}, I1{}, I2{}, I2{}, I1{});
+        else if (p.WMc == 1) f16(I1{}, I1{}, I1{}, I4{}, I1{});
+        else if (p.WNc == 1) f16(I1{}, I1{}, I4{}, I1{}, I1{});
+        else if (p.NT == 9) f16(I1{}, I1{}, I2{}, I2{}, std::integral_constant<int, 9>{});
+        else if (p.NT == 5) f16(I1{}, I1{}, I2{}, I2{}, std::integral_constant<int, 5>{});
+        else f16(I1{}, I1{}, I2{}, I2{}, I1{});
+    } else if (p.TMc == 2 && p.TNc == 2) launch_wgrad<2, 2, 2, 2, 1>(a, vp, vq, sqr, grid, st);
+    else if (p.TMc == 2) launch_wgrad<2, 1, 2, 2, 1>(a, vp, vq, sqr, grid, st);
+    else if (p.WMc == 1) launch_wgrad<1, 1, 1, 4, 1>(a, vp, vq, sqr, grid, st);
+    else if (p.WNc == 1) launch_wgrad<1, 1, 4, 1, 1>(a, vp, vq, sqr, grid, st);
+    else if (p.NT == 9) launch_wgrad<1, 1, 2, 2, 9>(a, vp, vq, sqr, grid, st);
+    else if (p.NT == 5) launch_wgrad<1, 1, 2, 2, 5>(a, vp, vq, sqr, grid, st);
+    else launch_wgrad<1, 1, 2, 2, 1>(a, vp, vq, sqr, grid, st);
+    int rc = HY_LAUNCH_CHECK("wgrad_kernel");
+    if (rc) return rc;
+    const long long total = (long long)d->ntaps * d->M * d->N;
+    const int lx = reduce_lx(total, p.nsplit);
+    const int outb = 4 * lx;
+    auto reduce = [&](auto lxc) {
+        constexpr int LX = decltype(lxc)::value;
+        if (dbias && !swap) {  // [nsplit][M] bias partials reduced by the same launch
+            const int nb_w = (int)ceil_div(total, outb);
+            hipLaunchKernelGGL(wgrad_bias_reduce_kernel<LX>, dim3(nb_w + ceil_div(d->M, outb)), dim3(256), 0, st,
+                               (const float*)ws, p.nsplit, d->ntaps, d->M, d->N, dst, d->sm, d->sn, d->st,
+                               d->accumulate, nb_w, (const float*)bias_ws, dbias);
+            return HY_LAUNCH_CHECK("wgrad_bias_reduce_kernel");
+        }
+        hipLaunchKernelGGL(wgrad_reduce_kernel<LX>, dim3(ceil_div(total, outb)), dim3(256), 0, st, (const float*)ws,
+                           p.nsplit, d->ntaps, d->M, d->N, dst, d->sm, d->sn, d->st, d->accumulate);
+        int r = HY_LAUNCH_CHECK("wgrad_reduce_kernel");
+        if (r || !dbias || swap) return r;
+        // [nsplit][M] partials = a [nsplit][1][M][1] slab: the same parallel deterministic reduce
+        hipLaunchKernelGGL(wgrad_reduce_kernel<LX>, dim3(ceil_div(d->M, outb)), dim3(256), 0, st,
+                           (const float*)bias_ws, p.nsplit, 1, d->M, 1, dbias, 1, 0, 0, d->accumulate);
+        return HY_LAUNCH_CHECK("wgrad_reduce_kernel(bias)");
+    };
+    if (lx == 16) rc = reduce(std::integral_constant<int, 16>{});
+    else if (lx == 8) rc = reduce(std::integral_constant<int, 8>{});
+    else rc = reduce(std::integral_constant<int, 4>{});
+    if (rc || !dbias || !swap) return rc;
+    if (swap) {  // P (= dY) is the tap-folded side here: plain column sums
+        const int P = d0->B * d0->Hq * d0->Wq;
+        return hyres_colsum(p_orig, P, d0->M, d0->ldp, dbias, d0->accumulate, bias_ws,
+                            hyres_colsum_workspace_bytes(P, d0->M), s);
+    }
+    return 0;
+}
+
+static int colsum_blocks(int P) {
+    // >= 128 rows per block, at most 512 partial rows
+    int nb = std::max(1, std::min(ceil_div(P, 128), 512));
+    int rows = ceil_div(P, nb);
+    return ceil_div(P, rows);
+}
+
+long long hyres_colsum_workspace_bytes(int P, int C) { return (long long)colsum_blocks(P) * C * 4; }
+
+int hyres_colsum(const float* x, int P, int C, int ld, float* dst, int accumulate, void* ws,
+                 long long ws_bytes, hyres_stream_t s) {
+    HY_REQUIRE(x && dst && P > 0 && C > 0, HYRES_E_ARG, "colsum: bad args");
+    const int nb = colsum_blocks(P);
+    const int rows = ceil_div(P, nb);
+    HY_REQUIRE(ws && ws_bytes >= (long long)nb * C * 4, HYRES_E_WORKSPACE, "colsum: workspace");
+    hipStream_t st = as_stream(s);
+    const bool vec = (C % 4 == 0) && (ld % 4 == 0) && aligned16(x);
+    if (vec)
+        hipLaunchKernelGGL(colsum_partial_kernel<4>, dim3(nb), dim3(256), 0, st, x, P, C, ld, rows, (float*)ws);
+    else
+        hipLaunchKernelGGL(colsum_partial_kernel<1>, dim3(nb), dim3(256), 0, st, x, P, C, ld, rows, (float*)ws);
+    int rc = HY_LAUNCH_CHECK("colsum_partial");
+    if (rc) return rc;
+    hipLaunchKernelGGL(colsum_final_kernel, dim3(ceil_div(C, 64)), dim3(256), 0, st, (const float*)ws, nb, C, dst,
+                       accumulate);
+    return HY_LAUNCH_CHECK("colsum_final");
+}
+
+}  // extern "C"
