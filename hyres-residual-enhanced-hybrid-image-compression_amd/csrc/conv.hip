@@ -48,6 +48,20 @@ __device__ __forceinline__ EpiChannel epi_channel(const hyres_epilogue& e, int n
     return c;
 }
 
+// Saved-activation operand of a backward epilogue (the ReLU mask's y, GDN-backward's x and norm): fp16 when
+// the whole epilogue is fp16 (H) or, with fp32 X/Y, when io_f16 carries HYRES_IO_AUX16 (AMP training keeps
+// its activations fp16 and its gradients fp32). A uniform kernel-argument branch.
+template <bool H>
+__device__ __forceinline__ float ld_aux(const hyres_epilogue& e, const float* p, long long i) {
+    if constexpr (H) return ldv<true>(p, i);
+    else return (e.io_f16 & HYRES_IO_AUX16) ? ldv<true>(p, i) : p[i];
+}
+template <bool H>
+__device__ __forceinline__ float4 ld_aux4(const hyres_epilogue& e, const float* p, long long i) {
+    if constexpr (H) return ldv4<true>(p, i);
+    else return (e.io_f16 & HYRES_IO_AUX16) ? ldv4<true>(p, i) : ld4(p + i);
+}
+
 // Apply the epilogue to one GEMM result v for output pixel ``pix`` / channel n and store it
 // (H: y and the activation operands res / aux0 / out2 are fp16 in HBM).
 template <bool H = false>
@@ -60,7 +74,7 @@ __device__ __forceinline__ void epi_store(const hyres_epilogue& e, float* y, int
             if (e.out2) stv<H>(e.out2, pix * e.ldo2 + n, v);  // pre-activation (PReLU backward)
             if (e.act == HYRES_ACT_RELU) v = fmaxf(v, 0.f);
             else if (e.act == HYRES_ACT_PRELU) v = v >= 0.f ? v : c.slope * v;
-            else if (e.act == HYRES_ACT_RELU_MASK) v = ldv<H>(e.aux0, pix * e.ld0 + n) > 0.f ? v : 0.f;
+            else if (e.act == HYRES_ACT_RELU_MASK) v = ld_aux<H>(e, e.aux0, pix * e.ld0 + n) > 0.f ? v : 0.f;
             break;
         }
         case HYRES_EPI_GDN:
@@ -73,9 +87,9 @@ __device__ __forceinline__ void epi_store(const hyres_epilogue& e, float* y, int
         }
         case HYRES_EPI_GDN_BWD:
         case HYRES_EPI_IGDN_BWD: {
-            const float xv = e.aux0[pix * e.ld0 + n];
+            const float xv = ld_aux<false>(e, e.aux0, pix * e.ld0 + n);
             const float gv = e.aux1[pix * e.ld1 + n];
-            const float nv = e.aux2[pix * e.ld2 + n];
+            const float nv = ld_aux<false>(e, e.aux2, pix * e.ld2 + n);
             const float f = (e.kind == HYRES_EPI_GDN_BWD) ? (1.0f / sqrtf(nv)) : sqrtf(nv);
             v = 2.0f * xv * v + gv * f;
             break;
@@ -113,7 +127,7 @@ __device__ __forceinline__ void epi_store4(const hyres_epilogue& e, float* y, in
 #pragma unroll
                 for (int c = 0; c < 4; ++c) o[c] = o[c] >= 0.f ? o[c] : slope * o[c];
             } else if (e.act == HYRES_ACT_RELU_MASK) {
-                const float4 y = ldv4<H>(e.aux0, pix * e.ld0 + n);
+                const float4 y = ld_aux4<H>(e, e.aux0, pix * e.ld0 + n);
                 o[0] = y.x > 0.f ? o[0] : 0.f;
                 o[1] = y.y > 0.f ? o[1] : 0.f;
                 o[2] = y.z > 0.f ? o[2] : 0.f;
@@ -135,9 +149,9 @@ __device__ __forceinline__ void epi_store4(const hyres_epilogue& e, float* y, in
         }
         case HYRES_EPI_GDN_BWD:
         case HYRES_EPI_IGDN_BWD: {
-            const float4 x = ld4(e.aux0 + pix * e.ld0 + n);
+            const float4 x = ld_aux4<false>(e, e.aux0, pix * e.ld0 + n);
             const float4 gg = ld4(e.aux1 + pix * e.ld1 + n);
-            const float4 nn = ld4(e.aux2 + pix * e.ld2 + n);
+            const float4 nn = ld_aux4<false>(e, e.aux2, pix * e.ld2 + n);
             const float xv[4] = {x.x, x.y, x.z, x.w}, gv[4] = {gg.x, gg.y, gg.z, gg.w}, nv[4] = {nn.x, nn.y, nn.z, nn.w};
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
@@ -471,7 +485,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
                         bs[u] = (ok[u] && e.bias) ? ld4(e.bias + n) : z4;
                         rs[u] = (ok[u] && e.res) ? ldv4<YH>(e.res, pix * e.ldres + n) : z4;
                         yo[u] = (!YH && ok[u] && e.accumulate) ? ld4(a.y + pix * g.ldy + n) : z4;
-                        mk[u] = (ok[u] && e.act == HYRES_ACT_RELU_MASK) ? ldv4<YH>(e.aux0, pix * e.ld0 + n) : z4;
+                        mk[u] = (ok[u] && e.act == HYRES_ACT_RELU_MASK) ? ld_aux4<YH>(e, e.aux0, pix * e.ld0 + n) : z4;
                     }
 #pragma unroll
                     for (int u = 0; u < U; ++u) {
@@ -1329,7 +1343,7 @@ static bool narrow_ok(const hyres_conv_geom* g) {
 
 template <int CO>
 static void launch_narrow(const ConvArgs& a, dim3 grid, hipStream_t st) {
-    if (a.e.io_f16 & 1) {
+    if (a.e.io_f16 & HYRES_IO_X16) {
         if (a.g.Ci == 64) hipLaunchKernelGGL((conv_narrow_kernel<CO, 1, true>), grid, dim3(256), 0, st, a);
         else hipLaunchKernelGGL((conv_narrow_kernel<CO, 2, true>), grid, dim3(256), 0, st, a);
         return;
@@ -1432,8 +1446,8 @@ static int launch_fwd(const ConvArgs& a, int mode, hipStream_t st) {
     constexpr int BM = 32 * TM * WM_, BN = 32 * TN * WN_;
     dim3 grid(ceil_div(a.M, BM), ceil_div(a.g.Co, BN), a.g.nphase * a.nsplit);
     if (a.xcd) grid = dim3(grid.x * grid.y, 1, grid.z);
-    if (a.e.io_f16) {
-        const int io = a.e.io_f16;
+    if (a.e.io_f16 & 3) {
+        const int io = a.e.io_f16 & 3;
 #define HY_H(MODE_, SPLIT_)                                                                                       \
     {                                                                                                            \
         if (io == 1) hipLaunchKernelGGL((conv_fwd_h_kernel<TM, TN, WM_, WN_, MODE_, SPLIT_, 1>), grid, dim3(256), 0, st, a); \
@@ -1742,11 +1756,11 @@ static int launch_wres16(const ConvArgs& a, hipStream_t st) {
     const int per = wres_blocks(ntiles, groups);
     const dim3 grid(per * groups);
     static const int variant = env_int("HYRES_WRES_VARIANT", 1);
-    if (a.e.io_f16 == 0 && variant == 0) {  // A/B: halo prefetch issued before the residual loads
+    if ((a.e.io_f16 & 3) == 0 && variant == 0) {  // A/B: halo prefetch issued before the residual loads
         hipLaunchKernelGGL((conv3x3_wres_f16_kernel<0, 0>), grid, dim3(512), 0, st, a, ntiles, groups);
         return HY_LAUNCH_CHECK("conv3x3_wres_f16_kernel");
     }
-    switch (a.e.io_f16) {
+    switch (a.e.io_f16 & 3) {
         case 0: hipLaunchKernelGGL(conv3x3_wres_f16_kernel<0>, grid, dim3(512), 0, st, a, ntiles, groups); break;
         case 1: hipLaunchKernelGGL(conv3x3_wres_f16_kernel<1>, grid, dim3(512), 0, st, a, ntiles, groups); break;
         case 2: hipLaunchKernelGGL(conv3x3_wres_f16_kernel<2>, grid, dim3(512), 0, st, a, ntiles, groups); break;
@@ -1759,7 +1773,7 @@ static int launch_wres16(const ConvArgs& a, hipStream_t st) {
 // block; HYRES_CONV_WRES32=0 turns it off
 static bool wres32_ok(const hyres_conv_geom* g, const hyres_epilogue* e) {
     static const int on = env_int("HYRES_CONV_WRES32", 1);
-    if (!on || e->f16_operands || e->io_f16 || e->square_input || g->nphase != 1 || g->ntaps != 9 || g->Ci != 64 ||
+    if (!on || e->f16_operands || (e->io_f16 & 3) || e->square_input || g->nphase != 1 || g->ntaps != 9 || g->Ci != 64 ||
         g->Co % 32 != 0)
         return false;
     if (g->ish != 1 || g->isw != 1 || g->Hi != g->Ho || g->Wi != g->Wo || g->Hq != g->Ho || g->Wq != g->Wo ||
@@ -1784,7 +1798,7 @@ static int launch_wres32(const ConvArgs& a, hipStream_t st) {
 static int launch_halo16(const ConvArgs& a, hipStream_t st) {
     const hyres_conv_geom& g = a.g;
     const int blocks = g.B * ((g.Ho + HALO_R - 1) / HALO_R) * (g.Wo / HALO_TW) * (g.Co / 64);
-    switch (a.e.io_f16) {
+    switch (a.e.io_f16 & 3) {
         case 0: hipLaunchKernelGGL(conv3x3_halo_f16_kernel<0>, dim3(blocks), dim3(256), 0, st, a); break;
         case 1: hipLaunchKernelGGL(conv3x3_halo_f16_kernel<1>, dim3(blocks), dim3(256), 0, st, a); break;
         case 2: hipLaunchKernelGGL(conv3x3_halo_f16_kernel<2>, dim3(blocks), dim3(256), 0, st, a); break;
@@ -1815,7 +1829,7 @@ static int stream_nt(const hyres_conv_geom* g, const hyres_epilogue* e) {
     static const int on = env_int("HYRES_CONV_STREAM1X1", 1);
     static const int on16 = env_int("HYRES_CONV_STREAM1X1_F16", 1);  // autocast: fp16-rounded operands
     static const long long min_px = env_int("HYRES_CONV_STREAM_PIXELS", 65536);
-    if (!on || (e->f16_operands && !on16) || e->io_f16 || e->square_input || e->kind != HYRES_EPI_BIAS) return 0;
+    if (!on || (e->f16_operands && !on16) || (e->io_f16 & 3) || e->square_input || e->kind != HYRES_EPI_BIAS) return 0;
     if (g->nphase != 1 || g->ntaps != 1 || g->ish != 1 || g->isw != 1 || g->dh[0] != 0 || g->dw[0] != 0) return 0;
     if (g->Hi != g->Hq || g->Wi != g->Wq || g->Ho != g->Hq || g->Wo != g->Wq) return 0;
     if ((long long)g->B * g->Hq * g->Wq < min_px) return 0;
@@ -1967,7 +1981,9 @@ int hyres_conv_forward(const hyres_conv_geom* g, const float* x, const float* w2
     if (e->kind == HYRES_EPI_GDN_BWD || e->kind == HYRES_EPI_IGDN_BWD)
         HY_REQUIRE(e->aux0 && e->aux1 && e->aux2, HYRES_E_ARG, "conv: GDN bwd epilogue needs aux0..2");
     if (e->act == HYRES_ACT_PRELU) HY_REQUIRE(e->slope, HYRES_E_ARG, "conv: PReLU needs slope");
-    if (e->io_f16) {
+    HY_REQUIRE(e->io_f16 >= 0 && e->io_f16 <= 4, HYRES_E_ARG, "conv: io_f16 %d (fp16 X/Y bits, or AUX16 alone)",
+               e->io_f16);
+    if (e->io_f16 & 3) {
         HY_REQUIRE(e->io_f16 >= 1 && e->io_f16 <= 3 && !e->accumulate &&
                        (e->kind == HYRES_EPI_BIAS || e->kind == HYRES_EPI_GDN || e->kind == HYRES_EPI_IGDN),
                    HYRES_E_ARG, "conv: fp16 activations are forward-only (no accumulate / GDN backward)");
@@ -2041,7 +2057,7 @@ int hyres_conv_kernel_name(const hyres_conv_geom* g, const hyres_epilogue* e, in
         return 0;
     }
     if (ch.mode == 0 && halo16_ok(g, e)) {
-        snprintf(buf, n, "%s<%d>", wres16_ok(g) ? "conv3x3_wres_f16_kernel" : "conv3x3_halo_f16_kernel", e->io_f16);
+        snprintf(buf, n, "%s<%d>", wres16_ok(g) ? "conv3x3_wres_f16_kernel" : "conv3x3_halo_f16_kernel", e->io_f16 & 3);
         return 0;
     }
     {
@@ -2053,9 +2069,9 @@ int hyres_conv_kernel_name(const hyres_conv_geom* g, const hyres_epilogue* e, in
     }
     static const char* tiles[5] = {"2, 2, 2, 2", "2, 1, 2, 2", "1, 1, 4, 1", "1, 2, 2, 2", "1, 1, 2, 2"};
     const bool f16 = e->f16_operands && ch.mode != 2;
-    if (e->io_f16) {
+    if (e->io_f16 & 3) {
         snprintf(buf, n, "conv_fwd_h_kernel<%s, %d, %s, %d>", tiles[ch.tile], ch.mode, split ? "true" : "false",
-                 e->io_f16);
+                 e->io_f16 & 3);
         return 0;
     }
     snprintf(buf, n, "conv_fwd_kernel<%s, %d, %s, %s>", tiles[ch.tile], ch.mode, split ? "true" : "false",

@@ -277,6 +277,7 @@ __global__ __launch_bounds__(256) void se_pool4_kernel(const float* x, const flo
     }
 }
 // backward: partial sums of gy*x per (b,c)
+template <bool H = false>
 __global__ void se_bwd_pool_kernel(const float* x, const float* gy, int HW, int C, int per, float* part) {
     const int b = blockIdx.x, ch = blockIdx.y;
     const int p0 = ch * per, p1 = min(HW, p0 + per);
@@ -284,7 +285,7 @@ __global__ void se_bwd_pool_kernel(const float* x, const float* gy, int HW, int 
         float s = 0.f;
         for (int p = p0; p < p1; ++p) {
             long long i = ((long long)b * HW + p) * C + c;
-            s += gy[i] * x[i];
+            s += gy[i] * ldv<H>(x, i);
         }
         part[((long long)b * gridDim.y + ch) * C + c] = s;
     }
@@ -413,6 +414,7 @@ __global__ void sa_mul_kernel(const float* x, const float* attn, float* y, long 
     }
 }
 // bwd 1: g_logit[p] = (sum_c gy*x) * a*(1-a)
+template <bool H = false>
 __global__ void sa_bwd_logit_kernel(const float* x, const float* gy, const float* attn, float* glogit, long long P,
                                     int C) {
     // 16 lanes per pixel (4 pixels per wave), 4 xor-shuffles
@@ -423,7 +425,7 @@ __global__ void sa_bwd_logit_kernel(const float* x, const float* gy, const float
     if (ok) {
         for (int c = 4 * l16; c < C; c += 64) {
             const float4 g = *reinterpret_cast<const float4*>(gy + p * C + c);
-            const float4 v = *reinterpret_cast<const float4*>(x + p * C + c);
+            const float4 v = ldv4<H>(x, p * C + c);
             s += (g.x * v.x + g.y * v.y) + (g.z * v.z + g.w * v.w);
         }
     }
@@ -629,9 +631,11 @@ int hyres_se_fwd_f16(const void* x, const float* w1, const float* w2, void* y, f
     return HY_LAUNCH_CHECK("se_scale_f16");
 }
 
-int hyres_se_bwd(const float* x, const float* gy, const float* w1, const float* w2, const float* pooled,
-                 const float* hidden, const float* sgate, float* gx, float* gw1, float* gw2, int B, int HW, int C,
-                 int Cr, void* ws, long long ws_bytes, hyres_stream_t s) {
+extern "C++" {
+template <bool H>
+static int se_bwd_impl(const float* x, const float* gy, const float* w1, const float* w2, const float* pooled,
+                       const float* hidden, const float* sgate, float* gx, float* gw1, float* gw2, int B, int HW, int C,
+                       int Cr, void* ws, long long ws_bytes, hyres_stream_t s) {
     HY_REQUIRE(x && gy && w1 && w2 && pooled && hidden && sgate && gx && gw1 && gw2, HYRES_E_ARG, "se_bwd: NULL");
     const int nch = se_chunks(HW);
     const long long need = (long long)B * nch * C * 4 + (long long)B * C * 4;
@@ -642,9 +646,9 @@ int hyres_se_bwd(const float* x, const float* gy, const float* w1, const float* 
     float* gpool = part + (long long)B * nch * C;
     hipStream_t st = as_stream(s);
     if (C % 4 == 0 && C <= 1024 && 256 % (C / 4) == 0 && aligned16(x) && aligned16(gy))
-        hipLaunchKernelGGL(se_pool4_kernel<true>, dim3(B, nch), dim3(256), 0, st, x, gy, HW, C, per, part);
+        hipLaunchKernelGGL((se_pool4_kernel<true, H>), dim3(B, nch), dim3(256), 0, st, x, gy, HW, C, per, part);
     else
-        hipLaunchKernelGGL(se_bwd_pool_kernel, dim3(B, nch), dim3(256), 0, st, x, gy, HW, C, per, part);
+        hipLaunchKernelGGL(se_bwd_pool_kernel<H>, dim3(B, nch), dim3(256), 0, st, x, gy, HW, C, per, part);
     int rc = HY_LAUNCH_CHECK("se_bwd_pool");
     if (rc) return rc;
     hipLaunchKernelGGL(se_fc_bwd_kernel, dim3(1), dim3(256), (size_t)B * (C + Cr) * 4, st, (const float*)part, nch, B,
@@ -655,6 +659,18 @@ int hyres_se_bwd(const float* x, const float* gy, const float* w1, const float* 
     hipLaunchKernelGGL(se_bwd_x_kernel, dim3(grid_for_r(n)), dim3(256), 0, st, gy, sgate, (const float*)gpool, gx, B,
                        HW, C);
     return HY_LAUNCH_CHECK("se_bwd_x");
+}
+}  // extern "C++"
+int hyres_se_bwd(const float* x, const float* gy, const float* w1, const float* w2, const float* pooled,
+                 const float* hidden, const float* sgate, float* gx, float* gw1, float* gw2, int B, int HW, int C,
+                 int Cr, void* ws, long long ws_bytes, hyres_stream_t s) {
+    return se_bwd_impl<false>(x, gy, w1, w2, pooled, hidden, sgate, gx, gw1, gw2, B, HW, C, Cr, ws, ws_bytes, s);
+}
+int hyres_se_bwd_f16(const void* x, const float* gy, const float* w1, const float* w2, const float* pooled,
+                     const float* hidden, const float* sgate, float* gx, float* gw1, float* gw2, int B, int HW, int C,
+                     int Cr, void* ws, long long ws_bytes, hyres_stream_t s) {
+    return se_bwd_impl<true>((const float*)x, gy, w1, w2, pooled, hidden, sgate, gx, gw1, gw2, B, HW, C, Cr, ws,
+                             ws_bytes, s);
 }
 
 static int sa_bwd_blocks(long long n) {  // >= 4 pixels per thread: the 98-tap weight fold is amortised
@@ -705,11 +721,14 @@ int hyres_spatial_attn_fwd_f16(const void* x, const float* w, float* pooled2, in
     return HY_LAUNCH_CHECK("sa_mul_f16");
 }
 
-int hyres_spatial_attn_bwd(const float* x, const float* w, const float* pooled2, const int* argmax, const float* attn,
-                           const float* gy, float* gx, float* gw, int B, int H, int W, int C, void* ws,
-                           long long ws_bytes, hyres_stream_t s) {
+extern "C++" {
+template <bool HF>
+static int spatial_attn_bwd_impl(const float* x, const float* w, const float* pooled2, const int* argmax,
+                                 const float* attn, const float* gy, float* gx, float* gw, int B, int H, int W, int C,
+                                 void* ws, long long ws_bytes, hyres_stream_t s) {
     HY_REQUIRE(x && w && pooled2 && argmax && attn && gy && gx && gw, HYRES_E_ARG, "spatial_attn_bwd: NULL");
-    HY_REQUIRE(C % 4 == 0 && C <= 1024 && aligned16(x) && aligned16(gy) && aligned16(gx), HYRES_E_ALIGN,
+    HY_REQUIRE(C % 4 == 0 && C <= 1024 && (reinterpret_cast<uintptr_t>(x) & 7) == 0 && aligned16(gy) && aligned16(gx),
+               HYRES_E_ALIGN,
                "spatial_attn: C %% 4 == 0 and 16B-aligned x/gy/gx required");
     long long P = (long long)B * H * W;
     HY_REQUIRE(ws && ws_bytes >= hyres_spatial_attn_workspace_bytes(B, H, W), HYRES_E_WORKSPACE,
@@ -718,8 +737,8 @@ int hyres_spatial_attn_bwd(const float* x, const float* w, const float* pooled2,
     float* gp2 = glogit + P;
     float* wpart = gp2 + 2 * P;
     hipStream_t st = as_stream(s);
-    hipLaunchKernelGGL(sa_bwd_logit_kernel, dim3((unsigned)((P + 15) / 16)), dim3(256), 0, st, x, gy, attn, glogit, P,
-                       C);
+    hipLaunchKernelGGL(sa_bwd_logit_kernel<HF>, dim3((unsigned)((P + 15) / 16)), dim3(256), 0, st, x, gy, attn, glogit,
+                       P, C);
     int rc = HY_LAUNCH_CHECK("sa_bwd_logit");
     if (rc) return rc;
     int nb = sa_bwd_blocks(P);
@@ -733,6 +752,18 @@ int hyres_spatial_attn_bwd(const float* x, const float* w, const float* pooled2,
     hipLaunchKernelGGL(sa_bwd_x_kernel, dim3(grid_for_r(P * C / 4)), dim3(256), 0, st, gy, attn, (const float*)gp2,
                        argmax, gx, P, C);
     return HY_LAUNCH_CHECK("sa_bwd_x");
+}
+}  // extern "C++"
+int hyres_spatial_attn_bwd(const float* x, const float* w, const float* pooled2, const int* argmax, const float* attn,
+                           const float* gy, float* gx, float* gw, int B, int H, int W, int C, void* ws,
+                           long long ws_bytes, hyres_stream_t s) {
+    return spatial_attn_bwd_impl<false>(x, w, pooled2, argmax, attn, gy, gx, gw, B, H, W, C, ws, ws_bytes, s);
+}
+int hyres_spatial_attn_bwd_f16(const void* x, const float* w, const float* pooled2, const int* argmax,
+                               const float* attn, const float* gy, float* gx, float* gw, int B, int H, int W, int C,
+                               void* ws, long long ws_bytes, hyres_stream_t s) {
+    return spatial_attn_bwd_impl<true>((const float*)x, w, pooled2, argmax, attn, gy, gx, gw, B, H, W, C, ws, ws_bytes,
+                                       s);
 }
 
 }  // extern "C"

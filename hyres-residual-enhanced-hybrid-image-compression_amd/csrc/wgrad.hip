@@ -626,9 +626,12 @@ __device__ __forceinline__ halfx4_t lds_tr4(const _Float16* p) {
     return __builtin_bit_cast(halfx4_t, v);
 }
 
-// ONE: a 1x1 stride-1 gradient on the base grid (Q row = P row): Q rows load like P rows, no pixel decode
-template <int TM, int TN, int WAVES_M, int WAVES_N, int NT, bool SQ, bool ONE = false>
+// ONE: a 1x1 stride-1 gradient on the base grid (Q row = P row): Q rows load like P rows, no pixel decode.
+// IOH: operands stored fp16 in HBM (AMP training's saved activations): bit 0 P, bit 1 Q (8-byte loads of 4
+// channels; the fp16 -> fp32 -> fp16 round trip into LDS is exact).
+template <int TM, int TN, int WAVES_M, int WAVES_N, int NT, bool SQ, bool ONE = false, int IOH = 0>
 __global__ __launch_bounds__(256) void wgrad_f16_kernel(const WgradArgs a) {
+    constexpr bool PH = (IOH & 1) != 0, QH = (IOH & 2) != 0;
     constexpr int BM = 32 * TM * WAVES_M;
     constexpr int BN = 32 * TN * WAVES_N;
     constexpr int PP = BM + 32, PQ = BN + 32;  // halves
@@ -691,7 +694,7 @@ __global__ __launch_bounds__(256) void wgrad_f16_kernel(const WgradArgs a) {
         for (int i = 0; i < P_V; ++i) {
             const long long qq = k0 + prow0 + i * PRS;
             float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (qq < Qtot && m0 + pc < d.M) v = ld4(a.p + qq * d.ldp + m0 + pc);
+            if (qq < Qtot && m0 + pc < d.M) v = ldv4<PH>(a.p, qq * d.ldp + m0 + pc);
             rp[i] = v;
         }
     };
@@ -702,7 +705,7 @@ __global__ __launch_bounds__(256) void wgrad_f16_kernel(const WgradArgs a) {
 #pragma unroll
             for (int i = 0; i < Q_V; ++i) {
                 const long long qq = k0 + qrow0 + i * QRS;
-                rq[i] = (qq < Qtot && n0 + qc < d.N) ? ld4(a.q + qq * d.ldq + n0 + qc) : make_float4(0.f, 0.f, 0.f, 0.f);
+                rq[i] = (qq < Qtot && n0 + qc < d.N) ? ldv4<QH>(a.q, qq * d.ldq + n0 + qc) : make_float4(0.f, 0.f, 0.f, 0.f);
             }
             return;
         }
@@ -712,7 +715,7 @@ __global__ __launch_bounds__(256) void wgrad_f16_kernel(const WgradArgs a) {
             if (q_b[i] >= 0 && n0 + qc < d.N && t < d.ntaps) {
                 const int ih = q_i[i] * d.sq + d.dh[t], iw = q_j[i] * d.sq + d.dw[t];
                 if (ih >= 0 && ih < d.Hqq && iw >= 0 && iw < d.Wqq)
-                    v = ld4(a.q + ((long long)(q_b[i] * d.Hqq + ih) * d.Wqq + iw) * d.ldq + n0 + qc);
+                    v = ldv4<QH>(a.q, ((long long)(q_b[i] * d.Hqq + ih) * d.Wqq + iw) * d.ldq + n0 + qc);
             }
             if constexpr (SQ) { v.x *= v.x; v.y *= v.y; v.z *= v.z; v.w *= v.w; }
             rq[i] = v;
@@ -856,8 +859,9 @@ __global__ __launch_bounds__(256) void wgrad_f16_kernel(const WgradArgs a) {
 // The tap's B rows are halo rows base + k*SQ: the transposed read takes per-lane addresses, so the stride
 // is just a pitch of SQ*PQ. Bias gradient = fp32 column sums of the unrounded P (as wgrad_f16_kernel).
 // ------------------------------------------------------------------------------------------------
-template <int KR, int KW, int SQ, int DIL = 1>
+template <int KR, int KW, int SQ, int DIL = 1, int IOH = 0>
 __global__ __launch_bounds__(256, 2) void wgrad_halo_f16_kernel(const WgradArgs a, int dhg, int dwg) {
+    constexpr bool PH = (IOH & 1) != 0, QH = (IOH & 2) != 0;  // fp16 operands in HBM (wgrad_f16_kernel)
     constexpr int BM = 64, BN = 64, NT = KR * KW, HC = 31 * SQ + DIL * (KW - 1) + 1;
     constexpr int PP = BM + 32, PQ = BN + 32;  // halves
     constexpr int PSZ = KT * PP, HSZ = KR * HC * PQ;
@@ -891,7 +895,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo_f16_kernel(const WgradArgs 
         const long long q0 = (long long)kc * 32;
 #pragma unroll
         for (int q = 0; q < P_V; ++q)
-            rp[q] = m0 + pc < d.M ? ld4(a.p + (q0 + prow0 + 16 * q) * d.ldp + m0 + pc) : make_float4(0.f, 0.f, 0.f, 0.f);
+            rp[q] = m0 + pc < d.M ? ldv4<PH>(a.p, (q0 + prow0 + 16 * q) * d.ldp + m0 + pc) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
         for (int q = 0; q < H_V; ++q) {
             const int e = tid + 256 * q;
@@ -899,7 +903,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo_f16_kernel(const WgradArgs 
             const int hr = pix / HC, hc = pix - (pix / HC) * HC;
             const int ih = i * SQ + dh0 + DIL * hr, iw = j0 * SQ + dwg + hc;
             const bool ok = e < H_E && (unsigned)ih < (unsigned)d.Hqq && (unsigned)iw < (unsigned)d.Wqq && n0 + c < d.N;
-            rh[q] = ok ? ld4(a.q + ((long long)(b * d.Hqq + ih) * d.Wqq + iw) * d.ldq + n0 + c)
+            rh[q] = ok ? ldv4<QH>(a.q, ((long long)(b * d.Hqq + ih) * d.Wqq + iw) * d.ldq + n0 + c)
                        : make_float4(0.f, 0.f, 0.f, 0.f);
         }
     };
@@ -1015,7 +1019,7 @@ constexpr int THIN_ROWS = 5, THIN_SPAN = 264;  // staged window: rows x columns 
 constexpr int THIN_COLS = THIN_SPAN;
 constexpr int THIN_STAGE = (THIN_ROWS * THIN_COLS + 255) / 256;  // staged window entries per thread
 
-template <int MW, int NC, int TG, int SQ>
+template <int MW, int NC, int TG, int SQ, bool PH = false>  // PH: P (the wide operand) fp16 in HBM
 __global__ __launch_bounds__(256) void wgrad_thin_kernel(const WgradArgs a, int rpb, int dhmin, int dwmin, int nrow,
                                                          int ncol) {
     constexpr int PCH = 64 / MW;            // pixels per P chunk (PCH x 64*MW floats = 16 KB)
@@ -1054,13 +1058,13 @@ __global__ __launch_bounds__(256) void wgrad_thin_kernel(const WgradArgs a, int 
     float4 pr4[PV];
     for (int r = r0; r < r1; ++r) {
         const int b = r / d.Hq, i = r - (r / d.Hq) * d.Hq;
-        const float* prow = a.p + (long long)r * d.Wq * d.ldp;
+        const long long prow = (long long)r * d.Wq * d.ldp;  // element offset of this row's first pixel
         auto load_chunk = [&](int c0) {
 #pragma unroll
             for (int k = 0; k < PV; ++k) {
                 const int idx = tid + 256 * k;
                 const int px = idx / (16 * MW), c4 = idx - (idx / (16 * MW)) * (16 * MW);
-                pr4[k] = c0 + px < d.Wq ? ld4(prow + (long long)(c0 + px) * d.ldp + 4 * c4)
+                pr4[k] = c0 + px < d.Wq ? ldv4<PH>(a.p, prow + (long long)(c0 + px) * d.ldp + 4 * c4)
                                         : make_float4(0.f, 0.f, 0.f, 0.f);
             }
         };
@@ -1424,7 +1428,36 @@ static hyres_wgrad_desc wgrad_swapped(const hyres_wgrad_desc* d) {
     e.N = d->M; e.ldq = d->ldp;
     for (int t = 0; t < d->ntaps; ++t) { e.dh[t] = -d->dh[t]; e.dw[t] = -d->dw[t]; }
     e.sm = d->sn; e.sn = d->sm;
+    e.io_f16 = ((d->io_f16 & 1) << 1) | ((d->io_f16 >> 1) & 1);
     return e;
+}
+
+// fp16 operands (desc.io_f16) the chosen kernel reads natively: the f16 MFMA kernels one of P / Q (both fp16
+// never occurs in AMP training: one side is always a gradient), the thin kernel a fp16 P; every other fp16
+// operand is converted into fp32 scratch before the launch (hyres_wgrad_workspace_bytes reserves it)
+static int wgrad_native_io(const hyres_wgrad_desc* d, bool thin) {
+    const int io = d->io_f16 & 3;
+    if (!io) return 0;
+    if (wgrad_f16_ok(d)) return (io == 3 || d->square_q) ? (io & 2) : io;  // square_q: only Q is read as fp16
+    if (thin) return io & 1;
+    return 0;
+}
+
+static long long wgrad_cvt_floats(const hyres_wgrad_desc* d, int native) {
+    const int cvt = (d->io_f16 & 3) & ~native;
+    long long n = 0;
+    if (cvt & 1) n += (long long)d->B * d->Hq * d->Wq * d->M + 8;  // + 16-byte alignment slack
+    if (cvt & 2) n += (long long)d->B * d->Hqq * d->Wqq * d->N + 8;
+    return n;
+}
+
+// fp16 [P][C] (pixel stride ld) -> contiguous fp32 [P][C]
+__global__ void half_to_float_2d_kernel(const _Float16* src, int ld, float* dst, long long P, int C) {
+    const long long n = P * C;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+        const long long p = i / C;
+        dst[i] = (float)src[p * ld + (i - p * C)];
+    }
 }
 
 // thin-operand weight-gradient plan (wgrad_thin_kernel): N <= 4, M in {64, 128}, the staged Q window fits
@@ -1459,16 +1492,21 @@ static bool thin_plan(const hyres_wgrad_desc* d, ThinPlan* tp) {
     return true;
 }
 
-static void launch_thin(const WgradArgs& a, const ThinPlan& p, hipStream_t st) {
+static void launch_thin(const WgradArgs& a, const ThinPlan& p, bool ph, hipStream_t st) {
     const dim3 grid(p.nblk, p.ngroups);
     auto go = [&](auto mw, auto nc, auto tg) {
         constexpr int MW_ = decltype(mw)::value, NC_ = decltype(nc)::value, TG_ = decltype(tg)::value;
-        if (p.sq == 1)
-            hipLaunchKernelGGL((wgrad_thin_kernel<MW_, NC_, TG_, 1>), grid, dim3(256), 0, st, a, p.rpb, p.dhmin,
-                               p.dwmin, p.nrow, p.ncol);
-        else
-            hipLaunchKernelGGL((wgrad_thin_kernel<MW_, NC_, TG_, 2>), grid, dim3(256), 0, st, a, p.rpb, p.dhmin,
-                               p.dwmin, p.nrow, p.ncol);
+        if (p.sq == 1) {
+            if (ph) hipLaunchKernelGGL((wgrad_thin_kernel<MW_, NC_, TG_, 1, true>), grid, dim3(256), 0, st, a, p.rpb,
+                                       p.dhmin, p.dwmin, p.nrow, p.ncol);
+            else hipLaunchKernelGGL((wgrad_thin_kernel<MW_, NC_, TG_, 1>), grid, dim3(256), 0, st, a, p.rpb, p.dhmin,
+                                    p.dwmin, p.nrow, p.ncol);
+        } else {
+            if (ph) hipLaunchKernelGGL((wgrad_thin_kernel<MW_, NC_, TG_, 2, true>), grid, dim3(256), 0, st, a, p.rpb,
+                                       p.dhmin, p.dwmin, p.nrow, p.ncol);
+            else hipLaunchKernelGGL((wgrad_thin_kernel<MW_, NC_, TG_, 2>), grid, dim3(256), 0, st, a, p.rpb, p.dhmin,
+                                    p.dwmin, p.nrow, p.ncol);
+        }
     };
     using I1 = std::integral_constant<int, 1>;
     using I2 = std::integral_constant<int, 2>;
@@ -1511,7 +1549,7 @@ long long hyres_wgrad_workspace_bytes(const hyres_wgrad_desc* d) {
     auto need = [&](const WgradPlan& q) {
         const long long bias = swap ? hyres_colsum_workspace_bytes(d->B * d->Hq * d->Wq, d->M) / 4 + 4
                                     : (long long)q.nsplit * e.M + 4;
-        return (wgrad_slab_floats(&e, q) + bias) * 4;
+        return (wgrad_slab_floats(&e, q) + bias + wgrad_cvt_floats(&e, wgrad_native_io(&e, false))) * 4;
     };
     long long bytes = need(p);
     ThinPlan tp;
@@ -1528,9 +1566,10 @@ int hyres_conv_wgrad(const hyres_wgrad_desc* d0, const float* pp, const float* q
     HY_REQUIRE(d0 && pp && qq && dst, HYRES_E_ARG, "wgrad: NULL");
     const long long need = hyres_wgrad_workspace_bytes(d0);
     HY_REQUIRE(ws && ws_bytes >= need, HYRES_E_WORKSPACE, "wgrad: workspace %lld < %lld", ws_bytes, need);
+    HY_REQUIRE(!(dbias && (d0->io_f16 & 1)), HYRES_E_ARG, "wgrad: the bias gradient needs an fp32 P");
     const float* p_orig = pp;
     const bool swap = wgrad_swap(d0);
-    const hyres_wgrad_desc dd = swap ? wgrad_swapped(d0) : *d0;
+    hyres_wgrad_desc dd = swap ? wgrad_swapped(d0) : *d0;
     const hyres_wgrad_desc* d = &dd;
     if (swap) std::swap(pp, qq);
     WgradPlan p = wgrad_plan(d);
@@ -1538,6 +1577,36 @@ int hyres_conv_wgrad(const hyres_wgrad_desc* d0, const float* pp, const float* q
     const bool thin = thin_plan(d, &tp) && aligned16(pp);
     if (thin) p.nsplit = tp.nblk;
     float* bias_ws = (float*)ws + wgrad_slab_floats(d, p);
+    int io = dd.io_f16 & 3;
+    {
+        // fp16 operands the chosen kernel cannot read: contiguous fp32 copies after the slab and bias partials
+        // (the plan does not depend on the operand dtype or pixel stride beyond the checks below)
+        const int native = wgrad_native_io(d, thin);
+        const int cvt = io & ~native;
+        auto al4 = [](long long n) { return (n + 3) & ~3LL; };
+        float* cws = (float*)ws + al4(wgrad_slab_floats(d, p) + (swap ? hyres_colsum_workspace_bytes(d0->B * d0->Hq * d0->Wq,
+                                                                                                      d0->M) / 4 + 4
+                                                                      : (long long)p.nsplit * d->M + 4));
+        hipStream_t st0 = as_stream(s);
+        if (cvt & 1) {
+            const long long P = (long long)dd.B * dd.Hq * dd.Wq;
+            hipLaunchKernelGGL(half_to_float_2d_kernel, dim3((unsigned)std::min<long long>((P * dd.M + 255) / 256, 8192)),
+                               dim3(256), 0, st0, (const _Float16*)pp, dd.ldp, cws, P, dd.M);
+            pp = cws; dd.ldp = dd.M; cws += al4(P * dd.M);
+        }
+        if (cvt & 2) {
+            const long long P = (long long)dd.B * dd.Hqq * dd.Wqq;
+            hipLaunchKernelGGL(half_to_float_2d_kernel, dim3((unsigned)std::min<long long>((P * dd.N + 255) / 256, 8192)),
+                               dim3(256), 0, st0, (const _Float16*)qq, dd.ldq, cws, P, dd.N);
+            qq = cws; dd.ldq = dd.N;
+        }
+        if (cvt) {
+            int rc0 = HY_LAUNCH_CHECK("half_to_float_2d");
+            if (rc0) return rc0;
+        }
+        io &= native;
+        dd.io_f16 = io;
+    }
     const bool vp = (d->M % 4 == 0) && (d->ldp % 4 == 0) && aligned16(pp);
     const bool vq = !p.tapn && (d->N % 4 == 0) && (d->ldq % 4 == 0) && aligned16(qq);
     HY_REQUIRE(!d->square_q || (vp && vq), HYRES_E_SHAPE, "wgrad: square_q needs the vector path");
@@ -1562,13 +1631,21 @@ int hyres_conv_wgrad(const hyres_wgrad_desc* d0, const float* pp, const float* q
         else if (p.WNc == 1) hipLaunchKernelGGL((wgrad1x1_kernel<1, 1, 4, 1>), grid, dim3(256), 0, st, a);
         else hipLaunchKernelGGL((wgrad1x1_kernel<1, 1, 2, 2>), grid, dim3(256), 0, st, a);
     } else if (thin) {
-        launch_thin(a, tp, st);
+        launch_thin(a, tp, (io & 1) != 0, st);
     } else if (p.halo && wgrad_f16_ok(d)) {
-        if (p.hk == 3 && p.hdil == 2)
-            hipLaunchKernelGGL((wgrad_halo_f16_kernel<3, 3, 1, 2>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
-        else if (p.hk == 3) hipLaunchKernelGGL((wgrad_halo_f16_kernel<3, 3, 1>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
-        else if (d->sq == 1) hipLaunchKernelGGL((wgrad_halo_f16_kernel<1, 5, 1>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
-        else hipLaunchKernelGGL((wgrad_halo_f16_kernel<1, 5, 2>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
+        auto halo16 = [&](auto ioc) {
+            constexpr int IO_ = decltype(ioc)::value;
+            if (p.hk == 3 && p.hdil == 2)
+                hipLaunchKernelGGL((wgrad_halo_f16_kernel<3, 3, 1, 2, IO_>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
+            else if (p.hk == 3)
+                hipLaunchKernelGGL((wgrad_halo_f16_kernel<3, 3, 1, 1, IO_>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
+            else if (d->sq == 1)
+                hipLaunchKernelGGL((wgrad_halo_f16_kernel<1, 5, 1, 1, IO_>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
+            else hipLaunchKernelGGL((wgrad_halo_f16_kernel<1, 5, 2, 1, IO_>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
+        };
+        if (io == 1) halo16(std::integral_constant<int, 1>{});
+        else if (io == 2) halo16(std::integral_constant<int, 2>{});
+        else halo16(std::integral_constant<int, 0>{});
     } else if (p.halo) {
         if (p.hk == 3 && p.hdil == 2)
             hipLaunchKernelGGL((wgrad_halo_kernel<3, 3, 1, 2>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
@@ -1579,13 +1656,26 @@ int hyres_conv_wgrad(const hyres_wgrad_desc* d0, const float* pp, const float* q
         static const int f16_one = env_int("HYRES_WGRAD_F16_1X1", 1);
         const bool one16 = f16_one && !sqr && d->ntaps == 1 && d->dh[0] == 0 && d->dw[0] == 0 && d->sq == 1 &&
                            d->Hqq == d->Hq && d->Wqq == d->Wq && p.ngroups == 1;
-        auto f16 = [&](auto tm, auto tn, auto wm_, auto wn_, auto ntc) {
+        auto f16io = [&](auto tm, auto tn, auto wm_, auto wn_, auto ntc, auto ioc) {
             constexpr int TM_ = decltype(tm)::value, TN_ = decltype(tn)::value;
             constexpr int WM2 = decltype(wm_)::value, WN2 = decltype(wn_)::value, NT_ = decltype(ntc)::value;
-            if (sqr) hipLaunchKernelGGL((wgrad_f16_kernel<TM_, TN_, WM2, WN2, NT_, true>), grid, dim3(256), 0, st, a);
-            else if (NT_ == 1 && one16)
-                hipLaunchKernelGGL((wgrad_f16_kernel<TM_, TN_, WM2, WN2, 1, false, true>), grid, dim3(256), 0, st, a);
-            else hipLaunchKernelGGL((wgrad_f16_kernel<TM_, TN_, WM2, WN2, NT_, false>), grid, dim3(256), 0, st, a);
+            constexpr int IO_ = decltype(ioc)::value;
+            if (sqr) {
+                if constexpr (IO_ != 1)  // GDN: Q = x (fp16 in AMP training), P = the fp32 norm gradient
+                    hipLaunchKernelGGL((wgrad_f16_kernel<TM_, TN_, WM2, WN2, NT_, true, false, IO_>), grid, dim3(256), 0,
+                                       st, a);
+            } else if (NT_ == 1 && one16) {
+                hipLaunchKernelGGL((wgrad_f16_kernel<TM_, TN_, WM2, WN2, 1, false, true, IO_>), grid, dim3(256), 0, st,
+                                   a);
+            } else {
+                hipLaunchKernelGGL((wgrad_f16_kernel<TM_, TN_, WM2, WN2, NT_, false, false, IO_>), grid, dim3(256), 0,
+                                   st, a);
+            }
+        };
+        auto f16 = [&](auto tm, auto tn, auto wm_, auto wn_, auto ntc) {
+            if (io == 1) f16io(tm, tn, wm_, wn_, ntc, std::integral_constant<int, 1>{});
+            else if (io == 2) f16io(tm, tn, wm_, wn_, ntc, std::integral_constant<int, 2>{});
+            else f16io(tm, tn, wm_, wn_, ntc, std::integral_constant<int, 0>{});
         };
         using I1 = std::integral_constant<int, 1>;
         using I2 = std::integral_constant<int, 2>;

@@ -19,6 +19,7 @@ MAX_TAPS = 49
 WPREP_CONV, WPREP_CONV_DGRAD, WPREP_DECONV, WPREP_DECONV_DGRAD = 0, 1, 2, 3
 EPI_BIAS, EPI_GDN, EPI_IGDN, EPI_GDN_BWD, EPI_IGDN_BWD = 0, 1, 2, 3, 4
 ACT_NONE, ACT_RELU, ACT_PRELU, ACT_RELU_MASK = 0, 1, 2, 3
+IO_X16, IO_Y16, IO_AUX16 = 1, 2, 4  # hyres_epilogue.io_f16 bits (fp16 activations in HBM)
 EB_REC = 64
 
 
@@ -49,7 +50,8 @@ class WgradDesc(ctypes.Structure):
                 ("B", "Hq", "Wq", "M", "ldp", "N", "ldq", "Hqq", "Wqq", "sq", "ntaps")] + [
         ("dh", ctypes.c_int * MAX_TAPS), ("dw", ctypes.c_int * MAX_TAPS),
         ("sm", ctypes.c_int), ("sn", ctypes.c_int), ("st", ctypes.c_int),
-        ("square_q", ctypes.c_int), ("accumulate", ctypes.c_int), ("f16_operands", ctypes.c_int)]
+        ("square_q", ctypes.c_int), ("accumulate", ctypes.c_int), ("f16_operands", ctypes.c_int),
+        ("io_f16", ctypes.c_int)]
 
 
 _P = ctypes.c_void_p
@@ -101,6 +103,12 @@ _SIGS = {
     "hyres_attn_gate_fwd": (_I, [_P, _P, _P, _P, _LL, _P]),
     "hyres_attn_gate_fwd_f16": (_I, [_P, _P, _P, _P, _LL, _P]),
     "hyres_attn_gate_bwd": (_I, [_P, _P, _P, _P, _P, _LL, _P]),
+    "hyres_attn_gate_bwd_f16": (_I, [_P, _P, _P, _P, _P, _LL, _P]),
+    "hyres_relu_bwd_2d_f16": (_I, [_P, _I, _P, _I, _P, _I, _LL, _I, _P]),
+    "hyres_prelu_bwd_f16": (_I, [_P, _I, _P, _I, _P, _I, _LL, _I, _P, _P, _P, _LL, _P]),
+    "hyres_gdn_dnorm_f16": (_I, [_P, _P, _P, _P, _LL, _I, _I, _P]),
+    "hyres_se_bwd_f16": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _LL, _P]),
+    "hyres_spatial_attn_bwd_f16": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _LL, _P]),
     "hyres_accumulate": (_I, [_P, _P, _LL, _P]),
     "hyres_scale": (_I, [_P, _P, _F, _P, _LL, _I, _P]),
     "hyres_add2d": (_I, [_P, _I, _P, _I, _LL, _I, _I, _P]),

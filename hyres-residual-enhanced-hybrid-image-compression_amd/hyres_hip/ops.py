@@ -540,6 +540,9 @@ def f16_convs() -> bool:
 
 
 F16_ACT = os.environ.get("HYRES_F16_ACT", "1") == "1"
+# AMP training stores the f16_region's activations (forward outputs saved for backward) as fp16 too, like
+# torch autocast, whose conv outputs are fp16 tensors (src/utils/engine.py:32); gradients stay fp32
+AMP_F16_ACT = os.environ.get("HYRES_AMP_F16_ACT", "1") == "1"
 _F16_REGION = [0]
 
 
@@ -555,18 +558,18 @@ def f16_region():
 
 
 def act_f16(tape: Optional["Tape"], H: int, W: int) -> bool:
-    """Store this activation as fp16 in HBM: inference (no tape) under ``torch.autocast(float16)`` — the
-    reference's C5 configuration ("fp16 activations": autocast makes every conv output fp16) — inside an
-    ``f16_region``. The latent-resolution entropy path (y, h_a, h_s, context, param_aggregation, the
-    likelihoods, the rANS symbols) stays fp32, so encoder and decoder index the same CDFs at any image size.
-    Arithmetic stays fp32 inside every kernel; HYRES_F16_ACT=0 keeps fp32 activations (fp16 operands only)."""
-    return tape is None and _F16_REGION[0] > 0 and F16_ACT and f16_convs()
+    """Store this activation as fp16 in HBM under ``torch.autocast(float16)`` inside an ``f16_region``: inference
+    (the reference's C5 configuration, "fp16 activations": autocast makes every conv output fp16) and AMP
+    training (train.sh --mixed-precision; HYRES_AMP_F16_ACT=0 keeps fp32 activations there), where the saved
+    activations are then read as fp16 by the backward kernels while gradients stay fp32. The latent-resolution
+    entropy path (y, h_a, h_s, context, param_aggregation, the likelihoods, the rANS symbols) stays fp32, so
+    encoder and decoder index the same CDFs at any image size. Arithmetic stays fp32 inside every kernel;
+    HYRES_F16_ACT=0 keeps fp32 activations everywhere (fp16 operands only)."""
+    return (tape is None or AMP_F16_ACT) and _F16_REGION[0] > 0 and F16_ACT and f16_convs()
 
 
 def _io_flags(x: "Node", y: "Node", tape: Optional["Tape"]) -> int:
-    io = (1 if x.half else 0) | (2 if y.half else 0)
-    assert io == 0 or tape is None, "fp16 activations are inference-only"
-    return io
+    return (L.IO_X16 if x.half else 0) | (L.IO_Y16 if y.half else 0)
 
 
 def _launch_conv(g: L.ConvGeom, x_ptr: int, w2: torch.Tensor, ldw: int, y_ptr: int, e: L.Epilogue) -> None:
@@ -681,13 +684,14 @@ def _act_backward(y: Node, gy: torch.Tensor, gy_ld: int, act: int, pre: Optional
         return gy, gy_ld
     gp = _empty((y.B, y.H, y.W, y.C), y.device)
     if act == L.ACT_RELU:
-        L.call("hyres_relu_bwd_2d", y.ptr(), y.ld, gy.data_ptr(), gy_ld, gp.data_ptr(), y.C, y.P, y.C,
-               L.stream())
+        L.call("hyres_relu_bwd_2d_f16" if y.half else "hyres_relu_bwd_2d", y.ptr(), y.ld, gy.data_ptr(), gy_ld,
+               gp.data_ptr(), y.C, y.P, y.C, L.stream())
     else:
         ws = _ws(L.load().hyres_reduce_workspace_bytes(y.P * y.C), y.device, slot=1)
         dslope = param_grad(slope) if slope.requires_grad else _empty((1,), y.device)
-        L.call("hyres_prelu_bwd", pre.data_ptr(), y.C, gy.data_ptr(), gy_ld, gp.data_ptr(), y.C, y.P, y.C,
-               slope.data_ptr(), dslope.data_ptr(), ws.data_ptr(), ws.numel(), L.stream())
+        L.call("hyres_prelu_bwd_f16" if pre.dtype == torch.float16 else "hyres_prelu_bwd", pre.data_ptr(), y.C,
+               gy.data_ptr(), gy_ld, gp.data_ptr(), y.C, y.P, y.C, slope.data_ptr(), dslope.data_ptr(), ws.data_ptr(),
+               ws.numel(), L.stream())
     return gp, y.C
 
 
@@ -732,7 +736,7 @@ def conv2d(tape: Optional[Tape], x: Node, weight: torch.Tensor, bias: Optional[t
     if act == L.ACT_PRELU:
         e.slope = slope.data_ptr()
         if tape is not None:
-            pre = _empty((B, Ho, Wo, Co), x.device)
+            pre = _empty((B, Ho, Wo, Co), x.device, y.v.dtype)  # stored by the epilogue in y's dtype
             e.out2 = pre.data_ptr()
             e.ldo2 = Co
     f16 = int(f16_convs())
@@ -761,6 +765,7 @@ def conv2d(tape: Optional[Tape], x: Node, weight: torch.Tensor, bias: Optional[t
             d.sm = Ci_w * KH * KW
             d.accumulate = 1
             d.f16_operands = f16 * AMP_WGRAD_F16
+            d.io_f16 = 2 if x.half else 0  # Q = the saved input activation
             _wgrad(d, gp.data_ptr(), x.ptr(), param_grad(weight), x.device,
                    param_grad(bias) if wants_grad(bias) else None, keep=(gp, x.v), side=True)
         if x.rg:
@@ -772,6 +777,7 @@ def conv2d(tape: Optional[Tape], x: Node, weight: torch.Tensor, bias: Optional[t
             w2d = _prepped(weight, gd, L.WPREP_CONV_DGRAD, Ci_w, Co, KH, KW, pad, mask)
             ed.accumulate = acc
             ed.f16_operands = f16
+            ed.io_f16 = L.IO_AUX16 if x.half else 0  # the ReLU mask reads x's fp16 values
             x.relu_mask_epilogue(ed, acc)
             _launch_conv(gd, gp.data_ptr(), w2d, gd.ntaps * Co, tgt.data_ptr(), ed)
 
@@ -817,6 +823,7 @@ def deconv2d(tape: Optional[Tape], x: Node, weight: torch.Tensor, bias: Optional
             L.call("hyres_wgrad_desc_deconv2d", ctypes.byref(d), B, H, W, Ci, x.ld, Co, gpld, K, pad)
             d.accumulate = 1
             d.f16_operands = f16 * AMP_WGRAD_F16
+            d.io_f16 = 1 if x.half else 0  # P = the saved input activation
             _wgrad(d, x.ptr(), gp.data_ptr(), param_grad(weight), x.device, keep=(gp, x.v), side=True)
         if x.rg:
             ed = L.Epilogue()
@@ -826,6 +833,7 @@ def deconv2d(tape: Optional[Tape], x: Node, weight: torch.Tensor, bias: Optional
             w2d = _prepped(weight, gd, L.WPREP_DECONV_DGRAD, Ci, Co, K, K, pad)
             ed.accumulate = acc
             ed.f16_operands = f16
+            ed.io_f16 = L.IO_AUX16 if x.half else 0
             x.relu_mask_epilogue(ed, acc)
             _launch_conv(gd, gp.data_ptr(), w2d, gd.ntaps * Co, tgt.data_ptr(), ed)
 
@@ -873,8 +881,8 @@ def gdn(tape: Optional[Tape], x: Node, beta: torch.Tensor, gamma: torch.Tensor, 
             L.call("hyres_add2d", gy.data_ptr(), gld, t.data_ptr(), C, y.P, C, 0, L.stream())
             gy = t
         dn = _empty((x.B, x.H, x.W, C), dev)
-        L.call("hyres_gdn_dnorm", gy.data_ptr(), y.ptr(), nrm.data_ptr(), dn.data_ptr(), y.P, C, int(inverse),
-               L.stream())
+        L.call("hyres_gdn_dnorm_f16" if y.half else "hyres_gdn_dnorm", gy.data_ptr(), y.ptr(), nrm.data_ptr(),
+               dn.data_ptr(), y.P, C, int(inverse), L.stream())
         if beta.requires_grad or gamma.requires_grad:
             dgp = _empty((C, C), dev)
             d = L.WgradDesc()
@@ -882,6 +890,7 @@ def gdn(tape: Optional[Tape], x: Node, beta: torch.Tensor, gamma: torch.Tensor, 
             d.square_q = 1
             d.accumulate = 0
             d.f16_operands = f16 * AMP_WGRAD_F16
+            d.io_f16 = 2 if x.half else 0
             _wgrad(d, dn.data_ptr(), x.ptr(), dgp, dev)
             dbp = _empty((C,), dev)
             _colsum_into(dn, y.P, C, C, dbp, acc=0)
@@ -901,6 +910,7 @@ def gdn(tape: Optional[Tape], x: Node, beta: torch.Tensor, gamma: torch.Tensor, 
             ed.aux2 = nrm.data_ptr()
             ed.ld2 = C
             ed.f16_operands = f16
+            ed.io_f16 = L.IO_AUX16 if x.half else 0  # x and the saved norm are fp16 (AMP training)
             _launch_conv(gd, dn.data_ptr(), w2d, C, tgt.data_ptr(), ed)
 
     tape.push(bwd)
@@ -913,10 +923,10 @@ def attn_gate(tape: Optional[Tape], a: Node, b: Node, x: Node) -> Node:
     n = a.P * a.C
     out = Node.new(a.B, a.H, a.W, a.C, a.device, dtype=a.v.dtype)
     if a.half:
-        assert b.half and x.half and tape is None
+        assert b.half and x.half
         L.call("hyres_attn_gate_fwd_f16", a.ptr(), b.ptr(), x.ptr(), out.ptr(), n, L.stream())
-        return out
-    L.call("hyres_attn_gate_fwd", a.ptr(), b.ptr(), x.ptr(), out.ptr(), n, L.stream())
+    else:
+        L.call("hyres_attn_gate_fwd", a.ptr(), b.ptr(), x.ptr(), out.ptr(), n, L.stream())
     if tape is None:
         return out
 
@@ -927,7 +937,8 @@ def attn_gate(tape: Optional[Tape], a: Node, b: Node, x: Node) -> Node:
         ga, acc_a = a.grad_target()
         gb, acc_b = b.grad_target()
         assert acc_a == 0 and acc_b == 0, "gate inputs are single-consumer"
-        L.call("hyres_attn_gate_bwd", a.ptr(), b.ptr(), g.data_ptr(), ga.data_ptr(), gb.data_ptr(), n, L.stream())
+        L.call("hyres_attn_gate_bwd_f16" if a.half else "hyres_attn_gate_bwd", a.ptr(), b.ptr(), g.data_ptr(),
+               ga.data_ptr(), gb.data_ptr(), n, L.stream())
         if x.rg:
             x.set_grad(g)
 

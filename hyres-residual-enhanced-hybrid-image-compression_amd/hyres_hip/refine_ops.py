@@ -18,13 +18,13 @@ def bilinear(tape: Optional[Tape], x: Node, Ho: int, Wo: int, scale_h: float, sc
     1/scale_factor when a scale_factor is given (enhancement.py:96,101), in/out for ``size=``
     (enhancement.py:98,103)."""
     y = out if out is not None else Node.new(x.B, Ho, Wo, x.C, x.device, dtype=x.v.dtype)
-    if x.half:  # fp16 activations (autocast inference)
-        assert y.half and tape is None
+    if x.half:  # fp16 activations (autocast; the backward below only reads gradients)
+        assert y.half
         L.call("hyres_bilinear_fwd_f16", x.ptr(), x.ld, y.ptr(), y.ld, x.B, x.H, x.W, Ho, Wo, x.C, float(scale_h),
                float(scale_w), L.stream())
-        return y
-    L.call("hyres_bilinear_fwd", x.ptr(), x.ld, y.ptr(), y.ld, x.B, x.H, x.W, Ho, Wo, x.C, float(scale_h),
-           float(scale_w), 0, L.stream())
+    else:
+        L.call("hyres_bilinear_fwd", x.ptr(), x.ld, y.ptr(), y.ld, x.B, x.H, x.W, Ho, Wo, x.C, float(scale_h),
+               float(scale_w), 0, L.stream())
     if tape is None:
         return y
 
@@ -53,7 +53,6 @@ def se_block(tape: Optional[Tape], x: Node, w1: torch.Tensor, w2: torch.Tensor) 
     wsb = L.load().hyres_se_workspace_bytes(B, HW, C)
     ws = _ws(wsb + B * C * 4, dev, slot=1)
     fn = "hyres_se_fwd_f16" if x.half else "hyres_se_fwd"
-    assert not x.half or tape is None
     L.call(fn, x.ptr(), w1.data_ptr(), w2.data_ptr(), y.ptr(), pooled.data_ptr(), hidden.data_ptr(),
            sgate.data_ptr(), B, HW, C, Cr, ws.data_ptr(), ws.numel(), L.stream())
     if tape is None:
@@ -69,7 +68,8 @@ def se_block(tape: Optional[Tape], x: Node, w1: torch.Tensor, w2: torch.Tensor) 
         tgt, acc = x.grad_target()
         gx = tgt if acc == 0 else _empty((x.B, x.H, x.W, C), dev)
         ws2 = _ws(wsb + B * C * 4, dev, slot=1)
-        L.call("hyres_se_bwd", x.ptr(), g.data_ptr(), w1.data_ptr(), w2.data_ptr(), pooled.data_ptr(),
+        L.call("hyres_se_bwd_f16" if x.half else "hyres_se_bwd", x.ptr(), g.data_ptr(), w1.data_ptr(),
+               w2.data_ptr(), pooled.data_ptr(),
                hidden.data_ptr(), sgate.data_ptr(), gx.data_ptr(), gw1.data_ptr(), gw2.data_ptr(), B, HW, C, Cr,
                ws2.data_ptr(), ws2.numel(), L.stream())
         if acc:
@@ -89,7 +89,6 @@ def spatial_attention_mul(tape: Optional[Tape], x: Node, w: torch.Tensor) -> Nod
     attn = _empty((B, H, W), dev)
     y = Node.new(B, H, W, C, dev, dtype=x.v.dtype)
     fn = "hyres_spatial_attn_fwd_f16" if x.half else "hyres_spatial_attn_fwd"
-    assert not x.half or tape is None
     L.call(fn, x.ptr(), w.data_ptr(), pooled2.data_ptr(), argmax.data_ptr(), attn.data_ptr(), y.ptr(), B, H, W, C,
            L.stream())
     if tape is None:
@@ -105,7 +104,8 @@ def spatial_attention_mul(tape: Optional[Tape], x: Node, w: torch.Tensor) -> Nod
         gw = param_grad(w) if w.requires_grad else _empty(w.shape, dev)
         wsb = L.load().hyres_spatial_attn_workspace_bytes(B, H, W)
         ws = _ws(wsb, dev, slot=1)
-        L.call("hyres_spatial_attn_bwd", x.ptr(), w.data_ptr(), pooled2.data_ptr(), argmax.data_ptr(),
+        L.call("hyres_spatial_attn_bwd_f16" if x.half else "hyres_spatial_attn_bwd", x.ptr(), w.data_ptr(),
+               pooled2.data_ptr(), argmax.data_ptr(),
                attn.data_ptr(), g.data_ptr(), gx.data_ptr(), gw.data_ptr(), B, H, W, C, ws.data_ptr(), ws.numel(),
                L.stream())
         if acc:

@@ -114,6 +114,9 @@ int hyres_conv_weight_prep_batch(const void* descs, int n, long long total, hyre
 #define HYRES_ACT_RELU_MASK 3 /* ReLU backward fused into an input-gradient: y = (aux0 > 0) ? y : 0,
                                  aux0 = the ReLU output of the layer whose gradient is produced */
 
+#define HYRES_IO_X16 1   /* hyres_epilogue.io_f16 bits */
+#define HYRES_IO_Y16 2
+#define HYRES_IO_AUX16 4
 typedef struct hyres_epilogue {
     int kind, act, accumulate;    /* accumulate: y += result (gradient accumulation) */
     int square_input;             /* GEMM A-operand prologue x -> x*x (GDN norm) */
@@ -127,11 +130,13 @@ typedef struct hyres_epilogue {
     int f16_operands;             /* 1: X and W2 rounded to fp16 in the LDS staging, v_mfma_f32_32x32x16_f16
                                    * with fp32 accumulation and fp32 epilogue (autocast-fp16 inference,
                                    * BASELINE configs[4]); ignored on the small-Ci and narrow paths */
-    int io_f16;                   /* fp16 activations in HBM (autocast inference, configs[4]): bit 0 = X is
-                                   * fp16, bit 1 = Y and the epilogue's activation operands (res, aux0,
-                                   * out2) are fp16 (bias/slope stay fp32). Forward only: no accumulate,
-                                   * no GDN-backward kinds. X-fp16 needs Ci % 32 == 0 (or the narrow
-                                   * Co <= 4 kernel, whose Y stays fp32). */
+    int io_f16;                   /* fp16 activations in HBM (autocast, configs[4] and AMP training): bit 0 =
+                                   * X is fp16, bit 1 = Y and the epilogue's activation operands (res, aux0,
+                                   * out2) are fp16 (bias/slope stay fp32); bits 0/1: no accumulate, no
+                                   * GDN-backward kinds. X-fp16 needs Ci % 32 == 0 (or the narrow Co <= 4
+                                   * kernel, whose Y stays fp32). Bit 2 (HYRES_IO_AUX16, backward convs with
+                                   * fp32 X/Y): the saved activations the epilogue reads — aux0 (the ReLU
+                                   * mask's y, GDN-backward's x) and aux2 (GDN-backward's norm) — are fp16. */
 } hyres_epilogue;
 
 /* Y = conv(X, W2) with the epilogue — nn.Conv2d / nn.ConvTranspose2d / GDN forward and their
@@ -178,6 +183,9 @@ typedef struct hyres_wgrad_desc {
     int square_q;                /* Q -> Q*Q (GDN gamma gradient) */
     int accumulate;
     int f16_operands;            /* AMP: P, Q rounded to fp16 on the f16 MFMA, fp32 accumulation */
+    int io_f16;                  /* fp16 operands in HBM (AMP training, fp16 saved activations): bit 0 = P is
+                                  * fp16, bit 1 = Q is fp16; read natively by the f16 weight-gradient kernels
+                                  * and the thin kernel (P), converted to fp32 scratch for the others */
 } hyres_wgrad_desc;
 int hyres_wgrad_desc_conv2d(hyres_wgrad_desc* d, int B, int H, int W, int Ci, int ldx, int Co,
                             int ldy, int KH, int KW, int stride, int pad, int dil);
@@ -222,6 +230,15 @@ int hyres_attn_gate_fwd(const float* a, const float* b, const float* x, float* o
 int hyres_attn_gate_fwd_f16(const void* a, const void* b, const void* x, void* out, long long n, hyres_stream_t s);
 int hyres_attn_gate_bwd(const float* a, const float* b, const float* g, float* ga, float* gb,
                         long long n, hyres_stream_t s);
+/* Backward passes with fp16 SAVED activations (AMP training: the forward wrote y / pre / a, b / x / norm as
+ * fp16; gradients stay fp32; fp32 arithmetic; 8B-aligned fp16 operands): same semantics as the fp32
+ * entry points of the same name without the suffix. */
+int hyres_relu_bwd_2d_f16(const void* y, int ldy_, const float* g, int ldg, float* gx, int ldgx, long long P,
+                          int C, hyres_stream_t s);
+int hyres_prelu_bwd_f16(const void* x, int ldx, const float* g, int ldg, float* gx, int ldgx, long long P,
+                        int C, const float* slope, float* dslope, void* ws, long long ws_bytes, hyres_stream_t s);
+int hyres_attn_gate_bwd_f16(const void* a, const void* b, const float* g, float* ga, float* gb, long long n,
+                            hyres_stream_t s);
 /* y (+)= x  (gradient fan-in) */
 int hyres_accumulate(const float* x, float* y, long long n, hyres_stream_t s);
 /* y[p*ldy + c] (+)= x[p*ldx + c]  over P pixels x C channels (strided gradient fan-in / copy) */
@@ -245,6 +262,9 @@ int hyres_gdn_reparam_bwd(const float* beta, const float* gamma, const float* db
 /* GDN backward helper: dn = g * y / n * (-0.5 GDN | +0.5 IGDN) */
 int hyres_gdn_dnorm(const float* g, const float* y, const float* n, float* dn, long long P, int C,
                     int inverse, hyres_stream_t s);
+/* the same with fp16 y and n (AMP training) */
+int hyres_gdn_dnorm_f16(const float* g, const void* y, const void* n, float* dn, long long P, int C,
+                        int inverse, hyres_stream_t s);
 
 /* ------------------------------------------------------------------------------------------ */
 /* quantisation, checkerboard context, entropy models                                         */
@@ -337,6 +357,13 @@ int hyres_se_fwd_f16(const void* x, const float* w1, const float* w2, void* y, f
                      float* sgate, int B, int HW, int C, int Cr, void* ws, long long ws_bytes, hyres_stream_t s);
 int hyres_spatial_attn_fwd_f16(const void* x, const float* w, float* pooled2, int* argmax, float* attn,
                                void* y, int B, int H, int W, int C, hyres_stream_t s);
+/* their backward passes with fp16 x (AMP training; gy, gx fp32) */
+int hyres_se_bwd_f16(const void* x, const float* gy, const float* w1, const float* w2, const float* pooled,
+                     const float* hidden, const float* sgate, float* gx, float* gw1, float* gw2, int B, int HW,
+                     int C, int Cr, void* ws, long long ws_bytes, hyres_stream_t s);
+int hyres_spatial_attn_bwd_f16(const void* x, const float* w, const float* pooled2, const int* argmax,
+                               const float* attn, const float* gy, float* gx, float* gw, int B, int H, int W,
+                               int C, void* ws, long long ws_bytes, hyres_stream_t s);
 
 /* ------------------------------------------------------------------------------------------ */
 /* losses and optimiser (src/losses/rd_loss.py:18-44, src/utils/engine.py:56-90)              */

@@ -1,0 +1,302 @@
+"""AMP training with fp16 SAVED activations (``ops.AMP_F16_ACT``): inside an ``f16_region`` the forward outputs
+that backward reads are stored as fp16 in HBM — as torch autocast's conv outputs are fp16 tensors
+(/root/reference/src/utils/engine.py:32, train.sh:19 ``--mixed-precision``) — while gradients stay fp32.
+
+Why exact comparisons are possible: every kernel computes in fp32 from its operands; the fp16-storage
+variants only change how a saved activation is read (8-byte loads of 4 halves, converted exactly) or how
+an output is written (rounded once). So on fp16-representable inputs
+  * each fp16-saved-activation backward entry point equals its fp32 twin BIT FOR BIT;
+  * a conv / deconv / GDN layer's weight and input gradients equal those of the fp32-storage layer bit for
+    bit when no activation mask is involved (the f16 MFMA kernels round their operands to fp16 anyway; the
+    fp32 weight-gradient kernels read an exact fp32 copy of the fp16 operand);
+  * a ResidualUnit chain matches torch (float64) with the same fp16 rounding points to 1e-4.
+The whole model under autocast is pinned to the reference's own autocast run in
+test_parity_gpu.py::test_amp_matches_reference_autocast_fixture (which now runs with fp16 activations)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from helpers import rel_err
+
+pytestmark = pytest.mark.gpu
+
+
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    return torch.device("cuda:0")
+
+
+def _rand(shape, seed, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.rand(shape, generator=g) * 2 - 1) * scale
+
+
+def _h(t):
+    """fp16-representable fp32 copy."""
+    return t.half().float()
+
+
+# ------------------------------------------------------------------------------------------ elementwise
+def test_f16_saved_activation_backward_entry_points_bitwise():
+    """relu / PReLU / attention gate / GDN dnorm / SE / spatial-attention backward with fp16 saved operands
+    equal the fp32 entry points on the same (fp16-representable) values, bit for bit (the PReLU slope gradient,
+a block reduction, within 1e-6: measured 1 ulp, the two instantiations contract their multiply-adds
+differently)."""
+    from hyres_hip import _lib as L
+    from hyres_hip import ops as O
+    D = dev()
+    B, H, W, C = 2, 16, 24, 64
+    P = B * H * W
+    y = _h(_rand((P, C), 1)).to(D)
+    g = _rand((P, C), 2).to(D)
+    s = L.stream()
+
+    def pair(name, args16, args32, outs, tol=None):
+        res = []
+        for fn, args in ((name + "_f16", args16), (name, args32)):
+            for o in outs:
+                o.zero_()
+            L.call(fn, *args)
+            res.append([o.clone() for o in outs])
+        torch.cuda.synchronize()
+        for k, (a, b) in enumerate(zip(*res)):
+            if tol is not None and tol[k] > 0:  # a reduction: FMA contraction may differ between the two builds
+                assert rel_err(a.cpu(), b.cpu()) <= tol[k], (name, k)
+                continue
+            if not torch.equal(a, b):
+                bad = (a != b).nonzero()
+                print(name, k, "mismatches", bad.shape[0], "first", bad[:4].tolist(), a[tuple(bad[0])].item(),
+                      b[tuple(bad[0])].item())
+            assert torch.equal(a, b), (name, k)
+
+    gx = torch.empty(P, C, device=D)
+    yh = y.half()
+    pair("hyres_relu_bwd_2d", (yh.data_ptr(), C, g.data_ptr(), C, gx.data_ptr(), C, P, C, s),
+         (y.data_ptr(), C, g.data_ptr(), C, gx.data_ptr(), C, P, C, s), [gx])
+    slope = torch.tensor([0.25], device=D)
+    dslope = torch.zeros(1, device=D)
+    ws = torch.empty(int(L.load().hyres_reduce_workspace_bytes(P * C)), dtype=torch.uint8, device=D)
+    pair("hyres_prelu_bwd", (yh.data_ptr(), C, g.data_ptr(), C, gx.data_ptr(), C, P, C, slope.data_ptr(),
+                             dslope.data_ptr(), ws.data_ptr(), ws.numel(), s),
+         (y.data_ptr(), C, g.data_ptr(), C, gx.data_ptr(), C, P, C, slope.data_ptr(), dslope.data_ptr(),
+          ws.data_ptr(), ws.numel(), s), [gx, dslope], tol=[0, 1e-6])
+    b = _h(_rand((P, C), 3)).to(D)
+    bh = b.half()
+    ga, gb = torch.empty(P, C, device=D), torch.empty(P, C, device=D)
+    pair("hyres_attn_gate_bwd", (yh.data_ptr(), bh.data_ptr(), g.data_ptr(), ga.data_ptr(), gb.data_ptr(), P * C, s),
+         (y.data_ptr(), b.data_ptr(), g.data_ptr(), ga.data_ptr(), gb.data_ptr(), P * C, s), [ga, gb])
+    nrm = _h(_rand((P, C), 4).abs() + 0.5).to(D)
+    nh = nrm.half()
+    dn = torch.empty(P, C, device=D)
+    for inv in (0, 1):
+        pair("hyres_gdn_dnorm", (g.data_ptr(), yh.data_ptr(), nh.data_ptr(), dn.data_ptr(), P, C, inv, s),
+             (g.data_ptr(), y.data_ptr(), nrm.data_ptr(), dn.data_ptr(), P, C, inv, s), [dn])
+    # SE / spatial attention: run the fp32 forward on the fp16-representable x for the saved state, then both
+    # backward flavours
+    Cr = 4
+    w1 = _rand((Cr, C), 5, 0.2).to(D)
+    w2 = _rand((C, Cr), 6, 0.2).to(D)
+    pooled, hidden, sgate = (torch.empty(B, C, device=D), torch.empty(B, Cr, device=D), torch.empty(B, C, device=D))
+    yse = torch.empty(P, C, device=D)
+    wsb = int(L.load().hyres_se_workspace_bytes(B, H * W, C)) + B * C * 4
+    ws = torch.empty(wsb, dtype=torch.uint8, device=D)
+    L.call("hyres_se_fwd", y.data_ptr(), w1.data_ptr(), w2.data_ptr(), yse.data_ptr(), pooled.data_ptr(),
+           hidden.data_ptr(), sgate.data_ptr(), B, H * W, C, Cr, ws.data_ptr(), ws.numel(), s)
+    gw1, gw2 = torch.zeros(Cr, C, device=D), torch.zeros(C, Cr, device=D)
+    pair("hyres_se_bwd", (yh.data_ptr(), g.data_ptr(), w1.data_ptr(), w2.data_ptr(), pooled.data_ptr(),
+                          hidden.data_ptr(), sgate.data_ptr(), gx.data_ptr(), gw1.data_ptr(), gw2.data_ptr(), B, H * W,
+                          C, Cr, ws.data_ptr(), ws.numel(), s),
+         (y.data_ptr(), g.data_ptr(), w1.data_ptr(), w2.data_ptr(), pooled.data_ptr(), hidden.data_ptr(),
+          sgate.data_ptr(), gx.data_ptr(), gw1.data_ptr(), gw2.data_ptr(), B, H * W, C, Cr, ws.data_ptr(),
+          ws.numel(), s), [gx, gw1, gw2])
+    wsa = _rand((1, 2, 7, 7), 7, 0.1).to(D)
+    pooled2 = torch.empty(P, 2, device=D)
+    amax = torch.empty(P, dtype=torch.int32, device=D)
+    attn = torch.empty(P, device=D)
+    ysa = torch.empty(P, C, device=D)
+    L.call("hyres_spatial_attn_fwd", y.data_ptr(), wsa.data_ptr(), pooled2.data_ptr(), amax.data_ptr(),
+           attn.data_ptr(), ysa.data_ptr(), B, H, W, C, s)
+    gw = torch.zeros(1, 2, 7, 7, device=D)
+    wsb = int(L.load().hyres_spatial_attn_workspace_bytes(B, H, W))
+    ws = torch.empty(wsb, dtype=torch.uint8, device=D)
+    pair("hyres_spatial_attn_bwd", (yh.data_ptr(), wsa.data_ptr(), pooled2.data_ptr(), amax.data_ptr(),
+                                    attn.data_ptr(), g.data_ptr(), gx.data_ptr(), gw.data_ptr(), B, H, W, C,
+                                    ws.data_ptr(), ws.numel(), s),
+         (y.data_ptr(), wsa.data_ptr(), pooled2.data_ptr(), amax.data_ptr(), attn.data_ptr(), g.data_ptr(),
+          gx.data_ptr(), gw.data_ptr(), B, H, W, C, ws.data_ptr(), ws.numel(), s), [gx, gw])
+
+
+# ------------------------------------------------------------------------------------------ conv layers
+LAYER_CASES = [
+    # kind, B, Ci, Co, H, W, K, stride, pad, dil
+    ("conv", 2, 64, 64, 32, 64, 3, 1, 1, 1),      # f16 halo weight gradient (Q = x fp16), 3x3 dgrad
+    ("conv", 2, 64, 64, 20, 64, 3, 1, 2, 2),      # dilated 3x3 (MultiScaleRefine)
+    ("conv", 4, 64, 128, 64, 64, 1, 1, 0, 1),     # 1x1: f16 ONE weight-gradient path
+    ("conv", 2, 128, 128, 32, 32, 5, 2, 2, 1),    # 5x5 stride 2 (g_a), Q stride 2
+    ("conv", 2, 64, 96, 12, 20, 3, 1, 1, 1),      # generic f16 weight gradient (rows not a multiple of 32)
+    ("conv", 2, 64, 3, 16, 64, 3, 1, 1, 1),       # Co = 3: swapped thin weight gradient with a fp16 P
+    ("deconv", 2, 128, 128, 16, 32, 5, 2, 2, 1),  # P = x fp16 (g_s)
+    ("deconv", 2, 128, 3, 16, 16, 5, 2, 2, 1),    # thin weight gradient with a fp16 P (g_s's last deconv)
+]
+
+
+@pytest.mark.parametrize("wgrad_f16", [1, 0])
+@pytest.mark.parametrize("case", LAYER_CASES)
+def test_layer_with_fp16_input_matches_fp32_storage(case, wgrad_f16, monkeypatch):
+    """One conv / deconv recorded on the tape under autocast inside an f16_region with its input stored fp16,
+    against the same layer on an fp32 node holding the same values (AMP_F16_ACT off): weight, bias and
+    input gradients bit-identical (no mask: act none); the fp16 output within fp16 rounding of the fp32 one.
+    wgrad_f16 = 0 (HYRES_AMP_WGRAD_F16=0): the fp32 weight-gradient kernels on the converted operand."""
+    from hyres_hip import ops as O
+    kind, B, Ci, Co, H, W, K, s, p, d = case
+    D = dev()
+    x = _h(_rand((B, Ci, H, W), 11)).to(D)
+    if kind == "conv":
+        w = _rand((Co, Ci, K, K), 12, 1.0 / (Ci * K * K) ** 0.5).to(D)
+    else:
+        w = _rand((Ci, Co, K, K), 12, 1.0 / (Ci * K * K / 4) ** 0.5).to(D)
+    b = _rand((Co,), 13, 0.1).to(D)
+    monkeypatch.setattr(O, "AMP_WGRAD_F16", wgrad_f16)
+    res = {}
+    for f16_act in (True, False):
+        monkeypatch.setattr(O, "AMP_F16_ACT", f16_act)
+        wd, bd = torch.nn.Parameter(w.clone()), torch.nn.Parameter(b.clone())
+        tape = O.Tape()
+        xn = O.to_nhwc(x, rg=True)
+        if f16_act:
+            xn = O.Node(xn.v.half(), rg=True)
+        with torch.autocast("cuda", dtype=torch.float16), O.f16_region():
+            if kind == "conv":
+                yn = O.conv2d(tape, xn, wd, bd, stride=s, pad=p, dil=d)
+            else:
+                yn = O.deconv2d(tape, xn, wd, bd)
+        assert yn.half == (f16_act and Co > 4)
+        gy = _rand((yn.B, yn.C, yn.H, yn.W), 14).to(D)
+        y = O.to_nchw(yn)
+        yn.set_grad(O.nchw_grad_to_nhwc(gy))
+        tape.backward()
+        torch.cuda.synchronize()
+        res[f16_act] = (y, O.to_nchw_grad(xn), wd.grad.clone(), bd.grad.clone())
+    (y16, gx16, gw16, gb16), (y32, gx32, gw32, gb32) = res[True], res[False]
+    print(case, "forward fp16-stored vs fp32:", rel_err(y16.cpu(), y32.cpu()),
+          "vs fp32 rounded:", rel_err(y16.cpu(), y32.half().float().cpu()))
+    assert rel_err(y16.cpu(), y32.cpu()) < 1e-3  # one fp16 rounding of the same fp32 value (+ summation order)
+    assert torch.equal(gx16, gx32)
+    assert torch.equal(gw16, gw32)
+    assert torch.equal(gb16, gb32)
+
+
+def test_gdn_with_fp16_activations_matches_fp32_storage(monkeypatch):
+    """GDN / IGDN in AMP training with fp16 x, y and saved norm: the norm gradient (gdn_dnorm_f16), the gamma
+    weight gradient (square_q with a fp16 Q) and the input gradient (GDN-backward epilogue reading fp16 x and
+    norm through HYRES_IO_AUX16) against the fp32-storage layer fed the fp16-rounded y and norm: 1e-5."""
+    from hyres_hip import ops as O
+    D = dev()
+    B, C, H, W = 2, 128, 16, 32
+    x = _h(_rand((B, C, H, W), 21)).to(D)
+    beta = (torch.rand(C, generator=torch.Generator().manual_seed(22)) + 0.5).to(D)
+    gamma = (0.1 * torch.eye(C) + 0.01 * torch.rand(C, C, generator=torch.Generator().manual_seed(23))).to(D)
+    for inverse in (False, True):
+        res = {}
+        for f16_act in (True, False):
+            monkeypatch.setattr(O, "AMP_F16_ACT", f16_act)
+            bp, gp = torch.nn.Parameter(beta.clone()), torch.nn.Parameter(gamma.clone())
+            tape = O.Tape()
+            xn = O.to_nhwc(x, rg=True)
+            if f16_act:
+                xn = O.Node(xn.v.half(), rg=True)
+            with torch.autocast("cuda", dtype=torch.float16), O.f16_region():
+                yn = O.gdn(tape, xn, bp, gp, inverse)
+            gy = _rand((B, C, H, W), 24).to(D)
+            y = O.to_nchw(yn)
+            yn.set_grad(O.nchw_grad_to_nhwc(gy))
+            tape.backward()
+            torch.cuda.synchronize()
+            res[f16_act] = (y, O.to_nchw_grad(xn), bp.grad.clone(), gp.grad.clone())
+        (y16, gx16, gb16, gg16), (y32, gx32, gb32, gg32) = res[True], res[False]
+        assert rel_err(y16.cpu(), y32.cpu()) < 1e-3
+        # the fp16 path's backward reads y and the norm rounded to fp16: bounded by that rounding
+        for a, r in ((gx16, gx32), (gb16, gb32), (gg16, gg32)):
+            assert rel_err(a.cpu(), r.cpu()) < 2e-3, (inverse, rel_err(a.cpu(), r.cpu()))
+
+
+def test_residual_unit_chain_fp16_activations_vs_torch():
+    """AttentionBlock's ResidualUnit (models/layers/attention.py:11-30): relu(x + 1x1(relu(3x3(relu(1x1(x)))))),
+    x fp16, under autocast inside an f16_region with fp16 saved activations. Torch (float64) with the same
+    rounding points: fp16 operands for every GEMM (forward, input and weight gradients), each stored
+    activation rounded to fp16, gradients fp32. The input-gradient convs apply the ReLU masks from the fp16
+    activations (HYRES_IO_AUX16). 1e-4 relative (summation order moves a few fp16 roundings by one ulp)."""
+    from hyres_hip import _lib as L
+    from hyres_hip import ops as O
+    D = dev()
+    B, N, H, W = 2, 128, 32, 64
+    x = _h(_rand((B, N, H, W), 31))
+    ws = [_rand((N // 2, N, 1, 1), 32, N ** -0.5), _rand((N // 2, N // 2, 3, 3), 33, (N / 2 * 9) ** -0.5),
+          _rand((N, N // 2, 1, 1), 34, (N / 2) ** -0.5)]
+    bs = [_rand((c,), 35 + i, 0.1) for i, c in enumerate((N // 2, N // 2, N))]
+    gy = _rand((B, N, H, W), 38)
+
+    # torch reference (float64), fp16 rounding where the HIP path rounds
+    def r16(t):
+        return t.half().double()
+    xd = x.double().requires_grad_()
+    wd = [w.double().requires_grad_() for w in ws]
+    bd = [b.double().requires_grad_() for b in bs]
+
+    class Round(torch.autograd.Function):  # fp16 storage of a forward output; gradients pass unrounded
+        @staticmethod
+        def forward(ctx, t):
+            return r16(t)
+
+        @staticmethod
+        def backward(ctx, g):
+            return g
+
+    class Conv16(torch.autograd.Function):
+        """f16-MFMA conv: fp16 operands in every GEMM (forward: x, w; backward: the incoming gradient and w /
+        x), fp32-or-better accumulation, the bias gradient from the unrounded gradient."""
+        @staticmethod
+        def forward(ctx, t, w, b, pad):
+            th, wh = r16(t), r16(w)
+            ctx.save_for_backward(th, wh)
+            ctx.pad = pad
+            return F.conv2d(th, wh, b, padding=pad)
+
+        @staticmethod
+        def backward(ctx, g):
+            th, wh = ctx.saved_tensors
+            gh = r16(g)
+            gx = torch.nn.grad.conv2d_input(th.shape, wh, gh, padding=ctx.pad)
+            gw = torch.nn.grad.conv2d_weight(th, wh.shape, gh, padding=ctx.pad)
+            return gx, gw, g.sum((0, 2, 3)), None
+
+    def conv(t, i, pad):
+        return Conv16.apply(t, wd[i], bd[i], pad)
+
+    t1 = Round.apply(F.relu(conv(xd, 0, 0)))
+    t2 = Round.apply(F.relu(conv(t1, 1, 1)))
+    y = Round.apply(F.relu(conv(t2, 2, 0) + xd))
+    y.backward(gy.double())
+
+    Dv = D
+    wp = [torch.nn.Parameter(w.to(Dv)) for w in ws]
+    bp = [torch.nn.Parameter(b.to(Dv)) for b in bs]
+    tape = O.Tape()
+    xn = O.to_nhwc(x.to(Dv), rg=True)
+    xn = O.Node(xn.v.half(), rg=True)
+    with torch.autocast("cuda", dtype=torch.float16), O.f16_region():
+        a1 = O.conv2d(tape, xn, wp[0], bp[0], act=L.ACT_RELU)
+        a2 = O.conv2d(tape, a1, wp[1], bp[1], pad=1, act=L.ACT_RELU)
+        yn = O.conv2d(tape, a2, wp[2], bp[2], act=L.ACT_RELU, res=xn)
+    assert a1.half and a2.half and yn.half
+    yh = O.to_nchw(yn)
+    yn.set_grad(O.nchw_grad_to_nhwc(gy.to(Dv)))
+    tape.backward()
+    torch.cuda.synchronize()
+    print("chain a1", rel_err(O.to_nchw(a1).cpu(), t1.detach().float()), "a2",
+          rel_err(O.to_nchw(a2).cpu(), t2.detach().float()), "y", rel_err(yh.cpu(), y.detach().float()))
+    assert rel_err(yh.cpu(), y.detach().float()) < 2e-3  # max-norm: one fp16 ulp of the largest |y|
+    assert rel_err(O.to_nchw_grad(xn).cpu(), xd.grad.float()) < 1e-4
+    for i in range(3):
+        assert rel_err(wp[i].grad.cpu(), wd[i].grad.float()) < 1e-4, i
+        assert rel_err(bp[i].grad.cpu(), bd[i].grad.float()) < 1e-4, i
