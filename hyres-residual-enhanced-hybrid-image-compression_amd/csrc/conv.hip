@@ -244,8 +244,12 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
     if constexpr (MODE == 2) nk = (ntap * Ci + KT - 1) / KT;
     else nk = ntap * (Ci / KT);
 
-    float4 ra[MODE == 2 ? 1 : A_V], rb[MODE == 2 ? 1 : B_V];
+    float4 ra[MODE == 2 || XH ? 1 : A_V], rb[MODE == 2 ? 1 : B_V];
+    // fp16 X: the raw halves stay in registers until the LDS store (converting at the load would make the
+    // prefetch of the next chunk wait for its data before this chunk's MFMAs)
+    half4_t rah[XH ? A_V : 1];
     float sa[MODE == 2 ? A_V : 1], sb[MODE == 2 ? B_V : 1];
+    static_assert(!XH || F16, "fp16 X is staged for the f16 MFMA");
 
     // vector path: raw buffer loads (out-of-range offset -> 0, no branches). The X resource starts at
     // the block's first image so 32-bit byte offsets suffice (host checks 3 images < 2 GB).
@@ -280,15 +284,13 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
                 const int ih = a_i[q] + o.x, iw = a_j[q] + o.y;
                 const bool ok = a_ok[q] && (unsigned)ih < (unsigned)g.Hi && (unsigned)iw < (unsigned)g.Wi;
                 const int off = ok ? (a_base[q] + (ih * g.Wi + iw) * g.ldx + c0) * XES : (int)0x80000000;
-                float4 v;
                 if constexpr (XH) {
-                    const half4_t h = __builtin_bit_cast(half4_t, __builtin_amdgcn_raw_buffer_load_b64(xr, off, 0, 0));
-                    v = make_float4((float)h.x, (float)h.y, (float)h.z, (float)h.w);
+                    rah[q] = __builtin_bit_cast(half4_t, __builtin_amdgcn_raw_buffer_load_b64(xr, off, 0, 0));
                 } else {
-                    v = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
+                    float4 v = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
+                    if constexpr (MODE == 1) { v.x *= v.x; v.y *= v.y; v.z *= v.z; v.w *= v.w; }
+                    ra[q] = v;
                 }
-                if constexpr (MODE == 1) { v.x *= v.x; v.y *= v.y; v.z *= v.z; v.w *= v.w; }
-                ra[q] = v;
             }
 #pragma unroll
             for (int q = 0; q < B_V; ++q) {
@@ -327,7 +329,17 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
             typedef _Float16 half4 __attribute__((ext_vector_type(4)));
 #pragma unroll
             for (int q = 0; q < A_V; ++q) {
-                const half4 h = {(_Float16)ra[q].x, (_Float16)ra[q].y, (_Float16)ra[q].z, (_Float16)ra[q].w};
+                half4 h;
+                if constexpr (XH && MODE == 1) {  // GDN norm: x^2 of the fp16 x, rounded for the MFMA
+                    const half4_t r = rah[q];
+                    const float4 v = make_float4((float)r.x * (float)r.x, (float)r.y * (float)r.y,
+                                                 (float)r.z * (float)r.z, (float)r.w * (float)r.w);
+                    h = half4{(_Float16)v.x, (_Float16)v.y, (_Float16)v.z, (_Float16)v.w};
+                } else if constexpr (XH) {
+                    h = __builtin_bit_cast(half4, rah[q]);
+                } else {
+                    h = half4{(_Float16)ra[q].x, (_Float16)ra[q].y, (_Float16)ra[q].z, (_Float16)ra[q].w};
+                }
                 *reinterpret_cast<half4*>(&Ah[(tid / 8 + 32 * q) * PADH + 4 * c4]) = h;
             }
 #pragma unroll
@@ -624,7 +636,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_halo_f16_kernel(const ConvArgs
     const int lr = lane & 31, lh = lane >> 5;
 
     // ---- halo staging (part p of chunk c: elements [p*PE, (p+1)*PE) of the 396 px x 8 float4)
-    float4 hreg[HALO_PV];
+    std::conditional_t<XH, half4_t, float4> hreg[HALO_PV];  // fp16 X: raw halves until the LDS store
     auto hload = [&](int part, int c) {
         const int ci0 = c * 32;
 #pragma unroll
@@ -637,8 +649,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_halo_f16_kernel(const ConvArgs
                             (unsigned)iw < (unsigned)g.Wi;
             const int off = ok ? ((ih * g.Wi + iw) * g.ldx + ci0 + 4 * c4) * XES : (int)0x80000000;
             if constexpr (XH) {
-                const half4_t h = __builtin_bit_cast(half4_t, __builtin_amdgcn_raw_buffer_load_b64(xr, off, 0, 0));
-                hreg[q] = make_float4((float)h.x, (float)h.y, (float)h.z, (float)h.w);
+                hreg[q] = __builtin_bit_cast(half4_t, __builtin_amdgcn_raw_buffer_load_b64(xr, off, 0, 0));
             } else {
                 hreg[q] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
             }
@@ -650,7 +661,9 @@ __global__ __launch_bounds__(256, 2) void conv3x3_halo_f16_kernel(const ConvArgs
             const int e = part * HALO_PE + tid + 256 * q;
             if (e < (part + 1) * HALO_PE && e < HALO_E) {
                 const int px = e >> 3, c4 = e & 7;
-                const half4_t h = {(_Float16)hreg[q].x, (_Float16)hreg[q].y, (_Float16)hreg[q].z, (_Float16)hreg[q].w};
+                half4_t h;
+                if constexpr (XH) h = hreg[q];
+                else h = half4_t{(_Float16)hreg[q].x, (_Float16)hreg[q].y, (_Float16)hreg[q].z, (_Float16)hreg[q].w};
                 *reinterpret_cast<half4_t*>(&hal[buf * HBUF + px * HALO_PH + 4 * c4]) = h;
             }
         }
@@ -803,7 +816,8 @@ __global__ __launch_bounds__(512, 2) void conv3x3_wres_f16_kernel(const ConvArgs
     };
     // halo chunks are prefetched TWO steps ahead (two register sets, alternating): one step of MFMA work
     // (~2.3k cycles per SIMD) does not cover an HBM-bound 50 KB-per-CU chunk load
-    auto hload = [&](float4 (&h)[WRES_HV], int step) {
+    using HRT = std::conditional_t<XH, half4_t, float4>;  // fp16 X: raw halves until the LDS store
+    auto hload = [&](HRT (&h)[WRES_HV], int step) {
         int b, i0, j0;
         tile_of(step >> 1, b, i0, j0);
         const int c = step & 1;
@@ -817,19 +831,20 @@ __global__ __launch_bounds__(512, 2) void conv3x3_wres_f16_kernel(const ConvArgs
             const bool ok = e < HALO_E && (unsigned)ih < (unsigned)g.Hi && (unsigned)iw < (unsigned)g.Wi;
             const int off = ok ? (base + (ih * g.Wi + iw) * g.ldx + 32 * c + 4 * c4) * XES : (int)0x80000000;
             if constexpr (XH) {
-                const half4_t hh = __builtin_bit_cast(half4_t, __builtin_amdgcn_raw_buffer_load_b64(xr, off, 0, 0));
-                h[v] = make_float4((float)hh.x, (float)hh.y, (float)hh.z, (float)hh.w);
+                h[v] = __builtin_bit_cast(half4_t, __builtin_amdgcn_raw_buffer_load_b64(xr, off, 0, 0));
             } else {
                 h[v] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
             }
         }
     };
-    auto hstore = [&](const float4 (&h)[WRES_HV], int buf) {
+    auto hstore = [&](const HRT (&h)[WRES_HV], int buf) {
 #pragma unroll
         for (int v = 0; v < WRES_HV; ++v) {
             const int e = tid + 512 * v;
             if (e < HALO_E) {
-                const half4_t hh = {(_Float16)h[v].x, (_Float16)h[v].y, (_Float16)h[v].z, (_Float16)h[v].w};
+                half4_t hh;
+                if constexpr (XH) hh = h[v];
+                else hh = half4_t{(_Float16)h[v].x, (_Float16)h[v].y, (_Float16)h[v].z, (_Float16)h[v].w};
                 *reinterpret_cast<half4_t*>(&Hs[buf * HBUF + (e >> 3) * HALO_PH + 4 * (e & 7)]) = hh;
             }
         }
@@ -853,7 +868,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3_wres_f16_kernel(const ConvArgs
         i = i0 + orow;
         pix = ((long long)b * g.Ho + i) * g.Wo + j0 + 32 * at + lr;
     };
-    auto body = [&](int s, float4 (&hl)[WRES_HV], const float4 (&hs)[WRES_HV]) {
+    auto body = [&](int s, HRT (&hl)[WRES_HV], const HRT (&hs)[WRES_HV]) {
         const int k = s >> 1, c = s & 1;
         // the epilogue's residual is loaded BEFORE the halo two steps ahead: vmcnt retires loads in issue
         // order, so waiting for it then does not wait for that halo too (the bias comes from LDS for the same
@@ -910,7 +925,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3_wres_f16_kernel(const ConvArgs
         if (s + 1 < steps) hstore(hs, (s + 1) & 1);
         __syncthreads();
     };
-    float4 hA[WRES_HV], hB[WRES_HV];
+    HRT hA[WRES_HV], hB[WRES_HV];
     if (steps > 0) {
         hload(hA, 0);
         hstore(hA, 0);
@@ -940,6 +955,16 @@ __global__ __launch_bounds__(512, 2) void conv3x3_wres_f16_kernel(const ConvArgs
 constexpr int WF_PK = 36;  // floats per staged row (32 + 4 pad)
 constexpr int WF_LDS_W = 2 * 9 * 32 * WF_PK;
 constexpr int WF_LDS_H = HALO_NPX * WF_PK;
+
+// Epilogue (BIAS kind: bias, residual, pre-activation store, ReLU / PReLU / ReLU-mask, accumulate): every operand
+// it reads (bias, residual, mask, old y) is requested at the START of the tile's second chunk through buffer
+// resources — an absent operand gets an empty resource, so its loads return 0 with no branch — and consumed only
+// after that chunk's 144 MFMAs. The generic epi_store4 issued each load behind its own branch and waited on it
+// (~8 serialised HBM round trips per tile; +14 % on a 3x3 with a residual).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t opnd_rsrc(const void* p, long long bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, p ? (int)std::min<long long>(bytes, 0x7FFFFFF0LL) : 0,
+                                             0x00020000);
+}
 
 __global__ __launch_bounds__(512, 2) void conv3x3_wres_f32_kernel(const ConvArgs a, int ntiles, int groups) {
     __shared__ __attribute__((aligned(16))) float lds[WF_LDS_W + WF_LDS_H];
@@ -1005,9 +1030,14 @@ __global__ __launch_bounds__(512, 2) void conv3x3_wres_f32_kernel(const ConvArgs
     floatx16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    const float slope = (a.e.act == HYRES_ACT_PRELU) ? a.e.slope[0] : 0.f;
-    const bool pre_res = a.e.kind == HYRES_EPI_BIAS && a.e.res != nullptr;
-    float4 rres[4];
+    const hyres_epilogue& e = a.e;
+    const float slope = (e.act == HYRES_ACT_PRELU) ? e.slope[0] : 0.f;
+    const long long npix = (long long)g.B * g.Ho * g.Wo;
+    const __amdgpu_buffer_rsrc_t r_bias = opnd_rsrc(e.bias, (long long)g.Co * 4);
+    const __amdgpu_buffer_rsrc_t r_res = opnd_rsrc(e.res, npix * e.ldres * 4);
+    const __amdgpu_buffer_rsrc_t r_mask = opnd_rsrc(e.act == HYRES_ACT_RELU_MASK ? e.aux0 : nullptr, npix * e.ld0 * 4);
+    const __amdgpu_buffer_rsrc_t r_old = opnd_rsrc(e.accumulate ? a.y : nullptr, npix * g.ldy * 4);
+    float4 ebias[4], eres[4], emask[4], eold[4];
     const int steps = mytiles * 2;
     if (steps > 0) {
         hload(0);
@@ -1020,10 +1050,20 @@ __global__ __launch_bounds__(512, 2) void conv3x3_wres_f32_kernel(const ConvArgs
         tile_of(k, b, i0, j0);
         const int i = i0 + orow;
         const long long pix = ((long long)b * g.Ho + i) * g.Wo + j0 + 32 * ph + lr;
-        if (c == 1 && pre_res) {  // the epilogue's residual, issued before the next halo (vmcnt order)
+        if (c == 1) {  // the epilogue's operands, issued before the next halo (vmcnt retires in issue order)
+            const bool okr = i < g.Ho;
 #pragma unroll
-            for (int qd = 0; qd < 4; ++qd)
-                rres[qd] = i < g.Ho ? ld4(a.e.res + pix * a.e.ldres + n0 + 8 * qd + 4 * lh) : make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int qd = 0; qd < 4; ++qd) {
+                const int n = n0 + 8 * qd + 4 * lh;
+                const int ob = n * 4;
+                const int orr = okr ? (int)((pix * e.ldres + n) * 4) : (int)0x80000000;
+                const int om = okr ? (int)((pix * e.ld0 + n) * 4) : (int)0x80000000;
+                const int oy = okr ? (int)((pix * g.ldy + n) * 4) : (int)0x80000000;
+                ebias[qd] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r_bias, ob, 0, 0));
+                eres[qd] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r_res, orr, 0, 0));
+                emask[qd] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r_mask, om, 0, 0));
+                eold[qd] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r_old, oy, 0, 0));
+            }
         }
         if (s + 1 < steps) hload(s + 1);
         const float* Wc = Ws + c * 9 * 32 * WF_PK;
@@ -1047,8 +1087,23 @@ __global__ __launch_bounds__(512, 2) void conv3x3_wres_f32_kernel(const ConvArgs
 #pragma unroll
                 for (int qd = 0; qd < 4; ++qd) {
                     const int n = n0 + 8 * qd + 4 * lh;
-                    const float4 v = make_float4(acc[4 * qd], acc[4 * qd + 1], acc[4 * qd + 2], acc[4 * qd + 3]);
-                    epi_store4<false>(a.e, a.y, g.ldy, pix, n, v, slope, pre_res ? &rres[qd] : nullptr);
+                    float o[4] = {acc[4 * qd] + ebias[qd].x + eres[qd].x, acc[4 * qd + 1] + ebias[qd].y + eres[qd].y,
+                                  acc[4 * qd + 2] + ebias[qd].z + eres[qd].z, acc[4 * qd + 3] + ebias[qd].w + eres[qd].w};
+                    if (e.out2) st4(e.out2 + pix * e.ldo2 + n, make_float4(o[0], o[1], o[2], o[3]));
+                    if (e.act == HYRES_ACT_RELU) {
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) o[k] = fmaxf(o[k], 0.f);
+                    } else if (e.act == HYRES_ACT_PRELU) {
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) o[k] = o[k] >= 0.f ? o[k] : slope * o[k];
+                    } else if (e.act == HYRES_ACT_RELU_MASK) {
+                        o[0] = emask[qd].x > 0.f ? o[0] : 0.f;
+                        o[1] = emask[qd].y > 0.f ? o[1] : 0.f;
+                        o[2] = emask[qd].z > 0.f ? o[2] : 0.f;
+                        o[3] = emask[qd].w > 0.f ? o[3] : 0.f;
+                    }
+                    st4(a.y + pix * g.ldy + n,
+                        make_float4(o[0] + eold[qd].x, o[1] + eold[qd].y, o[2] + eold[qd].z, o[3] + eold[qd].w));
                 }
             }
 #pragma unroll
@@ -1278,7 +1333,7 @@ __global__ __launch_bounds__(256) void conv_narrow_kernel(const ConvArgs a) {
         // then its FMAs serialised ~9 memory latencies per output pixel: 254 us -> see DESIGN §4)
         constexpr int TG = 9;
         for (int t0 = 0; t0 < ntap; t0 += TG) {
-            float4 xv[TG][S];
+            std::conditional_t<XH, half4_t, float4> xv[TG][S];  // fp16 X: converted at the FMAs
 #pragma unroll
             for (int u = 0; u < TG; ++u) {
                 const int t = t0 + u;
@@ -1289,9 +1344,8 @@ __global__ __launch_bounds__(256) void conv_narrow_kernel(const ConvArgs a) {
 #pragma unroll
                 for (int s2 = 0; s2 < S; ++s2) {
                     if constexpr (XH) {
-                        const half4_t h = __builtin_bit_cast(
+                        xv[u][s2] = __builtin_bit_cast(
                             half4_t, __builtin_amdgcn_raw_buffer_load_b64(xr, in ? off + 128 * s2 : off, 0, 0));
-                        xv[u][s2] = make_float4((float)h.x, (float)h.y, (float)h.z, (float)h.w);
                     } else {
                         xv[u][s2] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
                                                                   xr, in ? off + 256 * s2 : off, 0, 0));
@@ -1303,16 +1357,21 @@ __global__ __launch_bounds__(256) void conv_narrow_kernel(const ConvArgs a) {
                 const int t = t0 + u;
                 if (t >= ntap) break;
 #pragma unroll
-                for (int s2 = 0; s2 < S; ++s2)
+                for (int s2 = 0; s2 < S; ++s2) {
+                    float4 xf;
+                    if constexpr (XH) xf = make_float4((float)xv[u][s2].x, (float)xv[u][s2].y, (float)xv[u][s2].z,
+                                                       (float)xv[u][s2].w);
+                    else xf = xv[u][s2];
 #pragma unroll
                     for (int co = 0; co < CO; ++co) {
                         const float4 w =
                             *reinterpret_cast<const float4*>(&Ws[(t * CO + co) * CI + 64 * s2 + 4 * l16]);
-                        acc[co] = fmaf(xv[u][s2].x, w.x, acc[co]);
-                        acc[co] = fmaf(xv[u][s2].y, w.y, acc[co]);
-                        acc[co] = fmaf(xv[u][s2].z, w.z, acc[co]);
-                        acc[co] = fmaf(xv[u][s2].w, w.w, acc[co]);
+                        acc[co] = fmaf(xf.x, w.x, acc[co]);
+                        acc[co] = fmaf(xf.y, w.y, acc[co]);
+                        acc[co] = fmaf(xf.z, w.z, acc[co]);
+                        acc[co] = fmaf(xf.w, w.w, acc[co]);
                     }
+                }
             }
         }
 #pragma unroll
@@ -1773,9 +1832,13 @@ static int launch_wres16(const ConvArgs& a, hipStream_t st) {
 // block; HYRES_CONV_WRES32=0 turns it off
 static bool wres32_ok(const hyres_conv_geom* g, const hyres_epilogue* e) {
     static const int on = env_int("HYRES_CONV_WRES32", 1);
-    if (!on || e->f16_operands || (e->io_f16 & 3) || e->square_input || g->nphase != 1 || g->ntaps != 9 || g->Ci != 64 ||
-        g->Co % 32 != 0)
+    if (!on || e->f16_operands || e->io_f16 || e->square_input || e->kind != HYRES_EPI_BIAS || g->nphase != 1 ||
+        g->ntaps != 9 || g->Ci != 64 || g->Co % 32 != 0)
         return false;
+    // the epilogue operands are addressed with 32-bit byte offsets
+    const long long npix = (long long)g->B * g->Ho * g->Wo;
+    const int ld = std::max(g->ldy, std::max(e->res ? e->ldres : 0, e->aux0 ? e->ld0 : 0));
+    if (npix * ld * 4 >= 0x7FFFFFF0LL) return false;
     if (g->ish != 1 || g->isw != 1 || g->Hi != g->Ho || g->Wi != g->Wo || g->Hq != g->Ho || g->Wq != g->Wo ||
         g->Wo % HALO_TW != 0)
         return false;

@@ -617,6 +617,29 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo_kernel(const WgradArgs a, i
 // (one barrier per tap step).  Requires the vector path (M, N, ldp, ldq % 4 == 0) and no tap folding.
 // ------------------------------------------------------------------------------------------------
 constexpr int KTH = 64;
+
+// a staged operand quad: raw halves when the operand is fp16 in HBM (kept unconverted until the LDS store, so
+// the prefetch of the next chunk does not wait for its data), fp32 otherwise
+template <bool H>
+using quad_t = std::conditional_t<H, half4_t, float4>;
+template <bool H>
+__device__ __forceinline__ quad_t<H> ldq4(const float* p, long long i) {
+    if constexpr (H) return *reinterpret_cast<const half4_t*>(reinterpret_cast<const _Float16*>(p) + i);
+    else return ld4(p + i);
+}
+template <bool H>
+__device__ __forceinline__ quad_t<H> zq4() {
+    if constexpr (H) return half4_t{(_Float16)0.f, (_Float16)0.f, (_Float16)0.f, (_Float16)0.f};
+    else return make_float4(0.f, 0.f, 0.f, 0.f);
+}
+__device__ __forceinline__ float4 q2f(const float4& v) { return v; }
+__device__ __forceinline__ float4 q2f(const half4_t& v) {
+    return make_float4((float)v.x, (float)v.y, (float)v.z, (float)v.w);
+}
+__device__ __forceinline__ half4_t q2h(const half4_t& v) { return v; }
+__device__ __forceinline__ half4_t q2h(const float4& v) {
+    return half4_t{(_Float16)v.x, (_Float16)v.y, (_Float16)v.z, (_Float16)v.w};
+}
 typedef __fp16 fp16x4_t __attribute__((ext_vector_type(4)));
 typedef _Float16 halfx4_t __attribute__((ext_vector_type(4)));
 typedef _Float16 halfx8_t __attribute__((ext_vector_type(8)));
@@ -654,7 +677,8 @@ __global__ __launch_bounds__(256) void wgrad_f16_kernel(const WgradArgs a) {
 
     constexpr int P_V = KTH * BM / 4 / 256, Q_V = KTH * BN / 4 / 256;
     static_assert(P_V >= 1 && Q_V >= 1, "tile too small");
-    float4 rp[P_V], rq[Q_V];
+    quad_t<PH> rp[P_V];
+    quad_t<QH> rq[Q_V];
     // fixed per-thread channel quad (256 % (B/4) == 0): rows are tid/(B/4) + i*256/(B/4)
     const int pc = (tid % (BM / 4)) * 4, prow0 = tid / (BM / 4);
     const int qc = (tid % (BN / 4)) * 4, qrow0 = tid / (BN / 4);
@@ -693,9 +717,7 @@ __global__ __launch_bounds__(256) void wgrad_f16_kernel(const WgradArgs a) {
 #pragma unroll
         for (int i = 0; i < P_V; ++i) {
             const long long qq = k0 + prow0 + i * PRS;
-            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (qq < Qtot && m0 + pc < d.M) v = ldv4<PH>(a.p, qq * d.ldp + m0 + pc);
-            rp[i] = v;
+            rp[i] = (qq < Qtot && m0 + pc < d.M) ? ldq4<PH>(a.p, qq * d.ldp + m0 + pc) : zq4<PH>();
         }
     };
     int cur_kc = 0;  // ONE: the chunk load_q fetches (Q rows = P rows)
@@ -705,35 +727,42 @@ __global__ __launch_bounds__(256) void wgrad_f16_kernel(const WgradArgs a) {
 #pragma unroll
             for (int i = 0; i < Q_V; ++i) {
                 const long long qq = k0 + qrow0 + i * QRS;
-                rq[i] = (qq < Qtot && n0 + qc < d.N) ? ldv4<QH>(a.q, qq * d.ldq + n0 + qc) : make_float4(0.f, 0.f, 0.f, 0.f);
+                rq[i] = (qq < Qtot && n0 + qc < d.N) ? ldq4<QH>(a.q, qq * d.ldq + n0 + qc) : zq4<QH>();
             }
             return;
         }
 #pragma unroll
         for (int i = 0; i < Q_V; ++i) {
-            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            quad_t<QH> v = zq4<QH>();
             if (q_b[i] >= 0 && n0 + qc < d.N && t < d.ntaps) {
                 const int ih = q_i[i] * d.sq + d.dh[t], iw = q_j[i] * d.sq + d.dw[t];
                 if (ih >= 0 && ih < d.Hqq && iw >= 0 && iw < d.Wqq)
-                    v = ldv4<QH>(a.q, ((long long)(q_b[i] * d.Hqq + ih) * d.Wqq + iw) * d.ldq + n0 + qc);
+                    v = ldq4<QH>(a.q, ((long long)(q_b[i] * d.Hqq + ih) * d.Wqq + iw) * d.ldq + n0 + qc);
             }
-            if constexpr (SQ) { v.x *= v.x; v.y *= v.y; v.z *= v.z; v.w *= v.w; }
-            rq[i] = v;
+            rq[i] = v;  // SQ: squared at the LDS store
         }
     };
     auto store_p = [&](_Float16* Ps) {
 #pragma unroll
         for (int i = 0; i < P_V; ++i) {
-            if (do_bias) { bsum.x += rp[i].x; bsum.y += rp[i].y; bsum.z += rp[i].z; bsum.w += rp[i].w; }
-            const halfx4_t h = {(_Float16)rp[i].x, (_Float16)rp[i].y, (_Float16)rp[i].z, (_Float16)rp[i].w};
-            *reinterpret_cast<halfx4_t*>(&Ps[(prow0 + i * PRS) * PP + pc]) = h;
+            if (do_bias) {
+                const float4 f = q2f(rp[i]);
+                bsum.x += f.x; bsum.y += f.y; bsum.z += f.z; bsum.w += f.w;
+            }
+            *reinterpret_cast<half4_t*>(&Ps[(prow0 + i * PRS) * PP + pc]) = q2h(rp[i]);
         }
     };
     auto store_q = [&](_Float16* Qs) {
 #pragma unroll
         for (int i = 0; i < Q_V; ++i) {
-            const halfx4_t h = {(_Float16)rq[i].x, (_Float16)rq[i].y, (_Float16)rq[i].z, (_Float16)rq[i].w};
-            *reinterpret_cast<halfx4_t*>(&Qs[(qrow0 + i * QRS) * PQ + qc]) = h;
+            half4_t h;
+            if constexpr (SQ) {
+                const float4 f = q2f(rq[i]);
+                h = q2h(make_float4(f.x * f.x, f.y * f.y, f.z * f.z, f.w * f.w));
+            } else {
+                h = q2h(rq[i]);
+            }
+            *reinterpret_cast<half4_t*>(&Qs[(qrow0 + i * QRS) * PQ + qc]) = h;
         }
     };
 
@@ -886,7 +915,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo_f16_kernel(const WgradArgs 
     const int cpr = d.Wq / 32;
     // this thread's fixed channel quad of P (256 % (BM/4) == 0): rows tid/16 + 16*q
     const int pc = (tid % (BM / 4)) * 4, prow0 = tid / (BM / 4);
-    float4 rp[P_V], rh[H_V];
+    quad_t<PH> rp[P_V];
+    quad_t<QH> rh[H_V];
     auto load = [&](int kc) {
         const int b = kc / (d.Hq * cpr);
         const int rem = kc - b * d.Hq * cpr;
@@ -895,7 +925,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo_f16_kernel(const WgradArgs 
         const long long q0 = (long long)kc * 32;
 #pragma unroll
         for (int q = 0; q < P_V; ++q)
-            rp[q] = m0 + pc < d.M ? ldv4<PH>(a.p, (q0 + prow0 + 16 * q) * d.ldp + m0 + pc) : make_float4(0.f, 0.f, 0.f, 0.f);
+            rp[q] = m0 + pc < d.M ? ldq4<PH>(a.p, (q0 + prow0 + 16 * q) * d.ldp + m0 + pc) : zq4<PH>();
 #pragma unroll
         for (int q = 0; q < H_V; ++q) {
             const int e = tid + 256 * q;
@@ -903,8 +933,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo_f16_kernel(const WgradArgs 
             const int hr = pix / HC, hc = pix - (pix / HC) * HC;
             const int ih = i * SQ + dh0 + DIL * hr, iw = j0 * SQ + dwg + hc;
             const bool ok = e < H_E && (unsigned)ih < (unsigned)d.Hqq && (unsigned)iw < (unsigned)d.Wqq && n0 + c < d.N;
-            rh[q] = ok ? ldv4<QH>(a.q, ((long long)(b * d.Hqq + ih) * d.Wqq + iw) * d.ldq + n0 + c)
-                       : make_float4(0.f, 0.f, 0.f, 0.f);
+            rh[q] = ok ? ldq4<QH>(a.q, ((long long)(b * d.Hqq + ih) * d.Wqq + iw) * d.ldq + n0 + c) : zq4<QH>();
         }
     };
     const bool do_bias = a.bias_slab != nullptr && nt == 0 && grp == 0;
@@ -914,17 +943,16 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo_f16_kernel(const WgradArgs 
         _Float16* Hs = Ps + PSZ;
 #pragma unroll
         for (int q = 0; q < P_V; ++q) {
-            if (do_bias) { bsum.x += rp[q].x; bsum.y += rp[q].y; bsum.z += rp[q].z; bsum.w += rp[q].w; }
-            const halfx4_t h = {(_Float16)rp[q].x, (_Float16)rp[q].y, (_Float16)rp[q].z, (_Float16)rp[q].w};
-            *reinterpret_cast<halfx4_t*>(&Ps[(prow0 + 16 * q) * PP + pc]) = h;
+            if (do_bias) {
+                const float4 f = q2f(rp[q]);
+                bsum.x += f.x; bsum.y += f.y; bsum.z += f.z; bsum.w += f.w;
+            }
+            *reinterpret_cast<half4_t*>(&Ps[(prow0 + 16 * q) * PP + pc]) = q2h(rp[q]);
         }
 #pragma unroll
         for (int q = 0; q < H_V; ++q) {
             const int e = tid + 256 * q;
-            if (e < H_E) {
-                const halfx4_t h = {(_Float16)rh[q].x, (_Float16)rh[q].y, (_Float16)rh[q].z, (_Float16)rh[q].w};
-                *reinterpret_cast<halfx4_t*>(&Hs[(e / (BN / 4)) * PQ + (e % (BN / 4)) * 4]) = h;
-            }
+            if (e < H_E) *reinterpret_cast<half4_t*>(&Hs[(e / (BN / 4)) * PQ + (e % (BN / 4)) * 4]) = q2h(rh[q]);
         }
     };
 
@@ -1055,7 +1083,7 @@ __global__ __launch_bounds__(256) void wgrad_thin_kernel(const WgradArgs a, int 
 #pragma unroll
         for (int u = 0; u < TG; ++u) acc[w][u] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    float4 pr4[PV];
+    quad_t<PH> pr4[PV];  // fp16 P: raw halves, converted at the LDS store
     for (int r = r0; r < r1; ++r) {
         const int b = r / d.Hq, i = r - (r / d.Hq) * d.Hq;
         const long long prow = (long long)r * d.Wq * d.ldp;  // element offset of this row's first pixel
@@ -1064,8 +1092,7 @@ __global__ __launch_bounds__(256) void wgrad_thin_kernel(const WgradArgs a, int 
             for (int k = 0; k < PV; ++k) {
                 const int idx = tid + 256 * k;
                 const int px = idx / (16 * MW), c4 = idx - (idx / (16 * MW)) * (16 * MW);
-                pr4[k] = c0 + px < d.Wq ? ldv4<PH>(a.p, prow + (long long)(c0 + px) * d.ldp + 4 * c4)
-                                        : make_float4(0.f, 0.f, 0.f, 0.f);
+                pr4[k] = c0 + px < d.Wq ? ldq4<PH>(a.p, prow + (long long)(c0 + px) * d.ldp + 4 * c4) : zq4<PH>();
             }
         };
         load_chunk(0);
@@ -1096,7 +1123,7 @@ __global__ __launch_bounds__(256) void wgrad_thin_kernel(const WgradArgs a, int 
         for (int c0 = 0; c0 < d.Wq; c0 += PCH) {
             if (c0) __syncthreads();  // the previous chunk's readers of Ps are done
 #pragma unroll
-            for (int k = 0; k < PV; ++k) *reinterpret_cast<float4*>(&Ps[4 * (tid + 256 * k)]) = pr4[k];
+            for (int k = 0; k < PV; ++k) *reinterpret_cast<float4*>(&Ps[4 * (tid + 256 * k)]) = q2f(pr4[k]);
             __syncthreads();
             if (c0 + PCH < d.Wq) load_chunk(c0 + PCH);  // next chunk in flight during this chunk's FMAs
 #pragma unroll 2
@@ -1371,7 +1398,10 @@ static WgradPlan wgrad_plan(const hyres_wgrad_desc* d) {
         p.TMc = p.TNc = 1; p.WMc = p.WNc = 2;
         p.BM = p.BN = 64;
         p.mtiles = ceil_div(d->M, 64); p.ntiles = ceil_div(d->N, 64);
-        p.NT = p.hk == 3 ? 9 : 5;
+        // 3x3: all 9 taps per block (one 3-row halo per chunk), or HYRES_WGRAD_HALO_ROWS=1: one kernel row of 3
+        // taps per block — 3x the tiles, so a third of the pixel splits and of the split slab for the same grid
+        static const int halo_rows = env_int("HYRES_WGRAD_HALO_ROWS", 3);
+        p.NT = p.hk == 3 ? (halo_rows == 1 ? 3 : 9) : 5;
         p.ngroups = d->ntaps / p.NT;
     }
     const long long tiles = (long long)p.mtiles * p.ntiles * p.ngroups;
@@ -1635,7 +1665,11 @@ int hyres_conv_wgrad(const hyres_wgrad_desc* d0, const float* pp, const float* q
     } else if (p.halo && wgrad_f16_ok(d)) {
         auto halo16 = [&](auto ioc) {
             constexpr int IO_ = decltype(ioc)::value;
-            if (p.hk == 3 && p.hdil == 2)
+            if (p.hk == 3 && p.NT == 3 && p.hdil == 2)
+                hipLaunchKernelGGL((wgrad_halo_f16_kernel<1, 3, 1, 2, IO_>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
+            else if (p.hk == 3 && p.NT == 3)
+                hipLaunchKernelGGL((wgrad_halo_f16_kernel<1, 3, 1, 1, IO_>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
+            else if (p.hk == 3 && p.hdil == 2)
                 hipLaunchKernelGGL((wgrad_halo_f16_kernel<3, 3, 1, 2, IO_>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
             else if (p.hk == 3)
                 hipLaunchKernelGGL((wgrad_halo_f16_kernel<3, 3, 1, 1, IO_>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
@@ -1647,7 +1681,11 @@ int hyres_conv_wgrad(const hyres_wgrad_desc* d0, const float* pp, const float* q
         else if (io == 2) halo16(std::integral_constant<int, 2>{});
         else halo16(std::integral_constant<int, 0>{});
     } else if (p.halo) {
-        if (p.hk == 3 && p.hdil == 2)
+        if (p.hk == 3 && p.NT == 3 && p.hdil == 2)
+            hipLaunchKernelGGL((wgrad_halo_kernel<1, 3, 1, 2>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
+        else if (p.hk == 3 && p.NT == 3)
+            hipLaunchKernelGGL((wgrad_halo_kernel<1, 3, 1, 1>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
+        else if (p.hk == 3 && p.hdil == 2)
             hipLaunchKernelGGL((wgrad_halo_kernel<3, 3, 1, 2>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
         else if (p.hk == 3) hipLaunchKernelGGL((wgrad_halo_kernel<3, 3, 1>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
         else if (d->sq == 1) hipLaunchKernelGGL((wgrad_halo_kernel<1, 5, 1>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);

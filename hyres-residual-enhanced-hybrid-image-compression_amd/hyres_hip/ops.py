@@ -587,7 +587,8 @@ def _launch_conv(g: L.ConvGeom, x_ptr: int, w2: torch.Tensor, ldw: int, y_ptr: i
         KernelTimer.events.append((s0, s1, conv_flops(g), conv_bytes(g, e), conv_variant(g, e, conv_split(g, e) > 1)))
         if KernelTimer.all_convs:
             desc = (f"B{g.B} {g.Hi}x{g.Wi}x{g.Ci}->{g.Ho}x{g.Wo}x{g.Co} taps{g.ntaps} ph{g.nphase} "
-                    f"s{g.ish} epi{e.kind}{'+acc' if e.accumulate else ''}{'+res' if e.res else ''}")
+                    f"s{g.ish} epi{e.kind}{'+acc' if e.accumulate else ''}{'+res' if e.res else ''}"
+                    f"{' io%d' % e.io_f16 if e.io_f16 else ''}")
             KernelTimer.table.append((desc, s0, s1, conv_flops(g), conv_bytes(g, e)))
 
 

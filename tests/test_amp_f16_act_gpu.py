@@ -39,9 +39,10 @@ def _h(t):
 # ------------------------------------------------------------------------------------------ elementwise
 def test_f16_saved_activation_backward_entry_points_bitwise():
     """relu / PReLU / attention gate / GDN dnorm / SE / spatial-attention backward with fp16 saved operands
-    equal the fp32 entry points on the same (fp16-representable) values, bit for bit (the PReLU slope gradient,
-a block reduction, within 1e-6: measured 1 ulp, the two instantiations contract their multiply-adds
-differently)."""
+    equal the fp32 entry points on the same (fp16-representable) values, bit for bit — except where a sum of
+products feeds the result (the PReLU slope gradient, the spatial-attention logit sums): there the two
+instantiations contract their multiply-adds differently (v_fma_mix on the fp16 operand), measured 1 ulp,
+checked to 1e-6."""
     from hyres_hip import _lib as L
     from hyres_hip import ops as O
     D = dev()
@@ -123,7 +124,7 @@ differently)."""
                                     attn.data_ptr(), g.data_ptr(), gx.data_ptr(), gw.data_ptr(), B, H, W, C,
                                     ws.data_ptr(), ws.numel(), s),
          (y.data_ptr(), wsa.data_ptr(), pooled2.data_ptr(), amax.data_ptr(), attn.data_ptr(), g.data_ptr(),
-          gx.data_ptr(), gw.data_ptr(), B, H, W, C, ws.data_ptr(), ws.numel(), s), [gx, gw])
+          gx.data_ptr(), gw.data_ptr(), B, H, W, C, ws.data_ptr(), ws.numel(), s), [gx, gw], tol=[1e-6, 1e-6])
 
 
 # ------------------------------------------------------------------------------------------ conv layers
