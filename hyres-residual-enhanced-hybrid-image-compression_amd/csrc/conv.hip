@@ -34,7 +34,22 @@ struct ConvArgs {
     int xcd;     // 1: grid.x = M tiles x N tiles in XCD-aware order (grid.y = 1)
     int prio;    // 1: raise the wave priority while it issues its MFMA cluster (s_setprio)
     int x_bytes; // conv1x1_stream_kernel: bytes of X (buffer-resource range)
+    int rsrc_ok; // every epilogue operand / output spans < 2 GB: the epilogues may address them by buffer resources
 };
+
+// Buffer resource of an epilogue operand: an absent operand (p == NULL) gets an empty resource, so its loads return
+// 0 without a branch (a load behind a branch is waited on at the join: the epilogue's loads would serialise)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t opnd_rsrc(const void* p, long long bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, p ? (int)std::min<long long>(bytes, 0x7FFFFFF0LL) : 0,
+                                             0x00020000);
+}
+__device__ __forceinline__ float4 bload4(__amdgpu_buffer_rsrc_t r, int off) {
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+__device__ __forceinline__ half4_t bload4h(__amdgpu_buffer_rsrc_t r, int off) {
+    return __builtin_bit_cast(half4_t, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+}
+__device__ __forceinline__ float4 h2f4(half4_t h) { return make_float4((float)h.x, (float)h.y, (float)h.z, (float)h.w); }
 
 
 struct EpiChannel {
@@ -462,15 +477,29 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
                 Cs[(wm * TM * 32 + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh) * CP + wn * 32 + lr] = acc[tm][tn][r];
         __syncthreads();
         if constexpr (!split_k) {
-            // fast path (BIAS epilogue, float4 operands): the residual / old-y / ReLU-mask loads of U
-            // iterations are issued before any of them is consumed, so U loads per thread are in flight
-            if (a.vec4 && a.e.kind == HYRES_EPI_BIAS) {
+            // fast path (BIAS epilogue, float4 operands): the bias / residual / old-y / ReLU-mask loads of U
+            // iterations are issued before any of them is consumed. Per-lane validity goes into the buffer offset
+            // (out of range -> 0, no divergent branch: a load behind one is waited on where the branches join);
+            // an absent operand is skipped by a uniform branch around all U of its loads
+            if (a.vec4 && a.rsrc_ok && a.e.kind == HYRES_EPI_BIAS) {
                 constexpr int ITER = BM * (CW / 4) / 256;
                 constexpr int U = ITER >= 4 ? 4 : ITER;
                 static_assert(ITER % U == 0, "epilogue tiling");
                 const hyres_epilogue& e = a.e;
+                constexpr int ES = YH ? 2 : 4;  // residual / fp16-storage element bytes
+                const long long npo = (long long)g.B * g.Ho * g.Wo;
+                const bool mask = e.act == HYRES_ACT_RELU_MASK;
+                const bool m16 = YH || (e.io_f16 & HYRES_IO_AUX16);
+                const __amdgpu_buffer_rsrc_t r_bias = opnd_rsrc(e.bias, (long long)g.Co * 4);
+                const __amdgpu_buffer_rsrc_t r_res = opnd_rsrc(e.res, npo * e.ldres * ES);
+                const __amdgpu_buffer_rsrc_t r_m32 = opnd_rsrc(mask && !m16 ? e.aux0 : nullptr, npo * e.ld0 * 4);
+                const __amdgpu_buffer_rsrc_t r_m16 = opnd_rsrc(mask && m16 ? e.aux0 : nullptr, npo * e.ld0 * 2);
+                const __amdgpu_buffer_rsrc_t r_old = opnd_rsrc(!YH && e.accumulate ? a.y : nullptr, npo * g.ldy * 4);
+                constexpr int OOR = (int)0x80000000;
                 for (int it0 = 0; it0 < ITER; it0 += U) {
-                    float4 v[U], rs[U], yo[U], mk[U], bs[U];
+                    float4 v[U], yo[U], mk[U], bs[U];
+                    std::conditional_t<YH, half4_t, float4> rs[U];
+                    half4_t mh[U];
                     long long px[U];
                     int nn[U];
                     bool ok[U];
@@ -493,17 +522,47 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
                             pix = (long long)(b * g.Ho + i * g.osh + oph) * g.Wo + j * g.osw + opw;
                         }
                         px[u] = pix;
-                        const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-                        bs[u] = (ok[u] && e.bias) ? ld4(e.bias + n) : z4;
-                        rs[u] = (ok[u] && e.res) ? ldv4<YH>(e.res, pix * e.ldres + n) : z4;
-                        yo[u] = (!YH && ok[u] && e.accumulate) ? ld4(a.y + pix * g.ldy + n) : z4;
-                        mk[u] = (ok[u] && e.act == HYRES_ACT_RELU_MASK) ? ld_aux4<YH>(e, e.aux0, pix * e.ld0 + n) : z4;
+                    }
+                    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+                    for (int u = 0; u < U; ++u) { bs[u] = z4; yo[u] = z4; mk[u] = z4; }
+                    if (e.bias) {
+#pragma unroll
+                        for (int u = 0; u < U; ++u) bs[u] = bload4(r_bias, ok[u] ? nn[u] * 4 : OOR);
+                    }
+                    if (e.res) {
+#pragma unroll
+                        for (int u = 0; u < U; ++u) {
+                            const int orr = ok[u] ? (int)((px[u] * e.ldres + nn[u]) * ES) : OOR;
+                            if constexpr (YH) rs[u] = bload4h(r_res, orr);
+                            else rs[u] = bload4(r_res, orr);
+                        }
+                    } else {
+#pragma unroll
+                        for (int u = 0; u < U; ++u) {
+                            if constexpr (YH) rs[u] = half4_t{(_Float16)0.f, (_Float16)0.f, (_Float16)0.f, (_Float16)0.f};
+                            else rs[u] = z4;
+                        }
+                    }
+                    if (!YH && e.accumulate) {
+#pragma unroll
+                        for (int u = 0; u < U; ++u) yo[u] = bload4(r_old, ok[u] ? (int)((px[u] * g.ldy + nn[u]) * 4) : OOR);
+                    }
+                    if (mask && m16) {
+#pragma unroll
+                        for (int u = 0; u < U; ++u) mh[u] = bload4h(r_m16, ok[u] ? (int)((px[u] * e.ld0 + nn[u]) * 2) : OOR);
+                    } else if (mask) {
+#pragma unroll
+                        for (int u = 0; u < U; ++u) mk[u] = bload4(r_m32, ok[u] ? (int)((px[u] * e.ld0 + nn[u]) * 4) : OOR);
                     }
 #pragma unroll
                     for (int u = 0; u < U; ++u) {
                         if (!ok[u]) continue;
-                        float o[4] = {v[u].x + bs[u].x + rs[u].x, v[u].y + bs[u].y + rs[u].y,
-                                      v[u].z + bs[u].z + rs[u].z, v[u].w + bs[u].w + rs[u].w};
+                        float4 r4;
+                        if constexpr (YH) r4 = h2f4(rs[u]);
+                        else r4 = rs[u];
+                        float o[4] = {v[u].x + bs[u].x + r4.x, v[u].y + bs[u].y + r4.y,
+                                      v[u].z + bs[u].z + r4.z, v[u].w + bs[u].w + r4.w};
                         if (e.out2) stv4<YH>(e.out2, px[u] * e.ldo2 + nn[u], make_float4(o[0], o[1], o[2], o[3]));
                         if (e.act == HYRES_ACT_RELU) {
 #pragma unroll
@@ -511,11 +570,12 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
                         } else if (e.act == HYRES_ACT_PRELU) {
 #pragma unroll
                             for (int c = 0; c < 4; ++c) o[c] = o[c] >= 0.f ? o[c] : slope * o[c];
-                        } else if (e.act == HYRES_ACT_RELU_MASK) {
-                            o[0] = mk[u].x > 0.f ? o[0] : 0.f;
-                            o[1] = mk[u].y > 0.f ? o[1] : 0.f;
-                            o[2] = mk[u].z > 0.f ? o[2] : 0.f;
-                            o[3] = mk[u].w > 0.f ? o[3] : 0.f;
+                        } else if (mask) {
+                            const float4 q = m16 ? h2f4(mh[u]) : mk[u];
+                            o[0] = q.x > 0.f ? o[0] : 0.f;
+                            o[1] = q.y > 0.f ? o[1] : 0.f;
+                            o[2] = q.z > 0.f ? o[2] : 0.f;
+                            o[3] = q.w > 0.f ? o[3] : 0.f;
                         }
                         stv4<YH>(a.y, px[u] * g.ldy + nn[u],
                                  make_float4(o[0] + yo[u].x, o[1] + yo[u].y, o[2] + yo[u].z, o[3] + yo[u].w));
@@ -961,11 +1021,6 @@ constexpr int WF_LDS_H = HALO_NPX * WF_PK;
 // resources — an absent operand gets an empty resource, so its loads return 0 with no branch — and consumed only
 // after that chunk's 144 MFMAs. The generic epi_store4 issued each load behind its own branch and waited on it
 // (~8 serialised HBM round trips per tile; +14 % on a 3x3 with a residual).
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t opnd_rsrc(const void* p, long long bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, p ? (int)std::min<long long>(bytes, 0x7FFFFFF0LL) : 0,
-                                             0x00020000);
-}
-
 __global__ __launch_bounds__(512, 2) void conv3x3_wres_f32_kernel(const ConvArgs a, int ntiles, int groups) {
     __shared__ __attribute__((aligned(16))) float lds[WF_LDS_W + WF_LDS_H];
     __shared__ int2 tapoff[9];
@@ -2014,6 +2069,11 @@ int hyres_conv_forward(const hyres_conv_geom* g, const float* x, const float* w2
         auto al = [](const void* p, int ld) { return p == nullptr || (aligned16(p) && ld % 4 == 0); };
         a.vec4 = g->Co % 4 == 0 && al(y, g->ldy) && al(e->bias, 4) && al(e->res, e->ldres) && al(e->out2, e->ldo2) &&
                  al(e->aux0, e->ld0) && al(e->aux1, e->ld1) && al(e->aux2, e->ld2);
+    }
+    {
+        const long long npo = (long long)g->B * g->Ho * g->Wo;
+        const int ld = std::max(g->ldy, std::max(e->res ? e->ldres : 0, e->aux0 ? e->ld0 : 0));
+        a.rsrc_ok = npo * ld * 4 < 0x7FFFFFF0LL;
     }
     const long long need = plan_ws_bytes(g, plan);
     if (!ch.narrow && plan.nsplit > 1 && ws && ws_bytes >= need) {  // without workspace: single pass (correct, slower)
