@@ -1021,7 +1021,7 @@ constexpr int WF_LDS_H = HALO_NPX * WF_PK;
 // resources — an absent operand gets an empty resource, so its loads return 0 with no branch — and consumed only
 // after that chunk's 144 MFMAs. The generic epi_store4 issued each load behind its own branch and waited on it
 // (~8 serialised HBM round trips per tile; +14 % on a 3x3 with a residual).
-__global__ __launch_bounds__(512, 2) void conv3x3_wres_f32_kernel(const ConvArgs a, int ntiles, int groups) {
+__global__ __launch_bounds__(512, 2) void conv3x3_wres_f32_kernel(const ConvArgs a, int ntiles, int groups, int ablate) {
     __shared__ __attribute__((aligned(16))) float lds[WF_LDS_W + WF_LDS_H];
     __shared__ int2 tapoff[9];
     float* const Ws = lds;
@@ -1120,7 +1120,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3_wres_f32_kernel(const ConvArgs
                 eold[qd] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r_old, oy, 0, 0));
             }
         }
-        if (s + 1 < steps) hload(s + 1);
+        if (s + 1 < steps && !(ablate & 4)) hload(s + 1);
         const float* Wc = Ws + c * 9 * 32 * WF_PK;
 #pragma unroll
         for (int t = 0; t < 9; ++t) {
@@ -1138,7 +1138,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3_wres_f32_kernel(const ConvArgs
             }
         }
         if (c == 1) {
-            if (i < g.Ho) {
+            if (i < g.Ho && !(ablate & 1)) {
 #pragma unroll
                 for (int qd = 0; qd < 4; ++qd) {
                     const int n = n0 + 8 * qd + 4 * lh;
@@ -1164,9 +1164,16 @@ __global__ __launch_bounds__(512, 2) void conv3x3_wres_f32_kernel(const ConvArgs
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[r] = 0.f;
         }
+        if (ablate & 2) continue;
         __syncthreads();  // every wave is done with this chunk's halo
         if (s + 1 < steps) hstore();
         __syncthreads();
+    }
+    if (ablate & 1) {  // keep the accumulators live
+        float t = 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) t += acc[r];
+        if (t == 1.2345f) a.y[0] = t;
     }
 }
 
@@ -1909,7 +1916,10 @@ static int launch_wres32(const ConvArgs& a, hipStream_t st) {
     const int ntiles = g.B * ((g.Ho + HALO_R - 1) / HALO_R) * (g.Wo / HALO_TW);
     const int groups = g.Co / 32;
     const int per = wres_blocks(ntiles, groups);
-    hipLaunchKernelGGL(conv3x3_wres_f32_kernel, dim3(per * groups), dim3(512), 0, st, a, ntiles, groups);
+    // HYRES_WRES32_ABLATE (timing experiments only, wrong results): 1 no epilogue, 2 no halo store / barriers,
+    // 4 no halo loads
+    static const int ablate = env_int("HYRES_WRES32_ABLATE", 0);
+    hipLaunchKernelGGL(conv3x3_wres_f32_kernel, dim3(per * groups), dim3(512), 0, st, a, ntiles, groups, ablate);
     return HY_LAUNCH_CHECK("conv3x3_wres_f32_kernel");
 }
 

@@ -346,16 +346,22 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgradArgs a) {
 // rows (no tap shift / pixel decode); double-buffered [pixel][channel] LDS tiles, one barrier per chunk;
 // the bias gradient (column sums of P) rides on the A operand already in registers (one VALU add per
 // MFMA step in the wn == 0 waves) instead of a serial LDS pass per chunk.
-template <int TM, int TN, int WAVES_M, int WAVES_N>
-__global__ __launch_bounds__(256) void wgrad1x1_kernel(const WgradArgs a) {
+// G > 1: G groups of 4 waves per block, each over its own contiguous share of the block's pixel range with its
+// own LDS tiles, their tiles summed through LDS before the one slab write: the same grid of waves writes 1/G of
+// the split slabs (and the reduce reads 1/G), at 2 x (for G = 2) the LDS per block.
+template <int TM, int TN, int WAVES_M, int WAVES_N, int G = 1>
+__global__ __launch_bounds__(256 * G) void wgrad1x1_kernel(const WgradArgs a) {
     constexpr int BM = 32 * TM * WAVES_M, BN = 32 * TN * WAVES_N;
     constexpr int PP = BM + 4, PQ = BN + 4;
     constexpr int P_V = KT * BM / 4 / 256, Q_V = KT * BN / 4 / 256;
     static_assert(P_V >= 1 && Q_V >= 1, "tile too small");
-    __shared__ __attribute__((aligned(16))) float Psm[2 * KT * PP];
-    __shared__ __attribute__((aligned(16))) float Qsm[2 * KT * PQ];
+    static_assert(G == 1 || G * 2 * KT * PP >= BM * BN + BM, "LDS for the group combine");
+    __shared__ __attribute__((aligned(16))) float Psm_all[G * 2 * KT * PP];
+    __shared__ __attribute__((aligned(16))) float Qsm_all[G * 2 * KT * PQ];
     const hyres_wgrad_desc& d = a.d;
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x & 255, grp = threadIdx.x >> 8;
+    float* const Psm = Psm_all + grp * (2 * KT * PP);
+    float* const Qsm = Qsm_all + grp * (2 * KT * PQ);
     const int bid = blockIdx.x;
     const int lb = (bid & 7) * (gridDim.x >> 3) + (bid >> 3);  // XCD-aware order, as wgrad_kernel
     if (lb >= a.nblocks) return;
@@ -411,40 +417,86 @@ __global__ __launch_bounds__(256) void wgrad1x1_kernel(const WgradArgs a) {
     float bsum[TM];
 #pragma unroll
     for (int i = 0; i < TM; ++i) bsum[i] = 0.f;
-    const int kb = split * a.chunks_per_split;
-    const int ke = min(a.nchunks, kb + a.chunks_per_split);
+    // the block's chunks [kb0, ke0), this group's contiguous share [kb, ke); every group runs `iters` barrier
+    // steps (a group with fewer chunks idles through its last one)
+    const int kb0 = split * a.chunks_per_split;
+    const int ke0 = min(a.nchunks, kb0 + a.chunks_per_split);
+    const int share = (max(ke0 - kb0, 0) + G - 1) / G;
+    const int kb = min(ke0, kb0 + grp * share), ke = min(ke0, kb + share);
+    const int iters = share;
     if (kb < ke) {
         load(kb);
         store(0);
     }
     __syncthreads();
     int cur = 0;
-    for (int kc = kb; kc < ke; ++kc) {
+    for (int it = 0; it < iters; ++it) {
+        const int kc = kb + it;
+        const bool live = kc < ke;
         const bool next = kc + 1 < ke;
         if (next) load(kc + 1);  // in flight during this chunk's MFMAs
-        const float* Ps = Psm + cur * (KT * PP);
-        const float* Qs = Qsm + cur * (KT * PQ);
+        if (live) {
+            const float* Ps = Psm + cur * (KT * PP);
+            const float* Qs = Qsm + cur * (KT * PQ);
 #pragma unroll
-        for (int s2 = 0; s2 < KT / 2; ++s2) {
-            const int k = 2 * s2 + lh;
-            float av[TM], bv[TN];
+            for (int s2 = 0; s2 < KT / 2; ++s2) {
+                const int k = 2 * s2 + lh;
+                float av[TM], bv[TN];
 #pragma unroll
-            for (int tm = 0; tm < TM; ++tm) av[tm] = Ps[k * PP + wm * TM * 32 + tm * 32 + lr];
+                for (int tm = 0; tm < TM; ++tm) av[tm] = Ps[k * PP + wm * TM * 32 + tm * 32 + lr];
 #pragma unroll
-            for (int tn = 0; tn < TN; ++tn) bv[tn] = Qs[k * PQ + wn * TN * 32 + tn * 32 + lr];
-            if (do_bias) {
+                for (int tn = 0; tn < TN; ++tn) bv[tn] = Qs[k * PQ + wn * TN * 32 + tn * 32 + lr];
+                if (do_bias) {
 #pragma unroll
-                for (int tm = 0; tm < TM; ++tm) bsum[tm] += av[tm];
+                    for (int tm = 0; tm < TM; ++tm) bsum[tm] += av[tm];
+                }
+#pragma unroll
+                for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                    for (int tn = 0; tn < TN; ++tn)
+                        acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[tm], bv[tn], acc[tm][tn], 0, 0, 0);
             }
-#pragma unroll
-            for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-                for (int tn = 0; tn < TN; ++tn)
-                    acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[tm], bv[tn], acc[tm][tn], 0, 0, 0);
         }
         if (next) store(cur ^ 1);
         __syncthreads();
         cur ^= 1;
+    }
+    if constexpr (G > 1) {
+        // groups 1.. hand their tiles (accumulator layout, lane-major) and bias sums to group 0 through LDS;
+        // group 0 adds them in group order (deterministic) before the slab write
+        float* red = Psm_all;  // the loop ended with a barrier; the combine area spans groups 1.. of the LDS
+        constexpr int TILE = BM * BN;
+        for (int g2 = 1; g2 < G; ++g2) {
+            if (grp == g2) {
+#pragma unroll
+                for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                    for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+                        for (int r = 0; r < 16; ++r)
+                            red[(((wave * TM + tm) * TN + tn) * 16 + r) * 64 + lane] = acc[tm][tn][r];
+                if (do_bias) {
+#pragma unroll
+                    for (int tm = 0; tm < TM; ++tm) red[TILE + (wave * TM + tm) * 64 + lane] = bsum[tm];
+                }
+            }
+            __syncthreads();
+            if (grp == 0) {
+#pragma unroll
+                for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                    for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+                        for (int r = 0; r < 16; ++r)
+                            acc[tm][tn][r] += red[(((wave * TM + tm) * TN + tn) * 16 + r) * 64 + lane];
+                if (do_bias) {
+#pragma unroll
+                    for (int tm = 0; tm < TM; ++tm) bsum[tm] += red[TILE + (wave * TM + tm) * 64 + lane];
+                }
+            }
+            __syncthreads();
+        }
+        if (grp != 0) return;
     }
     if (do_bias) {
 #pragma unroll
@@ -1338,6 +1390,7 @@ namespace hyres {
 struct WgradPlan {
     int TMc, TNc, WMc, WNc, NT, BM, BN, mtiles, ntiles, ngroups, nchunks, nsplit, cps, tapn, nblocks;
     int halo, hk, hdh, hdw, hdil;  // wgrad_halo_kernel: K, first tap's (dh, dw), tap spacing
+    int g1x1;                      // wgrad1x1_kernel: 4-wave groups per block
 };
 
 // wgrad_halo_kernel applies: fp32, dense KxK taps (K = 3 or 5, dilation 1; K = 3 with dilation 2), Q stride
@@ -1431,6 +1484,16 @@ static WgradPlan wgrad_plan(const hyres_wgrad_desc* d) {
         if (tiles * p.nsplit > cap) p.nsplit = (int)std::max<long long>(1, (tiles * p.nsplit / cap) * cap / tiles);
         // and fill a partial single round when that grows the slab by <= 25 % (128^2 3x3: 455 -> 512)
         else if (cap / tiles <= maxsplit && 4 * (cap / tiles) <= 5LL * p.nsplit) p.nsplit = (int)(cap / tiles);
+    }
+    // 1x1 stride-1 fp32 gradients (wgrad1x1_kernel) outside the small grids: 2 groups of 4 waves per block share
+    // one split's pixels, so the same waves write half the slab (HYRES_WGRAD_1X1_GROUPS=1: one group). Isolated
+    // 128^2 64<->128: 65 -> 62 us; on the 32^2 grids it lost (24.6 -> 30.5 us: half the blocks)
+    static const int g1x1 = env_int("HYRES_WGRAD_1X1_GROUPS", 2);
+    p.g1x1 = 1;
+    if (g1x1 == 2 && !small && !halo && kt == KT && !p.tapn && !d->square_q && d->ntaps == 1 && d->dh[0] == 0 &&
+        d->dw[0] == 0 && d->sq == 1 && d->Hqq == d->Hq && d->Wqq == d->Wq && p.ngroups == 1 && p.nsplit >= 2) {
+        p.g1x1 = 2;
+        p.nsplit = (p.nsplit + 1) / 2;
     }
     p.cps = ceil_div(p.nchunks, p.nsplit);
     p.nsplit = ceil_div(p.nchunks, p.cps);
@@ -1655,11 +1718,17 @@ int hyres_conv_wgrad(const hyres_wgrad_desc* d0, const float* pp, const float* q
                      d->ntaps == 1 && d->dh[0] == 0 && d->dw[0] == 0 && d->sq == 1 && d->Hqq == d->Hq &&
                      d->Wqq == d->Wq && p.ngroups == 1;
     if (one) {
-        if (p.TMc == 2 && p.TNc == 2) hipLaunchKernelGGL((wgrad1x1_kernel<2, 2, 2, 2>), grid, dim3(256), 0, st, a);
-        else if (p.TMc == 2) hipLaunchKernelGGL((wgrad1x1_kernel<2, 1, 2, 2>), grid, dim3(256), 0, st, a);
-        else if (p.WMc == 1) hipLaunchKernelGGL((wgrad1x1_kernel<1, 1, 1, 4>), grid, dim3(256), 0, st, a);
-        else if (p.WNc == 1) hipLaunchKernelGGL((wgrad1x1_kernel<1, 1, 4, 1>), grid, dim3(256), 0, st, a);
-        else hipLaunchKernelGGL((wgrad1x1_kernel<1, 1, 2, 2>), grid, dim3(256), 0, st, a);
+        auto w1 = [&](auto gc) {
+            constexpr int G_ = decltype(gc)::value;
+            const dim3 blk(256 * G_);
+            if (p.TMc == 2 && p.TNc == 2) hipLaunchKernelGGL((wgrad1x1_kernel<2, 2, 2, 2, G_>), grid, blk, 0, st, a);
+            else if (p.TMc == 2) hipLaunchKernelGGL((wgrad1x1_kernel<2, 1, 2, 2, G_>), grid, blk, 0, st, a);
+            else if (p.WMc == 1) hipLaunchKernelGGL((wgrad1x1_kernel<1, 1, 1, 4, G_>), grid, blk, 0, st, a);
+            else if (p.WNc == 1) hipLaunchKernelGGL((wgrad1x1_kernel<1, 1, 4, 1, G_>), grid, blk, 0, st, a);
+            else hipLaunchKernelGGL((wgrad1x1_kernel<1, 1, 2, 2, G_>), grid, blk, 0, st, a);
+        };
+        if (p.g1x1 == 2) w1(std::integral_constant<int, 2>{});
+        else w1(std::integral_constant<int, 1>{});
     } else if (thin) {
         launch_thin(a, tp, (io & 1) != 0, st);
     } else if (p.halo && wgrad_f16_ok(d)) {
