@@ -106,8 +106,16 @@ __global__ void prelu_bwd_kernel(const float* x, int ldx, const float* g, int ld
 }
 __global__ void sum_partials_kernel(const float* part, int nb, float* out, int accumulate) {
     __shared__ float red[256];
-    float s = 0.f;
-    for (int i = threadIdx.x; i < nb; i += 256) s += part[i];
+    // 8 independent loads in flight per thread (a serial walk over nb/256 partials was latency-bound: ~19 us)
+    float s8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    int i = threadIdx.x;
+    for (; i + 7 * 256 < nb; i += 8 * 256)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s8[k] += part[i + k * 256];
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+        if (i + k * 256 < nb) s8[k] += part[i + k * 256];
+    const float s = ((s8[0] + s8[1]) + (s8[2] + s8[3])) + ((s8[4] + s8[5]) + (s8[6] + s8[7]));
     red[threadIdx.x] = s;
     __syncthreads();
     for (int k = 128; k > 0; k >>= 1) {

@@ -522,8 +522,44 @@ __global__ __launch_bounds__(256 * G) void wgrad1x1_kernel(const WgradArgs a) {
         }
 }
 
-template <int KR, int KW, int SQ, int DIL = 1>
-__global__ __launch_bounds__(256, 2) void wgrad_halo_kernel(const WgradArgs a, int dhg, int dwg) {
+// G groups of 256 threads of one block accumulated the same output tile over disjoint pixel ranges: add groups
+// 1..G-1 into group 0's floatx16 acc[NT] in group order (deterministic), CH taps per pass through `red`
+// (RED floats of LDS; thread-major so every wave's stores and loads are conflict-free). All threads call it.
+template <int NT, int G, int RED>
+__device__ __forceinline__ void combine_groups(floatx16 (&acc)[NT], float* red, int tid, int gq) {
+    constexpr int CH = RED / (16 * 256) < NT ? RED / (16 * 256) : NT;
+    static_assert(CH >= 1, "LDS too small for one tap");
+    constexpr int NCH = (NT + CH - 1) / CH;
+    static_for<NCH>([&](auto C) {
+        constexpr int c0 = decltype(C)::value * CH;
+        for (int g2 = 1; g2 < G; ++g2) {
+            if (gq == g2)
+                static_for<NT>([&](auto J) {
+                    constexpr int j = decltype(J)::value;
+                    if constexpr (j >= c0 && j < c0 + CH) {
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) red[((j - c0) * 16 + r) * 256 + tid] = acc[j][r];
+                    }
+                });
+            __syncthreads();
+            if (gq == 0)
+                static_for<NT>([&](auto J) {
+                    constexpr int j = decltype(J)::value;
+                    if constexpr (j >= c0 && j < c0 + CH) {
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) acc[j][r] += red[((j - c0) * 16 + r) * 256 + tid];
+                    }
+                });
+            __syncthreads();
+        }
+    });
+}
+
+// G = 2 (round 3): two 4-wave groups per 512-thread block share one pixel split (each its own contiguous half of
+// the split's chunks and its own LDS buffers: 1 block of 8 waves per CU instead of 2 of 4) and are summed through
+// LDS before the slab write, so the same waves write and the deferred reduce reads half the split slab.
+template <int KR, int KW, int SQ, int DIL = 1, int G = 1>
+__global__ __launch_bounds__(256 * G, G == 1 ? 2 : 1) void wgrad_halo_kernel(const WgradArgs a, int dhg, int dwg) {
     // DIL: tap spacing (2: MultiScaleRefine's dilated 3x3, enhancement.py:44-51): the KR halo rows are DIL
     // rows apart, the halo columns span 31*SQ + DIL*(KW-1) + 1 pixels
     constexpr int BM = 64, BN = 64, NT = KR * KW, HC = 31 * SQ + DIL * (KW - 1) + 1;  // halo columns of a 32-px chunk
@@ -532,9 +568,10 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo_kernel(const WgradArgs a, i
     constexpr int P_V = KT * BM / 4 / 256;
     constexpr int H_E = KR * HC * (BN / 4);
     constexpr int H_V = (H_E + 255) / 256;
-    __shared__ __attribute__((aligned(16))) float smem[2 * (PSZ + HSZ)];
+    __shared__ __attribute__((aligned(16))) float smem_all[G * 2 * (PSZ + HSZ)];
     const hyres_wgrad_desc& d = a.d;
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x & 255, gq = threadIdx.x >> 8;
+    float* const smem = smem_all + gq * (2 * (PSZ + HSZ));
     const int bid = blockIdx.x;
     const int lb = (bid & 7) * (gridDim.x >> 3) + (bid >> 3);  // XCD-aware order, as wgrad_kernel
     if (lb >= a.nblocks) return;
@@ -600,41 +637,49 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo_kernel(const WgradArgs a, i
     for (int j = 0; j < NT; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
-    const int kb = split * a.chunks_per_split;
-    const int ke = min(a.nchunks, kb + a.chunks_per_split);
+    // the split's chunks [kb0, ke0), this group's contiguous share [kb, ke); every group runs `iters` barrier
+    // steps (a group with fewer chunks idles through its last ones)
+    const int kb0 = split * a.chunks_per_split;
+    const int ke0 = min(a.nchunks, kb0 + a.chunks_per_split);
+    const int share = (max(ke0 - kb0, 0) + G - 1) / G;
+    const int kb = min(ke0, kb0 + gq * share), ke = min(ke0, kb + share);
     if (kb < ke) {
         load(kb);
         store(0);
     }
     __syncthreads();
     int cur = 0;
-    for (int kc = kb; kc < ke; ++kc) {
-        if (kc + 1 < ke) load(kc + 1);  // next chunk in flight during this chunk's NT x 16 MFMAs
-        const float* Ps = smem + cur * (PSZ + HSZ);
-        const float* Hs = Ps + PSZ;
-        static_for<NT>([&](auto J) {
-            constexpr int t = decltype(J)::value;
-            constexpr int hr = t / KW, hc = t % KW;
+    for (int it = 0; it < share; ++it) {
+        const int kc = kb + it;
+        const bool next = kc + 1 < ke;
+        if (next) load(kc + 1);  // next chunk in flight during this chunk's NT x 16 MFMAs
+        if (kc < ke) {
+            const float* Ps = smem + cur * (PSZ + HSZ);
+            const float* Hs = Ps + PSZ;
+            static_for<NT>([&](auto J) {
+                constexpr int t = decltype(J)::value;
+                constexpr int hr = t / KW, hc = t % KW;
 #pragma unroll
-            for (int s2 = 0; s2 < KT / 2; ++s2) {
-                const int k = lh * (KT / 2) + s2;
-                const float af = Ps[k * PP + wm * 32 + lr];
-                const float bf = Hs[(hr * HC + k * SQ + DIL * hc) * PQ + wn * 32 + lr];
-                acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(af, bf, acc[t], 0, 0, 0);
-            }
-        });
-        if (kc + 1 < ke) store(cur ^ 1);
+                for (int s2 = 0; s2 < KT / 2; ++s2) {
+                    const int k = lh * (KT / 2) + s2;
+                    const float af = Ps[k * PP + wm * 32 + lr];
+                    const float bf = Hs[(hr * HC + k * SQ + DIL * hc) * PQ + wn * 32 + lr];
+                    acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(af, bf, acc[t], 0, 0, 0);
+                }
+            });
+        }
+        if (next) store(cur ^ 1);
         __syncthreads();
         cur ^= 1;
     }
-    if (do_bias) {
-        float4* red = reinterpret_cast<float4*>(smem);  // the loop ended with a barrier
-        red[tid] = bsum;
+    if (do_bias) {  // block-uniform
+        float4* red = reinterpret_cast<float4*>(smem_all);  // the loop ended with a barrier
+        red[threadIdx.x] = bsum;
         __syncthreads();
-        if (tid < BM / 4) {
+        if (threadIdx.x < BM / 4) {
             float4 s4 = make_float4(0.f, 0.f, 0.f, 0.f);
-            for (int r = 0; r < 256 / (BM / 4); ++r) {
-                const float4 v = red[tid + r * (BM / 4)];
+            for (int r = 0; r < 256 * G / (BM / 4); ++r) {
+                const float4 v = red[threadIdx.x + r * (BM / 4)];
                 s4.x += v.x; s4.y += v.y; s4.z += v.z; s4.w += v.w;
             }
             float* dst = a.bias_slab + (long long)split * d.M + m0 + 4 * tid;
@@ -642,6 +687,11 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo_kernel(const WgradArgs a, i
             for (int c = 0; c < 4; ++c)
                 if (m0 + 4 * tid + c < d.M) dst[c] = sv[c];
         }
+        __syncthreads();
+    }
+    if constexpr (G > 1) {
+        combine_groups<NT, G, G * 2 * (PSZ + HSZ)>(acc, smem_all, tid, gq);
+        if (gq != 0) return;
     }
     const long long MN = (long long)d.M * d.N;
     static_for<NT>([&](auto J) {
@@ -940,8 +990,8 @@ __global__ __launch_bounds__(256) void wgrad_f16_kernel(const WgradArgs a) {
 // The tap's B rows are halo rows base + k*SQ: the transposed read takes per-lane addresses, so the stride
 // is just a pitch of SQ*PQ. Bias gradient = fp32 column sums of the unrounded P (as wgrad_f16_kernel).
 // ------------------------------------------------------------------------------------------------
-template <int KR, int KW, int SQ, int DIL = 1, int IOH = 0>
-__global__ __launch_bounds__(256, 2) void wgrad_halo_f16_kernel(const WgradArgs a, int dhg, int dwg) {
+template <int KR, int KW, int SQ, int DIL = 1, int IOH = 0, int G = 1>  // G: as wgrad_halo_kernel
+__global__ __launch_bounds__(256 * G, G == 1 ? 2 : 1) void wgrad_halo_f16_kernel(const WgradArgs a, int dhg, int dwg) {
     constexpr bool PH = (IOH & 1) != 0, QH = (IOH & 2) != 0;  // fp16 operands in HBM (wgrad_f16_kernel)
     constexpr int BM = 64, BN = 64, NT = KR * KW, HC = 31 * SQ + DIL * (KW - 1) + 1;
     constexpr int PP = BM + 32, PQ = BN + 32;  // halves
@@ -950,9 +1000,10 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo_f16_kernel(const WgradArgs 
     constexpr int H_E = KR * HC * (BN / 4);
     constexpr int H_V = (H_E + 255) / 256;
     static_assert((PSZ + HSZ) % 4 == 0, "8-byte aligned buffers for the transposed reads");
-    __shared__ __attribute__((aligned(16))) _Float16 smem[2 * (PSZ + HSZ)];
+    __shared__ __attribute__((aligned(16))) _Float16 smem_all[G * 2 * (PSZ + HSZ)];
     const hyres_wgrad_desc& d = a.d;
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x & 255, gq = threadIdx.x >> 8;
+    _Float16* const smem = smem_all + gq * (2 * (PSZ + HSZ));
     const int bid = blockIdx.x;
     const int lb = (bid & 7) * (gridDim.x >> 3) + (bid >> 3);  // XCD-aware order, as wgrad_kernel
     if (lb >= a.nblocks) return;
@@ -1018,20 +1069,25 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo_f16_kernel(const WgradArgs 
     for (int j = 0; j < NT; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
-    const int kb = split * a.chunks_per_split;
-    const int ke = min(a.nchunks, kb + a.chunks_per_split);
+    const int kb0 = split * a.chunks_per_split;
+    const int ke0 = min(a.nchunks, kb0 + a.chunks_per_split);
+    const int share = (max(ke0 - kb0, 0) + G - 1) / G;
+    const int kb = min(ke0, kb0 + gq * share), ke = min(ke0, kb + share);
     if (kb < ke) {
         load(kb);
         store(0);
     }
     __syncthreads();
     int cur = 0;
-    for (int kc = kb; kc < ke; ++kc) {
-        if (kc + 1 < ke) load(kc + 1);  // next chunk in flight during this chunk's NT x 2 MFMAs per wave
+    for (int it = 0; it < share; ++it) {
+        const int kc = kb + it;
+        const bool next = kc + 1 < ke;
+        if (next) load(kc + 1);  // next chunk in flight during this chunk's NT x 2 MFMAs per wave
         const _Float16* Ps = smem + cur * (PSZ + HSZ);
         const _Float16* Hs = Ps + PSZ;
 #pragma unroll
         for (int s = 0; s < KT / 16; ++s) {
+            if (kc >= ke) break;  // this group idles through the split's last step
             const _Float16* pa = Ps + (16 * s + tr_row) * PP + wm * 32 + tr_col;
             const halfx4_t alo = lds_tr4(pa), ahi = lds_tr4(pa + 4 * PP);
             const halfx8_t af = __builtin_shufflevector(alo, ahi, 0, 1, 2, 3, 4, 5, 6, 7);
@@ -1044,18 +1100,18 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo_f16_kernel(const WgradArgs 
                 acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af, bf, acc[t], 0, 0, 0);
             });
         }
-        if (kc + 1 < ke) store(cur ^ 1);
+        if (next) store(cur ^ 1);
         __syncthreads();
         cur ^= 1;
     }
-    if (do_bias) {
-        float4* red = reinterpret_cast<float4*>(smem);  // the loop ended with a barrier
-        red[tid] = bsum;
+    if (do_bias) {  // block-uniform
+        float4* red = reinterpret_cast<float4*>(smem_all);  // the loop ended with a barrier
+        red[threadIdx.x] = bsum;
         __syncthreads();
-        if (tid < BM / 4) {
+        if (threadIdx.x < BM / 4) {
             float4 s4 = make_float4(0.f, 0.f, 0.f, 0.f);
-            for (int r = 0; r < 256 / (BM / 4); ++r) {
-                const float4 v = red[tid + r * (BM / 4)];
+            for (int r = 0; r < 256 * G / (BM / 4); ++r) {
+                const float4 v = red[threadIdx.x + r * (BM / 4)];
                 s4.x += v.x; s4.y += v.y; s4.z += v.z; s4.w += v.w;
             }
             float* dst = a.bias_slab + (long long)split * d.M + m0 + 4 * tid;
@@ -1063,6 +1119,11 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo_f16_kernel(const WgradArgs 
             for (int c = 0; c < 4; ++c)
                 if (m0 + 4 * tid + c < d.M) dst[c] = sv[c];
         }
+        __syncthreads();
+    }
+    if constexpr (G > 1) {
+        combine_groups<NT, G, G * (PSZ + HSZ)>(acc, reinterpret_cast<float*>(smem_all), tid, gq);
+        if (gq != 0) return;
     }
     const int lr = lane & 31;
     const long long MN = (long long)d.M * d.N;
@@ -1313,6 +1374,30 @@ __global__ __launch_bounds__(256) void wgrad_bias_reduce_kernel(const float* sla
         wgrad_reduce_body<LX>(blockIdx.x - nb_w, bslab, nsplit, 1, M, 1, dbias, 1, 0, 0, accumulate);
 }
 
+// Deferred reduces of a whole gradient segment in one launch (hyres_wgrad_reduce_jobs): the job table rides in
+// the kernel arguments (captured by value in a HIP graph, no device table to keep alive); block b belongs to the
+// first job whose block range ends past b. Each job runs the per-layer reduce body with the layer's own lane
+// layout, so every output sums its partials in exactly the order wgrad_reduce_kernel does.
+struct WgradJobBatch {
+    hyres_wgrad_job j[HYRES_WGRAD_MAX_JOBS];
+    int end[HYRES_WGRAD_MAX_JOBS];  // exclusive prefix sums of the jobs' block counts
+    int n;
+};
+
+__global__ __launch_bounds__(256) void wgrad_reduce_batch_kernel(const WgradJobBatch b) {
+    const int blk = blockIdx.x;
+    int k = 0;
+    while (k < b.n - 1 && blk >= b.end[k]) ++k;
+    const int local = blk - (k ? b.end[k - 1] : 0);
+    const hyres_wgrad_job& j = b.j[k];
+    if (j.lanes == 16)
+        wgrad_reduce_body<16>(local, j.slab, j.nsplit, j.ntaps, j.M, j.N, j.dst, j.sm, j.sn, j.st, j.accumulate);
+    else if (j.lanes == 8)
+        wgrad_reduce_body<8>(local, j.slab, j.nsplit, j.ntaps, j.M, j.N, j.dst, j.sm, j.sn, j.st, j.accumulate);
+    else
+        wgrad_reduce_body<4>(local, j.slab, j.nsplit, j.ntaps, j.M, j.N, j.dst, j.sm, j.sn, j.st, j.accumulate);
+}
+
 // lanes per block row for the reduce: keep ~>= 1024 blocks when the split count is large
 static int reduce_lx(long long total, int nsplit) {
     if (nsplit <= 64 || (total + 63) / 64 >= 1024) return 16;
@@ -1363,23 +1448,6 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const float* x, int
     }
 }
 
-// Pass 2: block handles 64 columns; 4 thread rows split the partials, folded through LDS.
-__global__ __launch_bounds__(256) void colsum_final_kernel(const float* part, int nb, int C, float* dst,
-                                                           int accumulate) {
-    __shared__ float red[256];
-    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-    const int q = threadIdx.x >> 6;
-    float s = 0.f;
-    if (c < C)
-        for (int b = q; b < nb; b += 4) s += part[(long long)b * C + c];
-    red[threadIdx.x] = s;
-    __syncthreads();
-    if (q == 0 && c < C) {
-        s = red[threadIdx.x] + red[threadIdx.x + 64] + red[threadIdx.x + 128] + red[threadIdx.x + 192];
-        dst[c] = accumulate ? dst[c] + s : s;
-    }
-}
-
 }  // namespace hyres
 
 using namespace hyres;
@@ -1391,6 +1459,7 @@ struct WgradPlan {
     int TMc, TNc, WMc, WNc, NT, BM, BN, mtiles, ntiles, ngroups, nchunks, nsplit, cps, tapn, nblocks;
     int halo, hk, hdh, hdw, hdil;  // wgrad_halo_kernel: K, first tap's (dh, dw), tap spacing
     int g1x1;                      // wgrad1x1_kernel: 4-wave groups per block
+    int hg;                        // wgrad_halo(_f16)_kernel: 4-wave groups per block
 };
 
 // wgrad_halo_kernel applies: fp32, dense KxK taps (K = 3 or 5, dilation 1; K = 3 with dilation 2), Q stride
@@ -1488,6 +1557,17 @@ static WgradPlan wgrad_plan(const hyres_wgrad_desc* d) {
     // 1x1 stride-1 fp32 gradients (wgrad1x1_kernel) outside the small grids: 2 groups of 4 waves per block share
     // one split's pixels, so the same waves write half the slab (HYRES_WGRAD_1X1_GROUPS=1: one group). Isolated
     // 128^2 64<->128: 65 -> 62 us; on the 32^2 grids it lost (24.6 -> 30.5 us: half the blocks)
+    // halo kernels (3x3, dilated 3x3, 5x5 stride 2), HYRES_WGRAD_HALO_GROUPS=2: 2 groups of 4 waves per block on
+    // one split, 1 block per CU instead of 2: half the split slab written and reduced. Isolated 128^2 3x3 64->64
+    // (kernel + reduce) 206 -> 198 us fp32, 63 -> 57 us f16, 256^2 666 -> 673 us; in the live C2 step 40.0 ->
+    // 41.1 ms fp32 (the 146 KB block keeps the concurrent branches' blocks off its CU), AMP 21.9 -> 22.0 ms: off
+    // by default (profiles/r3o_halo_groups.txt)
+    static const int hg_env = env_int("HYRES_WGRAD_HALO_GROUPS", 1);
+    p.hg = 1;
+    if (p.halo && hg_env == 2 && !(p.hk == 5 && d->sq == 1) && p.nsplit >= 2) {
+        p.hg = 2;
+        p.nsplit = (p.nsplit + 1) / 2;
+    }
     static const int g1x1 = env_int("HYRES_WGRAD_1X1_GROUPS", 2);
     p.g1x1 = 1;
     if (g1x1 == 2 && !small && !halo && kt == KT && !p.tapn && !d->square_q && d->ntaps == 1 && d->dh[0] == 0 &&
@@ -1654,8 +1734,11 @@ long long hyres_wgrad_workspace_bytes(const hyres_wgrad_desc* d) {
     return bytes;
 }
 
-int hyres_conv_wgrad(const hyres_wgrad_desc* d0, const float* pp, const float* qq, float* dst, float* dbias,
-                     void* ws, long long ws_bytes, hyres_stream_t s) {
+// Launch the weight-gradient GEMM (and, for the swapped small-M layers, the bias column sums) and describe the
+// split-K slab reduce that remains as jobs[0] (weight) and jobs[1] (the [nsplit][M] bias partials, if any).
+static int wgrad_issue(const hyres_wgrad_desc* d0, const float* pp, const float* qq, float* dst, float* dbias,
+                       void* ws, long long ws_bytes, hyres_stream_t s, hyres_wgrad_job* jobs, int* njobs) {
+    *njobs = 0;
     HY_REQUIRE(d0 && pp && qq && dst, HYRES_E_ARG, "wgrad: NULL");
     const long long need = hyres_wgrad_workspace_bytes(d0);
     HY_REQUIRE(ws && ws_bytes >= need, HYRES_E_WORKSPACE, "wgrad: workspace %lld < %lld", ws_bytes, need);
@@ -1732,33 +1815,46 @@ int hyres_conv_wgrad(const hyres_wgrad_desc* d0, const float* pp, const float* q
     } else if (thin) {
         launch_thin(a, tp, (io & 1) != 0, st);
     } else if (p.halo && wgrad_f16_ok(d)) {
-        auto halo16 = [&](auto ioc) {
-            constexpr int IO_ = decltype(ioc)::value;
+        auto halo16 = [&](auto ioc, auto gc) {
+            constexpr int IO_ = decltype(ioc)::value, G_ = decltype(gc)::value;
+            const dim3 blk(256 * G_);
             if (p.hk == 3 && p.NT == 3 && p.hdil == 2)
-                hipLaunchKernelGGL((wgrad_halo_f16_kernel<1, 3, 1, 2, IO_>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
+                hipLaunchKernelGGL((wgrad_halo_f16_kernel<1, 3, 1, 2, IO_, G_>), grid, blk, 0, st, a, p.hdh, p.hdw);
             else if (p.hk == 3 && p.NT == 3)
-                hipLaunchKernelGGL((wgrad_halo_f16_kernel<1, 3, 1, 1, IO_>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
+                hipLaunchKernelGGL((wgrad_halo_f16_kernel<1, 3, 1, 1, IO_, G_>), grid, blk, 0, st, a, p.hdh, p.hdw);
             else if (p.hk == 3 && p.hdil == 2)
-                hipLaunchKernelGGL((wgrad_halo_f16_kernel<3, 3, 1, 2, IO_>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
+                hipLaunchKernelGGL((wgrad_halo_f16_kernel<3, 3, 1, 2, IO_, G_>), grid, blk, 0, st, a, p.hdh, p.hdw);
             else if (p.hk == 3)
-                hipLaunchKernelGGL((wgrad_halo_f16_kernel<3, 3, 1, 1, IO_>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
-            else if (d->sq == 1)
+                hipLaunchKernelGGL((wgrad_halo_f16_kernel<3, 3, 1, 1, IO_, G_>), grid, blk, 0, st, a, p.hdh, p.hdw);
+            else if (d->sq == 1)  // 5x5 stride 1: one group (3 blocks per CU)
                 hipLaunchKernelGGL((wgrad_halo_f16_kernel<1, 5, 1, 1, IO_>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
-            else hipLaunchKernelGGL((wgrad_halo_f16_kernel<1, 5, 2, 1, IO_>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
+            else hipLaunchKernelGGL((wgrad_halo_f16_kernel<1, 5, 2, 1, IO_, G_>), grid, blk, 0, st, a, p.hdh, p.hdw);
         };
-        if (io == 1) halo16(std::integral_constant<int, 1>{});
-        else if (io == 2) halo16(std::integral_constant<int, 2>{});
-        else halo16(std::integral_constant<int, 0>{});
+        auto halo16g = [&](auto ioc) {
+            if (p.hg == 2) halo16(ioc, std::integral_constant<int, 2>{});
+            else halo16(ioc, std::integral_constant<int, 1>{});
+        };
+        if (io == 1) halo16g(std::integral_constant<int, 1>{});
+        else if (io == 2) halo16g(std::integral_constant<int, 2>{});
+        else halo16g(std::integral_constant<int, 0>{});
     } else if (p.halo) {
-        if (p.hk == 3 && p.NT == 3 && p.hdil == 2)
-            hipLaunchKernelGGL((wgrad_halo_kernel<1, 3, 1, 2>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
-        else if (p.hk == 3 && p.NT == 3)
-            hipLaunchKernelGGL((wgrad_halo_kernel<1, 3, 1, 1>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
-        else if (p.hk == 3 && p.hdil == 2)
-            hipLaunchKernelGGL((wgrad_halo_kernel<3, 3, 1, 2>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
-        else if (p.hk == 3) hipLaunchKernelGGL((wgrad_halo_kernel<3, 3, 1>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
-        else if (d->sq == 1) hipLaunchKernelGGL((wgrad_halo_kernel<1, 5, 1>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
-        else hipLaunchKernelGGL((wgrad_halo_kernel<1, 5, 2>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
+        auto halo32 = [&](auto gc) {
+            constexpr int G_ = decltype(gc)::value;
+            const dim3 blk(256 * G_);
+            if (p.hk == 3 && p.NT == 3 && p.hdil == 2)
+                hipLaunchKernelGGL((wgrad_halo_kernel<1, 3, 1, 2, G_>), grid, blk, 0, st, a, p.hdh, p.hdw);
+            else if (p.hk == 3 && p.NT == 3)
+                hipLaunchKernelGGL((wgrad_halo_kernel<1, 3, 1, 1, G_>), grid, blk, 0, st, a, p.hdh, p.hdw);
+            else if (p.hk == 3 && p.hdil == 2)
+                hipLaunchKernelGGL((wgrad_halo_kernel<3, 3, 1, 2, G_>), grid, blk, 0, st, a, p.hdh, p.hdw);
+            else if (p.hk == 3)
+                hipLaunchKernelGGL((wgrad_halo_kernel<3, 3, 1, 1, G_>), grid, blk, 0, st, a, p.hdh, p.hdw);
+            else if (d->sq == 1)  // 5x5 stride 1: one group (3 blocks per CU)
+                hipLaunchKernelGGL((wgrad_halo_kernel<1, 5, 1>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
+            else hipLaunchKernelGGL((wgrad_halo_kernel<1, 5, 2, 1, G_>), grid, blk, 0, st, a, p.hdh, p.hdw);
+        };
+        if (p.hg == 2) halo32(std::integral_constant<int, 2>{});
+        else halo32(std::integral_constant<int, 1>{});
     } else if (wgrad_f16_ok(d)) {
         static const int f16_one = env_int("HYRES_WGRAD_F16_1X1", 1);
         const bool one16 = f16_one && !sqr && d->ntaps == 1 && d->dh[0] == 0 && d->dw[0] == 0 && d->sq == 1 &&
@@ -1805,33 +1901,77 @@ int hyres_conv_wgrad(const hyres_wgrad_desc* d0, const float* pp, const float* q
     if (rc) return rc;
     const long long total = (long long)d->ntaps * d->M * d->N;
     const int lx = reduce_lx(total, p.nsplit);
-    const int outb = 4 * lx;
-    auto reduce = [&](auto lxc) {
-        constexpr int LX = decltype(lxc)::value;
-        if (dbias && !swap) {  // [nsplit][M] bias partials reduced by the same launch
-            const int nb_w = (int)ceil_div(total, outb);
-            hipLaunchKernelGGL(wgrad_bias_reduce_kernel<LX>, dim3(nb_w + ceil_div(d->M, outb)), dim3(256), 0, st,
-                               (const float*)ws, p.nsplit, d->ntaps, d->M, d->N, dst, d->sm, d->sn, d->st,
-                               d->accumulate, nb_w, (const float*)bias_ws, dbias);
-            return HY_LAUNCH_CHECK("wgrad_bias_reduce_kernel");
-        }
-        hipLaunchKernelGGL(wgrad_reduce_kernel<LX>, dim3(ceil_div(total, outb)), dim3(256), 0, st, (const float*)ws,
-                           p.nsplit, d->ntaps, d->M, d->N, dst, d->sm, d->sn, d->st, d->accumulate);
-        int r = HY_LAUNCH_CHECK("wgrad_reduce_kernel");
-        if (r || !dbias || swap) return r;
-        // [nsplit][M] partials = a [nsplit][1][M][1] slab: the same parallel deterministic reduce
-        hipLaunchKernelGGL(wgrad_reduce_kernel<LX>, dim3(ceil_div(d->M, outb)), dim3(256), 0, st,
-                           (const float*)bias_ws, p.nsplit, 1, d->M, 1, dbias, 1, 0, 0, d->accumulate);
-        return HY_LAUNCH_CHECK("wgrad_reduce_kernel(bias)");
-    };
-    if (lx == 16) rc = reduce(std::integral_constant<int, 16>{});
-    else if (lx == 8) rc = reduce(std::integral_constant<int, 8>{});
-    else rc = reduce(std::integral_constant<int, 4>{});
-    if (rc || !dbias || !swap) return rc;
-    if (swap) {  // P (= dY) is the tap-folded side here: plain column sums
+    jobs[0] = hyres_wgrad_job{(const float*)ws, dst, p.nsplit, d->ntaps, d->M, d->N, d->sm, d->sn, d->st,
+                              d->accumulate, lx, 0};
+    *njobs = 1;
+    if (dbias && !swap) {  // [nsplit][M] partials = a [nsplit][1][M][1] slab, reduced with the weight's layout
+        jobs[1] = hyres_wgrad_job{(const float*)bias_ws, dbias, p.nsplit, 1, d->M, 1, 1, 0, 0, d->accumulate, lx, 0};
+        *njobs = 2;
+    }
+    if (dbias && swap) {  // P (= dY) is the tap-folded side here: plain column sums (own workspace after the slab)
         const int P = d0->B * d0->Hq * d0->Wq;
         return hyres_colsum(p_orig, P, d0->M, d0->ldp, dbias, d0->accumulate, bias_ws,
                             hyres_colsum_workspace_bytes(P, d0->M), s);
+    }
+    return 0;
+}
+
+int hyres_conv_wgrad(const hyres_wgrad_desc* d, const float* pp, const float* qq, float* dst, float* dbias,
+                     void* ws, long long ws_bytes, hyres_stream_t s) {
+    hyres_wgrad_job jobs[2];
+    int nj = 0;
+    int rc = wgrad_issue(d, pp, qq, dst, dbias, ws, ws_bytes, s, jobs, &nj);
+    if (rc || nj == 0) return rc;
+    const hyres_wgrad_job& w = jobs[0];
+    const long long total = (long long)w.ntaps * w.M * w.N;
+    const int outb = 4 * w.lanes;
+    hipStream_t st = as_stream(s);
+    auto reduce = [&](auto lxc) {
+        constexpr int LX = decltype(lxc)::value;
+        if (nj == 2) {  // the [nsplit][M] bias partials reduced by the same launch
+            const hyres_wgrad_job& b = jobs[1];
+            const int nb_w = (int)ceil_div(total, outb);
+            hipLaunchKernelGGL(wgrad_bias_reduce_kernel<LX>, dim3(nb_w + ceil_div(b.M, outb)), dim3(256), 0, st,
+                               w.slab, w.nsplit, w.ntaps, w.M, w.N, w.dst, w.sm, w.sn, w.st, w.accumulate, nb_w,
+                               b.slab, b.dst);
+            return HY_LAUNCH_CHECK("wgrad_bias_reduce_kernel");
+        }
+        hipLaunchKernelGGL(wgrad_reduce_kernel<LX>, dim3(ceil_div(total, outb)), dim3(256), 0, st, w.slab, w.nsplit,
+                           w.ntaps, w.M, w.N, w.dst, w.sm, w.sn, w.st, w.accumulate);
+        return HY_LAUNCH_CHECK("wgrad_reduce_kernel");
+    };
+    if (w.lanes == 16) return reduce(std::integral_constant<int, 16>{});
+    if (w.lanes == 8) return reduce(std::integral_constant<int, 8>{});
+    return reduce(std::integral_constant<int, 4>{});
+}
+
+int hyres_conv_wgrad_deferred(const hyres_wgrad_desc* d, const float* pp, const float* qq, float* dst,
+                              float* dbias, void* ws, long long ws_bytes, hyres_wgrad_job* jobs, int* njobs,
+                              hyres_stream_t s) {
+    HY_REQUIRE(jobs && njobs, HYRES_E_ARG, "wgrad_deferred: NULL job output");
+    return wgrad_issue(d, pp, qq, dst, dbias, ws, ws_bytes, s, jobs, njobs);
+}
+
+int hyres_wgrad_reduce_jobs(const hyres_wgrad_job* jobs, int n, hyres_stream_t s) {
+    HY_REQUIRE(n >= 0 && (n == 0 || jobs), HYRES_E_ARG, "wgrad_reduce_jobs: bad job list");
+    hipStream_t st = as_stream(s);
+    for (int i0 = 0; i0 < n; i0 += HYRES_WGRAD_MAX_JOBS) {
+        WgradJobBatch b{};
+        b.n = std::min(HYRES_WGRAD_MAX_JOBS, n - i0);
+        long long blocks = 0;
+        for (int k = 0; k < b.n; ++k) {
+            const hyres_wgrad_job& j = jobs[i0 + k];
+            HY_REQUIRE(j.slab && j.dst && j.nsplit >= 1 && j.ntaps >= 1 && j.M >= 1 && j.N >= 1 &&
+                           (j.lanes == 4 || j.lanes == 8 || j.lanes == 16),
+                       HYRES_E_ARG, "wgrad_reduce_jobs: bad job %d", i0 + k);
+            b.j[k] = j;
+            blocks += ceil_div((long long)j.ntaps * j.M * j.N, 4 * j.lanes);
+            HY_REQUIRE(blocks < (1LL << 31), HYRES_E_SHAPE, "wgrad_reduce_jobs: too many blocks");
+            b.end[k] = (int)blocks;
+        }
+        hipLaunchKernelGGL(wgrad_reduce_batch_kernel, dim3((unsigned)blocks), dim3(256), 0, st, b);
+        const int rc = HY_LAUNCH_CHECK("wgrad_reduce_batch_kernel");
+        if (rc) return rc;
     }
     return 0;
 }
@@ -1859,9 +1999,19 @@ int hyres_colsum(const float* x, int P, int C, int ld, float* dst, int accumulat
         hipLaunchKernelGGL(colsum_partial_kernel<1>, dim3(nb), dim3(256), 0, st, x, P, C, ld, rows, (float*)ws);
     int rc = HY_LAUNCH_CHECK("colsum_partial");
     if (rc) return rc;
-    hipLaunchKernelGGL(colsum_final_kernel, dim3(ceil_div(C, 64)), dim3(256), 0, st, (const float*)ws, nb, C, dst,
-                       accumulate);
-    return HY_LAUNCH_CHECK("colsum_final");
+    // the [nb][C] partials = a [nb][1][C][1] slab: the parallel deterministic split reduce (round 3; the former
+    // colsum_final walked nb/4 partial rows serially per thread: 24 us per launch on C = 64)
+    const int lx = reduce_lx(C, nb);
+    if (lx == 16)
+        hipLaunchKernelGGL(wgrad_reduce_kernel<16>, dim3(ceil_div(C, 64)), dim3(256), 0, st, (const float*)ws, nb, 1, C,
+                           1, dst, 1, 0, 0, accumulate);
+    else if (lx == 8)
+        hipLaunchKernelGGL(wgrad_reduce_kernel<8>, dim3(ceil_div(C, 32)), dim3(256), 0, st, (const float*)ws, nb, 1, C,
+                           1, dst, 1, 0, 0, accumulate);
+    else
+        hipLaunchKernelGGL(wgrad_reduce_kernel<4>, dim3(ceil_div(C, 16)), dim3(256), 0, st, (const float*)ws, nb, 1, C,
+                           1, dst, 1, 0, 0, accumulate);
+    return HY_LAUNCH_CHECK("colsum_reduce");
 }
 
 }  // extern "C"

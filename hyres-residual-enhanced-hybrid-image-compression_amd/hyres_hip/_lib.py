@@ -54,6 +54,16 @@ class WgradDesc(ctypes.Structure):
         ("io_f16", ctypes.c_int)]
 
 
+WGRAD_MAX_JOBS = 48
+
+
+class WgradJob(ctypes.Structure):
+    """hyres_wgrad_job: one deferred split-K slab reduce (include/hyres_hip.h)."""
+    _fields_ = [("slab", ctypes.c_void_p), ("dst", ctypes.c_void_p)] + [
+        (n, ctypes.c_int) for n in ("nsplit", "ntaps", "M", "N", "sm", "sn", "st", "accumulate", "lanes",
+                                    "reserved")]
+
+
 _P = ctypes.c_void_p
 _I = ctypes.c_int
 _LL = ctypes.c_longlong
@@ -90,6 +100,9 @@ _SIGS = {
     "hyres_wgrad_desc_deconv2d": (_I, [ctypes.POINTER(WgradDesc)] + [_I] * 9),
     "hyres_wgrad_workspace_bytes": (_LL, [ctypes.POINTER(WgradDesc)]),
     "hyres_conv_wgrad": (_I, [ctypes.POINTER(WgradDesc), _P, _P, _P, _P, _P, _LL, _P]),
+    "hyres_conv_wgrad_deferred": (_I, [ctypes.POINTER(WgradDesc), _P, _P, _P, _P, _P, _LL, ctypes.POINTER(WgradJob),
+                                       ctypes.POINTER(ctypes.c_int), _P]),
+    "hyres_wgrad_reduce_jobs": (_I, [ctypes.POINTER(WgradJob), _I, _P]),
     "hyres_colsum": (_I, [_P, _I, _I, _I, _P, _I, _P, _LL, _P]),
     "hyres_colsum_workspace_bytes": (_LL, [_I, _I]),
     "hyres_nchw_to_nhwc": (_I, [_P, _P, _I, _I, _I, _I, _I, _P]),

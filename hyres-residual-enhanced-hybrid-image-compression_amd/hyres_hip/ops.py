@@ -218,6 +218,7 @@ class Tape:
         for fn in reversed(self.ops):
             fn()
         self.ops.clear()
+        WgradBatch.flush()  # deferred weight-gradient reduces of the main stream
         SideStream.join()  # side-stream weight gradients complete before anyone reads .grad
 
 
@@ -238,6 +239,7 @@ class GradReady:
         ls = list(cls.listeners)
 
         def fire():
+            WgradBatch.flush()  # this segment's weight gradients final before the listeners act
             for f in ls:
                 f(name)
 
@@ -639,10 +641,82 @@ class SideStream:
         cls.used = False
 
 
+class WgradBatch:
+    """Deferred split-K reduces of the weight gradients (round 3, HYRES_WGRAD_DEFER=0 turns it off).
+
+    A weight gradient is a GEMM over the batch's pixels split into [nsplit][taps][M][N] partial slabs; the
+    per-layer path launches one small deterministic reduce per layer (~130 per C2 step, 8-40 us each, mostly
+    ramp and tail). Here each layer launches only its GEMM into a slab of its own, and the reduces of every
+    layer issued on a stream run as ONE ``hyres_wgrad_reduce_jobs`` launch (bit-identical results: same split
+    plan and per-output summation order) when the stream's gradients must be final: at a GradReady marker
+    (before the all-reduce listeners), when a branch stream is left, at the end of the tape backward, when a
+    new job would write a destination a pending job writes, or when HYRES_WGRAD_MAX_JOBS are pending."""
+
+    enabled = os.environ.get("HYRES_WGRAD_DEFER", "1") == "1"
+    _pending = {}  # stream handle -> {"jobs": [WgradJob], "keep": [tensors], "ranges": [(lo, hi)]}
+
+    @classmethod
+    def _entry(cls, handle: int) -> dict:
+        ent = cls._pending.get(handle)
+        if ent is None:
+            ent = {"jobs": [], "keep": [], "ranges": []}
+            cls._pending[handle] = ent
+        return ent
+
+    @classmethod
+    def launch(cls, desc: L.WgradDesc, p_ptr: int, q_ptr: int, dst: torch.Tensor, device,
+               dbias: Optional[torch.Tensor]) -> None:
+        lib = L.load()
+        nbytes = int(lib.hyres_wgrad_workspace_bytes(ctypes.byref(desc)))
+        stream = L.stream()
+        ent = cls._entry(int(stream.value or 0))
+        outs = [(dst.data_ptr(), dst.data_ptr() + 4 * dst.numel())]
+        if dbias is not None:
+            outs.append((dbias.data_ptr(), dbias.data_ptr() + 4 * dbias.numel()))
+        if any(lo < h and l < hi for lo, hi in outs for l, h in ent["ranges"]) or \
+                len(ent["jobs"]) + 2 > L.WGRAD_MAX_JOBS:
+            cls._flush_entry(ent, stream)
+        ws = torch.empty((max(nbytes, 16),), dtype=torch.uint8, device=device)
+        jobs = (L.WgradJob * 2)()
+        nj = ctypes.c_int(0)
+        L.call("hyres_conv_wgrad_deferred", ctypes.byref(desc), p_ptr, q_ptr, dst.data_ptr(),
+               None if dbias is None else dbias.data_ptr(), ws.data_ptr(), ws.numel(), jobs, ctypes.byref(nj),
+               stream)
+        if nj.value:
+            ent["jobs"].extend(jobs[i] for i in range(nj.value))
+            ent["keep"].append(ws)
+            ent["ranges"].extend(outs)
+
+    @classmethod
+    def _flush_entry(cls, ent: dict, stream) -> None:
+        if ent["jobs"]:
+            arr = (L.WgradJob * len(ent["jobs"]))(*ent["jobs"])
+            L.call("hyres_wgrad_reduce_jobs", arr, len(ent["jobs"]), stream)
+        ent["jobs"].clear()
+        ent["keep"].clear()  # stream-ordered: the caching allocator reuses the slabs after the reduce
+        ent["ranges"].clear()
+
+    @classmethod
+    def flush(cls) -> None:
+        """Run the current stream's pending reduces (its weight gradients are final after this, in stream
+        order)."""
+        if not cls._pending:
+            return
+        stream = L.stream()
+        ent = cls._pending.get(int(stream.value or 0))
+        if ent is not None and ent["jobs"]:
+            cls._flush_entry(ent, stream)
+
+    @classmethod
+    def pending(cls) -> int:
+        return sum(len(e["jobs"]) for e in cls._pending.values())
+
+
 def _wgrad(desc: L.WgradDesc, p_ptr: int, q_ptr: int, dst: torch.Tensor, device,
-           dbias: Optional[torch.Tensor] = None, keep=(), side: bool = False) -> None:
+           dbias: Optional[torch.Tensor] = None, keep=(), side: bool = False, defer: bool = True) -> None:
     """Weight gradient (+ the bias gradient = column sums of P when ``dbias`` is given, conv2d only).
-    ``side``: run on the side stream (``keep`` = tensors whose memory the kernels read)."""
+    ``side``: run on the side stream (``keep`` = tensors whose memory the kernels read). ``defer``: the
+    split-K reduce may be batched (WgradBatch); False when a kernel of this backward reads ``dst``."""
     side = side and SideStream.enabled and device.type == "cuda"
     if side:
         main = torch.cuda.current_stream(device)
@@ -653,6 +727,8 @@ def _wgrad(desc: L.WgradDesc, p_ptr: int, q_ptr: int, dst: torch.Tensor, device,
         SideStream.used = True
         with torch.cuda.stream(st):
             _wgrad_launch(desc, p_ptr, q_ptr, dst, device, dbias, slot=2)
+    elif defer and WgradBatch.enabled and device.type == "cuda" and not (KernelTimer.enabled and KernelTimer.all_convs):
+        WgradBatch.launch(desc, p_ptr, q_ptr, dst, device, dbias)
     else:
         _wgrad_launch(desc, p_ptr, q_ptr, dst, device, dbias, slot=7)
 
@@ -892,7 +968,7 @@ def gdn(tape: Optional[Tape], x: Node, beta: torch.Tensor, gamma: torch.Tensor, 
             d.accumulate = 0
             d.f16_operands = f16 * AMP_WGRAD_F16
             d.io_f16 = 2 if x.half else 0
-            _wgrad(d, dn.data_ptr(), x.ptr(), dgp, dev)
+            _wgrad(d, dn.data_ptr(), x.ptr(), dgp, dev, defer=False)  # read by the reparam backward below
             dbp = _empty((C,), dev)
             _colsum_into(dn, y.P, C, C, dbp, acc=0)
             L.call("hyres_gdn_reparam_bwd", beta.data_ptr(), gamma.data_ptr(), dbp.data_ptr(), dgp.data_ptr(),
@@ -1005,6 +1081,7 @@ def run_branches(tape: Optional[Tape], x: Node, fns) -> list:
         cell = {}
         if tape is not None:
             def leave(cell=cell):
+                WgradBatch.flush()  # the branch's weight gradients, before its stream is joined
                 torch.cuda.set_stream(cell["prev"])
             tape.push(leave)
         torch.cuda.set_stream(st)

@@ -197,6 +197,29 @@ long long hyres_wgrad_workspace_bytes(const hyres_wgrad_desc* d);
 int hyres_conv_wgrad(const hyres_wgrad_desc* d, const float* p, const float* q, float* dst,
                      float* dbias, void* workspace, long long ws_bytes, hyres_stream_t s);
 
+/* Deferred split-K reduce (same reference operation as hyres_conv_wgrad: the weight / bias gradient of
+ * one conv in loss.backward(), src/utils/engine.py:63 via models/checkerboard.py:35-88). A weight
+ * gradient is a GEMM over the batch's pixels, split over pixel ranges into [nsplit][ntaps][M][N]
+ * partial slabs; hyres_conv_wgrad reduces them with one launch per layer. The deferred form launches
+ * only the GEMM kernel and returns the reduce as up to two jobs (weight, then bias); the caller keeps
+ * the workspace untouched and the destinations unread until hyres_wgrad_reduce_jobs has run them on the
+ * same stream, where one launch reduces up to HYRES_WGRAD_MAX_JOBS jobs (a gradient segment of many
+ * layers). Jobs of one launch must not write overlapping destinations. The result is bit-identical to
+ * hyres_conv_wgrad's (same split plan, same per-output summation order). */
+#define HYRES_WGRAD_MAX_JOBS 48
+typedef struct hyres_wgrad_job {
+    const float* slab;   /* [nsplit][ntaps][M][N] partials in the workspace */
+    float* dst;          /* dst[m*sm + n*sn + t*st] (+)= sum over the nsplit partials */
+    int nsplit, ntaps, M, N;
+    int sm, sn, st, accumulate;
+    int lanes;           /* reduce layout the launcher chose (4, 8 or 16): fixes the summation order */
+    int reserved;
+} hyres_wgrad_job;
+int hyres_conv_wgrad_deferred(const hyres_wgrad_desc* d, const float* p, const float* q, float* dst,
+                              float* dbias, void* workspace, long long ws_bytes, hyres_wgrad_job* jobs,
+                              int* njobs, hyres_stream_t s);
+int hyres_wgrad_reduce_jobs(const hyres_wgrad_job* jobs, int n, hyres_stream_t s);
+
 /* column sums over pixels: dst[c] (+)= sum_p x[p*ld + c]  (bias gradients) */
 int hyres_colsum(const float* x, int P, int C, int ld, float* dst, int accumulate, void* workspace,
                  long long ws_bytes, hyres_stream_t s);
