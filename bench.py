@@ -197,7 +197,8 @@ MI355X_F16_PEAK_TFLOPS = 2500.0  # dense f16 MFMA (MI355X_MICROARCH.md), no spar
 def amp_leg(net, opt, aux_opt, crit, x, jpeg, jpeg_bpp, args):
     """train.sh's actual configuration (--mixed-precision, src/utils/engine.py:23-82): the C2 step under
     torch.autocast(float16) — every conv / deconv / GDN contraction and its input-gradient on the f16 MFMA
-    (v_mfma_f32_32x32x16_f16, fp16 operands, fp32 accumulation and fp32 activations/gradients in HBM) —
+    (v_mfma_f32_32x32x16_f16, fp16 operands, fp32 accumulation; the f16_region's activations stored fp16 in
+    HBM as autocast's conv outputs are, activation gradients fp32) —
     with the device GradScaler (scaled loss, unscale-before-clip, skip on inf/NaN, backoff/growth), as a HIP
     graph.  Reported beside the fp32 headline; dtype "f16-amp"."""
     from hyres_hip.graphs import CapturedStep

@@ -521,11 +521,17 @@ def conv_flops(g: L.ConvGeom) -> float:
 
 def conv_bytes(g: L.ConvGeom, e: L.Epilogue) -> float:
     """Algorithmic HBM bytes: input read once, weights once, output written (read too if accumulating),
-    residual / aux operands read once."""
+    residual / aux operands read once — each at its storage width (``io_f16``: fp16 X; fp16 Y with its
+    res / aux0 / out2 operands; fp16 saved activations aux0 / aux2 of a backward conv)."""
     px_in = g.B * g.Hi * g.Wi
     px_out = g.B * g.Hq * g.Wq * g.nphase
-    b = 4.0 * (px_in * g.Ci + g.ntaps * g.Ci * g.Co + px_out * g.Co * (2 if e.accumulate else 1))
-    b += 4.0 * px_out * g.Co * sum(1 for p in (e.res, e.aux0, e.aux1, e.aux2, e.out2) if p)
+    io = int(e.io_f16)
+    xw = 2.0 if io & L.IO_X16 else 4.0
+    yw = 2.0 if io & L.IO_Y16 else 4.0
+    auxw = 2.0 if io & (L.IO_Y16 | L.IO_AUX16) else 4.0
+    b = xw * px_in * g.Ci + 4.0 * g.ntaps * g.Ci * g.Co + yw * px_out * g.Co * (2 if e.accumulate else 1)
+    b += px_out * g.Co * (yw * sum(1 for p in (e.res, e.out2) if p) + auxw * (1 if e.aux0 else 0)
+                          + 4.0 * (1 if e.aux1 else 0) + (auxw if io & L.IO_AUX16 else 4.0) * (1 if e.aux2 else 0))
     return b
 
 
@@ -748,7 +754,8 @@ def _wgrad_launch(desc, p_ptr, q_ptr, dst, device, dbias, slot):
         d = desc
         q = d.B * d.Hq * d.Wq
         flops = 2.0 * q * d.ntaps * d.M * d.N
-        nbytes_alg = 4.0 * (q * d.M + d.B * d.Hqq * d.Wqq * d.N + d.ntaps * d.M * d.N)
+        nbytes_alg = ((2.0 if d.io_f16 & 1 else 4.0) * q * d.M + (2.0 if d.io_f16 & 2 else 4.0) * d.B * d.Hqq * d.Wqq * d.N
+                      + 4.0 * d.ntaps * d.M * d.N)
         name = (f"WGRAD B{d.B} P {d.Hq}x{d.Wq}x{d.M} Q {d.Hqq}x{d.Wqq}x{d.N} taps{d.ntaps} sq{d.sq}"
                 f"{' sqr' if d.square_q else ''}")
         KernelTimer.table.append((name, s0, s1, flops, nbytes_alg))
