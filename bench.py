@@ -97,7 +97,9 @@ def cpu_baseline(args, budget_s):
                       f"itself cannot run here (compressai absent)"}
 
 
-PMC_TRAFFIC = os.path.join(REPO, "profiles", os.environ.get("HYRES_PMC_TRAFFIC", "r3_v2_pmc_traffic.json"))  # scripts/profile_round.sh r3_v2
+# scripts/profile_round.sh r3z: the fp32 line's dominant kernel, and the AMP leg's dominant kernel from the same passes
+PMC_TRAFFIC = os.path.join(REPO, "profiles", os.environ.get("HYRES_PMC_TRAFFIC", "r3z_pmc_traffic.json"))
+PMC_TRAFFIC_AMP = os.path.join(REPO, "profiles", os.environ.get("HYRES_PMC_TRAFFIC_AMP", "r3z_pmc_traffic_amp.json"))
 EAGER_TIMED = 3  # eager steps behind the live per-launch roofline timing
 
 
@@ -121,12 +123,12 @@ def kernel_label(kernel):
     return "implicit-GEMM conv, fp32 MFMA, fused epilogue"
 
 
-def traffic_bytes_per_launch(kernel):
+def traffic_bytes_per_launch(kernel, path=None):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC passes of this same
     command (scripts/pmc_traffic.py: 2 x FETCH_SIZE + WRITE_SIZE, separate passes, gfx950 FETCH_SIZE
     correction); None when that summary is absent or was collected for another kernel."""
     try:
-        with open(PMC_TRAFFIC) as f:
+        with open(path or PMC_TRAFFIC) as f:
             d = json.load(f)
         if kernel is None or kernel not in d["kernel"]:
             return None
@@ -247,11 +249,18 @@ def amp_leg(net, opt, aux_opt, crit, x, jpeg, jpeg_bpp, args):
     del cap
     return {"dtype": "f16-amp", "value": round(B * H * W / ms / 1e3, 4), "unit": "Mpixels/s", "ms_per_step": round(ms, 3),
             "loss": loss, "loss_scale": scaler.get_scale(),
-            "roofline": roofline_of(ks, MI355X_F16_PEAK_TFLOPS, F16_RIDGE),
+            "roofline": with_traffic(roofline_of(ks, MI355X_F16_PEAK_TFLOPS, F16_RIDGE), ks["kernel"]),
             "roofline_f16_mfma_kernel": roofline_of(ks_mfma, MI355X_F16_PEAK_TFLOPS, F16_RIDGE),
             "note": "fp16 operands / fp32 accumulation (f16 MFMA; the HBM-bound 1x1 layers on the fp32 MFMA with "
                     "fp16-rounded operands); weight gradients "
                     + ("f16" if os.environ.get("HYRES_AMP_WGRAD_F16", "1") == "1" else "fp32")}
+
+
+def with_traffic(r, kernel):
+    """The AMP leg's roofline entry with its PMC-measured HBM bytes per launch (profiles/r3z_pmc_traffic_amp.json)."""
+    if r is not None:
+        r["traffic"] = traffic_bytes_per_launch(kernel, PMC_TRAFFIC_AMP)
+    return r
 
 
 MI355X_HBM_PEAK_GBS = 8000.0
