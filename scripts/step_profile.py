@@ -21,6 +21,8 @@ def main():
     ap.add_argument("--batch", type=int, default=16)
     ap.add_argument("--size", type=int, default=256)
     ap.add_argument("--eval", action="store_true", help="eval forward (encode+decode) instead of a train step")
+    ap.add_argument("--marker", action="store_true",
+                    help="a torch spin kernel between the warm-up and the timed steps (scripts/step_traffic.py)")
     args = ap.parse_args()
     from hyres_hip.graphs import CapturedStep
     from hyres_hip.loss import RateDistortionLoss
@@ -64,6 +66,9 @@ def main():
     for _ in range(2):
         step()
     torch.cuda.synchronize()
+    if args.marker:
+        torch.cuda._sleep(1000)
+        torch.cuda.synchronize()
     t0 = time.time()
     for _ in range(args.steps):
         step()
