@@ -125,13 +125,15 @@ __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<floa
 // float4 variant of epi_store for channels n..n+3 (all operands 16B aligned).
 template <bool H = false>
 __device__ __forceinline__ void epi_store4(const hyres_epilogue& e, float* y, int ldy, long long pix, int n, float4 v,
-                                           float slope, const float4* rpre = nullptr) {
+                                           float slope, bool use_pre = false,
+                                           float4 rpre = make_float4(0.f, 0.f, 0.f, 0.f)) {
     float o[4] = {v.x, v.y, v.z, v.w};
     switch (e.kind) {
         case HYRES_EPI_BIAS: {
             if (e.bias) { const float4 b = ld4(e.bias + n); o[0] += b.x; o[1] += b.y; o[2] += b.z; o[3] += b.w; }
-            if (e.res) {  // rpre: the residual already loaded by the caller (same value, same order)
-                const float4 r = rpre ? *rpre : ldv4<H>(e.res, pix * e.ldres + n);
+            if (e.res) {  // rpre: the residual already loaded by the caller (same value, same order; passed by value:
+                          // a pointer into the caller's register array put that array in scratch memory)
+                const float4 r = use_pre ? rpre : ldv4<H>(e.res, pix * e.ldres + n);
                 o[0] += r.x; o[1] += r.y; o[2] += r.z; o[3] += r.w;
             }
             if (e.out2) stv4<H>(e.out2, pix * e.ldo2 + n, make_float4(o[0], o[1], o[2], o[3]));
@@ -975,7 +977,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3_wres_f16_kernel(const ConvArgs
                         const int n = n0 + 32 * wn + 8 * qd + 4 * lh;
                         const float4 v = make_float4(acc[at][4 * qd], acc[at][4 * qd + 1], acc[at][4 * qd + 2],
                                                      acc[at][4 * qd + 3]);
-                        epi_store4<YH>(a.e, a.y, g.ldy, pix, n, v, slope, pre_res ? &rres[at][qd] : nullptr);
+                        epi_store4<YH>(a.e, a.y, g.ldy, pix, n, v, slope, pre_res, rres[at][qd]);
                     }
                 }
 #pragma unroll
