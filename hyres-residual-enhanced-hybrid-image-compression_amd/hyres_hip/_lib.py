@@ -13,7 +13,8 @@ from typing import Optional
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libhyres_hip.so")
+# HYRES_LIB_PATH: an alternative build for A/B timing runs (scripts only; the default is the in-tree library)
+LIB_PATH = os.environ.get("HYRES_LIB_PATH") or os.path.join(HERE, "libhyres_hip.so")
 
 MAX_TAPS = 49
 WPREP_CONV, WPREP_CONV_DGRAD, WPREP_DECONV, WPREP_DECONV_DGRAD = 0, 1, 2, 3
