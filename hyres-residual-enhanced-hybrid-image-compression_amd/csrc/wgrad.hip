@@ -1520,11 +1520,14 @@ static WgradPlan wgrad_plan(const hyres_wgrad_desc* d) {
         p.TMc = p.TNc = 1; p.WMc = p.WNc = 2;
         p.BM = p.BN = 64;
         p.mtiles = ceil_div(d->M, 64); p.ntiles = ceil_div(d->N, 64);
-        // 3x3: one kernel row of 3 taps per block (default), or all 9 taps per block (HYRES_WGRAD_HALO_ROWS=3: one
-        // 3-row halo per chunk) — rows of 3 give 3x the tiles, so a third of the pixel splits and of the split slab
-        // for the same grid. AMP step 21.56 -> 21.34 ms, fp32 42.82 -> 42.68 ms over 3 alternating repeats each
-        // (profiles/r3r_rows_ab.txt, r3y_rows_fp32_ab.txt)
-        static const int rows = env_int("HYRES_WGRAD_HALO_ROWS", 1);
+        // 3x3: one kernel row of 3 taps per block, or all 9 taps per block (one 3-row halo per chunk) — rows of 3
+        // give 3x the tiles, so a third of the pixel splits and of the split slab for the same grid. Default: rows
+        // for dilation 1 (AMP step 21.56 -> 21.34 ms, fp32 42.82 -> 42.68 ms over 3 alternating repeats each;
+        // 128^2 fp32 kernel 235 -> 208 us), all 9 taps for the dilated 3x3s (256^2: 678 vs 797 us fp32, 152 vs 219 us
+        // f16: their halo rows are 2 apart, so a row group re-stages most of the chunk). HYRES_WGRAD_HALO_ROWS = 1 / 3
+        // forces one (profiles/r3r_rows_ab.txt, r3y_rows_fp32_ab.txt)
+        static const int rows_env = env_int("HYRES_WGRAD_HALO_ROWS", 0);
+        const int rows = rows_env ? rows_env : (hdil == 2 ? 3 : 1);
         p.NT = p.hk == 3 ? (rows == 1 ? 3 : 9) : 5;
         p.ngroups = d->ntaps / p.NT;
     }
