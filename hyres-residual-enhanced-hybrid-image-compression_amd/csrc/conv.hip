@@ -627,13 +627,15 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
 
 // waves per SIMD the register allocation must allow: 4 (<= 128 VGPRs: 4 blocks per CU) for the vector-load tiles with
 // at most two accumulator tiles per wave — left to itself the compiler gave the 64x128 / 128x64 tiles 144 registers
-// (3 blocks per CU); with the bound they fit in 109-127 with no spill. The scalar-load path (MODE 2, the 3-channel
-// image side) would spill: the compiler's choice there. -DHYRES_CONV_WPE4=0 builds the unbounded variant (A/B).
+// (3 blocks per CU); with the bound they fit in 109-127 with no spill — and 3 (<= 168) for the 128x128 tiles (176-212
+// -> 142-154, 3 blocks per CU instead of 2; AMP step -0.5 %, fp32 neutral: profiles/r3aa_conv_wpe3_ab.txt). The
+// scalar-load path (MODE 2, the 3-channel image side) would spill: the compiler's choice there. -DHYRES_CONV_WPE4=0
+// builds the unbounded variant (A/B).
 #ifndef HYRES_CONV_WPE4
 #define HYRES_CONV_WPE4 1
 #endif
 template <int TM, int TN, int MODE>
-constexpr int conv_wpe() { return (HYRES_CONV_WPE4 && TM * TN <= 2 && MODE != 2) ? 4 : 1; }
+constexpr int conv_wpe() { return (HYRES_CONV_WPE4 && MODE != 2) ? (TM * TN <= 2 ? 4 : 3) : 1; }
 
 template <int TM, int TN, int WAVES_M, int WAVES_N, int MODE, bool SPLITK, bool F16 = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(conv_wpe<TM, TN, MODE>())))
