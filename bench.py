@@ -148,8 +148,13 @@ def eval_legs(net, x, jpeg, jpeg_bpp, args, reps=20):
     xk = torch.randint(0, 256, (1, 3, 512, 768), generator=g).float() / 255.0
     jk, bk = net.jpeg(xk)
     dev = x.device
-    for tag, xe, je, be in (("bs%d_%dx%d" % (x.shape[0], x.shape[2], x.shape[3]), x, jpeg, jpeg_bpp),
-                            ("kodak_1x768x512", xk.to(dev), jk.to(dev), bk)):
+    # C3's batch (bs=32): the bench batch twice, the second half mirrored (synthetic timing input)
+    x2 = torch.cat([x, torch.flip(x, dims=[3])]).contiguous()
+    j2 = torch.cat([jpeg, torch.flip(jpeg, dims=[3])]).contiguous()
+    legs = (("bs%d_%dx%d" % (x.shape[0], x.shape[2], x.shape[3]), x, jpeg, jpeg_bpp),
+            ("bs%d_%dx%d" % (x2.shape[0], x.shape[2], x.shape[3]), x2, j2, jpeg_bpp),
+            ("kodak_1x768x512", xk.to(dev), jk.to(dev), bk))
+    for tag, xe, je, be in legs:
         cap = CapturedStep(net, xe, je, be)
         torch.cuda.synchronize()
         t0 = time.time()
@@ -171,9 +176,7 @@ def eval_legs(net, x, jpeg, jpeg_bpp, args, reps=20):
         del cap
     # configs[4] precision: inference under torch.autocast(float16) -> fp16-operand f16 MFMA convs
     with torch.autocast("cuda", dtype=torch.float16):
-        for tag, xe, je, be in (("kodak_1x768x512_autocast_f16", xk.to(dev), jk.to(dev), bk),
-                                ("bs%d_%dx%d_autocast_f16" % (x.shape[0], x.shape[2], x.shape[3]), x, jpeg,
-                                 jpeg_bpp)):
+        for tag, xe, je, be in [(t + "_autocast_f16", a, b, c) for t, a, b, c in legs]:
             cap = CapturedStep(net, xe, je, be)
             torch.cuda.synchronize()
             t0 = time.time()
@@ -286,6 +289,26 @@ def roofline_of(ks, peak_tflops, ridge):
         base.update(bound="hbm", achieved=round(ach, 1), peak=MI355X_HBM_PEAK_GBS, unit="GB/s",
                     frac=round(ach / MI355X_HBM_PEAK_GBS, 4))
     return base
+
+
+def family_rooflines(by_variant, steps, peak_tflops, ridge, top=6):
+    """Every conv kernel family (template instantiation) of the live step on its own roofline — the dominant
+    kernel is one line; these are the rest of the conv GPU time. Per family: launches and GPU ms per step, the
+    achieved FLOP and algorithmic-byte rates over its HIP-event time, its mean intensity, and the fraction of
+    the roof that bounds it (MFMA above the ridge, HBM below). Largest ``top`` families by time."""
+    out = []
+    for k, (ms, flops, nbytes, n) in sorted(by_variant.items(), key=lambda kv: -kv[1][0])[:top]:
+        if ms <= 0:
+            continue
+        sec = ms * 1e-3
+        tf, gbs = flops / sec / 1e12, nbytes / sec / 1e9
+        inten = flops / max(nbytes, 1.0)
+        bound = "mfma" if inten >= ridge else "hbm"
+        out.append({"kernel": k, "launches_per_step": round(n / steps, 1), "ms_per_step": round(ms / steps, 3),
+                    "avg_launch_us": round(1000.0 * ms / n, 2), "tflops": round(tf, 2), "gbs": round(gbs, 1),
+                    "intensity_flop_per_byte": round(inten, 2), "bound": bound,
+                    "frac": round(tf / peak_tflops if bound == "mfma" else gbs / MI355X_HBM_PEAK_GBS, 4)})
+    return out
 
 
 def host_jpeg_legs(net, step_eager_cpu, x_cpu, reps=5, step_graph_cpu=None):
@@ -448,12 +471,12 @@ def main():
     # xGMI). HYRES_DIST_OVERLAP=1 (or --no-graph) selects the eager overlapped path.
     dist_mode = None
     if dist:
-        # default "graph+overlap": the captured step records an external event at each backward-progress
-        # marker and each gradient segment's RCCL all-reduce starts on a communication stream as soon as
-        # its event fires inside the replay (hyres_hip.graphs / ddp.FlatGradReducer.reduce_graphed);
-        # HYRES_DIST_MODE=graph+allreduce reduces after the replay; eager-overlap = the eager step
+        # default "graph+allreduce": replay, then the flat gradient in 32 MB buckets. "graph+overlap"
+        # (HYRES_DIST_MODE) starts each segment's all-reduce from an external event the replay records at its
+        # backward-progress marker (ddp.FlatGradReducer.reduce_graphed) — opt-in only: its one multi-rank
+        # rehearsal ran 9x slower than graph+allreduce; eager-overlap = the eager step
         overlap = args.no_graph or os.environ.get("HYRES_DIST_OVERLAP") == "1"
-        dist_mode = "eager-overlap" if overlap else os.environ.get("HYRES_DIST_MODE", "graph+overlap")
+        dist_mode = "eager-overlap" if overlap else os.environ.get("HYRES_DIST_MODE", "graph+allreduce")
         assert dist_mode in ("eager-overlap", "graph+overlap", "graph+allreduce"), dist_mode
     if dist:
         # RCCL all-reduce of refine / g_s / hyperprior gradient segments launched from backward-progress
@@ -562,6 +585,8 @@ def main():
         r = O.KernelTimer.summary()
         r["launches"] //= EAGER_TIMED
         r["by_variant_ms"] = {k: round(v / EAGER_TIMED, 3) for k, v in r.get("by_variant_ms", {}).items()}
+        r["families"] = family_rooflines(r.get("by_variant", {}), EAGER_TIMED, MI355X_FP32_PEAK_TFLOPS,
+                                         MI355X_FP32_PEAK_TFLOPS * 1e12 / (MI355X_HBM_PEAK_GBS * 1e9))
         return r
 
     ks = timed_steps()
@@ -604,8 +629,12 @@ def main():
         "metric_definition": ("BASELINE.json's metric, measured on configs[1] (the workload it is quoted on): one "
                               "step = forward (g_a 'encode' + hyperprior + checkerboard context + g_s 'decode' + "
                               "MultiScaleRefine) + RD-loss backward + clip + Adam + aux Adam at bs=16 per GPU, "
-                              "device-only (host JPEG precomputed); the eval-only encode+decode rate is in "
-                              "'eval', the with-host-JPEG rates in 'host_jpeg'"),
+                              "device-only (host JPEG precomputed). This TRAIN-STEP rate is stricter than "
+                              "SURVEY §8d's 'encode+decode' = eval-forward rate, which is reported as "
+                              "'encode_decode_eval' (eval.bs16_256x256; C3's bs=32 in eval.bs32_256x256); the "
+                              "with-host-JPEG rates are in 'host_jpeg'"),
+        "encode_decode_eval": None if not evals else {
+            k: evals[k]["mpix_s"] for k in evals if k.startswith("bs") and "mpix_s" in evals[k]},
         "value": round(value, 4),
         "unit": "Mpixels/s",
         "n_gpus": world,
@@ -631,7 +660,8 @@ def main():
                      "achieved_isolated": None if iso is None else round(iso, 3),
                      "frac_isolated": None if iso is None else round(iso / MI355X_FP32_PEAK_TFLOPS, 4),
                      "avg_launch_us_isolated": round(ks_iso["avg_us"], 2),
-                     "ms_by_variant": ks.get("by_variant_ms")},
+                     "ms_by_variant": ks.get("by_variant_ms"),
+                     "families": ks.get("families")},
         "graph": graphed is not None,
         "dist_mode": dist_mode,
         "eval": evals,

@@ -858,8 +858,10 @@ __global__ __launch_bounds__(512, 2) void conv3x3_wres_f16_kernel(const ConvArgs
     const int nrt = (g.Ho + HALO_R - 1) / HALO_R, nct = g.Wo / HALO_TW;
     // block -> (output-channel group, share of the tiles): the blocks of one XCD (b % 8) take one contiguous
     // range of tiles, interleaved, so that vertically adjacent tiles (two shared halo rows) run together on it
+    // group-major block order with nb % 8 == 0 (wres_blocks): hardware XCD = blockIdx.x % 8 = bg % 8, so the
+    // blocks of every channel group that walk the same tiles (same bg) sit on one XCD and share its L2 halos
     const int nb = gridDim.x / groups;  // blocks per channel group
-    const int grp = blockIdx.x % groups, bg = blockIdx.x / groups;
+    const int grp = blockIdx.x / nb, bg = blockIdx.x - grp * nb;
     const int n0 = grp * 64;
     const int xcd = bg & 7, nx = (nb + 7 - xcd) >> 3, jx = bg >> 3;  // blocks of this XCD, index among them
     const int q = ntiles >> 3, rr8 = ntiles & 7;
@@ -1037,7 +1039,7 @@ constexpr int WF_LDS_H = HALO_NPX * WF_PK;
 // resources — an absent operand gets an empty resource, so its loads return 0 with no branch — and consumed only
 // after that chunk's 144 MFMAs. The generic epi_store4 issued each load behind its own branch and waited on it
 // (~8 serialised HBM round trips per tile; +14 % on a 3x3 with a residual).
-__global__ __launch_bounds__(512, 2) void conv3x3_wres_f32_kernel(const ConvArgs a, int ntiles, int groups, int ablate) {
+__global__ __launch_bounds__(512, 2) void conv3x3_wres_f32_kernel(const ConvArgs a, int ntiles, int groups) {
     __shared__ __attribute__((aligned(16))) float lds[WF_LDS_W + WF_LDS_H];
     __shared__ int2 tapoff[9];
     float* const Ws = lds;
@@ -1045,8 +1047,8 @@ __global__ __launch_bounds__(512, 2) void conv3x3_wres_f32_kernel(const ConvArgs
     const hyres_conv_geom& g = a.g;
     const int tid = threadIdx.x;
     const int nrt = (g.Ho + HALO_R - 1) / HALO_R, nct = g.Wo / HALO_TW;
-    const int nb = gridDim.x / groups;
-    const int grp = blockIdx.x % groups, bg = blockIdx.x / groups;
+    const int nb = gridDim.x / groups;  // group-major, nb % 8 == 0: see conv3x3_wres_f16_kernel
+    const int grp = blockIdx.x / nb, bg = blockIdx.x - grp * nb;
     const int n0 = grp * 32;
     const int xcd = bg & 7, nx = (nb + 7 - xcd) >> 3, jx = bg >> 3;
     const int q = ntiles >> 3, rr8 = ntiles & 7;
@@ -1136,7 +1138,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3_wres_f32_kernel(const ConvArgs
                 eold[qd] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r_old, oy, 0, 0));
             }
         }
-        if (s + 1 < steps && !(ablate & 4)) hload(s + 1);
+        if (s + 1 < steps) hload(s + 1);
         const float* Wc = Ws + c * 9 * 32 * WF_PK;
 #pragma unroll
         for (int t = 0; t < 9; ++t) {
@@ -1154,7 +1156,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3_wres_f32_kernel(const ConvArgs
             }
         }
         if (c == 1) {
-            if (i < g.Ho && !(ablate & 1)) {
+            if (i < g.Ho) {
 #pragma unroll
                 for (int qd = 0; qd < 4; ++qd) {
                     const int n = n0 + 8 * qd + 4 * lh;
@@ -1180,16 +1182,9 @@ __global__ __launch_bounds__(512, 2) void conv3x3_wres_f32_kernel(const ConvArgs
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[r] = 0.f;
         }
-        if (ablate & 2) continue;
         __syncthreads();  // every wave is done with this chunk's halo
         if (s + 1 < steps) hstore();
         __syncthreads();
-    }
-    if (ablate & 1) {  // keep the accumulators live
-        float t = 0.f;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) t += acc[r];
-        if (t == 1.2345f) a.y[0] = t;
     }
 }
 
@@ -1869,13 +1864,10 @@ static int num_cus() {
     return g_cus;
 }
 
-// blocks per output-channel group: one per CU (persistent), or HYRES_WRES_TPB tiles per block — under the
-// concurrent branch streams of the train step a persistent grid cannot move work off CUs that are busy with
-// another kernel, smaller blocks can
-static int wres_blocks(int ntiles, int groups) {
-    static const int tpb = env_int("HYRES_WRES_TPB", 0);
-    if (tpb > 0) return std::max(1, ceil_div(ntiles, tpb));
-    return std::max(1, num_cus() / groups);
+// blocks per output-channel group: one per CU (persistent), a multiple of 8 so that the group-major block order
+// keeps block bg of every group on XCD bg % 8
+static int wres_blocks(int groups) {
+    return std::max(8, (num_cus() / groups) & ~7);
 }
 
 static bool wres16_ok(const hyres_conv_geom* g) {
@@ -1883,14 +1875,14 @@ static bool wres16_ok(const hyres_conv_geom* g) {
     if (!on || g->Ci != 64) return false;
     const long long tiles = (long long)g->B * ((g->Ho + HALO_R - 1) / HALO_R) * (g->Wo / HALO_TW);
     const int groups = g->Co / 64;
-    return tiles >= 2LL * std::max(1, num_cus() / groups) && (long long)g->B * g->Hi * g->Wi * g->ldx * 4 < 0x7FFFFFF0LL;
+    return tiles >= 2LL * wres_blocks(groups) && (long long)g->B * g->Hi * g->Wi * g->ldx * 4 < 0x7FFFFFF0LL;
 }
 
 static int launch_wres16(const ConvArgs& a, hipStream_t st) {
     const hyres_conv_geom& g = a.g;
     const int ntiles = g.B * ((g.Ho + HALO_R - 1) / HALO_R) * (g.Wo / HALO_TW);
     const int groups = g.Co / 64;
-    const int per = wres_blocks(ntiles, groups);
+    const int per = wres_blocks(groups);
     const dim3 grid(per * groups);
     static const int variant = env_int("HYRES_WRES_VARIANT", 1);
     if ((a.e.io_f16 & 3) == 0 && variant == 0) {  // A/B: halo prefetch issued before the residual loads
@@ -1924,18 +1916,15 @@ static bool wres32_ok(const hyres_conv_geom* g, const hyres_epilogue* e) {
         if (g->dh[t] < -1 || g->dh[t] > 1 || g->dw[t] < -1 || g->dw[t] > 1) return false;
     const long long tiles = (long long)g->B * ((g->Ho + HALO_R - 1) / HALO_R) * (g->Wo / HALO_TW);
     const int groups = g->Co / 32;
-    return tiles >= 2LL * std::max(1, num_cus() / groups) && (long long)g->B * g->Hi * g->Wi * g->ldx * 4 < 0x7FFFFFF0LL;
+    return tiles >= 2LL * wres_blocks(groups) && (long long)g->B * g->Hi * g->Wi * g->ldx * 4 < 0x7FFFFFF0LL;
 }
 
 static int launch_wres32(const ConvArgs& a, hipStream_t st) {
     const hyres_conv_geom& g = a.g;
     const int ntiles = g.B * ((g.Ho + HALO_R - 1) / HALO_R) * (g.Wo / HALO_TW);
     const int groups = g.Co / 32;
-    const int per = wres_blocks(ntiles, groups);
-    // HYRES_WRES32_ABLATE (timing experiments only, wrong results): 1 no epilogue, 2 no halo store / barriers,
-    // 4 no halo loads
-    static const int ablate = env_int("HYRES_WRES32_ABLATE", 0);
-    hipLaunchKernelGGL(conv3x3_wres_f32_kernel, dim3(per * groups), dim3(512), 0, st, a, ntiles, groups, ablate);
+    const int per = wres_blocks(groups);
+    hipLaunchKernelGGL(conv3x3_wres_f32_kernel, dim3(per * groups), dim3(512), 0, st, a, ntiles, groups);
     return HY_LAUNCH_CHECK("conv3x3_wres_f32_kernel");
 }
 

@@ -162,6 +162,22 @@ class CapturedStep:
         O.bump_weight_epoch()  # eager calls must not reuse buffers only the graph writes
         torch.cuda.synchronize(dev)
 
+    def close(self) -> None:
+        """Tear down in the only safe order: wait for any replay in flight, destroy the graph (its event-record
+        nodes point at the marker events), THEN release the marker events."""
+        g = getattr(self, "graph", None)
+        if g is not None:
+            torch.cuda.synchronize(self.x.device)
+            g.reset()
+            self.graph = None
+        self.marker_events = []
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 - interpreter shutdown
+            pass
+
     def replay(self, x: Optional[torch.Tensor] = None, jpeg_decoded: Optional[torch.Tensor] = None,
                jpeg_bpp: Optional[float] = None):
         """Run the captured step on the current stream; returns (outputs, loss dict or None) — static

@@ -496,7 +496,8 @@ class KernelTimer:
             groups = groups_all
         return {"kernel": var, "launches": n, "total_ms": ms, "avg_us": 1000.0 * ms / n, "flops": flops,
                 "flops_per_launch": flops / n, "bytes_per_launch": nbytes / n,
-                "by_variant_ms": {k: round(v[0], 3) for k, v in groups.items()}}
+                "by_variant_ms": {k: round(v[0], 3) for k, v in groups.items()},
+                "by_variant": {k: list(v) for k, v in groups.items()}}
 
 
 def conv_variant(g: L.ConvGeom, e: L.Epilogue, splitk: bool) -> str:
@@ -656,16 +657,19 @@ class WgradBatch:
     layer issued on a stream run as ONE ``hyres_wgrad_reduce_jobs`` launch (bit-identical results: same split
     plan and per-output summation order) when the stream's gradients must be final: at a GradReady marker
     (before the all-reduce listeners), when a branch stream is left, at the end of the tape backward, when a
-    new job would write a destination a pending job writes, or when HYRES_WGRAD_MAX_JOBS are pending."""
+    new job would write a destination a pending job writes, when HYRES_WGRAD_MAX_JOBS are pending, or when the
+    pending slabs would exceed ``max_bytes`` (they are caching-allocator blocks that stay alive until the flush,
+    inside a captured graph's pool too: the cap bounds that extra peak memory; scripts/mem_probe.py measures it)."""
 
     enabled = os.environ.get("HYRES_WGRAD_DEFER", "1") == "1"
+    max_bytes = 256 << 20
     _pending = {}  # stream handle -> {"jobs": [WgradJob], "keep": [tensors], "ranges": [(lo, hi)]}
 
     @classmethod
     def _entry(cls, handle: int) -> dict:
         ent = cls._pending.get(handle)
         if ent is None:
-            ent = {"jobs": [], "keep": [], "ranges": []}
+            ent = {"jobs": [], "keep": [], "ranges": [], "bytes": 0}
             cls._pending[handle] = ent
         return ent
 
@@ -680,7 +684,7 @@ class WgradBatch:
         if dbias is not None:
             outs.append((dbias.data_ptr(), dbias.data_ptr() + 4 * dbias.numel()))
         if any(lo < h and l < hi for lo, hi in outs for l, h in ent["ranges"]) or \
-                len(ent["jobs"]) + 2 > L.WGRAD_MAX_JOBS:
+                len(ent["jobs"]) + 2 > L.WGRAD_MAX_JOBS or ent["bytes"] + nbytes > cls.max_bytes:
             cls._flush_entry(ent, stream)
         ws = torch.empty((max(nbytes, 16),), dtype=torch.uint8, device=device)
         jobs = (L.WgradJob * 2)()
@@ -692,6 +696,7 @@ class WgradBatch:
             ent["jobs"].extend(jobs[i] for i in range(nj.value))
             ent["keep"].append(ws)
             ent["ranges"].extend(outs)
+            ent["bytes"] += nbytes
 
     @classmethod
     def _flush_entry(cls, ent: dict, stream) -> None:
@@ -701,6 +706,7 @@ class WgradBatch:
         ent["jobs"].clear()
         ent["keep"].clear()  # stream-ordered: the caching allocator reuses the slabs after the reduce
         ent["ranges"].clear()
+        ent["bytes"] = 0
 
     @classmethod
     def flush(cls) -> None:

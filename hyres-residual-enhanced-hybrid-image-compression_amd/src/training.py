@@ -96,8 +96,10 @@ def main(argv):
         sampler = DistributedSampler(train_dataset, num_replicas=world, rank=rank, shuffle=True)
     train_loader = DataLoader(train_dataset, batch_size=args.batch_size, num_workers=args.num_workers,
                               shuffle=sampler is None, sampler=sampler, pin_memory=False)
+    # DDP: rank r evaluates test images r, r + world, ... (no padding duplicates); test_epoch all-reduces the meters
+    test_shard = list(range(rank, len(test_dataset), world)) if world > 1 else None
     test_loader = DataLoader(test_dataset, batch_size=args.test_batch_size, num_workers=args.num_workers,
-                             shuffle=False, pin_memory=False)
+                             shuffle=False, sampler=test_shard, pin_memory=False)
 
     net = ResidualJPEGCompression(base_model=LightWeightCheckerboard(N=args.N, M=args.M),
                                   jpeg_quality=args.jpeg_quality).to(device)

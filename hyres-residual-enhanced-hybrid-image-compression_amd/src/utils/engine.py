@@ -17,9 +17,13 @@ Differences from the reference, by design:
     (TurboJPEGCompression.prefetch), so the host JPEG stage overlaps the device step;
   * forward + RD loss + backward replay as a HIP graph (hyres_hip.graphs.CapturedStep, one capture per
     batch shape / noisequant / precision, taken on an accumulation boundary); the host JPEG stage, the
-    H2D copies, the gradient all-reduce (each segment started from an event the replay records at its
-    backward-progress marker, as bench.py's N > 1 default), the optimiser and the aux step stay eager; a
-    capture failure on any rank makes every rank run eagerly. HYRES_TRAIN_GRAPH=0 runs every step eagerly (the reference's structure).
+    H2D copies, the gradient all-reduce (after the replay in 32 MB buckets, as bench.py's N > 1 default;
+    HYRES_DIST_MODE=graph+overlap starts each segment from an event the replay records at its
+    backward-progress marker), the optimiser and the aux step stay eager. Every step the ranks agree over a
+    host (gloo) group on the capture key and on capture success, so all ranks replay or all run eagerly and
+    issue the same collectives. HYRES_TRAIN_GRAPH=0 runs every step eagerly (the reference's structure);
+  * under DDP the test epoch is sharded (rank r takes images r, r + world, ...) and the meters' sums and
+    counts are all-reduced, instead of every rank evaluating the whole test set.
 """
 import os
 import time
@@ -63,13 +67,34 @@ class _GraphedStep:
         # loss multiplier inside the graph: 1/accumulation (x the GradScaler's device scale under AMP)
         self.ls = torch.full((1,), 1.0 / accumulation, dtype=torch.float32, device=device)
         self.enabled = os.environ.get("HYRES_TRAIN_GRAPH", "1") == "1" and device.type == "cuda"
+        self.overlap = os.environ.get("HYRES_DIST_MODE", "graph+allreduce") == "graph+overlap"
         self.last = None
+        self._host_group = None
+
+    def _agree(self, key) -> None:
+        """Per-step host check under DDP: every rank must be at the same capture key (same batch shape /
+        noisequant / precision), else a replaying rank and an eager or capturing rank would issue different
+        collectives and hang. Ranks that agree on the key also agree on whether it still needs a capture (the
+        same keys were seen in the same order). One 2-int all-reduce on a gloo group: no device sync."""
+        import torch.distributed as dist
+        if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+            return
+        if self._host_group is None:
+            self._host_group = dist.new_group(backend="gloo") if dist.get_backend() != "gloo" else dist.group.WORLD
+        h = hash(key) & 0x3FFFFFFF  # tuples of ints / bools hash identically in every process
+        t = torch.tensor([h, -h], dtype=torch.int64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self._host_group)
+        if int(t[0]) != h or int(-t[1]) != h:
+            raise RuntimeError(f"DDP ranks reached different graph-capture keys (this rank {key}); every rank must "
+                               "see the same batch shapes (DistributedSampler shards are equal-length)")
 
     def __call__(self, d, noisequant, boundary_start, reducer):
         """Returns the static loss dict of the replayed step, or None (run this step eagerly)."""
         if not self.enabled or d.device.type != "cpu" or not hasattr(self.model, "forward_device"):
             return None
         key = (tuple(d.shape), bool(noisequant), bool(self.amp))
+        if reducer is not None:
+            self._agree(key)
         cap = self.caps.get(key)
         if cap is None and not boundary_start:
             return None  # capturing zeroes the gradients: only where no partial accumulation exists
@@ -88,13 +113,13 @@ class _GraphedStep:
                 cap = CapturedStep(self.model, x, jd, float(bpp), noisequant=noisequant, criterion=self.criterion,
                                    zero_grad=self.zero_grad, amp=self.amp, loss_scale=self.ls,
                                    capture_error_mode="thread_local" if reducer is not None else "global",
-                                   reducer=reducer)
+                                   reducer=reducer if self.overlap else None)
             except Exception as exc:  # noqa: BLE001 - any capture failure: stay correct, run eagerly
                 err = exc
             finally:
                 if reducer is not None:
                     reducer.armed = armed
-            if not _all_ranks_ok(err is None, self.device):
+            if not _all_ranks_ok(err is None, self._host_group):
                 # every rank falls back together: a graphed rank and an eager rank would issue different
                 # collectives (segment markers vs buckets) and hang or mix up the all-reduce
                 print(f"HIP graph capture failed ({err!r} on this rank); training steps run eagerly")
@@ -106,18 +131,20 @@ class _GraphedStep:
         return cap.replay(x, jd, float(bpp))[1]
 
     def reduce(self, reducer):
-        """The boundary all-reduce after a replayed step: each segment's collectives start on the external
-        event the capture recorded at its backward-progress marker (overlapping the rest of the replay)."""
+        """The boundary all-reduce after a replayed step (graph+overlap: each segment's collectives start on
+        the external event the capture recorded at its backward-progress marker; otherwise no events were
+        recorded and the flat gradient is reduced after the replay in buckets)."""
         reducer.reduce_graphed(self.last.marker_events)
 
 
-def _all_ranks_ok(ok: bool, device) -> bool:
+def _all_ranks_ok(ok: bool, group) -> bool:
+    """Capture success agreed by every rank (MIN over the host gloo group)."""
     import torch.distributed as dist
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if group is None or not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return ok
-    flag = torch.tensor([1.0 if ok else 0.0], device=device if dist.get_backend() == "nccl" else "cpu")
-    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-    return bool(flag.item() == 1.0)
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int64)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
+    return bool(flag.item() == 1)
 
 
 def _lookahead(loader):
@@ -230,6 +257,7 @@ def test_epoch(epoch, test_dataloader, model, criterion, save_images=False, save
             if save_images and i < 6 and savepath:
                 _save_components(out_net, d, os.path.join(savepath, "best_recon"), i)
     _drain(pending, meters)
+    _all_reduce_meters(list(meters.values()) + [aux_meter], device)
     print(f"Test epoch {epoch}: Average losses:\tLoss: {meters['loss'].avg:.3f} |"
           f"\tBpp loss: {meters['bpp_loss'].avg:.4f} |\tResidual Bpp: {meters['residual_bpp_loss'].avg:.4f} |"
           f"\ty_Bpp loss: {meters['y_bpp_loss'].avg:.4f} |\tz_Bpp loss: {meters['z_bpp_loss'].avg:.4f} |"
@@ -244,6 +272,20 @@ def test_epoch(epoch, test_dataloader, model, criterion, save_images=False, save
                         meters["residual_bpp_loss"].avg, meters["y_bpp_loss"].avg, meters["z_bpp_loss"].avg,
                         aux_meter.avg])
     return meters["loss"].avg, meters["bpp_loss"].avg, meters["mse_loss"].avg
+
+
+def _all_reduce_meters(meters, device) -> None:
+    """DDP: each rank evaluated its shard of the test set; sum the meters' sums and counts over ranks so every
+    rank reports the mean over all test batches."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return
+    dev = device if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([[float(m.sum), float(m.count)] for m in meters], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    for m, (sm, cnt) in zip(meters, t.cpu().tolist()):
+        m.sum, m.count = sm, int(cnt)
+        m.avg = sm / cnt if cnt else 0.0
 
 
 def _save_components(out_net, d, recon_dir, i):

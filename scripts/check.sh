@@ -1,0 +1,38 @@
+#!/bin/bash
+# One GPU-box evidence pass, by phase: scripts/check.sh <tag> <phase>...
+#   tests   full -m gpu suite           smoke  __graft_entry__.smoke()
+#   bench   the driver's bench command  stats  rocprofv3 kernel stats of a short bench command
+#   pmc     FETCH_SIZE / WRITE_SIZE passes -> HBM bytes per launch of the fp32 and AMP dominant kernels
+#   steps   per-kernel tables of 10 replayed fp32 / AMP steps (scripts/profile_steps.sh)
+#   mem     peak device memory with the deferred weight-gradient reduces on / off (scripts/mem_probe.py)
+#   dist    the N>1 rehearsal (scripts/dist_rehearsal.sh)
+# Every step runs under its own time limit (scripts/gpu_run.sh) and the pass stops at the first crash-like exit.
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+tag=$1; shift
+BENCH="bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-eval"
+for ph in "$@"; do
+  case $ph in
+    tests) scripts/gpu_run.sh "gputests:600:python -u -m pytest tests -x -v --timeout 120 --timeout-method thread -m gpu -s" || exit $? ;;
+    smoke) scripts/gpu_run.sh "smoke:200:python -c 'import __graft_entry__ as g; g.smoke()'" || exit $? ;;
+    bench) scripts/gpu_run.sh "bench_full:500:python3 bench.py --gpus 1 --steps 20 --warmup 5" || exit $?
+           grep '^{' gpurun_out/bench_full.log > gpurun_out/${tag}_bench_line.json ;;
+    stats) scripts/gpu_run.sh "stats:400:rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${tag}_stats -o run -- python3 $BENCH" || exit $?
+           python3 scripts/prof_summary.py gpurun_out/${tag}_stats/run_kernel_stats.csv 11 > gpurun_out/${tag}_bench_summary.txt ;;
+    pmc)   scripts/gpu_run.sh \
+             "pmc_fetch:500:rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/${tag}_pmc_fetch -o run -- python3 $BENCH" \
+             "pmc_write:500:rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/${tag}_pmc_write -o run -- python3 $BENCH" || exit $?
+           for leg in fp32 amp; do
+             if [ $leg = fp32 ]; then sel="d['roofline']['kernel']"; out=${tag}_pmc_traffic.json; else sel="d['amp']['roofline']['kernel']"; out=${tag}_pmc_traffic_amp.json; fi
+             K=$(python3 -c "import json; d=json.load(open('gpurun_out/${tag}_bench_line.json')); print($sel.split(' (')[0])") || exit 1
+             python3 scripts/pmc_traffic.py gpurun_out/${tag}_pmc_fetch gpurun_out/${tag}_pmc_write --kernel "$K" --out gpurun_out/$out \
+               --command "rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE --kernel-trace --output-format csv -- python3 $BENCH" >> gpurun_out/pmc_traffic.log 2>&1
+           done ;;
+    steps) bash scripts/profile_steps.sh $tag || exit $? ;;
+    mem)   scripts/gpu_run.sh "mem_defer1:200:python3 scripts/mem_probe.py" "mem_defer0:200:HYRES_WGRAD_DEFER=0 python3 scripts/mem_probe.py" || exit $?
+           cat gpurun_out/mem_defer1.log gpurun_out/mem_defer0.log | grep WGRAD_DEFER > gpurun_out/${tag}_mem_probe.txt ;;
+    dist)  bash scripts/dist_rehearsal.sh; echo "dist rehearsal exit $?" ;;
+    *) echo "unknown phase $ph"; exit 2 ;;
+  esac
+done

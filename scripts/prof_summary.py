@@ -1,6 +1,10 @@
 """Summarise a rocprofv3 --kernel-trace --stats run into a short per-kernel table (ms per step).
 
-    python scripts/prof_summary.py <..._kernel_stats.csv | ..._results.db> <steps> [--csv out.csv]
+    python scripts/prof_summary.py <..._kernel_stats.csv | ..._results.db | ..._kernel_trace.csv> <steps> [--csv out.csv]
+
+A ``*_kernel_trace.csv`` (rocprofv3 --kernel-trace --output-format csv) of ``scripts/step_profile.py --marker`` is
+aggregated over the dispatches AFTER the marker (torch's spin kernel between warm-up and the timed steps) only, so
+``calls/step`` counts the replayed steps alone — the stats CSV also holds the capture's eager warm-up passes.
 
 Accepts either the CSV written with ``--output-format csv`` or the rocpd SQLite database that
 rocprofv3 writes by default; ``--csv`` re-exports a .db as a kernel_stats CSV (same columns as
@@ -30,6 +34,29 @@ def rows_from_db(path):
     return out
 
 
+def rows_from_trace(path):
+    """Per-kernel rows from a kernel trace, dispatches after the last spin/sleep marker kernel only."""
+    tr = list(csv.DictReader(open(path)))
+    name_k = "Kernel_Name"
+    t0_k, t1_k = "Start_Timestamp", "End_Timestamp"
+    tr.sort(key=lambda r: int(r[t0_k]))
+    marks = [i for i, r in enumerate(tr) if "spin" in r[name_k].lower() or "sleep" in r[name_k].lower()]
+    if marks:
+        tr = tr[marks[-1] + 1:]
+    agg = {}
+    for r in tr:
+        dur = int(r[t1_k]) - int(r[t0_k])
+        a = agg.setdefault(r[name_k], [0, 0.0, float("inf"), 0.0])
+        a[0] += 1
+        a[1] += dur
+        a[2] = min(a[2], dur)
+        a[3] = max(a[3], dur)
+    tot = sum(a[1] for a in agg.values()) or 1.0
+    return [{"Name": n, "Calls": str(c), "TotalDurationNs": str(int(t)), "AverageNs": f"{t / c:.3f}",
+             "Percentage": f"{100 * t / tot:.4f}", "MinNs": str(int(mn)), "MaxNs": str(int(mx))}
+            for n, (c, t, mn, mx) in agg.items()]
+
+
 def main():
     args = sys.argv[1:]
     csv_out = None
@@ -39,7 +66,12 @@ def main():
         del args[i:i + 2]
     path = args[0]
     steps = float(args[1]) if len(args) > 1 else 1.0
-    rows = rows_from_db(path) if path.endswith(".db") else list(csv.DictReader(open(path)))
+    if path.endswith(".db"):
+        rows = rows_from_db(path)
+    elif path.endswith("kernel_trace.csv"):
+        rows = rows_from_trace(path)
+    else:
+        rows = list(csv.DictReader(open(path)))
     if csv_out:
         with open(csv_out, "w", newline="") as f:
             w = csv.DictWriter(f, fieldnames=list(rows[0].keys()))

@@ -177,3 +177,30 @@ def _overlap_worker(rank, world, port):
 
 def test_overlapped_segment_reduce_gloo_world2():
     mp.spawn(_overlap_worker, args=(2, _free_port()), nprocs=2, join=True)
+
+
+def _engine_host_worker(rank, world, port):
+    """src/utils/engine.py's host-side DDP pieces: the sharded test epoch's meter all-reduce and the per-step
+    capture-key agreement (a rank at a different batch shape raises instead of hanging)."""
+    _init(rank, world, port)
+    try:
+        from src.losses import AverageMeter
+        from src.utils.engine import _GraphedStep, _all_reduce_meters, _all_ranks_ok
+        m = AverageMeter()
+        for v in ([1.0, 2.0] if rank == 0 else [4.0]):  # ragged shards: 2 batches on rank 0, 1 on rank 1
+            m.update(v)
+        _all_reduce_meters([m], "cpu")
+        assert m.count == 3 and abs(m.avg - 7.0 / 3) < 1e-12
+        gs = _GraphedStep.__new__(_GraphedStep)
+        gs._host_group = None
+        gs._agree(((16, 3, 256, 256), False, False))  # same key on both ranks: passes
+        assert _all_ranks_ok(rank == 0, gs._host_group) is False  # one rank failed: every rank falls back
+        assert _all_ranks_ok(True, gs._host_group) is True
+        with pytest.raises(RuntimeError, match="different graph-capture keys"):
+            gs._agree(((16 if rank == 0 else 12, 3, 256, 256), False, False))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_engine_ddp_host_agreement_gloo_world2():
+    mp.spawn(_engine_host_worker, args=(2, _free_port()), nprocs=2, join=True)
