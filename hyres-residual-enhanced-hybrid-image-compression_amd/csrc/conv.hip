@@ -101,10 +101,10 @@ __device__ __forceinline__ void epi_store(const hyres_epilogue& e, float* y, int
             break;
         }
         case HYRES_EPI_GDN_BWD:
-        case HYRES_EPI_IGDN_BWD: {
-            const float xv = ld_aux<false>(e, e.aux0, pix * e.ld0 + n);
-            const float gv = e.aux1[pix * e.ld1 + n];
-            const float nv = ld_aux<false>(e, e.aux2, pix * e.ld2 + n);
+        case HYRES_EPI_IGDN_BWD: {  // H (AMP fp16 gradients): x, the incoming gradient and the norm all fp16
+            const float xv = ld_aux<H>(e, e.aux0, pix * e.ld0 + n);
+            const float gv = ldv<H>(e.aux1, pix * e.ld1 + n);
+            const float nv = ld_aux<H>(e, e.aux2, pix * e.ld2 + n);
             const float f = (e.kind == HYRES_EPI_GDN_BWD) ? (1.0f / sqrtf(nv)) : sqrtf(nv);
             v = 2.0f * xv * v + gv * f;
             break;
@@ -112,7 +112,8 @@ __device__ __forceinline__ void epi_store(const hyres_epilogue& e, float* y, int
         default: break;
     }
     if constexpr (H) {
-        stv<true>(y, pix * ldy + n, v);  // host: no accumulate with fp16 output
+        if (e.accumulate) v += ldv<true>(y, pix * ldy + n);  // fp16 gradient accumulation (AMP): fp32 add
+        stv<true>(y, pix * ldy + n, v);
     } else {
         float* yp = y + pix * ldy + n;
         if (e.accumulate) v += *yp;
@@ -166,9 +167,9 @@ __device__ __forceinline__ void epi_store4(const hyres_epilogue& e, float* y, in
         }
         case HYRES_EPI_GDN_BWD:
         case HYRES_EPI_IGDN_BWD: {
-            const float4 x = ld_aux4<false>(e, e.aux0, pix * e.ld0 + n);
-            const float4 gg = ld4(e.aux1 + pix * e.ld1 + n);
-            const float4 nn = ld_aux4<false>(e, e.aux2, pix * e.ld2 + n);
+            const float4 x = ld_aux4<H>(e, e.aux0, pix * e.ld0 + n);
+            const float4 gg = ldv4<H>(e.aux1, pix * e.ld1 + n);
+            const float4 nn = ld_aux4<H>(e, e.aux2, pix * e.ld2 + n);
             const float xv[4] = {x.x, x.y, x.z, x.w}, gv[4] = {gg.x, gg.y, gg.z, gg.w}, nv[4] = {nn.x, nn.y, nn.z, nn.w};
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
@@ -180,6 +181,10 @@ __device__ __forceinline__ void epi_store4(const hyres_epilogue& e, float* y, in
         default: break;
     }
     if constexpr (H) {
+        if (e.accumulate) {
+            const float4 p = ldv4<true>(y, pix * ldy + n);
+            o[0] += p.x; o[1] += p.y; o[2] += p.z; o[3] += p.w;
+        }
         stv4<true>(y, pix * ldy + n, make_float4(o[0], o[1], o[2], o[3]));
     } else {
         float* yp = y + pix * ldy + n;
@@ -496,7 +501,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
                 const __amdgpu_buffer_rsrc_t r_res = opnd_rsrc(e.res, npo * e.ldres * ES);
                 const __amdgpu_buffer_rsrc_t r_m32 = opnd_rsrc(mask && !m16 ? e.aux0 : nullptr, npo * e.ld0 * 4);
                 const __amdgpu_buffer_rsrc_t r_m16 = opnd_rsrc(mask && m16 ? e.aux0 : nullptr, npo * e.ld0 * 2);
-                const __amdgpu_buffer_rsrc_t r_old = opnd_rsrc(!YH && e.accumulate ? a.y : nullptr, npo * g.ldy * 4);
+                const __amdgpu_buffer_rsrc_t r_old = opnd_rsrc(e.accumulate ? a.y : nullptr, npo * g.ldy * ES);
                 constexpr int OOR = (int)0x80000000;
                 for (int it0 = 0; it0 < ITER; it0 += U) {
                     float4 v[U], yo[U], mk[U], bs[U];
@@ -546,9 +551,13 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
                             else rs[u] = z4;
                         }
                     }
-                    if (!YH && e.accumulate) {
+                    if (e.accumulate) {  // YH: fp16 gradient accumulation (AMP)
 #pragma unroll
-                        for (int u = 0; u < U; ++u) yo[u] = bload4(r_old, ok[u] ? (int)((px[u] * g.ldy + nn[u]) * 4) : OOR);
+                        for (int u = 0; u < U; ++u) {
+                            const int oo = ok[u] ? (int)((px[u] * g.ldy + nn[u]) * ES) : OOR;
+                            if constexpr (YH) yo[u] = h2f4(bload4h(r_old, oo));
+                            else yo[u] = bload4(r_old, oo);
+                        }
                     }
                     if (mask && m16) {
 #pragma unroll
@@ -2122,9 +2131,9 @@ int hyres_conv_forward(const hyres_conv_geom* g, const float* x, const float* w2
     HY_REQUIRE(e->io_f16 >= 0 && e->io_f16 <= 4, HYRES_E_ARG, "conv: io_f16 %d (fp16 X/Y bits, or AUX16 alone)",
                e->io_f16);
     if (e->io_f16 & 3) {
-        HY_REQUIRE(e->io_f16 >= 1 && e->io_f16 <= 3 && !e->accumulate &&
-                       (e->kind == HYRES_EPI_BIAS || e->kind == HYRES_EPI_GDN || e->kind == HYRES_EPI_IGDN),
-                   HYRES_E_ARG, "conv: fp16 activations are forward-only (no accumulate / GDN backward)");
+        HY_REQUIRE(e->io_f16 >= 1 && e->io_f16 <= 3 && (!(e->kind == HYRES_EPI_GDN_BWD || e->kind == HYRES_EPI_IGDN_BWD)
+                                                         || (e->io_f16 & 2)),
+                   HYRES_E_ARG, "conv: a fp16 GDN-backward epilogue needs fp16 Y (its operands share Y's dtype)");
         HY_REQUIRE(!(e->io_f16 & 1) || mode != 2, HYRES_E_ARG, "conv: fp16 X needs Ci %% 32 == 0");
         HY_REQUIRE(!ch.narrow || !(e->io_f16 & 2), HYRES_E_ARG, "conv: the Co <= 4 kernel writes fp32 only");
     }

@@ -69,18 +69,19 @@ __global__ void add_clamp01_bwd_kernel(const float* pre, const float* g, float* 
 __global__ void relu_bwd_kernel(const float* y, const float* g, float* gx, long long n) {
     GRID_STRIDE(i, n) gx[i] = y[i] > 0.f ? g[i] : 0.f;
 }
-// H (here and below): the saved activation operand is fp16 in HBM (AMP training), gradients fp32
-template <bool H = false>
+// H (here and below): the saved activation operand is fp16 in HBM (AMP training); G: the gradients (in and out)
+// are fp16 too (AMP's fp16 activation gradients inside the f16_region), arithmetic fp32
+template <bool H = false, bool G = false>
 __global__ void relu_bwd_2d_kernel(const float* y, int ldy, const float* g, int ldg, float* gx, int ldgx,
                                    long long P, int C) {
     const long long n = P * C;
     GRID_STRIDE(i, n) {
         long long p = i / C;
         int c = (int)(i - p * C);
-        gx[p * ldgx + c] = ldv<H>(y, p * ldy + c) > 0.f ? g[p * ldg + c] : 0.f;
+        stv<G>(gx, p * ldgx + c, ldv<H>(y, p * ldy + c) > 0.f ? ldv<G>(g, p * ldg + c) : 0.f);
     }
 }
-template <bool H = false>
+template <bool H = false, bool G = false>
 __global__ void prelu_bwd_kernel(const float* x, int ldx, const float* g, int ldg, float* gx, int ldgx,
                                  long long P, int C, const float* slope, float* part) {
     const float a = slope[0];
@@ -90,8 +91,8 @@ __global__ void prelu_bwd_kernel(const float* x, int ldx, const float* g, int ld
         long long p = i / C;
         int c = (int)(i - p * C);
         float xv = ldv<H>(x, p * ldx + c);
-        float gv = g[p * ldg + c];
-        gx[p * ldgx + c] = xv > 0.f ? gv : a * gv;
+        float gv = ldv<G>(g, p * ldg + c);
+        stv<G>(gx, p * ldgx + c, xv > 0.f ? gv : a * gv);
         if (!(xv > 0.f)) s += xv * gv;
     }
     // block reduce
@@ -139,59 +140,62 @@ __global__ void attn_gate_fwd4h_kernel(const float* a, const float* b, const flo
         stv4<true>(out, 4 * i, make_float4(av.x * s.x + xv.x, av.y * s.y + xv.y, av.z * s.z + xv.z, av.w * s.w + xv.w));
     }
 }
-template <bool H = false>
+template <bool H = false, bool G = false>
 __global__ void attn_gate_bwd_kernel(const float* a, const float* b, const float* g, float* ga, float* gb,
                                      long long n) {
     GRID_STRIDE(i, n) {
         float s = 1.0f / (1.0f + expf(-ldv<H>(b, i)));
-        float gv = g[i];
-        ga[i] = gv * s;
-        gb[i] = gv * ldv<H>(a, i) * s * (1.0f - s);
+        float gv = ldv<G>(g, i);
+        stv<G>(ga, i, gv * s);
+        stv<G>(gb, i, gv * ldv<H>(a, i) * s * (1.0f - s));
     }
 }
+template <bool G = false>
 __global__ void accumulate_kernel(const float* x, float* y, long long n) {
-    GRID_STRIDE(i, n) y[i] += x[i];
+    GRID_STRIDE(i, n) stv<G>(y, i, ldv<G>(y, i) + ldv<G>(x, i));
 }
+// XH / YH: x / y stored fp16 (fp32 arithmetic)
+template <bool XH = false, bool YH = false>
 __global__ void add2d_kernel(const float* x, int ldx, float* y, int ldy, long long P, int C, int acc) {
     const long long n = P * C;
     GRID_STRIDE(i, n) {
         long long p = i / C;
         int c = (int)(i - p * C);
-        float v = x[p * ldx + c];
-        float* yp = y + p * ldy + c;
-        *yp = acc ? *yp + v : v;
+        float v = ldv<XH>(x, p * ldx + c);
+        if (acc) v += ldv<YH>(y, p * ldy + c);
+        stv<YH>(y, p * ldy + c, v);
     }
 }
 // float4 variants of the [P][C]-strided elementwise passes (C, every ld % 4 == 0, 16B-aligned, P*C < 2^31):
-// 32-bit index math, 16 B per lane
+// 32-bit index math, 16 B per lane (8 B for fp16 operands)
+template <bool XH = false, bool YH = false>
 __global__ __launch_bounds__(256) void add2d4_kernel(const float* x, int ldx, float* y, int ldy, int P, int C4,
                                                      int acc) {
     const int n = P * C4;
     for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
         const int p = i / C4, c = 4 * (i - (i / C4) * C4);
-        float4 v = *reinterpret_cast<const float4*>(x + (long long)p * ldx + c);
-        float4* yp = reinterpret_cast<float4*>(y + (long long)p * ldy + c);
+        float4 v = ldv4<XH>(x, (long long)p * ldx + c);
         if (acc) {
-            const float4 o = *yp;
+            const float4 o = ldv4<YH>(y, (long long)p * ldy + c);
             v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
         }
-        *yp = v;
+        stv4<YH>(y, (long long)p * ldy + c, v);
     }
 }
-template <bool H = false>
+template <bool H = false, bool G = false>
 __global__ __launch_bounds__(256) void relu_bwd_2d4_kernel(const float* y, int ldy, const float* g, int ldg,
                                                            float* gx, int ldgx, int P, int C4) {
     const int n = P * C4;
     for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
         const int p = i / C4, c = 4 * (i - (i / C4) * C4);
         const float4 yv = ldv4<H>(y, (long long)p * ldy + c);
-        const float4 gv = *reinterpret_cast<const float4*>(g + (long long)p * ldg + c);
-        *reinterpret_cast<float4*>(gx + (long long)p * ldgx + c) =
-            make_float4(yv.x > 0.f ? gv.x : 0.f, yv.y > 0.f ? gv.y : 0.f, yv.z > 0.f ? gv.z : 0.f,
-                        yv.w > 0.f ? gv.w : 0.f);
+        const float4 gv = ldv4<G>(g, (long long)p * ldg + c);
+        stv4<G>(gx, (long long)p * ldgx + c,
+                make_float4(yv.x > 0.f ? gv.x : 0.f, yv.y > 0.f ? gv.y : 0.f, yv.z > 0.f ? gv.z : 0.f,
+                            yv.w > 0.f ? gv.w : 0.f));
     }
 }
-template <bool H = false>
+template <bool H = false, bool G = false>
 __global__ __launch_bounds__(256) void prelu_bwd4_kernel(const float* x, int ldx, const float* g, int ldg, float* gx,
                                                          int ldgx, int P, int C4, const float* slope, float* part) {
     const float a = slope[0];
@@ -200,10 +204,10 @@ __global__ __launch_bounds__(256) void prelu_bwd4_kernel(const float* x, int ldx
     for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
         const int p = i / C4, c = 4 * (i - (i / C4) * C4);
         const float4 xv = ldv4<H>(x, (long long)p * ldx + c);
-        const float4 gv = *reinterpret_cast<const float4*>(g + (long long)p * ldg + c);
-        *reinterpret_cast<float4*>(gx + (long long)p * ldgx + c) =
-            make_float4(xv.x > 0.f ? gv.x : a * gv.x, xv.y > 0.f ? gv.y : a * gv.y, xv.z > 0.f ? gv.z : a * gv.z,
-                        xv.w > 0.f ? gv.w : a * gv.w);
+        const float4 gv = ldv4<G>(g, (long long)p * ldg + c);
+        stv4<G>(gx, (long long)p * ldgx + c,
+                make_float4(xv.x > 0.f ? gv.x : a * gv.x, xv.y > 0.f ? gv.y : a * gv.y, xv.z > 0.f ? gv.z : a * gv.z,
+                            xv.w > 0.f ? gv.w : a * gv.w));
         if (!(xv.x > 0.f)) s += xv.x * gv.x;
         if (!(xv.y > 0.f)) s += xv.y * gv.y;
         if (!(xv.z > 0.f)) s += xv.z * gv.z;
@@ -263,10 +267,10 @@ __global__ void gdn_reparam_bwd_kernel(const float* beta, const float* gamma, co
         }
     }
 }
-template <bool H = false>
+template <bool H = false, bool G = false>
 __global__ void gdn_dnorm_kernel(const float* g, const float* y, const float* nrm, float* dn, long long n,
                                  float coef) {
-    GRID_STRIDE(i, n) dn[i] = coef * g[i] * ldv<H>(y, i) / ldv<H>(nrm, i);
+    GRID_STRIDE(i, n) stv<G>(dn, i, coef * ldv<G>(g, i) * ldv<H>(y, i) / ldv<H>(nrm, i));
 }
 
 // ---------------------------------------------------------------- RNG
@@ -577,43 +581,44 @@ int hyres_relu_bwd(const float* y, const float* g, float* gx, long long n, hyres
     return HY_LAUNCH_CHECK("relu_bwd");
 }
 extern "C++" {
-template <bool H>
+template <bool H, bool G>
 static int relu_bwd_2d_impl(const float* y, int ldy, const float* g, int ldg, float* gx, int ldgx, long long P, int C,
                             hyres_stream_t s) {
     HY_REQUIRE(y && g && gx, HYRES_E_ARG, "relu_bwd_2d: NULL");
     if (vec4_2d(P, C, y, ldy, g, ldg, gx, ldgx)) {
-        hipLaunchKernelGGL(relu_bwd_2d4_kernel<H>, dim3(grid_for(P * C / 4)), dim3(256), 0, as_stream(s), y, ldy, g,
-                           ldg, gx, ldgx, (int)P, C / 4);
+        hipLaunchKernelGGL((relu_bwd_2d4_kernel<H, G>), dim3(grid_for(P * C / 4)), dim3(256), 0, as_stream(s), y, ldy,
+                           g, ldg, gx, ldgx, (int)P, C / 4);
         return HY_LAUNCH_CHECK("relu_bwd_2d4");
     }
-    hipLaunchKernelGGL(relu_bwd_2d_kernel<H>, dim3(grid_for(P * C)), dim3(256), 0, as_stream(s), y, ldy, g, ldg, gx,
-                       ldgx, P, C);
+    hipLaunchKernelGGL((relu_bwd_2d_kernel<H, G>), dim3(grid_for(P * C)), dim3(256), 0, as_stream(s), y, ldy, g, ldg,
+                       gx, ldgx, P, C);
     return HY_LAUNCH_CHECK("relu_bwd_2d");
 }
 }  // extern "C++"
 int hyres_relu_bwd_2d(const float* y, int ldy, const float* g, int ldg, float* gx, int ldgx, long long P, int C,
                       hyres_stream_t s) {
-    return relu_bwd_2d_impl<false>(y, ldy, g, ldg, gx, ldgx, P, C, s);
+    return relu_bwd_2d_impl<false, false>(y, ldy, g, ldg, gx, ldgx, P, C, s);
 }
-int hyres_relu_bwd_2d_f16(const void* y, int ldy, const float* g, int ldg, float* gx, int ldgx, long long P, int C,
-                          hyres_stream_t s) {
-    return relu_bwd_2d_impl<true>((const float*)y, ldy, g, ldg, gx, ldgx, P, C, s);
+int hyres_relu_bwd_2d_f16(const void* y, int ldy, const void* g, int ldg, void* gx, int ldgx, long long P, int C,
+                          int g16, hyres_stream_t s) {
+    if (g16) return relu_bwd_2d_impl<true, true>((const float*)y, ldy, (const float*)g, ldg, (float*)gx, ldgx, P, C, s);
+    return relu_bwd_2d_impl<true, false>((const float*)y, ldy, (const float*)g, ldg, (float*)gx, ldgx, P, C, s);
 }
 long long hyres_reduce_workspace_bytes(long long n) { return (long long)grid_for(n, 4) * 8 + 256; }  // fp64 partials
 
 extern "C++" {
-template <bool H>
+template <bool H, bool G>
 static int prelu_bwd_impl(const float* x, int ldx, const float* g, int ldg, float* gx, int ldgx, long long P, int C,
                           const float* slope, float* dslope, void* ws, long long ws_bytes, hyres_stream_t s) {
     HY_REQUIRE(x && g && gx && slope && dslope, HYRES_E_ARG, "prelu_bwd: NULL");
     int nb = grid_for(P * C, 4);
     HY_REQUIRE(ws && ws_bytes >= (long long)nb * 4, HYRES_E_WORKSPACE, "prelu_bwd: workspace");
     if (vec4_2d(P, C, x, ldx, g, ldg, gx, ldgx))
-        hipLaunchKernelGGL(prelu_bwd4_kernel<H>, dim3(nb), dim3(256), 0, as_stream(s), x, ldx, g, ldg, gx, ldgx,
+        hipLaunchKernelGGL((prelu_bwd4_kernel<H, G>), dim3(nb), dim3(256), 0, as_stream(s), x, ldx, g, ldg, gx, ldgx,
                            (int)P, C / 4, slope, (float*)ws);
     else
-        hipLaunchKernelGGL(prelu_bwd_kernel<H>, dim3(nb), dim3(256), 0, as_stream(s), x, ldx, g, ldg, gx, ldgx, P, C,
-                           slope, (float*)ws);
+        hipLaunchKernelGGL((prelu_bwd_kernel<H, G>), dim3(nb), dim3(256), 0, as_stream(s), x, ldx, g, ldg, gx, ldgx, P,
+                           C, slope, (float*)ws);
     int rc = HY_LAUNCH_CHECK("prelu_bwd");
     if (rc) return rc;
     hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(256), 0, as_stream(s), (const float*)ws, nb, dslope, 1);
@@ -622,11 +627,15 @@ static int prelu_bwd_impl(const float* x, int ldx, const float* g, int ldg, floa
 }  // extern "C++"
 int hyres_prelu_bwd(const float* x, int ldx, const float* g, int ldg, float* gx, int ldgx, long long P, int C,
                     const float* slope, float* dslope, void* ws, long long ws_bytes, hyres_stream_t s) {
-    return prelu_bwd_impl<false>(x, ldx, g, ldg, gx, ldgx, P, C, slope, dslope, ws, ws_bytes, s);
+    return prelu_bwd_impl<false, false>(x, ldx, g, ldg, gx, ldgx, P, C, slope, dslope, ws, ws_bytes, s);
 }
-int hyres_prelu_bwd_f16(const void* x, int ldx, const float* g, int ldg, float* gx, int ldgx, long long P, int C,
-                        const float* slope, float* dslope, void* ws, long long ws_bytes, hyres_stream_t s) {
-    return prelu_bwd_impl<true>((const float*)x, ldx, g, ldg, gx, ldgx, P, C, slope, dslope, ws, ws_bytes, s);
+int hyres_prelu_bwd_f16(const void* x, int ldx, const void* g, int ldg, void* gx, int ldgx, long long P, int C,
+                        const float* slope, float* dslope, void* ws, long long ws_bytes, int g16, hyres_stream_t s) {
+    if (g16)
+        return prelu_bwd_impl<true, true>((const float*)x, ldx, (const float*)g, ldg, (float*)gx, ldgx, P, C, slope,
+                                          dslope, ws, ws_bytes, s);
+    return prelu_bwd_impl<true, false>((const float*)x, ldx, (const float*)g, ldg, (float*)gx, ldgx, P, C, slope, dslope,
+                                       ws, ws_bytes, s);
 }
 int hyres_attn_gate_fwd(const float* a, const float* b, const float* x, float* out, long long n, hyres_stream_t s) {
     HY_REQUIRE(a && b && x && out, HYRES_E_ARG, "attn_gate_fwd: NULL");
@@ -642,32 +651,61 @@ int hyres_attn_gate_fwd_f16(const void* a, const void* b, const void* x, void* o
 int hyres_attn_gate_bwd(const float* a, const float* b, const float* g, float* ga, float* gb, long long n,
                         hyres_stream_t s) {
     HY_REQUIRE(a && b && g && ga && gb, HYRES_E_ARG, "attn_gate_bwd: NULL");
-    hipLaunchKernelGGL(attn_gate_bwd_kernel<false>, dim3(grid_for(n)), dim3(256), 0, as_stream(s), a, b, g, ga, gb, n);
+    hipLaunchKernelGGL((attn_gate_bwd_kernel<false, false>), dim3(grid_for(n)), dim3(256), 0, as_stream(s), a, b, g,
+                       ga, gb, n);
     return HY_LAUNCH_CHECK("attn_gate_bwd");
 }
-int hyres_attn_gate_bwd_f16(const void* a, const void* b, const float* g, float* ga, float* gb, long long n,
+int hyres_attn_gate_bwd_f16(const void* a, const void* b, const void* g, void* ga, void* gb, long long n, int g16,
                             hyres_stream_t s) {
     HY_REQUIRE(a && b && g && ga && gb, HYRES_E_ARG, "attn_gate_bwd_f16: NULL");
-    hipLaunchKernelGGL(attn_gate_bwd_kernel<true>, dim3(grid_for(n)), dim3(256), 0, as_stream(s), (const float*)a,
-                       (const float*)b, g, ga, gb, n);
+    if (g16)
+        hipLaunchKernelGGL((attn_gate_bwd_kernel<true, true>), dim3(grid_for(n)), dim3(256), 0, as_stream(s),
+                           (const float*)a, (const float*)b, (const float*)g, (float*)ga, (float*)gb, n);
+    else
+        hipLaunchKernelGGL((attn_gate_bwd_kernel<true, false>), dim3(grid_for(n)), dim3(256), 0, as_stream(s),
+                           (const float*)a, (const float*)b, (const float*)g, (float*)ga, (float*)gb, n);
     return HY_LAUNCH_CHECK("attn_gate_bwd_f16");
 }
 int hyres_accumulate(const float* x, float* y, long long n, hyres_stream_t s) {
     HY_REQUIRE(x && y, HYRES_E_ARG, "accumulate: NULL");
-    hipLaunchKernelGGL(accumulate_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(s), x, y, n);
+    hipLaunchKernelGGL(accumulate_kernel<false>, dim3(grid_for(n)), dim3(256), 0, as_stream(s), x, y, n);
     return HY_LAUNCH_CHECK("accumulate");
 }
+int hyres_accumulate_f16(const void* x, void* y, long long n, hyres_stream_t s) {
+    HY_REQUIRE(x && y, HYRES_E_ARG, "accumulate_f16: NULL");
+    hipLaunchKernelGGL(accumulate_kernel<true>, dim3(grid_for(n)), dim3(256), 0, as_stream(s), (const float*)x,
+                       (float*)y, n);
+    return HY_LAUNCH_CHECK("accumulate_f16");
+}
+extern "C++" {
+template <bool XH, bool YH>
+static int add2d_impl(const float* x, int ldx, float* y, int ldy, long long P, int C, int accumulate, hyres_stream_t s) {
+    if (vec4_2d(P, C, x, ldx, y, ldy, y, ldy)) {
+        hipLaunchKernelGGL((add2d4_kernel<XH, YH>), dim3(grid_for(P * C / 4)), dim3(256), 0, as_stream(s), x, ldx, y,
+                           ldy, (int)P, C / 4, accumulate);
+        return HY_LAUNCH_CHECK("add2d4");
+    }
+    hipLaunchKernelGGL((add2d_kernel<XH, YH>), dim3(grid_for(P * C)), dim3(256), 0, as_stream(s), x, ldx, y, ldy, P, C,
+                       accumulate);
+    return HY_LAUNCH_CHECK("add2d");
+}
+}  // extern "C++"
 int hyres_add2d(const float* x, int ldx, float* y, int ldy, long long P, int C, int accumulate,
                 hyres_stream_t s) {
     HY_REQUIRE(x && y, HYRES_E_ARG, "add2d: NULL");
-    if (vec4_2d(P, C, x, ldx, y, ldy, y, ldy)) {
-        hipLaunchKernelGGL(add2d4_kernel, dim3(grid_for(P * C / 4)), dim3(256), 0, as_stream(s), x, ldx, y, ldy, (int)P,
-                           C / 4, accumulate);
-        return HY_LAUNCH_CHECK("add2d4");
+    return add2d_impl<false, false>(x, ldx, y, ldy, P, C, accumulate, s);
+}
+int hyres_add2d_f16(const void* x, int ldx, void* y, int ldy, long long P, int C, int accumulate, int io,
+                    hyres_stream_t s) {
+    HY_REQUIRE(x && y && io >= 0 && io <= 3, HYRES_E_ARG, "add2d_f16: NULL or io %d", io);
+    const float* xf = (const float*)x;
+    float* yf = (float*)y;
+    switch (io) {
+        case 1: return add2d_impl<true, false>(xf, ldx, yf, ldy, P, C, accumulate, s);
+        case 2: return add2d_impl<false, true>(xf, ldx, yf, ldy, P, C, accumulate, s);
+        case 3: return add2d_impl<true, true>(xf, ldx, yf, ldy, P, C, accumulate, s);
+        default: return add2d_impl<false, false>(xf, ldx, yf, ldy, P, C, accumulate, s);
     }
-    hipLaunchKernelGGL(add2d_kernel, dim3(grid_for(P * C)), dim3(256), 0, as_stream(s), x, ldx, y, ldy, P, C,
-                       accumulate);
-    return HY_LAUNCH_CHECK("add2d");
 }
 int hyres_mul(const float* a, const float* b, float* y, long long n, hyres_stream_t s) {
     HY_REQUIRE(a && b && y, HYRES_E_ARG, "mul: NULL");
@@ -697,16 +735,20 @@ int hyres_gdn_dnorm(const float* g, const float* y, const float* n, float* dn, l
                     hyres_stream_t s) {
     HY_REQUIRE(g && y && n && dn, HYRES_E_ARG, "gdn_dnorm: NULL");
     long long cnt = P * C;
-    hipLaunchKernelGGL(gdn_dnorm_kernel<false>, dim3(grid_for(cnt)), dim3(256), 0, as_stream(s), g, y, n, dn, cnt,
-                       inverse ? 0.5f : -0.5f);
+    hipLaunchKernelGGL((gdn_dnorm_kernel<false, false>), dim3(grid_for(cnt)), dim3(256), 0, as_stream(s), g, y, n, dn,
+                       cnt, inverse ? 0.5f : -0.5f);
     return HY_LAUNCH_CHECK("gdn_dnorm");
 }
-int hyres_gdn_dnorm_f16(const float* g, const void* y, const void* n, float* dn, long long P, int C, int inverse,
+int hyres_gdn_dnorm_f16(const void* g, const void* y, const void* n, void* dn, long long P, int C, int inverse, int g16,
                         hyres_stream_t s) {
     HY_REQUIRE(g && y && n && dn, HYRES_E_ARG, "gdn_dnorm_f16: NULL");
     long long cnt = P * C;
-    hipLaunchKernelGGL(gdn_dnorm_kernel<true>, dim3(grid_for(cnt)), dim3(256), 0, as_stream(s), g, (const float*)y,
-                       (const float*)n, dn, cnt, inverse ? 0.5f : -0.5f);
+    if (g16)
+        hipLaunchKernelGGL((gdn_dnorm_kernel<true, true>), dim3(grid_for(cnt)), dim3(256), 0, as_stream(s),
+                           (const float*)g, (const float*)y, (const float*)n, (float*)dn, cnt, inverse ? 0.5f : -0.5f);
+    else
+        hipLaunchKernelGGL((gdn_dnorm_kernel<true, false>), dim3(grid_for(cnt)), dim3(256), 0, as_stream(s),
+                           (const float*)g, (const float*)y, (const float*)n, (float*)dn, cnt, inverse ? 0.5f : -0.5f);
     return HY_LAUNCH_CHECK("gdn_dnorm_f16");
 }
 int hyres_uniform_noise(float* out, long long n, unsigned long long seed, unsigned long long offset,

@@ -99,7 +99,7 @@ __device__ __forceinline__ void bw_range(float inv, int t, int in, int out, int&
 
 // one block row per input row (blockIdx.y = b*Hi + h): the vertical output range and weights are
 // block-uniform; threads over (w, channel group)
-template <int VEC>
+template <int VEC, bool G = false>  // G: gy / gx fp16 (AMP fp16 gradients), fp32 sums
 __global__ __launch_bounds__(256) void bilinear_bwd_kernel(const float* gy, int ldgy, float* gx, int ldgx, int B,
                                                            int Hi, int Wi, int Ho, int Wo, int C, float sh, float sw,
                                                            int acc) {
@@ -109,8 +109,8 @@ __global__ __launch_bounds__(256) void bilinear_bwd_kernel(const float* gy, int 
     int oh_lo, oh_hi;
     bw_range(1.0f / sh, h, Hi, Ho, oh_lo, oh_hi);
     const float isw = 1.0f / sw;
-    const float* gb = gy + (long long)b * Ho * Wo * ldgy;
-    float* gr = gx + (long long)row * Wi * ldgx;
+    const long long gb = (long long)b * Ho * Wo * ldgy;  // element offsets (the pointers may hold fp16)
+    const long long gr = (long long)row * Wi * ldgx;
     const int n = Wi * CG;
     for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
         const int w = i / CG;
@@ -122,29 +122,29 @@ __global__ __launch_bounds__(256) void bilinear_bwd_kernel(const float* gy, int 
             const float wh = bw_weight(sh, oh, Hi, h);
             if (wh == 0.f) continue;
             float4 rs = make_float4(0.f, 0.f, 0.f, 0.f);
-            const float* gq = gb + (long long)oh * Wo * ldgy + c;
+            const long long gq = gb + (long long)oh * Wo * ldgy + c;
             for (int ow = ow_lo; ow <= ow_hi; ++ow) {
                 const float ww = bw_weight(sw, ow, Wi, w);
                 if (ww == 0.f) continue;
-                const float* q = gq + ow * ldgy;
+                const long long q = gq + (long long)ow * ldgy;
                 if constexpr (VEC == 4) {
-                    const float4 v = ld4(q);
+                    const float4 v = ldv4<G>(gy, q);
                     rs.x += ww * v.x; rs.y += ww * v.y; rs.z += ww * v.z; rs.w += ww * v.w;
                 } else {
-                    rs.x += ww * q[0];
+                    rs.x += ww * ldv<G>(gy, q);
                 }
             }
             s.x += wh * rs.x; s.y += wh * rs.y; s.z += wh * rs.z; s.w += wh * rs.w;
         }
-        float* gp = gr + (long long)w * ldgx + c;
+        const long long gp = gr + (long long)w * ldgx + c;
         if constexpr (VEC == 4) {
             if (acc) {
-                const float4 o = ld4(gp);
+                const float4 o = ldv4<G>(gx, gp);
                 s.x += o.x; s.y += o.y; s.z += o.z; s.w += o.w;
             }
-            *reinterpret_cast<float4*>(gp) = s;
+            stv4<G>(gx, gp, s);
         } else {
-            *gp = acc ? *gp + s.x : s.x;
+            stv<G>(gx, gp, acc ? ldv<G>(gx, gp) + s.x : s.x);
         }
     }
 }
@@ -155,7 +155,7 @@ __global__ __launch_bounds__(256) void bilinear_bwd_kernel(const float* gy, int 
 // input-gradient element receives exactly one 0.25*gy term or nothing — a streaming kernel instead of
 // the general gather (which evaluates every candidate stencil weight per element); the same fp32 result
 // (0.5 * (0.5 * g) == 0.25 * g).
-template <int S>
+template <int S, bool G = false>
 __global__ __launch_bounds__(256) void bilinear_down_bwd_kernel(const float* gy, int ldgy, float* gx, int ldgx, int Hi,
                                                                 int Wi, int Ho, int Wo, int C, int acc) {
     constexpr int A0 = (S - 2) / 2;
@@ -165,7 +165,7 @@ __global__ __launch_bounds__(256) void bilinear_down_bwd_kernel(const float* gy,
     const int dh = h - A0;
     const bool hok = dh >= 0 && (dh % S) < 2;
     const long long gyr = ((long long)b * Ho + (hok ? dh / S : 0)) * Wo;
-    float* gr = gx + (long long)row * Wi * ldgx;
+    const long long gr = (long long)row * Wi * ldgx;
     const int n = Wi * CG;
     for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
         const int w = i / CG;
@@ -174,15 +174,15 @@ __global__ __launch_bounds__(256) void bilinear_down_bwd_kernel(const float* gy,
         const bool ok = hok && dw >= 0 && (dw % S) < 2;
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
         if (ok) {
-            const float4 g = ld4(gy + (gyr + dw / S) * ldgy + c);
+            const float4 g = ldv4<G>(gy, (gyr + dw / S) * ldgy + c);
             v = make_float4(0.25f * g.x, 0.25f * g.y, 0.25f * g.z, 0.25f * g.w);
         }
-        float* gp = gr + (long long)w * ldgx + c;
+        const long long gp = gr + (long long)w * ldgx + c;
         if (acc) {
-            const float4 o = ld4(gp);
+            const float4 o = ldv4<G>(gx, gp);
             v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
         }
-        *reinterpret_cast<float4*>(gp) = v;
+        stv4<G>(gx, gp, v);
     }
 }
 
@@ -247,7 +247,7 @@ __global__ void se_scale_kernel(const float* x, const float* sgate, float* y, in
 }
 // float4 variants (C % 4 == 0, 256 % (C/4) == 0): 256 threads = (C/4 channel groups) x (pixel lanes),
 // every thread busy, deterministic LDS fold over the pixel lanes. SQ: sum of gy*x (backward) instead of x.
-template <bool PROD, bool H = false>
+template <bool PROD, bool H = false, bool GH = false>  // GH: gy fp16
 __global__ __launch_bounds__(256) void se_pool4_kernel(const float* x, const float* gy, int HW, int C, int per,
                                                        float* part) {
     __shared__ float4 red[256];
@@ -260,7 +260,7 @@ __global__ __launch_bounds__(256) void se_pool4_kernel(const float* x, const flo
         const long long i = ((long long)b * HW + p) * C + 4 * g;
         float4 v = ldv4<H>(x, i);
         if constexpr (PROD) {
-            const float4 q = *reinterpret_cast<const float4*>(gy + i);
+            const float4 q = ldv4<GH>(gy, i);
             v.x *= q.x; v.y *= q.y; v.z *= q.z; v.w *= q.w;
         }
         s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
@@ -277,7 +277,7 @@ __global__ __launch_bounds__(256) void se_pool4_kernel(const float* x, const flo
     }
 }
 // backward: partial sums of gy*x per (b,c)
-template <bool H = false>
+template <bool H = false, bool G = false>
 __global__ void se_bwd_pool_kernel(const float* x, const float* gy, int HW, int C, int per, float* part) {
     const int b = blockIdx.x, ch = blockIdx.y;
     const int p0 = ch * per, p1 = min(HW, p0 + per);
@@ -285,7 +285,7 @@ __global__ void se_bwd_pool_kernel(const float* x, const float* gy, int HW, int 
         float s = 0.f;
         for (int p = p0; p < p1; ++p) {
             long long i = ((long long)b * HW + p) * C + c;
-            s += gy[i] * ldv<H>(x, i);
+            s += ldv<G>(gy, i) * ldv<H>(x, i);
         }
         part[((long long)b * gridDim.y + ch) * C + c] = s;
     }
@@ -331,13 +331,14 @@ __global__ void se_fc_bwd_kernel(const float* part, int nch, int B, const float*
         gpool[idx] = s / (float)HW;
     }
 }
+template <bool G = false>
 __global__ void se_bwd_x_kernel(const float* gy, const float* sgate, const float* gpool, float* gx, int B, int HW,
                                 int C) {
     const long long n = (long long)B * HW * C;
     GRID_STRIDE(i, n) {
         const int c = (int)(i % C);
         const int b = (int)(i / ((long long)HW * C));
-        gx[i] = gy[i] * sgate[b * C + c] + gpool[b * C + c];
+        stv<G>(gx, i, ldv<G>(gy, i) * sgate[b * C + c] + gpool[b * C + c]);
     }
 }
 
@@ -414,7 +415,7 @@ __global__ void sa_mul_kernel(const float* x, const float* attn, float* y, long 
     }
 }
 // bwd 1: g_logit[p] = (sum_c gy*x) * a*(1-a)
-template <bool H = false>
+template <bool H = false, bool G = false>
 __global__ void sa_bwd_logit_kernel(const float* x, const float* gy, const float* attn, float* glogit, long long P,
                                     int C) {
     // 16 lanes per pixel (4 pixels per wave), 4 xor-shuffles
@@ -424,7 +425,7 @@ __global__ void sa_bwd_logit_kernel(const float* x, const float* gy, const float
     float s = 0.f;
     if (ok) {
         for (int c = 4 * l16; c < C; c += 64) {
-            const float4 g = *reinterpret_cast<const float4*>(gy + p * C + c);
+            const float4 g = ldv4<G>(gy, p * C + c);
             const float4 v = ldv4<H>(x, p * C + c);
             s += (g.x * v.x + g.y * v.y) + (g.z * v.z + g.w * v.w);
         }
@@ -502,6 +503,7 @@ __global__ void sa_bwd_wfinal_kernel(const float* wpart, int nb, float* gw) {
     if (threadIdx.x == 0) gw[k] += red[0];
 }
 // bwd 3: gx = gy*a + g_avg/C + [c == argmax] * g_max     (float4 over channels; argmax saved by the pool)
+template <bool G = false>
 __global__ void sa_bwd_x_kernel(const float* gy, const float* attn, const float* gpooled2, const int* amax, float* gx,
                                 long long P, int C) {
     const int C4 = C >> 2;
@@ -513,12 +515,12 @@ __global__ void sa_bwd_x_kernel(const float* gy, const float* attn, const float*
         const float gavg = gpooled2[p * 2 + 0] / (float)C;
         const float gmax = gpooled2[p * 2 + 1];
         const int mi = amax[p];
-        float4 v = reinterpret_cast<const float4*>(gy)[i];
+        float4 v = ldv4<G>(gy, 4 * i);
         v.x = v.x * a + gavg + (c == mi ? gmax : 0.f);
         v.y = v.y * a + gavg + (c + 1 == mi ? gmax : 0.f);
         v.z = v.z * a + gavg + (c + 2 == mi ? gmax : 0.f);
         v.w = v.w * a + gavg + (c + 3 == mi ? gmax : 0.f);
-        reinterpret_cast<float4*>(gx)[i] = v;
+        stv4<G>(gx, 4 * i, v);
     }
 }
 
@@ -554,30 +556,43 @@ int hyres_bilinear_fwd_f16(const void* x, int ldx, void* y, int ldy, int B, int 
                        ldy, B, Hi, Wi, Ho, Wo, C, scale_h, scale_w, 0);
     return HY_LAUNCH_CHECK("bilinear_fwd_f16");
 }
-int hyres_bilinear_bwd(const float* gy, int ldgy, float* gx, int ldgx, int B, int Hi, int Wi, int Ho, int Wo, int C,
-                       float scale_h, float scale_w, int accumulate, hyres_stream_t s) {
+extern "C++" {
+template <bool G>
+static int bilinear_bwd_impl(const float* gy, int ldgy, float* gx, int ldgx, int B, int Hi, int Wi, int Ho, int Wo, int C,
+                             float scale_h, float scale_w, int accumulate, hyres_stream_t s) {
     HY_REQUIRE(gy && gx, HYRES_E_ARG, "bilinear_bwd: NULL");
-    const bool vec = C % 4 == 0 && ldgy % 4 == 0 && ldgx % 4 == 0 && aligned16(gy) && aligned16(gx);
+    const unsigned am = G ? 7u : 15u;  // 4-element vectors: 8 B (fp16) / 16 B (fp32)
+    const bool vec = C % 4 == 0 && ldgy % 4 == 0 && ldgx % 4 == 0 && (reinterpret_cast<uintptr_t>(gy) & am) == 0 &&
+                     (reinterpret_cast<uintptr_t>(gx) & am) == 0;
     HY_REQUIRE((long long)B * Hi <= 65535 && (long long)Wi * C < (1LL << 30), HYRES_E_SHAPE, "bilinear_bwd: too large");
     const dim3 grid(ceil_div((long long)Wi * (vec ? C / 4 : C), 256), B * Hi);
-    static const int down_on = [] { const char* v = getenv("HYRES_BILINEAR_DOWN_BWD"); return (v && *v) ? atoi(v) : 1; }();
-    for (int S = 2; S <= 4 && vec && down_on; S += 2) {
+    for (int S = 2; S <= 4 && vec; S += 2) {
         if (scale_h != (float)S || scale_w != (float)S || Hi != S * Ho || Wi != S * Wo) continue;
         if (S == 2)
-            hipLaunchKernelGGL(bilinear_down_bwd_kernel<2>, grid, dim3(256), 0, as_stream(s), gy, ldgy, gx, ldgx, Hi,
-                               Wi, Ho, Wo, C, accumulate);
+            hipLaunchKernelGGL((bilinear_down_bwd_kernel<2, G>), grid, dim3(256), 0, as_stream(s), gy, ldgy, gx, ldgx,
+                               Hi, Wi, Ho, Wo, C, accumulate);
         else
-            hipLaunchKernelGGL(bilinear_down_bwd_kernel<4>, grid, dim3(256), 0, as_stream(s), gy, ldgy, gx, ldgx, Hi,
-                               Wi, Ho, Wo, C, accumulate);
+            hipLaunchKernelGGL((bilinear_down_bwd_kernel<4, G>), grid, dim3(256), 0, as_stream(s), gy, ldgy, gx, ldgx,
+                               Hi, Wi, Ho, Wo, C, accumulate);
         return HY_LAUNCH_CHECK("bilinear_down_bwd");
     }
     if (vec)
-        hipLaunchKernelGGL(bilinear_bwd_kernel<4>, grid, dim3(256), 0, as_stream(s), gy, ldgy, gx, ldgx, B, Hi, Wi, Ho,
-                           Wo, C, scale_h, scale_w, accumulate);
+        hipLaunchKernelGGL((bilinear_bwd_kernel<4, G>), grid, dim3(256), 0, as_stream(s), gy, ldgy, gx, ldgx, B, Hi, Wi,
+                           Ho, Wo, C, scale_h, scale_w, accumulate);
     else
-        hipLaunchKernelGGL(bilinear_bwd_kernel<1>, grid, dim3(256), 0, as_stream(s), gy, ldgy, gx, ldgx, B, Hi, Wi, Ho,
-                           Wo, C, scale_h, scale_w, accumulate);
+        hipLaunchKernelGGL((bilinear_bwd_kernel<1, G>), grid, dim3(256), 0, as_stream(s), gy, ldgy, gx, ldgx, B, Hi, Wi,
+                           Ho, Wo, C, scale_h, scale_w, accumulate);
     return HY_LAUNCH_CHECK("bilinear_bwd");
+}
+}  // extern "C++"
+int hyres_bilinear_bwd(const float* gy, int ldgy, float* gx, int ldgx, int B, int Hi, int Wi, int Ho, int Wo, int C,
+                       float scale_h, float scale_w, int accumulate, hyres_stream_t s) {
+    return bilinear_bwd_impl<false>(gy, ldgy, gx, ldgx, B, Hi, Wi, Ho, Wo, C, scale_h, scale_w, accumulate, s);
+}
+int hyres_bilinear_bwd_f16(const void* gy, int ldgy, void* gx, int ldgx, int B, int Hi, int Wi, int Ho, int Wo, int C,
+                           float scale_h, float scale_w, int accumulate, hyres_stream_t s) {
+    return bilinear_bwd_impl<true>((const float*)gy, ldgy, (float*)gx, ldgx, B, Hi, Wi, Ho, Wo, C, scale_h, scale_w,
+                                   accumulate, s);
 }
 
 static int se_chunks(int HW) { return std::max(1, std::min(64, (HW + 1023) / 1024)); }
@@ -632,7 +647,7 @@ int hyres_se_fwd_f16(const void* x, const float* w1, const float* w2, void* y, f
 }
 
 extern "C++" {
-template <bool H>
+template <bool H, bool G>
 static int se_bwd_impl(const float* x, const float* gy, const float* w1, const float* w2, const float* pooled,
                        const float* hidden, const float* sgate, float* gx, float* gw1, float* gw2, int B, int HW, int C,
                        int Cr, void* ws, long long ws_bytes, hyres_stream_t s) {
@@ -646,9 +661,9 @@ static int se_bwd_impl(const float* x, const float* gy, const float* w1, const f
     float* gpool = part + (long long)B * nch * C;
     hipStream_t st = as_stream(s);
     if (C % 4 == 0 && C <= 1024 && 256 % (C / 4) == 0 && aligned16(x) && aligned16(gy))
-        hipLaunchKernelGGL((se_pool4_kernel<true, H>), dim3(B, nch), dim3(256), 0, st, x, gy, HW, C, per, part);
+        hipLaunchKernelGGL((se_pool4_kernel<true, H, G>), dim3(B, nch), dim3(256), 0, st, x, gy, HW, C, per, part);
     else
-        hipLaunchKernelGGL(se_bwd_pool_kernel<H>, dim3(B, nch), dim3(256), 0, st, x, gy, HW, C, per, part);
+        hipLaunchKernelGGL((se_bwd_pool_kernel<H, G>), dim3(B, nch), dim3(256), 0, st, x, gy, HW, C, per, part);
     int rc = HY_LAUNCH_CHECK("se_bwd_pool");
     if (rc) return rc;
     hipLaunchKernelGGL(se_fc_bwd_kernel, dim3(1), dim3(256), (size_t)B * (C + Cr) * 4, st, (const float*)part, nch, B,
@@ -656,7 +671,7 @@ static int se_bwd_impl(const float* x, const float* gy, const float* w1, const f
     rc = HY_LAUNCH_CHECK("se_fc_bwd");
     if (rc) return rc;
     long long n = (long long)B * HW * C;
-    hipLaunchKernelGGL(se_bwd_x_kernel, dim3(grid_for_r(n)), dim3(256), 0, st, gy, sgate, (const float*)gpool, gx, B,
+    hipLaunchKernelGGL(se_bwd_x_kernel<G>, dim3(grid_for_r(n)), dim3(256), 0, st, gy, sgate, (const float*)gpool, gx, B,
                        HW, C);
     return HY_LAUNCH_CHECK("se_bwd_x");
 }
@@ -664,13 +679,16 @@ static int se_bwd_impl(const float* x, const float* gy, const float* w1, const f
 int hyres_se_bwd(const float* x, const float* gy, const float* w1, const float* w2, const float* pooled,
                  const float* hidden, const float* sgate, float* gx, float* gw1, float* gw2, int B, int HW, int C,
                  int Cr, void* ws, long long ws_bytes, hyres_stream_t s) {
-    return se_bwd_impl<false>(x, gy, w1, w2, pooled, hidden, sgate, gx, gw1, gw2, B, HW, C, Cr, ws, ws_bytes, s);
+    return se_bwd_impl<false, false>(x, gy, w1, w2, pooled, hidden, sgate, gx, gw1, gw2, B, HW, C, Cr, ws, ws_bytes, s);
 }
-int hyres_se_bwd_f16(const void* x, const float* gy, const float* w1, const float* w2, const float* pooled,
-                     const float* hidden, const float* sgate, float* gx, float* gw1, float* gw2, int B, int HW, int C,
-                     int Cr, void* ws, long long ws_bytes, hyres_stream_t s) {
-    return se_bwd_impl<true>((const float*)x, gy, w1, w2, pooled, hidden, sgate, gx, gw1, gw2, B, HW, C, Cr, ws,
-                             ws_bytes, s);
+int hyres_se_bwd_f16(const void* x, const void* gy, const float* w1, const float* w2, const float* pooled,
+                     const float* hidden, const float* sgate, void* gx, float* gw1, float* gw2, int B, int HW, int C,
+                     int Cr, void* ws, long long ws_bytes, int g16, hyres_stream_t s) {
+    if (g16)
+        return se_bwd_impl<true, true>((const float*)x, (const float*)gy, w1, w2, pooled, hidden, sgate, (float*)gx, gw1,
+                                       gw2, B, HW, C, Cr, ws, ws_bytes, s);
+    return se_bwd_impl<true, false>((const float*)x, (const float*)gy, w1, w2, pooled, hidden, sgate, (float*)gx, gw1,
+                                    gw2, B, HW, C, Cr, ws, ws_bytes, s);
 }
 
 static int sa_bwd_blocks(long long n) {  // >= 4 pixels per thread: the 98-tap weight fold is amortised
@@ -722,14 +740,15 @@ int hyres_spatial_attn_fwd_f16(const void* x, const float* w, float* pooled2, in
 }
 
 extern "C++" {
-template <bool HF>
+template <bool HF, bool G>
 static int spatial_attn_bwd_impl(const float* x, const float* w, const float* pooled2, const int* argmax,
                                  const float* attn, const float* gy, float* gx, float* gw, int B, int H, int W, int C,
                                  void* ws, long long ws_bytes, hyres_stream_t s) {
     HY_REQUIRE(x && w && pooled2 && argmax && attn && gy && gx && gw, HYRES_E_ARG, "spatial_attn_bwd: NULL");
-    HY_REQUIRE(C % 4 == 0 && C <= 1024 && (reinterpret_cast<uintptr_t>(x) & 7) == 0 && aligned16(gy) && aligned16(gx),
-               HYRES_E_ALIGN,
-               "spatial_attn: C %% 4 == 0 and 16B-aligned x/gy/gx required");
+    const unsigned am = G ? 7u : 15u;
+    HY_REQUIRE(C % 4 == 0 && C <= 1024 && (reinterpret_cast<uintptr_t>(x) & 7) == 0 &&
+                   (reinterpret_cast<uintptr_t>(gy) & am) == 0 && (reinterpret_cast<uintptr_t>(gx) & am) == 0,
+               HYRES_E_ALIGN, "spatial_attn: C %% 4 == 0 and aligned x/gy/gx required");
     long long P = (long long)B * H * W;
     HY_REQUIRE(ws && ws_bytes >= hyres_spatial_attn_workspace_bytes(B, H, W), HYRES_E_WORKSPACE,
                "spatial_attn_bwd: workspace");
@@ -737,8 +756,8 @@ static int spatial_attn_bwd_impl(const float* x, const float* w, const float* po
     float* gp2 = glogit + P;
     float* wpart = gp2 + 2 * P;
     hipStream_t st = as_stream(s);
-    hipLaunchKernelGGL(sa_bwd_logit_kernel<HF>, dim3((unsigned)((P + 15) / 16)), dim3(256), 0, st, x, gy, attn, glogit,
-                       P, C);
+    hipLaunchKernelGGL((sa_bwd_logit_kernel<HF, G>), dim3((unsigned)((P + 15) / 16)), dim3(256), 0, st, x, gy, attn,
+                       glogit, P, C);
     int rc = HY_LAUNCH_CHECK("sa_bwd_logit");
     if (rc) return rc;
     int nb = sa_bwd_blocks(P);
@@ -749,7 +768,7 @@ static int spatial_attn_bwd_impl(const float* x, const float* w, const float* po
     hipLaunchKernelGGL(sa_bwd_wfinal_kernel, dim3(98), dim3(256), 0, st, (const float*)wpart, nb, gw);
     rc = HY_LAUNCH_CHECK("sa_bwd_wfinal");
     if (rc) return rc;
-    hipLaunchKernelGGL(sa_bwd_x_kernel, dim3(grid_for_r(P * C / 4)), dim3(256), 0, st, gy, attn, (const float*)gp2,
+    hipLaunchKernelGGL(sa_bwd_x_kernel<G>, dim3(grid_for_r(P * C / 4)), dim3(256), 0, st, gy, attn, (const float*)gp2,
                        argmax, gx, P, C);
     return HY_LAUNCH_CHECK("sa_bwd_x");
 }
@@ -757,13 +776,16 @@ static int spatial_attn_bwd_impl(const float* x, const float* w, const float* po
 int hyres_spatial_attn_bwd(const float* x, const float* w, const float* pooled2, const int* argmax, const float* attn,
                            const float* gy, float* gx, float* gw, int B, int H, int W, int C, void* ws,
                            long long ws_bytes, hyres_stream_t s) {
-    return spatial_attn_bwd_impl<false>(x, w, pooled2, argmax, attn, gy, gx, gw, B, H, W, C, ws, ws_bytes, s);
+    return spatial_attn_bwd_impl<false, false>(x, w, pooled2, argmax, attn, gy, gx, gw, B, H, W, C, ws, ws_bytes, s);
 }
 int hyres_spatial_attn_bwd_f16(const void* x, const float* w, const float* pooled2, const int* argmax,
-                               const float* attn, const float* gy, float* gx, float* gw, int B, int H, int W, int C,
-                               void* ws, long long ws_bytes, hyres_stream_t s) {
-    return spatial_attn_bwd_impl<true>((const float*)x, w, pooled2, argmax, attn, gy, gx, gw, B, H, W, C, ws, ws_bytes,
-                                       s);
+                               const float* attn, const void* gy, void* gx, float* gw, int B, int H, int W, int C,
+                               void* ws, long long ws_bytes, int g16, hyres_stream_t s) {
+    if (g16)
+        return spatial_attn_bwd_impl<true, true>((const float*)x, w, pooled2, argmax, attn, (const float*)gy, (float*)gx,
+                                                 gw, B, H, W, C, ws, ws_bytes, s);
+    return spatial_attn_bwd_impl<true, false>((const float*)x, w, pooled2, argmax, attn, (const float*)gy, (float*)gx, gw,
+                                              B, H, W, C, ws, ws_bytes, s);
 }
 
 }  // extern "C"

@@ -1408,7 +1408,7 @@ static int reduce_lx(long long total, int nsplit) {
 // Column sums of a [P][C] (pixel stride ld) matrix, deterministic two-pass.
 // Pass 1: a block owns a row range; its 256 threads are laid out TR x TC over (rows, channel groups of
 // VEC floats) so every wave reads whole contiguous rows; the TR partial rows are folded through LDS.
-template <int VEC>
+template <int VEC, bool H = false>  // H: x stored fp16 (AMP fp16 gradients), fp32 sums
 __global__ __launch_bounds__(256) void colsum_partial_kernel(const float* x, int P, int C, int ld,
                                                              int rows_per_block, float* part) {
     __shared__ float red[256 * VEC];
@@ -1425,12 +1425,12 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const float* x, int
         for (int v = 0; v < VEC; ++v) acc[v] = 0.f;
         if (tr < TR && gi < groups) {
             for (int r = r0 + tr; r < r1; r += TR) {
-                const float* p = x + (long long)r * ld + gi * VEC;
+                const long long o = (long long)r * ld + gi * VEC;
                 if constexpr (VEC == 4) {
-                    float4 q = *reinterpret_cast<const float4*>(p);
+                    float4 q = ldv4<H>(x, o);
                     acc[0] += q.x; acc[1] += q.y; acc[2] += q.z; acc[3] += q.w;
                 } else {
-                    acc[0] += p[0];
+                    acc[0] += ldv<H>(x, o);
                 }
             }
         }
@@ -1610,13 +1610,13 @@ static hyres_wgrad_desc wgrad_swapped(const hyres_wgrad_desc* d) {
     return e;
 }
 
-// fp16 operands (desc.io_f16) the chosen kernel reads natively: the f16 MFMA kernels one of P / Q (both fp16
-// never occurs in AMP training: one side is always a gradient), the thin kernel a fp16 P; every other fp16
-// operand is converted into fp32 scratch before the launch (hyres_wgrad_workspace_bytes reserves it)
+// fp16 operands (desc.io_f16) the chosen kernel reads natively: the f16 MFMA kernels either or both (AMP training:
+// the saved activation and, with fp16 activation gradients, the gradient), the thin kernel a fp16 P; every other
+// fp16 operand is converted into fp32 scratch before the launch (hyres_wgrad_workspace_bytes reserves it)
 static int wgrad_native_io(const hyres_wgrad_desc* d, bool thin) {
     const int io = d->io_f16 & 3;
     if (!io) return 0;
-    if (wgrad_f16_ok(d)) return (io == 3 || d->square_q) ? (io & 2) : io;  // square_q: only Q is read as fp16
+    if (wgrad_f16_ok(d)) return io;
     if (thin) return io & 1;
     return 0;
 }
@@ -1747,7 +1747,6 @@ static int wgrad_issue(const hyres_wgrad_desc* d0, const float* pp, const float*
     HY_REQUIRE(d0 && pp && qq && dst, HYRES_E_ARG, "wgrad: NULL");
     const long long need = hyres_wgrad_workspace_bytes(d0);
     HY_REQUIRE(ws && ws_bytes >= need, HYRES_E_WORKSPACE, "wgrad: workspace %lld < %lld", ws_bytes, need);
-    HY_REQUIRE(!(dbias && (d0->io_f16 & 1)), HYRES_E_ARG, "wgrad: the bias gradient needs an fp32 P");
     const float* p_orig = pp;
     const bool swap = wgrad_swap(d0);
     hyres_wgrad_desc dd = swap ? wgrad_swapped(d0) : *d0;
@@ -1841,6 +1840,7 @@ static int wgrad_issue(const hyres_wgrad_desc* d0, const float* pp, const float*
         };
         if (io == 1) halo16g(std::integral_constant<int, 1>{});
         else if (io == 2) halo16g(std::integral_constant<int, 2>{});
+        else if (io == 3) halo16g(std::integral_constant<int, 3>{});
         else halo16g(std::integral_constant<int, 0>{});
     } else if (p.halo) {
         auto halo32 = [&](auto gc) {
@@ -1869,9 +1869,9 @@ static int wgrad_issue(const hyres_wgrad_desc* d0, const float* pp, const float*
             constexpr int WM2 = decltype(wm_)::value, WN2 = decltype(wn_)::value, NT_ = decltype(ntc)::value;
             constexpr int IO_ = decltype(ioc)::value;
             if (sqr) {
-                if constexpr (IO_ != 1)  // GDN: Q = x (fp16 in AMP training), P = the fp32 norm gradient
-                    hipLaunchKernelGGL((wgrad_f16_kernel<TM_, TN_, WM2, WN2, NT_, true, false, IO_>), grid, dim3(256), 0,
-                                       st, a);
+                // GDN: Q = x (fp16 in AMP training), P = the norm gradient (fp16 with AMP fp16 gradients)
+                hipLaunchKernelGGL((wgrad_f16_kernel<TM_, TN_, WM2, WN2, NT_, true, false, IO_>), grid, dim3(256), 0, st,
+                                   a);
             } else if (NT_ == 1 && one16) {
                 hipLaunchKernelGGL((wgrad_f16_kernel<TM_, TN_, WM2, WN2, 1, false, true, IO_>), grid, dim3(256), 0, st,
                                    a);
@@ -1883,6 +1883,7 @@ static int wgrad_issue(const hyres_wgrad_desc* d0, const float* pp, const float*
         auto f16 = [&](auto tm, auto tn, auto wm_, auto wn_, auto ntc) {
             if (io == 1) f16io(tm, tn, wm_, wn_, ntc, std::integral_constant<int, 1>{});
             else if (io == 2) f16io(tm, tn, wm_, wn_, ntc, std::integral_constant<int, 2>{});
+            else if (io == 3) f16io(tm, tn, wm_, wn_, ntc, std::integral_constant<int, 3>{});
             else f16io(tm, tn, wm_, wn_, ntc, std::integral_constant<int, 0>{});
         };
         using I1 = std::integral_constant<int, 1>;
@@ -1915,6 +1916,9 @@ static int wgrad_issue(const hyres_wgrad_desc* d0, const float* pp, const float*
     }
     if (dbias && swap) {  // P (= dY) is the tap-folded side here: plain column sums (own workspace after the slab)
         const int P = d0->B * d0->Hq * d0->Wq;
+        if (d0->io_f16 & 1)
+            return hyres_colsum_f16(p_orig, P, d0->M, d0->ldp, dbias, d0->accumulate, bias_ws,
+                                    hyres_colsum_workspace_bytes(P, d0->M), s);
         return hyres_colsum(p_orig, P, d0->M, d0->ldp, dbias, d0->accumulate, bias_ws,
                             hyres_colsum_workspace_bytes(P, d0->M), s);
     }
@@ -1990,15 +1994,19 @@ static int colsum_blocks(int P) {
 
 long long hyres_colsum_workspace_bytes(int P, int C) { return (long long)colsum_blocks(P) * C * 4; }
 
-int hyres_colsum(const float* x, int P, int C, int ld, float* dst, int accumulate, void* ws,
-                 long long ws_bytes, hyres_stream_t s) {
+static int colsum_impl(const float* x, int P, int C, int ld, float* dst, int accumulate, void* ws, long long ws_bytes,
+                       bool h, hyres_stream_t s) {
     HY_REQUIRE(x && dst && P > 0 && C > 0, HYRES_E_ARG, "colsum: bad args");
     const int nb = colsum_blocks(P);
     const int rows = ceil_div(P, nb);
     HY_REQUIRE(ws && ws_bytes >= (long long)nb * C * 4, HYRES_E_WORKSPACE, "colsum: workspace");
     hipStream_t st = as_stream(s);
     const bool vec = (C % 4 == 0) && (ld % 4 == 0) && aligned16(x);
-    if (vec)
+    if (vec && h)
+        hipLaunchKernelGGL((colsum_partial_kernel<4, true>), dim3(nb), dim3(256), 0, st, x, P, C, ld, rows, (float*)ws);
+    else if (h)
+        hipLaunchKernelGGL((colsum_partial_kernel<1, true>), dim3(nb), dim3(256), 0, st, x, P, C, ld, rows, (float*)ws);
+    else if (vec)
         hipLaunchKernelGGL(colsum_partial_kernel<4>, dim3(nb), dim3(256), 0, st, x, P, C, ld, rows, (float*)ws);
     else
         hipLaunchKernelGGL(colsum_partial_kernel<1>, dim3(nb), dim3(256), 0, st, x, P, C, ld, rows, (float*)ws);
@@ -2017,6 +2025,15 @@ int hyres_colsum(const float* x, int P, int C, int ld, float* dst, int accumulat
         hipLaunchKernelGGL(wgrad_reduce_kernel<4>, dim3(ceil_div(C, 16)), dim3(256), 0, st, (const float*)ws, nb, 1, C,
                            1, dst, 1, 0, 0, accumulate);
     return HY_LAUNCH_CHECK("colsum_reduce");
+}
+
+int hyres_colsum(const float* x, int P, int C, int ld, float* dst, int accumulate, void* ws,
+                 long long ws_bytes, hyres_stream_t s) {
+    return colsum_impl(x, P, C, ld, dst, accumulate, ws, ws_bytes, false, s);
+}
+int hyres_colsum_f16(const void* x, int P, int C, int ld, float* dst, int accumulate, void* ws,
+                     long long ws_bytes, hyres_stream_t s) {
+    return colsum_impl((const float*)x, P, C, ld, dst, accumulate, ws, ws_bytes, true, s);
 }
 
 }  // extern "C"

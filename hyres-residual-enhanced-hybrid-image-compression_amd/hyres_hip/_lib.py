@@ -106,6 +106,7 @@ _SIGS = {
     "hyres_wgrad_reduce_jobs": (_I, [ctypes.POINTER(WgradJob), _I, _P]),
     "hyres_colsum": (_I, [_P, _I, _I, _I, _P, _I, _P, _LL, _P]),
     "hyres_colsum_workspace_bytes": (_LL, [_I, _I]),
+    "hyres_colsum_f16": (_I, [_P, _I, _I, _I, _P, _I, _P, _LL, _P]),
     "hyres_nchw_to_nhwc": (_I, [_P, _P, _I, _I, _I, _I, _I, _P]),
     "hyres_nhwc_to_nchw": (_I, [_P, _I, _P, _I, _I, _I, _I, _P]),
     "hyres_axpby": (_I, [_P, _P, _F, _P, _LL, _P]),
@@ -117,15 +118,17 @@ _SIGS = {
     "hyres_attn_gate_fwd": (_I, [_P, _P, _P, _P, _LL, _P]),
     "hyres_attn_gate_fwd_f16": (_I, [_P, _P, _P, _P, _LL, _P]),
     "hyres_attn_gate_bwd": (_I, [_P, _P, _P, _P, _P, _LL, _P]),
-    "hyres_attn_gate_bwd_f16": (_I, [_P, _P, _P, _P, _P, _LL, _P]),
-    "hyres_relu_bwd_2d_f16": (_I, [_P, _I, _P, _I, _P, _I, _LL, _I, _P]),
-    "hyres_prelu_bwd_f16": (_I, [_P, _I, _P, _I, _P, _I, _LL, _I, _P, _P, _P, _LL, _P]),
-    "hyres_gdn_dnorm_f16": (_I, [_P, _P, _P, _P, _LL, _I, _I, _P]),
-    "hyres_se_bwd_f16": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _LL, _P]),
-    "hyres_spatial_attn_bwd_f16": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _LL, _P]),
+    "hyres_attn_gate_bwd_f16": (_I, [_P, _P, _P, _P, _P, _LL, _I, _P]),
+    "hyres_relu_bwd_2d_f16": (_I, [_P, _I, _P, _I, _P, _I, _LL, _I, _I, _P]),
+    "hyres_prelu_bwd_f16": (_I, [_P, _I, _P, _I, _P, _I, _LL, _I, _P, _P, _P, _LL, _I, _P]),
+    "hyres_gdn_dnorm_f16": (_I, [_P, _P, _P, _P, _LL, _I, _I, _I, _P]),
+    "hyres_se_bwd_f16": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _LL, _I, _P]),
+    "hyres_spatial_attn_bwd_f16": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _LL, _I, _P]),
     "hyres_accumulate": (_I, [_P, _P, _LL, _P]),
+    "hyres_accumulate_f16": (_I, [_P, _P, _LL, _P]),
     "hyres_scale": (_I, [_P, _P, _F, _P, _LL, _I, _P]),
     "hyres_add2d": (_I, [_P, _I, _P, _I, _LL, _I, _I, _P]),
+    "hyres_add2d_f16": (_I, [_P, _I, _P, _I, _LL, _I, _I, _I, _P]),
     "hyres_mul": (_I, [_P, _P, _P, _LL, _P]),
     "hyres_zero": (_I, [_P, _LL, _P]),
     "hyres_gdn_reparam_fwd": (_I, [_P, _P, _P, _P, _I, _P]),
@@ -153,6 +156,7 @@ _SIGS = {
     "hyres_eb_aux_loss": (_I, [_P, _P, _P, _P, _P, _I, _P]),
     "hyres_bilinear_fwd": (_I, [_P, _I, _P, _I, _I, _I, _I, _I, _I, _I, _F, _F, _I, _P]),
     "hyres_bilinear_bwd": (_I, [_P, _I, _P, _I, _I, _I, _I, _I, _I, _I, _F, _F, _I, _P]),
+    "hyres_bilinear_bwd_f16": (_I, [_P, _I, _P, _I, _I, _I, _I, _I, _I, _I, _F, _F, _I, _P]),
     "hyres_se_fwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _LL, _P]),
     "hyres_se_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _LL, _P]),
     "hyres_se_workspace_bytes": (_LL, [_I, _I, _I]),

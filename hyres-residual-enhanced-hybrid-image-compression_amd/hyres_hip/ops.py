@@ -103,6 +103,17 @@ class Node:
         """fp16 storage (autocast inference with fp16 activations, see ``act_f16``)."""
         return self.v.dtype == torch.float16
 
+    @property
+    def ghalf(self) -> bool:
+        """fp16 gradient storage: the gradient of an fp16 activation is fp16, as under torch autocast
+        (src/utils/engine.py:32,50-53: autograd gives an fp16 tensor an fp16 gradient); HYRES_AMP_F16_GRAD=0
+        keeps fp32 gradients for fp16 activations."""
+        return AMP_F16_GRAD and self.v.dtype == torch.float16
+
+    @property
+    def gdt(self) -> torch.dtype:
+        return torch.float16 if self.ghalf else torch.float32
+
     def slice(self, c0: int, c1: int, rg: Optional[bool] = None) -> "Node":
         return Node(self.v[..., c0:c1], self.rg if rg is None else rg, parent=self, c0=c0)
 
@@ -146,7 +157,7 @@ class Node:
         g, ld = self.pending
         self.pending = None
         tgt, acc = self.grad_target()
-        L.call("hyres_add2d", g.data_ptr(), ld, tgt.data_ptr(), self.C, self.P, self.C, acc, L.stream())
+        add2d(g, ld, tgt, self.C, self.P, self.C, acc)
 
     def grad_target_epi(self, e: "L.Epilogue"):
         """``grad_target`` for an input-gradient conv: a deferred residual gradient is folded into its
@@ -170,7 +181,7 @@ class Node:
             pg, _ = self.parent._zeroed_grad()
             return pg[..., self.c0:self.c0 + self.C], 1
         if self._g is None:
-            self._g = _empty(self.v.shape, self.v.device)
+            self._g = _empty(self.v.shape, self.v.device, self.gdt)
         acc = 1 if self.gflag else 0
         if acc:
             self.gmasked = False  # a later, unmasked contribution: the producer re-applies the mask
@@ -190,7 +201,7 @@ class Node:
             self._materialize()
         self.gmasked = False  # the caller accumulates an unmasked contribution
         if self._g is None:
-            self._g = zeros(self.v.shape, self.v.device)
+            self._g = zero_(_empty(self.v.shape, self.v.device, self.gdt))
             self.gflag = True
         elif not self.gflag:
             zero_(self._g)
@@ -200,8 +211,23 @@ class Node:
     def set_grad(self, g: torch.Tensor) -> None:
         """Seed this node's gradient (accumulating if already present)."""
         tgt, acc = self.grad_target()
-        L.call("hyres_add2d", g.data_ptr(), g.stride(2), tgt.data_ptr(), tgt.stride(2), self.P, self.C,
-               acc, L.stream())
+        add2d(g, g.stride(2), tgt, tgt.stride(2), self.P, self.C, acc)
+
+
+def add2d(x: torch.Tensor, ldx: int, y: torch.Tensor, ldy: int, P: int, C: int, acc: int) -> None:
+    """y[p, c] (+)= x[p, c] over [P][C] with pixel strides ldx / ldy, each side fp32 or fp16 (its tensor's dtype)."""
+    io = (1 if x.dtype == torch.float16 else 0) | (2 if y.dtype == torch.float16 else 0)
+    if io:
+        L.call("hyres_add2d_f16", x.data_ptr(), ldx, y.data_ptr(), ldy, P, C, acc, io, L.stream())
+    else:
+        L.call("hyres_add2d", x.data_ptr(), ldx, y.data_ptr(), ldy, P, C, acc, L.stream())
+
+
+def accumulate(x: torch.Tensor, y: torch.Tensor) -> None:
+    """y += x elementwise (same dtype)."""
+    assert x.dtype == y.dtype
+    fn = "hyres_accumulate_f16" if x.dtype == torch.float16 else "hyres_accumulate"
+    L.call(fn, x.data_ptr(), y.data_ptr(), x.numel(), L.stream())
 
 
 class Tape:
@@ -552,6 +578,8 @@ F16_ACT = os.environ.get("HYRES_F16_ACT", "1") == "1"
 # AMP training stores the f16_region's activations (forward outputs saved for backward) as fp16 too, like
 # torch autocast, whose conv outputs are fp16 tensors (src/utils/engine.py:32); gradients stay fp32
 AMP_F16_ACT = os.environ.get("HYRES_AMP_F16_ACT", "1") == "1"
+# ... and their gradients fp16 (autocast's own semantics; Node.ghalf)
+AMP_F16_GRAD = os.environ.get("HYRES_AMP_F16_GRAD", "1") == "1"
 _F16_REGION = [0]
 
 
@@ -603,7 +631,17 @@ def _launch_conv(g: L.ConvGeom, x_ptr: int, w2: torch.Tensor, ldw: int, y_ptr: i
 
 def _colsum_into(g: torch.Tensor, P: int, C: int, ld: int, dst: torch.Tensor, acc: int = 1) -> None:
     ws = _ws(L.load().hyres_colsum_workspace_bytes(P, C), g.device, slot=1)
-    L.call("hyres_colsum", g.data_ptr(), P, C, ld, dst.data_ptr(), acc, ws.data_ptr(), ws.numel(), L.stream())
+    fn = "hyres_colsum_f16" if g.dtype == torch.float16 else "hyres_colsum"
+    L.call(fn, g.data_ptr(), P, C, ld, dst.data_ptr(), acc, ws.data_ptr(), ws.numel(), L.stream())
+
+
+def _dgrad_io(gp: torch.Tensor, x: "Node") -> int:
+    """io_f16 of an input-gradient conv: X = the incoming gradient ``gp``, Y = x's gradient, the ReLU mask (x's
+    values) fp16 with Y or alone (AUX16: fp16 activation, fp32 gradient)."""
+    io = (L.IO_X16 if gp.dtype == torch.float16 else 0) | (L.IO_Y16 if x.ghalf else 0)
+    if x.half and not x.ghalf:
+        io |= L.IO_AUX16
+    return io
 
 
 class SideStream:
@@ -772,16 +810,23 @@ def _act_backward(y: Node, gy: torch.Tensor, gy_ld: int, act: int, pre: Optional
     """Gradient wrt the pre-activation (contiguous [P,C] buffer or the incoming view)."""
     if act == L.ACT_NONE or (act == L.ACT_RELU and y.gmasked):
         return gy, gy_ld
-    gp = _empty((y.B, y.H, y.W, y.C), y.device)
+    gp = _empty((y.B, y.H, y.W, y.C), y.device, gy.dtype)
+    g16 = int(gy.dtype == torch.float16)
     if act == L.ACT_RELU:
-        L.call("hyres_relu_bwd_2d_f16" if y.half else "hyres_relu_bwd_2d", y.ptr(), y.ld, gy.data_ptr(), gy_ld,
-               gp.data_ptr(), y.C, y.P, y.C, L.stream())
+        if y.half:
+            L.call("hyres_relu_bwd_2d_f16", y.ptr(), y.ld, gy.data_ptr(), gy_ld, gp.data_ptr(), y.C, y.P, y.C, g16,
+                   L.stream())
+        else:
+            L.call("hyres_relu_bwd_2d", y.ptr(), y.ld, gy.data_ptr(), gy_ld, gp.data_ptr(), y.C, y.P, y.C, L.stream())
     else:
         ws = _ws(L.load().hyres_reduce_workspace_bytes(y.P * y.C), y.device, slot=1)
         dslope = param_grad(slope) if slope.requires_grad else _empty((1,), y.device)
-        L.call("hyres_prelu_bwd_f16" if pre.dtype == torch.float16 else "hyres_prelu_bwd", pre.data_ptr(), y.C,
-               gy.data_ptr(), gy_ld, gp.data_ptr(), y.C, y.P, y.C, slope.data_ptr(), dslope.data_ptr(), ws.data_ptr(),
-               ws.numel(), L.stream())
+        if pre.dtype == torch.float16:
+            L.call("hyres_prelu_bwd_f16", pre.data_ptr(), y.C, gy.data_ptr(), gy_ld, gp.data_ptr(), y.C, y.P, y.C,
+                   slope.data_ptr(), dslope.data_ptr(), ws.data_ptr(), ws.numel(), g16, L.stream())
+        else:
+            L.call("hyres_prelu_bwd", pre.data_ptr(), y.C, gy.data_ptr(), gy_ld, gp.data_ptr(), y.C, y.P, y.C,
+                   slope.data_ptr(), dslope.data_ptr(), ws.data_ptr(), ws.numel(), L.stream())
     return gp, y.C
 
 
@@ -845,7 +890,7 @@ def conv2d(tape: Optional[Tape], x: Node, weight: torch.Tensor, bias: Optional[t
         P = y.P
         if res is not None and res.rg and not res.defer_residual(gp, gpld):
             tgt, acc = res.grad_target()
-            L.call("hyres_add2d", gp.data_ptr(), gpld, tgt.data_ptr(), res.grad_ld(), P, Co, acc, L.stream())
+            add2d(gp, gpld, tgt, res.grad_ld(), P, Co, acc)
         if wants_grad(bias) and not wants_grad(weight):
             _colsum_into(gp, P, Co, gpld, param_grad(bias))
         if wants_grad(weight):
@@ -855,7 +900,8 @@ def conv2d(tape: Optional[Tape], x: Node, weight: torch.Tensor, bias: Optional[t
             d.sm = Ci_w * KH * KW
             d.accumulate = 1
             d.f16_operands = f16 * AMP_WGRAD_F16
-            d.io_f16 = 2 if x.half else 0  # Q = the saved input activation
+            # P = the (fp16 under AMP) gradient, Q = the saved input activation
+            d.io_f16 = (1 if gp.dtype == torch.float16 else 0) | (2 if x.half else 0)
             _wgrad(d, gp.data_ptr(), x.ptr(), param_grad(weight), x.device,
                    param_grad(bias) if wants_grad(bias) else None, keep=(gp, x.v), side=True)
         if x.rg:
@@ -867,7 +913,7 @@ def conv2d(tape: Optional[Tape], x: Node, weight: torch.Tensor, bias: Optional[t
             w2d = _prepped(weight, gd, L.WPREP_CONV_DGRAD, Ci_w, Co, KH, KW, pad, mask)
             ed.accumulate = acc
             ed.f16_operands = f16
-            ed.io_f16 = L.IO_AUX16 if x.half else 0  # the ReLU mask reads x's fp16 values
+            ed.io_f16 = _dgrad_io(gp, x)
             x.relu_mask_epilogue(ed, acc)
             _launch_conv(gd, gp.data_ptr(), w2d, gd.ntaps * Co, tgt.data_ptr(), ed)
 
@@ -913,7 +959,8 @@ def deconv2d(tape: Optional[Tape], x: Node, weight: torch.Tensor, bias: Optional
             L.call("hyres_wgrad_desc_deconv2d", ctypes.byref(d), B, H, W, Ci, x.ld, Co, gpld, K, pad)
             d.accumulate = 1
             d.f16_operands = f16 * AMP_WGRAD_F16
-            d.io_f16 = 1 if x.half else 0  # P = the saved input activation
+            # P = the saved input activation, Q = the (fp16 under AMP) gradient
+            d.io_f16 = (1 if x.half else 0) | (2 if gp.dtype == torch.float16 else 0)
             _wgrad(d, x.ptr(), gp.data_ptr(), param_grad(weight), x.device, keep=(gp, x.v), side=True)
         if x.rg:
             ed = L.Epilogue()
@@ -923,7 +970,7 @@ def deconv2d(tape: Optional[Tape], x: Node, weight: torch.Tensor, bias: Optional
             w2d = _prepped(weight, gd, L.WPREP_DECONV_DGRAD, Ci, Co, K, K, pad)
             ed.accumulate = acc
             ed.f16_operands = f16
-            ed.io_f16 = L.IO_AUX16 if x.half else 0
+            ed.io_f16 = _dgrad_io(gp, x)
             x.relu_mask_epilogue(ed, acc)
             _launch_conv(gd, gp.data_ptr(), w2d, gd.ntaps * Co, tgt.data_ptr(), ed)
 
@@ -967,12 +1014,16 @@ def gdn(tape: Optional[Tape], x: Node, beta: torch.Tensor, gamma: torch.Tensor, 
             return
         gld = y.grad_ld()
         if gld != C:
-            t = _empty((x.B, x.H, x.W, C), dev)
-            L.call("hyres_add2d", gy.data_ptr(), gld, t.data_ptr(), C, y.P, C, 0, L.stream())
+            t = _empty((x.B, x.H, x.W, C), dev, gy.dtype)
+            add2d(gy, gld, t, C, y.P, C, 0)
             gy = t
-        dn = _empty((x.B, x.H, x.W, C), dev)
-        L.call("hyres_gdn_dnorm_f16" if y.half else "hyres_gdn_dnorm", gy.data_ptr(), y.ptr(), nrm.data_ptr(),
-               dn.data_ptr(), y.P, C, int(inverse), L.stream())
+        dn = _empty((x.B, x.H, x.W, C), dev, gy.dtype)  # the norm's gradient: fp16 with y's (AMP)
+        if y.half:
+            L.call("hyres_gdn_dnorm_f16", gy.data_ptr(), y.ptr(), nrm.data_ptr(), dn.data_ptr(), y.P, C, int(inverse),
+                   int(gy.dtype == torch.float16), L.stream())
+        else:
+            L.call("hyres_gdn_dnorm", gy.data_ptr(), y.ptr(), nrm.data_ptr(), dn.data_ptr(), y.P, C, int(inverse),
+                   L.stream())
         if beta.requires_grad or gamma.requires_grad:
             dgp = _empty((C, C), dev)
             d = L.WgradDesc()
@@ -980,7 +1031,7 @@ def gdn(tape: Optional[Tape], x: Node, beta: torch.Tensor, gamma: torch.Tensor, 
             d.square_q = 1
             d.accumulate = 0
             d.f16_operands = f16 * AMP_WGRAD_F16
-            d.io_f16 = 2 if x.half else 0
+            d.io_f16 = (1 if dn.dtype == torch.float16 else 0) | (2 if x.half else 0)
             _wgrad(d, dn.data_ptr(), x.ptr(), dgp, dev, defer=False)  # read by the reparam backward below
             dbp = _empty((C,), dev)
             _colsum_into(dn, y.P, C, C, dbp, acc=0)
@@ -1000,7 +1051,7 @@ def gdn(tape: Optional[Tape], x: Node, beta: torch.Tensor, gamma: torch.Tensor, 
             ed.aux2 = nrm.data_ptr()
             ed.ld2 = C
             ed.f16_operands = f16
-            ed.io_f16 = L.IO_AUX16 if x.half else 0  # x and the saved norm are fp16 (AMP training)
+            ed.io_f16 = _dgrad_io(dn, x)  # x and the saved norm fp16 (AMP training), gy / dn / x's gradient with them
             _launch_conv(gd, dn.data_ptr(), w2d, C, tgt.data_ptr(), ed)
 
     tape.push(bwd)
@@ -1027,8 +1078,12 @@ def attn_gate(tape: Optional[Tape], a: Node, b: Node, x: Node) -> Node:
         ga, acc_a = a.grad_target()
         gb, acc_b = b.grad_target()
         assert acc_a == 0 and acc_b == 0, "gate inputs are single-consumer"
-        L.call("hyres_attn_gate_bwd_f16" if a.half else "hyres_attn_gate_bwd", a.ptr(), b.ptr(), g.data_ptr(),
-               ga.data_ptr(), gb.data_ptr(), n, L.stream())
+        if a.half:
+            assert ga.dtype == gb.dtype == g.dtype
+            L.call("hyres_attn_gate_bwd_f16", a.ptr(), b.ptr(), g.data_ptr(), ga.data_ptr(), gb.data_ptr(), n,
+                   int(g.dtype == torch.float16), L.stream())
+        else:
+            L.call("hyres_attn_gate_bwd", a.ptr(), b.ptr(), g.data_ptr(), ga.data_ptr(), gb.data_ptr(), n, L.stream())
         if x.rg:
             x.set_grad(g)
 
@@ -1139,6 +1194,8 @@ def to_nchw(x: Node) -> torch.Tensor:
 
 def to_nchw_grad(x: Node) -> torch.Tensor:
     g = x.grad()
+    if g.dtype == torch.float16:  # AMP fp16 gradient: returned as fp32 NCHW
+        return g.permute(0, 3, 1, 2).float().contiguous()
     out = _empty((x.B, x.C, x.H, x.W), x.device)
     L.call("hyres_nhwc_to_nchw", g.data_ptr(), x.grad_ld(), out.data_ptr(), x.B, x.C, x.H, x.W, L.stream())
     return out

@@ -9,7 +9,7 @@ from typing import Optional
 import torch
 
 from . import _lib as L
-from .ops import Node, Tape, _empty, param_grad, _ws
+from .ops import Node, Tape, _empty, accumulate, param_grad, _ws
 
 
 def bilinear(tape: Optional[Tape], x: Node, Ho: int, Wo: int, scale_h: float, scale_w: float,
@@ -33,7 +33,9 @@ def bilinear(tape: Optional[Tape], x: Node, Ho: int, Wo: int, scale_h: float, sc
         if g is None or not x.rg:
             return
         tgt, acc = x.grad_target()
-        L.call("hyres_bilinear_bwd", g.data_ptr(), y.grad_ld(), tgt.data_ptr(), x.grad_ld(), x.B, x.H, x.W, Ho, Wo,
+        assert g.dtype == tgt.dtype
+        fn = "hyres_bilinear_bwd_f16" if g.dtype == torch.float16 else "hyres_bilinear_bwd"  # AMP fp16 gradients
+        L.call(fn, g.data_ptr(), y.grad_ld(), tgt.data_ptr(), x.grad_ld(), x.B, x.H, x.W, Ho, Wo,
                x.C, float(scale_h), float(scale_w), acc, L.stream())
 
     tape.push(bwd)
@@ -66,14 +68,19 @@ def se_block(tape: Optional[Tape], x: Node, w1: torch.Tensor, w2: torch.Tensor) 
         gw1 = param_grad(w1)
         gw2 = param_grad(w2)
         tgt, acc = x.grad_target()
-        gx = tgt if acc == 0 else _empty((x.B, x.H, x.W, C), dev)
+        assert g.dtype == tgt.dtype
+        gx = tgt if acc == 0 else _empty((x.B, x.H, x.W, C), dev, tgt.dtype)
         ws2 = _ws(wsb + B * C * 4, dev, slot=1)
-        L.call("hyres_se_bwd_f16" if x.half else "hyres_se_bwd", x.ptr(), g.data_ptr(), w1.data_ptr(),
-               w2.data_ptr(), pooled.data_ptr(),
-               hidden.data_ptr(), sgate.data_ptr(), gx.data_ptr(), gw1.data_ptr(), gw2.data_ptr(), B, HW, C, Cr,
-               ws2.data_ptr(), ws2.numel(), L.stream())
+        if x.half:
+            L.call("hyres_se_bwd_f16", x.ptr(), g.data_ptr(), w1.data_ptr(), w2.data_ptr(), pooled.data_ptr(),
+                   hidden.data_ptr(), sgate.data_ptr(), gx.data_ptr(), gw1.data_ptr(), gw2.data_ptr(), B, HW, C, Cr,
+                   ws2.data_ptr(), ws2.numel(), int(g.dtype == torch.float16), L.stream())
+        else:
+            L.call("hyres_se_bwd", x.ptr(), g.data_ptr(), w1.data_ptr(), w2.data_ptr(), pooled.data_ptr(),
+                   hidden.data_ptr(), sgate.data_ptr(), gx.data_ptr(), gw1.data_ptr(), gw2.data_ptr(), B, HW, C, Cr,
+                   ws2.data_ptr(), ws2.numel(), L.stream())
         if acc:
-            L.call("hyres_accumulate", gx.data_ptr(), tgt.data_ptr(), gx.numel(), L.stream())
+            accumulate(gx, tgt)
 
     tape.push(bwd)
     return y
@@ -100,16 +107,21 @@ def spatial_attention_mul(tape: Optional[Tape], x: Node, w: torch.Tensor) -> Nod
             return
         assert y.grad_ld() == C
         tgt, acc = x.grad_target()
-        gx = tgt if acc == 0 else _empty((B, H, W, C), dev)
+        assert g.dtype == tgt.dtype
+        gx = tgt if acc == 0 else _empty((B, H, W, C), dev, tgt.dtype)
         gw = param_grad(w) if w.requires_grad else _empty(w.shape, dev)
         wsb = L.load().hyres_spatial_attn_workspace_bytes(B, H, W)
         ws = _ws(wsb, dev, slot=1)
-        L.call("hyres_spatial_attn_bwd_f16" if x.half else "hyres_spatial_attn_bwd", x.ptr(), w.data_ptr(),
-               pooled2.data_ptr(), argmax.data_ptr(),
-               attn.data_ptr(), g.data_ptr(), gx.data_ptr(), gw.data_ptr(), B, H, W, C, ws.data_ptr(), ws.numel(),
-               L.stream())
+        if x.half:
+            L.call("hyres_spatial_attn_bwd_f16", x.ptr(), w.data_ptr(), pooled2.data_ptr(), argmax.data_ptr(),
+                   attn.data_ptr(), g.data_ptr(), gx.data_ptr(), gw.data_ptr(), B, H, W, C, ws.data_ptr(), ws.numel(),
+                   int(g.dtype == torch.float16), L.stream())
+        else:
+            L.call("hyres_spatial_attn_bwd", x.ptr(), w.data_ptr(), pooled2.data_ptr(), argmax.data_ptr(),
+                   attn.data_ptr(), g.data_ptr(), gx.data_ptr(), gw.data_ptr(), B, H, W, C, ws.data_ptr(), ws.numel(),
+                   L.stream())
         if acc:
-            L.call("hyres_accumulate", gx.data_ptr(), tgt.data_ptr(), gx.numel(), L.stream())
+            accumulate(gx, tgt)
 
     tape.push(bwd)
     return y

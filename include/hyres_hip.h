@@ -224,6 +224,9 @@ int hyres_wgrad_reduce_jobs(const hyres_wgrad_job* jobs, int n, hyres_stream_t s
 int hyres_colsum(const float* x, int P, int C, int ld, float* dst, int accumulate, void* workspace,
                  long long ws_bytes, hyres_stream_t s);
 long long hyres_colsum_workspace_bytes(int P, int C);
+/* the same over a fp16 x (AMP fp16 gradients), fp32 sums */
+int hyres_colsum_f16(const void* x, int P, int C, int ld, float* dst, int accumulate, void* workspace,
+                     long long ws_bytes, hyres_stream_t s);
 
 /* ------------------------------------------------------------------------------------------ */
 /* layout / elementwise                                                                       */
@@ -254,19 +257,26 @@ int hyres_attn_gate_fwd_f16(const void* a, const void* b, const void* x, void* o
 int hyres_attn_gate_bwd(const float* a, const float* b, const float* g, float* ga, float* gb,
                         long long n, hyres_stream_t s);
 /* Backward passes with fp16 SAVED activations (AMP training: the forward wrote y / pre / a, b / x / norm as
- * fp16; gradients stay fp32; fp32 arithmetic; 8B-aligned fp16 operands): same semantics as the fp32
- * entry points of the same name without the suffix. */
-int hyres_relu_bwd_2d_f16(const void* y, int ldy_, const float* g, int ldg, float* gx, int ldgx, long long P,
-                          int C, hyres_stream_t s);
-int hyres_prelu_bwd_f16(const void* x, int ldx, const float* g, int ldg, float* gx, int ldgx, long long P,
-                        int C, const float* slope, float* dslope, void* ws, long long ws_bytes, hyres_stream_t s);
-int hyres_attn_gate_bwd_f16(const void* a, const void* b, const float* g, float* ga, float* gb, long long n,
+ * fp16; fp32 arithmetic; 8B-aligned fp16 operands): same semantics as the fp32 entry points of the same name
+ * without the suffix. g16 = 1: the gradients in and out (g, gx / ga, gb) are fp16 as well — autocast's own
+ * semantics inside the f16 region (the gradient of an fp16 tensor is fp16, src/utils/engine.py:32,50-53);
+ * g16 = 0: fp32 gradients. */
+int hyres_relu_bwd_2d_f16(const void* y, int ldy_, const void* g, int ldg, void* gx, int ldgx, long long P,
+                          int C, int g16, hyres_stream_t s);
+int hyres_prelu_bwd_f16(const void* x, int ldx, const void* g, int ldg, void* gx, int ldgx, long long P,
+                        int C, const float* slope, float* dslope, void* ws, long long ws_bytes, int g16,
+                        hyres_stream_t s);
+int hyres_attn_gate_bwd_f16(const void* a, const void* b, const void* g, void* ga, void* gb, long long n, int g16,
                             hyres_stream_t s);
-/* y (+)= x  (gradient fan-in) */
+/* y (+)= x  (gradient fan-in); _f16: both fp16 */
 int hyres_accumulate(const float* x, float* y, long long n, hyres_stream_t s);
+int hyres_accumulate_f16(const void* x, void* y, long long n, hyres_stream_t s);
 /* y[p*ldy + c] (+)= x[p*ldx + c]  over P pixels x C channels (strided gradient fan-in / copy) */
 int hyres_add2d(const float* x, int ldx, float* y, int ldy, long long P, int C, int accumulate,
                 hyres_stream_t s);
+/* the same with fp16 storage: io bit 0 = x fp16, bit 1 = y fp16 (fp32 add) */
+int hyres_add2d_f16(const void* x, int ldx, void* y, int ldy, long long P, int C, int accumulate, int io,
+                    hyres_stream_t s);
 /* y = a * b elementwise (in-place allowed: CheckboardMaskedConv2d's weight.data *= mask) */
 int hyres_mul(const float* a, const float* b, float* y, long long n, hyres_stream_t s);
 /* stream-ordered memset 0 (hipMemsetAsync) */
@@ -285,9 +295,9 @@ int hyres_gdn_reparam_bwd(const float* beta, const float* gamma, const float* db
 /* GDN backward helper: dn = g * y / n * (-0.5 GDN | +0.5 IGDN) */
 int hyres_gdn_dnorm(const float* g, const float* y, const float* n, float* dn, long long P, int C,
                     int inverse, hyres_stream_t s);
-/* the same with fp16 y and n (AMP training) */
-int hyres_gdn_dnorm_f16(const float* g, const void* y, const void* n, float* dn, long long P, int C,
-                        int inverse, hyres_stream_t s);
+/* the same with fp16 y and n (AMP training); g16: g and dn fp16 too */
+int hyres_gdn_dnorm_f16(const void* g, const void* y, const void* n, void* dn, long long P, int C,
+                        int inverse, int g16, hyres_stream_t s);
 
 /* ------------------------------------------------------------------------------------------ */
 /* quantisation, checkerboard context, entropy models                                         */
@@ -380,13 +390,17 @@ int hyres_se_fwd_f16(const void* x, const float* w1, const float* w2, void* y, f
                      float* sgate, int B, int HW, int C, int Cr, void* ws, long long ws_bytes, hyres_stream_t s);
 int hyres_spatial_attn_fwd_f16(const void* x, const float* w, float* pooled2, int* argmax, float* attn,
                                void* y, int B, int H, int W, int C, hyres_stream_t s);
-/* their backward passes with fp16 x (AMP training; gy, gx fp32) */
-int hyres_se_bwd_f16(const void* x, const float* gy, const float* w1, const float* w2, const float* pooled,
-                     const float* hidden, const float* sgate, float* gx, float* gw1, float* gw2, int B, int HW,
-                     int C, int Cr, void* ws, long long ws_bytes, hyres_stream_t s);
+/* their backward passes with fp16 x (AMP training); g16 = 1: gy, gx fp16 too (autocast's fp16 activation
+ * gradients), g16 = 0: gy, gx fp32. Weight gradients fp32. */
+int hyres_se_bwd_f16(const void* x, const void* gy, const float* w1, const float* w2, const float* pooled,
+                     const float* hidden, const float* sgate, void* gx, float* gw1, float* gw2, int B, int HW,
+                     int C, int Cr, void* ws, long long ws_bytes, int g16, hyres_stream_t s);
 int hyres_spatial_attn_bwd_f16(const void* x, const float* w, const float* pooled2, const int* argmax,
-                               const float* attn, const float* gy, float* gx, float* gw, int B, int H, int W,
-                               int C, void* ws, long long ws_bytes, hyres_stream_t s);
+                               const float* attn, const void* gy, void* gx, float* gw, int B, int H, int W,
+                               int C, void* ws, long long ws_bytes, int g16, hyres_stream_t s);
+/* bilinear backward over fp16 gy / gx (AMP fp16 gradients; fp32 sums; 8B-aligned when C % 4 == 0) */
+int hyres_bilinear_bwd_f16(const void* gy, int ldgy, void* gx, int ldgx, int B, int Hi, int Wi, int Ho, int Wo,
+                           int C, float scale_h, float scale_w, int accumulate, hyres_stream_t s);
 
 /* ------------------------------------------------------------------------------------------ */
 /* losses and optimiser (src/losses/rd_loss.py:18-44, src/utils/engine.py:56-90)              */

@@ -1,6 +1,7 @@
 """AMP training with fp16 SAVED activations (``ops.AMP_F16_ACT``): inside an ``f16_region`` the forward outputs
 that backward reads are stored as fp16 in HBM — as torch autocast's conv outputs are fp16 tensors
-(/root/reference/src/utils/engine.py:32, train.sh:19 ``--mixed-precision``) — while gradients stay fp32.
+(/root/reference/src/utils/engine.py:32, train.sh:19 ``--mixed-precision``) — and (``ops.AMP_F16_GRAD``, round 4)
+their gradients are fp16 as well, as autograd gives an fp16 tensor an fp16 gradient.
 
 Why exact comparisons are possible: every kernel computes in fp32 from its operands; the fp16-storage
 variants only change how a saved activation is read (8-byte loads of 4 halves, converted exactly) or how
@@ -72,25 +73,25 @@ checked to 1e-6."""
 
     gx = torch.empty(P, C, device=D)
     yh = y.half()
-    pair("hyres_relu_bwd_2d", (yh.data_ptr(), C, g.data_ptr(), C, gx.data_ptr(), C, P, C, s),
+    pair("hyres_relu_bwd_2d", (yh.data_ptr(), C, g.data_ptr(), C, gx.data_ptr(), C, P, C, 0, s),
          (y.data_ptr(), C, g.data_ptr(), C, gx.data_ptr(), C, P, C, s), [gx])
     slope = torch.tensor([0.25], device=D)
     dslope = torch.zeros(1, device=D)
     ws = torch.empty(int(L.load().hyres_reduce_workspace_bytes(P * C)), dtype=torch.uint8, device=D)
     pair("hyres_prelu_bwd", (yh.data_ptr(), C, g.data_ptr(), C, gx.data_ptr(), C, P, C, slope.data_ptr(),
-                             dslope.data_ptr(), ws.data_ptr(), ws.numel(), s),
+                             dslope.data_ptr(), ws.data_ptr(), ws.numel(), 0, s),
          (y.data_ptr(), C, g.data_ptr(), C, gx.data_ptr(), C, P, C, slope.data_ptr(), dslope.data_ptr(),
           ws.data_ptr(), ws.numel(), s), [gx, dslope], tol=[0, 1e-6])
     b = _h(_rand((P, C), 3)).to(D)
     bh = b.half()
     ga, gb = torch.empty(P, C, device=D), torch.empty(P, C, device=D)
-    pair("hyres_attn_gate_bwd", (yh.data_ptr(), bh.data_ptr(), g.data_ptr(), ga.data_ptr(), gb.data_ptr(), P * C, s),
+    pair("hyres_attn_gate_bwd", (yh.data_ptr(), bh.data_ptr(), g.data_ptr(), ga.data_ptr(), gb.data_ptr(), P * C, 0, s),
          (y.data_ptr(), b.data_ptr(), g.data_ptr(), ga.data_ptr(), gb.data_ptr(), P * C, s), [ga, gb])
     nrm = _h(_rand((P, C), 4).abs() + 0.5).to(D)
     nh = nrm.half()
     dn = torch.empty(P, C, device=D)
     for inv in (0, 1):
-        pair("hyres_gdn_dnorm", (g.data_ptr(), yh.data_ptr(), nh.data_ptr(), dn.data_ptr(), P, C, inv, s),
+        pair("hyres_gdn_dnorm", (g.data_ptr(), yh.data_ptr(), nh.data_ptr(), dn.data_ptr(), P, C, inv, 0, s),
              (g.data_ptr(), y.data_ptr(), nrm.data_ptr(), dn.data_ptr(), P, C, inv, s), [dn])
     # SE / spatial attention: run the fp32 forward on the fp16-representable x for the saved state, then both
     # backward flavours
@@ -106,7 +107,7 @@ checked to 1e-6."""
     gw1, gw2 = torch.zeros(Cr, C, device=D), torch.zeros(C, Cr, device=D)
     pair("hyres_se_bwd", (yh.data_ptr(), g.data_ptr(), w1.data_ptr(), w2.data_ptr(), pooled.data_ptr(),
                           hidden.data_ptr(), sgate.data_ptr(), gx.data_ptr(), gw1.data_ptr(), gw2.data_ptr(), B, H * W,
-                          C, Cr, ws.data_ptr(), ws.numel(), s),
+                          C, Cr, ws.data_ptr(), ws.numel(), 0, s),
          (y.data_ptr(), g.data_ptr(), w1.data_ptr(), w2.data_ptr(), pooled.data_ptr(), hidden.data_ptr(),
           sgate.data_ptr(), gx.data_ptr(), gw1.data_ptr(), gw2.data_ptr(), B, H * W, C, Cr, ws.data_ptr(),
           ws.numel(), s), [gx, gw1, gw2])
@@ -122,9 +123,132 @@ checked to 1e-6."""
     ws = torch.empty(wsb, dtype=torch.uint8, device=D)
     pair("hyres_spatial_attn_bwd", (yh.data_ptr(), wsa.data_ptr(), pooled2.data_ptr(), amax.data_ptr(),
                                     attn.data_ptr(), g.data_ptr(), gx.data_ptr(), gw.data_ptr(), B, H, W, C,
-                                    ws.data_ptr(), ws.numel(), s),
+                                    ws.data_ptr(), ws.numel(), 0, s),
          (y.data_ptr(), wsa.data_ptr(), pooled2.data_ptr(), amax.data_ptr(), attn.data_ptr(), g.data_ptr(),
           gx.data_ptr(), gw.data_ptr(), B, H, W, C, ws.data_ptr(), ws.numel(), s), [gx, gw], tol=[1e-6, 1e-6])
+
+
+def test_f16_gradient_backward_entry_points_match_rounded_fp32():
+    """g16 = 1 (AMP fp16 activation gradients, autocast's own semantics): the same entry points with the incoming
+    gradient and the produced gradients fp16. Every kernel computes in fp32 from exactly converted operands and
+    rounds its output once, so on fp16-representable inputs each fp16 gradient equals the fp32 entry point's
+    result rounded to fp16, BIT FOR BIT (weight / slope gradients stay fp32: 1e-6 where FMA contraction may
+    differ). Also the fp16 add2d / accumulate / colsum / bilinear-backward entry points against fp32."""
+    from hyres_hip import _lib as L
+    D = dev()
+    B, H, W, C = 2, 16, 24, 64
+    P = B * H * W
+    s = L.stream()
+    y = _h(_rand((P, C), 1)).to(D)
+    yh = y.half()
+    g = _h(_rand((P, C), 2)).to(D)
+    gh = g.half()
+
+    def check(got16, want32, what):
+        want = want32.half()
+        if not torch.equal(got16, want):
+            bad = (got16 != want).nonzero()
+            print(what, "mismatches", bad.shape[0], got16[tuple(bad[0])].item(), want[tuple(bad[0])].item())
+        assert torch.equal(got16, want), what
+
+    gx32, gx16 = torch.empty(P, C, device=D), torch.empty(P, C, device=D, dtype=torch.float16)
+    L.call("hyres_relu_bwd_2d", y.data_ptr(), C, g.data_ptr(), C, gx32.data_ptr(), C, P, C, s)
+    L.call("hyres_relu_bwd_2d_f16", yh.data_ptr(), C, gh.data_ptr(), C, gx16.data_ptr(), C, P, C, 1, s)
+    check(gx16, gx32, "relu")
+    slope = torch.tensor([0.25], device=D)
+    d32, d16 = torch.zeros(1, device=D), torch.zeros(1, device=D)
+    ws = torch.empty(int(L.load().hyres_reduce_workspace_bytes(P * C)), dtype=torch.uint8, device=D)
+    L.call("hyres_prelu_bwd", y.data_ptr(), C, g.data_ptr(), C, gx32.data_ptr(), C, P, C, slope.data_ptr(),
+           d32.data_ptr(), ws.data_ptr(), ws.numel(), s)
+    L.call("hyres_prelu_bwd_f16", yh.data_ptr(), C, gh.data_ptr(), C, gx16.data_ptr(), C, P, C, slope.data_ptr(),
+           d16.data_ptr(), ws.data_ptr(), ws.numel(), 1, s)
+    check(gx16, gx32, "prelu")
+    assert rel_err(d16.cpu(), d32.cpu()) <= 1e-6
+    b = _h(_rand((P, C), 3)).to(D)
+    bh = b.half()
+    ga32, gb32 = torch.empty(P, C, device=D), torch.empty(P, C, device=D)
+    ga16, gb16 = torch.empty_like(gx16), torch.empty_like(gx16)
+    L.call("hyres_attn_gate_bwd", y.data_ptr(), b.data_ptr(), g.data_ptr(), ga32.data_ptr(), gb32.data_ptr(), P * C, s)
+    L.call("hyres_attn_gate_bwd_f16", yh.data_ptr(), bh.data_ptr(), gh.data_ptr(), ga16.data_ptr(), gb16.data_ptr(),
+           P * C, 1, s)
+    check(ga16, ga32, "gate a")
+    check(gb16, gb32, "gate b")
+    nrm = _h(_rand((P, C), 4).abs() + 0.5).to(D)
+    for inv in (0, 1):
+        L.call("hyres_gdn_dnorm", g.data_ptr(), y.data_ptr(), nrm.data_ptr(), gx32.data_ptr(), P, C, inv, s)
+        L.call("hyres_gdn_dnorm_f16", gh.data_ptr(), yh.data_ptr(), nrm.half().data_ptr(), gx16.data_ptr(), P, C, inv,
+               1, s)
+        check(gx16, gx32, f"gdn dnorm inv={inv}")
+    # add2d with every storage combination, accumulate on and off
+    for io in (1, 2, 3):
+        for acc in (0, 1):
+            base = _h(_rand((P, C), 5)).to(D)
+            dst32 = base.clone()
+            L.call("hyres_add2d", g.data_ptr(), C, dst32.data_ptr(), C, P, C, acc, s)
+            src = gh if io & 1 else g
+            dst = base.half() if io & 2 else base.clone()
+            L.call("hyres_add2d_f16", src.data_ptr(), C, dst.data_ptr(), C, P, C, acc, io, s)
+            if io & 2:
+                check(dst, dst32, f"add2d io={io} acc={acc}")
+            else:
+                assert torch.equal(dst, dst32), (io, acc)
+    acc16 = y.half()
+    L.call("hyres_accumulate_f16", gh.data_ptr(), acc16.data_ptr(), P * C, s)
+    check(acc16, y + g, "accumulate")
+    # bias column sums over a fp16 gradient: the same sums as over its fp32 copy, bit for bit
+    c32, c16 = torch.zeros(C, device=D), torch.zeros(C, device=D)
+    wsc = torch.empty(int(L.load().hyres_colsum_workspace_bytes(P, C)), dtype=torch.uint8, device=D)
+    L.call("hyres_colsum", g.data_ptr(), P, C, C, c32.data_ptr(), 0, wsc.data_ptr(), wsc.numel(), s)
+    L.call("hyres_colsum_f16", gh.data_ptr(), P, C, C, c16.data_ptr(), 0, wsc.data_ptr(), wsc.numel(), s)
+    torch.cuda.synchronize()
+    assert torch.equal(c16, c32)
+    # bilinear backward (general gather and the exact x1/2 down-sampling kernel), accumulate on
+    for (Hi, Wi, Ho, Wo, sc) in ((H, W, 2 * H, 2 * W, 0.5), (H, W, H // 2, W // 2, 2.0)):
+        gy = _h(_rand((B * Ho * Wo, C), 6)).to(D)
+        base = _h(_rand((P, C), 7)).to(D)
+        o32, o16 = base.clone(), base.half()
+        L.call("hyres_bilinear_bwd", gy.data_ptr(), C, o32.data_ptr(), C, B, Hi, Wi, Ho, Wo, C, sc, sc, 1, s)
+        L.call("hyres_bilinear_bwd_f16", gy.half().data_ptr(), C, o16.data_ptr(), C, B, Hi, Wi, Ho, Wo, C, sc, sc, 1, s)
+        check(o16, o32, f"bilinear bwd {Ho}x{Wo}")
+    # SE / spatial attention backward with fp16 gy / gx
+    Cr = 4
+    w1 = _rand((Cr, C), 5, 0.2).to(D)
+    w2 = _rand((C, Cr), 6, 0.2).to(D)
+    pooled, hidden, sgate = (torch.empty(B, C, device=D), torch.empty(B, Cr, device=D), torch.empty(B, C, device=D))
+    yse = torch.empty(P, C, device=D)
+    wsb = int(L.load().hyres_se_workspace_bytes(B, H * W, C)) + B * C * 4
+    ws = torch.empty(wsb, dtype=torch.uint8, device=D)
+    L.call("hyres_se_fwd", y.data_ptr(), w1.data_ptr(), w2.data_ptr(), yse.data_ptr(), pooled.data_ptr(),
+           hidden.data_ptr(), sgate.data_ptr(), B, H * W, C, Cr, ws.data_ptr(), ws.numel(), s)
+    gws = [torch.zeros(Cr, C, device=D), torch.zeros(C, Cr, device=D), torch.zeros(Cr, C, device=D),
+           torch.zeros(C, Cr, device=D)]
+    L.call("hyres_se_bwd", y.data_ptr(), g.data_ptr(), w1.data_ptr(), w2.data_ptr(), pooled.data_ptr(),
+           hidden.data_ptr(), sgate.data_ptr(), gx32.data_ptr(), gws[0].data_ptr(), gws[1].data_ptr(), B, H * W, C, Cr,
+           ws.data_ptr(), ws.numel(), s)
+    L.call("hyres_se_bwd_f16", yh.data_ptr(), gh.data_ptr(), w1.data_ptr(), w2.data_ptr(), pooled.data_ptr(),
+           hidden.data_ptr(), sgate.data_ptr(), gx16.data_ptr(), gws[2].data_ptr(), gws[3].data_ptr(), B, H * W, C, Cr,
+           ws.data_ptr(), ws.numel(), 1, s)
+    check(gx16, gx32, "se gx")
+    assert rel_err(gws[2].cpu(), gws[0].cpu()) <= 1e-6 and rel_err(gws[3].cpu(), gws[1].cpu()) <= 1e-6
+    wsa = _rand((1, 2, 7, 7), 7, 0.1).to(D)
+    pooled2 = torch.empty(P, 2, device=D)
+    amax = torch.empty(P, dtype=torch.int32, device=D)
+    attn = torch.empty(P, device=D)
+    ysa = torch.empty(P, C, device=D)
+    L.call("hyres_spatial_attn_fwd", y.data_ptr(), wsa.data_ptr(), pooled2.data_ptr(), amax.data_ptr(),
+           attn.data_ptr(), ysa.data_ptr(), B, H, W, C, s)
+    gw32, gw16 = torch.zeros(1, 2, 7, 7, device=D), torch.zeros(1, 2, 7, 7, device=D)
+    wsb = int(L.load().hyres_spatial_attn_workspace_bytes(B, H, W))
+    ws = torch.empty(wsb, dtype=torch.uint8, device=D)
+    L.call("hyres_spatial_attn_bwd", y.data_ptr(), wsa.data_ptr(), pooled2.data_ptr(), amax.data_ptr(),
+           attn.data_ptr(), g.data_ptr(), gx32.data_ptr(), gw32.data_ptr(), B, H, W, C, ws.data_ptr(), ws.numel(), s)
+    L.call("hyres_spatial_attn_bwd_f16", yh.data_ptr(), wsa.data_ptr(), pooled2.data_ptr(), amax.data_ptr(),
+           attn.data_ptr(), gh.data_ptr(), gx16.data_ptr(), gw16.data_ptr(), B, H, W, C, ws.data_ptr(), ws.numel(), 1,
+           s)
+    torch.cuda.synchronize()
+    # the logit sums may contract differently (1 ulp): gx within one fp16 ulp of the rounded fp32 result
+    assert (gx16.float() - gx32.half().float()).abs().max() <= 1e-3 * gx32.abs().max()
+    assert rel_err(gw16.cpu(), gw32.cpu()) <= 1e-6
 
 
 # ------------------------------------------------------------------------------------------ conv layers
@@ -172,7 +296,7 @@ def test_layer_with_fp16_input_matches_fp32_storage(case, wgrad_f16, monkeypatch
             else:
                 yn = O.deconv2d(tape, xn, wd, bd)
         assert yn.half == (f16_act and Co > 4)
-        gy = _rand((yn.B, yn.C, yn.H, yn.W), 14).to(D)
+        gy = _h(_rand((yn.B, yn.C, yn.H, yn.W), 14)).to(D)  # fp16-representable: the fp16 gradient holds it exactly
         y = O.to_nchw(yn)
         yn.set_grad(O.nchw_grad_to_nhwc(gy))
         tape.backward()
@@ -182,7 +306,8 @@ def test_layer_with_fp16_input_matches_fp32_storage(case, wgrad_f16, monkeypatch
     print(case, "forward fp16-stored vs fp32:", rel_err(y16.cpu(), y32.cpu()),
           "vs fp32 rounded:", rel_err(y16.cpu(), y32.half().float().cpu()))
     assert rel_err(y16.cpu(), y32.cpu()) < 1e-3  # one fp16 rounding of the same fp32 value (+ summation order)
-    assert torch.equal(gx16, gx32)
+    # fp16 activation gradients (O.AMP_F16_GRAD): x's gradient is the fp32 layer's, rounded once to fp16
+    assert torch.equal(gx16, gx32.half().float() if O.AMP_F16_GRAD else gx32)
     assert torch.equal(gw16, gw32)
     assert torch.equal(gb16, gb32)
 
@@ -244,14 +369,18 @@ def test_residual_unit_chain_fp16_activations_vs_torch():
     wd = [w.double().requires_grad_() for w in ws]
     bd = [b.double().requires_grad_() for b in bs]
 
-    class Round(torch.autograd.Function):  # fp16 storage of a forward output; gradients pass unrounded
+    g16 = O.AMP_F16_GRAD
+
+    class Round(torch.autograd.Function):
+        """fp16 storage of a forward output; its gradient is stored fp16 too (O.AMP_F16_GRAD: autocast's fp16
+        activation gradients), i.e. rounded where the HIP path stores it."""
         @staticmethod
         def forward(ctx, t):
             return r16(t)
 
         @staticmethod
         def backward(ctx, g):
-            return g
+            return r16(g) if g16 else g
 
     class Conv16(torch.autograd.Function):
         """f16-MFMA conv: fp16 operands in every GEMM (forward: x, w; backward: the incoming gradient and w /
@@ -297,7 +426,8 @@ def test_residual_unit_chain_fp16_activations_vs_torch():
     print("chain a1", rel_err(O.to_nchw(a1).cpu(), t1.detach().float()), "a2",
           rel_err(O.to_nchw(a2).cpu(), t2.detach().float()), "y", rel_err(yh.cpu(), y.detach().float()))
     assert rel_err(yh.cpu(), y.detach().float()) < 2e-3  # max-norm: one fp16 ulp of the largest |y|
-    assert rel_err(O.to_nchw_grad(xn).cpu(), xd.grad.float()) < 1e-4
+    # x's gradient (conv path + residual path, summed in fp32) is stored fp16 with fp16 gradients: one rounding
+    assert rel_err(O.to_nchw_grad(xn).cpu(), xd.grad.float()) < (1e-3 if g16 else 1e-4)
     for i in range(3):
         assert rel_err(wp[i].grad.cpu(), wd[i].grad.float()) < 1e-4, i
         assert rel_err(bp[i].grad.cpu(), bd[i].grad.float()) < 1e-4, i
