@@ -468,15 +468,14 @@ def main():
     # N > 1: the captured forward/backward graph replays, then the flat gradients are all-reduced in two
     # 32 MB RCCL buckets (measured at N=1: 44.5 ms graph vs 49 ms for the eager step whose all-reduce
     # overlaps backward — the eager host enqueue costs more than an unoverlapped 41.5 MB all-reduce over
-    # xGMI). HYRES_DIST_OVERLAP=1 (or --no-graph) selects the eager overlapped path.
+    # xGMI). HYRES_DIST_MODE=eager-overlap (or --no-graph) selects the eager overlapped path.
     dist_mode = None
     if dist:
         # default "graph+allreduce": replay, then the flat gradient in 32 MB buckets. "graph+overlap"
         # (HYRES_DIST_MODE) starts each segment's all-reduce from an external event the replay records at its
         # backward-progress marker (ddp.FlatGradReducer.reduce_graphed) — opt-in only: its one multi-rank
         # rehearsal ran 9x slower than graph+allreduce; eager-overlap = the eager step
-        overlap = args.no_graph or os.environ.get("HYRES_DIST_OVERLAP") == "1"
-        dist_mode = "eager-overlap" if overlap else os.environ.get("HYRES_DIST_MODE", "graph+allreduce")
+        dist_mode = "eager-overlap" if args.no_graph else os.environ.get("HYRES_DIST_MODE", "graph+allreduce")
         assert dist_mode in ("eager-overlap", "graph+overlap", "graph+allreduce"), dist_mode
     if dist:
         # RCCL all-reduce of refine / g_s / hyperprior gradient segments launched from backward-progress

@@ -851,7 +851,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_halo_f16_kernel(const ConvArgs
 constexpr int WRES_LDS_B = 2 * 9 * 64 * HALO_PH;  // halves: [chunk][tap][co][40]
 constexpr int WRES_HV = (HALO_E + 511) / 512;     // halo float4 per thread per chunk (7)
 
-template <int IO, int V = 1>
+template <int IO>
 __global__ __launch_bounds__(512, 2) void conv3x3_wres_f16_kernel(const ConvArgs a, int ntiles, int groups) {
     constexpr bool XH = (IO & 1) != 0, YH = (IO & 2) != 0;
     constexpr int XES = XH ? 2 : 4;
@@ -960,7 +960,6 @@ __global__ __launch_bounds__(512, 2) void conv3x3_wres_f16_kernel(const ConvArgs
         // the epilogue's residual is loaded BEFORE the halo two steps ahead: vmcnt retires loads in issue
         // order, so waiting for it then does not wait for that halo too (the bias comes from LDS for the same
         // reason)
-        if (V == 0 && s + 2 < steps) hload(hl, s + 2);
         if (c == 1 && pre_res) {
 #pragma unroll
             for (int at = 0; at < 2; ++at) {
@@ -973,7 +972,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3_wres_f16_kernel(const ConvArgs
                                             : make_float4(0.f, 0.f, 0.f, 0.f);
             }
         }
-        if (V != 0 && s + 2 < steps) hload(hl, s + 2);
+        if (s + 2 < steps) hload(hl, s + 2);
         const _Float16* H = Hs + (s & 1) * HBUF;
         const _Float16* Bc = Bs + c * 9 * 64 * HALO_PH;
 #pragma unroll
@@ -1848,10 +1847,9 @@ int hyres_conv_weight_prep_batch(const void* descs, int n, long long total, hyre
 }
 
 
-// conv3x3_halo_f16_kernel applies (see above); HYRES_CONV_HALO16=0 turns it off
+// conv3x3_halo_f16_kernel applies (see above)
 static bool halo16_ok(const hyres_conv_geom* g, const hyres_epilogue* e) {
-    static const int on = env_int("HYRES_CONV_HALO16", 1);
-    if (!on || !e->f16_operands || g->nphase != 1 || g->ntaps != 9 || g->Ci % 32 != 0 || g->Co % 64 != 0) return false;
+    if (!e->f16_operands || g->nphase != 1 || g->ntaps != 9 || g->Ci % 32 != 0 || g->Co % 64 != 0) return false;
     if (g->ish != 1 || g->isw != 1 || g->Hi != g->Ho || g->Wi != g->Wo || g->Hq != g->Ho || g->Wq != g->Wo) return false;
     if (g->Wo % HALO_TW != 0 || e->square_input) return false;
     for (int t = 0; t < 9; ++t)
@@ -1860,7 +1858,7 @@ static bool halo16_ok(const hyres_conv_geom* g, const hyres_epilogue* e) {
 }
 
 // conv3x3_wres_f16_kernel: the halo16 geometry with Ci == 64, enough 256-pixel tiles per block to amortise
-// the one-time weight conversion (>= 2 per block); HYRES_CONV_WRES16=0 turns it off
+// the one-time weight conversion (>= 2 per block)
 static int g_cus = 0;
 static int num_cus() {
     if (!g_cus) {
@@ -1880,8 +1878,7 @@ static int wres_blocks(int groups) {
 }
 
 static bool wres16_ok(const hyres_conv_geom* g) {
-    static const int on = env_int("HYRES_CONV_WRES16", 1);
-    if (!on || g->Ci != 64) return false;
+    if (g->Ci != 64) return false;
     const long long tiles = (long long)g->B * ((g->Ho + HALO_R - 1) / HALO_R) * (g->Wo / HALO_TW);
     const int groups = g->Co / 64;
     return tiles >= 2LL * wres_blocks(groups) && (long long)g->B * g->Hi * g->Wi * g->ldx * 4 < 0x7FFFFFF0LL;
@@ -1893,11 +1890,6 @@ static int launch_wres16(const ConvArgs& a, hipStream_t st) {
     const int groups = g.Co / 64;
     const int per = wres_blocks(groups);
     const dim3 grid(per * groups);
-    static const int variant = env_int("HYRES_WRES_VARIANT", 1);
-    if ((a.e.io_f16 & 3) == 0 && variant == 0) {  // A/B: halo prefetch issued before the residual loads
-        hipLaunchKernelGGL((conv3x3_wres_f16_kernel<0, 0>), grid, dim3(512), 0, st, a, ntiles, groups);
-        return HY_LAUNCH_CHECK("conv3x3_wres_f16_kernel");
-    }
     switch (a.e.io_f16 & 3) {
         case 0: hipLaunchKernelGGL(conv3x3_wres_f16_kernel<0>, grid, dim3(512), 0, st, a, ntiles, groups); break;
         case 1: hipLaunchKernelGGL(conv3x3_wres_f16_kernel<1>, grid, dim3(512), 0, st, a, ntiles, groups); break;
@@ -1908,10 +1900,9 @@ static int launch_wres16(const ConvArgs& a, hipStream_t st) {
 }
 
 // conv3x3_wres_f32_kernel: fp32 operands, the halo16 geometry with Ci == 64 and Co % 32 == 0, >= 2 tiles per
-// block; HYRES_CONV_WRES32=0 turns it off
+// block
 static bool wres32_ok(const hyres_conv_geom* g, const hyres_epilogue* e) {
-    static const int on = env_int("HYRES_CONV_WRES32", 1);
-    if (!on || e->f16_operands || e->io_f16 || e->square_input || e->kind != HYRES_EPI_BIAS || g->nphase != 1 ||
+    if (e->f16_operands || e->io_f16 || e->square_input || e->kind != HYRES_EPI_BIAS || g->nphase != 1 ||
         g->ntaps != 9 || g->Ci != 64 || g->Co % 32 != 0)
         return false;
     // the epilogue operands are addressed with 32-bit byte offsets
@@ -1966,12 +1957,10 @@ struct ConvChoice {
 };
 // conv1x1_stream_kernel eligibility: single-tap stride-1 fp32 1x1 with K = Ci in {64, 96, 128}, Co in
 // {64, 96, 128} (or 192 with K = 64), BIAS epilogue with no streamed operand (residual / ReLU mask /
-// old y), grids >= HYRES_CONV_STREAM_PIXELS output pixels (default 65536). Returns NT (Co / 32) or 0.
+// old y), grids >= 65536 output pixels. Returns NT (Co / 32) or 0.
 static int stream_nt(const hyres_conv_geom* g, const hyres_epilogue* e) {
-    static const int on = env_int("HYRES_CONV_STREAM1X1", 1);
-    static const int on16 = env_int("HYRES_CONV_STREAM1X1_F16", 1);  // autocast: fp16-rounded operands
-    static const long long min_px = env_int("HYRES_CONV_STREAM_PIXELS", 65536);
-    if (!on || (e->f16_operands && !on16) || (e->io_f16 & 3) || e->square_input || e->kind != HYRES_EPI_BIAS) return 0;
+    constexpr long long min_px = 65536;
+    if ((e->io_f16 & 3) || e->square_input || e->kind != HYRES_EPI_BIAS) return 0;
     if (g->nphase != 1 || g->ntaps != 1 || g->ish != 1 || g->isw != 1 || g->dh[0] != 0 || g->dw[0] != 0) return 0;
     if (g->Hi != g->Hq || g->Wi != g->Wq || g->Ho != g->Hq || g->Wo != g->Wq) return 0;
     if ((long long)g->B * g->Hq * g->Wq < min_px) return 0;
@@ -1992,10 +1981,9 @@ static ConvChoice choose_conv(const hyres_conv_geom* g, const hyres_epilogue* e,
     ConvChoice c{};
     c.mode = (g->Ci % KT == 0) ? (e->square_input ? 1 : 0) : 2;
     c.narrow = narrow_ok(g) && !e->square_input && e->kind == HYRES_EPI_BIAS && aligned;
-    static const int shortk = env_int("HYRES_CONV_SHORTK", 1);
-    static const long long small_px = env_int("HYRES_CONV_SMALL_PIXELS", 65536);
+    constexpr long long small_px = 65536;
     const bool f16 = e->f16_operands && c.mode != 2;
-    const bool short_k = shortk && c.mode != 2 && g->nphase == 1 && g->ntaps == 1 && g->Ci <= 4 * KT;
+    const bool short_k = c.mode != 2 && g->nphase == 1 && g->ntaps == 1 && g->Ci <= 4 * KT;
     const long long mtot = (long long)g->B * g->Hq * g->Wq * g->nphase;
     if (short_k && g->Co > 64) c.tile = 3;
     else if (short_k && g->Co > 32) c.tile = 4;
@@ -2024,10 +2012,8 @@ static ConvPlan conv_plan(const hyres_conv_geom* g, int tile) {
     const int nk = (g->Ci % KT == 0) ? maxtap * (g->Ci / KT) : ceil_div((long long)maxtap * g->Ci, KT);
     p.nsplit = 1;
     p.cps = nk;
-    static const int sb_env = env_int("HYRES_CONV_SPLIT_BLOCKS", 512);
-    static const int sc_env = env_int("HYRES_CONV_SPLIT_MINCHUNKS", 4);
-    const int sb = g_tune[1] >= 0 ? g_tune[1] : sb_env;
-    const int sc = g_tune[2] > 0 ? g_tune[2] : sc_env;
+    const int sb = g_tune[1] >= 0 ? g_tune[1] : 512;
+    const int sc = g_tune[2] > 0 ? g_tune[2] : 4;
     if (blocks < sb && nk >= 2 * sc) {
         // split K so that ~sb blocks are in flight, at least sc chunks per split
         int want = (int)std::min<long long>(ceil_div(sb, blocks), 64);
@@ -2080,10 +2066,8 @@ int hyres_conv_forward(const hyres_conv_geom* g, const float* x, const float* w2
     ConvArgs a;
     a.g = *g; a.x = x; a.w2 = w2; a.ldw = ldw; a.y = y; a.e = *e;
     a.M = g->B * g->Hq * g->Wq;
-    static const int xcd_order = env_int("HYRES_CONV_XCD", 1);
-    static const int mfma_prio = env_int("HYRES_CONV_PRIO", 1);
-    a.xcd = xcd_order;
-    a.prio = mfma_prio;
+    a.xcd = 1;
+    a.prio = 1;
     const ConvChoice ch = choose_conv(g, e, aligned16(x) && aligned16(w2) && g->ldx % 4 == 0 && ldw % 4 == 0);
     ConvPlan plan = conv_plan(g, ch.tile);
     a.nsplit = 1;
@@ -2165,8 +2149,7 @@ int hyres_conv_forward(const hyres_conv_geom* g, const float* x, const float* w2
         if (nt && mode == 0 && a.vec4 && xb < 0x7FFFFFF0LL && aligned16(x) && aligned16(w2) && ldw % 4 == 0) {
             a.x_bytes = (int)xb;
             a.nsplit = 1;
-            static const int per_cu = env_int("HYRES_CONV_STREAM_BLOCKS_PER_CU", 0);
-            return launch_stream(a, nt, g->Ci / 8, per_cu, st);
+            return launch_stream(a, nt, g->Ci / 8, 0, st);
         }
     }
     int rc;

@@ -12,12 +12,6 @@ namespace hyres {
 
 constexpr int KT = 32;  // K chunk (floats)
 
-// integer environment knob (read once per call site through a function-local static)
-inline int env_int(const char* name, int dflt) {
-    const char* e = getenv(name);
-    return (e && *e) ? atoi(e) : dflt;
-}
-
 // tile / split-K overrides set through hyres_conv_tuning (conv.hip; -1 = the planners' heuristics)
 extern int g_tune[7];
 

@@ -1466,15 +1466,12 @@ struct WgradPlan {
 // 1 or 2 (5x5 only), base rows of a multiple of 32 pixels, both operands >= 32 channels on the float4 path.
 // *dil = the tap spacing.
 static bool halo_ok(const hyres_wgrad_desc* d, int* K, int* dil) {
-    static const int on = env_int("HYRES_WGRAD_HALO", 1);
-    static const int f16_on = env_int("HYRES_WGRAD_HALO_F16", 1);  // AMP: wgrad_halo_f16_kernel
-    if (!on || (d->f16_operands && !f16_on) || d->square_q || (d->sq != 1 && d->sq != 2)) return false;
+    if (d->square_q || (d->sq != 1 && d->sq != 2)) return false;
     if (d->Wq % 32 != 0 || d->M < 32 || d->N < 32 || d->M % 4 || d->N % 4 || d->ldp % 4 || d->ldq % 4) return false;
     const int k = d->ntaps == 9 ? 3 : d->ntaps == 25 ? 5 : 0;
     if (!k || (d->sq == 2 && k != 5)) return false;  // stride 2 only for the 5x5 (de)convs (3x3 s2: 123 KB LDS)
-    static const int dil_on = env_int("HYRES_WGRAD_HALO_DIL", 1);
     const int D = d->dw[1] - d->dw[0];
-    if (D != 1 && !(dil_on && D == 2 && k == 3 && d->sq == 1)) return false;
+    if (D != 1 && !(D == 2 && k == 3 && d->sq == 1)) return false;
     for (int t = 0; t < d->ntaps; ++t)
         if (d->dh[t] != d->dh[0] + D * (t / k) || d->dw[t] != d->dw[0] + D * (t % k)) return false;
     *K = k;
@@ -1524,29 +1521,25 @@ static WgradPlan wgrad_plan(const hyres_wgrad_desc* d) {
         // give 3x the tiles, so a third of the pixel splits and of the split slab for the same grid. Default: rows
         // for dilation 1 (AMP step 21.56 -> 21.34 ms, fp32 42.82 -> 42.68 ms over 3 alternating repeats each;
         // 128^2 fp32 kernel 235 -> 208 us), all 9 taps for the dilated 3x3s (256^2: 678 vs 797 us fp32, 152 vs 219 us
-        // f16: their halo rows are 2 apart, so a row group re-stages most of the chunk). HYRES_WGRAD_HALO_ROWS = 1 / 3
-        // forces one (profiles/r3r_rows_ab.txt, r3y_rows_fp32_ab.txt)
-        static const int rows_env = env_int("HYRES_WGRAD_HALO_ROWS", 0);
-        const int rows = rows_env ? rows_env : (hdil == 2 ? 3 : 1);
+        // f16: their halo rows are 2 apart, so a row group re-stages most of the chunk; profiles/r3r_rows_ab.txt,
+        // r3y_rows_fp32_ab.txt)
+        const int rows = hdil == 2 ? 3 : 1;
         p.NT = p.hk == 3 ? (rows == 1 ? 3 : 9) : 5;
         p.ngroups = d->ntaps / p.NT;
     }
     const long long tiles = (long long)p.mtiles * p.ntiles * p.ngroups;
     // ~2048 blocks (swept on MI355X: 1024 -> 2048 is -0.6 % step time; fewer splits hurt), >= 8 chunks
-    // (256 pixels; f16: 4 chunks of 64) per split, <= 512 splits (tunable: HYRES_WGRAD_BLOCKS,
-    // HYRES_WGRAD_MINCHUNKS, HYRES_WGRAD_MAXSPLIT). Small grids (<= 16384 pixels, the 32^2 region at
+    // (256 pixels; f16: 4 chunks of 64) per split, <= 512 splits (hyres_conv_tuning keys 3, 4, 6 override them for
+    // sweeps). Small grids (<= 16384 pixels, the 32^2 region at
     // bs 16): ~4096 blocks, fp32 multi-tap splits down to 4 chunks. The split count is capped so that the partial
     // slab stays <= 16 M floats (64 MB): for the wide 1x1 layers (M x N ~ 0.5 M) the slab write + reduce
     // otherwise costs more than the parallelism buys (scripts/tile_sweep.py --wgrad)
     const long long Q = (long long)d->B * d->Hq * d->Wq;
     const bool small = Q <= 16384;
-    static const int tb_env = env_int("HYRES_WGRAD_BLOCKS", 2048);
-    static const int mc_env = env_int("HYRES_WGRAD_MINCHUNKS", 8);
-    const int tb = g_tune[3] > 0 ? g_tune[3] : (small ? 2 * tb_env : tb_env);
-    const int mc0 = g_tune[4] > 0 ? g_tune[4] : ((small && kt == KT && d->ntaps > 1) ? mc_env / 2 : mc_env);
+    const int tb = g_tune[3] > 0 ? g_tune[3] : (small ? 4096 : 2048);
+    const int mc0 = g_tune[4] > 0 ? g_tune[4] : ((small && kt == KT && d->ntaps > 1) ? 4 : 8);
     const int mc = std::max(1, mc0 * KT / kt);
-    static const int ms_env = env_int("HYRES_WGRAD_MAXSPLIT", 512);
-    const int ms = g_tune[6] > 0 ? g_tune[6] : ms_env;
+    const int ms = g_tune[6] > 0 ? g_tune[6] : 512;
     const long long slab_cap = std::max<long long>(4, (16LL << 20) / ((long long)d->ntaps * d->M * d->N));
     const long long want = std::min<long long>(std::max<long long>(1, (tb + tiles - 1) / tiles), slab_cap);
     const long long maxsplit = std::max<long long>(1, p.nchunks / mc);
@@ -1560,22 +1553,13 @@ static WgradPlan wgrad_plan(const hyres_wgrad_desc* d) {
         else if (cap / tiles <= maxsplit && 4 * (cap / tiles) <= 5LL * p.nsplit) p.nsplit = (int)(cap / tiles);
     }
     // 1x1 stride-1 fp32 gradients (wgrad1x1_kernel) outside the small grids: 2 groups of 4 waves per block share
-    // one split's pixels, so the same waves write half the slab (HYRES_WGRAD_1X1_GROUPS=1: one group). Isolated
-    // 128^2 64<->128: 65 -> 62 us; on the 32^2 grids it lost (24.6 -> 30.5 us: half the blocks)
-    // halo kernels (3x3, dilated 3x3, 5x5 stride 2), HYRES_WGRAD_HALO_GROUPS=2: 2 groups of 4 waves per block on
-    // one split, 1 block per CU instead of 2: half the split slab written and reduced. Isolated 128^2 3x3 64->64
-    // (kernel + reduce) 206 -> 198 us fp32, 63 -> 57 us f16, 256^2 666 -> 673 us; in the live C2 step 40.0 ->
-    // 41.1 ms fp32 (the 146 KB block keeps the concurrent branches' blocks off its CU), AMP 21.9 -> 22.0 ms: off
-    // by default (profiles/r3o_halo_groups.txt)
-    static const int hg_env = env_int("HYRES_WGRAD_HALO_GROUPS", 1);
+    // one split's pixels, so the same waves write half the slab. Isolated 128^2 64<->128: 65 -> 62 us; on the 32^2
+    // grids it lost (24.6 -> 30.5 us: half the blocks). (Two groups per block for the halo kernels — half their
+    // split slab — won isolated but lost in the live step, 40.0 -> 41.1 ms: the 146 KB block keeps the concurrent
+    // branches' blocks off its CU; profiles/r3o_halo_groups.txt. Removed in round 4.)
     p.hg = 1;
-    if (p.halo && hg_env == 2 && !(p.hk == 5 && d->sq == 1) && p.nsplit >= 2) {
-        p.hg = 2;
-        p.nsplit = (p.nsplit + 1) / 2;
-    }
-    static const int g1x1 = env_int("HYRES_WGRAD_1X1_GROUPS", 2);
     p.g1x1 = 1;
-    if (g1x1 == 2 && !small && !halo && kt == KT && !p.tapn && !d->square_q && d->ntaps == 1 && d->dh[0] == 0 &&
+    if (!small && !halo && kt == KT && !p.tapn && !d->square_q && d->ntaps == 1 && d->dh[0] == 0 &&
         d->dw[0] == 0 && d->sq == 1 && d->Hqq == d->Hq && d->Wqq == d->Wq && p.ngroups == 1 && p.nsplit >= 2) {
         p.g1x1 = 2;
         p.nsplit = (p.nsplit + 1) / 2;
@@ -1644,8 +1628,7 @@ struct ThinPlan {
 };
 
 static bool thin_plan(const hyres_wgrad_desc* d, ThinPlan* tp) {
-    static const int on = env_int("HYRES_WGRAD_THIN", 1);
-    if (!on || d->N > 4 || (d->M != 64 && d->M != 128) || d->square_q || d->ntaps < 1 || d->ntaps > 25)
+    if (d->N > 4 || (d->M != 64 && d->M != 128) || d->square_q || d->ntaps < 1 || d->ntaps > 25)
         return false;
     int hmin = 1 << 30, hmax = -(1 << 30), wmin = 1 << 30, wmax = -(1 << 30);
     for (int t = 0; t < d->ntaps; ++t) {
@@ -1800,8 +1783,7 @@ static int wgrad_issue(const hyres_wgrad_desc* d0, const float* pp, const float*
     dim3 grid(ceil_div(p.nblocks, 8) * 8);
     hipStream_t st = as_stream(s);
     const bool sqr = d->square_q != 0;
-    static const int w1x1 = env_int("HYRES_WGRAD_1X1", 1);
-    const bool one = w1x1 && !thin && !p.halo && !wgrad_f16_ok(d) && !sqr && !p.tapn && vp && vq &&
+    const bool one = !thin && !p.halo && !wgrad_f16_ok(d) && !sqr && !p.tapn && vp && vq &&
                      d->ntaps == 1 && d->dh[0] == 0 && d->dw[0] == 0 && d->sq == 1 && d->Hqq == d->Hq &&
                      d->Wqq == d->Wq && p.ngroups == 1;
     if (one) {
@@ -1834,10 +1816,7 @@ static int wgrad_issue(const hyres_wgrad_desc* d0, const float* pp, const float*
                 hipLaunchKernelGGL((wgrad_halo_f16_kernel<1, 5, 1, 1, IO_>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
             else hipLaunchKernelGGL((wgrad_halo_f16_kernel<1, 5, 2, 1, IO_, G_>), grid, blk, 0, st, a, p.hdh, p.hdw);
         };
-        auto halo16g = [&](auto ioc) {
-            if (p.hg == 2) halo16(ioc, std::integral_constant<int, 2>{});
-            else halo16(ioc, std::integral_constant<int, 1>{});
-        };
+        auto halo16g = [&](auto ioc) { halo16(ioc, std::integral_constant<int, 1>{}); };
         if (io == 1) halo16g(std::integral_constant<int, 1>{});
         else if (io == 2) halo16g(std::integral_constant<int, 2>{});
         else if (io == 3) halo16g(std::integral_constant<int, 3>{});
@@ -1858,11 +1837,9 @@ static int wgrad_issue(const hyres_wgrad_desc* d0, const float* pp, const float*
                 hipLaunchKernelGGL((wgrad_halo_kernel<1, 5, 1>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
             else hipLaunchKernelGGL((wgrad_halo_kernel<1, 5, 2, 1, G_>), grid, blk, 0, st, a, p.hdh, p.hdw);
         };
-        if (p.hg == 2) halo32(std::integral_constant<int, 2>{});
-        else halo32(std::integral_constant<int, 1>{});
+        halo32(std::integral_constant<int, 1>{});
     } else if (wgrad_f16_ok(d)) {
-        static const int f16_one = env_int("HYRES_WGRAD_F16_1X1", 1);
-        const bool one16 = f16_one && !sqr && d->ntaps == 1 && d->dh[0] == 0 && d->dw[0] == 0 && d->sq == 1 &&
+        const bool one16 = !sqr && d->ntaps == 1 && d->dh[0] == 0 && d->dw[0] == 0 && d->sq == 1 &&
                            d->Hqq == d->Hq && d->Wqq == d->Wq && p.ngroups == 1;
         auto f16io = [&](auto tm, auto tn, auto wm_, auto wn_, auto ntc, auto ioc) {
             constexpr int TM_ = decltype(tm)::value, TN_ = decltype(tn)::value;

@@ -31,7 +31,6 @@ from __future__ import annotations
 
 import contextlib
 import ctypes
-import os
 from typing import Callable, Optional
 
 import torch
@@ -130,10 +129,7 @@ class CapturedStep:
         O.bump_weight_epoch()  # record every weight re-layout inside the graph
         # "thread_local" when an RCCL process group exists: its watchdog thread polls events while the
         # main thread captures (no collective is ever inside the graph)
-        # HYRES_MAIN_PRIORITY: stream priority of the captured main stream (the graph's kernels keep it;
-        # the branch streams' is HYRES_BRANCH_PRIORITY)
-        prio = int(os.environ.get("HYRES_MAIN_PRIORITY", "0"))
-        cap_stream = torch.cuda.Stream(device=dev, priority=prio) if prio else None
+        cap_stream = None
         # external events at the backward-progress markers (training + a reducer with segments only)
         self.marker_events = []
         listener = None

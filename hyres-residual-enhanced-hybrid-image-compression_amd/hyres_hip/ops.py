@@ -654,8 +654,7 @@ class SideStream:
     the side stream owns workspace slot 2."""
 
     enabled = os.environ.get("HYRES_SIDE_STREAM", "0") == "1"
-    count = max(1, int(os.environ.get("HYRES_SIDE_STREAMS", "1")))  # weight-gradient streams (round robin)
-    priority = int(os.environ.get("HYRES_SIDE_PRIORITY", "0"))
+    count = 1  # weight-gradient streams (round robin)
     _streams = {}
     _rr = 0
     used = False
@@ -664,7 +663,7 @@ class SideStream:
     def get(cls, device: torch.device, rotate: bool = False) -> torch.cuda.Stream:
         sts = cls._streams.get(device.index)
         if sts is None:
-            sts = [torch.cuda.Stream(device=device, priority=cls.priority) for _ in range(cls.count)]
+            sts = [torch.cuda.Stream(device=device) for _ in range(cls.count)]
             cls._streams[device.index] = sts
         if rotate:
             cls._rr = (cls._rr + 1) % len(sts)
@@ -1098,11 +1097,9 @@ class BranchStreams:
     """HIP streams for independent sub-graphs (AttentionBlock's two branches, MultiScaleRefine's three
     scales): a branch's kernels run concurrently with the other branches' in forward and backward."""
 
+    # (default stream priority: a high-priority branch or main stream measured 25-40 % slower steps, round 2;
+    # limiting the branches to small grids +1.5 %; those switches were removed in round 4)
     enabled = True
-    # branches run concurrently only when the shared input has at most this many pixels (B*H*W);
-    # HYRES_BRANCH_MAX_PIXELS, default: always.  HYRES_BRANCH_PRIORITY: stream priority of branch k > 0
-    max_pixels = int(os.environ.get("HYRES_BRANCH_MAX_PIXELS", str(1 << 40)))
-    priority = int(os.environ.get("HYRES_BRANCH_PRIORITY", "0"))
     _streams = {}
 
     @classmethod
@@ -1110,7 +1107,7 @@ class BranchStreams:
         key = (device.index, k)
         st = cls._streams.get(key)
         if st is None:
-            st = torch.cuda.Stream(device=device, priority=cls.priority)
+            st = torch.cuda.Stream(device=device)
             cls._streams[key] = st
         return st
 
@@ -1122,7 +1119,7 @@ def run_branches(tape: Optional[Tape], x: Node, fns) -> list:
     closures are enqueued on their streams (so their kernels overlap), and a join closure (pushed first,
     so it runs last) makes the current stream wait for them and adds the proxies' gradients into x's.
     Forward ends with the current stream waiting for every branch."""
-    if not BranchStreams.enabled or x.device.type != "cuda" or len(fns) < 2 or x.P > BranchStreams.max_pixels:
+    if not BranchStreams.enabled or x.device.type != "cuda" or len(fns) < 2:
         return [fn(tape, x) for fn in fns]
     dev = x.device
     main = torch.cuda.current_stream(dev)
