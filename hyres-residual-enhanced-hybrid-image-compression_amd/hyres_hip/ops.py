@@ -1057,6 +1057,27 @@ def gdn(tape: Optional[Tape], x: Node, beta: torch.Tensor, gamma: torch.Tensor, 
     return y
 
 
+# the fused ResidualUnit / RBB inference kernel (hyres_ru_fused_f16); tests and bench.py flip it for A/B
+RU_FUSED = True
+
+
+def residual_unit_fused(tape: Optional[Tape], x: Node, c1, c2, c3, final_relu: bool) -> Optional[Node]:
+    """ResidualUnit (final_relu, models/layers/attention.py:11-30) / ResidualBottleneckBlock (compressai) forward as
+    ONE launch when it applies — autocast inference (no tape) with fp16 activations, N = 128, W % 64 == 0 — else None
+    (the caller runs the three convs). c1, c2, c3: the 1x1 N->N/2, 3x3 N/2->N/2 and 1x1 N/2->N Conv2d modules."""
+    if (tape is not None or not RU_FUSED or not x.half or not x.contiguous or x.device.type != "cuda"
+            or not f16_convs() or c1.bias is None or c2.bias is None or c3.bias is None):
+        return None
+    if not L.load().hyres_ru_fused_f16_ok(x.B, x.H, x.W, x.C) or tuple(c2.weight.shape[2:]) != (3, 3):
+        return None
+    y = Node.new(x.B, x.H, x.W, x.C, x.device, rg=False, dtype=torch.float16)
+    L.call("hyres_ru_fused_f16", x.ptr(), y.ptr(), x.B, x.H, x.W, x.C, c1.weight.data_ptr(), c1.bias.data_ptr(),
+           c2.weight.data_ptr(), c2.bias.data_ptr(), c3.weight.data_ptr(), c3.bias.data_ptr(), int(final_relu),
+           L.stream())
+    y.relu_out = final_relu
+    return y
+
+
 def attn_gate(tape: Optional[Tape], a: Node, b: Node, x: Node) -> Node:
     """AttentionBlock combine (models/layers/attention.py:44-47): out = a * sigmoid(b) + x."""
     assert a.contiguous and b.contiguous and x.contiguous

@@ -29,6 +29,9 @@ class ResidualUnit(HipModule):
         self.relu = ReLU(inplace=True)
 
     def hip(self, tape, x):
+        y = O.residual_unit_fused(tape, x, self.conv[0], self.conv[2], self.conv[4], final_relu=True)
+        if y is not None:  # autocast inference: one launch, t1 / t2 on chip (csrc/ru_fused.hip)
+            return y
         t = self.conv[0].hip(tape, x, act=L.ACT_RELU)
         t = self.conv[2].hip(tape, t, act=L.ACT_RELU)
         return self.conv[4].hip(tape, t, act=L.ACT_RELU, res=x)

@@ -220,6 +220,17 @@ int hyres_conv_wgrad_deferred(const hyres_wgrad_desc* d, const float* p, const f
                               int* njobs, hyres_stream_t s);
 int hyres_wgrad_reduce_jobs(const hyres_wgrad_job* jobs, int n, hyres_stream_t s);
 
+/* Fused ResidualUnit / ResidualBottleneckBlock forward, autocast inference with fp16 activations (round 4):
+ * y = [relu](x + W3 * relu(W2 (*) relu(W1 * x + b1) + b2) + b3) in ONE launch, t1 / t2 kept on chip (fp16, the
+ * unfused path's rounding points). Replaces the three-conv chain of the ResidualUnit in models/layers/attention.py:11-30
+ * (final_relu = 1) and of compressai's ResidualBottleneckBlock at models/checkerboard.py:38,42,51,56 (final_relu = 0).
+ * x, y: [B][H][W][N] fp16, N = 128, W % 64 == 0 (hyres_ru_fused_f16_ok); weights / biases fp32 in the PyTorch
+ * layouts (w1 [N/2][N], w2 [N/2][N/2][3][3], w3 [N][N/2]), converted to fp16 on load; 16-byte aligned. */
+int hyres_ru_fused_f16_ok(int B, int H, int W, int N);
+int hyres_ru_fused_f16(const void* x, void* y, int B, int H, int W, int N, const float* w1, const float* b1,
+                       const float* w2, const float* b2, const float* w3, const float* b3, int final_relu,
+                       hyres_stream_t s);
+
 /* column sums over pixels: dst[c] (+)= sum_p x[p*ld + c]  (bias gradients) */
 int hyres_colsum(const float* x, int P, int C, int ld, float* dst, int accumulate, void* workspace,
                  long long ws_bytes, hyres_stream_t s);
