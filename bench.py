@@ -187,6 +187,24 @@ def eval_legs(net, x, jpeg, jpeg_bpp, args, reps=20):
             npx = xe.shape[0] * xe.shape[2] * xe.shape[3]
             res[tag] = {"ms": round(ms, 3), "mpix_s": round(npx / ms / 1e3, 3)}
             del cap
+    # A/B of the fused ResidualUnit / RBB inference kernel (csrc/ru_fused.hip): the bench batch under autocast with
+    # the three-conv chain instead
+    from hyres_hip import ops as O
+    O.RU_FUSED = False
+    try:
+        with torch.autocast("cuda", dtype=torch.float16):
+            cap = CapturedStep(net, x, jpeg, jpeg_bpp)
+            torch.cuda.synchronize()
+            t0 = time.time()
+            for _ in range(reps):
+                cap.replay()
+            torch.cuda.synchronize()
+            ms = (time.time() - t0) * 1000 / reps
+            del cap
+    finally:
+        O.RU_FUSED = True
+    res[legs[0][0] + "_autocast_f16_ru_unfused"] = {"ms": round(ms, 3), "mpix_s": round(x.shape[0] * x.shape[2] *
+                                                                                       x.shape[3] / ms / 1e3, 3)}
     res["analysis_synthesis_bs%d" % x.shape[0]] = analysis_synthesis(net, x, reps)
     res["kodak_codec"] = codec_leg(net, xk.to(dev), jk.to(dev))
     # configs[4]: the same codec under autocast (fp16 MFMA operands, fp16 activations above the latent)

@@ -18,6 +18,9 @@
 //      + b2, ReLU, fp16 into LDS (the t1 buffers are free by then).
 //   3. y = W3 t2 + b3 + x (ReLU for the ResidualUnit), W3's fragments in registers, the residual read as fp16,
 //      y stored fp16. The next tile's first x chunk is loaded into registers during this phase.
+// Training (AMP, t1 / t2 outputs given): the same launch also writes t1 (each tile's own pixels) and t2 to HBM — the
+// backward needs them (weight-gradient operands, ReLU masks) — and the three convs' backward closures are recorded
+// as usual (hyres_hip.ops.residual_unit_fused): only the re-reads of t1, t2 and x disappear.
 // The fp16 rounding points are the unfused autocast path's (t1, t2 stored fp16; every GEMM on fp16 operands), so the
 // results agree with it up to fp32 summation order (tests/test_ru_fused_gpu.py).
 #include "common.h"
@@ -51,6 +54,7 @@ struct RuArgs {
     const _Float16* x;  // [B][H][W][128] fp16
     _Float16* y;        // [B][H][W][128] fp16
     const float *w1, *b1, *w2, *b2, *w3, *b3;  // PyTorch layouts: w1 [64][128], w2 [64][64][3][3], w3 [128][64]
+    _Float16 *t1, *t2;  // training (AMP): the intermediates [B][H][W][64] fp16 for the backward, or NULL
     int B, H, W, ntiles, final_relu;
 };
 
@@ -170,6 +174,9 @@ __global__ __launch_bounds__(512, 1) void ru_fused_f16_kernel(const RuArgs a) {
             const int hr = px / RU_HW, hc = px - hr * RU_HW;
             const int ih = i0 - 1 + hr, iw = j0 - 1 + hc;
             const bool inside = px < RU_HNPX && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+            // training: the tile's own (center) pixels of t1 also go to HBM — every pixel is the center of one tile
+            const bool center = a.t1 != nullptr && inside && hr >= 1 && hr <= RU_R && hc >= 1 && hc <= RU_TW;
+            const long long tpix = ((long long)b * H + ih) * W + iw;
 #pragma unroll
             for (int qd = 0; qd < 4; ++qd) {
                 const int co = 8 * qd + 4 * lh;  // within the 32-channel block cb1
@@ -179,6 +186,7 @@ __global__ __launch_bounds__(512, 1) void ru_fused_f16_kernel(const RuArgs a) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) h[r] = (_Float16)(inside ? fmaxf(acc1[i][4 * qd + r] + bv[r], 0.f) : 0.f);
                 *reinterpret_cast<half4_t*>(&T[cb1 * RU_TBUF + px * RU_PH + co]) = h;
+                if (center) *reinterpret_cast<half4_t*>(&a.t1[tpix * RU_M + 32 * cb1 + co]) = h;
             }
         }
         __syncthreads();
@@ -212,6 +220,8 @@ __global__ __launch_bounds__(512, 1) void ru_fused_f16_kernel(const RuArgs a) {
 #pragma unroll
         for (int at = 0; at < 2; ++at) {
             const int px = orow * RU_TW + 32 * at + lr;
+            const bool store = a.t2 != nullptr && i0 + orow < H;
+            const long long tpix = ((long long)b * H + i0 + orow) * W + j0 + 32 * at + lr;
 #pragma unroll
             for (int qd = 0; qd < 4; ++qd) {
                 const int co = 8 * qd + 4 * lh;
@@ -221,6 +231,7 @@ __global__ __launch_bounds__(512, 1) void ru_fused_f16_kernel(const RuArgs a) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) h[r] = (_Float16)fmaxf(acc2[at][4 * qd + r] + bv[r], 0.f);
                 *reinterpret_cast<half4_t*>(&T[wn * RU_TBUF + px * RU_PH + co]) = h;
+                if (store) *reinterpret_cast<half4_t*>(&a.t2[tpix * RU_M + 32 * wn + co]) = h;
             }
         }
         __syncthreads();
@@ -281,8 +292,10 @@ int hyres_ru_fused_f16_ok(int B, int H, int W, int N) {
 
 int hyres_ru_fused_f16(const void* x, void* y, int B, int H, int W, int N, const float* w1, const float* b1,
                        const float* w2, const float* b2, const float* w3, const float* b3, int final_relu,
-                       hyres_stream_t s) {
+                       void* t1, void* t2, hyres_stream_t s) {
     HY_REQUIRE(x && y && w1 && b1 && w2 && b2 && w3 && b3 && x != y, HYRES_E_ARG, "ru_fused_f16: NULL or in place");
+    HY_REQUIRE((t1 == nullptr) == (t2 == nullptr) && (!t1 || (aligned16(t1) && aligned16(t2))), HYRES_E_ARG,
+               "ru_fused_f16: t1 and t2 both NULL (inference) or both 16-byte aligned outputs (training)");
     HY_REQUIRE(hyres_ru_fused_f16_ok(B, H, W, N), HYRES_E_SHAPE,
                "ru_fused_f16: N = 128, W %% 64 == 0 and a batch < 2 GB needed (B %d H %d W %d N %d)", B, H, W, N);
     HY_REQUIRE(aligned16(x) && aligned16(y) && aligned16(w1) && aligned16(w3) && aligned16(b1) && aligned16(b2) &&
@@ -292,6 +305,8 @@ int hyres_ru_fused_f16(const void* x, void* y, int B, int H, int W, int N, const
     a.x = (const _Float16*)x;
     a.y = (_Float16*)y;
     a.w1 = w1; a.b1 = b1; a.w2 = w2; a.b2 = b2; a.w3 = w3; a.b3 = b3;
+    a.t1 = (_Float16*)t1;
+    a.t2 = (_Float16*)t2;
     a.B = B; a.H = H; a.W = W;
     a.ntiles = B * ((H + RU_R - 1) / RU_R) * (W / RU_TW);
     a.final_relu = final_relu ? 1 : 0;

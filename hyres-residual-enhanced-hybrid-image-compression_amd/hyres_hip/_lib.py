@@ -105,7 +105,7 @@ _SIGS = {
                                        ctypes.POINTER(ctypes.c_int), _P]),
     "hyres_wgrad_reduce_jobs": (_I, [ctypes.POINTER(WgradJob), _I, _P]),
     "hyres_ru_fused_f16_ok": (_I, [_I, _I, _I, _I]),
-    "hyres_ru_fused_f16": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _P]),
+    "hyres_ru_fused_f16": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P]),
     "hyres_colsum": (_I, [_P, _I, _I, _I, _P, _I, _P, _LL, _P]),
     "hyres_colsum_workspace_bytes": (_LL, [_I, _I]),
     "hyres_colsum_f16": (_I, [_P, _I, _I, _I, _P, _I, _P, _LL, _P]),

@@ -186,7 +186,7 @@ class ResidualBottleneckBlock(HipModule):
 
     def hip(self, tape: Optional[Tape], x: Node) -> Node:
         y = O.residual_unit_fused(tape, x, self.conv1, self.conv2, self.conv3, final_relu=False)
-        if y is not None:  # autocast inference: one launch (csrc/ru_fused.hip)
+        if y is not None:  # autocast with fp16 activations: one launch (csrc/ru_fused.hip)
             return y
         t = self.conv1.hip(tape, x, act=L.ACT_RELU)
         t = self.conv2.hip(tape, t, act=L.ACT_RELU)

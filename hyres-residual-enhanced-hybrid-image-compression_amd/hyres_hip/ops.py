@@ -834,7 +834,7 @@ def _act_backward(y: Node, gy: torch.Tensor, gy_ld: int, act: int, pre: Optional
 # --------------------------------------------------------------------------------------------------
 def conv2d(tape: Optional[Tape], x: Node, weight: torch.Tensor, bias: Optional[torch.Tensor], stride=1,
            pad=0, dil=1, act=L.ACT_NONE, slope=None, res: Optional[Node] = None, out: Optional[Node] = None,
-           mask: Optional[torch.Tensor] = None) -> Node:
+           mask: Optional[torch.Tensor] = None, computed: bool = False) -> Node:
     """nn.Conv2d (+ fused bias / residual / ReLU / PReLU epilogue), NHWC, on MFMA.
 
     Reference call sites: models/layers/common.py:4-11, compressai conv() (k5 s2 p2),
@@ -853,8 +853,8 @@ def conv2d(tape: Optional[Tape], x: Node, weight: torch.Tensor, bias: Optional[t
     y = out if out is not None else Node.new(B, Ho, Wo, Co, x.device, dtype=ydt)
     assert (y.B, y.H, y.W, y.C) == (B, Ho, Wo, Co), ((y.B, y.H, y.W, y.C), (B, Ho, Wo, Co))
     g = _filter_taps(_geom("hyres_geom_conv2d", B, H, W, Ci, x.ld, Co, y.ld, KH, KW, stride, pad, dil), mask)
-    if KH == 1 and KW == 1 and mask is None:
-        w2, ldw = weight, Ci_w  # OIHW == OHWI for 1x1
+    if (KH == 1 and KW == 1 and mask is None) or computed:
+        w2, ldw = weight, Ci_w  # OIHW == OHWI for 1x1 (computed: no forward launch, no re-layout)
     else:
         w2, ldw = _prepped(weight, g, L.WPREP_CONV, Ci, Co, KH, KW, pad, mask), g.ntaps * Ci
     e = L.Epilogue()
@@ -875,7 +875,10 @@ def conv2d(tape: Optional[Tape], x: Node, weight: torch.Tensor, bias: Optional[t
             e.ldo2 = Co
     f16 = int(f16_convs())
     e.f16_operands = f16
-    _launch_conv(g, x.ptr(), w2, ldw, y.ptr(), e)
+    if computed:  # ``out`` already holds this conv's output (a fused forward): only record the backward
+        assert out is not None and pre is None
+    else:
+        _launch_conv(g, x.ptr(), w2, ldw, y.ptr(), e)
     y.relu_out = act == L.ACT_RELU
     Trace.act(y, act, pre)
     if tape is None:
@@ -1063,19 +1066,33 @@ RU_FUSED = True
 
 def residual_unit_fused(tape: Optional[Tape], x: Node, c1, c2, c3, final_relu: bool) -> Optional[Node]:
     """ResidualUnit (final_relu, models/layers/attention.py:11-30) / ResidualBottleneckBlock (compressai) forward as
-    ONE launch when it applies — autocast inference (no tape) with fp16 activations, N = 128, W % 64 == 0 — else None
-    (the caller runs the three convs). c1, c2, c3: the 1x1 N->N/2, 3x3 N/2->N/2 and 1x1 N/2->N Conv2d modules."""
-    if (tape is not None or not RU_FUSED or not x.half or not x.contiguous or x.device.type != "cuda"
+    ONE launch when it applies — autocast with fp16 activations (inference, or AMP training with the fp16 region's
+    activations), N = 128, W % 64 == 0 — else None (the caller runs the three convs). c1, c2, c3: the 1x1 N->N/2,
+    3x3 N/2->N/2 and 1x1 N/2->N Conv2d modules. In training the launch also writes the two intermediates, and the
+    three convs' backward closures are recorded on the tape exactly as the unfused chain records them."""
+    if (not RU_FUSED or not x.half or not x.contiguous or x.device.type != "cuda"
             or not f16_convs() or c1.bias is None or c2.bias is None or c3.bias is None):
         return None
     if not L.load().hyres_ru_fused_f16_ok(x.B, x.H, x.W, x.C) or tuple(c2.weight.shape[2:]) != (3, 3):
         return None
-    y = Node.new(x.B, x.H, x.W, x.C, x.device, rg=False, dtype=torch.float16)
+    train = tape is not None
+    if train and not act_f16(tape, x.H, x.W):
+        return None
+    y = Node.new(x.B, x.H, x.W, x.C, x.device, rg=train, dtype=torch.float16)
+    t1 = t2 = None
+    if train:
+        t1 = Node.new(x.B, x.H, x.W, x.C // 2, x.device, dtype=torch.float16)
+        t2 = Node.new(x.B, x.H, x.W, x.C // 2, x.device, dtype=torch.float16)
     L.call("hyres_ru_fused_f16", x.ptr(), y.ptr(), x.B, x.H, x.W, x.C, c1.weight.data_ptr(), c1.bias.data_ptr(),
            c2.weight.data_ptr(), c2.bias.data_ptr(), c3.weight.data_ptr(), c3.bias.data_ptr(), int(final_relu),
-           L.stream())
-    y.relu_out = final_relu
-    return y
+           None if t1 is None else t1.ptr(), None if t2 is None else t2.ptr(), L.stream())
+    if not train:
+        y.relu_out = final_relu
+        return y
+    act3 = L.ACT_RELU if final_relu else L.ACT_NONE
+    conv2d(tape, x, c1.weight, c1.bias, act=L.ACT_RELU, out=t1, computed=True)
+    conv2d(tape, t1, c2.weight, c2.bias, pad=1, act=L.ACT_RELU, out=t2, computed=True)
+    return conv2d(tape, t2, c3.weight, c3.bias, act=act3, res=x, out=y, computed=True)
 
 
 def attn_gate(tape: Optional[Tape], a: Node, b: Node, x: Node) -> Node:

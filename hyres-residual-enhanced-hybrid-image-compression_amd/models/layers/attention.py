@@ -30,7 +30,7 @@ class ResidualUnit(HipModule):
 
     def hip(self, tape, x):
         y = O.residual_unit_fused(tape, x, self.conv[0], self.conv[2], self.conv[4], final_relu=True)
-        if y is not None:  # autocast inference: one launch, t1 / t2 on chip (csrc/ru_fused.hip)
+        if y is not None:  # autocast with fp16 activations: one launch, t1 / t2 on chip (csrc/ru_fused.hip)
             return y
         t = self.conv[0].hip(tape, x, act=L.ACT_RELU)
         t = self.conv[2].hip(tape, t, act=L.ACT_RELU)

@@ -229,7 +229,9 @@ int hyres_wgrad_reduce_jobs(const hyres_wgrad_job* jobs, int n, hyres_stream_t s
 int hyres_ru_fused_f16_ok(int B, int H, int W, int N);
 int hyres_ru_fused_f16(const void* x, void* y, int B, int H, int W, int N, const float* w1, const float* b1,
                        const float* w2, const float* b2, const float* w3, const float* b3, int final_relu,
-                       hyres_stream_t s);
+                       void* t1, void* t2, hyres_stream_t s);
+/* t1, t2: NULL (inference), or [B][H][W][N/2] fp16 outputs receiving the two intermediates (AMP training: the
+ * backward of the three convs reads them). */
 
 /* column sums over pixels: dst[c] (+)= sum_p x[p*ld + c]  (bias gradients) */
 int hyres_colsum(const float* x, int P, int C, int ld, float* dst, int accumulate, void* workspace,

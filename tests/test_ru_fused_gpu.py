@@ -103,3 +103,39 @@ def test_ru_fused_eval_forward_matches_unfused(monkeypatch):
     dbits = res[True][1] / res[False][1] - 1
     print(f"fused vs unfused eval: dPSNR {dpsnr:.5f} dB, bits {dbits:.2e}")
     assert abs(dpsnr) < 0.01 and abs(dbits) < 5e-3
+
+
+@pytest.mark.parametrize("final_relu", [True, False])
+def test_ru_fused_amp_training_matches_unfused(final_relu, monkeypatch):
+    """AMP training (fp16 activations and gradients inside an f16_region): the fused forward also writes t1 / t2 and
+    records the three convs' backward; output, input gradient and every weight / bias gradient match the unfused
+    chain up to fp32 summation order (a ReLU decision at an fp16 tie may flip: normwise 1e-2)."""
+    from hyres_hip import ops as O
+    from hyres_hip.layers import ResidualBottleneckBlock
+    from models.layers.attention import ResidualUnit
+    D = dev()
+    N, B, H, W = 128, 2, 16, 64
+    torch.manual_seed(9)
+    mod = (ResidualUnit(N) if final_relu else ResidualBottleneckBlock(N, N)).to(D).train()
+    x = _rand((B, N, H, W), 12).to(D)
+    gy = _rand((B, N, H, W), 13).half().float().to(D)
+    res = {}
+    for fused in (True, False):
+        monkeypatch.setattr(O, "RU_FUSED", fused)
+        for p in mod.parameters():
+            p.grad = None
+        tape = O.Tape()
+        xn = O.to_nhwc(x, rg=True)
+        xn = O.Node(xn.v.half(), rg=True)
+        with torch.autocast("cuda", dtype=torch.float16), O.f16_region():
+            yn = mod.hip(tape, xn)
+        assert yn.half
+        y = O.to_nchw(yn)
+        yn.set_grad(O.nchw_grad_to_nhwc(gy))
+        tape.backward()
+        torch.cuda.synchronize()
+        res[fused] = [y.cpu(), O.to_nchw_grad(xn).cpu()] + [p.grad.detach().cpu().clone() for p in mod.parameters()]
+    errs = [rel_err(a, b) for a, b in zip(res[True], res[False])]
+    print("fused vs unfused (y, gx, params):", ["%.1e" % e for e in errs])
+    assert errs[0] < 2e-3
+    assert max(errs[1:]) < 1e-2
