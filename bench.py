@@ -267,8 +267,36 @@ def amp_leg(net, opt, aux_opt, crit, x, jpeg, jpeg_bpp, args):
     # the dominant f16-MFMA-bound kernel (intensity above the f16 ridge 2500 / 8 = 312 FLOP/B) as well
     ks_mfma = O.KernelTimer.summary(pick=lambda k, v: v[1] / max(v[2], 1.0) >= F16_RIDGE)
     opt.zero_grad()
+    nrep = max(5, args.steps // 2)
+    torch.cuda.synchronize()
+    t0 = time.time()
+    for _ in range(nrep):
+        cap.replay()
+        opt.zero_grad()
+    torch.cuda.synchronize()
+    ms_a = (time.time() - t0) * 1000 / nrep
     del cap
+    # round-4 A/B on the same box: the step with fp32 activation gradients and the unfused ResidualUnits (round 3's
+    # AMP path) — the gain of fp16 activation gradients + the fused RU forward
+    saved = (O.AMP_F16_GRAD, O.RU_FUSED)
+    O.AMP_F16_GRAD, O.RU_FUSED = False, False
+    try:
+        scaler_b = DeviceGradScaler(dev)
+        cap_b = CapturedStep(net, x, jpeg, jpeg_bpp, noisequant=False, criterion=crit, zero_grad=opt.zero_grad,
+                             amp=True, loss_scale=scaler_b.scale)
+        torch.cuda.synchronize()
+        t0 = time.time()
+        for _ in range(nrep):
+            cap_b.replay()
+            opt.zero_grad()
+        torch.cuda.synchronize()
+        ms_b = (time.time() - t0) * 1000 / nrep
+        del cap_b
+    finally:
+        O.AMP_F16_GRAD, O.RU_FUSED = saved
+    opt.zero_grad()
     return {"dtype": "f16-amp", "value": round(B * H * W / ms / 1e3, 4), "unit": "Mpixels/s", "ms_per_step": round(ms, 3),
+            "fwd_bwd_ms": round(ms_a, 3), "ab_fp32_grads_unfused_ru_fwd_bwd_ms": round(ms_b, 3),
             "loss": loss, "loss_scale": scaler.get_scale(),
             "roofline": with_traffic(roofline_of(ks, MI355X_F16_PEAK_TFLOPS, F16_RIDGE), ks["kernel"]),
             "roofline_f16_mfma_kernel": roofline_of(ks_mfma, MI355X_F16_PEAK_TFLOPS, F16_RIDGE),
