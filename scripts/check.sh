@@ -6,6 +6,7 @@
 #   steps   per-kernel tables of 10 replayed fp32 / AMP steps (scripts/profile_steps.sh)
 #   mem     peak device memory with the deferred weight-gradient reduces on / off (scripts/mem_probe.py)
 #   dist    the N>1 rehearsal (scripts/dist_rehearsal.sh)
+#   probe   scripts/bf16x6_probe (fp32 GEMM: native f32 MFMA vs the bf16x6 split, speed and error)
 # Every step runs under its own time limit (scripts/gpu_run.sh) and the pass stops at the first crash-like exit.
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
@@ -33,6 +34,7 @@ for ph in "$@"; do
     mem)   scripts/gpu_run.sh "mem_defer1:200:python3 scripts/mem_probe.py" "mem_defer0:200:HYRES_WGRAD_DEFER=0 python3 scripts/mem_probe.py" || exit $?
            cat gpurun_out/mem_defer1.log gpurun_out/mem_defer0.log | grep WGRAD_DEFER > gpurun_out/${tag}_mem_probe.txt ;;
     dist)  bash scripts/dist_rehearsal.sh; echo "dist rehearsal exit $?" ;;
+    probe) scripts/gpu_run.sh "bf16x6_probe:120:scripts/bf16x6_probe" || exit $? ;;
     *) echo "unknown phase $ph"; exit 2 ;;
   esac
 done
