@@ -1197,6 +1197,208 @@ __global__ __launch_bounds__(512, 2) void conv3x3_wres_f32_kernel(const ConvArgs
 }
 
 // ------------------------------------------------------------------------------------------------
+// fp32-accurate weight-resident 3x3 conv on the bf16 MFMA ("bf16x6", hyres_conv_tuning key 7 = 1; opt-in).
+// conv3x3_wres_f32_kernel above runs at ~0.7 of the fp32 MFMA peak, and that peak (157 TF/s) is 1/16 of the bf16
+// MFMA's. Here every fp32 operand is split into three bf16 pieces x = x0 + x1 + x2 (x0 = bf16(x), x1 = bf16(x - x0),
+// x2 = bf16(x - x0 - x1): 24 significant bits, |x - x0 - x1 - x2| <= 2^-25 |x|) and each product is formed from the
+// six cross products with i + j <= 2 (the dropped ones are below 2^-26 |x y|) with fp32 accumulation on
+// v_mfma_f32_32x32x16_bf16 (products of bf16 values are exact in fp32): per product the error is at most about
+// 2^-25 relative, below the half-ulp rounding (2^-24) of the fp32 MFMA's own fmaf chain; 6 bf16 MFMAs per 16-deep K
+// step against 8 fp32 ones per 2 x 8, i.e. 2.67x fewer MFMA cycles. The weights of the block's 32-channel output
+// slice are split once into LDS (3 planes x 4 chunks of 16 input channels x 9 taps x 32 rows of 32 B: 108 KB), the
+// halo of each 16-channel chunk is split when staged (3 planes x 396 px x 32 B: 37 KB; 9 taps reuse it). Both
+// images swizzle the 16-B half of a 32-B row by bit 3 of the row: every ds_read_b128 lane group then hits 16
+// distinct 16-B slots (conflict-free). Same tiles, waves, tile order and epilogue as conv3x3_wres_f32_kernel.
+constexpr int BF6_WPL = 4 * 9 * 32 * 16;  // bf16 per weight plane
+constexpr int BF6_HPL = HALO_NPX * 16;    // bf16 per halo plane
+constexpr int BF6_HE = HALO_NPX * 4;      // float4 per 16-channel halo chunk
+constexpr int BF6_HV = (BF6_HE + 511) / 512;
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+
+// 16-B segment (0 / 1) of element k (0..15) of row r in a swizzled [row][16] bf16 image, as an element offset
+__device__ __forceinline__ int bf6_off(int r, int k) { return r * 16 + ((((k >> 3) ^ (r >> 3)) & 1) << 3) + (k & 7); }
+
+__device__ __forceinline__ void bf6_split4(float4 v, bf16x4_t& h, bf16x4_t& m, bf16x4_t& l) {
+    const float x[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const __bf16 a = (__bf16)x[i];
+        const float r1 = x[i] - (float)a;
+        const __bf16 b = (__bf16)r1;
+        h[i] = a;
+        m[i] = b;
+        l[i] = (__bf16)(r1 - (float)b);
+    }
+}
+
+__global__ __launch_bounds__(512, 1) void conv3x3_wres_bf6_kernel(const ConvArgs a, int ntiles, int groups) {
+    __shared__ __attribute__((aligned(16))) __bf16 lds[3 * BF6_WPL + 3 * BF6_HPL];
+    __shared__ int2 tapoff[9];
+    __bf16* const Ws = lds;
+    __bf16* const Hs = lds + 3 * BF6_WPL;
+    const hyres_conv_geom& g = a.g;
+    const int tid = threadIdx.x;
+    const int nrt = (g.Ho + HALO_R - 1) / HALO_R, nct = g.Wo / HALO_TW;
+    const int nb = gridDim.x / groups;  // group-major, nb % 8 == 0: see conv3x3_wres_f16_kernel
+    const int grp = blockIdx.x / nb, bg = blockIdx.x - grp * nb;
+    const int n0 = grp * 32;
+    const int xcd = bg & 7, nx = (nb + 7 - xcd) >> 3, jx = bg >> 3;
+    const int q = ntiles >> 3, rr8 = ntiles & 7;
+    const int tbeg = xcd * q + min(xcd, rr8), tcnt = q + (xcd < rr8 ? 1 : 0);
+    const int mytiles = jx < tcnt ? (tcnt - 1 - jx) / nx + 1 : 0;
+    if (tid < 9) tapoff[tid] = make_int2(g.dh[tid], g.dw[tid]);
+    // weights W2[co][t][ci] (fp32) -> three bf16 planes, row (chunk c = ci / 16, tap t, co), element ci % 16
+    for (int f = tid; f < 32 * 9 * 16; f += 512) {
+        const int co = f / 144, rem = f - co * 144, t = rem >> 4, ci = 4 * (rem & 15);
+        bf16x4_t h, m, l;
+        bf6_split4(ld4(a.w2 + (long long)(n0 + co) * a.ldw + t * 64 + ci), h, m, l);
+        const int row = ((ci >> 4) * 9 + t) * 32 + co;
+        const int o = bf6_off(row, ci & 15);
+        *reinterpret_cast<bf16x4_t*>(&Ws[o]) = h;
+        *reinterpret_cast<bf16x4_t*>(&Ws[BF6_WPL + o]) = m;
+        *reinterpret_cast<bf16x4_t*>(&Ws[2 * BF6_WPL + o]) = l;
+    }
+    const long long img = (long long)g.Hi * g.Wi * g.ldx;
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)a.x, (short)0, (int)std::min<long long>((long long)g.B * img * 4, 0x7FFFFFF0LL), 0x00020000);
+    const int lane = tid & 63, wave = tid >> 6;
+    const int orow = wave & 3, ph = wave >> 2;  // output row in the tile, 32-pixel half
+    const int lr = lane & 31, lh = lane >> 5;
+
+    auto tile_of = [&](int k, int& b, int& i0, int& j0) {
+        int l = tbeg + jx + k * nx;
+        const int rt = l % nrt; l /= nrt;
+        const int ct = l % nct;
+        b = l / nct;
+        i0 = rt * HALO_R;
+        j0 = ct * HALO_TW;
+    };
+    float4 hreg[BF6_HV];
+    auto hload = [&](int step) {  // step = 4 * tile + chunk (16 channels)
+        int b, i0, j0;
+        tile_of(step >> 2, b, i0, j0);
+        const int c = step & 3;
+        const int base = b * (int)img;
+#pragma unroll
+        for (int v = 0; v < BF6_HV; ++v) {
+            const int e = tid + 512 * v;
+            const int px = e >> 2, c4 = e & 3;
+            const int hr = px / HALO_HW, hc = px - hr * HALO_HW;
+            const int ih = i0 - 1 + hr, iw = j0 - 1 + hc;
+            const bool ok = e < BF6_HE && (unsigned)ih < (unsigned)g.Hi && (unsigned)iw < (unsigned)g.Wi;
+            const int off = ok ? (base + (ih * g.Wi + iw) * g.ldx + 16 * c + 4 * c4) * 4 : (int)0x80000000;
+            hreg[v] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
+        }
+    };
+    auto hstore = [&]() {
+#pragma unroll
+        for (int v = 0; v < BF6_HV; ++v) {
+            const int e = tid + 512 * v;
+            if (e < BF6_HE) {
+                bf16x4_t h, m, l;
+                bf6_split4(hreg[v], h, m, l);
+                const int o = bf6_off(e >> 2, 4 * (e & 3));
+                *reinterpret_cast<bf16x4_t*>(&Hs[o]) = h;
+                *reinterpret_cast<bf16x4_t*>(&Hs[BF6_HPL + o]) = m;
+                *reinterpret_cast<bf16x4_t*>(&Hs[2 * BF6_HPL + o]) = l;
+            }
+        }
+    };
+    floatx16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    const hyres_epilogue& e = a.e;
+    const float slope = (e.act == HYRES_ACT_PRELU) ? e.slope[0] : 0.f;
+    const long long npix = (long long)g.B * g.Ho * g.Wo;
+    const __amdgpu_buffer_rsrc_t r_bias = opnd_rsrc(e.bias, (long long)g.Co * 4);
+    const __amdgpu_buffer_rsrc_t r_res = opnd_rsrc(e.res, npix * e.ldres * 4);
+    const __amdgpu_buffer_rsrc_t r_mask = opnd_rsrc(e.act == HYRES_ACT_RELU_MASK ? e.aux0 : nullptr, npix * e.ld0 * 4);
+    const __amdgpu_buffer_rsrc_t r_old = opnd_rsrc(e.accumulate ? a.y : nullptr, npix * g.ldy * 4);
+    float4 ebias[4], eres[4], emask[4], eold[4];
+    const int steps = mytiles * 4;
+    if (steps > 0) {
+        hload(0);
+        hstore();
+    }
+    __syncthreads();
+    for (int s = 0; s < steps; ++s) {
+        const int k = s >> 2, c = s & 3;
+        int b, i0, j0;
+        tile_of(k, b, i0, j0);
+        const int i = i0 + orow;
+        const long long pix = ((long long)b * g.Ho + i) * g.Wo + j0 + 32 * ph + lr;
+        if (c == 3) {  // the epilogue's operands, issued before the next halo (vmcnt retires in issue order)
+            const bool okr = i < g.Ho;
+#pragma unroll
+            for (int qd = 0; qd < 4; ++qd) {
+                const int n = n0 + 8 * qd + 4 * lh;
+                const int ob = n * 4;
+                const int orr = okr ? (int)((pix * e.ldres + n) * 4) : (int)0x80000000;
+                const int om = okr ? (int)((pix * e.ld0 + n) * 4) : (int)0x80000000;
+                const int oy = okr ? (int)((pix * g.ldy + n) * 4) : (int)0x80000000;
+                ebias[qd] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r_bias, ob, 0, 0));
+                eres[qd] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r_res, orr, 0, 0));
+                emask[qd] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r_mask, om, 0, 0));
+                eold[qd] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r_old, oy, 0, 0));
+            }
+        }
+        if (s + 1 < steps) hload(s + 1);
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+            const int2 o = tapoff[t];
+            const int wrow = (c * 9 + t) * 32 + lr;                                    // A: weights, row = co
+            const int hrow = (orow + 1 + o.x) * HALO_HW + 32 * ph + lr + 1 + o.y;     // B: halo, row = pixel
+            const int wo = wrow * 16 + (((lh ^ (wrow >> 3)) & 1) << 3);
+            const int ho = hrow * 16 + (((lh ^ (hrow >> 3)) & 1) << 3);
+            const bf16x8_t w0 = *reinterpret_cast<const bf16x8_t*>(&Ws[wo]);
+            const bf16x8_t w1 = *reinterpret_cast<const bf16x8_t*>(&Ws[BF6_WPL + wo]);
+            const bf16x8_t w2 = *reinterpret_cast<const bf16x8_t*>(&Ws[2 * BF6_WPL + wo]);
+            const bf16x8_t x0 = *reinterpret_cast<const bf16x8_t*>(&Hs[ho]);
+            const bf16x8_t x1 = *reinterpret_cast<const bf16x8_t*>(&Hs[BF6_HPL + ho]);
+            const bf16x8_t x2 = *reinterpret_cast<const bf16x8_t*>(&Hs[2 * BF6_HPL + ho]);
+            // the small cross products first, the leading one last
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w2, x0, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1, x1, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w0, x2, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1, x0, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w0, x1, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w0, x0, acc, 0, 0, 0);
+        }
+        if (c == 3) {
+            if (i < g.Ho) {
+#pragma unroll
+                for (int qd = 0; qd < 4; ++qd) {
+                    const int n = n0 + 8 * qd + 4 * lh;
+                    float o[4] = {acc[4 * qd] + ebias[qd].x + eres[qd].x, acc[4 * qd + 1] + ebias[qd].y + eres[qd].y,
+                                  acc[4 * qd + 2] + ebias[qd].z + eres[qd].z, acc[4 * qd + 3] + ebias[qd].w + eres[qd].w};
+                    if (e.out2) st4(e.out2 + pix * e.ldo2 + n, make_float4(o[0], o[1], o[2], o[3]));
+                    if (e.act == HYRES_ACT_RELU) {
+#pragma unroll
+                        for (int kk = 0; kk < 4; ++kk) o[kk] = fmaxf(o[kk], 0.f);
+                    } else if (e.act == HYRES_ACT_PRELU) {
+#pragma unroll
+                        for (int kk = 0; kk < 4; ++kk) o[kk] = o[kk] >= 0.f ? o[kk] : slope * o[kk];
+                    } else if (e.act == HYRES_ACT_RELU_MASK) {
+                        o[0] = emask[qd].x > 0.f ? o[0] : 0.f;
+                        o[1] = emask[qd].y > 0.f ? o[1] : 0.f;
+                        o[2] = emask[qd].z > 0.f ? o[2] : 0.f;
+                        o[3] = emask[qd].w > 0.f ? o[3] : 0.f;
+                    }
+                    st4(a.y + pix * g.ldy + n,
+                        make_float4(o[0] + eold[qd].x, o[1] + eold[qd].y, o[2] + eold[qd].z, o[3] + eold[qd].w));
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+        }
+        __syncthreads();  // every wave is done with this chunk's halo
+        if (s + 1 < steps) hstore();
+        __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
 // Streaming 1x1 conv (K = Ci <= 128, Co = 32*NT): the K-short pointwise layers of the ResidualUnits /
 // RBBs at 64^2..256^2 sit at the fp32 ridge (64-128 FLOP per output element against 8-12 bytes), and the
 // tiled kernel above runs them as lock-stepped blocks (load, then MFMA, then epilogue), so their MFMA and
@@ -1696,7 +1898,7 @@ static void dense_taps(hyres_conv_geom* g, int KH, int KW, int sgn, int dil, int
 
 // keys: HYRES_TUNE_TILE, _SPLIT_BLOCKS, _SPLIT_MINCHUNKS, _WGRAD_BLOCKS, _WGRAD_MINCHUNKS, _WGRAD_NT,
 // _WGRAD_MAXSPLIT
-int g_tune[7] = {-1, -1, -1, -1, -1, -1, -1};
+int g_tune[8] = {-1, -1, -1, -1, -1, -1, -1, 0};
 
 }  // namespace hyres
 
@@ -1919,11 +2121,18 @@ static bool wres32_ok(const hyres_conv_geom* g, const hyres_epilogue* e) {
     return tiles >= 2LL * wres_blocks(groups) && (long long)g->B * g->Hi * g->Wi * g->ldx * 4 < 0x7FFFFFF0LL;
 }
 
+// fp32 GEMM mode of the weight-resident 3x3 (hyres_conv_tuning key 7): 0 = native fp32 MFMA, 1 = bf16x6
+static bool wres_bf6() { return g_tune[7] == 1; }
+
 static int launch_wres32(const ConvArgs& a, hipStream_t st) {
     const hyres_conv_geom& g = a.g;
     const int ntiles = g.B * ((g.Ho + HALO_R - 1) / HALO_R) * (g.Wo / HALO_TW);
     const int groups = g.Co / 32;
     const int per = wres_blocks(groups);
+    if (wres_bf6()) {
+        hipLaunchKernelGGL(conv3x3_wres_bf6_kernel, dim3(per * groups), dim3(512), 0, st, a, ntiles, groups);
+        return HY_LAUNCH_CHECK("conv3x3_wres_bf6_kernel");
+    }
     hipLaunchKernelGGL(conv3x3_wres_f32_kernel, dim3(per * groups), dim3(512), 0, st, a, ntiles, groups);
     return HY_LAUNCH_CHECK("conv3x3_wres_f32_kernel");
 }
@@ -2030,7 +2239,7 @@ static long long plan_ws_bytes(const hyres_conv_geom* g, const ConvPlan& p) {
 }
 
 int hyres_conv_tuning(int key, int value, int* old) {
-    HY_REQUIRE(key >= 0 && key < 7, HYRES_E_ARG, "conv_tuning: key %d", key);
+    HY_REQUIRE(key >= 0 && key < 8, HYRES_E_ARG, "conv_tuning: key %d", key);
     if (old) *old = g_tune[key];
     g_tune[key] = value;
     return ok();
@@ -2183,7 +2392,7 @@ int hyres_conv_kernel_name(const hyres_conv_geom* g, const hyres_epilogue* e, in
         return 0;
     }
     if (ch.mode == 0 && wres32_ok(g, e)) {
-        snprintf(buf, n, "conv3x3_wres_f32_kernel");
+        snprintf(buf, n, wres_bf6() ? "conv3x3_wres_bf6_kernel" : "conv3x3_wres_f32_kernel");
         return 0;
     }
     if (ch.mode == 0 && halo16_ok(g, e)) {

@@ -13,6 +13,6 @@ namespace hyres {
 constexpr int KT = 32;  // K chunk (floats)
 
 // tile / split-K overrides set through hyres_conv_tuning (conv.hip; -1 = the planners' heuristics)
-extern int g_tune[7];
+extern int g_tune[8];
 
 }  // namespace hyres

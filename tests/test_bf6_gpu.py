@@ -1,0 +1,98 @@
+"""fp32 GEMM on the bf16 MFMA ("bf16x6", hyres_conv_tuning key HYRES_TUNE_F32_GEMM = 7, csrc/conv.hip
+conv3x3_wres_bf6_kernel): each fp32 operand is split into three bf16 pieces and each product formed from the six
+cross products with i + j <= 2, fp32 accumulation. Claim under test: it is as accurate as the native fp32 MFMA
+(v_mfma_f32_32x32x2_f32, an fmaf chain) — per product ~2^-25 relative against fp32's 2^-24 rounding — so the fp32
+parity bars of the model hold unchanged. Checked against float64 on the 3x3 64->64 convs the kernel serves
+(forward with bias / residual / ReLU, input-gradient with the ReLU mask and accumulation) and on a whole C2-shape
+train step's gradients against the native path."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from helpers import rel_err
+
+pytestmark = pytest.mark.gpu
+
+
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    return torch.device("cuda:0")
+
+
+def _rand(shape, seed, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.rand(shape, generator=g) * 2 - 1) * scale
+
+
+class _Bf6:
+    def __init__(self, on):
+        self.on = on
+
+    def __enter__(self):
+        import ctypes
+        from hyres_hip import _lib as L
+        self.old = ctypes.c_int(0)
+        L.call("hyres_conv_tuning", 7, 1 if self.on else 0, ctypes.byref(self.old))
+        return self
+
+    def __exit__(self, *a):
+        from hyres_hip import _lib as L
+        L.call("hyres_conv_tuning", 7, self.old.value, None)
+
+
+def test_bf6_conv3x3_as_accurate_as_fp32():
+    from hyres_hip import _lib as L
+    from hyres_hip import ops as O
+    import ctypes
+    D = dev()
+    B, C, H, W = 4, 64, 128, 128  # 256 tiles: the weight-resident kernel's eligibility (2 tiles per block)
+    x = _rand((B, C, H, W), 1).to(D)
+    w = _rand((C, C, 3, 3), 2, (C * 9) ** -0.5).to(D)
+    b = _rand((C,), 3, 0.1).to(D)
+    r = _rand((B, C, H, W), 4).to(D)
+    ref = F.relu(F.conv2d(x.double(), w.double(), b.double(), padding=1) + r.double())
+    outs, names = {}, {}
+    for on in (False, True):
+        with _Bf6(on):
+            xn, rn = O.to_nhwc(x), O.to_nhwc(r)
+            g = O._geom("hyres_geom_conv2d", B, H, W, C, C, C, C, 3, 3, 1, 1, 1)
+            e = L.Epilogue()
+            e.kind, e.act, e.bias, e.res, e.ldres = L.EPI_BIAS, L.ACT_RELU, b.data_ptr(), rn.ptr(), C
+            names[on] = O.conv_variant(g, e, False)
+            yn = O.conv2d(None, xn, torch.nn.Parameter(w), b, pad=1, act=L.ACT_RELU, res=rn)
+            outs[on] = O.to_nchw(yn).double()
+    torch.cuda.synchronize()
+    assert names[True] == "conv3x3_wres_bf6_kernel" and names[False] == "conv3x3_wres_f32_kernel", names
+    e32, e6 = rel_err(outs[False].cpu(), ref.cpu()), rel_err(outs[True].cpu(), ref.cpu())
+    d = (outs[True] - ref).abs().max().item(), (outs[False] - ref).abs().max().item()
+    print(f"3x3 64->64 +res relu, max-norm error vs fp64: native fp32 {e32:.2e}, bf16x6 {e6:.2e} (abs {d})")
+    assert e6 <= 2.0 * e32 + 1e-9 and e6 < 1e-6
+
+
+def test_bf6_train_step_gradients_match_native_fp32():
+    """The C2 train step at bs 4 / 128^2 (every ResidualUnit / MultiScaleRefine 64-channel 3x3 forward and
+    input-gradient on the weight-resident kernel): loss and every parameter gradient with bf16x6 against the native
+    fp32 path, normwise — the two differ by fp32 rounding only (measured ~1e-6; ReLU / round() decisions at exact
+    fp32 ties aside, bounded 1e-4)."""
+    from hyres_hip.loss import RateDistortionLoss
+    from hyres_hip.weights import synthetic_state_dict
+    from models import ResidualJPEGCompression
+    D = dev()
+    torch.manual_seed(0)
+    x = torch.rand((4, 3, 128, 128), generator=torch.Generator().manual_seed(8))
+    res = {}
+    for on in (False, True):
+        net = ResidualJPEGCompression(jpeg_quality=50)
+        torch.nn.Module.load_state_dict(net, synthetic_state_dict(net.state_dict()), strict=True)
+        net = net.to(D).train()
+        with _Bf6(on):
+            out = net(x, noisequant=False)
+            c = RateDistortionLoss(lmbda=0.045, alpha=0)(out, x.to(D))
+            c["loss"].backward()
+        torch.cuda.synchronize()
+        res[on] = (float(c["loss"].detach()), torch.cat([p.grad.reshape(-1) for n, p in sorted(net.named_parameters())
+                                                          if p.grad is not None]).double().cpu())
+    dl = abs(res[True][0] / res[False][0] - 1)
+    dg = float((res[True][1] - res[False][1]).norm() / res[False][1].norm())
+    print(f"bf16x6 vs native fp32 train step: loss {dl:.2e}, flat gradient {dg:.2e}")
+    assert dl < 1e-5 and dg < 1e-4
