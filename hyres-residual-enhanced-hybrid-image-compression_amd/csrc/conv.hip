@@ -196,26 +196,60 @@ __device__ __forceinline__ void epi_store4(const hyres_epilogue& e, float* y, in
     }
 }
 
-template <int TM, int TN, int WAVES_M, int WAVES_N, int MODE, bool SPLITK, bool F16, int IO>
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+
+// fp32 -> three bf16 pieces h + m + l (24 significant bits, remainder <= 2^-25 |x|): the bf16x6 fp32 GEMM's operands
+__device__ __forceinline__ void bf6_split4(float4 v, bf16x4_t& h, bf16x4_t& m, bf16x4_t& l) {
+    const float x[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const __bf16 a = (__bf16)x[i];
+        const float r1 = x[i] - (float)a;
+        const __bf16 b = (__bf16)r1;
+        h[i] = a;
+        m[i] = b;
+        l[i] = (__bf16)(r1 - (float)b);
+    }
+}
+
+// acc += a * b to fp32 accuracy from the three-piece operands: the six cross products with i + j <= 2, the
+// smallest first
+__device__ __forceinline__ floatx16 bf6_mfma(const bf16x8_t (&a)[3], const bf16x8_t (&b)[3], floatx16 acc) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], acc, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], acc, 0, 0, 0);
+}
+
+template <int TM, int TN, int WAVES_M, int WAVES_N, int MODE, bool SPLITK, bool F16, int IO, bool B6 = false>
 __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
     // MODE 0: Ci % 32 == 0 (float4 loads); 1: same + square A (GDN); 2: generic scalar (small Ci).
     // F16: operands rounded to fp16 when staged into LDS ([row][32 halves], pitch PADH halves) and
     // consumed by v_mfma_f32_32x32x16_f16 (lane r,h holds row r, k = 8h..8h+7), fp32 accumulation.
     // IO (fp16 activations in HBM, autocast inference): bit 0 X is fp16 (8-byte loads of 4 channels),
     // bit 1 Y / res / aux0 / out2 are fp16; arithmetic stays fp32 (F16: fp16 MFMA operands as before).
+    // B6: fp32 operands split into three bf16 planes when staged ([plane][row][32], pitch PADH), products to fp32
+    // accuracy on v_mfma_f32_32x32x16_bf16 (bf6_mfma; hyres_conv_tuning key 7, conv3x3_wres_bf6_kernel's numerics)
     static_assert(!F16 || MODE != 2, "fp16 operands on the Ci % 32 == 0 paths only");
+    static_assert(!B6 || (!F16 && IO == 0 && MODE != 2), "bf16x6: fp32 operands on the vector path");
     static_assert(!(IO & 1) || MODE != 2, "fp16 X on the Ci % 32 == 0 paths only");
     constexpr bool XH = (IO & 1) != 0, YH = (IO & 2) != 0;
     constexpr int XES = XH ? 2 : 4;  // X element bytes
     constexpr int PADH = 40;
     constexpr int BM = 32 * TM * WAVES_M;
     constexpr int BN = 32 * TN * WAVES_N;
-    constexpr int SMEM = ((BM + BN) * PADK > BM * (32 * WAVES_N + 8)) ? (BM + BN) * PADK : BM * (32 * WAVES_N + 8);
+    constexpr int SOP = B6 ? 3 * (BM + BN) * PADH / 2 : (BM + BN) * PADK;  // operand staging (floats)
+    constexpr int SMEM = (SOP > BM * (32 * WAVES_N + 8)) ? SOP : BM * (32 * WAVES_N + 8);
     __shared__ __attribute__((aligned(16))) float smem[SMEM];
     float* const As = smem;
     float* const Bs = smem + BM * PADK;
     _Float16* const Ah = reinterpret_cast<_Float16*>(smem);
     _Float16* const Bh = Ah + BM * PADH;
+    __bf16* const Pb = reinterpret_cast<__bf16*>(smem);  // B6: plane p = Pb + p * (BM + BN) * PADH, A rows then B
+    constexpr int PLANE = (BM + BN) * PADH;
 
     const hyres_conv_geom& g = a.g;
     const int tid = threadIdx.x;
@@ -347,7 +381,26 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
         }
     };
     auto store_chunk = [&]() {
-        if constexpr (F16) {
+        if constexpr (B6) {
+#pragma unroll
+            for (int q = 0; q < A_V; ++q) {
+                bf16x4_t h, m, l;
+                bf6_split4(ra[q], h, m, l);
+                const int o = (tid / 8 + 32 * q) * PADH + 4 * c4;
+                *reinterpret_cast<bf16x4_t*>(&Pb[o]) = h;
+                *reinterpret_cast<bf16x4_t*>(&Pb[PLANE + o]) = m;
+                *reinterpret_cast<bf16x4_t*>(&Pb[2 * PLANE + o]) = l;
+            }
+#pragma unroll
+            for (int q = 0; q < B_V; ++q) {
+                bf16x4_t h, m, l;
+                bf6_split4(rb[q], h, m, l);
+                const int o = (BM + tid / 8 + 32 * q) * PADH + 4 * c4;
+                *reinterpret_cast<bf16x4_t*>(&Pb[o]) = h;
+                *reinterpret_cast<bf16x4_t*>(&Pb[PLANE + o]) = m;
+                *reinterpret_cast<bf16x4_t*>(&Pb[2 * PLANE + o]) = l;
+            }
+        } else if constexpr (F16) {
             typedef _Float16 half4 __attribute__((ext_vector_type(4)));
 #pragma unroll
             for (int q = 0; q < A_V; ++q) {
@@ -415,6 +468,30 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
         store_chunk();
         __syncthreads();
         if (kc + 1 < kend) load_chunk(kc + 1);
+        if constexpr (B6) {
+            if (a.prio) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int s16 = 0; s16 < 2; ++s16) {
+                bf16x8_t af[TM][3], bf[TN][3];
+#pragma unroll
+                for (int p = 0; p < 3; ++p) {
+#pragma unroll
+                    for (int tm = 0; tm < TM; ++tm)
+                        af[tm][p] = *reinterpret_cast<const bf16x8_t*>(
+                            &Pb[p * PLANE + (wm * TM * 32 + tm * 32 + lr) * PADH + 16 * s16 + 8 * lh]);
+#pragma unroll
+                    for (int tn = 0; tn < TN; ++tn)
+                        bf[tn][p] = *reinterpret_cast<const bf16x8_t*>(
+                            &Pb[p * PLANE + (BM + wn * TN * 32 + tn * 32 + lr) * PADH + 16 * s16 + 8 * lh]);
+                }
+#pragma unroll
+                for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                    for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = bf6_mfma(af[tm], bf[tn], acc[tm][tn]);
+            }
+            if (a.prio) __builtin_amdgcn_s_setprio(0);
+            continue;
+        }
         if constexpr (F16) {
             typedef _Float16 half8 __attribute__((ext_vector_type(8)));
             if (a.prio) __builtin_amdgcn_s_setprio(1);
@@ -650,6 +727,13 @@ template <int TM, int TN, int WAVES_M, int WAVES_N, int MODE, bool SPLITK, bool 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(conv_wpe<TM, TN, MODE>())))
 void conv_fwd_kernel(const ConvArgs a) {
     conv_fwd_body<TM, TN, WAVES_M, WAVES_N, MODE, SPLITK, F16, 0>(a);
+}
+
+// fp32 operands, bf16x6 products (hyres_conv_tuning key 7): the compiler's register allocation (the three-plane
+// fragments do not fit the 4-waves-per-SIMD bound of conv_fwd_kernel)
+template <int TM, int TN, int WAVES_M, int WAVES_N, int MODE, bool SPLITK>
+__global__ __launch_bounds__(256) void conv_fwd_b6_kernel(const ConvArgs a) {
+    conv_fwd_body<TM, TN, WAVES_M, WAVES_N, MODE, SPLITK, false, 0, true>(a);
 }
 
 // fp16 activations in HBM (IO = 1: X fp16, 2: Y fp16, 3: both); fp16 MFMA operands except on the
@@ -1213,24 +1297,8 @@ constexpr int BF6_WPL = 4 * 9 * 32 * 16;  // bf16 per weight plane
 constexpr int BF6_HPL = HALO_NPX * 16;    // bf16 per halo plane
 constexpr int BF6_HE = HALO_NPX * 4;      // float4 per 16-channel halo chunk
 constexpr int BF6_HV = (BF6_HE + 511) / 512;
-typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
-
 // 16-B segment (0 / 1) of element k (0..15) of row r in a swizzled [row][16] bf16 image, as an element offset
 __device__ __forceinline__ int bf6_off(int r, int k) { return r * 16 + ((((k >> 3) ^ (r >> 3)) & 1) << 3) + (k & 7); }
-
-__device__ __forceinline__ void bf6_split4(float4 v, bf16x4_t& h, bf16x4_t& m, bf16x4_t& l) {
-    const float x[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const __bf16 a = (__bf16)x[i];
-        const float r1 = x[i] - (float)a;
-        const __bf16 b = (__bf16)r1;
-        h[i] = a;
-        m[i] = b;
-        l[i] = (__bf16)(r1 - (float)b);
-    }
-}
 
 __global__ __launch_bounds__(512, 1) void conv3x3_wres_bf6_kernel(const ConvArgs a, int ntiles, int groups) {
     __shared__ __attribute__((aligned(16))) __bf16 lds[3 * BF6_WPL + 3 * BF6_HPL];
@@ -1816,6 +1884,16 @@ static int launch_fwd(const ConvArgs& a, int mode, hipStream_t st) {
             else hipLaunchKernelGGL((conv_fwd_kernel<TM, TN, WM_, WN_, 1, false, true>), grid, dim3(256), 0, st, a);
         }
         return HY_LAUNCH_CHECK("conv_fwd_kernel(f16)");
+    }
+    if (g_tune[7] == 1 && mode != 2) {  // fp32 GEMM on the bf16 MFMA (bf16x6)
+        if (a.nsplit > 1) {
+            if (mode == 0) hipLaunchKernelGGL((conv_fwd_b6_kernel<TM, TN, WM_, WN_, 0, true>), grid, dim3(256), 0, st, a);
+            else hipLaunchKernelGGL((conv_fwd_b6_kernel<TM, TN, WM_, WN_, 1, true>), grid, dim3(256), 0, st, a);
+        } else {
+            if (mode == 0) hipLaunchKernelGGL((conv_fwd_b6_kernel<TM, TN, WM_, WN_, 0, false>), grid, dim3(256), 0, st, a);
+            else hipLaunchKernelGGL((conv_fwd_b6_kernel<TM, TN, WM_, WN_, 1, false>), grid, dim3(256), 0, st, a);
+        }
+        return HY_LAUNCH_CHECK("conv_fwd_b6_kernel");
     }
     // split-K launches are a separate instantiation (partials to the slab, no epilogue)
     if (a.nsplit > 1) {
@@ -2411,6 +2489,10 @@ int hyres_conv_kernel_name(const hyres_conv_geom* g, const hyres_epilogue* e, in
     if (e->io_f16 & 3) {
         snprintf(buf, n, "conv_fwd_h_kernel<%s, %d, %s, %d>", tiles[ch.tile], ch.mode, split ? "true" : "false",
                  e->io_f16 & 3);
+        return 0;
+    }
+    if (g_tune[7] == 1 && !f16 && ch.mode != 2) {
+        snprintf(buf, n, "conv_fwd_b6_kernel<%s, %d, %s>", tiles[ch.tile], ch.mode, split ? "true" : "false");
         return 0;
     }
     snprintf(buf, n, "conv_fwd_kernel<%s, %d, %s, %s>", tiles[ch.tile], ch.mode, split ? "true" : "false",

@@ -25,11 +25,14 @@ def main():
     ap.add_argument("--res", action="store_true", help="fused residual add (RU / RBB tail)")
     ap.add_argument("--f16", action="store_true", help="fp16 operands (autocast)")
     ap.add_argument("--tile", type=int, default=-1, help="force a conv tile (hyres_conv_tuning key 0)")
+    ap.add_argument("--bf6", action="store_true", help="fp32 GEMM on the bf16 MFMA (hyres_conv_tuning key 7)")
     a = ap.parse_args()
     from hyres_hip import _lib as L
     from hyres_hip import ops as O
     if a.tile >= 0:
         L.call("hyres_conv_tuning", 0, a.tile, None)
+    if a.bf6:
+        L.call("hyres_conv_tuning", 7, 1, None)
     dev = torch.device("cuda:0")
     x = O.Node(torch.randn(a.B, a.H, a.H, a.Ci, device=dev), rg=False)
     w = torch.randn(a.Co, a.Ci, a.K, a.K, device=dev) / (a.Ci * a.K * a.K) ** 0.5
@@ -52,7 +55,7 @@ def main():
     Ho = y.H
     flops = 2.0 * a.B * Ho * Ho * a.K * a.K * a.Ci * a.Co
     byts = 4.0 * (a.B * a.H * a.H * a.Ci + a.B * Ho * Ho * a.Co * (2 if a.res else 1) + a.K * a.K * a.Ci * a.Co)
-    print(f"conv B{a.B} {a.H}x{a.H}x{a.Ci} -> {Ho}x{Ho}x{a.Co} K{a.K} s{a.stride}{' +res' if a.res else ''}{' f16' if a.f16 else ''}: {us:.1f} us, "
+    print(f"conv B{a.B} {a.H}x{a.H}x{a.Ci} -> {Ho}x{Ho}x{a.Co} K{a.K} s{a.stride}{' +res' if a.res else ''}{' f16' if a.f16 else ''}{' bf16x6' if a.bf6 else ''}: {us:.1f} us, "
           f"{flops / us / 1e6:.1f} TFLOP/s, {byts / us / 1e3:.0f} GB/s")
 
 
