@@ -69,6 +69,41 @@ def test_bf6_conv3x3_as_accurate_as_fp32():
     assert e6 <= 2.0 * e32 + 1e-9 and e6 < 1e-6
 
 
+@pytest.mark.parametrize("case", [
+    # B, Ci, Co, H, K, stride, (the implicit-GEMM families of the fp32 step)
+    (2, 128, 128, 64, 5, 2),   # g_a 5x5 stride 2 (128x128 tiles)
+    (4, 64, 128, 64, 1, 1),    # short-K 1x1 (64x128 tiles)
+    (16, 96, 96, 32, 3, 1),    # AttentionBlock(192) 3x3 at 32^2 (64x64 tiles, small grid)
+    (2, 384, 192, 16, 3, 1),   # hyperprior 3x3 (split-K)
+])
+def test_bf6_implicit_gemm_conv_as_accurate_as_fp32(case):
+    """conv_fwd_b6_kernel (hyres_conv_tuning key 7 on the implicit-GEMM conv): forward with bias, every tile family
+    and split-K, against float64; error no worse than twice the native fp32 kernel's."""
+    from hyres_hip import _lib as L
+    from hyres_hip import ops as O
+    B, Ci, Co, H, K, s = case
+    D = dev()
+    x = _rand((B, Ci, H, H), 21).to(D)
+    w = _rand((Co, Ci, K, K), 22, (Ci * K * K) ** -0.5).to(D)
+    b = _rand((Co,), 23, 0.1).to(D)
+    ref = F.conv2d(x.double(), w.double(), b.double(), stride=s, padding=K // 2)
+    outs, names = {}, {}
+    for on in (False, True):
+        with _Bf6(on):
+            xn = O.to_nhwc(x)
+            yn = O.conv2d(None, xn, torch.nn.Parameter(w), b, stride=s, pad=K // 2)
+            outs[on] = O.to_nchw(yn).double()
+            g = O._geom("hyres_geom_conv2d", B, H, H, Ci, Ci, Co, Co, K, K, s, K // 2, 1)
+            e = L.Epilogue()
+            e.kind, e.bias = L.EPI_BIAS, b.data_ptr()
+            names[on] = O.conv_variant(g, e, O.conv_split(g, e) > 1)
+    torch.cuda.synchronize()
+    e32, e6 = rel_err(outs[False].cpu(), ref.cpu()), rel_err(outs[True].cpu(), ref.cpu())
+    print(case, names, f"error vs fp64: native {e32:.2e}, bf16x6 {e6:.2e}")
+    assert names[True].startswith("conv_fwd_b6_kernel") or names[True].startswith("conv3x3_wres_bf6")
+    assert e6 <= 2.0 * e32 + 1e-9 and e6 < 1e-6
+
+
 def test_bf6_train_step_gradients_match_native_fp32():
     """The C2 train step at bs 4 / 128^2 (every ResidualUnit / MultiScaleRefine 64-channel 3x3 forward and
     input-gradient on the weight-resident kernel): loss and every parameter gradient with bf16x6 against the native
