@@ -113,13 +113,13 @@ def test_bf6_train_step_gradients_match_native_fp32():
     from hyres_hip.weights import synthetic_state_dict
     from models import ResidualJPEGCompression
     D = dev()
-    torch.manual_seed(0)
     x = torch.rand((4, 3, 128, 128), generator=torch.Generator().manual_seed(8))
     res = {}
     for on in (False, True):
         net = ResidualJPEGCompression(jpeg_quality=50)
         torch.nn.Module.load_state_dict(net, synthetic_state_dict(net.state_dict()), strict=True)
         net = net.to(D).train()
+        torch.manual_seed(0)  # the training noise seeds come from torch's CPU generator: same draws in both runs
         with _Bf6(on):
             out = net(x, noisequant=False)
             c = RateDistortionLoss(lmbda=0.045, alpha=0)(out, x.to(D))
