@@ -127,6 +127,9 @@ class CapturedStep:
         self.graph = torch.cuda.CUDAGraph()
         O.PrepBatch.prepare(dev)  # descriptor table uploaded now: the capture records ONE batched re-layout
         O.bump_weight_epoch()  # record every weight re-layout inside the graph
+        # the graph's batched re-layout reads this descriptor table by address: keep it alive for the graph's
+        # lifetime (an eager step after the capture may register new entries and rebuild the table)
+        self._prep_table = O.PrepBatch.table(dev)
         # "thread_local" when an RCCL process group exists: its watchdog thread polls events while the
         # main thread captures (no collective is ever inside the graph)
         cap_stream = None
@@ -156,6 +159,9 @@ class CapturedStep:
             if listener is not None:
                 O.GradReady.listeners.remove(listener)
         O.bump_weight_epoch()  # eager calls must not reuse buffers only the graph writes
+        # ... and the scratch buffers its kernels were recorded with: an eager call that grows a workspace slot
+        # replaces the slot's tensor, and the old one must outlive the graph
+        self._ws_keep = list(O.Workspace._bufs.values())
         torch.cuda.synchronize(dev)
 
     def close(self) -> None:
@@ -167,6 +173,8 @@ class CapturedStep:
             g.reset()
             self.graph = None
         self.marker_events = []
+        self._prep_table = None
+        self._ws_keep = []
 
     def __del__(self):
         try:

@@ -418,6 +418,13 @@ class PrepBatch:
         return False
 
     @classmethod
+    def table(cls, device) -> Optional[torch.Tensor]:
+        """The current device descriptor table (a captured graph that recorded the batch launch holds it: a
+        later eager rebuild must not free the table the graph's kernel reads)."""
+        st = cls._state.get(device.index) if device.type == "cuda" else None
+        return None if st is None else st["table"]
+
+    @classmethod
     def prepare(cls, device) -> None:
         """Build the descriptor table now (outside graph capture) so a capture can record the batch."""
         st = cls._state.get(device.index) if device.type == "cuda" else None
