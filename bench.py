@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--no-host-jpeg", action="store_true", help="skip the with-host-JPEG legs")
     ap.add_argument("--no-amp", action="store_true", help="skip the f16-amp (train.sh --mixed-precision) leg")
     ap.add_argument("--jpeg-procs", type=int, default=None, help="JPEG worker processes (default min(8, cpus))")
+    ap.add_argument("--fp32-gemm", choices=["default", "native", "bf16x6"], default="default",
+                    help="fp32 conv GEMMs: the native fp32 MFMA or the bf16x6 split (hyres_conv_tuning key 7)")
     return ap.parse_args()
 
 
@@ -98,8 +100,8 @@ def cpu_baseline(args, budget_s):
 
 
 # scripts/profile_round.sh r3z: the fp32 line's dominant kernel, and the AMP leg's dominant kernel from the same passes
-PMC_TRAFFIC = os.path.join(REPO, "profiles", os.environ.get("HYRES_PMC_TRAFFIC", "r3z_pmc_traffic.json"))
-PMC_TRAFFIC_AMP = os.path.join(REPO, "profiles", os.environ.get("HYRES_PMC_TRAFFIC_AMP", "r3z_pmc_traffic_amp.json"))
+PMC_TRAFFIC = os.path.join(REPO, "profiles", os.environ.get("HYRES_PMC_TRAFFIC", "r4b_pmc_traffic.json"))
+PMC_TRAFFIC_AMP = os.path.join(REPO, "profiles", os.environ.get("HYRES_PMC_TRAFFIC_AMP", "r4b_pmc_traffic_amp.json"))
 EAGER_TIMED = 3  # eager steps behind the live per-launch roofline timing
 
 
@@ -306,7 +308,7 @@ def amp_leg(net, opt, aux_opt, crit, x, jpeg, jpeg_bpp, args):
 
 
 def with_traffic(r, kernel):
-    """The AMP leg's roofline entry with its PMC-measured HBM bytes per launch (profiles/r3z_pmc_traffic_amp.json)."""
+    """The AMP leg's roofline entry with its PMC-measured HBM bytes per launch (profiles/r4b_pmc_traffic_amp.json)."""
     if r is not None:
         r["traffic"] = traffic_bytes_per_launch(kernel, PMC_TRAFFIC_AMP)
     return r
@@ -496,6 +498,9 @@ def main():
         tdist.init_process_group(os.environ.get("HYRES_BENCH_BACKEND", "nccl"))
     dev = torch.device("cuda", local)
 
+    from hyres_hip import _lib as L
+    if args.fp32_gemm != "default":
+        L.call("hyres_conv_tuning", 7, 1 if args.fp32_gemm == "bf16x6" else 0, None)
     from hyres_hip.weights import synthetic_state_dict
     from hyres_hip.loss import RateDistortionLoss
     from hyres_hip.optim import FusedAdam

@@ -35,8 +35,9 @@ for ph in "$@"; do
            cat gpurun_out/mem_defer1.log gpurun_out/mem_defer0.log | grep WGRAD_DEFER > gpurun_out/${tag}_mem_probe.txt ;;
     dist)  bash scripts/dist_rehearsal.sh; echo "dist rehearsal exit $?" ;;
     probe) scripts/gpu_run.sh "bf16x6_probe:120:scripts/bf16x6_probe" \
-             "bf6_micro:300:for H in 128 256; do for m in '' --bf6; do python3 scripts/conv_micro.py --H \$H \$m; python3 scripts/conv_micro.py --H \$H --res --relu \$m; done; done" || exit $?
-           grep -h "us," gpurun_out/bf16x6_probe.log gpurun_out/bf6_micro.log > gpurun_out/${tag}_bf6_micro.txt ;;
+             "bf6_micro:300:for H in 128 256; do for m in '' --bf6; do python3 scripts/conv_micro.py --H \$H \$m; python3 scripts/conv_micro.py --H \$H --res --relu \$m; done; done" \
+             "bf6_families:400:bash scripts/bf6_families.sh" || exit $?
+           grep -h "us," gpurun_out/bf16x6_probe.log gpurun_out/bf6_micro.log gpurun_out/bf6_families.log > gpurun_out/${tag}_bf6_micro.txt ;;
     *) echo "unknown phase $ph"; exit 2 ;;
   esac
 done
