@@ -1281,7 +1281,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3_wres_f32_kernel(const ConvArgs
 }
 
 // ------------------------------------------------------------------------------------------------
-// fp32-accurate weight-resident 3x3 conv on the bf16 MFMA ("bf16x6", hyres_conv_tuning key 7 = 1; opt-in).
+// fp32-accurate weight-resident 3x3 conv on the bf16 MFMA ("bf16x6", hyres_conv_tuning key 7 = 1, the default).
 // conv3x3_wres_f32_kernel above runs at ~0.7 of the fp32 MFMA peak, and that peak (157 TF/s) is 1/16 of the bf16
 // MFMA's. Here every fp32 operand is split into three bf16 pieces x = x0 + x1 + x2 (x0 = bf16(x), x1 = bf16(x - x0),
 // x2 = bf16(x - x0 - x1): 24 significant bits, |x - x0 - x1 - x2| <= 2^-25 |x|) and each product is formed from the
@@ -1342,8 +1342,9 @@ __global__ __launch_bounds__(512, 1) void conv3x3_wres_bf6_kernel(const ConvArgs
         i0 = rt * HALO_R;
         j0 = ct * HALO_TW;
     };
-    float4 hreg[BF6_HV];
-    auto hload = [&](int step) {  // step = 4 * tile + chunk (16 channels)
+    // halo chunks are prefetched TWO steps ahead (two register sets, alternating, as conv3x3_wres_f16_kernel): one
+    // 16-channel step is 54 MFMAs per wave (~1.7k cycles), too short to cover an HBM load issued one step ahead
+    auto hload = [&](float4 (&hreg)[BF6_HV], int step) {  // step = 4 * tile + chunk (16 channels)
         int b, i0, j0;
         tile_of(step >> 2, b, i0, j0);
         const int c = step & 3;
@@ -1359,7 +1360,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_wres_bf6_kernel(const ConvArgs
             hreg[v] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
         }
     };
-    auto hstore = [&]() {
+    auto hstore = [&](const float4 (&hreg)[BF6_HV]) {
 #pragma unroll
         for (int v = 0; v < BF6_HV; ++v) {
             const int e = tid + 512 * v;
@@ -1385,12 +1386,15 @@ __global__ __launch_bounds__(512, 1) void conv3x3_wres_bf6_kernel(const ConvArgs
     const __amdgpu_buffer_rsrc_t r_old = opnd_rsrc(e.accumulate ? a.y : nullptr, npix * g.ldy * 4);
     float4 ebias[4], eres[4], emask[4], eold[4];
     const int steps = mytiles * 4;
+    float4 hA[BF6_HV], hB[BF6_HV];
     if (steps > 0) {
-        hload(0);
-        hstore();
+        hload(hA, 0);
+        hstore(hA);
     }
+    if (steps > 1) hload(hB, 1);
     __syncthreads();
-    for (int s = 0; s < steps; ++s) {
+    // step s: the set that held step s's halo (stored) receives step s + 2; the other holds step s + 1
+    auto body = [&](int s, float4 (&hl)[BF6_HV], const float4 (&hs)[BF6_HV]) {
         const int k = s >> 2, c = s & 3;
         int b, i0, j0;
         tile_of(k, b, i0, j0);
@@ -1411,7 +1415,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_wres_bf6_kernel(const ConvArgs
                 eold[qd] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r_old, oy, 0, 0));
             }
         }
-        if (s + 1 < steps) hload(s + 1);
+        if (s + 2 < steps) hload(hl, s + 2);
 #pragma unroll
         for (int t = 0; t < 9; ++t) {
             const int2 o = tapoff[t];
@@ -1461,8 +1465,12 @@ __global__ __launch_bounds__(512, 1) void conv3x3_wres_bf6_kernel(const ConvArgs
             for (int r = 0; r < 16; ++r) acc[r] = 0.f;
         }
         __syncthreads();  // every wave is done with this chunk's halo
-        if (s + 1 < steps) hstore();
+        if (s + 1 < steps) hstore(hs);
         __syncthreads();
+    };
+    for (int s = 0; s < steps; s += 2) {
+        body(s, hA, hB);
+        if (s + 1 < steps) body(s + 1, hB, hA);
     }
 }
 
@@ -1976,7 +1984,7 @@ static void dense_taps(hyres_conv_geom* g, int KH, int KW, int sgn, int dil, int
 
 // keys: HYRES_TUNE_TILE, _SPLIT_BLOCKS, _SPLIT_MINCHUNKS, _WGRAD_BLOCKS, _WGRAD_MINCHUNKS, _WGRAD_NT,
 // _WGRAD_MAXSPLIT
-int g_tune[8] = {-1, -1, -1, -1, -1, -1, -1, 0};
+int g_tune[8] = {-1, -1, -1, -1, -1, -1, -1, 1};  // key 7: bf16x6 fp32 GEMMs by default
 
 }  // namespace hyres
 

@@ -167,9 +167,10 @@ int hyres_conv_plan(const hyres_conv_geom* g, const hyres_epilogue* e, int* tile
 #define HYRES_TUNE_WGRAD_MINCHUNKS 4  /* minimum 32-pixel chunks per split */
 #define HYRES_TUNE_WGRAD_NT 5         /* 1: no tap grouping (one tap per block column group) */
 #define HYRES_TUNE_WGRAD_MAXSPLIT 6   /* maximum split count */
-#define HYRES_TUNE_F32_GEMM 7         /* fp32 GEMM of the weight-resident 3x3: 0 native fp32 MFMA (default), 1 bf16x6
-                                       * (each fp32 operand split into 3 bf16 pieces, 6 cross products, fp32 accumulation:
-                                       * per-product error <= ~2^-25, i.e. fp32-accurate, on the 16x faster bf16 MFMA) */
+#define HYRES_TUNE_F32_GEMM 7         /* GEMM of the fp32 convolutions (forward and input-gradient; weight gradients stay
+                                       * native): 1 bf16x6 (default: each fp32 operand split into 3 bf16 pieces, the 6
+                                       * cross products with i + j <= 2, fp32 accumulation — per-product error <= ~2^-25,
+                                       * i.e. fp32-accurate, on the 16x faster bf16 MFMA), 0 the native fp32 MFMA */
 int hyres_conv_tuning(int key, int value, int* old);
 
 /* Weight gradient:  dW[t][m][n] = sum_q P[q][m] * Q[shift_t(q)][n]  over a base grid q (B,Hq,Wq).

@@ -129,14 +129,29 @@ def test_conv_kernel_name_follows_the_launch_routing():
     """hyres_conv_kernel_name (the profiler label bench.py's roofline line uses) reports the launcher's
     own tile choice: 128x64 tiles for 3x3 64-channel layers, half-height tiles for short-K 1x1 layers,
     the VALU narrow kernel for <= 4 output channels, split-K / fp16 / GDN-square flags."""
+    import ctypes
     from hyres_hip import _lib as L
     from hyres_hip.ops import _geom, conv_variant
     e = L.Epilogue()
     e.kind = L.EPI_BIAS
     g3 = _geom("hyres_geom_conv2d", 16, 128, 128, 64, 64, 64, 64, 3, 3, 1, 1, 1)
+    g3b = _geom("hyres_geom_conv2d", 16, 128, 128, 96, 96, 64, 64, 3, 3, 1, 1, 1)  # Ci = 96: implicit GEMM
+    # the default fp32 GEMM: bf16x6 on the bf16 MFMA (hyres_conv_tuning key 7 = 1)
+    assert conv_variant(g3, e, False) == "conv3x3_wres_bf6_kernel"
+    assert conv_variant(g3b, e, False) == "conv_fwd_b6_kernel<2, 1, 2, 2, 0, false>"
+    assert conv_variant(g3b, e, True) == "conv_fwd_b6_kernel<2, 1, 2, 2, 0, true>"
+    old = ctypes.c_int(0)
+    L.call("hyres_conv_tuning", 7, 0, ctypes.byref(old))  # the native fp32 MFMA from here on
+    assert old.value == 1
+    try:
+        _native_routing(L, e, g3, g3b, _geom, conv_variant)
+    finally:
+        L.call("hyres_conv_tuning", 7, old.value, None)
+
+
+def _native_routing(L, e, g3, g3b, _geom, conv_variant):
     # fp32 3x3 with Ci = 64, W % 64 == 0 and >= 2 tiles per block: the weight-resident persistent kernel
     assert conv_variant(g3, e, False) == "conv3x3_wres_f32_kernel"
-    g3b = _geom("hyres_geom_conv2d", 16, 128, 128, 96, 96, 64, 64, 3, 3, 1, 1, 1)  # Ci = 96: implicit GEMM
     assert conv_variant(g3b, e, False) == "conv_fwd_kernel<2, 1, 2, 2, 0, false, false>"
     assert conv_variant(g3b, e, True) == "conv_fwd_kernel<2, 1, 2, 2, 0, true, false>"
     g1 = _geom("hyres_geom_conv2d", 16, 128, 128, 64, 64, 128, 128, 1, 1, 1, 0, 1)

@@ -29,6 +29,17 @@ def _rand(shape, seed, scale=1.0):
     return (torch.rand(shape, generator=g) * 2 - 1) * scale
 
 
+@pytest.fixture(params=["bf16x6", "native"])
+def fp32_gemm(request):
+    """The fp32 convs' GEMM (hyres_conv_tuning key 7): bf16x6 on the bf16 MFMA (the default) and the native fp32
+    MFMA — every test taking this fixture holds its fp32 bars on both."""
+    from hyres_hip import _lib as L
+    old = ctypes.c_int(0)
+    L.call("hyres_conv_tuning", 7, 1 if request.param == "bf16x6" else 0, ctypes.byref(old))
+    yield request.param
+    L.call("hyres_conv_tuning", 7, old.value, None)
+
+
 # ------------------------------------------------------------------------------------------------ ops
 CONV_CASES = [
     # B, Ci, Co, H, W, K, stride, pad, dil
@@ -70,7 +81,7 @@ CONV_CASES = [
 
 
 @pytest.mark.parametrize("case", CONV_CASES)
-def test_conv2d_fwd_bwd(case):
+def test_conv2d_fwd_bwd(case, fp32_gemm):
     from hyres_hip import _lib as L
     from hyres_hip import ops as O
     B, Ci, Co, H, W, K, s, p, d = case
@@ -99,7 +110,7 @@ def test_conv2d_fwd_bwd(case):
 
 @pytest.mark.parametrize("case", [(2, 183, 183, 64, 128, 96), (1, 260, 260, 128, 64, 64), (2, 16, 16, 64, 128, 64),
                                   (1, 9, 23, 96, 96, 128)])
-def test_conv1x1_epilogue_chain(case):
+def test_conv1x1_epilogue_chain(case, fp32_gemm):
     """1x1 convs through a chain that exercises every streamed epilogue operand: a = relu(conv1(x) + r)
     (residual), b = relu(conv2(a)) (its dgrad takes the ReLU mask), y = conv3(b) + conv4(x) (x fans out:
     conv4's dgrad accumulates into conv1's). In the first two cases (>= 65536 pixels, K in {64, 96, 128})
@@ -149,7 +160,7 @@ def test_conv1x1_epilogue_chain(case):
 
 @pytest.mark.parametrize("case", [(2, 192, 128, 4, 4), (2, 128, 128, 8, 8), (2, 128, 3, 16, 16),
                                   (2, 128, 192, 4, 4), (2, 64, 64, 32, 32)])  # last: halo wgrad, Q stride 2
-def test_deconv2d_fwd_bwd(case):
+def test_deconv2d_fwd_bwd(case, fp32_gemm):
     from hyres_hip import ops as O
     B, Ci, Co, H, W = case
     x = _rand((B, Ci, H, W), 5)
@@ -176,7 +187,7 @@ def test_deconv2d_fwd_bwd(case):
 
 
 @pytest.mark.parametrize("inverse", [False, True])
-def test_gdn_fwd_bwd(inverse):
+def test_gdn_fwd_bwd(inverse, fp32_gemm):
     from oracle.compressai_restated import GDN as RefGDN
     from hyres_hip.layers import GDN
     from hyres_hip import ops as O
@@ -267,7 +278,7 @@ def test_bilinear_se_spatial_attention():
     assert rel_err(wd.grad.cpu(), wr.grad) < TOL
 
 
-def test_checkerboard_masked_conv():
+def test_checkerboard_masked_conv(fp32_gemm):
     """CheckboardMaskedConv2d: weight masked in place, forward/dgrad on the 12 live taps, dense dW."""
     from hyres_hip import ops as O
     from models.layers.checkerboard import CheckboardMaskedConv2d
@@ -502,7 +513,7 @@ def _check_grads(net, ref, terms, tol=1e-3, slope_tol=5e-4):
     return rows
 
 
-def test_model_train_step_matches_reference():
+def test_model_train_step_matches_reference(fp32_gemm):
     """C2 semantics: train mode, noisequant=False, lambda=0.045, recorded noise -> loss and aux loss vs the
     reference fixture (1e-4), every parameter gradient vs the fp64 oracle (pinned to the fixture's gradient
     summaries in test_oracle_golden.py) within 1e-3 normwise.  Decision-exact: where a ReLU / PReLU input or
@@ -1197,7 +1208,7 @@ def test_checkerboard_index_sets_bit_exact_on_gpu():
     assert torch.equal(yna, y * ~anchor)
 
 
-def test_c2_size_train_step_vs_fp64_oracle():
+def test_c2_size_train_step_vs_fp64_oracle(fp32_gemm):
     """BASELINE config C2 at its full size (bs=16, 256x256, train, noisequant=False, lambda=0.045): the HIP
     train step (the bench's tile routing, split-K factors and XCD-ordered grids) vs the fp64 oracle on the
     host with the same recorded noise: loss within 1e-4 and every parameter gradient normwise within 1e-3,
