@@ -1142,6 +1142,164 @@ __global__ __launch_bounds__(256 * G, G == 1 ? 2 : 1) void wgrad_halo_f16_kernel
 }
 
 // ------------------------------------------------------------------------------------------------
+// fp32 halo-staged weight gradient on the bf16 MFMA ("bf16x6", hyres_conv_tuning key 7 = 1, the default fp32 GEMM):
+// wgrad_halo_f16_kernel's schedule and transposed LDS images, with each fp32 operand split when staged into three
+// bf16 planes (x = x0 + x1 + x2, 24 significant bits) and every product formed from the six cross products with
+// i + j <= 2 in fp32 accumulation (bf6_mfma: per product ~2^-25 relative, below the fp32 MFMA's own rounding).
+// Per 32-pixel chunk a wave issues NT x 2 x 6 v_mfma_f32_32x32x16_bf16 (32 cycles each) against NT x 16
+// v_mfma_f32_32x32x2_f32 (64 cycles each) in wgrad_halo_kernel: 2.67x fewer MFMA cycles. LDS: 2 buffers x 3 planes
+// x (P chunk + Q halo) <= 158 KB, one 4-wave block per CU. Bias gradient = fp32 column sums of the unsplit P.
+// ------------------------------------------------------------------------------------------------
+template <int KR, int KW, int SQ, int DIL = 1>
+__global__ __launch_bounds__(256, 1) void wgrad_halo_bf6_kernel(const WgradArgs a, int dhg, int dwg) {
+    constexpr int BM = 64, BN = 64, NT = KR * KW, HC = 31 * SQ + DIL * (KW - 1) + 1;
+    constexpr int PP = BM + 32, PQ = BN + 32;  // bf16 row pitches (the transposed reads' conflict-free pitch)
+    constexpr int PSZ = KT * PP, HSZ = KR * HC * PQ, PLANE = PSZ + HSZ, BUF = 3 * PLANE;
+    constexpr int P_V = KT * BM / 4 / 256;
+    constexpr int H_E = KR * HC * (BN / 4);
+    constexpr int H_V = (H_E + 255) / 256;
+    static_assert(PLANE % 4 == 0, "8-byte aligned planes for the transposed reads");
+    static_assert(2 * BUF * 2 <= 160 * 1024, "LDS");
+    __shared__ __attribute__((aligned(16))) __bf16 smem[2 * BUF];
+    const hyres_wgrad_desc& d = a.d;
+    const int tid = threadIdx.x;
+    const int bid = blockIdx.x;
+    const int lb = (bid & 7) * (gridDim.x >> 3) + (bid >> 3);  // XCD-aware order, as wgrad_kernel
+    if (lb >= a.nblocks) return;
+    int rr = lb;
+    const int mt = rr % a.mtiles; rr /= a.mtiles;
+    const int nt = rr % a.ntiles; rr /= a.ntiles;
+    const int grp = rr % a.ngroups;
+    const int split = rr / a.ngroups;
+    const int m0 = mt * BM, n0 = nt * BN;
+    const int t0 = grp * NT;
+    const int dh0 = dhg + grp * KR * DIL;
+    const int cpr = d.Wq / 32;
+    const int pc = (tid % (BM / 4)) * 4, prow0 = tid / (BM / 4);  // this thread's fixed P channel quad
+    float4 rp[P_V], rh[H_V];
+    auto load = [&](int kc) {
+        const int b = kc / (d.Hq * cpr);
+        const int rem = kc - b * d.Hq * cpr;
+        const int i = rem / cpr;
+        const int j0 = (rem - i * cpr) * 32;
+        const long long q0 = (long long)kc * 32;
+#pragma unroll
+        for (int q = 0; q < P_V; ++q)
+            rp[q] = m0 + pc < d.M ? ld4(a.p + (q0 + prow0 + 16 * q) * d.ldp + m0 + pc) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int q = 0; q < H_V; ++q) {
+            const int e = tid + 256 * q;
+            const int pix = e / (BN / 4), c = (e % (BN / 4)) * 4;
+            const int hr = pix / HC, hc = pix - (pix / HC) * HC;
+            const int ih = i * SQ + dh0 + DIL * hr, iw = j0 * SQ + dwg + hc;
+            const bool ok = e < H_E && (unsigned)ih < (unsigned)d.Hqq && (unsigned)iw < (unsigned)d.Wqq && n0 + c < d.N;
+            rh[q] = ok ? ld4(a.q + ((long long)(b * d.Hqq + ih) * d.Wqq + iw) * d.ldq + n0 + c)
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    const bool do_bias = a.bias_slab != nullptr && nt == 0 && grp == 0;
+    float4 bsum = make_float4(0.f, 0.f, 0.f, 0.f);
+    auto put = [&](__bf16* base, int o, const float4& v) {
+        bf16x4_t h, m, l;
+        bf6_split4(v, h, m, l);
+        *reinterpret_cast<bf16x4_t*>(&base[o]) = h;
+        *reinterpret_cast<bf16x4_t*>(&base[PLANE + o]) = m;
+        *reinterpret_cast<bf16x4_t*>(&base[2 * PLANE + o]) = l;
+    };
+    auto store = [&](int buf) {
+        __bf16* B0 = smem + buf * BUF;
+#pragma unroll
+        for (int q = 0; q < P_V; ++q) {
+            if (do_bias) { bsum.x += rp[q].x; bsum.y += rp[q].y; bsum.z += rp[q].z; bsum.w += rp[q].w; }
+            put(B0, (prow0 + 16 * q) * PP + pc, rp[q]);
+        }
+#pragma unroll
+        for (int q = 0; q < H_V; ++q) {
+            const int e = tid + 256 * q;
+            if (e < H_E) put(B0, PSZ + (e / (BN / 4)) * PQ + (e % (BN / 4)) * 4, rh[q]);
+        }
+    };
+
+    const int lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    // transposed-read lane address (wgrad_f16_kernel): half lh takes k rows 8lh..8lh+7 of a 16-k step
+    const int lh = lane >> 5, lg = (lane >> 4) & 1, lq = (lane >> 2) & 3, lp = lane & 3;
+    const int tr_row = 8 * lh + lq, tr_col = 16 * lg + 4 * lp;
+    auto frag = [&](const __bf16* p, int pitch) {  // 8 consecutive k of one row / column, transposed read
+        const halfx4_t lo = lds_tr4(reinterpret_cast<const _Float16*>(p));
+        const halfx4_t hi = lds_tr4(reinterpret_cast<const _Float16*>(p + 4 * pitch));
+        return __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+    };
+    floatx16 acc[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+    const int kb = split * a.chunks_per_split;
+    const int ke = min(a.nchunks, kb + a.chunks_per_split);
+    if (kb < ke) {
+        load(kb);
+        store(0);
+    }
+    __syncthreads();
+    int cur = 0;
+    for (int kc = kb; kc < ke; ++kc) {
+        const bool next = kc + 1 < ke;
+        if (next) load(kc + 1);  // next chunk in flight during this chunk's NT x 12 MFMAs per wave
+        const __bf16* Ps = smem + cur * BUF;
+        const __bf16* Hs = Ps + PSZ;
+#pragma unroll
+        for (int s = 0; s < KT / 16; ++s) {
+            bf16x8_t af[3];
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) af[pl] = frag(Ps + pl * PLANE + (16 * s + tr_row) * PP + wm * 32 + tr_col, PP);
+            static_for<NT>([&](auto J) {
+                constexpr int t = decltype(J)::value;
+                constexpr int hr = t / KW, hc = t % KW;
+                const int ob = (hr * HC + DIL * hc + SQ * (16 * s + tr_row)) * PQ + wn * 32 + tr_col;
+                bf16x8_t bf[3];
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl) bf[pl] = frag(Hs + pl * PLANE + ob, SQ * PQ);
+                acc[t] = bf6_mfma(af, bf, acc[t]);
+            });
+        }
+        if (next) store(cur ^ 1);
+        __syncthreads();
+        cur ^= 1;
+    }
+    if (do_bias) {  // block-uniform
+        float4* red = reinterpret_cast<float4*>(smem);  // the loop ended with a barrier
+        red[tid] = bsum;
+        __syncthreads();
+        if (tid < BM / 4) {
+            float4 s4 = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int r = 0; r < 256 / (BM / 4); ++r) {
+                const float4 v = red[tid + r * (BM / 4)];
+                s4.x += v.x; s4.y += v.y; s4.z += v.z; s4.w += v.w;
+            }
+            float* dst = a.bias_slab + (long long)split * d.M + m0 + 4 * tid;
+            const float sv[4] = {s4.x, s4.y, s4.z, s4.w};
+            for (int c = 0; c < 4; ++c)
+                if (m0 + 4 * tid + c < d.M) dst[c] = sv[c];
+        }
+    }
+    const int lr = lane & 31;
+    const long long MN = (long long)d.M * d.N;
+    static_for<NT>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        const int n = n0 + wn * 32 + lr;
+        if (n < d.N) {
+            float* out = a.slab + ((long long)split * d.ntaps + t0 + j) * MN + n;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                if (m < d.M) out[(long long)m * d.N] = acc[j][r];
+            }
+        }
+    });
+}
+
+// ------------------------------------------------------------------------------------------------
 // Thin-operand weight gradient: dW[t][m][n] = sum_q P[q][m] * Q[shift_t(q)][n] with N <= 4 (the 3-channel
 // image side: refine conv 3->64 / 64->3 at 256^2 (the latter through the swapped descriptor), g_a's 5x5 s2
 // conv 3->128, g_s's deconv 128->3) and M = 64*MW wide channels. An MFMA tile would be >90 % padding and
@@ -1821,6 +1979,18 @@ static int wgrad_issue(const hyres_wgrad_desc* d0, const float* pp, const float*
         else if (io == 2) halo16g(std::integral_constant<int, 2>{});
         else if (io == 3) halo16g(std::integral_constant<int, 3>{});
         else halo16g(std::integral_constant<int, 0>{});
+    } else if (p.halo && f32_gemm_bf6() && io == 0) {  // fp32 operands, bf16x6 products
+        if (p.hk == 3 && p.NT == 3 && p.hdil == 2)
+            hipLaunchKernelGGL((wgrad_halo_bf6_kernel<1, 3, 1, 2>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
+        else if (p.hk == 3 && p.NT == 3)
+            hipLaunchKernelGGL((wgrad_halo_bf6_kernel<1, 3, 1, 1>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
+        else if (p.hk == 3 && p.hdil == 2)
+            hipLaunchKernelGGL((wgrad_halo_bf6_kernel<3, 3, 1, 2>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
+        else if (p.hk == 3)
+            hipLaunchKernelGGL((wgrad_halo_bf6_kernel<3, 3, 1, 1>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
+        else if (d->sq == 1)
+            hipLaunchKernelGGL((wgrad_halo_bf6_kernel<1, 5, 1, 1>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
+        else hipLaunchKernelGGL((wgrad_halo_bf6_kernel<1, 5, 2, 1>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
     } else if (p.halo) {
         auto halo32 = [&](auto gc) {
             constexpr int G_ = decltype(gc)::value;
