@@ -1705,7 +1705,9 @@ static WgradPlan wgrad_plan(const hyres_wgrad_desc* d) {
     if (p.halo) {
         // whole rounds only: the halo kernel runs 2 blocks per CU (3 for 5x5 stride 1); a partial last round
         // of long split-K blocks costs as much as a full one, so drop it (e.g. 800 -> 500 blocks)
-        const long long cap = 256LL * ((p.hk == 5 && d->sq == 1) ? 3 : 2);
+        // (the bf16x6 kernel: 1 block per CU when it stages all 9 taps' halo, 158 KB of LDS)
+        const bool b6_9 = f32_gemm_bf6() && !wgrad_f16_ok(d) && p.NT == 9;
+        const long long cap = 256LL * (b6_9 ? 1 : (p.hk == 5 && d->sq == 1) ? 3 : 2);
         if (tiles * p.nsplit > cap) p.nsplit = (int)std::max<long long>(1, (tiles * p.nsplit / cap) * cap / tiles);
         // and fill a partial single round when that grows the slab by <= 25 % (128^2 3x3: 455 -> 512)
         else if (cap / tiles <= maxsplit && 4 * (cap / tiles) <= 5LL * p.nsplit) p.nsplit = (int)(cap / tiles);
@@ -1979,7 +1981,7 @@ static int wgrad_issue(const hyres_wgrad_desc* d0, const float* pp, const float*
         else if (io == 2) halo16g(std::integral_constant<int, 2>{});
         else if (io == 3) halo16g(std::integral_constant<int, 3>{});
         else halo16g(std::integral_constant<int, 0>{});
-    } else if (p.halo && f32_gemm_bf6() && io == 0) {  // fp32 operands, bf16x6 products
+    } else if (p.halo && f32_gemm_bf6()) {  // fp32 operands (fp16 ones were converted above), bf16x6 products
         if (p.hk == 3 && p.NT == 3 && p.hdil == 2)
             hipLaunchKernelGGL((wgrad_halo_bf6_kernel<1, 3, 1, 2>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
         else if (p.hk == 3 && p.NT == 3)
