@@ -1142,6 +1142,155 @@ __global__ __launch_bounds__(256 * G, G == 1 ? 2 : 1) void wgrad_halo_f16_kernel
 }
 
 // ------------------------------------------------------------------------------------------------
+// fp32 1x1 weight gradient on the bf16 MFMA ("bf16x6", the default fp32 GEMM): wgrad1x1_kernel's chunking (32-pixel
+// chunks, P and Q rows of the same pixels as contiguous float4 rows, double-buffered, one barrier per chunk) with
+// the staged tiles split into three bf16 planes in the transposed [pixel][channel] layout of wgrad_f16_kernel (pitch
+// B + 32 halves, ds_read_b64_tr_b16) and bf6_mfma products: 2 x 6 v_mfma_f32_32x32x16_bf16 per tile and chunk
+// against 16 v_mfma_f32_32x32x2_f32, at an intensity (~21 FLOP/B at 128^2 64 <-> 128) where the fp32 MFMA and HBM
+// cost about the same. Bias gradient = fp32 column sums of the unsplit P from the staging registers.
+// ------------------------------------------------------------------------------------------------
+template <int TM, int TN, int WAVES_M, int WAVES_N>
+__global__ __launch_bounds__(256) void wgrad1x1_bf6_kernel(const WgradArgs a) {
+    constexpr int BM = 32 * TM * WAVES_M, BN = 32 * TN * WAVES_N;
+    constexpr int PP = BM + 32, PQ = BN + 32;  // bf16 row pitches
+    constexpr int PSZ = KT * PP, QSZ = KT * PQ, PLANE = PSZ + QSZ, BUF = 3 * PLANE;
+    constexpr int P_V = KT * BM / 4 / 256, Q_V = KT * BN / 4 / 256;
+    static_assert(P_V >= 1 && Q_V >= 1, "tile too small");
+    static_assert(PLANE % 4 == 0 && 2 * BUF * 2 <= 160 * 1024, "LDS");
+    __shared__ __attribute__((aligned(16))) __bf16 smem[2 * BUF];
+    const hyres_wgrad_desc& d = a.d;
+    const int tid = threadIdx.x;
+    const int bid = blockIdx.x;
+    const int lb = (bid & 7) * (gridDim.x >> 3) + (bid >> 3);  // XCD-aware order, as wgrad_kernel
+    if (lb >= a.nblocks) return;
+    int rr = lb;
+    const int mt = rr % a.mtiles; rr /= a.mtiles;
+    const int nt = rr % a.ntiles; rr /= a.ntiles;
+    const int split = rr;
+    const int m0 = mt * BM, n0 = nt * BN;
+    const long long Qtot = (long long)d.B * d.Hq * d.Wq;
+    // fixed per-thread channel quads (256 % (B / 4) == 0): rows tid / (B / 4) + i * 256 / (B / 4)
+    const int pc = (tid % (BM / 4)) * 4, prow0 = tid / (BM / 4);
+    const int qc = (tid % (BN / 4)) * 4, qrow0 = tid / (BN / 4);
+    constexpr int PRS = 256 / (BM / 4), QRS = 256 / (BN / 4);
+    float4 rp[P_V], rq[Q_V];
+    auto load = [&](int kc) {
+        const long long k0 = (long long)kc * KT;
+#pragma unroll
+        for (int i = 0; i < P_V; ++i) {
+            const long long row = k0 + prow0 + i * PRS;
+            rp[i] = (row < Qtot && m0 + pc < d.M) ? ld4(a.p + row * d.ldp + m0 + pc) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int i = 0; i < Q_V; ++i) {
+            const long long row = k0 + qrow0 + i * QRS;
+            rq[i] = (row < Qtot && n0 + qc < d.N) ? ld4(a.q + row * d.ldq + n0 + qc) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    const bool do_bias = a.bias_slab != nullptr && nt == 0;
+    float4 bsum = make_float4(0.f, 0.f, 0.f, 0.f);
+    auto put = [&](__bf16* base, int o, const float4& v) {
+        bf16x4_t h, m, l;
+        bf6_split4(v, h, m, l);
+        *reinterpret_cast<bf16x4_t*>(&base[o]) = h;
+        *reinterpret_cast<bf16x4_t*>(&base[PLANE + o]) = m;
+        *reinterpret_cast<bf16x4_t*>(&base[2 * PLANE + o]) = l;
+    };
+    auto store = [&](int buf) {
+        __bf16* B0 = smem + buf * BUF;
+#pragma unroll
+        for (int i = 0; i < P_V; ++i) {
+            if (do_bias) { bsum.x += rp[i].x; bsum.y += rp[i].y; bsum.z += rp[i].z; bsum.w += rp[i].w; }
+            put(B0, (prow0 + i * PRS) * PP + pc, rp[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < Q_V; ++i) put(B0, PSZ + (qrow0 + i * QRS) * PQ + qc, rq[i]);
+    };
+    const int lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+    const int lh = lane >> 5, lg = (lane >> 4) & 1, lq = (lane >> 2) & 3, lp = lane & 3;
+    const int tr_row = 8 * lh + lq, tr_col = 16 * lg + 4 * lp;
+    auto frag = [&](const __bf16* p, int pitch) {
+        const halfx4_t lo = lds_tr4(reinterpret_cast<const _Float16*>(p));
+        const halfx4_t hi = lds_tr4(reinterpret_cast<const _Float16*>(p + 4 * pitch));
+        return __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+    };
+    floatx16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    const int kb = split * a.chunks_per_split;
+    const int ke = min(a.nchunks, kb + a.chunks_per_split);
+    if (kb < ke) {
+        load(kb);
+        store(0);
+    }
+    __syncthreads();
+    int cur = 0;
+    for (int kc = kb; kc < ke; ++kc) {
+        const bool next = kc + 1 < ke;
+        if (next) load(kc + 1);  // in flight during this chunk's MFMAs
+        const __bf16* Ps = smem + cur * BUF;
+        const __bf16* Qs = Ps + PSZ;
+#pragma unroll
+        for (int s = 0; s < KT / 16; ++s) {
+            bf16x8_t af[TM][3], bf[TN][3];
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl)
+                    af[tm][pl] = frag(Ps + pl * PLANE + (16 * s + tr_row) * PP + wm * TM * 32 + tm * 32 + tr_col, PP);
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl)
+                    bf[tn][pl] = frag(Qs + pl * PLANE + (16 * s + tr_row) * PQ + wn * TN * 32 + tn * 32 + tr_col, PQ);
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = bf6_mfma(af[tm], bf[tn], acc[tm][tn]);
+        }
+        if (next) store(cur ^ 1);
+        __syncthreads();
+        cur ^= 1;
+    }
+    if (do_bias) {  // block-uniform
+        float4* red = reinterpret_cast<float4*>(smem);  // the loop ended with a barrier
+        red[tid] = bsum;
+        __syncthreads();
+        if (tid < BM / 4) {
+            float4 s4 = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int r = 0; r < PRS; ++r) {
+                const float4 v = red[tid + r * (BM / 4)];
+                s4.x += v.x; s4.y += v.y; s4.z += v.z; s4.w += v.w;
+            }
+            float* dst = a.bias_slab + (long long)split * d.M + m0 + 4 * tid;
+            const float sv[4] = {s4.x, s4.y, s4.z, s4.w};
+            for (int c = 0; c < 4; ++c)
+                if (m0 + 4 * tid + c < d.M) dst[c] = sv[c];
+        }
+    }
+    const int lr = lane & 31;
+    const long long MN = (long long)d.M * d.N;
+    float* out = a.slab + (long long)split * MN;
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) {
+            const int n = n0 + wn * TN * 32 + tn * 32 + lr;
+            if (n >= d.N) continue;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + wm * TM * 32 + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                if (m < d.M) out[(long long)m * d.N + n] = acc[tm][tn][r];
+            }
+        }
+}
+
+// ------------------------------------------------------------------------------------------------
 // fp32 halo-staged weight gradient on the bf16 MFMA ("bf16x6", hyres_conv_tuning key 7 = 1, the default fp32 GEMM):
 // wgrad_halo_f16_kernel's schedule and transposed LDS images, with each fp32 operand split when staged into three
 // bf16 planes (x = x0 + x1 + x2, 24 significant bits) and every product formed from the six cross products with
@@ -1719,7 +1868,7 @@ static WgradPlan wgrad_plan(const hyres_wgrad_desc* d) {
     // branches' blocks off its CU; profiles/r3o_halo_groups.txt. Removed in round 4.)
     p.hg = 1;
     p.g1x1 = 1;
-    if (!small && !halo && kt == KT && !p.tapn && !d->square_q && d->ntaps == 1 && d->dh[0] == 0 &&
+    if (!small && !halo && kt == KT && !f32_gemm_bf6() && !p.tapn && !d->square_q && d->ntaps == 1 && d->dh[0] == 0 &&
         d->dw[0] == 0 && d->sq == 1 && d->Hqq == d->Hq && d->Wqq == d->Wq && p.ngroups == 1 && p.nsplit >= 2) {
         p.g1x1 = 2;
         p.nsplit = (p.nsplit + 1) / 2;
@@ -1946,7 +2095,13 @@ static int wgrad_issue(const hyres_wgrad_desc* d0, const float* pp, const float*
     const bool one = !thin && !p.halo && !wgrad_f16_ok(d) && !sqr && !p.tapn && vp && vq &&
                      d->ntaps == 1 && d->dh[0] == 0 && d->dw[0] == 0 && d->sq == 1 && d->Hqq == d->Hq &&
                      d->Wqq == d->Wq && p.ngroups == 1;
-    if (one) {
+    if (one && f32_gemm_bf6()) {  // bf16x6 products (the plan keeps one 4-wave group per block for it)
+        if (p.TMc == 2 && p.TNc == 2) hipLaunchKernelGGL((wgrad1x1_bf6_kernel<2, 2, 2, 2>), grid, dim3(256), 0, st, a);
+        else if (p.TMc == 2) hipLaunchKernelGGL((wgrad1x1_bf6_kernel<2, 1, 2, 2>), grid, dim3(256), 0, st, a);
+        else if (p.WMc == 1) hipLaunchKernelGGL((wgrad1x1_bf6_kernel<1, 1, 1, 4>), grid, dim3(256), 0, st, a);
+        else if (p.WNc == 1) hipLaunchKernelGGL((wgrad1x1_bf6_kernel<1, 1, 4, 1>), grid, dim3(256), 0, st, a);
+        else hipLaunchKernelGGL((wgrad1x1_bf6_kernel<1, 1, 2, 2>), grid, dim3(256), 0, st, a);
+    } else if (one) {
         auto w1 = [&](auto gc) {
             constexpr int G_ = decltype(gc)::value;
             const dim3 blk(256 * G_);
