@@ -153,6 +153,10 @@ def kernel_label(kernel):
         return "weight-resident persistent 3x3 conv, f16 MFMA, fp16 halo tiles in LDS"
     if kernel.startswith("conv3x3_halo_f16"):
         return "halo-staged 3x3 conv, f16 MFMA"
+    if kernel.startswith("conv_fwd_h_kernel"):
+        io = kernel.replace(" ", "").rstrip(">").split(",")[-1]
+        return (f"implicit-GEMM conv, f16 MFMA, fp16 activations in HBM (io {io}: bit 0 X, bit 1 Y/residual/aux), "
+                "fused epilogue")
     if "true>" in kernel.replace(" ", "").split(",")[-1]:
         return "implicit-GEMM conv, f16 MFMA, fused epilogue"
     return "implicit-GEMM conv, fp32 MFMA, fused epilogue"
