@@ -101,8 +101,8 @@ def cpu_baseline(args, budget_s):
 
 
 # scripts/profile_round.sh r3z: the fp32 line's dominant kernel, and the AMP leg's dominant kernel from the same passes
-PMC_TRAFFIC = os.path.join(REPO, "profiles", os.environ.get("HYRES_PMC_TRAFFIC", "r4b_pmc_traffic.json"))
-PMC_TRAFFIC_AMP = os.path.join(REPO, "profiles", os.environ.get("HYRES_PMC_TRAFFIC_AMP", "r4b_pmc_traffic_amp.json"))
+PMC_TRAFFIC = os.path.join(REPO, "profiles", os.environ.get("HYRES_PMC_TRAFFIC", "r4d_pmc_traffic.json"))
+PMC_TRAFFIC_AMP = os.path.join(REPO, "profiles", os.environ.get("HYRES_PMC_TRAFFIC_AMP", "r4d_pmc_traffic_amp.json"))
 EAGER_TIMED = 3  # eager steps behind the live per-launch roofline timing
 
 
@@ -345,7 +345,7 @@ def amp_leg(net, opt, aux_opt, crit, x, jpeg, jpeg_bpp, args):
 
 
 def with_traffic(r, kernel):
-    """The AMP leg's roofline entry with its PMC-measured HBM bytes per launch (profiles/r4b_pmc_traffic_amp.json)."""
+    """The AMP leg's roofline entry with its PMC-measured HBM bytes per launch (profiles/r4d_pmc_traffic_amp.json)."""
     if r is not None:
         r["traffic"] = traffic_bytes_per_launch(kernel, PMC_TRAFFIC_AMP)
     return r
@@ -696,9 +696,12 @@ def main():
     value = world * B * S * S * args.steps / elapsed / 1e6
 
     achieved = ks["flops"] / (ks["total_ms"] * 1e-3) / 1e12 if ks["total_ms"] > 0 else 0.0
-    iso = None
-    if ks_iso["kernel"] == ks["kernel"] and ks_iso["total_ms"] > 0:
-        iso = ks_iso["flops"] / (ks_iso["total_ms"] * 1e-3) / 1e12
+    # the same instantiation's entry in the isolated steps (it need not be the top kernel there)
+    iso = iso_us = None
+    ent = ks_iso.get("by_variant", {}).get(ks["kernel"])
+    if ent is not None and ent[0] > 0:
+        iso = ent[1] / (ent[0] * 1e-3) / 1e12
+        iso_us = 1000.0 * ent[0] / ent[3]
 
 
     if rank != 0:
@@ -784,7 +787,7 @@ def main():
                      "timing": f"HIP events around each launch of {EAGER_TIMED} eager steps after the timed region",
                      "achieved_isolated": None if iso is None else round(iso, 3),
                      "frac_isolated": None if iso is None else round(iso / kernel_peak(ks["kernel"]), 4),
-                     "avg_launch_us_isolated": round(ks_iso["avg_us"], 2),
+                     "avg_launch_us_isolated": None if iso_us is None else round(iso_us, 2),
                      "ms_by_variant": ks.get("by_variant_ms"),
                      "families": ks.get("families")},
         "graph": graphed is not None,

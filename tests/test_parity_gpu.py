@@ -700,8 +700,18 @@ def test_c3_bs32_eval_gc_path_parity():
         idx = [0, 31]
         out2 = net(x[idx], jpeg=(jpeg[idx], jpeg_bpp))
     torch.cuda.synchronize()
-    assert rel_err(out2["x_hat"].cpu(), out["x_hat"].cpu()[idx]) < TOL  # split-K order differs with B
-    assert _lik_flip_fraction(out2["likelihoods"]["y"].cpu(), out["likelihoods"]["y"].cpu()[idx]) <= 1e-5
+    # batch independence, decision-aware as _check_against_oracle: bs 32 and bs 2 take different kernels (the
+    # weight-resident 3x3 needs >= 2 tiles per CU, split-K factors follow the grid), so fp32 rounding differs and a
+    # y - mu within that noise of k + .5 may round the other way; each such flip perturbs x_hat only in its
+    # receptive field
+    ly2, ly = out2["likelihoods"]["y"].cpu().double(), out["likelihoods"]["y"].cpu()[idx].double()
+    nflip = int(((ly2 - ly).abs() > 1e-3 * ly.abs().clamp_min(1e-9)).sum())
+    assert nflip <= max(2, 1e-5 * ly.numel()), nflip
+    xa, xb = out2["x_hat"].cpu().double(), out["x_hat"].cpu()[idx].double()
+    nbad = int(((xa - xb).abs() / xb.abs().max() > TOL).sum())
+    print(f"bs32 vs bs2: {nflip} likelihood flips, {nbad} x_hat values beyond {TOL}, "
+          f"x_hat normwise {rel_err(xa, xb):.2e}")
+    assert nbad <= nflip * 64 * 64 * 3, (nbad, nflip)
     _check_against_oracle(out, idx, x, jpeg, float(jpeg_bpp))
 
 
