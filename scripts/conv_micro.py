@@ -25,14 +25,13 @@ def main():
     ap.add_argument("--res", action="store_true", help="fused residual add (RU / RBB tail)")
     ap.add_argument("--f16", action="store_true", help="fp16 operands (autocast)")
     ap.add_argument("--tile", type=int, default=-1, help="force a conv tile (hyres_conv_tuning key 0)")
-    ap.add_argument("--bf6", action="store_true", help="fp32 GEMM on the bf16 MFMA (hyres_conv_tuning key 7)")
+    ap.add_argument("--bf6", action="store_true", help="fp32 GEMM on the bf16 MFMA (hyres_conv_tuning key 7; default here: native)")
     a = ap.parse_args()
     from hyres_hip import _lib as L
     from hyres_hip import ops as O
     if a.tile >= 0:
         L.call("hyres_conv_tuning", 0, a.tile, None)
-    if a.bf6:
-        L.call("hyres_conv_tuning", 7, 1, None)
+    L.call("hyres_conv_tuning", 7, 1 if a.bf6 else 0, None)  # the native fp32 MFMA unless --bf6
     dev = torch.device("cuda:0")
     x = O.Node(torch.randn(a.B, a.H, a.H, a.Ci, device=dev), rg=False)
     w = torch.randn(a.Co, a.Ci, a.K, a.K, device=dev) / (a.Ci * a.K * a.K) ** 0.5
