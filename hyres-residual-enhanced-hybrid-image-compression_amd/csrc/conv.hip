@@ -1334,17 +1334,22 @@ __global__ __launch_bounds__(512, 1) void conv3x3_wres_bf6_kernel(const ConvArgs
             hreg[v] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
         }
     };
-    auto hstore = [&](const float4 (&hreg)[BF6_HV]) {
+    // the next step's halo is split into its bf16 pieces in registers DURING this step's MFMAs (hsplit, independent
+    // VALU work the scheduler interleaves with them); between the two barriers only the LDS stores remain (hput)
+    bf16x4_t sp[BF6_HV][3];
+    auto hsplit = [&](const float4 (&hreg)[BF6_HV]) {
+#pragma unroll
+        for (int v = 0; v < BF6_HV; ++v) bf6_split4(hreg[v], sp[v][0], sp[v][1], sp[v][2]);
+    };
+    auto hput = [&]() {
 #pragma unroll
         for (int v = 0; v < BF6_HV; ++v) {
             const int e = tid + 512 * v;
             if (e < BF6_HE) {
-                bf16x4_t h, m, l;
-                bf6_split4(hreg[v], h, m, l);
                 const int o = bf6_off(e >> 2, 4 * (e & 3));
-                *reinterpret_cast<bf16x4_t*>(&Hs[o]) = h;
-                *reinterpret_cast<bf16x4_t*>(&Hs[BF6_HPL + o]) = m;
-                *reinterpret_cast<bf16x4_t*>(&Hs[2 * BF6_HPL + o]) = l;
+                *reinterpret_cast<bf16x4_t*>(&Hs[o]) = sp[v][0];
+                *reinterpret_cast<bf16x4_t*>(&Hs[BF6_HPL + o]) = sp[v][1];
+                *reinterpret_cast<bf16x4_t*>(&Hs[2 * BF6_HPL + o]) = sp[v][2];
             }
         }
     };
@@ -1363,7 +1368,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_wres_bf6_kernel(const ConvArgs
     float4 hA[BF6_HV], hB[BF6_HV];
     if (steps > 0) {
         hload(hA, 0);
-        hstore(hA);
+        hsplit(hA);
+        hput();
     }
     if (steps > 1) hload(hB, 1);
     __syncthreads();
@@ -1410,6 +1416,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_wres_bf6_kernel(const ConvArgs
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1, x0, acc, 0, 0, 0);
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w0, x1, acc, 0, 0, 0);
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w0, x0, acc, 0, 0, 0);
+            if (t == 1 && s + 1 < steps) hsplit(hs);  // step s + 1's halo (loaded a step ago) -> bf16 pieces
         }
         if (c == 3) {
             if (i < g.Ho) {
@@ -1439,7 +1446,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_wres_bf6_kernel(const ConvArgs
             for (int r = 0; r < 16; ++r) acc[r] = 0.f;
         }
         __syncthreads();  // every wave is done with this chunk's halo
-        if (s + 1 < steps) hstore(hs);
+        if (s + 1 < steps) hput();
         __syncthreads();
     };
     for (int s = 0; s < steps; s += 2) {
