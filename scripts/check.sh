@@ -7,6 +7,8 @@
 #   mem     peak device memory with the deferred weight-gradient reduces on / off (scripts/mem_probe.py)
 #   dist    the N>1 rehearsal (scripts/dist_rehearsal.sh)
 #   probe   scripts/bf16x6_probe (fp32 GEMM: native f32 MFMA vs the bf16x6 split, speed and error)
+#   sq      SQ-counter passes of the bf16x6 kernels in isolation (scripts/pmc_sq.sh)
+#   layers  per-launch conv tables of one fp32 / AMP step (scripts/layer_table.py)
 # Every step runs under its own time limit (scripts/gpu_run.sh) and the pass stops at the first crash-like exit.
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
@@ -34,6 +36,9 @@ for ph in "$@"; do
     mem)   scripts/gpu_run.sh "mem_defer1:200:python3 scripts/mem_probe.py" "mem_defer0:200:HYRES_WGRAD_DEFER=0 python3 scripts/mem_probe.py" || exit $?
            cat gpurun_out/mem_defer1.log gpurun_out/mem_defer0.log | grep WGRAD_DEFER > gpurun_out/${tag}_mem_probe.txt ;;
     dist)  bash scripts/dist_rehearsal.sh; echo "dist rehearsal exit $?" ;;
+    sq)    bash scripts/pmc_sq.sh $tag || exit $? ;;
+    layers) scripts/gpu_run.sh "layers_fp32:200:python3 scripts/layer_table.py" "layers_amp:200:python3 scripts/layer_table.py --amp" || exit $?
+           cp gpurun_out/layers_fp32.log gpurun_out/${tag}_layers_fp32.txt; cp gpurun_out/layers_amp.log gpurun_out/${tag}_layers_amp.txt ;;
     probe) scripts/gpu_run.sh "bf16x6_probe:120:scripts/bf16x6_probe" \
              "bf6_micro:300:for H in 128 256; do for m in '' --bf6; do python3 scripts/conv_micro.py --H \$H \$m; python3 scripts/conv_micro.py --H \$H --res --relu \$m; done; done" \
              "bf6_families:400:bash scripts/bf6_families.sh" || exit $?
