@@ -37,6 +37,8 @@ for ph in "$@"; do
            cat gpurun_out/mem_defer1.log gpurun_out/mem_defer0.log | grep WGRAD_DEFER > gpurun_out/${tag}_mem_probe.txt ;;
     dist)  bash scripts/dist_rehearsal.sh; echo "dist rehearsal exit $?" ;;
     sq)    bash scripts/pmc_sq.sh $tag || exit $? ;;
+    ru)    scripts/gpu_run.sh "ru_micro:200:python3 scripts/ru_micro.py && python3 scripts/ru_micro.py --H 64 --W 64" || exit $?
+           grep "us," gpurun_out/ru_micro.log > gpurun_out/${tag}_ru_micro.txt ;;
     layers) scripts/gpu_run.sh "layers_fp32:200:python3 scripts/layer_table.py" "layers_amp:200:python3 scripts/layer_table.py --amp" || exit $?
            cp gpurun_out/layers_fp32.log gpurun_out/${tag}_layers_fp32.txt; cp gpurun_out/layers_amp.log gpurun_out/${tag}_layers_amp.txt ;;
     probe) scripts/gpu_run.sh "bf16x6_probe:120:scripts/bf16x6_probe" \
