@@ -116,7 +116,8 @@ FP32_GEMM_NOTE = {
               "the fp32 MFMA's own 2^-24 rounding; measured error vs fp64 equal to the native fp32 kernel's "
               "(tests/test_bf6_gpu.py) and the fp32 parity suite / C2 fp64-oracle test pass unchanged with it. "
               "The reference's own fp32 convs run with PyTorch's default cudnn.allow_tf32=True (10-bit mantissa "
-              "operands) on its NVIDIA hardware. Weight gradients stay on the native fp32 MFMA.",
+              "operands) on its NVIDIA hardware. Covers forward, input-gradient and the halo-staged / 1x1 weight "
+              "gradients (the generic tap-folded weight-gradient kernel stays on the fp32 MFMA).",
     "native": "fp32 conv GEMMs on the native fp32 MFMA (v_mfma_f32_32x32x2_f32)",
 }
 
