@@ -316,27 +316,34 @@ def amp_leg(net, opt, aux_opt, crit, x, jpeg, jpeg_bpp, args):
     torch.cuda.synchronize()
     ms_a = (time.time() - t0) * 1000 / nrep
     del cap
-    # round-4 A/B on the same box: the step with fp32 activation gradients and the unfused ResidualUnits (round 3's
-    # AMP path) — the gain of fp16 activation gradients + the fused RU forward
-    saved = (O.AMP_F16_GRAD, O.RU_FUSED)
-    O.AMP_F16_GRAD, O.RU_FUSED = False, False
-    try:
-        scaler_b = DeviceGradScaler(dev)
-        cap_b = CapturedStep(net, x, jpeg, jpeg_bpp, noisequant=False, criterion=crit, zero_grad=opt.zero_grad,
-                             amp=True, loss_scale=scaler_b.scale)
-        torch.cuda.synchronize()
-        t0 = time.time()
-        for _ in range(nrep):
-            cap_b.replay()
-            opt.zero_grad()
-        torch.cuda.synchronize()
-        ms_b = (time.time() - t0) * 1000 / nrep
-        del cap_b
-    finally:
-        O.AMP_F16_GRAD, O.RU_FUSED = saved
+    # round-4 A/B on the same box: the step with the unfused ResidualUnits, and with fp32 activation gradients and
+    # the unfused ResidualUnits (round 3's AMP path) — the gains of the fused RU forward and of fp16 gradients
+    def ab(f16_grad, ru_fused):
+        saved = (O.AMP_F16_GRAD, O.RU_FUSED)
+        O.AMP_F16_GRAD, O.RU_FUSED = f16_grad, ru_fused
+        try:
+            scaler_b = DeviceGradScaler(dev)
+            cap_b = CapturedStep(net, x, jpeg, jpeg_bpp, noisequant=False, criterion=crit, zero_grad=opt.zero_grad,
+                                 amp=True, loss_scale=scaler_b.scale)
+            torch.cuda.synchronize()
+            t0 = time.time()
+            for _ in range(nrep):
+                cap_b.replay()
+                opt.zero_grad()
+            torch.cuda.synchronize()
+            ms_ab = (time.time() - t0) * 1000 / nrep
+            cap_b.close()
+            del cap_b
+        finally:
+            O.AMP_F16_GRAD, O.RU_FUSED = saved
+        return ms_ab
+
+    ms_u = ab(True, False)
+    ms_b = ab(False, False)
     opt.zero_grad()
     return {"dtype": "f16-amp", "value": round(B * H * W / ms / 1e3, 4), "unit": "Mpixels/s", "ms_per_step": round(ms, 3),
-            "fwd_bwd_ms": round(ms_a, 3), "ab_fp32_grads_unfused_ru_fwd_bwd_ms": round(ms_b, 3),
+            "fwd_bwd_ms": round(ms_a, 3), "ab_unfused_ru_fwd_bwd_ms": round(ms_u, 3),
+            "ab_fp32_grads_unfused_ru_fwd_bwd_ms": round(ms_b, 3),
             "loss": loss, "loss_scale": scaler.get_scale(),
             "roofline": with_traffic(roofline_of(ks, MI355X_F16_PEAK_TFLOPS, F16_RIDGE), ks["kernel"]),
             "roofline_f16_mfma_kernel": roofline_of(ks_mfma, MI355X_F16_PEAK_TFLOPS, F16_RIDGE),
