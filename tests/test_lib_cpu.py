@@ -221,3 +221,25 @@ def test_conv_plan_split_follows_the_tile():
     assert lib.hyres_conv_workspace_bytes(ctypes.byref(h)) >= ns * 16 * 16 * 16 * 128 * 4
     big = _geom("hyres_geom_conv2d", 16, 128, 128, 64, 64, 64, 64, 3, 3, 1, 1, 1)
     assert plan(big) == (1, 1)
+
+
+def test_fp32_gemm_env_switch():
+    """HYRES_FP32_GEMM selects the fp32 convs' GEMM at library load: bf16x6 (default, hyres_conv_tuning key 7 = 1)
+    or the native fp32 MFMA (key 7 = 0); anything else is refused."""
+    import os
+    import subprocess
+    import sys
+    from conftest import PKG
+    code = ("import ctypes, sys; sys.path.insert(0, %r); from hyres_hip import _lib as L; o = ctypes.c_int(-1); "
+            "L.call('hyres_conv_tuning', 7, 1, ctypes.byref(o)); print(o.value)") % PKG
+    for env, want in ((None, "1"), ("bf16x6", "1"), ("native", "0")):
+        e = dict(os.environ)
+        e.pop("HYRES_FP32_GEMM", None)
+        if env is not None:
+            e["HYRES_FP32_GEMM"] = env
+        out = subprocess.run([sys.executable, "-c", code], env=e, capture_output=True, text=True, timeout=120)
+        assert out.returncode == 0, out.stderr
+        assert out.stdout.strip().splitlines()[-1] == want, (env, out.stdout)
+    e = dict(os.environ, HYRES_FP32_GEMM="tf32")
+    out = subprocess.run([sys.executable, "-c", code], env=e, capture_output=True, text=True, timeout=120)
+    assert out.returncode != 0 and "HYRES_FP32_GEMM" in out.stderr
