@@ -1568,6 +1568,107 @@ __global__ __launch_bounds__(256, 2) void conv1x1_stream_kernel(const ConvArgs a
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Streaming 1x1 conv with fp16 activations in HBM (AMP training / autocast, io_f16 = 3: X and Y / residual / mask /
+// old y all fp16), K = Ci in {64, 96, 128}, Co = 32 * NT in {64, 96, 128}, on the f16 MFMA. These layers (the
+// ResidualUnits' 1x1 convs and their input-gradients with the ReLU mask and the accumulated residual gradient) are
+// HBM-latency-bound on the tiled kernel (64-row blocks of 2-4 K chunks, each load then barrier then MFMA: ~0.3 of
+// HBM). Here, as conv1x1_stream_kernel, each WAVE streams its own 32-pixel tiles with no barrier after the one-time
+// weight staging (W -> fp16 in LDS, pitch K + 8 halves): the wave's X fragments come HBM -> registers in the MFMA
+// layout (lane (r, h): pixel p0 + r, channels 16j + 8h .. + 7, one 16-byte load per k-step) with a rolling prefetch
+// of the next tile, the product is formed transposed (C^T = W X^T) so each lane's accumulator holds 4 consecutive
+// channels of one pixel, and the epilogue operands of the tile (residual, ReLU mask, old y: fp16, 8 bytes per
+// channel quad) are requested BEFORE its MFMAs. Arithmetic: fp16 operands, fp32 accumulation, fp32 epilogue, one
+// rounding at the fp16 store — the tiled f16 kernel's, in the same K order.
+typedef _Float16 half8s_t __attribute__((ext_vector_type(8)));
+
+template <int NT, int KC>
+__global__ __launch_bounds__(256, 2) void conv1x1_stream_h_kernel(const ConvArgs a) {
+    constexpr int K = 16 * KC, KP = K + 8, CO = 32 * NT;
+    __shared__ __attribute__((aligned(16))) _Float16 Ws[CO * KP];
+    __shared__ __attribute__((aligned(16))) float bs[CO];
+    const hyres_conv_geom& g = a.g;
+    const hyres_epilogue& e = a.e;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int lr = lane & 31, lh = lane >> 5;
+    for (int i = tid; i < CO * (K / 4); i += 256) {
+        const int co = i / (K / 4), k4 = i - co * (K / 4);
+        const float4 w = ld4(a.w2 + (long long)co * a.ldw + 4 * k4);
+        *reinterpret_cast<half4_t*>(&Ws[co * KP + 4 * k4]) = half4_t{(_Float16)w.x, (_Float16)w.y, (_Float16)w.z,
+                                                                     (_Float16)w.w};
+    }
+    for (int i = tid; i < CO; i += 256) bs[i] = e.bias ? e.bias[i] : 0.f;
+    __syncthreads();
+
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, a.x_bytes, 0x00020000);
+    const _Float16* const res = reinterpret_cast<const _Float16*>(e.res);
+    const _Float16* const msk = reinterpret_cast<const _Float16*>(e.act == HYRES_ACT_RELU_MASK ? e.aux0 : nullptr);
+    _Float16* const y = reinterpret_cast<_Float16*>(a.y);
+    const int ntile = (a.M + 31) / 32;
+    const int gw = blockIdx.x * 4 + wave, nw = gridDim.x * 4;
+    auto load_x = [&](int tile, int j) -> half8s_t {
+        const int p = tile * 32 + lr;
+        const int off = (tile < ntile && p < a.M) ? (p * g.ldx + 16 * j + 8 * lh) * 2 : (int)0x80000000;
+        return __builtin_bit_cast(half8s_t, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
+    };
+    half8s_t xv[KC];
+#pragma unroll
+    for (int j = 0; j < KC; ++j) xv[j] = load_x(gw, j);
+    const half4_t hz = {(_Float16)0.f, (_Float16)0.f, (_Float16)0.f, (_Float16)0.f};
+    for (int tile = gw; tile < ntile; tile += nw) {
+        const int p = tile * 32 + lr;
+        const bool pok = p < a.M;
+        // the tile's epilogue operands first: their latency runs under the MFMAs
+        half4_t rs[NT][4], mk[NT][4], od[NT][4];
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int n = 32 * t + 8 * q + 4 * lh;
+                rs[t][q] = (res && pok) ? *reinterpret_cast<const half4_t*>(res + (long long)p * e.ldres + n) : hz;
+                mk[t][q] = (msk && pok) ? *reinterpret_cast<const half4_t*>(msk + (long long)p * e.ld0 + n) : hz;
+                od[t][q] = (e.accumulate && pok) ? *reinterpret_cast<const half4_t*>(y + (long long)p * g.ldy + n) : hz;
+            }
+        floatx16 acc[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+#pragma unroll
+        for (int j = 0; j < KC; ++j) {
+            const half8s_t x = xv[j];
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                const half8s_t w = *reinterpret_cast<const half8s_t*>(&Ws[(32 * t + lr) * KP + 16 * j + 8 * lh]);
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(w, x, acc[t], 0, 0, 0);
+            }
+            xv[j] = load_x(tile + nw, j);  // rolling prefetch of the wave's next tile
+        }
+        if (!pok) continue;
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int n = 32 * t + 8 * q + 4 * lh;
+                const float4 b4 = *reinterpret_cast<const float4*>(&bs[n]);
+                float o[4] = {acc[t][4 * q] + b4.x + (float)rs[t][q].x, acc[t][4 * q + 1] + b4.y + (float)rs[t][q].y,
+                              acc[t][4 * q + 2] + b4.z + (float)rs[t][q].z, acc[t][4 * q + 3] + b4.w + (float)rs[t][q].w};
+                if (e.act == HYRES_ACT_RELU) {
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) o[c] = fmaxf(o[c], 0.f);
+                } else if (e.act == HYRES_ACT_RELU_MASK) {
+                    o[0] = (float)mk[t][q].x > 0.f ? o[0] : 0.f;
+                    o[1] = (float)mk[t][q].y > 0.f ? o[1] : 0.f;
+                    o[2] = (float)mk[t][q].z > 0.f ? o[2] : 0.f;
+                    o[3] = (float)mk[t][q].w > 0.f ? o[3] : 0.f;
+                }
+                const half4_t h = {(_Float16)(o[0] + (float)od[t][q].x), (_Float16)(o[1] + (float)od[t][q].y),
+                                   (_Float16)(o[2] + (float)od[t][q].z), (_Float16)(o[3] + (float)od[t][q].w)};
+                *reinterpret_cast<half4_t*>(y + (long long)p * g.ldy + n) = h;
+            }
+    }
+}
+
 // split-K reduction + epilogue: one thread per (phase, m, n)
 template <bool H>
 __global__ void conv_splitk_reduce_kernel(const ConvArgs a) {
@@ -1975,7 +2076,7 @@ static void dense_taps(hyres_conv_geom* g, int KH, int KW, int sgn, int dil, int
 
 // keys: HYRES_TUNE_TILE, _SPLIT_BLOCKS, _SPLIT_MINCHUNKS, _WGRAD_BLOCKS, _WGRAD_MINCHUNKS, _WGRAD_NT,
 // _WGRAD_MAXSPLIT
-int g_tune[8] = {-1, -1, -1, -1, -1, -1, -1, 1};  // key 7: bf16x6 fp32 GEMMs by default
+int g_tune[9] = {-1, -1, -1, -1, -1, -1, -1, 1, 1};  // key 7: bf16x6 fp32 GEMMs; key 8: fp16 streaming 1x1
 
 }  // namespace hyres
 
@@ -2257,6 +2358,48 @@ static int stream_nt(const hyres_conv_geom* g, const hyres_epilogue* e) {
     return 0;
 }
 
+// conv1x1_stream_h_kernel eligibility: fp16 X and Y (io_f16 = 3), single-tap stride-1 1x1 with Ci and Co in
+// {64, 96, 128}, BIAS epilogue with ReLU / ReLU-mask / none (no pre-activation copy), grids >= 16384 output pixels,
+// 16-byte X rows and 8-byte epilogue operands. Returns NT (Co / 32) or 0.
+static int stream_h_nt(const hyres_conv_geom* g, const hyres_epilogue* e) {
+    if (g_tune[8] == 0 || (e->io_f16 & 3) != 3 || e->square_input || e->kind != HYRES_EPI_BIAS || e->out2) return 0;
+    if (e->act != HYRES_ACT_NONE && e->act != HYRES_ACT_RELU && e->act != HYRES_ACT_RELU_MASK) return 0;
+    if (g->nphase != 1 || g->ntaps != 1 || g->ish != 1 || g->isw != 1 || g->dh[0] != 0 || g->dw[0] != 0) return 0;
+    if (g->Hi != g->Hq || g->Wi != g->Wq || g->Ho != g->Hq || g->Wo != g->Wq) return 0;
+    if ((long long)g->B * g->Hq * g->Wq < 16384) return 0;
+    if (g->Ci != 64 && g->Ci != 96 && g->Ci != 128) return 0;
+    if (g->Co != 64 && g->Co != 96 && g->Co != 128) return 0;
+    if (g->ldx % 8 || g->ldy % 4 || (e->res && e->ldres % 4) || (e->act == HYRES_ACT_RELU_MASK && e->ld0 % 4)) return 0;
+    return g->Co / 32;
+}
+
+extern "C++" {
+template <int NT, int KC>
+static int launch_stream_h_one(const ConvArgs& a, hipStream_t st) {
+    static int occ = -1;
+    if (occ < 0) {
+        int n = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, conv1x1_stream_h_kernel<NT, KC>, 256, 0) != hipSuccess ||
+            n < 1)
+            n = 1;
+        occ = n;
+    }
+    const int blocks = std::max(1, std::min(ceil_div(ceil_div(a.M, 32), 4), 256 * occ));
+    hipLaunchKernelGGL((conv1x1_stream_h_kernel<NT, KC>), dim3(blocks), dim3(256), 0, st, a);
+    return HY_LAUNCH_CHECK("conv1x1_stream_h_kernel");
+}
+}  // extern "C++"
+
+static int launch_stream_h(const ConvArgs& a, int nt, int kc, hipStream_t st) {
+#define HY_STREAM_H(NT, KC) \
+    if (nt == NT && kc == KC) return launch_stream_h_one<NT, KC>(a, st);
+    HY_STREAM_H(2, 4) HY_STREAM_H(2, 6) HY_STREAM_H(2, 8)
+    HY_STREAM_H(3, 4) HY_STREAM_H(3, 6) HY_STREAM_H(3, 8)
+    HY_STREAM_H(4, 4) HY_STREAM_H(4, 6) HY_STREAM_H(4, 8)
+#undef HY_STREAM_H
+    return set_error(HYRES_E_ARG, "conv1x1_stream_h: no instantiation for NT=%d KC=%d", nt, kc);
+}
+
 static const int TILE_BM[5] = {128, 128, 128, 64, 64};
 static const int TILE_BN[5] = {128, 64, 32, 128, 64};
 
@@ -2316,7 +2459,7 @@ static long long plan_ws_bytes(const hyres_conv_geom* g, const ConvPlan& p) {
 }
 
 int hyres_conv_tuning(int key, int value, int* old) {
-    HY_REQUIRE(key >= 0 && key < 8, HYRES_E_ARG, "conv_tuning: key %d", key);
+    HY_REQUIRE(key >= 0 && key < 9, HYRES_E_ARG, "conv_tuning: key %d", key);
     if (old) *old = g_tune[key];
     g_tune[key] = value;
     return ok();
@@ -2438,6 +2581,17 @@ int hyres_conv_forward(const hyres_conv_geom* g, const float* x, const float* w2
             return launch_stream(a, nt, g->Ci / 8, 0, st);
         }
     }
+    {
+        const int nt = stream_h_nt(g, e);
+        const long long xb = (long long)a.M * g->ldx * 2;
+        if (nt && mode == 0 && xb < 0x7FFFFFF0LL && aligned16(x) && aligned16(w2) && ldw % 4 == 0 &&
+            (reinterpret_cast<uintptr_t>(y) & 7) == 0 && (reinterpret_cast<uintptr_t>(e->res) & 7) == 0 &&
+            (reinterpret_cast<uintptr_t>(e->aux0) & 7) == 0) {
+            a.x_bytes = (int)xb;
+            a.nsplit = 1;
+            return launch_stream_h(a, nt, g->Ci / 16, st);
+        }
+    }
     int rc;
     switch (ch.tile) {
         case 0: rc = launch_fwd<2, 2, 2, 2>(a, mode, st); break;
@@ -2480,6 +2634,11 @@ int hyres_conv_kernel_name(const hyres_conv_geom* g, const hyres_epilogue* e, in
         const int nt = stream_nt(g, e);
         if (nt && ch.mode == 0) {
             snprintf(buf, n, "conv1x1_stream_kernel<%d, %d%s>", nt, g->Ci / 8, e->f16_operands ? ", true" : "");
+            return 0;
+        }
+        const int nth = stream_h_nt(g, e);
+        if (nth && ch.mode == 0) {  // (the launch also checks pointer alignment; the label assumes it)
+            snprintf(buf, n, "conv1x1_stream_h_kernel<%d, %d>", nth, g->Ci / 16);
             return 0;
         }
     }

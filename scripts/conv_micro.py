@@ -26,20 +26,27 @@ def main():
     ap.add_argument("--f16", action="store_true", help="fp16 operands (autocast)")
     ap.add_argument("--tile", type=int, default=-1, help="force a conv tile (hyres_conv_tuning key 0)")
     ap.add_argument("--bf6", action="store_true", help="fp32 GEMM on the bf16 MFMA (hyres_conv_tuning key 7; default here: native)")
+    ap.add_argument("--io16", action="store_true", help="fp16 activations in HBM (X, Y, residual; implies --f16)")
+    ap.add_argument("--no-stream-h", action="store_true", help="fp16 1x1 on the tiled kernel (hyres_conv_tuning key 8 = 0)")
     a = ap.parse_args()
     from hyres_hip import _lib as L
     from hyres_hip import ops as O
     if a.tile >= 0:
         L.call("hyres_conv_tuning", 0, a.tile, None)
     L.call("hyres_conv_tuning", 7, 1 if a.bf6 else 0, None)  # the native fp32 MFMA unless --bf6
+    L.call("hyres_conv_tuning", 8, 0 if a.no_stream_h else 1, None)
+    if a.io16:
+        a.f16 = True
     dev = torch.device("cuda:0")
-    x = O.Node(torch.randn(a.B, a.H, a.H, a.Ci, device=dev), rg=False)
+    adt = torch.float16 if a.io16 else torch.float32
+    x = O.Node(torch.randn(a.B, a.H, a.H, a.Ci, device=dev).to(adt), rg=False)
     w = torch.randn(a.Co, a.Ci, a.K, a.K, device=dev) / (a.Ci * a.K * a.K) ** 0.5
     b = torch.randn(a.Co, device=dev)
     act = L.ACT_RELU if a.relu else L.ACT_NONE
-    res = O.Node(torch.randn(a.B, a.H // a.stride, a.H // a.stride, a.Co, device=dev), rg=False) if a.res else None
+    res = O.Node(torch.randn(a.B, a.H // a.stride, a.H // a.stride, a.Co, device=dev).to(adt), rg=False) if a.res else None
     ctx = torch.autocast("cuda", dtype=torch.float16) if a.f16 else torch.autocast("cuda", enabled=False)
-    with ctx:
+    import contextlib
+    with ctx, (O.f16_region() if a.io16 else contextlib.nullcontext()):
         for _ in range(3):
             y = O.conv2d(None, x, w, b, stride=a.stride, pad=a.K // 2, act=act, res=res)
         torch.cuda.synchronize()
@@ -53,8 +60,9 @@ def main():
     us = 1000 * e0.elapsed_time(e1) / a.iters
     Ho = y.H
     flops = 2.0 * a.B * Ho * Ho * a.K * a.K * a.Ci * a.Co
-    byts = 4.0 * (a.B * a.H * a.H * a.Ci + a.B * Ho * Ho * a.Co * (2 if a.res else 1) + a.K * a.K * a.Ci * a.Co)
-    print(f"conv B{a.B} {a.H}x{a.H}x{a.Ci} -> {Ho}x{Ho}x{a.Co} K{a.K} s{a.stride}{' +res' if a.res else ''}{' f16' if a.f16 else ''}{' bf16x6' if a.bf6 else ''}: {us:.1f} us, "
+    es = 2.0 if a.io16 else 4.0
+    byts = es * (a.B * a.H * a.H * a.Ci + a.B * Ho * Ho * a.Co * (2 if a.res else 1)) + 4.0 * a.K * a.K * a.Ci * a.Co
+    print(f"conv B{a.B} {a.H}x{a.H}x{a.Ci} -> {Ho}x{Ho}x{a.Co} K{a.K} s{a.stride}{' +res' if a.res else ''}{' f16' if a.f16 else ''}{' io16' if a.io16 else ''}{' tiled' if a.no_stream_h else ''}{' bf16x6' if a.bf6 else ''}: {us:.1f} us, "
           f"{flops / us / 1e6:.1f} TFLOP/s, {byts / us / 1e3:.0f} GB/s")
 
 

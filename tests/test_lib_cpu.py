@@ -193,7 +193,11 @@ def _native_routing(L, e, g3, g3b, _geom, conv_variant):
     e.io_f16 = 3
     assert conv_variant(g3, e, False) == "conv3x3_wres_f16_kernel<3>"
     assert conv_variant(g1b, e, False) == "conv_fwd_h_kernel<2, 1, 2, 2, 0, false, 3>"
-    assert conv_variant(g1, e, False) == "conv_fwd_h_kernel<1, 2, 2, 2, 0, false, 3>"  # not the fp32 stream kernel
+    # 1x1 K <= 128 with fp16 X and Y on >= 16384 pixels: the fp16 streaming kernel (not the fp32 one)
+    assert conv_variant(g1, e, False) == "conv1x1_stream_h_kernel<4, 4>"
+    e.square_input = 1  # (GDN's square prologue stays on the tiles)
+    assert conv_variant(g1, e, False) == "conv_fwd_h_kernel<1, 2, 2, 2, 1, false, 3>"
+    e.square_input = 0
     e.io_f16 = 2
     e.f16_operands = 0
     assert conv_variant(gs, e, False) == "conv_fwd_h_kernel<1, 1, 2, 2, 2, false, 2>"  # fp32 image in, fp16 out
