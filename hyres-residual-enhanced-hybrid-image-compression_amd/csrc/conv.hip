@@ -354,30 +354,25 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
             }
         }
     };
-    // B6: the loaded chunk is split into its bf16 pieces right after this chunk's MFMAs (split_chunk, before the
-    // barrier: VALU work that overlaps the MFMAs of waves still computing), so only LDS stores sit between barriers
-    bf16x4_t spa[B6 ? A_V : 1][3], spb[B6 ? B_V : 1][3];
-    auto split_chunk = [&]() {
-        if constexpr (B6) {
-#pragma unroll
-            for (int q = 0; q < A_V; ++q) bf6_split4(ra[q], spa[q][0], spa[q][1], spa[q][2]);
-#pragma unroll
-            for (int q = 0; q < B_V; ++q) bf6_split4(rb[q], spb[q][0], spb[q][1], spb[q][2]);
-        }
-    };
     auto store_chunk = [&]() {
         if constexpr (B6) {
 #pragma unroll
             for (int q = 0; q < A_V; ++q) {
+                bf16x4_t h, m, l;
+                bf6_split4(ra[q], h, m, l);
                 const int o = (tid / 8 + 32 * q) * PADH + 4 * c4;
-#pragma unroll
-                for (int p = 0; p < 3; ++p) *reinterpret_cast<bf16x4_t*>(&Pb[p * PLANE + o]) = spa[q][p];
+                *reinterpret_cast<bf16x4_t*>(&Pb[o]) = h;
+                *reinterpret_cast<bf16x4_t*>(&Pb[PLANE + o]) = m;
+                *reinterpret_cast<bf16x4_t*>(&Pb[2 * PLANE + o]) = l;
             }
 #pragma unroll
             for (int q = 0; q < B_V; ++q) {
+                bf16x4_t h, m, l;
+                bf6_split4(rb[q], h, m, l);
                 const int o = (BM + tid / 8 + 32 * q) * PADH + 4 * c4;
-#pragma unroll
-                for (int p = 0; p < 3; ++p) *reinterpret_cast<bf16x4_t*>(&Pb[p * PLANE + o]) = spb[q][p];
+                *reinterpret_cast<bf16x4_t*>(&Pb[o]) = h;
+                *reinterpret_cast<bf16x4_t*>(&Pb[PLANE + o]) = m;
+                *reinterpret_cast<bf16x4_t*>(&Pb[2 * PLANE + o]) = l;
             }
         } else if constexpr (F16) {
             typedef _Float16 half4 __attribute__((ext_vector_type(4)));
@@ -441,10 +436,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
         ld_t = kbeg / cpt;
         ld_c = (kbeg - ld_t * cpt) * KT;
     }
-    if (kbeg < kend) {
-        load_chunk(kbeg);
-        split_chunk();
-    }
+    if (kbeg < kend) load_chunk(kbeg);
     for (int kc = kbeg; kc < kend; ++kc) {
         __syncthreads();
         store_chunk();
@@ -472,7 +464,6 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
                     for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = bf6_mfma(af[tm], bf[tn], acc[tm][tn]);
             }
             if (a.prio) __builtin_amdgcn_s_setprio(0);
-            if (kc + 1 < kend) split_chunk();
             continue;
         }
         if constexpr (F16) {
@@ -712,11 +703,10 @@ void conv_fwd_kernel(const ConvArgs a) {
     conv_fwd_body<TM, TN, WAVES_M, WAVES_N, MODE, SPLITK, F16, 0>(a);
 }
 
-// fp32 operands, bf16x6 products (hyres_conv_tuning key 7): at least 2 waves per SIMD (the three-plane fragments do
-// not fit the 4-waves-per-SIMD bound of conv_fwd_kernel)
+// fp32 operands, bf16x6 products (hyres_conv_tuning key 7): the compiler's register allocation (the three-plane
+// fragments do not fit the 4-waves-per-SIMD bound of conv_fwd_kernel)
 template <int TM, int TN, int WAVES_M, int WAVES_N, int MODE, bool SPLITK>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
-void conv_fwd_b6_kernel(const ConvArgs a) {
+__global__ __launch_bounds__(256) void conv_fwd_b6_kernel(const ConvArgs a) {
     conv_fwd_body<TM, TN, WAVES_M, WAVES_N, MODE, SPLITK, false, 0, true>(a);
 }
 
