@@ -1566,10 +1566,10 @@ __global__ __launch_bounds__(256, 2) void conv1x1_stream_kernel(const ConvArgs a
 // HBM). Here, as conv1x1_stream_kernel, each WAVE streams its own 32-pixel tiles with no barrier after the one-time
 // weight staging (W -> fp16 in LDS, pitch K + 8 halves): the wave's X fragments come HBM -> registers in the MFMA
 // layout (lane (r, h): pixel p0 + r, channels 16j + 8h .. + 7, one 16-byte load per k-step) with a rolling prefetch
-// of the next tile, the product is formed transposed (C^T = W X^T) so each lane's accumulator holds 4 consecutive
-// channels of one pixel, and the epilogue operands of the tile (residual, ReLU mask, old y: fp16, 8 bytes per
-// channel quad) are requested BEFORE its MFMAs. Arithmetic: fp16 operands, fp32 accumulation, fp32 epilogue, one
-// rounding at the fp16 store — the tiled f16 kernel's, in the same K order.
+// of the next tile, and the product is formed transposed (C^T = W X^T) so each lane's accumulator holds 4 consecutive
+// channels of one pixel. Layers with a streamed epilogue operand (residual, ReLU mask, old y) stay on the tiles
+// (measured: stream_h_nt). Arithmetic: fp16 operands, fp32 accumulation, fp32 epilogue, one rounding at the fp16
+// store — the tiled f16 kernel's, in the same K order.
 typedef _Float16 half8s_t __attribute__((ext_vector_type(8)));
 
 template <int NT, int KC>
@@ -1591,8 +1591,6 @@ __global__ __launch_bounds__(256, 2) void conv1x1_stream_h_kernel(const ConvArgs
     __syncthreads();
 
     const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, a.x_bytes, 0x00020000);
-    const _Float16* const res = reinterpret_cast<const _Float16*>(e.res);
-    const _Float16* const msk = reinterpret_cast<const _Float16*>(e.act == HYRES_ACT_RELU_MASK ? e.aux0 : nullptr);
     _Float16* const y = reinterpret_cast<_Float16*>(a.y);
     const int ntile = (a.M + 31) / 32;
     const int gw = blockIdx.x * 4 + wave, nw = gridDim.x * 4;
@@ -1604,21 +1602,9 @@ __global__ __launch_bounds__(256, 2) void conv1x1_stream_h_kernel(const ConvArgs
     half8s_t xv[KC];
 #pragma unroll
     for (int j = 0; j < KC; ++j) xv[j] = load_x(gw, j);
-    const half4_t hz = {(_Float16)0.f, (_Float16)0.f, (_Float16)0.f, (_Float16)0.f};
     for (int tile = gw; tile < ntile; tile += nw) {
         const int p = tile * 32 + lr;
         const bool pok = p < a.M;
-        // the tile's epilogue operands first: their latency runs under the MFMAs
-        half4_t rs[NT][4], mk[NT][4], od[NT][4];
-#pragma unroll
-        for (int t = 0; t < NT; ++t)
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int n = 32 * t + 8 * q + 4 * lh;
-                rs[t][q] = (res && pok) ? *reinterpret_cast<const half4_t*>(res + (long long)p * e.ldres + n) : hz;
-                mk[t][q] = (msk && pok) ? *reinterpret_cast<const half4_t*>(msk + (long long)p * e.ld0 + n) : hz;
-                od[t][q] = (e.accumulate && pok) ? *reinterpret_cast<const half4_t*>(y + (long long)p * g.ldy + n) : hz;
-            }
         floatx16 acc[NT];
 #pragma unroll
         for (int t = 0; t < NT; ++t)
@@ -1641,19 +1627,13 @@ __global__ __launch_bounds__(256, 2) void conv1x1_stream_h_kernel(const ConvArgs
             for (int q = 0; q < 4; ++q) {
                 const int n = 32 * t + 8 * q + 4 * lh;
                 const float4 b4 = *reinterpret_cast<const float4*>(&bs[n]);
-                float o[4] = {acc[t][4 * q] + b4.x + (float)rs[t][q].x, acc[t][4 * q + 1] + b4.y + (float)rs[t][q].y,
-                              acc[t][4 * q + 2] + b4.z + (float)rs[t][q].z, acc[t][4 * q + 3] + b4.w + (float)rs[t][q].w};
+                float o[4] = {acc[t][4 * q] + b4.x, acc[t][4 * q + 1] + b4.y, acc[t][4 * q + 2] + b4.z,
+                              acc[t][4 * q + 3] + b4.w};
                 if (e.act == HYRES_ACT_RELU) {
 #pragma unroll
                     for (int c = 0; c < 4; ++c) o[c] = fmaxf(o[c], 0.f);
-                } else if (e.act == HYRES_ACT_RELU_MASK) {
-                    o[0] = (float)mk[t][q].x > 0.f ? o[0] : 0.f;
-                    o[1] = (float)mk[t][q].y > 0.f ? o[1] : 0.f;
-                    o[2] = (float)mk[t][q].z > 0.f ? o[2] : 0.f;
-                    o[3] = (float)mk[t][q].w > 0.f ? o[3] : 0.f;
                 }
-                const half4_t h = {(_Float16)(o[0] + (float)od[t][q].x), (_Float16)(o[1] + (float)od[t][q].y),
-                                   (_Float16)(o[2] + (float)od[t][q].z), (_Float16)(o[3] + (float)od[t][q].w)};
+                const half4_t h = {(_Float16)o[0], (_Float16)o[1], (_Float16)o[2], (_Float16)o[3]};
                 *reinterpret_cast<half4_t*>(y + (long long)p * g.ldy + n) = h;
             }
     }
@@ -2349,17 +2329,21 @@ static int stream_nt(const hyres_conv_geom* g, const hyres_epilogue* e) {
 }
 
 // conv1x1_stream_h_kernel eligibility: fp16 X and Y (io_f16 = 3), single-tap stride-1 1x1 with Ci and Co in
-// {64, 96, 128}, BIAS epilogue with ReLU / ReLU-mask / none (no pre-activation copy), grids >= 16384 output pixels,
-// 16-byte X rows and 8-byte epilogue operands. Returns NT (Co / 32) or 0.
+// {64, 96, 128}, BIAS epilogue with ReLU / none and no streamed operand, grids >= 16384 output pixels, 16-byte X rows.
+// Returns NT (Co / 32) or 0.
 static int stream_h_nt(const hyres_conv_geom* g, const hyres_epilogue* e) {
     if (g_tune[8] == 0 || (e->io_f16 & 3) != 3 || e->square_input || e->kind != HYRES_EPI_BIAS || e->out2) return 0;
-    if (e->act != HYRES_ACT_NONE && e->act != HYRES_ACT_RELU && e->act != HYRES_ACT_RELU_MASK) return 0;
+    // a streamed epilogue operand (residual, ReLU mask, old y) measured slower than the tiles (128^2 64->128 +res
+    // 45.2 vs 43.5 us, 64^2 16.5 vs 13.9 us; without one 24.8 vs 30.7 and 60.3 vs 80.8 us: profiles/r4e_h1x1.txt),
+    // as for the fp32 streaming kernel: those layers stay tiled
+    if (e->res || e->act == HYRES_ACT_RELU_MASK || e->accumulate) return 0;
+    if (e->act != HYRES_ACT_NONE && e->act != HYRES_ACT_RELU) return 0;
     if (g->nphase != 1 || g->ntaps != 1 || g->ish != 1 || g->isw != 1 || g->dh[0] != 0 || g->dw[0] != 0) return 0;
     if (g->Hi != g->Hq || g->Wi != g->Wq || g->Ho != g->Hq || g->Wo != g->Wq) return 0;
     if ((long long)g->B * g->Hq * g->Wq < 16384) return 0;
     if (g->Ci != 64 && g->Ci != 96 && g->Ci != 128) return 0;
     if (g->Co != 64 && g->Co != 96 && g->Co != 128) return 0;
-    if (g->ldx % 8 || g->ldy % 4 || (e->res && e->ldres % 4) || (e->act == HYRES_ACT_RELU_MASK && e->ld0 % 4)) return 0;
+    if (g->ldx % 8 || g->ldy % 4) return 0;
     return g->Co / 32;
 }
 
@@ -2575,8 +2559,7 @@ int hyres_conv_forward(const hyres_conv_geom* g, const float* x, const float* w2
         const int nt = stream_h_nt(g, e);
         const long long xb = (long long)a.M * g->ldx * 2;
         if (nt && mode == 0 && xb < 0x7FFFFFF0LL && aligned16(x) && aligned16(w2) && ldw % 4 == 0 &&
-            (reinterpret_cast<uintptr_t>(y) & 7) == 0 && (reinterpret_cast<uintptr_t>(e->res) & 7) == 0 &&
-            (reinterpret_cast<uintptr_t>(e->aux0) & 7) == 0) {
+            (reinterpret_cast<uintptr_t>(y) & 7) == 0) {
             a.x_bytes = (int)xb;
             a.nsplit = 1;
             return launch_stream_h(a, nt, g->Ci / 16, st);

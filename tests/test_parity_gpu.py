@@ -677,6 +677,8 @@ def _check_against_oracle(out, idx, x, jpeg, jpeg_bpp):
     assert nflip <= max(2, 1e-5 * ly_r.numel()), nflip
     dx = (xh.double() - ref["x_hat"].double()).abs() / ref["x_hat"].abs().max()
     nbad = int((dx > TOL).sum())
+    print(f"vs oracle: {nflip} y-likelihood flips, {nbad} x_hat values beyond {TOL} (max {float(dx.max()):.2e}, "
+          f"normwise {rel_err(xh.double(), ref['x_hat'].double()):.2e})")
     assert nbad <= nflip * 64 * 64 * 3, (nbad, nflip)  # each flip perturbs at most a 64x64-pixel window
     assert rel_err(out["likelihoods"]["z"].cpu()[idx], ref["likelihoods"]["z"]) < TOL
     bh = _bpp_per_image(out["likelihoods"]["y"].cpu()[idx], out["likelihoods"]["z"].cpu()[idx], H, W)
@@ -715,7 +717,7 @@ def test_c3_bs32_eval_gc_path_parity():
     _check_against_oracle(out, idx, x, jpeg, float(jpeg_bpp))
 
 
-def test_c5_kodak_size_eval_parity():
+def test_c5_kodak_size_eval_parity(fp32_gemm):
     """BASELINE config C5 shape: one 768x512 image (Kodak size, W != H; latents 96x64 / 24x16), eval,
     MultiScaleRefine on the HIP path, fp32 (the fp16-operand variant: test_c5_fp16_autocast_eval)."""
     net, _ = _hip_model()
