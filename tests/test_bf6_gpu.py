@@ -104,3 +104,73 @@ def test_bf6_implicit_gemm_conv_as_accurate_as_fp32(case):
     print(case, names, f"error vs fp64: native {e32:.2e}, bf16x6 {e6:.2e}")
     assert names[True].startswith("conv_fwd_b6_kernel") or names[True].startswith("conv3x3_wres_bf6")
     assert e6 <= 2.0 * e32 + 1e-9 and e6 < 1e-5
+
+
+@pytest.mark.parametrize("B,H,W,act", [(1, 256, 384, "relu"), (1, 512, 768, "prelu"), (2, 128, 192, "none")])
+def test_bf6_conv3x3_wide_images(B, H, W, act):
+    """The weight-resident 3x3 at the Kodak shapes (one 768x512 image: g_a / g_s at 384x256, MultiScaleRefine at full
+    size with its PReLU), against float64: bf16x6 no worse than twice the native kernel."""
+    from hyres_hip import _lib as L
+    from hyres_hip import ops as O
+    D = dev()
+    C = 64
+    x = _rand((B, C, H, W), 31).to(D)
+    w = _rand((C, C, 3, 3), 32, (C * 9) ** -0.5).to(D)
+    b = _rand((C,), 33, 0.1).to(D)
+    slope = torch.tensor([0.25], device=D)
+    ref = F.conv2d(x.double(), w.double(), b.double(), padding=1)
+    if act == "relu":
+        ref = F.relu(ref)
+    elif act == "prelu":
+        ref = torch.where(ref >= 0, ref, 0.25 * ref)
+    a = {"relu": L.ACT_RELU, "prelu": L.ACT_PRELU, "none": L.ACT_NONE}[act]
+    outs, names = {}, {}
+    for on in (False, True):
+        with _Bf6(on):
+            xn = O.to_nhwc(x)
+            g = O._geom("hyres_geom_conv2d", B, H, W, C, C, C, C, 3, 3, 1, 1, 1)
+            e = L.Epilogue()
+            e.kind, e.act, e.bias = L.EPI_BIAS, a, b.data_ptr()
+            names[on] = O.conv_variant(g, e, False)
+            yn = O.conv2d(None, xn, torch.nn.Parameter(w), b, pad=1, act=a, slope=slope if act == "prelu" else None)
+            outs[on] = O.to_nchw(yn).double()
+    torch.cuda.synchronize()
+    e32, e6 = rel_err(outs[False].cpu(), ref.cpu()), rel_err(outs[True].cpu(), ref.cpu())
+    print(B, H, W, act, names, f"error vs fp64: native {e32:.2e}, bf16x6 {e6:.2e}")
+    assert e6 <= 2.0 * e32 + 1e-9 and e6 < 1e-5
+
+
+def test_bf6_kodak_layers_match_native():
+    """Layer by layer (every conv output with a fused ReLU / PReLU, in forward order, ops.Trace.acts) of the eval
+    forward on one 768x512 image, bf16x6 against the native fp32 MFMA: g_a up to the latent y has no discontinuity
+    (the first round() is after it), so every layer there must agree to fp32 noise (1e-5 max-norm relative); the
+    first layers that differ more are printed with their shapes."""
+    from hyres_hip import ops as O
+    from hyres_hip.weights import synthetic_state_dict
+    from models import ResidualJPEGCompression
+    D = dev()
+    net = ResidualJPEGCompression(jpeg_quality=50)
+    torch.nn.Module.load_state_dict(net, synthetic_state_dict(net.state_dict()), strict=True)
+    net = net.to(D).eval()
+    g = torch.Generator().manual_seed(7)
+    base = F.interpolate(torch.rand(1, 3, 16, 24, generator=g), size=(512, 768), mode="bilinear", align_corners=False)
+    x = ((base * 0.8 + 0.2 * torch.rand(1, 3, 512, 768, generator=g)) * 255).floor() / 255
+    jpeg, jb = net.jpeg(x)
+    runs = {}
+    for on in (False, True):
+        O.Trace.nodes, O.Trace.acts = {}, []
+        with _Bf6(on), torch.no_grad():
+            net(x, jpeg=(jpeg, jb))
+        torch.cuda.synchronize()
+        runs[on] = ([(tuple(n.v.shape), O.to_nchw(n).double().cpu()) for _, n, _ in O.Trace.acts],
+                    {k: O.Trace.value(k).double().cpu() for k in ("y",) if k in O.Trace.nodes})
+        O.Trace.nodes, O.Trace.acts = None, None
+    a, b = runs[False][0], runs[True][0]
+    assert len(a) == len(b)
+    rows = [(i, a[i][0], rel_err(b[i][1], a[i][1])) for i in range(len(a))]
+    bad = [r for r in rows if r[2] > 1e-5]
+    print("layers beyond 1e-5 (index, NHWC shape, max-norm rel diff):", bad[:12])
+    if "y" in runs[False][1]:
+        ey = rel_err(runs[True][1]["y"], runs[False][1]["y"])
+        print(f"latent y: {ey:.2e}")
+        assert ey < 1e-5
