@@ -716,16 +716,16 @@ def main():
         if dist:
             tdist.destroy_process_group()
         return
-    # the fp32 convs' GEMM: bf16x6 (the default, hyres_conv_tuning key 7 = 1) or the native fp32 MFMA; with bf16x6
-    # the same step is re-captured and timed once more on the native fp32 MFMA (A/B on this box)
+    # the fp32 convs' GEMM (hyres_conv_tuning key 7: 1 bf16x6, 0 the native fp32 MFMA); the same step is re-captured
+    # and timed once more on the other GEMM (A/B on this box)
     cur = ctypes.c_int(0)
     L.call("hyres_conv_tuning", 7, 1, ctypes.byref(cur))  # read (and restore) the current mode
     L.call("hyres_conv_tuning", 7, cur.value, None)
     fp32_gemm = "bf16x6" if cur.value == 1 else "native"
-    native = None
-    if world == 1 and fp32_gemm == "bf16x6" and graphed is not None:
+    other = None
+    if world == 1 and graphed is not None:
         from hyres_hip.graphs import CapturedStep
-        L.call("hyres_conv_tuning", 7, 0, None)
+        L.call("hyres_conv_tuning", 7, 1 - cur.value, None)
         try:
             gn = CapturedStep(net, x, jpeg, jpeg_bpp, noisequant=False, criterion=crit, zero_grad=opt.zero_grad)
             for _ in range(args.warmup):
@@ -738,11 +738,12 @@ def main():
             ms_n = (time.time() - t0) * 1000 / args.steps
             gn.close()
             del gn
-            native = {"ms_per_step": round(ms_n, 3), "value": round(B * S * S / ms_n / 1e3, 4),
-                      "note": "the same graphed C2 step with the fp32 convs on the native fp32 MFMA "
-                              "(v_mfma_f32_32x32x2_f32) instead of bf16x6, timed after the headline on this box"}
+            name = "native" if cur.value == 1 else "bf16x6"
+            other = {"fp32_gemm": name, "ms_per_step": round(ms_n, 3), "value": round(B * S * S / ms_n / 1e3, 4),
+                     "note": f"the same graphed C2 step with the fp32 convs on the {name} GEMM, timed after the "
+                             "headline on this box"}
         finally:
-            L.call("hyres_conv_tuning", 7, 1, None)
+            L.call("hyres_conv_tuning", 7, cur.value, None)
     evals = None
     if world == 1 and not args.no_eval:
         evals = eval_legs(net, x, jpeg, jpeg_bpp, args)
@@ -782,7 +783,7 @@ def main():
                    "global_batch": B * world, "image": [S, S], "parallelism": f"dp{world}"},
         "fp32_gemm": fp32_gemm,
         "fp32_gemm_note": FP32_GEMM_NOTE[fp32_gemm],
-        "native_fp32_mfma": native,
+        "fp32_gemm_ab": other,
         "roofline": {"bound": "mfma", "kernel": f"{ks['kernel']} ({kernel_label(ks['kernel'])})",
                      "achieved": round(achieved, 3), "peak": kernel_peak(ks["kernel"]), "unit": "TFLOP/s",
                      "peak_note": peak_note(ks["kernel"]),
