@@ -140,6 +140,37 @@ def test_bf6_conv3x3_wide_images(B, H, W, act):
     assert e6 <= 2.0 * e32 + 1e-9 and e6 < 1e-5
 
 
+@pytest.mark.parametrize("case", [
+    # B, Ci (read), Ci_w (weight row), Co, H, W, K, ldy (output pixel stride)
+    (1, 192, 192, 384, 64, 96, 3, 768),   # h_s's last conv into the [latent_params | context] buffer (split-K)
+    (1, 384, 768, 640, 64, 96, 1, 640),   # param_aggregation.0, anchor pass: the first 384 of 768 input channels
+    (1, 768, 768, 640, 64, 96, 1, 640),
+    (1, 640, 640, 512, 64, 96, 1, 512),
+])
+def test_bf6_latent_layers_kodak(case):
+    """The latent-resolution layers of one 768x512 image (64 x 96 latents: small grids, split-K, a strided output, a
+    partial-channel read of the weight rows), bf16x6 against the native kernel and float64."""
+    from hyres_hip import ops as O
+    B, Ci, Ciw, Co, H, W, K, ldy = case
+    D = dev()
+    x = _rand((B, Ci, H, W), 41).to(D)
+    w = _rand((Co, Ciw, K, K), 42, (Ci * K * K) ** -0.5).to(D)
+    b = _rand((Co,), 43, 0.1).to(D)
+    ref = F.conv2d(x.double(), w[:, :Ci].double(), b.double(), padding=K // 2)
+    outs = {}
+    for on in (False, True):
+        with _Bf6(on):
+            xn = O.to_nhwc(x)
+            big = O.Node.new(B, H, W, ldy, D)
+            yo = big.slice(0, Co)
+            O.conv2d(None, xn, torch.nn.Parameter(w), b, pad=K // 2, out=yo)
+            outs[on] = big.v[..., :Co].permute(0, 3, 1, 2).double()
+    torch.cuda.synchronize()
+    e32, e6 = rel_err(outs[False].cpu(), ref.cpu()), rel_err(outs[True].cpu(), ref.cpu())
+    print(case, f"error vs fp64: native {e32:.2e}, bf16x6 {e6:.2e}")
+    assert e6 <= 2.0 * e32 + 1e-9 and e6 < 1e-5
+
+
 def test_bf6_kodak_layers_match_native():
     """Layer by layer (every conv output with a fused ReLU / PReLU, in forward order, ops.Trace.acts) of the eval
     forward on one 768x512 image, bf16x6 against the native fp32 MFMA: g_a up to the latent y has no discontinuity
@@ -163,14 +194,14 @@ def test_bf6_kodak_layers_match_native():
             net(x, jpeg=(jpeg, jb))
         torch.cuda.synchronize()
         runs[on] = ([(tuple(n.v.shape), O.to_nchw(n).double().cpu()) for _, n, _ in O.Trace.acts],
-                    {k: O.Trace.value(k).double().cpu() for k in ("y",) if k in O.Trace.nodes})
+                    {k: O.Trace.value(k).double().cpu() for k in O.Trace.nodes})
         O.Trace.nodes, O.Trace.acts = None, None
     a, b = runs[False][0], runs[True][0]
     assert len(a) == len(b)
     rows = [(i, a[i][0], rel_err(b[i][1], a[i][1])) for i in range(len(a))]
     bad = [r for r in rows if r[2] > 1e-5]
     print("layers beyond 1e-5 (index, NHWC shape, max-norm rel diff):", bad[:12])
-    if "y" in runs[False][1]:
-        ey = rel_err(runs[True][1]["y"], runs[False][1]["y"])
-        print(f"latent y: {ey:.2e}")
-        assert ey < 1e-5
+    for k in runs[False][1]:
+        print(f"stage {k}: {tuple(runs[False][1][k].shape)} bf16x6 vs native {rel_err(runs[True][1][k], runs[False][1][k]):.2e}")
+    ey = rel_err(runs[True][1]["y"], runs[False][1]["y"])
+    assert ey < 1e-5
