@@ -171,6 +171,32 @@ def test_bf6_latent_layers_kodak(case):
     assert e6 <= 2.0 * e32 + 1e-9 and e6 < 1e-5
 
 
+@pytest.mark.parametrize("garbage", [0.0, 1e3])
+def test_bf6_partial_channel_read_of_strided_buffer(garbage):
+    """param_aggregation.0 in the anchor pass exactly as the model runs it: the input is the first 2M = 384 channels of
+    the [latent | ctx] NHWC buffer (pixel stride 768) whose ctx half is not yet written (filled here with 0 or with
+    large values), the weight rows 768 wide; bf16x6 and native against float64 on the live half only."""
+    from hyres_hip import ops as O
+    D = dev()
+    B, H, W, M2, Co = 1, 64, 96, 384, 640
+    lat = _rand((B, M2, H, W), 51).to(D)
+    w = _rand((Co, 2 * M2, 1, 1), 52, M2 ** -0.5).to(D)
+    b = _rand((Co,), 53, 0.1).to(D)
+    ref = F.conv2d(lat.double(), w[:, :M2].double(), b.double())
+    outs = {}
+    for on in (False, True):
+        with _Bf6(on):
+            lc = O.Node.new(B, H, W, 2 * M2, D)
+            lc.v.fill_(garbage)
+            lc.v[..., :M2] = lat.permute(0, 2, 3, 1)
+            yn = O.conv2d(None, lc.slice(0, M2), torch.nn.Parameter(w), b)
+            outs[on] = O.to_nchw(yn).double()
+    torch.cuda.synchronize()
+    e32, e6 = rel_err(outs[False].cpu(), ref.cpu()), rel_err(outs[True].cpu(), ref.cpu())
+    print(f"garbage {garbage}: error vs fp64: native {e32:.2e}, bf16x6 {e6:.2e}")
+    assert e32 < 1e-5 and e6 < 1e-5
+
+
 def test_bf6_kodak_layers_match_native():
     """Layer by layer (every conv output with a fused ReLU / PReLU, in forward order, ops.Trace.acts) of the eval
     forward on one 768x512 image, bf16x6 against the native fp32 MFMA: g_a up to the latent y has no discontinuity
