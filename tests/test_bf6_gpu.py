@@ -229,5 +229,14 @@ def test_bf6_kodak_layers_match_native():
     print("layers beyond 1e-5 (index, NHWC shape, max-norm rel diff):", bad[:12])
     for k in runs[False][1]:
         print(f"stage {k}: {tuple(runs[False][1][k].shape)} bf16x6 vs native {rel_err(runs[True][1][k], runs[False][1][k]):.2e}")
+    # the first diverging layer recomputed in float64 from its traced input, for both runs
+    pa = net.residual_model.param_aggregation
+    w0, b0 = pa[0].weight.detach().double().cpu(), pa[0].bias.detach().double().cpu()
+    for on in (False, True):
+        lat = runs[on][1]["latent_params"]
+        want = F.relu(F.conv2d(lat, w0[:, :lat.shape[1]], b0))
+        got = [t for shp, t in runs[on][0] if shp[-1] == 640]
+        print(f"bf16x6={on}: param_aggregation.0 (anchor) vs float64 from the traced latent: "
+              f"{rel_err(got[0], want):.2e}; non-anchor count {len(got)}")
     ey = rel_err(runs[True][1]["y"], runs[False][1]["y"])
     assert ey < 1e-5
