@@ -37,6 +37,7 @@ for ph in "$@"; do
            cat gpurun_out/mem_defer1.log gpurun_out/mem_defer0.log | grep WGRAD_DEFER > gpurun_out/${tag}_mem_probe.txt ;;
     dist)  bash scripts/dist_rehearsal.sh; echo "dist rehearsal exit $?" ;;
     sq)    bash scripts/pmc_sq.sh $tag || exit $? ;;
+    ab)    bash scripts/ab_alt.sh $tag || exit $? ;;
     h1x1)  scripts/gpu_run.sh "h1x1:300:for s in '--H 128 --Ci 64 --Co 128 --K 1 --res --relu' '--H 128 --Ci 128 --Co 64 --K 1 --relu' '--H 64 --Ci 64 --Co 128 --K 1 --res --relu' '--H 256 --Ci 64 --Co 64 --K 1 --relu'; do for m in '' --no-stream-h; do python3 scripts/conv_micro.py --io16 \$s \$m; done; done" || exit $?
            grep "us," gpurun_out/h1x1.log > gpurun_out/${tag}_h1x1.txt ;;
     ru)    scripts/gpu_run.sh "ru_micro:200:python3 scripts/ru_micro.py && python3 scripts/ru_micro.py --H 64 --W 64" || exit $?
