@@ -240,3 +240,35 @@ def test_bf6_kodak_layers_match_native():
               f"{rel_err(got[0], want):.2e}; non-anchor count {len(got)}")
     ey = rel_err(runs[True][1]["y"], runs[False][1]["y"])
     assert ey < 1e-5
+
+
+def test_bf6_refine_layers_match_native():
+    """MultiScaleRefine alone (bs 2, 256x256, eval) on one fixed input, bf16x6 against the native fp32 MFMA, layer by
+    layer (every conv output with a fused PReLU, in forward order) and the traced stages: the path has no
+    discontinuity, so everything must agree to fp32 noise; the first layers that differ more are printed."""
+    from hyres_hip import ops as O
+    from hyres_hip.weights import synthetic_state_dict
+    from models import ResidualJPEGCompression
+    D = dev()
+    net = ResidualJPEGCompression(jpeg_quality=50)
+    torch.nn.Module.load_state_dict(net, synthetic_state_dict(net.state_dict()), strict=True)
+    net = net.to(D).eval()
+    x = torch.rand((2, 3, 256, 256), generator=torch.Generator().manual_seed(3)).to(D)
+    runs = {}
+    for on in (False, True):
+        O.Trace.nodes, O.Trace.acts = {}, []
+        with _Bf6(on), torch.no_grad():
+            out = net.refine.hip(None, O.to_nhwc(x))
+            res = O.to_nchw(out).double().cpu()
+        torch.cuda.synchronize()
+        runs[on] = ([(tuple(n.v.shape), O.to_nchw(n).double().cpu()) for _, n, _ in O.Trace.acts],
+                    {k: O.Trace.value(k).double().cpu() for k in O.Trace.nodes}, res)
+        O.Trace.nodes, O.Trace.acts = None, None
+    a, b = runs[False][0], runs[True][0]
+    rows = [(i, a[i][0], rel_err(b[i][1], a[i][1])) for i in range(len(a))]
+    print("refine layers (index, NHWC shape, bf16x6 vs native):", [(i, s, f"{e:.1e}") for i, s, e in rows])
+    for k in runs[False][1]:
+        print(f"stage {k}: bf16x6 vs native {rel_err(runs[True][1][k], runs[False][1][k]):.2e}")
+    e = rel_err(runs[True][2], runs[False][2])
+    print(f"refine output: {e:.2e}")
+    assert max(r[2] for r in rows) < 1e-5 and e < 1e-5
