@@ -271,4 +271,19 @@ def test_bf6_refine_layers_match_native():
         print(f"stage {k}: bf16x6 vs native {rel_err(runs[True][1][k], runs[False][1][k]):.2e}")
     e = rel_err(runs[True][2], runs[False][2])
     print(f"refine output: {e:.2e}")
+    # the same with the three scales serialised on one stream, and bf16x6 twice (run-to-run)
+    extra = {}
+    for tag, on, branches in (("bf6_serial", True, False), ("native_serial", False, False), ("bf6_again", True, True)):
+        O.BranchStreams.enabled = branches
+        try:
+            with _Bf6(on), torch.no_grad():
+                extra[tag] = O.to_nchw(net.refine.hip(None, O.to_nhwc(x))).double().cpu()
+            torch.cuda.synchronize()
+        finally:
+            O.BranchStreams.enabled = True
+    print("bf6 serial vs native serial %.2e, bf6 serial vs native branches %.2e, bf6 branches run-to-run %.2e, "
+          "native serial vs native branches %.2e" % (rel_err(extra["bf6_serial"], extra["native_serial"]),
+                                                     rel_err(extra["bf6_serial"], runs[False][2]),
+                                                     rel_err(extra["bf6_again"], runs[True][2]),
+                                                     rel_err(extra["native_serial"], runs[False][2])))
     assert max(r[2] for r in rows) < 1e-5 and e < 1e-5
