@@ -1255,7 +1255,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3_wres_f32_kernel(const ConvArgs
 }
 
 // ------------------------------------------------------------------------------------------------
-// fp32-accurate weight-resident 3x3 conv on the bf16 MFMA ("bf16x6", hyres_conv_tuning key 7 = 1, the default).
+// fp32-accurate weight-resident 3x3 conv on the bf16 MFMA ("bf16x6", hyres_conv_tuning key 7 = 1; opt-in).
 // conv3x3_wres_f32_kernel above runs at ~0.7 of the fp32 MFMA peak, and that peak (157 TF/s) is 1/16 of the bf16
 // MFMA's. Here every fp32 operand is split into three bf16 pieces x = x0 + x1 + x2 (x0 = bf16(x), x1 = bf16(x - x0),
 // x2 = bf16(x - x0 - x1): 24 significant bits, |x - x0 - x1 - x2| <= 2^-25 |x|) and each product is formed from the
@@ -2046,7 +2046,7 @@ static void dense_taps(hyres_conv_geom* g, int KH, int KW, int sgn, int dil, int
 
 // keys: HYRES_TUNE_TILE, _SPLIT_BLOCKS, _SPLIT_MINCHUNKS, _WGRAD_BLOCKS, _WGRAD_MINCHUNKS, _WGRAD_NT,
 // _WGRAD_MAXSPLIT
-int g_tune[9] = {-1, -1, -1, -1, -1, -1, -1, 1, 1};  // key 7: bf16x6 fp32 GEMMs; key 8: fp16 streaming 1x1
+int g_tune[9] = {-1, -1, -1, -1, -1, -1, -1, 0, 1};  // key 7: fp32 GEMMs native (1: bf16x6); key 8: fp16 streaming 1x1
 
 }  // namespace hyres
 

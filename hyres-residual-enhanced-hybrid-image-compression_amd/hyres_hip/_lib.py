@@ -206,13 +206,13 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         fn.restype = res
         fn.argtypes = args
     _lib = lib
-    # HYRES_FP32_GEMM=native: the fp32 convs on the native fp32 MFMA instead of the bf16x6 split (the library default;
-    # hyres_conv_tuning key 7)
-    mode = os.environ.get("HYRES_FP32_GEMM", "bf16x6")
+    # HYRES_FP32_GEMM=bf16x6: the fp32 convs on the bf16 MFMA through the three-way split instead of the native fp32
+    # MFMA (the library default; hyres_conv_tuning key 7)
+    mode = os.environ.get("HYRES_FP32_GEMM", "native")
     if mode not in ("bf16x6", "native"):
         raise ValueError(f"HYRES_FP32_GEMM={mode!r}: 'bf16x6' or 'native'")
-    if mode == "native":
-        lib.hyres_conv_tuning(7, 0, None)
+    if mode == "bf16x6":
+        lib.hyres_conv_tuning(7, 1, None)
     return lib
 
 
