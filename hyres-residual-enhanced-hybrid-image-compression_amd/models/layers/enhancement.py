@@ -112,6 +112,7 @@ class MultiScaleRefine(HipModule):
 
         def scale2(tape, f):  # 1/2: F.interpolate(scale_factor=0.5) -> source scale 2.0; back with size=
             f2 = R.bilinear(tape, f, H // 2, W // 2, 2.0, 2.0)
+            O.Trace.add("refine_f2_in", f2)
             f2 = self.scale2.hip(tape, f2)
             R.bilinear(tape, f2, H, W, (H // 2) / H, (W // 2) / W, out=multi.slice(mid, 2 * mid))
             return f2

@@ -271,6 +271,23 @@ def test_bf6_refine_layers_match_native():
         print(f"stage {k}: bf16x6 vs native {rel_err(runs[True][1][k], runs[False][1][k]):.2e}")
     e = rel_err(runs[True][2], runs[False][2])
     print(f"refine output: {e:.2e}")
+    from hyres_hip import _lib as L
+    g2 = O._geom("hyres_geom_conv2d", 2, 128, 128, 64, 64, 64, 64, 3, 3, 1, 1, 1)
+    e2 = L.Epilogue()
+    e2.kind, e2.act = L.EPI_BIAS, L.ACT_PRELU
+    with _Bf6(True):
+        print("1/2-scale first conv kernel under bf16x6:", O.conv_variant(g2, e2, O.conv_split(g2, e2) > 1))
+    # bf16x6 with branches three more times: the 1/2-scale block's input (the bilinear output) and first conv
+    reps = []
+    for _ in range(3):
+        O.Trace.nodes, O.Trace.acts = {}, []
+        with _Bf6(True), torch.no_grad():
+            net.refine.hip(None, O.to_nhwc(x))
+        torch.cuda.synchronize()
+        reps.append((O.Trace.value("refine_f2_in").double().cpu(), O.to_nchw(O.Trace.acts[3][1]).double().cpu()))
+        O.Trace.nodes, O.Trace.acts = None, None
+    print("bf6 branches, reps vs first: f2 input %s, layer 3 %s" % (
+        ["%.1e" % rel_err(r[0], reps[0][0]) for r in reps[1:]], ["%.1e" % rel_err(r[1], reps[0][1]) for r in reps[1:]]))
     # the same with the three scales serialised on one stream, and bf16x6 twice (run-to-run)
     extra = {}
     for tag, on, branches in (("bf6_serial", True, False), ("native_serial", False, False), ("bf6_again", True, True)):
