@@ -308,3 +308,78 @@ def test_bf6_refine_layers_match_native():
     # the 1/2-scale block's first conv, 4e-2 apart; the reason this GEMM is opt-in) — printed above, not asserted
     assert rel_err(extra["bf6_serial"], extra["native_serial"]) < 1e-5
     assert rel_err(extra["native_serial"], runs[False][2]) < 1e-6
+
+
+@pytest.mark.parametrize("case", [
+    # (B, H, W, Ci, Co, k, out channels of the host buffer, channel offset) — the MultiScaleRefine / latent convs
+    (2, 256, 256, 64, 64, 3, 192, 0), (2, 256, 256, 64, 64, 3, 64, 0), (2, 128, 128, 64, 64, 3, 192, 64),
+    (2, 64, 64, 64, 64, 3, 192, 128), (2, 128, 128, 64, 64, 3, 64, 0), (1, 64, 96, 384, 640, 1, 640, 0),
+    (1, 64, 96, 640, 512, 1, 512, 0)])
+def test_bf6_writes_stay_inside_the_output(case):
+    """Every bf16x6 conv writes its output view and nothing else: the view sits inside a sentinel-filled buffer (one
+    image before and after it, the other channels of a wider pixel stride), which must be untouched after the conv."""
+    from hyres_hip import ops as O
+    D = dev()
+    B, H, W, Ci, Co, k, Cb, c0 = case
+    x = O.to_nhwc(_rand((B, Ci, H, W), 61).to(D))
+    w = torch.nn.Parameter(_rand((Co, Ci, k, k), 62, (Ci * k * k) ** -0.5).to(D))
+    b = _rand((Co,), 63, 0.1).to(D)
+    slope = torch.full((1,), 0.25, device=D)
+    for on in (False, True):
+        big = torch.full((B + 2, H, W, Cb), 12345.0, device=D)
+        out = O.Node(big[1:B + 1, ..., c0:c0 + Co])
+        with _Bf6(on), torch.no_grad():
+            O.conv2d(None, x, w, b, pad=k // 2, act=L_ACT_PRELU(), slope=slope, out=out)
+        torch.cuda.synchronize()
+        keep = torch.ones_like(big, dtype=torch.bool)
+        keep[1:B + 1, ..., c0:c0 + Co] = False
+        bad = int((big[keep] != 12345.0).sum())
+        print(case, "bf16x6" if on else "native", "writes outside the view:", bad)
+        assert bad == 0
+
+
+def L_ACT_PRELU():
+    from hyres_hip import _lib as L
+    return L.ACT_PRELU
+
+
+def test_bf6_refine_branch_determinism():
+    """MultiScaleRefine (bs 2, 256x256, eval) with its branch streams, bf16x6 switched on for a subset of the three
+    scales (the others native), three runs each: the run-to-run spread of the 1/2-scale input and of the output."""
+    from hyres_hip import ops as O
+    from hyres_hip.weights import synthetic_state_dict
+    from models import ResidualJPEGCompression
+    D = dev()
+    net = ResidualJPEGCompression(jpeg_quality=50)
+    torch.nn.Module.load_state_dict(net, synthetic_state_dict(net.state_dict()), strict=True)
+    net = net.to(D).eval()
+    x = torch.rand((2, 3, 256, 256), generator=torch.Generator().manual_seed(3)).to(D)
+    rf = net.refine
+    seqs = [rf.scale1, rf.scale2, rf.scale3]
+    origs = [s.hip for s in seqs]
+
+    def wrap(fn, on):
+        def hip(*a, **kw):
+            with _Bf6(on):
+                return fn(*a, **kw)
+        return hip
+    rows = []
+    try:
+        for subset in ((), (0,), (1,), (2,), (1, 2), (0, 1, 2)):
+            for i, s in enumerate(seqs):
+                s.hip = wrap(origs[i], i in subset)
+            reps = []
+            for _ in range(3):
+                O.Trace.nodes, O.Trace.acts = {}, []
+                with torch.no_grad():
+                    out = rf.hip(None, O.to_nhwc(x))
+                torch.cuda.synchronize()
+                reps.append((O.Trace.value("refine_f2_in").double().cpu(), O.to_nchw(out).double().cpu()))
+                O.Trace.nodes, O.Trace.acts = None, None
+            rows.append((subset, max(rel_err(r[0], reps[0][0]) for r in reps[1:]),
+                         max(rel_err(r[1], reps[0][1]) for r in reps[1:])))
+    finally:
+        for i, s in enumerate(seqs):
+            s.hip = origs[i]
+    for subset, ef, eo in rows:
+        print(f"bf16x6 on scales {[i + 1 for i in subset]}: run-to-run f2 input {ef:.1e}, output {eo:.1e}")
