@@ -383,3 +383,37 @@ def test_bf6_refine_branch_determinism():
             s.hip = origs[i]
     for subset, ef, eo in rows:
         print(f"bf16x6 on scales {[i + 1 for i in subset]}: run-to-run f2 input {ef:.1e}, output {eo:.1e}")
+
+
+@pytest.mark.parametrize("dil", [1, 2])
+def test_bf6_conv_concurrent_with_bilinear(dil):
+    """Isolates the MultiScaleRefine run-to-run spread: the 1/2-scale bilinear of the SE output on a side stream while
+    the full-scale 3x3 conv (dilation 1: conv3x3_wres_*; 2: the implicit GEMM) reads the same tensor on the main
+    stream; the bilinear output against the same bilinear run alone."""
+    from hyres_hip import ops as O
+    from hyres_hip import refine_ops as R
+    D = dev()
+    B, H, W, C = 2, 256, 256, 64
+    feat = O.to_nhwc(_rand((B, C, H, W), 71).to(D))
+    w = torch.nn.Parameter(_rand((C, C, 3, 3), 72, (C * 9) ** -0.5).to(D))
+    b = _rand((C,), 73, 0.1).to(D)
+    slope = torch.full((1,), 0.25, device=D)
+    with torch.no_grad():
+        ref = R.bilinear(None, feat, H // 2, W // 2, 2.0, 2.0).v.clone()
+    torch.cuda.synchronize()
+    side = torch.cuda.Stream(device=D)
+    for on in (False, True):
+        worst = 0.0
+        for _ in range(5):
+            multi = O.Node.new(B, H, W, 3 * C, D)
+            with _Bf6(on), torch.no_grad():
+                fork = torch.cuda.Event()
+                fork.record()
+                O.conv2d(None, feat, w, b, pad=dil, dil=dil, act=L_ACT_PRELU(), slope=slope, out=multi.slice(0, C))
+                side.wait_event(fork)
+                with torch.cuda.stream(side):
+                    f2 = R.bilinear(None, feat, H // 2, W // 2, 2.0, 2.0)
+                torch.cuda.current_stream().wait_stream(side)
+            torch.cuda.synchronize()
+            worst = max(worst, (f2.v - ref).abs().max().item())
+        print(f"dil {dil} {'bf16x6' if on else 'native'}: bilinear beside the conv, max |diff| vs alone {worst:.2e}")
