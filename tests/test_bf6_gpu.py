@@ -417,3 +417,49 @@ def test_bf6_conv_concurrent_with_bilinear(dil):
             torch.cuda.synchronize()
             worst = max(worst, (f2.v - ref).abs().max().item())
         print(f"dil {dil} {'bf16x6' if on else 'native'}: bilinear beside the conv, max |diff| vs alone {worst:.2e}")
+
+
+@pytest.mark.parametrize("mode", ["native", "bf16x6", "f16"])
+def test_conv_beside_side_stream_kernels(mode):
+    """Which side-stream results change while a full-scale 3x3 conv (conv3x3_wres_*) runs on the main stream: a
+    bilinear of the conv's own input, a bilinear of an unrelated tensor, a plain copy of an unrelated tensor; and the
+    conv's own output. Each against the same kernel run alone."""
+    from hyres_hip import ops as O
+    from hyres_hip import refine_ops as R
+    D = dev()
+    B, H, W, C = 2, 256, 256, 64
+    half = mode == "f16"
+    dt = torch.float16 if half else torch.float32
+    feat = O.Node(O.to_nhwc(_rand((B, C, H, W), 71).to(D)).v.to(dt).contiguous())
+    other = O.Node(O.to_nhwc(_rand((B, C, H, W), 74).to(D)).v.to(dt).contiguous())
+    w = torch.nn.Parameter(_rand((C, C, 3, 3), 72, (C * 9) ** -0.5).to(D))
+    b = _rand((C,), 73, 0.1).to(D)
+    slope = torch.full((1,), 0.25, device=D)
+    side = torch.cuda.Stream(device=D)
+
+    def conv():
+        with torch.autocast("cuda", dtype=torch.float16, enabled=half):
+            return O.conv2d(None, feat, w, b, pad=1, act=L_ACT_PRELU(), slope=slope)
+
+    def sides():
+        return (R.bilinear(None, feat, H // 2, W // 2, 2.0, 2.0).v, R.bilinear(None, other, H // 2, W // 2, 2.0, 2.0).v,
+                other.v.clone())
+    with _Bf6(mode == "bf16x6"), torch.no_grad():
+        y0 = conv().v.clone()
+        ref = [t.clone() for t in sides()]
+        torch.cuda.synchronize()
+        worst = [0.0] * 4
+        for _ in range(5):
+            fork = torch.cuda.Event()
+            fork.record()
+            y = conv()
+            side.wait_event(fork)
+            with torch.cuda.stream(side):
+                got = sides()
+            torch.cuda.current_stream().wait_stream(side)
+            torch.cuda.synchronize()
+            for i, (g_, r_) in enumerate(zip(got, ref)):
+                worst[i] = max(worst[i], (g_.float() - r_.float()).abs().max().item())
+            worst[3] = max(worst[3], (y.v.float() - y0.float()).abs().max().item())
+    print(f"{mode}: max |diff| vs alone — bilinear(conv input) {worst[0]:.2e}, bilinear(other) {worst[1]:.2e}, "
+          f"copy(other) {worst[2]:.2e}, conv output {worst[3]:.2e}")
