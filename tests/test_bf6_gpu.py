@@ -463,3 +463,55 @@ def test_conv_beside_side_stream_kernels(mode):
             worst[3] = max(worst[3], (y.v.float() - y0.float()).abs().max().item())
     print(f"{mode}: max |diff| vs alone — bilinear(conv input) {worst[0]:.2e}, bilinear(other) {worst[1]:.2e}, "
           f"copy(other) {worst[2]:.2e}, conv output {worst[3]:.2e}")
+
+
+def test_bf6_kernels_beside_a_bilinear():
+    """Each bf16x6 kernel family (and its native counterpart) on the main stream while a side stream resamples an
+    unrelated tensor three times: the largest change of the resampled values against the same resampling alone."""
+    from hyres_hip import ops as O
+    from hyres_hip import refine_ops as R
+    D = dev()
+    other = O.to_nhwc(_rand((2, 64, 256, 256), 74).to(D))
+    side = torch.cuda.Stream(device=D)
+    slope = torch.full((1,), 0.25, device=D)
+    with torch.no_grad():
+        ref = R.bilinear(None, other, 128, 128, 2.0, 2.0).v.clone()
+    torch.cuda.synchronize()
+
+    def fwd(B, H, W, Ci, Co, k, dil=1, bwd=False):
+        x = O.to_nhwc(_rand((B, Ci, H, W), 75).to(D), rg=bwd)
+        w = torch.nn.Parameter(_rand((Co, Ci, k, k), 76, (Ci * k * k) ** -0.5).to(D))
+        b = torch.nn.Parameter(_rand((Co,), 77, 0.1).to(D))
+        gy = O.nchw_grad_to_nhwc(_rand((B, Co, H, W), 78).to(D)) if bwd else None
+
+        def run():
+            tape = O.Tape() if bwd else None
+            y = O.conv2d(tape, x, w, b, pad=dil * (k // 2), dil=dil, act=L_ACT_PRELU(), slope=slope)
+            if bwd:
+                y.set_grad(gy)
+                tape.backward()
+        return run
+    cases = {"3x3 2x256² (weight-resident)": fwd(2, 256, 256, 64, 64, 3),
+             "3x3 dil2 2x256² (implicit GEMM)": fwd(2, 256, 256, 64, 64, 3, 2),
+             "3x3 2x128² (implicit GEMM)": fwd(2, 128, 128, 64, 64, 3),
+             "1x1 64x96 384->640": fwd(1, 64, 96, 384, 640, 1),
+             "3x3 2x128² fwd+bwd (dgrad, halo wgrad)": fwd(2, 128, 128, 64, 64, 3, bwd=True),
+             "1x1 2x128² 128->64 fwd+bwd (1x1 wgrad)": fwd(2, 128, 128, 128, 64, 1, bwd=True)}
+    for name, run in cases.items():
+        for on in (False, True):
+            worst = 0.0
+            with _Bf6(on):
+                run()
+                torch.cuda.synchronize()
+                for _ in range(4):
+                    fork = torch.cuda.Event()
+                    fork.record()
+                    with torch.no_grad() if "bwd" not in name else torch.enable_grad():
+                        run()
+                    side.wait_event(fork)
+                    with torch.cuda.stream(side), torch.no_grad():
+                        got = [R.bilinear(None, other, 128, 128, 2.0, 2.0).v for _ in range(3)]
+                    torch.cuda.current_stream().wait_stream(side)
+                    torch.cuda.synchronize()
+                    worst = max([worst] + [(g_ - ref).abs().max().item() for g_ in got])
+            print(f"{name:42s} {'bf16x6' if on else 'native'}: side-stream bilinear max |diff| vs alone {worst:.2e}")
