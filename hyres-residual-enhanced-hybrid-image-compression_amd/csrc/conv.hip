@@ -1279,6 +1279,12 @@ __global__ __launch_bounds__(512, 1) void conv3x3_wres_bf6_kernel(const ConvArgs
     __shared__ int2 tapoff[9];
     __bf16* const Ws = lds;
     __bf16* const Hs = lds + 3 * BF6_WPL;
+    // The block takes the whole VGPR file of its SIMDs (2 waves x 256; the code needs 220). With the compiler's 224,
+    // waves of OTHER kernels co-resident on those SIMDs (a bilinear on a side stream) computed wrong values while this
+    // kernel's own output stayed exact (round 4, tests/test_bf6_gpu.py::test_bf6_kernels_beside_a_bilinear: 0.25 off,
+    // gone with this line; the native and f16 weight-resident kernels and every other bf16x6 kernel do not show it).
+    // Cause not identified; no cost to this kernel (its LDS already limits the CU to one block).
+    asm volatile("" ::: "v255");
     const hyres_conv_geom& g = a.g;
     const int tid = threadIdx.x;
     const int nrt = (g.Ho + HALO_R - 1) / HALO_R, nct = g.Wo / HALO_TW;

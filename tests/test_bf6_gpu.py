@@ -303,9 +303,11 @@ def test_bf6_refine_layers_match_native():
                                                      rel_err(extra["bf6_serial"], runs[False][2]),
                                                      rel_err(extra["bf6_again"], runs[True][2]),
                                                      rel_err(extra["native_serial"], runs[False][2])))
-    # what holds: bf16x6 with the scales serialised agrees with native to fp32 noise, and native is the same with and
-    # without the branch streams. With the branch streams, bf16x6 was measured to vary run to run (round 4: layer 3,
-    # the 1/2-scale block's first conv, 4e-2 apart; the reason this GEMM is opt-in) — printed above, not asserted
+    # bf16x6 agrees with native to fp32 noise serialised and with the branch streams, and each is the same run to run
+    # (round 4 found the bf16x6 weight-resident conv corrupting co-resident waves of the branch kernels: 4e-2 here)
+    assert rel_err(runs[True][2], runs[False][2]) < 1e-5
+    assert rel_err(extra["bf6_again"], runs[True][2]) == 0.0
+    assert all(rel_err(r[0], reps[0][0]) == 0.0 and rel_err(r[1], reps[0][1]) == 0.0 for r in reps[1:])
     assert rel_err(extra["bf6_serial"], extra["native_serial"]) < 1e-5
     assert rel_err(extra["native_serial"], runs[False][2]) < 1e-6
 
@@ -383,40 +385,7 @@ def test_bf6_refine_branch_determinism():
             s.hip = origs[i]
     for subset, ef, eo in rows:
         print(f"bf16x6 on scales {[i + 1 for i in subset]}: run-to-run f2 input {ef:.1e}, output {eo:.1e}")
-
-
-@pytest.mark.parametrize("dil", [1, 2])
-def test_bf6_conv_concurrent_with_bilinear(dil):
-    """Isolates the MultiScaleRefine run-to-run spread: the 1/2-scale bilinear of the SE output on a side stream while
-    the full-scale 3x3 conv (dilation 1: conv3x3_wres_*; 2: the implicit GEMM) reads the same tensor on the main
-    stream; the bilinear output against the same bilinear run alone."""
-    from hyres_hip import ops as O
-    from hyres_hip import refine_ops as R
-    D = dev()
-    B, H, W, C = 2, 256, 256, 64
-    feat = O.to_nhwc(_rand((B, C, H, W), 71).to(D))
-    w = torch.nn.Parameter(_rand((C, C, 3, 3), 72, (C * 9) ** -0.5).to(D))
-    b = _rand((C,), 73, 0.1).to(D)
-    slope = torch.full((1,), 0.25, device=D)
-    with torch.no_grad():
-        ref = R.bilinear(None, feat, H // 2, W // 2, 2.0, 2.0).v.clone()
-    torch.cuda.synchronize()
-    side = torch.cuda.Stream(device=D)
-    for on in (False, True):
-        worst = 0.0
-        for _ in range(5):
-            multi = O.Node.new(B, H, W, 3 * C, D)
-            with _Bf6(on), torch.no_grad():
-                fork = torch.cuda.Event()
-                fork.record()
-                O.conv2d(None, feat, w, b, pad=dil, dil=dil, act=L_ACT_PRELU(), slope=slope, out=multi.slice(0, C))
-                side.wait_event(fork)
-                with torch.cuda.stream(side):
-                    f2 = R.bilinear(None, feat, H // 2, W // 2, 2.0, 2.0)
-                torch.cuda.current_stream().wait_stream(side)
-            torch.cuda.synchronize()
-            worst = max(worst, (f2.v - ref).abs().max().item())
-        print(f"dil {dil} {'bf16x6' if on else 'native'}: bilinear beside the conv, max |diff| vs alone {worst:.2e}")
+    assert all(ef == 0.0 and eo == 0.0 for _, ef, eo in rows)
 
 
 @pytest.mark.parametrize("mode", ["native", "bf16x6", "f16"])
@@ -463,6 +432,7 @@ def test_conv_beside_side_stream_kernels(mode):
             worst[3] = max(worst[3], (y.v.float() - y0.float()).abs().max().item())
     print(f"{mode}: max |diff| vs alone — bilinear(conv input) {worst[0]:.2e}, bilinear(other) {worst[1]:.2e}, "
           f"copy(other) {worst[2]:.2e}, conv output {worst[3]:.2e}")
+    assert worst == [0.0] * 4
 
 
 def test_bf6_kernels_beside_a_bilinear():
@@ -515,3 +485,4 @@ def test_bf6_kernels_beside_a_bilinear():
                     torch.cuda.synchronize()
                     worst = max([worst] + [(g_ - ref).abs().max().item() for g_ in got])
             print(f"{name:42s} {'bf16x6' if on else 'native'}: side-stream bilinear max |diff| vs alone {worst:.2e}")
+            assert worst == 0.0, (name, on)

@@ -31,19 +31,14 @@ def _rand(shape, seed, scale=1.0):
 
 @pytest.fixture(params=["native", "bf16x6"])
 def fp32_gemm(request):
-    """The fp32 convs' GEMM (hyres_conv_tuning key 7): the native fp32 MFMA (the default) and the opt-in bf16x6 split
-    on the bf16 MFMA — every test taking this fixture holds its fp32 bars on both. bf16x6 runs with the concurrent
-    branch streams serialised: with them, bf16x6 results were observed to vary run to run (DESIGN §4 "bf16x6",
-    tests/test_bf6_gpu.py::test_bf6_refine_layers_match_native), which is why it is not the default."""
+    """The fp32 convs' GEMM (hyres_conv_tuning key 7): the native fp32 MFMA and the bf16x6 split on the bf16 MFMA —
+    every test taking this fixture holds its fp32 bars on both, with the concurrent branch streams on."""
     from hyres_hip import _lib as L
-    from hyres_hip import ops as O
     old = ctypes.c_int(0)
     L.call("hyres_conv_tuning", 7, 1 if request.param == "bf16x6" else 0, ctypes.byref(old))
-    O.BranchStreams.enabled = request.param != "bf16x6"
     try:
         yield request.param
     finally:
-        O.BranchStreams.enabled = True
         L.call("hyres_conv_tuning", 7, old.value, None)
 
 
