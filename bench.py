@@ -101,8 +101,12 @@ def cpu_baseline(args, budget_s):
 
 
 # scripts/profile_round.sh r3z: the fp32 line's dominant kernel, and the AMP leg's dominant kernel from the same passes
-PMC_TRAFFIC = os.path.join(REPO, "profiles", os.environ.get("HYRES_PMC_TRAFFIC", "r4d_pmc_traffic.json"))
-PMC_TRAFFIC_AMP = os.path.join(REPO, "profiles", os.environ.get("HYRES_PMC_TRAFFIC_AMP", "r4d_pmc_traffic_amp.json"))
+# committed PMC summaries, newest first: the first one collected for the kernel being priced is used
+# (r4d: the bf16x6 weight-resident conv; r4b: the native one, both after the XCD fix)
+PMC_TRAFFIC = [os.path.join(REPO, "profiles", f) for f in
+               os.environ.get("HYRES_PMC_TRAFFIC", "r4d_pmc_traffic.json,r4b_pmc_traffic.json").split(",")]
+PMC_TRAFFIC_AMP = [os.path.join(REPO, "profiles", f) for f in
+                   os.environ.get("HYRES_PMC_TRAFFIC_AMP", "r4d_pmc_traffic_amp.json").split(",")]
 EAGER_TIMED = 3  # eager steps behind the live per-launch roofline timing
 
 
@@ -167,14 +171,16 @@ def traffic_bytes_per_launch(kernel, path=None):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC passes of this same
     command (scripts/pmc_traffic.py: 2 x FETCH_SIZE + WRITE_SIZE, separate passes, gfx950 FETCH_SIZE
     correction); None when that summary is absent or was collected for another kernel."""
-    try:
-        with open(path or PMC_TRAFFIC) as f:
-            d = json.load(f)
-        if kernel is None or kernel not in d["kernel"]:
-            return None
-        return d["traffic_bytes_per_launch"]
-    except (OSError, KeyError, ValueError):
-        return None
+    paths = path or PMC_TRAFFIC
+    for p in [paths] if isinstance(paths, str) else paths:
+        try:
+            with open(p) as f:
+                d = json.load(f)
+            if kernel is not None and kernel in d["kernel"]:
+                return d["traffic_bytes_per_launch"]
+        except (OSError, KeyError, ValueError):
+            pass
+    return None
 
 
 def eval_legs(net, x, jpeg, jpeg_bpp, args, reps=20):
