@@ -12,7 +12,7 @@ import test_parity_gpu as T  # noqa: E402
 from hyres_hip import _lib as L  # noqa: E402
 from hyres_hip import ops as O  # noqa: E402
 
-CONFIGS = ((1, True), (1, True)) if "--quick" in sys.argv else ((1, True), (1, True), (0, True), (1, False), (0, False))
+CONFIGS = ((1, True),) if "--once" in sys.argv else ((1, True), (1, True)) if "--quick" in sys.argv else ((1, True), (1, True), (0, True), (1, False), (0, False))
 for sh, br in CONFIGS:
     old = ctypes.c_int(0)
     L.call("hyres_conv_tuning", 8, sh, ctypes.byref(old))
