@@ -2052,7 +2052,7 @@ static void dense_taps(hyres_conv_geom* g, int KH, int KW, int sgn, int dil, int
 
 // keys: HYRES_TUNE_TILE, _SPLIT_BLOCKS, _SPLIT_MINCHUNKS, _WGRAD_BLOCKS, _WGRAD_MINCHUNKS, _WGRAD_NT,
 // _WGRAD_MAXSPLIT
-int g_tune[9] = {-1, -1, -1, -1, -1, -1, -1, 0, 1};  // key 7: fp32 GEMMs native (1: bf16x6); key 8: fp16 streaming 1x1
+int g_tune[9] = {-1, -1, -1, -1, -1, -1, -1, 1, 1};  // key 7: fp32 GEMMs bf16x6 (0: native fp32 MFMA); key 8: fp16 streaming 1x1
 
 }  // namespace hyres
 

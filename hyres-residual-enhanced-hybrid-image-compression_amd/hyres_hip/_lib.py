@@ -206,13 +206,12 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         fn.restype = res
         fn.argtypes = args
     _lib = lib
-    # HYRES_FP32_GEMM=bf16x6: the fp32 convs on the bf16 MFMA through the three-way split instead of the native fp32
-    # MFMA (the library default; hyres_conv_tuning key 7)
-    mode = os.environ.get("HYRES_FP32_GEMM", "native")
+    # HYRES_FP32_GEMM: the fp32 convs' GEMM — bf16x6 (the library default: the three-way bf16 split on the bf16 MFMA)
+    # or native (the fp32 MFMA); hyres_conv_tuning key 7
+    mode = os.environ.get("HYRES_FP32_GEMM", "bf16x6")
     if mode not in ("bf16x6", "native"):
         raise ValueError(f"HYRES_FP32_GEMM={mode!r}: 'bf16x6' or 'native'")
-    if mode == "bf16x6":
-        lib.hyres_conv_tuning(7, 1, None)
+    lib.hyres_conv_tuning(7, 1 if mode == "bf16x6" else 0, None)
     return lib
 
 

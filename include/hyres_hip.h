@@ -168,10 +168,10 @@ int hyres_conv_plan(const hyres_conv_geom* g, const hyres_epilogue* e, int* tile
 #define HYRES_TUNE_WGRAD_NT 5         /* 1: no tap grouping (one tap per block column group) */
 #define HYRES_TUNE_WGRAD_MAXSPLIT 6   /* maximum split count */
 #define HYRES_TUNE_F32_GEMM 7         /* GEMM of the fp32 convolutions (forward, input-gradient, and the halo-staged /
-                                       * 1x1 weight gradients): 0 the native fp32 MFMA (default), 1 bf16x6 (each fp32 operand
-                                       * split into 3 bf16 pieces, the 6 cross products with i + j <= 2, fp32 accumulation —
-                                       * per-product error <= ~2^-25, i.e. fp32-accurate, on the 16x faster bf16 MFMA;
-                                       * opt-in: DESIGN §4 "bf16x6") */
+                                       * 1x1 weight gradients): 1 bf16x6 (default: each fp32 operand split into 3 bf16
+                                       * pieces, the 6 cross products with i + j <= 2, fp32 accumulation — per-product
+                                       * error <= ~2^-25, i.e. fp32-accurate, on the 16x faster bf16 MFMA; DESIGN §4
+                                       * "bf16x6"), 0 the native fp32 MFMA */
 #define HYRES_TUNE_STREAM_H 8         /* 1 (default): fp16-activation 1x1 convs with K, Co <= 128 on >= 16384 pixels on the
                                        * streaming kernel (conv1x1_stream_h_kernel); 0: the tiled kernel (A/B) */
 int hyres_conv_tuning(int key, int value, int* old);

@@ -1,6 +1,7 @@
 #!/bin/bash
 # One GPU-box evidence pass, by phase: scripts/check.sh <tag> <phase>...
 #   tests   full -m gpu suite           smoke  __graft_entry__.smoke()
+#   tests1  the suite without the AMP-fixture test; ampfix  that test alone (its failure does not stop the pass)
 #   bench   the driver's bench command  stats  rocprofv3 kernel stats of a short bench command
 #   pmc     FETCH_SIZE / WRITE_SIZE passes -> HBM bytes per launch of the fp32 and AMP dominant kernels
 #   steps   per-kernel tables of 10 replayed fp32 / AMP steps (scripts/profile_steps.sh)
@@ -18,6 +19,8 @@ BENCH="bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-eval"
 for ph in "$@"; do
   case $ph in
     tests) scripts/gpu_run.sh "gputests:600:python -u -m pytest tests -x -v --timeout 120 --timeout-method thread -m gpu -s" || exit $? ;;
+    tests1) scripts/gpu_run.sh "gputests:600:python -u -m pytest tests -x -v --timeout 120 --timeout-method thread -m gpu -s --deselect tests/test_parity_gpu.py::test_amp_matches_reference_autocast_fixture" || exit $? ;;
+    ampfix) scripts/gpu_run.sh "ampfix:200:python -u -m pytest tests/test_parity_gpu.py -v --timeout 180 --timeout-method thread -m gpu -s -k test_amp_matches_reference_autocast_fixture" ;;
     smoke) scripts/gpu_run.sh "smoke:200:python -c 'import __graft_entry__ as g; g.smoke()'" || exit $? ;;
     bench) scripts/gpu_run.sh "bench_full:500:python3 bench.py --gpus 1 --steps 20 --warmup 5" || exit $?
            grep '^{' gpurun_out/bench_full.log > gpurun_out/${tag}_bench_line.json ;;

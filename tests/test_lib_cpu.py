@@ -136,17 +136,18 @@ def test_conv_kernel_name_follows_the_launch_routing():
     e.kind = L.EPI_BIAS
     g3 = _geom("hyres_geom_conv2d", 16, 128, 128, 64, 64, 64, 64, 3, 3, 1, 1, 1)
     g3b = _geom("hyres_geom_conv2d", 16, 128, 128, 96, 96, 64, 64, 3, 3, 1, 1, 1)  # Ci = 96: implicit GEMM
-    # bf16x6 on the bf16 MFMA (hyres_conv_tuning key 7 = 1, opt-in)
+    # bf16x6 on the bf16 MFMA (hyres_conv_tuning key 7 = 1, the default)
     old = ctypes.c_int(0)
     L.call("hyres_conv_tuning", 7, 1, ctypes.byref(old))
     try:
-        assert old.value == 0  # the default: the native fp32 MFMA
+        assert old.value == 1  # the default
         assert conv_variant(g3, e, False) == "conv3x3_wres_bf6_kernel"
         assert conv_variant(g3b, e, False) == "conv_fwd_b6_kernel<2, 1, 2, 2, 0, false>"
         assert conv_variant(g3b, e, True) == "conv_fwd_b6_kernel<2, 1, 2, 2, 0, true>"
+        L.call("hyres_conv_tuning", 7, 0, None)  # the native fp32 MFMA
+        _native_routing(L, e, g3, g3b, _geom, conv_variant)
     finally:
         L.call("hyres_conv_tuning", 7, old.value, None)
-    _native_routing(L, e, g3, g3b, _geom, conv_variant)
 
 
 def _native_routing(L, e, g3, g3b, _geom, conv_variant):
@@ -228,15 +229,15 @@ def test_conv_plan_split_follows_the_tile():
 
 
 def test_fp32_gemm_env_switch():
-    """HYRES_FP32_GEMM selects the fp32 convs' GEMM at library load: the native fp32 MFMA (default,
-    hyres_conv_tuning key 7 = 0) or bf16x6 (key 7 = 1); anything else is refused."""
+    """HYRES_FP32_GEMM selects the fp32 convs' GEMM at library load: bf16x6 (default, hyres_conv_tuning key 7 = 1)
+    or the native fp32 MFMA (key 7 = 0); anything else is refused."""
     import os
     import subprocess
     import sys
     from conftest import PKG
     code = ("import ctypes, sys; sys.path.insert(0, %r); from hyres_hip import _lib as L; o = ctypes.c_int(-1); "
             "L.call('hyres_conv_tuning', 7, 1, ctypes.byref(o)); print(o.value)") % PKG
-    for env, want in ((None, "0"), ("bf16x6", "1"), ("native", "0")):
+    for env, want in ((None, "1"), ("bf16x6", "1"), ("native", "0")):
         e = dict(os.environ)
         e.pop("HYRES_FP32_GEMM", None)
         if env is not None:
