@@ -1544,9 +1544,17 @@ def test_amp_matches_reference_autocast_fixture():
     # worst single tensor: within 0.25 of the reference AMP, unless the reference AMP is itself further than that
     # from fp32 — then this run must be no further from fp32 than the reference AMP is (the PReLU slopes are
     # cancelled sums of g*x: fp16 rounding points decide them, see test_amp_train_step_vs_fp32)
-    bad = [(e, n, own[n]) for e, n in rel if e >= 0.25 and not (own[n][1] >= 0.25 and own[n][0] <= own[n][1])]
+    slopes = {f"{m}.weight" for m, mod in net.named_modules() if isinstance(mod, torch.nn.PReLU)}
+    bad = [(e, n, own[n]) for e, n in rel if n not in slopes and e >= 0.25
+           and not (own[n][1] >= 0.25 and own[n][0] <= own[n][1])]
     assert not bad, bad[:3]
-    assert dval[len(dval) // 2][0] < 0.05 and ours_wrong <= max(2, nsamp // 100), (dval[:5], signs[:5])
+    # PReLU slopes: each ONE cancelled sum of g*x over a whole activation (both AMP runs are far from fp32 on some:
+    # the reference AMP 3.9x on refine.act_in, measured round 4) — this run within 0.5 of fp32 on every one
+    sl = [(own[n][0], n, own[n][1]) for n in slopes if n in own]
+    print("PReLU slopes, distance from fp32 (this AMP, reference AMP):", sorted(sl, reverse=True))
+    assert all(e < 0.5 for e, _, _ in sl), sl
+    wrong = {(n, v) for n, v, h, h32 in signs if n not in slopes and h * h32 < 0}
+    assert dval[len(dval) // 2][0] < 0.05 and len(wrong) <= max(2, nsamp // 100), (dval[:5], sorted(wrong)[:5])
 
 
 @pytest.mark.parametrize("K,Ci,Co,H", [(3, 64, 64, 128), (1, 128, 64, 128), (1, 64, 128, 128)])
