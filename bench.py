@@ -102,11 +102,11 @@ def cpu_baseline(args, budget_s):
 
 # scripts/profile_round.sh r3z: the fp32 line's dominant kernel, and the AMP leg's dominant kernel from the same passes
 # committed PMC summaries, newest first: the first one collected for the kernel being priced is used
-# (r4d: the bf16x6 weight-resident conv; r4b: the native one, both after the XCD fix)
+# (r4i: the bf16x6 weight-resident conv; r4b: the native one, both after the XCD fix)
 PMC_TRAFFIC = [os.path.join(REPO, "profiles", f) for f in
-               os.environ.get("HYRES_PMC_TRAFFIC", "r4d_pmc_traffic.json,r4b_pmc_traffic.json").split(",")]
+               os.environ.get("HYRES_PMC_TRAFFIC", "r4i_pmc_traffic.json,r4b_pmc_traffic.json").split(",")]
 PMC_TRAFFIC_AMP = [os.path.join(REPO, "profiles", f) for f in
-                   os.environ.get("HYRES_PMC_TRAFFIC_AMP", "r4d_pmc_traffic_amp.json").split(",")]
+                   os.environ.get("HYRES_PMC_TRAFFIC_AMP", "r4i_pmc_traffic_amp.json").split(",")]
 EAGER_TIMED = 3  # eager steps behind the live per-launch roofline timing
 
 
@@ -359,7 +359,7 @@ def amp_leg(net, opt, aux_opt, crit, x, jpeg, jpeg_bpp, args):
 
 
 def with_traffic(r, kernel):
-    """The AMP leg's roofline entry with its PMC-measured HBM bytes per launch (profiles/r4d_pmc_traffic_amp.json)."""
+    """The AMP leg's roofline entry with its PMC-measured HBM bytes per launch (profiles/r4i_pmc_traffic_amp.json)."""
     if r is not None:
         r["traffic"] = traffic_bytes_per_launch(kernel, PMC_TRAFFIC_AMP)
     return r
