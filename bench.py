@@ -750,6 +750,28 @@ def main():
                              "headline on this box"}
         finally:
             L.call("hyres_conv_tuning", 7, cur.value, None)
+    # the same step with the concurrent branch streams off (every kernel on the main stream), A/B on this box
+    serial = None
+    if world == 1 and graphed is not None:
+        from hyres_hip.graphs import CapturedStep
+        O.BranchStreams.enabled = False
+        try:
+            gs = CapturedStep(net, x, jpeg, jpeg_bpp, noisequant=False, criterion=crit, zero_grad=opt.zero_grad)
+            for _ in range(args.warmup):
+                step(gr=gs)
+            torch.cuda.synchronize()
+            t0 = time.time()
+            for _ in range(args.steps):
+                step(gr=gs)
+            torch.cuda.synchronize()
+            ms_s = (time.time() - t0) * 1000 / args.steps
+            gs.close()
+            del gs
+            serial = {"ms_per_step": round(ms_s, 3), "value": round(B * S * S / ms_s / 1e3, 4),
+                      "note": "the same graphed C2 step with MultiScaleRefine's / AttentionBlock's branches on one "
+                              "stream, timed after the headline on this box"}
+        finally:
+            O.BranchStreams.enabled = True
     evals = None
     if world == 1 and not args.no_eval:
         evals = eval_legs(net, x, jpeg, jpeg_bpp, args)
@@ -790,6 +812,7 @@ def main():
         "fp32_gemm": fp32_gemm,
         "fp32_gemm_note": FP32_GEMM_NOTE[fp32_gemm],
         "fp32_gemm_ab": other,
+        "branch_streams_off_ab": serial,
         "roofline": {"bound": "mfma", "kernel": f"{ks['kernel']} ({kernel_label(ks['kernel'])})",
                      "achieved": round(achieved, 3), "peak": kernel_peak(ks["kernel"]), "unit": "TFLOP/s",
                      "peak_note": peak_note(ks["kernel"]),
