@@ -248,3 +248,21 @@ def test_fp32_gemm_env_switch():
     e = dict(os.environ, HYRES_FP32_GEMM="tf32")
     out = subprocess.run([sys.executable, "-c", code], env=e, capture_output=True, text=True, timeout=120)
     assert out.returncode != 0 and "HYRES_FP32_GEMM" in out.stderr
+
+
+def test_bench_prices_each_kernel_with_its_own_pmc_summary():
+    """bench.py's roofline ``traffic`` comes from the committed PMC summary collected for the kernel it prices
+    (bf16x6 and native weight-resident convs, the AMP kernel), and is None for a kernel no summary covers."""
+    import importlib.util
+    import json
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(REPO, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    for kernel, paths in (("conv3x3_wres_bf6_kernel", b.PMC_TRAFFIC), ("conv3x3_wres_f32_kernel", b.PMC_TRAFFIC),
+                          ("conv_fwd_h_kernel<1, 2, 2, 2, 0, false, 3>", b.PMC_TRAFFIC_AMP)):
+        got = b.traffic_bytes_per_launch(kernel, paths)
+        want = next(json.load(open(p))["traffic_bytes_per_launch"] for p in paths
+                    if os.path.exists(p) and kernel in json.load(open(p))["kernel"])
+        assert got == want and got > 0
+    assert b.traffic_bytes_per_launch("no_such_kernel") is None
+    assert b.traffic_bytes_per_launch(None) is None
