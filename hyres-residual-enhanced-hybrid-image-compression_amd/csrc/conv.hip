@@ -1255,7 +1255,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3_wres_f32_kernel(const ConvArgs
 }
 
 // ------------------------------------------------------------------------------------------------
-// fp32-accurate weight-resident 3x3 conv on the bf16 MFMA ("bf16x6", hyres_conv_tuning key 7 = 1; opt-in).
+// fp32-accurate weight-resident 3x3 conv on the bf16 MFMA ("bf16x6", hyres_conv_tuning key 7 = 1, the default).
 // conv3x3_wres_f32_kernel above runs at ~0.7 of the fp32 MFMA peak, and that peak (157 TF/s) is 1/16 of the bf16
 // MFMA's. Here every fp32 operand is split into three bf16 pieces x = x0 + x1 + x2 (x0 = bf16(x), x1 = bf16(x - x0),
 // x2 = bf16(x - x0 - x1): 24 significant bits, |x - x0 - x1 - x2| <= 2^-25 |x|) and each product is formed from the
