@@ -1145,7 +1145,6 @@ class BranchStreams:
     # (default stream priority: a high-priority branch or main stream measured 25-40 % slower steps, round 2;
     # limiting the branches to small grids +1.5 %; those switches were removed in round 4)
     enabled = True
-    side_first = False
     _streams = {}
 
     @classmethod
@@ -1184,10 +1183,8 @@ def run_branches(tape: Optional[Tape], x: Node, fns) -> list:
         tape.push(join_bwd)
     fork = torch.cuda.Event()
     fork.record(main)  # x is ready here; branch 0 is enqueued on main after this point
-    outs = [None] * n
-    bstate = {}
-
-    def side(k):
+    outs = [fns[0](tape, proxies[0])]
+    for k in range(1, n):
         st = streams[k]
         st.wait_event(fork)
         x.v.record_stream(st)
@@ -1199,34 +1196,19 @@ def run_branches(tape: Optional[Tape], x: Node, fns) -> list:
             tape.push(leave)
         torch.cuda.set_stream(st)
         try:
-            outs[k] = fns[k](tape, proxies[k])
+            outs.append(fns[k](tape, proxies[k]))
         finally:
             torch.cuda.set_stream(main)
         if tape is not None:
             def enter(st=st, cell=cell):
                 cur = torch.cuda.current_stream(dev)
                 cell["prev"] = cur
-                if "ready" in bstate:  # side_first: branch 0's backward is already enqueued on cur
-                    st.wait_event(bstate["ready"])
-                else:
-                    st.wait_stream(cur)
+                st.wait_stream(cur)
                 torch.cuda.set_stream(st)
             tape.push(enter)
-        if isinstance(outs[k], Node):
-            outs[k].v.record_stream(main)
-    # side_first: the side branches' kernels are enqueued (and so dispatched) before branch 0's (A/B switch)
-    if not BranchStreams.side_first:
-        outs[0] = fns[0](tape, proxies[0])
-    for k in range(1, n):
-        side(k)
-    if BranchStreams.side_first:
-        outs[0] = fns[0](tape, proxies[0])
-        if tape is not None:
-            def ready():  # runs first in backward: the output gradients are complete here
-                ev = torch.cuda.Event()
-                ev.record(torch.cuda.current_stream(dev))
-                bstate["ready"] = ev
-            tape.push(ready)
+        o = outs[-1]
+        if isinstance(o, Node):
+            o.v.record_stream(main)
     for k in range(1, n):
         main.wait_stream(streams[k])
     return outs

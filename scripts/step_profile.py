@@ -23,10 +23,7 @@ def main():
     ap.add_argument("--eval", action="store_true", help="eval forward (encode+decode) instead of a train step")
     ap.add_argument("--marker", action="store_true",
                     help="a torch spin kernel between the warm-up and the timed steps (scripts/step_traffic.py)")
-    ap.add_argument("--side-first", action="store_true", help="ops.BranchStreams.side_first (A/B)")
     args = ap.parse_args()
-    from hyres_hip import ops as O
-    O.BranchStreams.side_first = args.side_first
     from hyres_hip.graphs import CapturedStep
     from hyres_hip.loss import RateDistortionLoss
     from hyres_hip.optim import DeviceGradScaler, FusedAdam

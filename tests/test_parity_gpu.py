@@ -1592,30 +1592,3 @@ def test_wgrad_many_split_reduce_deterministic(K, Ci, Co, H):
     F.conv2d(xr, wr, None, padding=K // 2).backward(gyr)
     assert rel_err(outs[0][0].cpu(), wr.grad) < 1e-5
     assert rel_err(outs[0][1].cpu(), gyr.sum((0, 2, 3))) < 1e-5
-
-
-def test_branch_side_first_order_same_gradients():
-    """ops.BranchStreams.side_first (the side branches enqueued before branch 0, A/B switch) changes only the
-    enqueue order: the train step's loss and every gradient are bit-identical to the default order."""
-    from hyres_hip import ops as O
-    g = load_npz("hyres_train_nq_b2_64.npz")
-    D = dev()
-    res = {}
-    for sf in (False, True):
-        O.BranchStreams.side_first = sf
-        try:
-            net, _ = _hip_model()
-            net.train()
-            net.residual_model.noise.injected = _nhwc_noise(g, NQ_KEYS, D)
-            out = net(g["x"], noisequant=True, jpeg=(g["jpeg_decoded"], float(g["jpeg_bpp"])))
-            from hyres_hip.loss import RateDistortionLoss
-            crit = RateDistortionLoss(lmbda=0.045, alpha=0)(out, g["x"].to(D))
-            crit["loss"].backward()
-            torch.cuda.synchronize()
-            res[sf] = (float(crit["loss"]), {n: p.grad.detach().clone() for n, p in net.named_parameters()
-                                             if p.grad is not None})
-        finally:
-            O.BranchStreams.side_first = False
-    assert res[False][0] == res[True][0]
-    bad = [n for n, t in res[False][1].items() if not torch.equal(t, res[True][1][n])]
-    assert not bad, bad[:5]
