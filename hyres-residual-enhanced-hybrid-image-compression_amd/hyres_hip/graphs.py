@@ -177,7 +177,12 @@ class CapturedStep:
         self._ws_keep = []
 
     def __del__(self):
+        # A finalizer may run while ANOTHER graph is being captured (garbage collection inside the capture): a
+        # device synchronize there would invalidate that capture. Owners release graphs with close(); here the
+        # graph is only torn down when no capture is in progress, else it is left to the process's end.
         try:
+            if torch.cuda.is_current_stream_capturing():
+                return
             self.close()
         except Exception:  # noqa: BLE001 - interpreter shutdown
             pass

@@ -163,7 +163,10 @@ class Node:
         """``grad_target`` for an input-gradient conv: a deferred residual gradient is folded into its
         epilogue as ``e.res`` (the ReLU mask, if the conv applies it, then covers both). Returns
         (tensor, accumulate, keep-alive tensor or None)."""
-        if self.pending is not None and self.parent is None and not self.gflag:
+        # the conv reads e.res in the dtype of the gradient it writes: fold only a same-dtype pending gradient
+        # (a mixed pair, e.g. an fp16 gradient deferred onto an fp32-gradient node, goes through add2d)
+        if (self.pending is not None and self.parent is None and not self.gflag
+                and self.pending[0].dtype == self.gdt):
             g, ld = self.pending
             self.pending = None
             tgt, acc = self.grad_target()

@@ -84,6 +84,8 @@ def main(argv):
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group("nccl")
+        from src.utils.engine import host_group
+        host_group()  # the per-step host agreement group, created once per run (not once per epoch)
     device = torch.device("cuda", local if world > 1 else 0)
 
     train_tf = transforms.Compose([transforms.RandomCrop(args.patch_size), transforms.ToTensor()])
@@ -100,6 +102,10 @@ def main(argv):
     test_shard = list(range(rank, len(test_dataset), world)) if world > 1 else None
     test_loader = DataLoader(test_dataset, batch_size=args.test_batch_size, num_workers=args.num_workers,
                              shuffle=False, sampler=test_shard, pin_memory=False)
+    # rank 0's best-checkpoint image dump walks the WHOLE test set alone (the reference's first test images and
+    # metrics), with no collective: the other ranks are already in the next epoch
+    full_test_loader = test_loader if world == 1 else DataLoader(
+        test_dataset, batch_size=args.test_batch_size, num_workers=args.num_workers, shuffle=False, pin_memory=False)
 
     net = ResidualJPEGCompression(base_model=LightWeightCheckerboard(N=args.N, M=args.M),
                                   jpeg_quality=args.jpeg_quality).to(device)
@@ -173,7 +179,8 @@ def main(argv):
             save_checkpoint(state, filename=os.path.join(args.savepath, f"checkpoint_last_{epoch}.pth.tar"))
             if is_best:
                 best_loss = loss
-                test_epoch(epoch, test_loader, net, criterion, save_images=True, savepath=args.savepath)
+                test_epoch(epoch, full_test_loader, net, criterion, save_images=True, savepath=args.savepath,
+                           all_reduce=False)
                 DelfileList(args.savepath, "checkpoint_best")
                 save_checkpoint(state, filename=os.path.join(args.savepath, f"checkpoint_best_loss_{epoch}.pth.tar"))
     if world > 1:

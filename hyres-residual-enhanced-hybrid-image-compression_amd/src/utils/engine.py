@@ -69,7 +69,7 @@ class _GraphedStep:
         self.enabled = os.environ.get("HYRES_TRAIN_GRAPH", "1") == "1" and device.type == "cuda"
         self.overlap = os.environ.get("HYRES_DIST_MODE", "graph+allreduce") == "graph+overlap"
         self.last = None
-        self._host_group = None
+        self._host_group = host_group()
 
     def _agree(self, key) -> None:
         """Per-step host check under DDP: every rank must be at the same capture key (same batch shape /
@@ -77,10 +77,8 @@ class _GraphedStep:
         collectives and hang. Ranks that agree on the key also agree on whether it still needs a capture (the
         same keys were seen in the same order). One 2-int all-reduce on a gloo group: no device sync."""
         import torch.distributed as dist
-        if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
-            return
         if self._host_group is None:
-            self._host_group = dist.new_group(backend="gloo") if dist.get_backend() != "gloo" else dist.group.WORLD
+            return
         h = hash(key) & 0x3FFFFFFF  # tuples of ints / bools hash identically in every process
         t = torch.tensor([h, -h], dtype=torch.int64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self._host_group)
@@ -130,11 +128,36 @@ class _GraphedStep:
         self.last = cap
         return cap.replay(x, jd, float(bpp))[1]
 
+    def close(self) -> None:
+        """Release every captured graph explicitly (end of the epoch), not from a finalizer."""
+        for cap in self.caps.values():
+            cap.close()
+        self.caps.clear()
+        self.last = None
+
     def reduce(self, reducer):
         """The boundary all-reduce after a replayed step (graph+overlap: each segment's collectives start on
         the external event the capture recorded at its backward-progress marker; otherwise no events were
         recorded and the flat gradient is reduced after the replay in buckets)."""
         reducer.reduce_graphed(self.last.marker_events)
+
+
+_HOST_GROUP = [None, None]  # (default process group it was made for, the gloo group)
+
+
+def host_group():
+    """The host-side (gloo) process group for the per-step agreement all-reduces, created ONCE per process group
+    (``dist.new_group`` is itself a collective every rank must issue in the same order, and each group keeps its
+    TCP pairs and threads for the life of the run): src/training.py creates it right after
+    ``init_process_group``; later calls return the cached group. None without DDP."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return None
+    world = dist.group.WORLD
+    if _HOST_GROUP[0] is not world:
+        _HOST_GROUP[0] = world
+        _HOST_GROUP[1] = dist.new_group(backend="gloo") if dist.get_backend() != "gloo" else world
+    return _HOST_GROUP[1]
 
 
 def _all_ranks_ok(ok: bool, group) -> bool:
@@ -234,6 +257,7 @@ def train_one_epoch(model, criterion, train_dataloader, optimizer, aux_optimizer
                   f"\ty_Bpp loss: {meters['y_bpp_loss'].val:.4f} |\tz_Bpp loss: {meters['z_bpp_loss'].val:.4f} |"
                   f"\tMSE loss: {meters['mse_loss'].val:.3f} |"
                   f"\tAux loss: {float(aux_loss.detach()) if aux_loss is not None else 0.0:.2f}")
+    graphed.close()
     _drain(pending, meters, nan_flags)
     print(f"Train epoch {epoch}: Average losses:\tLoss: {meters['loss'].avg:.3f} |"
           f"\tBpp loss: {meters['bpp_loss'].avg:.4f} |\tResidual Bpp: {meters['residual_bpp_loss'].avg:.4f} |"
@@ -242,7 +266,10 @@ def train_one_epoch(model, criterion, train_dataloader, optimizer, aux_optimizer
     return meters["loss"].avg, meters["bpp_loss"].avg, meters["mse_loss"].avg
 
 
-def test_epoch(epoch, test_dataloader, model, criterion, save_images=False, savepath=None):
+def test_epoch(epoch, test_dataloader, model, criterion, save_images=False, savepath=None, all_reduce=True):
+    """``all_reduce``: under DDP each rank evaluated its shard and the meters are summed over ranks (a collective:
+    every rank must call it). The best-checkpoint image dump runs on rank 0 ALONE over the unsharded test set
+    (src/training.py) with ``all_reduce=False``, so it joins no collective the other ranks do not issue."""
     model.eval()
     device = next(model.parameters()).device
     meters = {k: AverageMeter() for k in _KEYS}
@@ -257,7 +284,8 @@ def test_epoch(epoch, test_dataloader, model, criterion, save_images=False, save
             if save_images and i < 6 and savepath:
                 _save_components(out_net, d, os.path.join(savepath, "best_recon"), i)
     _drain(pending, meters)
-    _all_reduce_meters(list(meters.values()) + [aux_meter], device)
+    if all_reduce:
+        _all_reduce_meters(list(meters.values()) + [aux_meter], device)
     print(f"Test epoch {epoch}: Average losses:\tLoss: {meters['loss'].avg:.3f} |"
           f"\tBpp loss: {meters['bpp_loss'].avg:.4f} |\tResidual Bpp: {meters['residual_bpp_loss'].avg:.4f} |"
           f"\ty_Bpp loss: {meters['y_bpp_loss'].avg:.4f} |\tz_Bpp loss: {meters['z_bpp_loss'].avg:.4f} |"

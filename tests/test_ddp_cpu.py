@@ -185,14 +185,15 @@ def _engine_host_worker(rank, world, port):
     _init(rank, world, port)
     try:
         from src.losses import AverageMeter
-        from src.utils.engine import _GraphedStep, _all_reduce_meters, _all_ranks_ok
+        from src.utils.engine import _GraphedStep, _all_reduce_meters, _all_ranks_ok, host_group
         m = AverageMeter()
         for v in ([1.0, 2.0] if rank == 0 else [4.0]):  # ragged shards: 2 batches on rank 0, 1 on rank 1
             m.update(v)
         _all_reduce_meters([m], "cpu")
         assert m.count == 3 and abs(m.avg - 7.0 / 3) < 1e-12
         gs = _GraphedStep.__new__(_GraphedStep)
-        gs._host_group = None
+        gs._host_group = host_group()
+        assert gs._host_group is not None and host_group() is gs._host_group  # one group per run, not per epoch
         gs._agree(((16, 3, 256, 256), False, False))  # same key on both ranks: passes
         assert _all_ranks_ok(rank == 0, gs._host_group) is False  # one rank failed: every rank falls back
         assert _all_ranks_ok(True, gs._host_group) is True
@@ -204,3 +205,52 @@ def _engine_host_worker(rank, world, port):
 
 def test_engine_ddp_host_agreement_gloo_world2():
     mp.spawn(_engine_host_worker, args=(2, _free_port()), nprocs=2, join=True)
+
+
+class _FakeNet(torch.nn.Module):
+    """Stands in for ResidualJPEGCompression in test_epoch (CPU): the output dict's image tensors and aux_loss."""
+
+    def __init__(self):
+        super().__init__()
+        self.p = torch.nn.Parameter(torch.zeros(1))
+
+    def forward(self, d):
+        return {"x_hat": d.clamp(0, 1), "jpeg_decoded": d, "residual": d - 0.5, "residual_hat": d - 0.5}
+
+    def aux_loss(self):
+        return self.p.sum() + 1.0
+
+
+def _fake_criterion(out, d):
+    v = d.mean()
+    return {k: v * (i + 1) for i, k in enumerate(("loss", "bpp_loss", "residual_bpp_loss", "y_bpp_loss",
+                                                   "z_bpp_loss", "mse_loss"))}
+
+
+def _save_epoch_worker(rank, world, port, savepath):
+    """The best-checkpoint image dump (src/training.py: ``if args.save and rank == 0``) runs test_epoch on rank 0
+    ALONE over the whole test set. It must issue no collective: rank 1 is already in the next epoch's all-reduce,
+    and a meter all-reduce on rank 0 would pair with it (wrong sums or a hang)."""
+    _init(rank, world, port)
+    try:
+        from src.utils.engine import test_epoch
+        data = [torch.full((1, 3, 8, 8), 0.1 * (i + 1)) for i in range(4)]
+        shard = data[rank::world]
+        net = _FakeNet()
+        loss, _, _ = test_epoch(0, shard, net, _fake_criterion)  # sharded epoch: meters summed over ranks
+        assert abs(loss - sum(float(t.mean()) for t in data) / len(data)) < 1e-6
+        if rank == 0:
+            loss0, _, _ = test_epoch(0, data, net, _fake_criterion, save_images=True, savepath=savepath,
+                                     all_reduce=False)
+            assert abs(loss0 - loss) < 1e-6  # the whole test set on rank 0 alone
+            assert os.path.exists(os.path.join(savepath, "best_metrics.csv"))
+            assert os.path.exists(os.path.join(savepath, "best_recon", "recon_3.png"))
+        nxt = torch.tensor([float(rank + 1)])  # "the next epoch's" collective
+        dist.all_reduce(nxt)
+        assert float(nxt) == 3.0
+    finally:
+        dist.destroy_process_group()
+
+
+def test_best_checkpoint_save_epoch_gloo_world2(tmp_path):
+    mp.spawn(_save_epoch_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
