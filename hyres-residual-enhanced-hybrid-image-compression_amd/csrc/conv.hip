@@ -919,6 +919,9 @@ __global__ __launch_bounds__(512, 2) void conv3x3_wres_f16_kernel(const ConvArgs
     typedef _Float16 half8 __attribute__((ext_vector_type(8)));
     _Float16* const Bs = lds;
     _Float16* const Hs = lds + WRES_LDS_B;
+    // whole VGPR file (as conv3x3_wres_bf6_kernel, DESIGN §4 "Cross-kernel interference"): IO 1 allocated 248 and left
+    // a 16-VGPR hole beside its two waves per SIMD; the others already allocate 256 (and the clobber made IO 3 spill)
+    if constexpr (IO == 1) asm volatile("" ::: "v255");
 
     const hyres_conv_geom& g = a.g;
     const int tid = threadIdx.x;
@@ -1274,17 +1277,19 @@ constexpr int BF6_HV = (BF6_HE + 511) / 512;
 // 16-B segment (0 / 1) of element k (0..15) of row r in a swizzled [row][16] bf16 image, as an element offset
 __device__ __forceinline__ int bf6_off(int r, int k) { return r * 16 + ((((k >> 3) ^ (r >> 3)) & 1) << 3) + (k & 7); }
 
+template <bool GUARD>
 __global__ __launch_bounds__(512, 1) void conv3x3_wres_bf6_kernel(const ConvArgs a, int ntiles, int groups) {
     __shared__ __attribute__((aligned(16))) __bf16 lds[3 * BF6_WPL + 3 * BF6_HPL];
     __shared__ int2 tapoff[9];
     __bf16* const Ws = lds;
     __bf16* const Hs = lds + 3 * BF6_WPL;
-    // The block takes the whole VGPR file of its SIMDs (2 waves x 256; the code needs 220). With the compiler's 224,
-    // waves of OTHER kernels co-resident on those SIMDs (a bilinear on a side stream) computed wrong values while this
-    // kernel's own output stayed exact (round 4, tests/test_bf6_gpu.py::test_bf6_kernels_beside_a_bilinear: 0.25 off,
-    // gone with this line; the native and f16 weight-resident kernels and every other bf16x6 kernel do not show it).
-    // Cause not identified; no cost to this kernel (its LDS already limits the CU to one block).
-    asm volatile("" ::: "v255");
+    // GUARD: the block takes the whole VGPR file of its SIMDs (2 waves x 256; the code needs 220). With the compiler's
+    // 224, waves of OTHER kernels co-resident on those SIMDs (a bilinear on a side stream) computed wrong values while
+    // this kernel's own output stayed exact (round 4, tests/test_bf6_gpu.py::test_bf6_kernels_beside_a_bilinear: 0.25
+    // off, gone with this line). The error signature and the probes that isolate it: DESIGN §4 "Cross-kernel
+    // interference" (scripts/diag_bf6_mechanism.py, scripts/coresidency_probe.hip). No cost to this kernel (its LDS
+    // already limits the CU to one block). GUARD = false exists only for that diagnosis (hyres_conv_tuning key 9 = 0).
+    if constexpr (GUARD) asm volatile("" ::: "v255");
     const hyres_conv_geom& g = a.g;
     const int tid = threadIdx.x;
     const int nrt = (g.Ho + HALO_R - 1) / HALO_R, nct = g.Wo / HALO_TW;
@@ -2052,7 +2057,9 @@ static void dense_taps(hyres_conv_geom* g, int KH, int KW, int sgn, int dil, int
 
 // keys: HYRES_TUNE_TILE, _SPLIT_BLOCKS, _SPLIT_MINCHUNKS, _WGRAD_BLOCKS, _WGRAD_MINCHUNKS, _WGRAD_NT,
 // _WGRAD_MAXSPLIT
-int g_tune[9] = {-1, -1, -1, -1, -1, -1, -1, 1, 1};  // key 7: fp32 GEMMs bf16x6 (0: native fp32 MFMA); key 8: fp16 streaming 1x1
+// key 7: fp32 GEMMs bf16x6 (0: native fp32 MFMA); key 8: fp16 streaming 1x1; key 9: the bf16x6 weight-resident 3x3's
+// whole-VGPR-file guard (0 = diagnostic unguarded build, DESIGN §4 "Cross-kernel interference")
+int g_tune[10] = {-1, -1, -1, -1, -1, -1, -1, 1, 1, 1};
 
 }  // namespace hyres
 
@@ -2284,7 +2291,10 @@ static int launch_wres32(const ConvArgs& a, hipStream_t st) {
     const int groups = g.Co / 32;
     const int per = wres_blocks(groups);
     if (wres_bf6()) {
-        hipLaunchKernelGGL(conv3x3_wres_bf6_kernel, dim3(per * groups), dim3(512), 0, st, a, ntiles, groups);
+        if (g_tune[9] == 0)  // diagnostic only: the allocation that let other kernels' waves share its SIMDs
+            hipLaunchKernelGGL(conv3x3_wres_bf6_kernel<false>, dim3(per * groups), dim3(512), 0, st, a, ntiles, groups);
+        else
+            hipLaunchKernelGGL(conv3x3_wres_bf6_kernel<true>, dim3(per * groups), dim3(512), 0, st, a, ntiles, groups);
         return HY_LAUNCH_CHECK("conv3x3_wres_bf6_kernel");
     }
     hipLaunchKernelGGL(conv3x3_wres_f32_kernel, dim3(per * groups), dim3(512), 0, st, a, ntiles, groups);
@@ -2439,7 +2449,7 @@ static long long plan_ws_bytes(const hyres_conv_geom* g, const ConvPlan& p) {
 }
 
 int hyres_conv_tuning(int key, int value, int* old) {
-    HY_REQUIRE(key >= 0 && key < 9, HYRES_E_ARG, "conv_tuning: key %d", key);
+    HY_REQUIRE(key >= 0 && key < 10, HYRES_E_ARG, "conv_tuning: key %d", key);
     if (old) *old = g_tune[key];
     g_tune[key] = value;
     return ok();

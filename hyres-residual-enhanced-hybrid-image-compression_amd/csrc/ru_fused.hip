@@ -24,6 +24,7 @@
 // The fp16 rounding points are the unfused autocast path's (t1, t2 stored fp16; every GEMM on fp16 operands), so the
 // results agree with it up to fp32 summation order (tests/test_ru_fused_gpu.py).
 #include "common.h"
+#include "conv_common.h"
 
 namespace hyres {
 
@@ -58,8 +59,14 @@ struct RuArgs {
     int B, H, W, ntiles, final_relu;
 };
 
+// GUARD: the whole VGPR file of its SIMDs (2 waves x 256; the code needs 228). With the compiler's 232 a 48-VGPR hole
+// per SIMD let another stream's waves share them, and a side-stream bilinear then lost loaded values (round 5,
+// scripts/bf6_interference_repro.hip ru: 20 of 20 runs wrong; DESIGN §4 "Cross-kernel interference"). No cost: the
+// 158.7 KB of LDS already limits the CU to one block. GUARD = false only for that diagnosis (hyres_conv_tuning key 9 = 0).
+template <bool GUARD>
 __global__ __launch_bounds__(512, 1) void ru_fused_f16_kernel(const RuArgs a) {
     __shared__ __attribute__((aligned(16))) _Float16 lds[RU_W2 + 2 * RU_TBUF];
+    if constexpr (GUARD) asm volatile("" ::: "v255");
     _Float16* const W2s = lds;
     _Float16* const T = lds + RU_W2;  // two buffers: x chunks (phase 1), t1 chunks (phase 2), t2 chunks (phase 3)
 
@@ -316,7 +323,10 @@ int hyres_ru_fused_f16(const void* x, void* y, int B, int H, int W, int N, const
         cus = 256;
     // one block per CU, at most one per tile, a multiple of 8 (XCD-contiguous tile ranges)
     const int blocks = std::max(8, (std::min(cus, a.ntiles) + 7) & ~7);
-    hipLaunchKernelGGL(ru_fused_f16_kernel, dim3(blocks), dim3(512), 0, as_stream(s), a);
+    if (g_tune[9] == 0)  // diagnostic only (DESIGN §4 "Cross-kernel interference")
+        hipLaunchKernelGGL(ru_fused_f16_kernel<false>, dim3(blocks), dim3(512), 0, as_stream(s), a);
+    else
+        hipLaunchKernelGGL(ru_fused_f16_kernel<true>, dim3(blocks), dim3(512), 0, as_stream(s), a);
     return HY_LAUNCH_CHECK("ru_fused_f16_kernel");
 }
 

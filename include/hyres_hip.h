@@ -174,6 +174,10 @@ int hyres_conv_plan(const hyres_conv_geom* g, const hyres_epilogue* e, int* tile
                                        * "bf16x6"), 0 the native fp32 MFMA */
 #define HYRES_TUNE_STREAM_H 8         /* 1 (default): fp16-activation 1x1 convs with K, Co <= 128 on >= 16384 pixels on the
                                        * streaming kernel (conv1x1_stream_h_kernel); 0: the tiled kernel (A/B) */
+#define HYRES_TUNE_WRES_BF6_GUARD 9   /* 1 (default): the bf16x6 weight-resident 3x3 conv and the fused f16 ResidualUnit declare the whole VGPR file of
+                                       * its SIMDs, so no other kernel's wave shares them; 0: DIAGNOSTIC ONLY, the
+                                       * allocation under which co-resident waves computed wrong values (DESIGN §4
+                                       * "Cross-kernel interference") */
 int hyres_conv_tuning(int key, int value, int* old);
 
 /* Weight gradient:  dW[t][m][n] = sum_q P[q][m] * Q[shift_t(q)][n]  over a base grid q (B,Hq,Wq).

@@ -123,39 +123,51 @@ __global__ __launch_bounds__(256) void victim(const float* x, float* y, int Hi, 
 
 // ------------------------------------------------------------------------------------------------ hog
 constexpr int HOG_LDS = 74240;  // bf16 elements = 148,480 B (the conv's 148.7 KB: one block per CU)
+typedef float float2v __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 
-__device__ __forceinline__ void split3(float x, __bf16& h, __bf16& m, __bf16& l) {
-    h = (__bf16)x;
-    const float r = x - (float)h;
-    m = (__bf16)r;
-    l = (__bf16)(r - (float)m);
+// MODE = 4 * CVT + MF.  CVT: 0 none, 1 v_cvt_pk_bf16_f32 splits, 2 v_cvt_pk_f16_f32 splits (ru_fused_f16_kernel's
+// convert).  MF: 0 none, 1 v_mfma_f32_32x32x16_bf16, 2 v_mfma_f32_32x32x16_f16, 3 v_mfma_f32_32x32x2f32.
+template <int CVT>
+__device__ __forceinline__ float2v split2(float2v x) {  // x -> hi + mid + lo pieces; returns a dependent sum
+    if constexpr (CVT == 1) {
+        const bf16x2 h = __builtin_convertvector(x, bf16x2);
+        const float2v r = x - __builtin_convertvector(h, float2v);
+        const bf16x2 m = __builtin_convertvector(r, bf16x2);
+        const bf16x2 l = __builtin_convertvector(r - __builtin_convertvector(m, float2v), bf16x2);
+        return __builtin_convertvector(m, float2v) + __builtin_convertvector(l, float2v);
+    } else if constexpr (CVT == 2) {
+        const f16x2 h = __builtin_convertvector(x, f16x2);
+        const float2v r = x - __builtin_convertvector(h, float2v);
+        const f16x2 m = __builtin_convertvector(r, f16x2);
+        const f16x2 l = __builtin_convertvector(r - __builtin_convertvector(m, float2v), f16x2);
+        return __builtin_convertvector(m, float2v) + __builtin_convertvector(l, float2v);
+    } else {
+        return x * 0.5f + 0.25f;
+    }
 }
 
 template <int MODE, int NREG>
 __global__ __launch_bounds__(512, 1) void hog(const float* in, float* out, int iters) {
-    __shared__ __attribute__((aligned(16))) __bf16 lds[HOG_LDS];
-    if constexpr (NREG == 200) asm volatile("" ::: "v199");
+    constexpr int CVT = MODE >> 2, MF = MODE & 3;
+    __shared__ __attribute__((aligned(16))) unsigned short lds[HOG_LDS];
     if constexpr (NREG == 216) asm volatile("" ::: "v215");
     if constexpr (NREG == 224) asm volatile("" ::: "v223");
     if constexpr (NREG == 232) asm volatile("" ::: "v231");
-    if constexpr (NREG == 240) asm volatile("" ::: "v239");
-    if constexpr (NREG == 248) asm volatile("" ::: "v247");
     if constexpr (NREG == 256) asm volatile("" ::: "v255");
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 31, lh = lane >> 5;
-    for (int i = tid; i < HOG_LDS / 4; i += 512) {
-        const float4 v = *reinterpret_cast<const float4*>(in + 4 * ((blockIdx.x * 997 + i) & 65535));
-        __bf16 h[4], m[4], l[4];
-        split3(v.x, h[0], m[0], l[0]);
-        split3(v.y, h[1], m[1], l[1]);
-        split3(v.z, h[2], m[2], l[2]);
-        split3(v.w, h[3], m[3], l[3]);
-        for (int k = 0; k < 4; ++k) lds[4 * i + k] = (k & 1) ? m[k] : h[k];
+    for (int i = tid; i < HOG_LDS / 2; i += 512) {  // operand images: bf16 / f16 bit patterns of small numbers
+        const float v = in[(blockIdx.x * 997 + i) & 262143];
+        const unsigned u = __float_as_uint(v * 0.125f);
+        lds[2 * i] = (unsigned short)(u >> 16);
+        lds[2 * i + 1] = (unsigned short)(0x3000 | (u & 0x03FF));
     }
     __syncthreads();
     floatx16 acc;
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    float4 hv = *reinterpret_cast<const float4*>(in + 4 * ((blockIdx.x * 512 + tid) & 65535));
-    float keep = 0.f;
+    float2v hv = {in[(blockIdx.x * 512 + tid) & 262143], in[(blockIdx.x * 512 + tid + 7) & 262143]};
+    float2v hw = hv * 0.5f;
     for (int it = 0; it < iters; ++it) {
 #pragma unroll
         for (int t = 0; t < 9; ++t) {
@@ -166,14 +178,14 @@ __global__ __launch_bounds__(512, 1) void hog(const float* in, float* out, int i
             const bf16x8 x0 = *reinterpret_cast<const bf16x8*>(&lds[(base + 40960) & ~7]);
             const bf16x8 x1 = *reinterpret_cast<const bf16x8*>(&lds[(base + 49152) & ~7]);
             const bf16x8 x2 = *reinterpret_cast<const bf16x8*>(&lds[(base + 57344) & ~7]);
-            if constexpr (MODE == 0 || MODE == 1) {
+            if constexpr (MF == 1) {
                 acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w2, x0, acc, 0, 0, 0);
                 acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1, x1, acc, 0, 0, 0);
                 acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w0, x2, acc, 0, 0, 0);
                 acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1, x0, acc, 0, 0, 0);
                 acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w0, x1, acc, 0, 0, 0);
                 acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w0, x0, acc, 0, 0, 0);
-            } else if constexpr (MODE == 2) {
+            } else if constexpr (MF == 2) {
                 const f16x8 a0 = __builtin_bit_cast(f16x8, w0), a1 = __builtin_bit_cast(f16x8, w1);
                 const f16x8 b0 = __builtin_bit_cast(f16x8, x0), b1 = __builtin_bit_cast(f16x8, x1);
                 const f16x8 a2 = __builtin_bit_cast(f16x8, w2), b2 = __builtin_bit_cast(f16x8, x2);
@@ -183,7 +195,7 @@ __global__ __launch_bounds__(512, 1) void hog(const float* in, float* out, int i
                 acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b0, acc, 0, 0, 0);
                 acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b1, acc, 0, 0, 0);
                 acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b0, acc, 0, 0, 0);
-            } else if constexpr (MODE == 3) {
+            } else if constexpr (MF == 3) {
                 const floatx4v p = __builtin_bit_cast(floatx4v, w0), q = __builtin_bit_cast(floatx4v, x0);
                 const floatx4v p1 = __builtin_bit_cast(floatx4v, w1), q1 = __builtin_bit_cast(floatx4v, x1);
 #pragma unroll
@@ -191,30 +203,26 @@ __global__ __launch_bounds__(512, 1) void hog(const float* in, float* out, int i
                     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(p[u], q[u], acc, 0, 0, 0);
                     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(p1[u], q1[u], acc, 0, 0, 0);
                 }
-            } else {  // MODE 4: VALU only
-                const floatx4v p = __builtin_bit_cast(floatx4v, w0 + w1), q = __builtin_bit_cast(floatx4v, x0 + x2);
-#pragma unroll
-                for (int u = 0; u < 4; ++u) acc[(t + u) & 15] += p[u] * q[u] + (float)w2[u];
+            } else {  // no MFMA: keep the LDS reads live
+                const floatx4v p = __builtin_bit_cast(floatx4v, w0) + __builtin_bit_cast(floatx4v, x2);
+                const floatx4v q = __builtin_bit_cast(floatx4v, x0) + __builtin_bit_cast(floatx4v, w2);
+                acc[t] += p[0] * q[1] + __builtin_bit_cast(floatx4v, w1)[2] + __builtin_bit_cast(floatx4v, x1)[3];
             }
-            if constexpr (MODE == 0 || MODE == 4) {  // the conv's per-step split work, interleaved with the MFMAs
-                __bf16 h, m, l;
-                split3(hv.x + (float)t, h, m, l);
-                hv.y += (float)h;
-                hv.z += (float)m;
-                hv.w += (float)l;
-            }
+            // the conv's per-step split work, interleaved with the MFMAs (three pieces of two operands per tap)
+            hv = split2<CVT>(hv + (float)t);
+            hw = split2<CVT>(hw + hv);
+            hv = split2<CVT>(hv - hw);
         }
         __syncthreads();
         if ((it & 1) == 0) {
             const int o = ((it * 131 + tid * 8) & (HOG_LDS / 2 - 1)) & ~7;
-            bf16x8 st;
-            for (int k = 0; k < 8; ++k) st[k] = (__bf16)(acc[k] * 1e-3f);
-            *reinterpret_cast<bf16x8*>(&lds[HOG_LDS / 2 + o]) = st;
+            for (int k = 0; k < 8; ++k) lds[HOG_LDS / 2 + o + k] = (unsigned short)(__float_as_uint(acc[k]) >> 20);
         }
         __syncthreads();
     }
+    float keep = 0.f;
     for (int r = 0; r < 16; ++r) keep += acc[r];
-    out[blockIdx.x * 512 + tid] = keep + hv.x + hv.y + hv.z + hv.w;
+    out[blockIdx.x * 512 + tid] = keep + hv[0] + hv[1] + hw[0] + hw[1];
 }
 
 // ------------------------------------------------------------------------------------------------ host
@@ -237,14 +245,14 @@ struct HogCfg {
     int mode, nreg;
     HogFn fn;
 };
-#define HOGS(M) {M, 0, hog<M, 0>}, {M, 200, hog<M, 200>}, {M, 216, hog<M, 216>}, {M, 224, hog<M, 224>}, \
-                {M, 232, hog<M, 232>}, {M, 240, hog<M, 240>}, {M, 248, hog<M, 248>}, {M, 256, hog<M, 256>}
+#define HOGS(M) {M, 216, hog<M, 216>}, {M, 224, hog<M, 224>}, {M, 232, hog<M, 232>}, {M, 256, hog<M, 256>}
 
-static const char* MODE_NAME[] = {"bf16x6 (cvt+bf16 mfma)", "bf16 mfma", "f16 mfma", "fp32 mfma", "valu splits"};
+static const char* CVT_NAME[] = {"no cvt", "cvt_pk_bf16", "cvt_pk_f16"};
+static const char* MF_NAME[] = {"no mfma", "bf16 mfma", "f16 mfma", "fp32 mfma"};
 static const char* KIND_NAME[] = {"bilinear(pk_f32)", "scalar(v_fma)", "intmix(int)"};
 
 int main(int argc, char** argv) {
-    const int reps = argc > 1 ? atoi(argv[1]) : 3;
+    const int reps = argc > 1 ? atoi(argv[1]) : 10;
     Geo g;
     std::vector<float> hx(g.in_elems());
     std::mt19937 rng(74);
@@ -255,10 +263,10 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&dx, hx.size() * 4));
     for (int k = 0; k < 3; ++k) CK(hipMalloc(&dref[k], g.out_elems() * 4));
     CK(hipMalloc(&dout, g.out_elems() * 4 * NV));
-    CK(hipMalloc(&hin, 65536 * 4 * 4));
+    CK(hipMalloc(&hin, 262144 * 4));
     CK(hipMalloc(&hout, 256 * 512 * 4));
     CK(hipMemcpy(dx, hx.data(), hx.size() * 4, hipMemcpyHostToDevice));
-    CK(hipMemcpy(hin, hx.data(), 65536 * 4 * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(hin, hx.data(), 262144 * 4, hipMemcpyHostToDevice));
     hipStream_t sa, sb;
     CK(hipStreamCreateWithFlags(&sa, hipStreamNonBlocking));
     CK(hipStreamCreateWithFlags(&sb, hipStreamNonBlocking));
@@ -268,82 +276,84 @@ int main(int argc, char** argv) {
         CK(hipStreamSynchronize(sa));
         CK(hipMemcpy(ref[k].data(), dref[k], g.out_elems() * 4, hipMemcpyDeviceToHost));
     }
-    // the bilinear against a host evaluation of the same formula (fp32): sanity of the reference itself
     {
         int bad = 0;
         for (size_t i = 0; i < g.out_elems(); i += 97) {
             const int c = i % g.C, ow = (i / g.C) % g.Wo, oh = (i / g.C / g.Wo) % g.Ho, b = i / g.C / g.Wo / g.Ho;
-            double s = 0;
+            double sm = 0;
             for (int dy = 0; dy < 2; ++dy)
                 for (int dxx = 0; dxx < 2; ++dxx)
-                    s += 0.25 * hx[(((size_t)b * g.Hi + 2 * oh + dy) * g.Wi + 2 * ow + dxx) * g.C + c];
-            bad += std::fabs(s - ref[0][i]) > 1e-6;
+                    sm += 0.25 * hx[(((size_t)b * g.Hi + 2 * oh + dy) * g.Wi + 2 * ow + dxx) * g.C + c];
+            bad += std::fabs(sm - ref[0][i]) > 1e-6;
         }
         printf("reference bilinear vs host formula: %d bad of %zu sampled\n", bad, g.out_elems() / 97);
     }
     std::vector<float> got(g.out_elems() * NV);
-    // the four taps of output i (x1/2: weights 0.25 each)
     auto taps = [&](size_t i, float t[4]) {
         const int c = i % g.C, ow = (i / g.C) % g.Wo, oh = (i / g.C / g.Wo) % g.Ho, b = i / g.C / g.Wo / g.Ho;
         for (int k = 0; k < 4; ++k) t[k] = hx[(((size_t)b * g.Hi + 2 * oh + (k >> 1)) * g.Wi + 2 * ow + (k & 1)) * g.C + c];
     };
-    auto check = [&](int kind, const char* what, bool detail) {
-        CK(hipMemcpy(got.data(), dout, got.size() * 4, hipMemcpyDeviceToHost));
-        size_t bad = 0, badbits = 0;
+    // Error statistics. A thread handles one output pixel's 4 channels (a float4): lane = i % 64 of the row's
+    // 2048 threads, so a 16-lane group (one pass of the 16-wide SIMD over a wave64 instruction) = one pixel's 16
+    // channel groups. An "event" = one (victim launch, row, wave, 16-lane group) with a wrong value.
+    struct Stat {
+        size_t wrong = 0, events = 0, full_groups = 0, reps_hit = 0;
+        size_t comp[4] = {0, 0, 0, 0}, tap[6] = {0, 0, 0, 0, 0, 0};
         double worst = 0;
+    };
+    auto check = [&](int kind, Stat& st, bool show) {
+        CK(hipMemcpy(got.data(), dout, got.size() * 4, hipMemcpyDeviceToHost));
+        const size_t before = st.wrong;
+        std::vector<int> grp;  // wrong lanes per (launch, row, wave, group)
+        long long cur = -1;
+        int cnt = 0;
+        auto flush = [&]() {
+            if (cur >= 0) {
+                st.events++;
+                if (cnt == 16 * 4 || cnt >= 16) st.full_groups += cnt >= 16;
+            }
+        };
         int shown = 0;
-        int tapmatch[6] = {0, 0, 0, 0, 0, 0};  // tap 0..3 dropped/doubled, lane-neighbour value, other
         for (int v = 0; v < NV; ++v)
             for (size_t i = 0; i < g.out_elems(); ++i) {
                 const float a = got[v * g.out_elems() + i], r = ref[kind][i];
                 if (memcmp(&a, &r, 4) == 0) continue;
-                ++bad;
-                const double d = std::fabs((double)a - r);
-                worst = std::max(worst, d);
+                ++st.wrong;
+                st.worst = std::max(st.worst, std::fabs((double)a - r));
+                const int c = i % g.C;
+                const long long pix = (long long)(i / g.C);  // (b, oh, ow) flattened
+                const long long key = (long long)v * (1LL << 40) + pix;  // one pixel = one 16-lane group
+                if (key != cur) {
+                    flush();
+                    cur = key;
+                    cnt = 0;
+                }
+                ++cnt;
+                st.comp[c & 3]++;
                 if (kind == 0) {
                     float t[4];
                     taps(i, t);
                     int m = 5;
                     for (int k = 0; k < 4; ++k)
                         if (std::fabs(std::fabs(a - r) - 0.25f * std::fabs(t[k])) < 1e-6f) m = k;
-                    if (m == 5 && i + 4 < g.out_elems() && std::fabs(a - ref[0][i + 4]) < 1e-7f) m = 4;
-                    tapmatch[m]++;
-                    if (detail && shown < 6) {
-                        const int c = i % g.C, ow = (i / g.C) % g.Wo, oh = (i / g.C / g.Wo) % g.Ho;
-                        printf("      out[%zu] (oh %d ow %d c %d) got %.6f want %.6f; taps %.4f %.4f %.4f %.4f -> %s\n", i,
-                               oh, ow, c, a, r, t[0], t[1], t[2], t[3],
-                               m < 4 ? "err = 0.25 x one tap" : (m == 4 ? "= neighbour pixel's value" : "other"));
+                    st.tap[m]++;
+                    if (show && shown < 4) {
+                        const int ow = (i / g.C) % g.Wo, oh = (i / g.C / g.Wo) % g.Ho;
+                        printf("        launch %d oh %d ow %d (wave lane group %d) c %d: got %.6f want %.6f, err/0.25 = "
+                               "%.4f, taps %.4f %.4f %.4f %.4f\n", v, oh, ow, ow & 3, c, a, r, (a - r) / 0.25f, t[0],
+                               t[1], t[2], t[3]);
                         ++shown;
                     }
-                } else {
-                    unsigned ua, ur;
-                    memcpy(&ua, &a, 4);
-                    memcpy(&ur, &r, 4);
-                    badbits += __builtin_popcount(ua ^ ur);
                 }
             }
-        printf("    %-18s %-44s wrong %8zu of %zu, max |diff| %.3e", KIND_NAME[kind], what, bad, got.size(), worst);
-        if (kind == 0 && bad)
-            printf("  [tap-sized %d/%d/%d/%d, neighbour %d, other %d]", tapmatch[0], tapmatch[1], tapmatch[2], tapmatch[3],
-                   tapmatch[4], tapmatch[5]);
-        if (kind != 0 && bad) printf("  [mean flipped bits %.1f]", (double)badbits / bad);
-        printf("\n");
-        return bad;
+        flush();
+        if (st.wrong > before) st.reps_hit++;
     };
-    // controls: each victim alone at one wave per SIMD (one 256-thread block per CU via 150 KB of dynamic LDS)
-    printf("== controls\n");
-    for (int kind = 0; kind < 3; ++kind) {
-        CK(hipFuncSetAttribute((const void*)(kind == 0 ? (const void*)victim<0> : kind == 1 ? (const void*)victim<1> : (const void*)victim<2>),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024));
-        for (int v = 0; v < NV; ++v) launch_victim(kind, dx, dout + v * g.out_elems(), g, sa, 150 * 1024);
-        CK(hipStreamSynchronize(sa));
-        check(kind, "alone, 1 wave/SIMD", true);
-    }
-    HogCfg cfgs[] = {HOGS(0), HOGS(1), HOGS(2), HOGS(3), HOGS(4)};
+    HogCfg cfgs[] = {HOGS(5), HOGS(1), HOGS(4), HOGS(10), HOGS(2), HOGS(8), HOGS(7), HOGS(6), HOGS(9), HOGS(0)};
+    // size the hog to ~4 ms
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    // size the hog to ~4 ms
     int iters = 400;
     {
         hipLaunchKernelGGL(cfgs[0].fn, dim3(256), dim3(512), 0, sa, hin, hout, iters);
@@ -354,32 +364,29 @@ int main(int argc, char** argv) {
         float ms = 0;
         CK(hipEventElapsedTime(&ms, e0, e1));
         iters = std::max(50, (int)(iters * 4.0f / std::max(ms, 0.01f)));
-        printf("hog bf16x6 %d iters -> %.3f ms; using %d iters\n", 400, ms, iters);
+        printf("hog mode 5 %d iters -> %.3f ms; using %d iters, %d reps x %d victim launches per config\n", 400, ms,
+               iters, reps, NV);
     }
     for (const HogCfg& h : cfgs) {
         hipFuncAttributes fa;
         CK(hipFuncGetAttributes(&fa, (const void*)h.fn));
-        printf("== hog mode %d %-24s nreg %3d (numRegs %d, LDS %zu B)\n", h.mode, MODE_NAME[h.mode], h.nreg, fa.numRegs,
-               fa.sharedSizeBytes);
+        printf("== hog %-12s + %-10s nreg %3d (numRegs %d)\n", CVT_NAME[h.mode >> 2], MF_NAME[h.mode & 3], h.nreg,
+               fa.numRegs);
         for (int kind = 0; kind < 3; ++kind) {
-            size_t bad = 0;
+            Stat st;
             for (int r = 0; r < reps; ++r) {
                 CK(hipMemset(dout, 0, g.out_elems() * 4 * NV));
                 CK(hipDeviceSynchronize());
                 hipLaunchKernelGGL(h.fn, dim3(256), dim3(512), 0, sa, hin, hout, iters);
                 for (int v = 0; v < NV; ++v) launch_victim(kind, dx, dout + v * g.out_elems(), g, sb, 0);
                 CK(hipDeviceSynchronize());
-                char what[96];
-                snprintf(what, sizeof what, "beside the hog (rep %d)", r);
-                bad += check(kind, what, r == 0);
+                check(kind, st, st.wrong == 0);
             }
-            if (bad && (h.nreg == 224 || h.nreg == 0)) {  // control: the same pair on ONE stream (serialised)
-                CK(hipMemset(dout, 0, g.out_elems() * 4 * NV));
-                hipLaunchKernelGGL(h.fn, dim3(256), dim3(512), 0, sa, hin, hout, iters);
-                for (int v = 0; v < NV; ++v) launch_victim(kind, dx, dout + v * g.out_elems(), g, sa, 0);
-                CK(hipDeviceSynchronize());
-                check(kind, "after the hog, same stream", false);
-            }
+            printf("    %-18s reps hit %2zu/%d  wrong %7zu  events %4zu (full 16-lane %4zu)  comp x/y/z/w %zu/%zu/%zu/%zu", KIND_NAME[kind],
+                   st.reps_hit, reps, st.wrong, st.events, st.full_groups, st.comp[0], st.comp[1], st.comp[2], st.comp[3]);
+            if (kind == 0 && st.wrong)
+                printf("  taps a/q/r/d %zu/%zu/%zu/%zu other %zu", st.tap[0], st.tap[1], st.tap[2], st.tap[3], st.tap[5]);
+            printf("  max %.2e\n", st.worst);
         }
         fflush(stdout);
     }

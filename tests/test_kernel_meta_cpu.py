@@ -33,11 +33,25 @@ def _find(meta, fragment):
 
 
 def test_wres_bf6_takes_the_whole_vgpr_file(meta):
-    (k,) = _find(meta, "conv3x3_wres_bf6_kernel")
+    (k,) = _find(meta, "conv3x3_wres_bf6_kernelILb1E")  # GUARD = true: the instantiation every default launch uses
     r = kernel_meta.residency(k)
     assert k["threads"] == 512 and k["alloc"] == 256, k
     assert r["waves_per_simd"] == 2 and r["hole_vgprs"] == 0, r
     assert k["scratch"] == 0
+    # the diagnostic instantiation (hyres_conv_tuning key 9 = 0) keeps the allocation that showed the interference
+    (d,) = _find(meta, "conv3x3_wres_bf6_kernelILb0E")
+    assert d["alloc"] == 224 and kernel_meta.residency(d)["hole_vgprs"] == 64, d
+
+
+def test_other_cvt_mfma_persistent_kernels_take_the_whole_vgpr_file(meta):
+    """ru_fused_f16_kernel beside a side-stream bilinear showed the same interference in its 232-VGPR build (round 5,
+    scripts/bf6_interference_repro.hip ru); it and every weight-resident f16 3x3 now leave no hole."""
+    (k,) = _find(meta, "ru_fused_f16_kernelILb1E")
+    assert k["alloc"] == 256 and kernel_meta.residency(k)["hole_vgprs"] == 0, k
+    (d,) = _find(meta, "ru_fused_f16_kernelILb0E")  # diagnostic build
+    assert d["alloc"] == 232, d
+    for k in _find(meta, "conv3x3_wres_f16_kernel"):
+        assert k["alloc"] == 256 and kernel_meta.residency(k)["hole_vgprs"] == 0, k
 
 
 def test_no_default_path_kernel_uses_scratch(meta):

@@ -993,6 +993,68 @@ def test_captured_train_step_matches_eager():
     assert l1 != l2 and abs(l1 - l2) < 0.05 * abs(l1)
 
 
+def test_captured_step_survives_eager_step_with_new_layouts_and_bigger_workspace():
+    """Regression (round 4, commit 5e08bd4): an eager step between two replays that registers NEW weight layouts
+    (rebuilding the batched re-layout's descriptor table) and GROWS a workspace slot (replacing its buffer) must not
+    free what the graph recorded: the graph's weight_prep_batch_kernel read the freed descriptor table (illegal
+    address) before CapturedStep kept both alive. Capture at bs 2 64x64; eager step at bs 4 128x128; replay; the
+    replay's loss and every parameter gradient equal a fresh eager step's, bit for bit (src/utils/engine.py:33,50-53
+    mixes eager and graphed steps the same way)."""
+    from hyres_hip import ops as O
+    from hyres_hip.graphs import CapturedStep
+    from hyres_hip.loss import RateDistortionLoss
+    g = load_npz("hyres_train_b2_64.npz")
+    net, _ = _hip_model()
+    net.train()
+    D = dev()
+    x, j = g["x"].to(D), g["jpeg_decoded"].to(D)
+    rm = net.residual_model
+    injected = {"z": g["noise_z"].permute(0, 2, 3, 1).contiguous().to(D),
+                "y": g["noise_y"].permute(0, 2, 3, 1).contiguous().to(D)}
+    crit = RateDistortionLoss(lmbda=0.045, alpha=0)
+    params = [p for p in net.parameters() if p.requires_grad]
+
+    def zero():
+        for p in params:
+            if p.grad is not None:
+                p.grad.zero_()
+
+    rm.noise.injected = injected
+    zero()
+    cap = CapturedStep(net, x, j, 0.25, criterion=crit, zero_grad=zero)
+    st = O.PrepBatch._state[D.index]
+    n_entries, table_ptr = len(st["entries"]), st["table"].data_ptr()
+    ws_before = {k: (b.data_ptr(), b.numel()) for k, b in O.Workspace._bufs.items()}
+    # the eager step in between: a bigger geometry -> new layouts (e.g. other conv routes) and bigger scratch
+    rm.noise.injected = None
+    gen = torch.Generator().manual_seed(11)
+    xb = torch.rand((4, 3, 128, 128), generator=gen).to(D)
+    jb = (xb + 0.02 * torch.randn((4, 3, 128, 128), generator=gen).to(D)).clamp(0, 1)
+    crit(net.forward_device(xb, jb, 0.3), xb)["loss"].backward()
+    O.PrepBatch.prepare(D)  # what the next capture / batch run would do: rebuild the table from the new entries
+    torch.cuda.synchronize()
+    grew = [k for k, b in O.Workspace._bufs.items() if k not in ws_before or ws_before[k][1] < b.numel()]
+    assert len(st["entries"]) > n_entries and st["table"].data_ptr() != table_ptr, "no new layout registered"
+    assert grew, "no workspace slot grew"
+    del xb, jb
+    torch.cuda.empty_cache()  # hand the replaced buffers back to the device: a dangling read would now fault
+    rm.noise.injected = injected
+    zero()
+    _, cc = cap.replay()
+    torch.cuda.synchronize()
+    loss_r = float(cc["loss"])
+    grads_r = [p.grad.detach().clone() for p in params]
+    zero()
+    c = crit(net.forward_device(x, j, 0.25), x)
+    c["loss"].backward()
+    torch.cuda.synchronize()
+    assert float(c["loss"]) == loss_r
+    for p, gr in zip(params, grads_r):
+        assert torch.equal(p.grad, gr), p.shape
+    rm.noise.injected = None
+    cap.close()
+
+
 def test_overlapped_rccl_reducer_single_rank():
     """The RCCL path of hyres_hip.ddp.FlatGradReducer with backward-overlapped segments, on a one-rank
     nccl (= RCCL) group: markers fire during the real model's tape backward, collectives are enqueued
