@@ -578,12 +578,12 @@ def main():
     # xGMI). HYRES_DIST_MODE=eager-overlap (or --no-graph) selects the eager overlapped path.
     dist_mode = None
     if dist:
-        # default "graph+allreduce": replay, then the flat gradient in 32 MB buckets. "graph+overlap"
-        # (HYRES_DIST_MODE) starts each segment's all-reduce from an external event the replay records at its
-        # backward-progress marker (ddp.FlatGradReducer.reduce_graphed) — opt-in only: its one multi-rank
-        # rehearsal ran 9x slower than graph+allreduce; eager-overlap = the eager step
+        # default "graph+allreduce": replay, then the flat gradient in 32 MB buckets; "eager-overlap": the eager
+        # step with each gradient segment's all-reduce started at its backward-progress marker. (The round-3/4
+        # "graph+overlap" mode — collectives started from events recorded inside the replay — was removed in
+        # round 5: it needs more live streams than the 4 hardware queues per process)
         dist_mode = "eager-overlap" if args.no_graph else os.environ.get("HYRES_DIST_MODE", "graph+allreduce")
-        assert dist_mode in ("eager-overlap", "graph+overlap", "graph+allreduce"), dist_mode
+        assert dist_mode in ("eager-overlap", "graph+allreduce"), dist_mode
     if dist:
         # RCCL all-reduce of refine / g_s / hyperprior gradient segments launched from backward-progress
         # markers (overlapped with the rest of backward), the remainder (g_a) after backward
@@ -608,8 +608,7 @@ def main():
         # the RCCL all-reduce and the aux step stay eager (a handful of launches)
         from hyres_hip.graphs import CapturedStep
         graphed = CapturedStep(net, x, jpeg, jpeg_bpp, noisequant=False, criterion=crit, zero_grad=opt.zero_grad,
-                               capture_error_mode="thread_local" if dist else "global",
-                               reducer=reducer if dist_mode == "graph+overlap" else None)
+                               capture_error_mode="thread_local" if dist else "global")
 
     def fwd_bwd(eager=False, gr=None):
         gr = gr or graphed
@@ -623,10 +622,7 @@ def main():
     def step(eager=False, gr=None):
         c = fwd_bwd(eager, gr)
         if reducer is not None:
-            if graphed is not None and not eager:
-                reducer.reduce_graphed(graphed.marker_events)  # empty list -> after-replay buckets
-            else:
-                reducer.all_reduce()
+            reducer.all_reduce()
         opt.step()
         opt.zero_grad()
         aux = net.aux_loss()

@@ -495,57 +495,6 @@ extern "C" {
 int hyres_version(void) { return 10000; }
 const char* hyres_last_error_string(void) { return g_err.c_str(); }
 
-int hyres_event_create(void** ev) {
-    HY_REQUIRE(ev, HYRES_E_ARG, "event_create: NULL");
-    hipEvent_t e = nullptr;
-    hipError_t err = hipEventCreateWithFlags(&e, hipEventDisableTiming);
-    HY_REQUIRE(err == hipSuccess, (int)err, "hipEventCreateWithFlags: %s", hipGetErrorString(err));
-    *ev = (void*)e;
-    return 0;
-}
-int hyres_event_destroy(void* ev) {
-    HY_REQUIRE(ev, HYRES_E_ARG, "event_destroy: NULL");
-    hipError_t err = hipEventDestroy((hipEvent_t)ev);
-    HY_REQUIRE(err == hipSuccess, (int)err, "hipEventDestroy: %s", hipGetErrorString(err));
-    return 0;
-}
-int hyres_event_record_external(void* ev, hyres_stream_t s) {
-    HY_REQUIRE(ev, HYRES_E_ARG, "event_record_external: NULL");
-    hipStream_t st = as_stream(s);
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    unsigned long long id = 0;
-    hipGraph_t graph = nullptr;
-    const hipGraphNode_t* deps = nullptr;
-    size_t ndeps = 0;
-    hipError_t err = hipStreamGetCaptureInfo_v2(st, &cs, &id, &graph, &deps, &ndeps);
-    if (err != hipSuccess) {
-        (void)hipGetLastError();  // never leave a sticky error behind for the caller's runtime
-        return ::hyres::set_error((int)err, "hipStreamGetCaptureInfo_v2: %s", hipGetErrorString(err));
-    }
-    if (cs != hipStreamCaptureStatusActive) {
-        err = hipEventRecord((hipEvent_t)ev, st);
-    } else {
-        // hipEventRecordWithFlags(hipEventRecordExternal) is refused inside a capture on this runtime, so the
-        // event-record node is added to the captured graph by hand, after the stream's current frontier, and
-        // becomes the stream's new frontier (the captured work that follows is ordered after it)
-        hipGraphNode_t node = nullptr;
-        err = hipGraphAddEventRecordNode(&node, graph, deps, ndeps, (hipEvent_t)ev);
-        if (err == hipSuccess)
-            err = hipStreamUpdateCaptureDependencies(st, &node, 1, hipStreamSetCaptureDependencies);
-    }
-    if (err != hipSuccess) {
-        (void)hipGetLastError();
-        return ::hyres::set_error((int)err, "event record (capture %d): %s", (int)cs, hipGetErrorString(err));
-    }
-    return 0;
-}
-int hyres_stream_wait_event(hyres_stream_t s, void* ev) {
-    HY_REQUIRE(ev, HYRES_E_ARG, "stream_wait_event: NULL");
-    hipError_t err = hipStreamWaitEvent(as_stream(s), (hipEvent_t)ev, 0);
-    HY_REQUIRE(err == hipSuccess, (int)err, "hipStreamWaitEvent: %s", hipGetErrorString(err));
-    return 0;
-}
-
 int hyres_nchw_to_nhwc(const float* x, float* y, int B, int C, int H, int W, int ldy, hyres_stream_t s) {
     HY_REQUIRE(x && y && ldy >= C, HYRES_E_ARG, "nchw_to_nhwc: bad args");
     long long n = (long long)B * C * H * W;

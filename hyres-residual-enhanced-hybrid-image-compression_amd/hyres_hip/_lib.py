@@ -77,10 +77,6 @@ _PP = ctypes.POINTER(ctypes.c_void_p)
 _SIGS = {
     "hyres_version": (_I, []),
     "hyres_last_error_string": (ctypes.c_char_p, []),
-    "hyres_event_create": (_I, [ctypes.POINTER(ctypes.c_void_p)]),
-    "hyres_event_destroy": (_I, [_P]),
-    "hyres_event_record_external": (_I, [_P, _P]),
-    "hyres_stream_wait_event": (_I, [_P, _P]),
     "hyres_geom_conv2d": (_I, [ctypes.POINTER(ConvGeom)] + [_I] * 12),
     "hyres_geom_conv2d_dgrad": (_I, [ctypes.POINTER(ConvGeom)] + [_I] * 12),
     "hyres_geom_deconv2d": (_I, [ctypes.POINTER(ConvGeom)] + [_I] * 9),

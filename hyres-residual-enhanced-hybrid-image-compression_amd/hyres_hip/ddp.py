@@ -48,12 +48,12 @@ def _merge(ranges):
 class FlatGradReducer:
     """All-reduce (mean) of the flat gradient buffer.
 
-    Without ``names``/``segments``: after backward, in ``bucket_bytes`` buckets. With them, a segment's
-    buckets are launched as soon as its backward-progress marker fires (``on_marker``, registered as a
-    hyres_hip.ops.GradReady listener by ``overlap()``): the RCCL collective is enqueued behind the
-    side stream that carries the weight gradients, so it runs while the rest of backward computes.
-    ``all_reduce()`` then reduces whatever no marker covered, waits for every collective and scales by
-    1/world."""
+    Without ``names``/``segments``, or after a graph replay: after backward, in ``bucket_bytes`` buckets (the
+    default data-parallel step). With them and an EAGER backward (``overlap()``), a segment's
+    buckets are launched as soon as its backward-progress marker fires (``on_marker``, a hyres_hip.ops.GradReady
+    listener): the RCCL collective is enqueued behind the side stream that carries the weight gradients, so it
+    runs while the rest of backward computes. ``all_reduce()`` then reduces whatever no marker covered, waits for
+    every collective and scales by 1/world."""
 
     def __init__(self, flat, world_size: int, bucket_bytes: int = 32 << 20, group=None, names=None,
                  segments=None):
@@ -88,7 +88,6 @@ class FlatGradReducer:
         self.fired = []
         self.works = []
         self.armed = True  # gradient accumulation: markers fire only on the boundary micro-batch
-        self._comm = None  # stream the graph-triggered collectives are enqueued from (reduce_graphed)
 
     def overlap(self):
         """Register ``on_marker`` as a GradReady listener (eager backward)."""
@@ -135,48 +134,6 @@ class FlatGradReducer:
         self.works = []
         self.fired = []
         self._scale(self.flat.grad)
-
-    def reduce_graphed(self, marker_events) -> None:
-        """All-reduce after a replay of a graph captured with ``CapturedStep(..., reducer=self)``,
-        overlapped with the replay's backward.
-
-        ``marker_events``: [(segment name, external event)] recorded INSIDE the graph where that segment's
-        gradients became final (hipEventRecordWithFlags(hipEventRecordExternal) nodes).  The host runs
-        this right after ``graph.replay()``: a communication stream waits for each marker's event and
-        enqueues that segment's collectives, so they start while the rest of the replayed backward still
-        computes (no collective is inside the graph: RCCL runs eagerly, only its start is ordered by the
-        graph); the segments no marker covers (g_a) follow the end of the replay, then one 1/world scale.
-        Every rank issues the same collectives in the same order (the marker list is fixed by the
-        capture), as RCCL requires."""
-        g = self.flat.grad
-        if not g.is_cuda or not marker_events:
-            self.all_reduce()
-            return
-        main = torch.cuda.current_stream(g.device)
-        if self._comm is None:
-            self._comm = torch.cuda.Stream(device=g.device)
-        comm = self._comm
-        done = set()
-        with torch.cuda.stream(comm):
-            for name, ev in marker_events:
-                ranges = self.segments.get(name)
-                if not ranges or name in done:
-                    continue
-                done.add(name)
-                ev.wait(comm)  # hyres_hip.graphs.GraphEvent: recorded inside this replay
-                self._launch(ranges)
-            comm.wait_stream(main)  # end of the replay: the remaining segments' gradients are final
-            ranges = list(self.rest)
-            for mk, rs in self.segments.items():
-                if mk not in done:
-                    ranges.extend(rs)
-            self._launch(ranges)
-        for w in self.works:
-            w.wait()  # current (main) stream waits for every collective
-        main.wait_stream(comm)
-        self.works = []
-        self.fired = []
-        self._scale(g)
 
     def _scale(self, g: torch.Tensor):
         if self.world == 1:

@@ -12,12 +12,8 @@ What is captured and what stays eager:
     libhyres_hip launch of the reference's forward/backward (models/hyres.py:23-77,
     src/utils/engine.py:33-55);
   * eager: the optimiser (FusedAdam's bias correction reads the host step count), the RCCL gradient
-    all-reduce and the aux (quantiles) step — 3-10 launches per step.  With ``reducer=`` the capture
-    records an EXTERNAL event (hipEventRecordExternal) at every backward-progress marker
-    (hyres_hip.ops.GradReady: refine, g_s, hyperprior group complete); after ``replay()`` the host
-    enqueues each segment's RCCL all-reduce on a communication stream that waits on that event
-    (``FlatGradReducer.reduce_graphed``), so the collectives overlap the rest of the replayed backward
-    while the graph itself holds no collective.
+    all-reduce (after the replay, hyres_hip.ddp.FlatGradReducer.all_reduce) and the aux (quantiles) step —
+    3-10 launches per step. The graph holds no collective.
 Graph-safety of the captured region:
   * weights: the conv weight re-layout cache (hyres_hip.ops._prepped) is invalidated before capture so
     every re-layout kernel is recorded and re-runs on each replay (weights change every optimiser step),
@@ -30,39 +26,11 @@ Graph-safety of the captured region:
 from __future__ import annotations
 
 import contextlib
-import ctypes
 from typing import Callable, Optional
 
 import torch
 
 from . import ops as O
-
-
-class GraphEvent:
-    """A HIP event recorded as an EXTERNAL node of a graph being captured (torch refuses
-    ``Event(external=True)`` on ROCm, so the C-ABI makes the hipEventRecordWithFlags call): every replay
-    records it when the captured work before it has finished, and ``wait(stream)`` — issued by the host
-    after ``replay()`` — orders that stream's later work after this replay's record."""
-
-    def __init__(self):
-        from . import _lib as L
-        self._L = L
-        h = ctypes.c_void_p()
-        L.call("hyres_event_create", ctypes.byref(h))
-        self.handle = h
-
-    def record(self, stream: torch.cuda.Stream) -> None:
-        self._L.call("hyres_event_record_external", self.handle, ctypes.c_void_p(stream.cuda_stream))
-
-    def wait(self, stream: torch.cuda.Stream) -> None:
-        self._L.call("hyres_stream_wait_event", ctypes.c_void_p(stream.cuda_stream), self.handle)
-
-    def __del__(self):
-        try:
-            if self.handle:
-                self._L.load().hyres_event_destroy(self.handle)
-        except Exception:  # noqa: BLE001 - interpreter shutdown
-            pass
 
 
 def _prepare_noise(net: torch.nn.Module, device: torch.device) -> None:
@@ -85,7 +53,7 @@ class CapturedStep:
                  noisequant: bool = False, criterion: Optional[Callable] = None,
                  zero_grad: Optional[Callable[[], None]] = None, warmup: int = 2,
                  capture_error_mode: str = "global", amp: bool = False,
-                 loss_scale: Optional[torch.Tensor] = None, reducer=None):
+                 loss_scale: Optional[torch.Tensor] = None):
         assert x.is_cuda, "CapturedStep needs device tensors"
         self.net = net
         self.train = criterion is not None
@@ -132,32 +100,8 @@ class CapturedStep:
         self._prep_table = O.PrepBatch.table(dev)
         # "thread_local" when an RCCL process group exists: its watchdog thread polls events while the
         # main thread captures (no collective is ever inside the graph)
-        cap_stream = None
-        # external events at the backward-progress markers (training + a reducer with segments only)
-        self.marker_events = []
-        listener = None
-        if reducer is not None and self.train and getattr(reducer, "segments", None):
-            def listener(name):
-                if name not in reducer.segments or any(n == name for n, _ in self.marker_events):
-                    return
-                ev = GraphEvent()
-                cur = torch.cuda.current_stream(dev)
-                if O.SideStream.used:  # weight gradients on side streams: record once they are complete too
-                    sides = O.SideStream.all(dev)
-                    sides[0].wait_stream(cur)
-                    for o in sides[1:]:
-                        sides[0].wait_stream(o)
-                    ev.record(sides[0])  # the side stream rejoins at the end of the tape backward
-                else:
-                    ev.record(cur)
-                self.marker_events.append((name, ev))
-            O.GradReady.listeners.append(listener)
-        try:
-            with torch.cuda.graph(self.graph, stream=cap_stream, capture_error_mode=capture_error_mode):
-                self.out, self.crit = run()
-        finally:
-            if listener is not None:
-                O.GradReady.listeners.remove(listener)
+        with torch.cuda.graph(self.graph, capture_error_mode=capture_error_mode):
+            self.out, self.crit = run()
         O.bump_weight_epoch()  # eager calls must not reuse buffers only the graph writes
         # ... and the scratch buffers its kernels were recorded with: an eager call that grows a workspace slot
         # replaces the slot's tensor, and the old one must outlive the graph
@@ -165,14 +109,12 @@ class CapturedStep:
         torch.cuda.synchronize(dev)
 
     def close(self) -> None:
-        """Tear down in the only safe order: wait for any replay in flight, destroy the graph (its event-record
-        nodes point at the marker events), THEN release the marker events."""
+        """Wait for any replay in flight, then destroy the graph and release what it recorded."""
         g = getattr(self, "graph", None)
         if g is not None:
             torch.cuda.synchronize(self.x.device)
             g.reset()
             self.graph = None
-        self.marker_events = []
         self._prep_table = None
         self._ws_keep = []
 

@@ -17,9 +17,9 @@ Differences from the reference, by design:
     (TurboJPEGCompression.prefetch), so the host JPEG stage overlaps the device step;
   * forward + RD loss + backward replay as a HIP graph (hyres_hip.graphs.CapturedStep, one capture per
     batch shape / noisequant / precision, taken on an accumulation boundary); the host JPEG stage, the
-    H2D copies, the gradient all-reduce (after the replay in 32 MB buckets, as bench.py's N > 1 default;
-    HYRES_DIST_MODE=graph+overlap starts each segment from an event the replay records at its
-    backward-progress marker), the optimiser and the aux step stay eager. Every step the ranks agree over a
+    H2D copies, the gradient all-reduce (after the replay in 32 MB buckets, as bench.py's N > 1 default),
+    the optimiser and the aux step stay eager; with HYRES_TRAIN_GRAPH=0 the eager backward overlaps the
+    all-reduce segment by segment. Every step the ranks agree over a
     host (gloo) group on the capture key and on capture success, so all ranks replay or all run eagerly and
     issue the same collectives. HYRES_TRAIN_GRAPH=0 runs every step eagerly (the reference's structure);
   * under DDP the test epoch is sharded (rank r takes images r, r + world, ...) and the meters' sums and
@@ -67,7 +67,6 @@ class _GraphedStep:
         # loss multiplier inside the graph: 1/accumulation (x the GradScaler's device scale under AMP)
         self.ls = torch.full((1,), 1.0 / accumulation, dtype=torch.float32, device=device)
         self.enabled = os.environ.get("HYRES_TRAIN_GRAPH", "1") == "1" and device.type == "cuda"
-        self.overlap = os.environ.get("HYRES_DIST_MODE", "graph+allreduce") == "graph+overlap"
         self.last = None
         self._host_group = host_group()
 
@@ -110,8 +109,7 @@ class _GraphedStep:
             try:
                 cap = CapturedStep(self.model, x, jd, float(bpp), noisequant=noisequant, criterion=self.criterion,
                                    zero_grad=self.zero_grad, amp=self.amp, loss_scale=self.ls,
-                                   capture_error_mode="thread_local" if reducer is not None else "global",
-                                   reducer=reducer if self.overlap else None)
+                                   capture_error_mode="thread_local" if reducer is not None else "global")
             except Exception as exc:  # noqa: BLE001 - any capture failure: stay correct, run eagerly
                 err = exc
             finally:
@@ -136,10 +134,8 @@ class _GraphedStep:
         self.last = None
 
     def reduce(self, reducer):
-        """The boundary all-reduce after a replayed step (graph+overlap: each segment's collectives start on
-        the external event the capture recorded at its backward-progress marker; otherwise no events were
-        recorded and the flat gradient is reduced after the replay in buckets)."""
-        reducer.reduce_graphed(self.last.marker_events)
+        """The boundary all-reduce after a replayed step: the flat gradient in buckets, after the replay."""
+        reducer.all_reduce()
 
 
 _HOST_GROUP = [None, None]  # (default process group it was made for, the gloo group)

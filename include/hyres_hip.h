@@ -34,17 +34,6 @@ typedef void* hyres_stream_t; /* hipStream_t */
 int hyres_version(void);
 const char* hyres_last_error_string(void);
 
-/* Graph-ordered events for the data-parallel gradient path (replaces the reference's nn.DataParallel
- * gradient gather, src/training.py:211-212).  The only runtime objects the library creates: an event
- * recorded with hipEventRecordExternal while a stream is being captured becomes an event-record NODE of
- * the graph, so each replay records it when the backward reaches that point; a stream outside the graph
- * waits on it (hyres_stream_wait_event) and starts that gradient segment's RCCL all-reduce while the rest
- * of the replay computes (hyres_hip/ddp.py reduce_graphed).  Outside capture the record is a plain
- * hipEventRecord. */
-int hyres_event_create(void** ev);                               /* hipEventDisableTiming */
-int hyres_event_destroy(void* ev);
-int hyres_event_record_external(void* ev, hyres_stream_t s);
-int hyres_stream_wait_event(hyres_stream_t s, void* ev);
 
 /* ------------------------------------------------------------------------------------------ */
 /* convolution geometry (implicit GEMM, NHWC).                                                */

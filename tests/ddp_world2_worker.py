@@ -1,15 +1,14 @@
 """Worker for tests/test_ddp_gpu.py: the HIP-path data-parallel step (configs[3] / SURVEY §8e, replacing the
 reference's nn.DataParallel, src/training.py:211-212) on WORLD_SIZE ranks that share device 0 over gloo
 (RCCL refuses two ranks on one device; gloo all-reduces CUDA tensors through the host with the same stream
-ordering, so the graph-triggered overlap path runs unchanged).
+ordering, so the after-replay reduction runs unchanged).
 
 Launched by ``python -m torch.distributed.run --nproc-per-node 2 … tests/ddp_world2_worker.py OUT``, before
 the launching test touches anything but its own process.  Each rank:
-  1. captures the train step (forward + RD loss + tape backward) as a HIP graph with the reducer's
-     backward-progress markers recorded as external events (``CapturedStep(reducer=…)``);
+  1. captures the train step (forward + RD loss + tape backward) as a HIP graph (``CapturedStep``);
   2. replays it on its half of a bs=4 64² batch (STE quantisation, injected EntropyBottleneck noise) and
-     all-reduces with ``FlatGradReducer.reduce_graphed`` (segments start on the markers' events);
-  3. replays again and reduces after the replay (``all_reduce``): must equal (2) bit for bit;
+     all-reduces the flat gradient after the replay (``FlatGradReducer.all_reduce``, bench.py's N > 1 mode);
+  3. replays and reduces again: must equal (2) bit for bit (run-to-run determinism of the DDP step);
   4. takes one FusedAdam(clip 1.0) step; rank 0 then broadcasts its parameters, every rank checks equality;
 Rank 0 finally re-runs each rank's shard single-process (their mean must equal the reduced gradient bit for
 bit) and the whole bs=4 batch (fresh models, same weights), and saves the flat gradients + losses to OUT.
@@ -71,15 +70,13 @@ def main():
 
     red = FlatGradReducer(opt.flat, world, names=names, segments=HYRES_SEGMENTS)
     cap = CapturedStep(net, x, j, float(bpp), criterion=crit, zero_grad=opt.zero_grad,
-                       capture_error_mode="thread_local", reducer=red)
-    markers = [n for n, _ in cap.marker_events]
-    assert markers == ["refine", "g_s", "hyper"], markers
+                       capture_error_mode="thread_local")
 
     opt.zero_grad()
     _, c = cap.replay()
-    red.reduce_graphed(cap.marker_events)
+    red.all_reduce()
     torch.cuda.synchronize()
-    g_overlap = opt.flat.grad.clone()
+    g_ddp = opt.flat.grad.clone()
     loss = c["loss"].detach().clone()
     dist.all_reduce(loss)
     loss_mean = float(loss) / world
@@ -88,7 +85,7 @@ def main():
     cap.replay()
     red.all_reduce()
     torch.cuda.synchronize()
-    same_after = bool(torch.equal(opt.flat.grad, g_overlap))
+    same_after = bool(torch.equal(opt.flat.grad, g_ddp))
 
     opt.step()
     torch.cuda.synchronize()
@@ -124,7 +121,7 @@ def main():
         g_all, loss_all = single(slice(0, x_all.shape[0]))
         offs = np.array(opt.flat.offsets, dtype=np.int64)
         sizes = np.array([p.numel() for p in opt.flat.params], dtype=np.int64)
-        np.savez(out_path, g_ddp=g_overlap.cpu().numpy(), g_mean=g_mean.cpu().numpy(),
+        np.savez(out_path, g_ddp=g_ddp.cpu().numpy(), g_mean=g_mean.cpu().numpy(),
                  g_single=g_all.cpu().numpy(), loss_ddp=np.float64(loss_mean), loss_single=np.float64(loss_all),
                  same_after=np.bool_(same_after), params_equal=np.bool_(params_equal_all),
                  offsets=offs, sizes=sizes, names=np.array(names))

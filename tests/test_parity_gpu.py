@@ -1097,13 +1097,10 @@ def test_overlapped_rccl_reducer_single_rank():
         tdist.destroy_process_group()
 
 
-@pytest.mark.parametrize("overlap", [False, True])
-def test_captured_step_with_rccl_group_single_rank(overlap):
+def test_captured_step_with_rccl_group_single_rank():
     """The N > 1 bench path: the train step captured (capture_error_mode thread_local) while an RCCL
-    process group is live, replayed, then the flat gradients all-reduced — after the replay in buckets, or
-    (overlap, the default N > 1 mode) segment by segment from the external events the capture recorded at
-    the backward-progress markers (``FlatGradReducer.reduce_graphed``); the reduced gradients equal the
-    eager step's."""
+    process group is live, replayed, then the flat gradients all-reduced after the replay in buckets; the
+    reduced gradients equal the eager step's."""
     import os
     import socket
     import torch.distributed as tdist
@@ -1135,15 +1132,11 @@ def test_captured_step_with_rccl_group_single_rank(overlap):
         red.all_reduce()  # a completed collective before the capture (the watchdog has work to poll)
         opt.zero_grad()
         cap = CapturedStep(net, x, j, 0.0, criterion=crit, zero_grad=opt.zero_grad,
-                           capture_error_mode="thread_local", reducer=red if overlap else None)
-        assert [n for n, _ in cap.marker_events] == (["refine", "g_s", "hyper"] if overlap else [])
+                           capture_error_mode="thread_local")
         for _ in range(2):
             opt.zero_grad()
             cap.replay()
-            if overlap:
-                red.reduce_graphed(cap.marker_events)
-            else:
-                red.all_reduce()
+            red.all_reduce()
             torch.cuda.synchronize()
             assert red.fired == []
             assert torch.equal(opt.flat.grad, ref)
