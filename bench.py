@@ -92,8 +92,20 @@ def cpu_baseline(args, budget_s):
             torch.backends.mkldnn.enabled = prev
         t = min(times[1:]) if len(times) > 1 else times[0]
         res[tag] = {"value": round(B * S * S / t / 1e6, 4), "steps": len(times)}
+    # configs[0] (C1): the reference's CPU forward only, one 256x256 image, eval (models/hyres.py:23-77)
+    x1, j1 = x[:1], jpeg[:1]
+    c1 = []
+    with torch.no_grad():
+        for _ in range(4):
+            t0 = time.time()
+            orc.forward(x1, j1, jpeg_bpp, training=False)
+            c1.append(time.time() - t0)
+    t1 = min(c1[1:])
     return {"value": res["mkldnn_on"]["value"], "unit": "Mpixels/s", "cores": threads, "kind": "port",
             "value_mkldnn_off": res["mkldnn_off"]["value"],
+            "c1_eval_forward": {"ms": round(1000 * t1, 1), "mpix_s": round(S * S / t1 / 1e6, 4),
+                                "sample": f"configs[0]: oracle eval forward, 1x3x{S}x{S}, min over 3 runs after one "
+                                          f"warm-up, {threads} threads"},
             "sample": f"oracle (torch-CPU fp32 port of the reference math) train step (fwd+RD loss+bwd) at batch "
                       f"{B}x{S}x{S} on the JPEG stage's output, min over {res['mkldnn_on']['steps']} / "
                       f"{res['mkldnn_off']['steps']} steps with mkldnn on / off, {threads} threads; the reference "

@@ -1650,6 +1650,170 @@ __global__ __launch_bounds__(256, 2) void conv1x1_stream_h_kernel(const ConvArgs
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Streaming 1x1 conv on the bf16 MFMA with fp32 accuracy (bf16x6, round 5): the fp32 ResidualUnit / RBB 1x1 layers and
+// their input-gradients, K = Ci in {64, 128}, Co = 32 * NT in {64, 128}, with the streamed epilogue operands the tiled
+// kernel fuses: residual (F & 1), ReLU mask (F & 2), accumulate into y (F & 4). These layers are HBM-bound (at bs 16,
+// 128^2: 64->128 + residual moves 335 MB for 17 GFLOP) and ran on the 64-row implicit-GEMM tiles at ~3.3 TB/s: every
+// block loads, waits at a barrier, multiplies, then streams its epilogue, so HBM idles while the MFMAs run and the
+// other way round. Here, as conv1x1_stream_kernel, each WAVE streams its own 32-pixel tiles with no barrier after the
+// one-time weight staging, and EVERY streamed operand rolls a tile ahead in registers:
+//   * W [Co][K] is split once per block into three bf16 planes in LDS (pitch K + 8: conflict-free ds_read_b128);
+//   * the wave's X tile goes HBM -> registers in the MFMA B layout (lane (r, h): pixel p0 + r, channels 16s + 8h .. +7
+//     for k-step s: two float4), is split into its three bf16 pieces in registers (bf6_split4), and each float4 is
+//     reloaded for the wave's NEXT tile right after its split;
+//   * the epilogue operands (residual, mask, old y: one float4 per (co tile t, quad q)) of co tile t + 1 are issued
+//     when co tile t starts (two register sets), so each is in flight during a whole co tile's MFMAs;
+//   * the 32-output co tiles are done one at a time (one accumulator; the X pieces re-split per co tile from the
+//     raw fp32 registers — a few VALU ops against six MFMAs per k-step): what keeps every operand in flight within
+//     the VGPR file without spills;
+//   * C^T = W X^T: lane (r, h) holds pixel p0 + r, channels 32t + 8q + 4h .. +3 in acc[t][4q..4q+3] — float4 stores.
+// Products: bf6_mfma (six bf16 cross products per 16-deep k-step, fp32 accumulation), the same arithmetic as every
+// other bf16x6 kernel. Its waves fill the VGPR file exactly (4 x 128 or 2 x 256; see conv3x3_wres_bf6_kernel: a
+// kernel that converts with v_cvt_pk_bf16_f32 and runs bf16 MFMAs must not leave room for other kernels' waves).
+// VGPR allocation per wave: 128 (4 waves per SIMD, the file full; one epilogue operand set) where the operands fit in
+// it, else 256 (2 waves, two operand sets)
+template <int NT, int KS, int F>
+constexpr int stream_b6_vgprs() {
+    return (NT == 2 && KS == 4 && (F == 0 || F == 1 || F == 2 || F == 4)) ? 128 : 256;
+}
+template <int NT, int KS, int F>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(512 / stream_b6_vgprs<NT, KS, F>())))
+void conv1x1_stream_b6_kernel(const ConvArgs a) {
+    constexpr int K = 16 * KS, KP = K + 8, CO = 32 * NT;
+    constexpr bool RES = (F & 1) != 0, MASK = (F & 2) != 0, ACC = (F & 4) != 0;
+    constexpr int WPL = CO * KP;  // bf16 per weight plane
+    __shared__ __attribute__((aligned(16))) __bf16 Ws[3 * WPL];
+    __shared__ __attribute__((aligned(16))) float bs[CO];
+    // exactly 2 or 4 waves' worth of VGPRs: no room for another kernel's wave on these SIMDs
+    if constexpr (stream_b6_vgprs<NT, KS, F>() == 128) asm volatile("" ::: "v127");
+    else asm volatile("" ::: "v255");
+    const hyres_conv_geom& g = a.g;
+    const hyres_epilogue& e = a.e;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int lr = lane & 31, lh = lane >> 5;
+    for (int i = tid; i < CO * (K / 4); i += 256) {
+        const int co = i / (K / 4), k4 = i - co * (K / 4);
+        bf16x4_t h, m, l;
+        bf6_split4(ld4(a.w2 + (long long)co * a.ldw + 4 * k4), h, m, l);
+        const int o = co * KP + 4 * k4;
+        *reinterpret_cast<bf16x4_t*>(&Ws[o]) = h;
+        *reinterpret_cast<bf16x4_t*>(&Ws[WPL + o]) = m;
+        *reinterpret_cast<bf16x4_t*>(&Ws[2 * WPL + o]) = l;
+    }
+    for (int i = tid; i < CO; i += 256) bs[i] = e.bias ? e.bias[i] : 0.f;
+    const float slope = (e.act == HYRES_ACT_PRELU) ? e.slope[0] : 0.f;
+    __syncthreads();
+
+    const long long npix = a.M;
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, a.x_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t r_res = opnd_rsrc(RES ? e.res : nullptr, npix * e.ldres * 4);
+    const __amdgpu_buffer_rsrc_t r_mask = opnd_rsrc(MASK ? e.aux0 : nullptr, npix * e.ld0 * 4);
+    const __amdgpu_buffer_rsrc_t r_old = opnd_rsrc(ACC ? a.y : nullptr, npix * g.ldy * 4);
+    constexpr int OOR = (int)0x80000000;
+    const int ntile = (a.M + 31) / 32;
+    const int gw = blockIdx.x * 4 + wave, nw = gridDim.x * 4;
+    auto xoff = [&](int tile, int s, int u) -> int {
+        const int p = tile * 32 + lr;
+        return (tile < ntile && p < a.M) ? (p * g.ldx + 16 * s + 8 * lh + 4 * u) * 4 : OOR;
+    };
+    auto ooff = [&](int tile, int ld, int t, int q) -> int {
+        const int p = tile * 32 + lr;
+        return (tile < ntile && p < a.M) ? (p * ld + 32 * t + 8 * q + 4 * lh) * 4 : OOR;
+    };
+    static_assert(NT % 2 == 0, "the epilogue operands alternate between two register sets per co tile");
+    // epilogue operands: with two register sets (256-VGPR variants) co tile t's are in set t & 1 while co tile t + 1's
+    // (or the next tile's co tile 0) are in flight in the other, issued when co tile t starts; with one set (128-VGPR
+    // variants, 4 waves per SIMD) the next co tile's are issued right after this one's epilogue
+    constexpr int SETS = stream_b6_vgprs<NT, KS, F>() == 128 ? 1 : 2;
+    float4 xv[KS][2];
+    float4 eres[RES ? SETS : 1][4], emask[MASK ? SETS : 1][4], eold[ACC ? SETS : 1][4];
+    auto load_epi = [&](int tile, int t, int set) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if constexpr (RES) eres[set][q] = bload4(r_res, ooff(tile, e.ldres, t, q));
+            if constexpr (MASK) emask[set][q] = bload4(r_mask, ooff(tile, e.ld0, t, q));
+            if constexpr (ACC) eold[set][q] = bload4(r_old, ooff(tile, g.ldy, t, q));
+        }
+    };
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) xv[s][u] = bload4(xr, xoff(gw, s, u));
+    load_epi(gw, 0, 0);
+    for (int tile = gw; tile < ntile; tile += nw) {
+        const int p = tile * 32 + lr;
+        const bool pok = p < a.M;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const int cur = SETS == 2 ? (t & 1) : 0;
+            if constexpr (SETS == 2) {
+                if (t + 1 < NT) load_epi(tile, t + 1, cur ^ 1);
+                else load_epi(tile + nw, 0, cur ^ 1);
+            }
+            floatx16 acc;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+            for (int s = 0; s < KS; ++s) {
+                // the X pieces are re-split per co tile (a few VALU ops) rather than held for all k-steps
+                // (the empty asm makes each co tile's split its own computation: common-subexpression elimination
+                // would otherwise keep every k-step's pieces live across all co tiles and spill)
+                typedef float f32x4v_t __attribute__((ext_vector_type(4)));
+                f32x4v_t v0 = __builtin_bit_cast(f32x4v_t, xv[s][0]), v1 = __builtin_bit_cast(f32x4v_t, xv[s][1]);
+                asm volatile("" : "+v"(v0), "+v"(v1));
+                const float4 x0 = __builtin_bit_cast(float4, v0), x1 = __builtin_bit_cast(float4, v1);
+                bf16x4_t h0, m0, l0, h1, m1, l1;
+                bf6_split4(x0, h0, m0, l0);
+                bf6_split4(x1, h1, m1, l1);
+                const bf16x8_t xb[3] = {__builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7),
+                                        __builtin_shufflevector(m0, m1, 0, 1, 2, 3, 4, 5, 6, 7),
+                                        __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7)};
+                if (t == NT - 1) {
+#pragma unroll
+                    for (int u = 0; u < 2; ++u) xv[s][u] = bload4(xr, xoff(tile + nw, s, u));  // the next tile's X
+                }
+                const int o = (32 * t + lr) * KP + 16 * s + 8 * lh;
+                const bf16x8_t wb[3] = {*reinterpret_cast<const bf16x8_t*>(&Ws[o]),
+                                        *reinterpret_cast<const bf16x8_t*>(&Ws[WPL + o]),
+                                        *reinterpret_cast<const bf16x8_t*>(&Ws[2 * WPL + o])};
+                acc = bf6_mfma(wb, xb, acc);
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int n = 32 * t + 8 * q + 4 * lh;
+                const float4 b4 = *reinterpret_cast<const float4*>(&bs[n]);
+                float o[4] = {acc[4 * q] + b4.x, acc[4 * q + 1] + b4.y, acc[4 * q + 2] + b4.z, acc[4 * q + 3] + b4.w};
+                if constexpr (RES) {
+                    o[0] += eres[cur][q].x; o[1] += eres[cur][q].y; o[2] += eres[cur][q].z; o[3] += eres[cur][q].w;
+                }
+                if (pok && e.out2) st4(e.out2 + (long long)p * e.ldo2 + n, make_float4(o[0], o[1], o[2], o[3]));
+                if constexpr (MASK) {
+                    o[0] = emask[cur][q].x > 0.f ? o[0] : 0.f;
+                    o[1] = emask[cur][q].y > 0.f ? o[1] : 0.f;
+                    o[2] = emask[cur][q].z > 0.f ? o[2] : 0.f;
+                    o[3] = emask[cur][q].w > 0.f ? o[3] : 0.f;
+                } else if (e.act == HYRES_ACT_RELU) {
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) o[c] = fmaxf(o[c], 0.f);
+                } else if (e.act == HYRES_ACT_PRELU) {
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) o[c] = o[c] >= 0.f ? o[c] : slope * o[c];
+                }
+                if constexpr (ACC) {
+                    o[0] += eold[cur][q].x; o[1] += eold[cur][q].y; o[2] += eold[cur][q].z; o[3] += eold[cur][q].w;
+                }
+                if (pok) st4(a.y + (long long)p * g.ldy + n, make_float4(o[0], o[1], o[2], o[3]));
+            }
+            if constexpr (SETS == 1) {
+                if (t + 1 < NT) load_epi(tile, t + 1, 0);
+                else load_epi(tile + nw, 0, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);  // keep the next co tile's LDS reads and splits out of this one
+        }
+    }
+}
+
 // split-K reduction + epilogue: one thread per (phase, m, n)
 template <bool H>
 __global__ void conv_splitk_reduce_kernel(const ConvArgs a) {
@@ -2058,8 +2222,9 @@ static void dense_taps(hyres_conv_geom* g, int KH, int KW, int sgn, int dil, int
 // keys: HYRES_TUNE_TILE, _SPLIT_BLOCKS, _SPLIT_MINCHUNKS, _WGRAD_BLOCKS, _WGRAD_MINCHUNKS, _WGRAD_NT,
 // _WGRAD_MAXSPLIT
 // key 7: fp32 GEMMs bf16x6 (0: native fp32 MFMA); key 8: fp16 streaming 1x1; key 9: the bf16x6 weight-resident 3x3's
-// whole-VGPR-file guard (0 = diagnostic unguarded build, DESIGN §4 "Cross-kernel interference")
-int g_tune[10] = {-1, -1, -1, -1, -1, -1, -1, 1, 1, 1};
+// whole-VGPR-file guard (0 = diagnostic unguarded build, DESIGN §4 "Cross-kernel interference"); key 10: the bf16x6
+// streaming 1x1 kernel (0 = those layers on the tiled implicit GEMM, for A/B)
+int g_tune[11] = {-1, -1, -1, -1, -1, -1, -1, 1, 1, 1, 1};
 
 }  // namespace hyres
 
@@ -2363,6 +2528,22 @@ static int stream_h_nt(const hyres_conv_geom* g, const hyres_epilogue* e) {
     return g->Co / 32;
 }
 
+// conv1x1_stream_b6_kernel eligibility (bf16x6 fp32 GEMMs, hyres_conv_tuning key 10 = 1): fp32 X / Y, single-tap
+// stride-1 1x1 with (Ci, Co) in {(64, 64), (64, 128), (128, 64)}, BIAS epilogue with none / ReLU / PReLU / ReLU mask,
+// any of residual / mask / accumulate, grids >= 65536 output pixels. Returns the packed choice NT | KS << 4 | F << 8,
+// or 0.
+static int stream_b6_cfg(const hyres_conv_geom* g, const hyres_epilogue* e) {
+    if (g_tune[7] != 1 || g_tune[10] == 0) return 0;
+    if (e->io_f16 || e->f16_operands || e->square_input || e->kind != HYRES_EPI_BIAS) return 0;
+    if (g->nphase != 1 || g->ntaps != 1 || g->ish != 1 || g->isw != 1 || g->dh[0] != 0 || g->dw[0] != 0) return 0;
+    if (g->Hi != g->Hq || g->Wi != g->Wq || g->Ho != g->Hq || g->Wo != g->Wq) return 0;
+    if ((long long)g->B * g->Hq * g->Wq < 65536) return 0;
+    const bool shape = (g->Ci == 64 && (g->Co == 64 || g->Co == 128)) || (g->Ci == 128 && g->Co == 64);
+    if (!shape) return 0;
+    const int F = (e->res ? 1 : 0) | (e->act == HYRES_ACT_RELU_MASK ? 2 : 0) | (e->accumulate ? 4 : 0);
+    return (g->Co / 32) | ((g->Ci / 16) << 4) | (F << 8);
+}
+
 extern "C++" {
 template <int NT, int KC>
 static int launch_stream_h_one(const ConvArgs& a, hipStream_t st) {
@@ -2379,6 +2560,44 @@ static int launch_stream_h_one(const ConvArgs& a, hipStream_t st) {
     return HY_LAUNCH_CHECK("conv1x1_stream_h_kernel");
 }
 }  // extern "C++"
+
+extern "C++" {
+template <int NT, int KS, int F>
+static int launch_stream_b6_one(const ConvArgs& a, hipStream_t st) {
+    static int occ = -1;
+    if (occ < 0) {
+        int n = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, conv1x1_stream_b6_kernel<NT, KS, F>, 256, 0) != hipSuccess ||
+            n < 1)
+            n = 1;
+        occ = n;
+    }
+    const int blocks = std::max(1, std::min(ceil_div(ceil_div(a.M, 32), 4), num_cus() * occ));
+    hipLaunchKernelGGL((conv1x1_stream_b6_kernel<NT, KS, F>), dim3(blocks), dim3(256), 0, st, a);
+    return HY_LAUNCH_CHECK("conv1x1_stream_b6_kernel");
+}
+template <int NT, int KS>
+static int launch_stream_b6_f(const ConvArgs& a, int f, hipStream_t st) {
+    switch (f) {
+        case 0: return launch_stream_b6_one<NT, KS, 0>(a, st);
+        case 1: return launch_stream_b6_one<NT, KS, 1>(a, st);
+        case 2: return launch_stream_b6_one<NT, KS, 2>(a, st);
+        case 3: return launch_stream_b6_one<NT, KS, 3>(a, st);
+        case 4: return launch_stream_b6_one<NT, KS, 4>(a, st);
+        case 5: return launch_stream_b6_one<NT, KS, 5>(a, st);
+        case 6: return launch_stream_b6_one<NT, KS, 6>(a, st);
+        default: return launch_stream_b6_one<NT, KS, 7>(a, st);
+    }
+}
+}  // extern "C++"
+
+static int launch_stream_b6(const ConvArgs& a, int cfg, hipStream_t st) {
+    const int nt = cfg & 15, ks = (cfg >> 4) & 15, f = cfg >> 8;
+    if (nt == 2 && ks == 4) return launch_stream_b6_f<2, 4>(a, f, st);
+    if (nt == 4 && ks == 4) return launch_stream_b6_f<4, 4>(a, f, st);
+    if (nt == 2 && ks == 8) return launch_stream_b6_f<2, 8>(a, f, st);
+    return set_error(HYRES_E_ARG, "conv1x1_stream_b6: no instantiation for NT=%d KS=%d", nt, ks);
+}
 
 static int launch_stream_h(const ConvArgs& a, int nt, int kc, hipStream_t st) {
 #define HY_STREAM_H(NT, KC) \
@@ -2449,7 +2668,7 @@ static long long plan_ws_bytes(const hyres_conv_geom* g, const ConvPlan& p) {
 }
 
 int hyres_conv_tuning(int key, int value, int* old) {
-    HY_REQUIRE(key >= 0 && key < 10, HYRES_E_ARG, "conv_tuning: key %d", key);
+    HY_REQUIRE(key >= 0 && key < 11, HYRES_E_ARG, "conv_tuning: key %d", key);
     if (old) *old = g_tune[key];
     g_tune[key] = value;
     return ok();
@@ -2563,6 +2782,16 @@ int hyres_conv_forward(const hyres_conv_geom* g, const float* x, const float* w2
         return wres16_ok(g) ? launch_wres16(a, st) : launch_halo16(a, st);
     }
     {
+        const int cfg = stream_b6_cfg(g, e);
+        const long long xb = (long long)a.M * g->ldx * 4;
+        if (cfg && mode == 0 && a.vec4 && a.rsrc_ok && xb < 0x7FFFFFF0LL && aligned16(x) && aligned16(w2) &&
+            ldw % 4 == 0) {
+            a.x_bytes = (int)xb;
+            a.nsplit = 1;
+            return launch_stream_b6(a, cfg, st);
+        }
+    }
+    {
         const int nt = stream_nt(g, e);
         const long long xb = (long long)a.M * g->ldx * 4;
         if (nt && mode == 0 && a.vec4 && xb < 0x7FFFFFF0LL && aligned16(x) && aligned16(w2) && ldw % 4 == 0) {
@@ -2618,6 +2847,13 @@ int hyres_conv_kernel_name(const hyres_conv_geom* g, const hyres_epilogue* e, in
     if (ch.mode == 0 && halo16_ok(g, e)) {
         snprintf(buf, n, "%s<%d>", wres16_ok(g) ? "conv3x3_wres_f16_kernel" : "conv3x3_halo_f16_kernel", e->io_f16 & 3);
         return 0;
+    }
+    {
+        const int cfg = stream_b6_cfg(g, e);
+        if (cfg && ch.mode == 0) {
+            snprintf(buf, n, "conv1x1_stream_b6_kernel<%d, %d, %d>", cfg & 15, (cfg >> 4) & 15, cfg >> 8);
+            return 0;
+        }
     }
     {
         const int nt = stream_nt(g, e);

@@ -74,3 +74,13 @@ def test_persistent_kernels_with_room_beside_them(meta):
         print(f"{name[:64]:64s} alloc {alloc:3d}  hole {hole:3d}{'  <- another kernel wave fits' if hole >= 40 else ''}")
     names = {r[0].split("(")[0].split("::")[-1].split("<")[0] for r in rows}
     assert {"conv3x3_wres_bf6_kernel", "ru_fused_f16_kernel", "conv3x3_wres_f32_kernel"} <= names
+
+
+def test_stream_b6_kernels_fill_the_vgpr_file(meta):
+    """conv1x1_stream_b6_kernel (bf16x6 streaming 1x1, round 5) converts with v_cvt_pk_bf16_f32 and runs bf16 MFMAs:
+    every instantiation allocates exactly 128 (4 waves per SIMD) or 256 (2 waves) VGPRs — no hole — and spills
+    nothing."""
+    ks = _find(meta, "conv1x1_stream_b6_kernel")
+    assert len(ks) == 24
+    for k in ks:
+        assert k["alloc"] in (128, 256) and kernel_meta.residency(k)["hole_vgprs"] == 0 and k["scratch"] == 0, k

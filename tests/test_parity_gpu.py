@@ -1487,6 +1487,11 @@ def test_amp_train_step_vs_fp32():
     assert not torch.equal(x16, x32), "fp16 operand path did not engage"
 
 
+# per-tensor direction / distance of the AMP train-step gradients from this build's fp32 ones (2x the worst measured)
+AMP_COS_GAP = 0.05
+AMP_NORMWISE = 0.35
+
+
 def test_amp_matches_reference_autocast_fixture():
     """The AMP path (train.sh:19 ``--mixed-precision``; engine.py:32 forward + criterion under autocast) against
     the REFERENCE's own autocast run (tests/golden/make_golden.py ``amp_fixtures``: the reference under
@@ -1617,6 +1622,22 @@ def test_amp_matches_reference_autocast_fixture():
     assert all(e < 0.5 for e, _, _ in sl), sl
     wrong = {(n, v) for n, v, h, h32 in signs if n not in slopes and h * h32 < 0}
     assert dval[len(dval) // 2][0] < 0.05 and len(wrong) <= max(2, nsamp // 100), (dval[:5], sorted(wrong)[:5])
+    # every other tensor, whole, against this build's fp32 gradient (itself pinned to the reference's fp32 fixtures and
+    # the fp64 oracle): direction (1 - cosine) and normwise distance. The bars below are ~2x the worst tensor measured
+    # (round 5, printed), so a tensor off by a sign pattern, a missing term or a 25 % scale cannot pass — unlike the
+    # norm-only bar above
+    dirn = []
+    for n, gh in amp.items():
+        b32 = f32.get(n)
+        if n in slopes or b32 is None or float(b32.norm()) == 0.0:
+            continue
+        nb = float(b32.norm())
+        cos = float(gh @ b32) / max(float(gh.norm()) * nb, 1e-300)
+        dirn.append((1.0 - cos, float((gh - b32).norm()) / nb, n))
+    dirn.sort(reverse=True)
+    print("AMP vs this build's fp32, per tensor: worst 1-cos", [("%.2e" % c, "%.3f" % r, n) for c, r, n in dirn[:4]],
+          "worst normwise", sorted(((r, n) for _, r, n in dirn), reverse=True)[:3])
+    assert all(c <= AMP_COS_GAP and r <= AMP_NORMWISE for c, r, _ in dirn), dirn[:3]
 
 
 @pytest.mark.parametrize("K,Ci,Co,H", [(3, 64, 64, 128), (1, 128, 64, 128), (1, 64, 128, 128)])
