@@ -1671,11 +1671,12 @@ __global__ __launch_bounds__(256, 2) void conv1x1_stream_h_kernel(const ConvArgs
 // Products: bf6_mfma (six bf16 cross products per 16-deep k-step, fp32 accumulation), the same arithmetic as every
 // other bf16x6 kernel. Its waves fill the VGPR file exactly (4 x 128 or 2 x 256; see conv3x3_wres_bf6_kernel: a
 // kernel that converts with v_cvt_pk_bf16_f32 and runs bf16 MFMAs must not leave room for other kernels' waves).
-// VGPR allocation per wave: 128 (4 waves per SIMD, the file full; one epilogue operand set) where the operands fit in
-// it, else 256 (2 waves, two operand sets)
+// VGPR allocation per wave: 256 (2 waves per SIMD, two epilogue operand sets). Measured (profiles/r5e_stream_b6.txt):
+// 128 VGPRs / 4 waves per SIMD with one operand set was slower (256^2 64->64: 153 vs 143 us), and so was prefetching
+// X two tiles and the operands a whole tile ahead (128^2 128->64: 50.4 vs 46.7 us, 64^2 64->128 +res 23.9 vs 20.1)
 template <int NT, int KS, int F>
 constexpr int stream_b6_vgprs() {
-    return (NT == 2 && KS == 4 && (F == 0 || F == 1 || F == 2 || F == 4)) ? 128 : 256;
+    return 256;
 }
 template <int NT, int KS, int F>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(512 / stream_b6_vgprs<NT, KS, F>())))

@@ -1,6 +1,6 @@
 """conv1x1_stream_b6_kernel (csrc/conv.hip, round 5): the fp32 1x1 convs of the ResidualUnits / RBBs and their
 input-gradients (models/layers/attention.py:11-30, compressai ResidualBottleneckBlock at models/checkerboard.py:38-56)
-on a per-wave streaming kernel with bf16x6 products, every epilogue operand rolling a co tile ahead.
+on a per-wave streaming kernel with bf16x6 products, every epilogue operand issued a co tile ahead.
 
 Against float64 torch, through the C-ABI (hyres_conv_forward with a hand-built epilogue, so every operand combination
 the model's forward and backward use is reached): the three shapes (Ci, Co) in {(64, 128), (128, 64), (64, 64)} x
