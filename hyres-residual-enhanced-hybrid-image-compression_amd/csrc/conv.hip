@@ -1678,7 +1678,7 @@ template <int NT, int KS, int F>
 constexpr int stream_b6_vgprs() {
     return 256;
 }
-template <int NT, int KS, int F>
+template <int NT, int KS, int F, bool CE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(512 / stream_b6_vgprs<NT, KS, F>())))
 void conv1x1_stream_b6_kernel(const ConvArgs a) {
     constexpr int K = 16 * KS, KP = K + 8, CO = 32 * NT;
@@ -1686,6 +1686,10 @@ void conv1x1_stream_b6_kernel(const ConvArgs a) {
     constexpr int WPL = CO * KP;  // bf16 per weight plane
     __shared__ __attribute__((aligned(16))) __bf16 Ws[3 * WPL];
     __shared__ __attribute__((aligned(16))) float bs[CO];
+    // CE: per-wave epilogue scratch, one 32 x 32 co tile (pitch 36 floats: the MFMA-layout float4 writes of 16 lanes
+    // land on 16 distinct 4-bank groups)
+    constexpr int EP = 36;
+    __shared__ __attribute__((aligned(16))) float Es[CE ? 4 * 32 * EP : 4];
     // exactly 2 or 4 waves' worth of VGPRs: no room for another kernel's wave on these SIMDs
     if constexpr (stream_b6_vgprs<NT, KS, F>() == 128) asm volatile("" ::: "v127");
     else asm volatile("" ::: "v255");
@@ -1718,9 +1722,19 @@ void conv1x1_stream_b6_kernel(const ConvArgs a) {
         const int p = tile * 32 + lr;
         return (tile < ntile && p < a.M) ? (p * g.ldx + 16 * s + 8 * lh + 4 * u) * 4 : OOR;
     };
+    // epilogue operand q of co tile t. MFMA layout: lane (r, h) -> pixel p0 + r, channels 32t + 8q + 4h (one wave
+    // instruction touches 32 pixel rows x 32 B). CE (coalesced): lane l -> pixel p0 + (l >> 3) + 8q, channels
+    // 32t + 4 (l & 7) (one instruction = 8 pixel rows x 128 B contiguous; profiles/r5h_access_probe.txt: the 32-B
+    // shape caps a read+write stream at ~3.0-3.5 TB/s, full rows reach 5.3-5.9)
+    const int cr = lane >> 3, cc = 4 * (lane & 7);
     auto ooff = [&](int tile, int ld, int t, int q) -> int {
-        const int p = tile * 32 + lr;
-        return (tile < ntile && p < a.M) ? (p * ld + 32 * t + 8 * q + 4 * lh) * 4 : OOR;
+        if constexpr (CE) {
+            const int p = tile * 32 + cr + 8 * q;
+            return (tile < ntile && p < a.M) ? (p * ld + 32 * t + cc) * 4 : OOR;
+        } else {
+            const int p = tile * 32 + lr;
+            return (tile < ntile && p < a.M) ? (p * ld + 32 * t + 8 * q + 4 * lh) * 4 : OOR;
+        }
     };
     static_assert(NT % 2 == 0, "the epilogue operands alternate between two register sets per co tile");
     // epilogue operands: with two register sets (256-VGPR variants) co tile t's are in set t & 1 while co tile t + 1's
@@ -1743,8 +1757,6 @@ void conv1x1_stream_b6_kernel(const ConvArgs a) {
         for (int u = 0; u < 2; ++u) xv[s][u] = bload4(xr, xoff(gw, s, u));
     load_epi(gw, 0, 0);
     for (int tile = gw; tile < ntile; tile += nw) {
-        const int p = tile * 32 + lr;
-        const bool pok = p < a.M;
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
             const int cur = SETS == 2 ? (t & 1) : 0;
@@ -1780,11 +1792,28 @@ void conv1x1_stream_b6_kernel(const ConvArgs a) {
                                         *reinterpret_cast<const bf16x8_t*>(&Ws[2 * WPL + o])};
                 acc = bf6_mfma(wb, xb, acc);
             }
+            float* const es = Es + wave * 32 * EP;
+            if constexpr (CE) {
+                // the accumulator goes to the wave's scratch in the MFMA layout and comes back as pixel rows
+                // (LDS instructions of one wave execute in order: the fences only keep the compiler from moving the
+                // previous co tile's reads past these writes or these writes past the reads below)
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    *reinterpret_cast<float4*>(&es[lr * EP + 8 * q + 4 * lh]) =
+                        make_float4(acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]);
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const int n = 32 * t + 8 * q + 4 * lh;
+                const int n = CE ? 32 * t + cc : 32 * t + 8 * q + 4 * lh;
                 const float4 b4 = *reinterpret_cast<const float4*>(&bs[n]);
-                float o[4] = {acc[4 * q] + b4.x, acc[4 * q + 1] + b4.y, acc[4 * q + 2] + b4.z, acc[4 * q + 3] + b4.w};
+                float4 av;
+                if constexpr (CE) av = *reinterpret_cast<const float4*>(&es[(cr + 8 * q) * EP + cc]);
+                else av = make_float4(acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]);
+                const int p = CE ? tile * 32 + cr + 8 * q : tile * 32 + lr;
+                const bool pok = p < a.M;
+                float o[4] = {av.x + b4.x, av.y + b4.y, av.z + b4.z, av.w + b4.w};
                 if constexpr (RES) {
                     o[0] += eres[cur][q].x; o[1] += eres[cur][q].y; o[2] += eres[cur][q].z; o[3] += eres[cur][q].w;
                 }
@@ -2225,7 +2254,7 @@ static void dense_taps(hyres_conv_geom* g, int KH, int KW, int sgn, int dil, int
 // key 7: fp32 GEMMs bf16x6 (0: native fp32 MFMA); key 8: fp16 streaming 1x1; key 9: the bf16x6 weight-resident 3x3's
 // whole-VGPR-file guard (0 = diagnostic unguarded build, DESIGN §4 "Cross-kernel interference"); key 10: the bf16x6
 // streaming 1x1 kernel (0 = those layers on the tiled implicit GEMM, for A/B)
-int g_tune[11] = {-1, -1, -1, -1, -1, -1, -1, 1, 1, 1, 1};
+int g_tune[12] = {-1, -1, -1, -1, -1, -1, -1, 1, 1, 1, 1, 1};
 
 }  // namespace hyres
 
@@ -2563,19 +2592,24 @@ static int launch_stream_h_one(const ConvArgs& a, hipStream_t st) {
 }  // extern "C++"
 
 extern "C++" {
-template <int NT, int KS, int F>
-static int launch_stream_b6_one(const ConvArgs& a, hipStream_t st) {
+template <int NT, int KS, int F, bool CE>
+static int launch_stream_b6_ce(const ConvArgs& a, hipStream_t st) {
     static int occ = -1;
     if (occ < 0) {
         int n = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, conv1x1_stream_b6_kernel<NT, KS, F>, 256, 0) != hipSuccess ||
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, conv1x1_stream_b6_kernel<NT, KS, F, CE>, 256, 0) !=
+                hipSuccess ||
             n < 1)
             n = 1;
         occ = n;
     }
     const int blocks = std::max(1, std::min(ceil_div(ceil_div(a.M, 32), 4), num_cus() * occ));
-    hipLaunchKernelGGL((conv1x1_stream_b6_kernel<NT, KS, F>), dim3(blocks), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((conv1x1_stream_b6_kernel<NT, KS, F, CE>), dim3(blocks), dim3(256), 0, st, a);
     return HY_LAUNCH_CHECK("conv1x1_stream_b6_kernel");
+}
+template <int NT, int KS, int F>
+static int launch_stream_b6_one(const ConvArgs& a, hipStream_t st) {
+    return g_tune[11] == 0 ? launch_stream_b6_ce<NT, KS, F, false>(a, st) : launch_stream_b6_ce<NT, KS, F, true>(a, st);
 }
 template <int NT, int KS>
 static int launch_stream_b6_f(const ConvArgs& a, int f, hipStream_t st) {
@@ -2669,7 +2703,7 @@ static long long plan_ws_bytes(const hyres_conv_geom* g, const ConvPlan& p) {
 }
 
 int hyres_conv_tuning(int key, int value, int* old) {
-    HY_REQUIRE(key >= 0 && key < 11, HYRES_E_ARG, "conv_tuning: key %d", key);
+    HY_REQUIRE(key >= 0 && key < 12, HYRES_E_ARG, "conv_tuning: key %d", key);
     if (old) *old = g_tune[key];
     g_tune[key] = value;
     return ok();
@@ -2852,7 +2886,8 @@ int hyres_conv_kernel_name(const hyres_conv_geom* g, const hyres_epilogue* e, in
     {
         const int cfg = stream_b6_cfg(g, e);
         if (cfg && ch.mode == 0) {
-            snprintf(buf, n, "conv1x1_stream_b6_kernel<%d, %d, %d>", cfg & 15, (cfg >> 4) & 15, cfg >> 8);
+            snprintf(buf, n, "conv1x1_stream_b6_kernel<%d, %d, %d, %s>", cfg & 15, (cfg >> 4) & 15, cfg >> 8,
+                     g_tune[11] == 0 ? "false" : "true");
             return 0;
         }
     }

@@ -170,6 +170,9 @@ int hyres_conv_plan(const hyres_conv_geom* g, const hyres_epilogue* e, int* tile
 #define HYRES_TUNE_STREAM_B6 10       /* 1 (default): the fp32 1x1 convs with (Ci, Co) in {(64,64), (64,128), (128,64)} on
                                        * >= 65536 pixels on the bf16x6 streaming kernel (conv1x1_stream_b6_kernel, any of
                                        * residual / ReLU mask / accumulate); 0: the tiled implicit GEMM (A/B) */
+#define HYRES_TUNE_STREAM_CE 11       /* 1 (default): conv1x1_stream_b6_kernel stages each co tile's accumulator through LDS
+                                       * so its epilogue reads / writes whole 128-byte pixel-row pieces; 0: the MFMA
+                                       * lane layout straight to HBM (32 B per pixel row per wave instruction; A/B) */
 int hyres_conv_tuning(int key, int value, int* old);
 
 /* Weight gradient:  dW[t][m][n] = sum_q P[q][m] * Q[shift_t(q)][n]  over a base grid q (B,Hq,Wq).

@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--no-stream-h", action="store_true", help="fp16 1x1 on the tiled kernel (hyres_conv_tuning key 8 = 0)")
     ap.add_argument("--no-stream-b6", action="store_true",
                     help="bf16x6 fp32 1x1 on the tiled kernel (hyres_conv_tuning key 10 = 0)")
+    ap.add_argument("--no-stream-ce", action="store_true",
+                    help="streaming bf16x6 1x1 with the MFMA-layout epilogue (hyres_conv_tuning key 11 = 0)")
     a = ap.parse_args()
     from hyres_hip import _lib as L
     from hyres_hip import ops as O
@@ -38,6 +40,7 @@ def main():
     L.call("hyres_conv_tuning", 7, 1 if a.bf6 else 0, None)  # the native fp32 MFMA unless --bf6
     L.call("hyres_conv_tuning", 8, 0 if a.no_stream_h else 1, None)
     L.call("hyres_conv_tuning", 10, 0 if a.no_stream_b6 else 1, None)
+    L.call("hyres_conv_tuning", 11, 0 if a.no_stream_ce else 1, None)
     if a.io16:
         a.f16 = True
     dev = torch.device("cuda:0")
@@ -65,7 +68,7 @@ def main():
     flops = 2.0 * a.B * Ho * Ho * a.K * a.K * a.Ci * a.Co
     es = 2.0 if a.io16 else 4.0
     byts = es * (a.B * a.H * a.H * a.Ci + a.B * Ho * Ho * a.Co * (2 if a.res else 1)) + 4.0 * a.K * a.K * a.Ci * a.Co
-    print(f"conv B{a.B} {a.H}x{a.H}x{a.Ci} -> {Ho}x{Ho}x{a.Co} K{a.K} s{a.stride}{' +res' if a.res else ''}{' f16' if a.f16 else ''}{' io16' if a.io16 else ''}{' tiled' if a.no_stream_h or a.no_stream_b6 else ''}{' bf16x6' if a.bf6 else ''}: {us:.1f} us, "
+    print(f"conv B{a.B} {a.H}x{a.H}x{a.Ci} -> {Ho}x{Ho}x{a.Co} K{a.K} s{a.stride}{' +res' if a.res else ''}{' f16' if a.f16 else ''}{' io16' if a.io16 else ''}{' tiled' if a.no_stream_h or a.no_stream_b6 else ''}{' mfma-epi' if a.no_stream_ce else ''}{' bf16x6' if a.bf6 else ''}: {us:.1f} us, "
           f"{flops / us / 1e6:.1f} TFLOP/s, {byts / us / 1e3:.0f} GB/s")
 
 

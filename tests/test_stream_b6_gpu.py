@@ -5,7 +5,8 @@ on a per-wave streaming kernel with bf16x6 products, every epilogue operand issu
 Against float64 torch, through the C-ABI (hyres_conv_forward with a hand-built epilogue, so every operand combination
 the model's forward and backward use is reached): the three shapes (Ci, Co) in {(64, 128), (128, 64), (64, 64)} x
 all eight combinations of residual / ReLU mask / accumulate, with ReLU, PReLU or no activation and the pre-activation
-copy (out2), on a ragged pixel count (5 x 117 x 117 = 68,445: the last 32-pixel tile is partial). Bar: normwise error
+copy (out2), on a ragged pixel count (5 x 117 x 117 = 68,445: the last 32-pixel tile is partial), with the coalesced
+(LDS-staged, hyres_conv_tuning key 11 = 1) and the MFMA-layout epilogue. Bar: normwise error
 vs fp64 <= 2e-6 and no worse than twice the tiled implicit GEMM's on the same call (hyres_conv_tuning key 10 = 0).
 """
 import ctypes
@@ -28,7 +29,7 @@ def _rand(shape, seed, scale=1.0):
     return (torch.rand(shape, generator=g) * 2 - 1) * scale
 
 
-def _run(Ci, Co, F, act, out2, stream_on):
+def _run(Ci, Co, F, act, out2, stream_on, ce=1):
     from hyres_hip import _lib as L
     from hyres_hip import ops as O
     D = dev()
@@ -57,8 +58,9 @@ def _run(Ci, Co, F, act, out2, stream_on):
     e.slope = slope.data_ptr()
     if out2:
         e.out2, e.ldo2 = pre.data_ptr(), Co
-    old_key = ctypes.c_int(0)
+    old_key, old_ce = ctypes.c_int(0), ctypes.c_int(0)
     L.call("hyres_conv_tuning", 10, 1 if stream_on else 0, ctypes.byref(old_key))
+    L.call("hyres_conv_tuning", 11, ce, ctypes.byref(old_ce))
     try:
         name = O.conv_variant(g, e, False)
         L.call("hyres_conv_forward", ctypes.byref(g), x.data_ptr(), w2.data_ptr(), Ci, y.data_ptr(), ctypes.byref(e),
@@ -66,6 +68,7 @@ def _run(Ci, Co, F, act, out2, stream_on):
         torch.cuda.synchronize()
     finally:
         L.call("hyres_conv_tuning", 10, old_key.value, None)
+        L.call("hyres_conv_tuning", 11, old_ce.value, None)
     # float64 reference of the epilogue order: acc + bias (+ res) -> out2 -> act / mask -> (+ old)
     r = x.double() @ w.double().reshape(Co, Ci).t() + b.double()
     if F & 1:
@@ -93,7 +96,11 @@ def test_stream_b6_matches_fp64(Ci, Co, F):
     act = acts[(F + Ci // 64) % 3]
     out2 = F in (1, 4, 7)
     name_s, err_s = _run(Ci, Co, F, act, out2, True)
+    name_m, err_m = _run(Ci, Co, F, act, out2, True, ce=0)
     name_t, err_t = _run(Ci, Co, F, act, out2, False)
-    print(f"{Ci}->{Co} F={F} act={act} out2={out2}: {name_s} {err_s:.2e}, {name_t} {err_t:.2e}")
-    assert name_s.startswith("conv1x1_stream_b6_kernel<") and not name_t.startswith("conv1x1_stream_b6"), (name_s, name_t)
-    assert err_s < 2e-6 and err_s <= 2 * err_t + 1e-9
+    print(f"{Ci}->{Co} F={F} act={act} out2={out2}: {name_s} {err_s:.2e}, {name_m} {err_m:.2e}, {name_t} {err_t:.2e}")
+    assert name_s.startswith("conv1x1_stream_b6_kernel<") and name_s.endswith(", true>"), name_s
+    assert name_m.startswith("conv1x1_stream_b6_kernel<") and name_m.endswith(", false>"), name_m
+    assert not name_t.startswith("conv1x1_stream_b6"), name_t
+    for err in (err_s, err_m):
+        assert err < 2e-6 and err <= 2 * err_t + 1e-9
