@@ -1277,7 +1277,10 @@ constexpr int BF6_HV = (BF6_HE + 511) / 512;
 // 16-B segment (0 / 1) of element k (0..15) of row r in a swizzled [row][16] bf16 image, as an element offset
 __device__ __forceinline__ int bf6_off(int r, int k) { return r * 16 + ((((k >> 3) ^ (r >> 3)) & 1) << 3) + (k & 7); }
 
-template <bool GUARD>
+// V (round 5 A/B, hyres_conv_tuning key 12): bit 0 — each tap's six fragments are read one tap ahead into a second
+// register set (explicit software pipeline of the LDS reads against the previous tap's six MFMAs); bit 1 — waves
+// 4..7 (the second-dispatched half, the arbitration loser on a shared SIMD) run at static priority 1
+template <bool GUARD, int V>
 __global__ __launch_bounds__(512, 1) void conv3x3_wres_bf6_kernel(const ConvArgs a, int ntiles, int groups) {
     __shared__ __attribute__((aligned(16))) __bf16 lds[3 * BF6_WPL + 3 * BF6_HPL];
     __shared__ int2 tapoff[9];
@@ -1407,6 +1410,54 @@ __global__ __launch_bounds__(512, 1) void conv3x3_wres_bf6_kernel(const ConvArgs
             }
         }
         if (s + 2 < steps) hload(hl, s + 2);
+        if constexpr ((V & 1) != 0) {
+            // explicit software pipeline: tap t + 1's six fragments are read (hand-issued ds_read_b128, so the
+            // compiler cannot sink them to their uses) while tap t's MFMAs run; each MFMA pair waits only for its
+            // own two reads (the LDS return counter retires in order; any other LGKM op only makes a wait longer)
+            typedef __attribute__((address_space(3))) __bf16 lds_bf16;
+            const unsigned wbase = (unsigned)(size_t)(lds_bf16*)Ws, hbase = (unsigned)(size_t)(lds_bf16*)Hs;
+            auto rd = [&](unsigned addr) -> bf16x8_t {
+                bf16x8_t r;
+                asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(addr) : "memory");
+                return r;
+            };
+            auto frag = [&](int t, bf16x8_t (&wv)[3], bf16x8_t (&xv)[3]) {
+                const int wrow = (c * 9 + t) * 32 + lr;
+                const int hrow = (orow + 1 + g.dh[t]) * HALO_HW + 32 * ph + lr + 1 + g.dw[t];
+                const unsigned wo = wbase + 2u * (wrow * 16 + (((lh ^ (wrow >> 3)) & 1) << 3));
+                const unsigned ho = hbase + 2u * (hrow * 16 + (((lh ^ (hrow >> 3)) & 1) << 3));
+                wv[2] = rd(wo + 4u * BF6_WPL);
+                xv[0] = rd(ho);
+                wv[1] = rd(wo + 2u * BF6_WPL);
+                xv[1] = rd(ho + 2u * BF6_HPL);
+                wv[0] = rd(wo);
+                xv[2] = rd(ho + 4u * BF6_HPL);
+            };
+            bf16x8_t fw[2][3], fx[2][3];
+            hsplit(hs);  // unconditional (unused after the last step): no branch inside the tap loop
+            frag(0, fw[0], fx[0]);
+#pragma unroll
+            for (int t = 0; t < 9; ++t) {
+                bf16x8_t(&w)[3] = fw[t & 1];
+                bf16x8_t(&x)[3] = fx[t & 1];
+                if (t + 1 < 9) {
+                    frag(t + 1, fw[(t + 1) & 1], fx[(t + 1) & 1]);
+                    asm volatile("s_waitcnt lgkmcnt(10)" : "+v"(w[2]), "+v"(x[0]));
+                } else {
+                    asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(w[2]), "+v"(x[0]));
+                }
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[2], x[0], acc, 0, 0, 0);
+                if (t + 1 < 9) asm volatile("s_waitcnt lgkmcnt(8)" : "+v"(w[1]), "+v"(x[1]));
+                else asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(w[1]), "+v"(x[1]));
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[1], x[1], acc, 0, 0, 0);
+                if (t + 1 < 9) asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(w[0]), "+v"(x[2]));
+                else asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(w[0]), "+v"(x[2]));
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0], x[2], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[1], x[0], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0], x[1], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0], x[0], acc, 0, 0, 0);
+            }
+        } else {
 #pragma unroll
         for (int t = 0; t < 9; ++t) {
             const int2 o = tapoff[t];
@@ -1428,6 +1479,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_wres_bf6_kernel(const ConvArgs
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w0, x1, acc, 0, 0, 0);
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w0, x0, acc, 0, 0, 0);
             if (t == 1 && s + 1 < steps) hsplit(hs);  // step s + 1's halo (loaded a step ago) -> bf16 pieces
+        }
         }
         if (c == 3) {
             if (i < g.Ho) {
@@ -1460,6 +1512,9 @@ __global__ __launch_bounds__(512, 1) void conv3x3_wres_bf6_kernel(const ConvArgs
         if (s + 1 < steps) hput();
         __syncthreads();
     };
+    if constexpr ((V & 2) != 0) {
+        if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+    }
     for (int s = 0; s < steps; s += 2) {
         body(s, hA, hB);
         if (s + 1 < steps) body(s + 1, hB, hA);
@@ -2254,7 +2309,7 @@ static void dense_taps(hyres_conv_geom* g, int KH, int KW, int sgn, int dil, int
 // key 7: fp32 GEMMs bf16x6 (0: native fp32 MFMA); key 8: fp16 streaming 1x1; key 9: the bf16x6 weight-resident 3x3's
 // whole-VGPR-file guard (0 = diagnostic unguarded build, DESIGN §4 "Cross-kernel interference"); key 10: the bf16x6
 // streaming 1x1 kernel (0 = those layers on the tiled implicit GEMM, for A/B)
-int g_tune[12] = {-1, -1, -1, -1, -1, -1, -1, 1, 1, 1, 1, 1};
+int g_tune[13] = {-1, -1, -1, -1, -1, -1, -1, 1, 1, 1, 1, 1, 0};
 
 }  // namespace hyres
 
@@ -2486,10 +2541,17 @@ static int launch_wres32(const ConvArgs& a, hipStream_t st) {
     const int groups = g.Co / 32;
     const int per = wres_blocks(groups);
     if (wres_bf6()) {
+        const dim3 grid(per * groups);
         if (g_tune[9] == 0)  // diagnostic only: the allocation that let other kernels' waves share its SIMDs
-            hipLaunchKernelGGL(conv3x3_wres_bf6_kernel<false>, dim3(per * groups), dim3(512), 0, st, a, ntiles, groups);
+            hipLaunchKernelGGL((conv3x3_wres_bf6_kernel<false, 0>), grid, dim3(512), 0, st, a, ntiles, groups);
+        else if (g_tune[12] == 1)
+            hipLaunchKernelGGL((conv3x3_wres_bf6_kernel<true, 1>), grid, dim3(512), 0, st, a, ntiles, groups);
+        else if (g_tune[12] == 2)
+            hipLaunchKernelGGL((conv3x3_wres_bf6_kernel<true, 2>), grid, dim3(512), 0, st, a, ntiles, groups);
+        else if (g_tune[12] == 3)
+            hipLaunchKernelGGL((conv3x3_wres_bf6_kernel<true, 3>), grid, dim3(512), 0, st, a, ntiles, groups);
         else
-            hipLaunchKernelGGL(conv3x3_wres_bf6_kernel<true>, dim3(per * groups), dim3(512), 0, st, a, ntiles, groups);
+            hipLaunchKernelGGL((conv3x3_wres_bf6_kernel<true, 0>), grid, dim3(512), 0, st, a, ntiles, groups);
         return HY_LAUNCH_CHECK("conv3x3_wres_bf6_kernel");
     }
     hipLaunchKernelGGL(conv3x3_wres_f32_kernel, dim3(per * groups), dim3(512), 0, st, a, ntiles, groups);
@@ -2703,7 +2765,7 @@ static long long plan_ws_bytes(const hyres_conv_geom* g, const ConvPlan& p) {
 }
 
 int hyres_conv_tuning(int key, int value, int* old) {
-    HY_REQUIRE(key >= 0 && key < 12, HYRES_E_ARG, "conv_tuning: key %d", key);
+    HY_REQUIRE(key >= 0 && key < 13, HYRES_E_ARG, "conv_tuning: key %d", key);
     if (old) *old = g_tune[key];
     g_tune[key] = value;
     return ok();

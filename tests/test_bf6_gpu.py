@@ -486,3 +486,35 @@ def test_bf6_kernels_beside_a_bilinear():
                     worst = max([worst] + [(g_ - ref).abs().max().item() for g_ in got])
             print(f"{name:42s} {'bf16x6' if on else 'native'}: side-stream bilinear max |diff| vs alone {worst:.2e}")
             assert worst == 0.0, (name, on)
+
+
+@pytest.mark.parametrize("variant", [1, 2, 3])
+def test_wres_bf6_variants_bit_identical(variant):
+    """conv3x3_wres_bf6_kernel's scheduling variants (hyres_conv_tuning key 12: bit 0 the hand-pipelined fragment
+    reads, bit 1 static priority for waves 4..7) change only WHEN the LDS reads issue, not the MFMA order: the output
+    must equal variant 0 bit for bit (128^2 with residual + ReLU, and a Kodak-size image with PReLU)."""
+    import ctypes
+    from hyres_hip import _lib as L
+    from hyres_hip import ops as O
+    D = dev()
+    C = 64
+    slope = torch.tensor([0.25], device=D)
+    for (B, H, W, act) in [(4, 128, 128, "relu"), (1, 512, 768, "prelu")]:
+        x = _rand((B, C, H, W), 51).to(D)
+        w = torch.nn.Parameter(_rand((C, C, 3, 3), 52, (C * 9) ** -0.5).to(D))
+        b = _rand((C,), 53, 0.1).to(D)
+        r = _rand((B, C, H, W), 54).to(D)
+        a = L.ACT_RELU if act == "relu" else L.ACT_PRELU
+        outs = {}
+        for v in (0, variant):
+            old = ctypes.c_int(0)
+            with _Bf6(True):
+                L.call("hyres_conv_tuning", 12, v, ctypes.byref(old))
+                try:
+                    xn, rn = O.to_nhwc(x), O.to_nhwc(r)
+                    yn = O.conv2d(None, xn, w, b, pad=1, act=a, res=rn, slope=slope if act == "prelu" else None)
+                    outs[v] = O.to_nchw(yn).clone()
+                finally:
+                    L.call("hyres_conv_tuning", 12, old.value, None)
+        torch.cuda.synchronize()
+        assert torch.equal(outs[0], outs[variant]), (B, H, W, act, (outs[0] - outs[variant]).abs().max().item())

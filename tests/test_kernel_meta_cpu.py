@@ -33,11 +33,14 @@ def _find(meta, fragment):
 
 
 def test_wres_bf6_takes_the_whole_vgpr_file(meta):
-    (k,) = _find(meta, "conv3x3_wres_bf6_kernelILb1E")  # GUARD = true: the instantiation every default launch uses
-    r = kernel_meta.residency(k)
-    assert k["threads"] == 512 and k["alloc"] == 256, k
-    assert r["waves_per_simd"] == 2 and r["hole_vgprs"] == 0, r
-    assert k["scratch"] == 0
+    # GUARD = true: every instantiation a default launch can pick (the variants of hyres_conv_tuning key 12)
+    ks = _find(meta, "conv3x3_wres_bf6_kernelILb1E")
+    assert len(ks) == 4
+    for k in ks:
+        r = kernel_meta.residency(k)
+        assert k["threads"] == 512 and k["alloc"] == 256, k
+        assert r["waves_per_simd"] == 2 and r["hole_vgprs"] == 0, r
+        assert k["scratch"] == 0
     # the diagnostic instantiation (hyres_conv_tuning key 9 = 0) keeps the allocation that showed the interference
     (d,) = _find(meta, "conv3x3_wres_bf6_kernelILb0E")
     assert d["alloc"] == 224 and kernel_meta.residency(d)["hole_vgprs"] == 64, d
