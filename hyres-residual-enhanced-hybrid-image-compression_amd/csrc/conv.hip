@@ -1277,9 +1277,10 @@ constexpr int BF6_HV = (BF6_HE + 511) / 512;
 // 16-B segment (0 / 1) of element k (0..15) of row r in a swizzled [row][16] bf16 image, as an element offset
 __device__ __forceinline__ int bf6_off(int r, int k) { return r * 16 + ((((k >> 3) ^ (r >> 3)) & 1) << 3) + (k & 7); }
 
-// V (round 5 A/B, hyres_conv_tuning key 12): bit 0 — each tap's six fragments are read one tap ahead into a second
-// register set (explicit software pipeline of the LDS reads against the previous tap's six MFMAs); bit 1 — waves
-// 4..7 (the second-dispatched half, the arbitration loser on a shared SIMD) run at static priority 1
+// V (hyres_conv_tuning key 12, default 1): bit 0 — each tap's six fragments are read one tap ahead into a second
+// register set (hand-issued ds_read_b128: the compiler sank its own reads next to their MFMAs, waiting on each) —
+// 133 -> 125 us at 128^2, 481 -> 453 us at 256^2 (profiles/r5i_wres_variants_micro.txt); bit 1 — waves 4..7 at static
+// priority 1: no effect (kept for the A/B). Every variant forms the same MFMAs in the same order (bit-identical)
 template <bool GUARD, int V>
 __global__ __launch_bounds__(512, 1) void conv3x3_wres_bf6_kernel(const ConvArgs a, int ntiles, int groups) {
     __shared__ __attribute__((aligned(16))) __bf16 lds[3 * BF6_WPL + 3 * BF6_HPL];
@@ -2309,7 +2310,7 @@ static void dense_taps(hyres_conv_geom* g, int KH, int KW, int sgn, int dil, int
 // key 7: fp32 GEMMs bf16x6 (0: native fp32 MFMA); key 8: fp16 streaming 1x1; key 9: the bf16x6 weight-resident 3x3's
 // whole-VGPR-file guard (0 = diagnostic unguarded build, DESIGN §4 "Cross-kernel interference"); key 10: the bf16x6
 // streaming 1x1 kernel (0 = those layers on the tiled implicit GEMM, for A/B)
-int g_tune[13] = {-1, -1, -1, -1, -1, -1, -1, 1, 1, 1, 1, 1, 0};
+int g_tune[13] = {-1, -1, -1, -1, -1, -1, -1, 1, 1, 1, 1, 1, 1};
 
 }  // namespace hyres
 

@@ -208,6 +208,11 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     if mode not in ("bf16x6", "native"):
         raise ValueError(f"HYRES_FP32_GEMM={mode!r}: 'bf16x6' or 'native'")
     lib.hyres_conv_tuning(7, 1 if mode == "bf16x6" else 0, None)
+    # HYRES_TUNE="key=value,...": A/B overrides of other hyres_conv_tuning keys (include/hyres_hip.h HYRES_TUNE_*)
+    for kv in filter(None, os.environ.get("HYRES_TUNE", "").split(",")):
+        k, v = kv.split("=")
+        if lib.hyres_conv_tuning(int(k), int(v), None) != 0:
+            raise ValueError(f"HYRES_TUNE: bad key {kv!r}")
     return lib
 
 

@@ -173,8 +173,9 @@ int hyres_conv_plan(const hyres_conv_geom* g, const hyres_epilogue* e, int* tile
 #define HYRES_TUNE_STREAM_CE 11       /* 1 (default): conv1x1_stream_b6_kernel stages each co tile's accumulator through LDS
                                        * so its epilogue reads / writes whole 128-byte pixel-row pieces; 0: the MFMA
                                        * lane layout straight to HBM (32 B per pixel row per wave instruction; A/B) */
-#define HYRES_TUNE_WRES_BF6_V 12      /* conv3x3_wres_bf6_kernel variant (A/B): bit 0 fragments read one tap ahead,
-                                       * bit 1 static priority 1 for waves 4..7 */
+#define HYRES_TUNE_WRES_BF6_V 12      /* conv3x3_wres_bf6_kernel variant: bit 0 (default 1) each tap's fragments read
+                                       * one tap ahead, bit 1 static priority 1 for waves 4..7; 0: reads as the compiler
+                                       * schedules them (A/B) */
 int hyres_conv_tuning(int key, int value, int* old);
 
 /* Weight gradient:  dW[t][m][n] = sum_q P[q][m] * Q[shift_t(q)][n]  over a base grid q (B,Hq,Wq).

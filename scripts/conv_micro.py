@@ -30,8 +30,8 @@ def main():
     ap.add_argument("--no-stream-h", action="store_true", help="fp16 1x1 on the tiled kernel (hyres_conv_tuning key 8 = 0)")
     ap.add_argument("--no-stream-b6", action="store_true",
                     help="bf16x6 fp32 1x1 on the tiled kernel (hyres_conv_tuning key 10 = 0)")
-    ap.add_argument("--no-stream-ce", action="store_true",
-                    help="streaming bf16x6 1x1 with the MFMA-layout epilogue (hyres_conv_tuning key 11 = 0)")
+    ap.add_argument("--stream-cm", type=int, default=1,
+                    help="streaming bf16x6 1x1 access mode (hyres_conv_tuning key 11: 0 MFMA layout, 1 LDS-staged epilogue)")
     ap.add_argument("--wres-v", type=int, default=0, help="conv3x3_wres_bf6_kernel variant (hyres_conv_tuning key 12)")
     a = ap.parse_args()
     from hyres_hip import _lib as L
@@ -41,7 +41,7 @@ def main():
     L.call("hyres_conv_tuning", 7, 1 if a.bf6 else 0, None)  # the native fp32 MFMA unless --bf6
     L.call("hyres_conv_tuning", 8, 0 if a.no_stream_h else 1, None)
     L.call("hyres_conv_tuning", 10, 0 if a.no_stream_b6 else 1, None)
-    L.call("hyres_conv_tuning", 11, 0 if a.no_stream_ce else 1, None)
+    L.call("hyres_conv_tuning", 11, a.stream_cm, None)
     L.call("hyres_conv_tuning", 12, a.wres_v, None)
     if a.io16:
         a.f16 = True
@@ -70,7 +70,7 @@ def main():
     flops = 2.0 * a.B * Ho * Ho * a.K * a.K * a.Ci * a.Co
     es = 2.0 if a.io16 else 4.0
     byts = es * (a.B * a.H * a.H * a.Ci + a.B * Ho * Ho * a.Co * (2 if a.res else 1)) + 4.0 * a.K * a.K * a.Ci * a.Co
-    print(f"conv B{a.B} {a.H}x{a.H}x{a.Ci} -> {Ho}x{Ho}x{a.Co} K{a.K} s{a.stride}{' +res' if a.res else ''}{' f16' if a.f16 else ''}{' io16' if a.io16 else ''}{' tiled' if a.no_stream_h or a.no_stream_b6 else ''}{' mfma-epi' if a.no_stream_ce else ''}{f' wres-v{a.wres_v}' if a.wres_v else ''}{' bf16x6' if a.bf6 else ''}: {us:.1f} us, "
+    print(f"conv B{a.B} {a.H}x{a.H}x{a.Ci} -> {Ho}x{Ho}x{a.Co} K{a.K} s{a.stride}{' +res' if a.res else ''}{' f16' if a.f16 else ''}{' io16' if a.io16 else ''}{' tiled' if a.no_stream_h or a.no_stream_b6 else ''}{f' cm{a.stream_cm}' if a.stream_cm != 1 else ''}{f' wres-v{a.wres_v}' if a.wres_v else ''}{' bf16x6' if a.bf6 else ''}: {us:.1f} us, "
           f"{flops / us / 1e6:.1f} TFLOP/s, {byts / us / 1e3:.0f} GB/s")
 
 

@@ -9,7 +9,7 @@ rm -f gpurun_out/r5_ce_micro.log
 for args in "--H 128 --Ci 64 --Co 128 --K 1 --res --relu" "--H 128 --Ci 128 --Co 64 --K 1 --relu" \
             "--H 64 --Ci 64 --Co 128 --K 1 --res --relu" "--H 256 --Ci 64 --Co 64 --K 1 --relu" \
             "--H 256 --Ci 64 --Co 64 --K 1 --res"; do
-  for v in "" "--no-stream-ce" "--no-stream-b6"; do
+  for v in "" "--stream-cm 0" "--no-stream-b6"; do
     timeout -k 10 60 python -u scripts/conv_micro.py --bf6 $args $v --iters 50 2>&1 | grep conv >> gpurun_out/r5_ce_micro.log || exit 1
   done
 done

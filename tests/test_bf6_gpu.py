@@ -518,3 +518,4 @@ def test_wres_bf6_variants_bit_identical(variant):
                     L.call("hyres_conv_tuning", 12, old.value, None)
         torch.cuda.synchronize()
         assert torch.equal(outs[0], outs[variant]), (B, H, W, act, (outs[0] - outs[variant]).abs().max().item())
+
