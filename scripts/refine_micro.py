@@ -1,7 +1,11 @@
-"""Microbenchmark MultiScaleRefine's resampling kernels at the C2 shapes (B16, 64 ch, 256x256), alone.
+"""Isolated timings of MultiScaleRefine's HBM-bound pieces at the C2 shapes (bs16, 256^2, 64 channels): the four
+bilinear resamplings (enhancement.py:96-103), SpatialAttention (pool + 7x7 + multiply, enhancement.py:15-21 on the
+192-channel concat) and SEBlock's scale, with HIP events, against their algorithmic HBM bytes.
 
-    python scripts/refine_micro.py
+    python scripts/refine_micro.py [--iters 50]
 """
+import argparse
+import ctypes
 import os
 import sys
 
@@ -11,8 +15,8 @@ sys.path.insert(0, os.path.join(REPO, "hyres-residual-enhanced-hybrid-image-comp
 import torch  # noqa: E402
 
 
-def timeit(fn, iters=20):
-    for _ in range(3):
+def timeit(fn, iters):
+    for _ in range(5):
         fn()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -25,26 +29,43 @@ def timeit(fn, iters=20):
 
 
 def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--B", type=int, default=16)
+    ap.add_argument("--H", type=int, default=256)
+    a = ap.parse_args()
     from hyres_hip import _lib as L
-    dev = torch.device("cuda:0")
-    B, C, H = 16, 64, 256
-    x = torch.randn(B, H, H, C, device=dev)
-    for f in (2, 4):
-        h = H // f
-        y = torch.empty(B, h, h, C, device=dev)
-        up = torch.empty(B, H, H, C, device=dev)
-        st = L.stream()
-        down = timeit(lambda: L.call("hyres_bilinear_fwd", x.data_ptr(), C, y.data_ptr(), C, B, H, H, h, h, C,
-                                     float(f), float(f), 0, st))
-        upt = timeit(lambda: L.call("hyres_bilinear_fwd", y.data_ptr(), C, up.data_ptr(), C, B, h, h, H, H, C,
-                                    1.0 / f, 1.0 / f, 0, st))
-        dbw = timeit(lambda: L.call("hyres_bilinear_bwd", y.data_ptr(), C, up.data_ptr(), C, B, H, H, h, h, C,
-                                    float(f), float(f), 0, st))
-        ubw = timeit(lambda: L.call("hyres_bilinear_bwd", up.data_ptr(), C, y.data_ptr(), C, B, h, h, H, H, C,
-                                    1.0 / f, 1.0 / f, 0, st))
-        big = B * H * H * C * 4
-        print(f"x1/{f}: down fwd {down:.1f} us ({(big + big / f / f) / down / 1e3:.0f} GB/s), up fwd {upt:.1f} us "
-              f"({(big + big / f / f) / upt / 1e3:.0f} GB/s), down bwd {dbw:.1f} us, up bwd {ubw:.1f} us")
+    D = torch.device("cuda:0")
+    B, H, C = a.B, a.H, 64
+    feat = torch.randn(B, H, H, C, device=D)
+    multi = torch.randn(B, H, H, 3 * C, device=D)
+    h2 = torch.randn(B, H // 2, H // 2, C, device=D)
+    h4 = torch.randn(B, H // 4, H // 4, C, device=D)
+    st = L.stream()
+    cases = [
+        ("bilinear down x1/2", lambda: L.call("hyres_bilinear_fwd", feat.data_ptr(), C, h2.data_ptr(), C, B, H, H, H // 2,
+                                               H // 2, C, 2.0, 2.0, 0, st), 4 * B * C * (H * H + (H // 2) ** 2)),
+        ("bilinear up x2 -> concat", lambda: L.call("hyres_bilinear_fwd", h2.data_ptr(), C, multi[..., C:].data_ptr(),
+                                                    3 * C, B, H // 2, H // 2, H, H, C, 0.5, 0.5, 0, st),
+         4 * B * C * (H * H + (H // 2) ** 2)),
+        ("bilinear down x1/4", lambda: L.call("hyres_bilinear_fwd", feat.data_ptr(), C, h4.data_ptr(), C, B, H, H, H // 4,
+                                               H // 4, C, 4.0, 4.0, 0, st), 4 * B * C * (H * H // 4 + (H // 4) ** 2)),
+        ("bilinear up x4 -> concat", lambda: L.call("hyres_bilinear_fwd", h4.data_ptr(), C,
+                                                    multi[..., 2 * C:].data_ptr(), 3 * C, B, H // 4, H // 4, H, H, C,
+                                                    0.25, 0.25, 0, st), 4 * B * C * (H * H + (H // 4) ** 2)),
+    ]
+    P = B * H * H
+    w = torch.randn(1, 2, 7, 7, device=D)
+    pooled2 = torch.empty(P, 2, device=D)
+    amax = torch.empty(P, dtype=torch.int32, device=D)
+    attn = torch.empty(P, device=D)
+    y = torch.empty_like(multi)
+    cases.append(("spatial attention fwd (C=192)", lambda: L.call(
+        "hyres_spatial_attn_fwd", multi.data_ptr(), w.data_ptr(), pooled2.data_ptr(), amax.data_ptr(), attn.data_ptr(),
+        y.data_ptr(), B, H, H, 3 * C, st), 4 * P * 3 * C * 3))
+    for name, fn, byts in cases:
+        us = timeit(fn, a.iters)
+        print(f"{name:32s} B{B} {H}^2: {us:8.1f} us, {byts / us / 1e3:6.0f} GB/s (algorithmic {byts / 1e6:.0f} MB)")
 
 
 if __name__ == "__main__":

@@ -21,11 +21,15 @@ def main():
     ap.add_argument("--batch", type=int, default=16)
     ap.add_argument("--size", type=int, default=256)
     ap.add_argument("--eval", action="store_true", help="eval forward (encode+decode) instead of a train step")
+    ap.add_argument("--serial", action="store_true", help="branch streams off (every kernel on the main stream)")
     ap.add_argument("--marker", action="store_true",
                     help="a torch spin kernel between the warm-up and the timed steps (scripts/step_traffic.py)")
     args = ap.parse_args()
     from hyres_hip.graphs import CapturedStep
     from hyres_hip.loss import RateDistortionLoss
+    from hyres_hip import ops as O
+    if args.serial:
+        O.BranchStreams.enabled = False
     from hyres_hip.optim import DeviceGradScaler, FusedAdam
     from hyres_hip.weights import synthetic_state_dict
     from models import ResidualJPEGCompression
