@@ -14,6 +14,13 @@ static inline int grid_for_r(long long n) {
     long long b = (n + 255) / 256;
     return (int)std::max<long long>(1, std::min<long long>(b, 8192));
 }
+// the PW_UNR-unrolled pointwise kernels: each thread takes PW_UNR float4 per pass, 8 blocks of 256 per CU resident
+static inline int pw_grid(long long n4) {
+    long long b = (n4 + 256LL * 4 - 1) / (256LL * 4);
+    return (int)std::max<long long>(1, std::min<long long>(b, 2048));
+}
+
+constexpr int PW_UNR = 4;  // float4 per thread in flight in the pointwise kernels below
 
 // torch area_pixel_compute_source_index (linear, align_corners=False): max(scale*(o+0.5)-0.5, 0)
 __device__ __forceinline__ void src_index(float scale, int o, int in, int& i0, int& i1, float& l0, float& l1) {
@@ -226,15 +233,30 @@ __global__ void se_fc_kernel(const float* part, int nch, const float* w1, const 
     }
 }
 // fp16 activations (autocast inference): x, y fp16, 4 channels per thread
-__global__ void se_scale4h_kernel(const float* x, const float* sgate, float* y, int B, int HW, int C) {
-    const int C4 = C >> 2;
-    const long long n = (long long)B * HW * C4;
-    GRID_STRIDE(i, n) {
-        const int c = 4 * (int)(i % C4);
-        const int b = (int)(i / ((long long)HW * C4));
-        const float4 v = ldv4<true>(x, 4 * i);
-        const float4 gt = ld4(sgate + b * C + c);
-        stv4<true>(y, 4 * i, make_float4(v.x * gt.x, v.y * gt.y, v.z * gt.z, v.w * gt.w));
+// y = x * gate[b][c], 4 channels per thread (C % 4 == 0), 32-bit indices (B * HW * C / 4 < 2^31, host), UNR in flight;
+// H: x, y fp16 (autocast inference)
+template <bool H>
+__global__ __launch_bounds__(256) void se_scale4_kernel(const float* x, const float* sgate, float* y, int B, int HW,
+                                                        int C) {
+    const int C4 = C >> 2, HWC4 = HW * C4;
+    const int n = B * HWC4;
+    const int stride = gridDim.x * 256;
+    for (int i0 = blockIdx.x * 256 + threadIdx.x; i0 < n; i0 += stride * PW_UNR) {
+        float4 v[PW_UNR];
+#pragma unroll
+        for (int u = 0; u < PW_UNR; ++u) {
+            const int i = i0 + u * stride;
+            if (i < n) v[u] = ldv4<H>(x, 4LL * i);
+        }
+#pragma unroll
+        for (int u = 0; u < PW_UNR; ++u) {
+            const int i = i0 + u * stride;
+            if (i >= n) continue;
+            const int b = i / HWC4;
+            const int c = 4 * (i - (i / C4) * C4);
+            const float4 gt = ld4(sgate + b * C + c);
+            stv4<H>(y, 4LL * i, make_float4(v[u].x * gt.x, v[u].y * gt.y, v[u].z * gt.z, v[u].w * gt.w));
+        }
     }
 }
 __global__ void se_scale_kernel(const float* x, const float* sgate, float* y, int B, int HW, int C) {
@@ -329,6 +351,32 @@ __global__ void se_fc_bwd_kernel(const float* part, int nch, int B, const float*
         float s = 0.f;
         for (int j = 0; j < Cr; ++j) s += w1[j * C + c] * gh[b * Cr + j];
         gpool[idx] = s / (float)HW;
+    }
+}
+// gx = gy * gate[b][c] + gpool[b][c], 4 channels per thread (as se_scale4_kernel)
+template <bool G>
+__global__ __launch_bounds__(256) void se_bwd_x4_kernel(const float* gy, const float* sgate, const float* gpool,
+                                                        float* gx, int B, int HW, int C) {
+    const int C4 = C >> 2, HWC4 = HW * C4;
+    const int n = B * HWC4;
+    const int stride = gridDim.x * 256;
+    for (int i0 = blockIdx.x * 256 + threadIdx.x; i0 < n; i0 += stride * PW_UNR) {
+        float4 v[PW_UNR];
+#pragma unroll
+        for (int u = 0; u < PW_UNR; ++u) {
+            const int i = i0 + u * stride;
+            if (i < n) v[u] = ldv4<G>(gy, 4LL * i);
+        }
+#pragma unroll
+        for (int u = 0; u < PW_UNR; ++u) {
+            const int i = i0 + u * stride;
+            if (i >= n) continue;
+            const int b = i / HWC4;
+            const int c = 4 * (i - (i / C4) * C4);
+            const float4 gt = ld4(sgate + b * C + c), gp = ld4(gpool + b * C + c);
+            stv4<G>(gx, 4LL * i, make_float4(v[u].x * gt.x + gp.x, v[u].y * gt.y + gp.y, v[u].z * gt.z + gp.z,
+                                             v[u].w * gt.w + gp.w));
+        }
     }
 }
 template <bool G = false>
@@ -618,7 +666,11 @@ int hyres_se_fwd(const float* x, const float* w1, const float* w2, float* y, flo
     rc = HY_LAUNCH_CHECK("se_fc");
     if (rc) return rc;
     long long n = (long long)B * HW * C;
-    hipLaunchKernelGGL(se_scale_kernel, dim3(grid_for_r(n)), dim3(256), 0, st, x, (const float*)sgate, y, B, HW, C);
+    if (C % 4 == 0 && aligned16(x) && aligned16(y) && n / 4 < (1LL << 31))
+        hipLaunchKernelGGL(se_scale4_kernel<false>, dim3(pw_grid(n / 4)), dim3(256), 0, st, x, (const float*)sgate, y, B,
+                           HW, C);
+    else
+        hipLaunchKernelGGL(se_scale_kernel, dim3(grid_for_r(n)), dim3(256), 0, st, x, (const float*)sgate, y, B, HW, C);
     return HY_LAUNCH_CHECK("se_scale");
 }
 
@@ -641,7 +693,8 @@ int hyres_se_fwd_f16(const void* x, const float* w1, const float* w2, void* y, f
     rc = HY_LAUNCH_CHECK("se_fc");
     if (rc) return rc;
     const long long n = (long long)B * HW * C / 4;
-    hipLaunchKernelGGL(se_scale4h_kernel, dim3(grid_for_r(n)), dim3(256), 0, st, (const float*)x, (const float*)sgate,
+    HY_REQUIRE(n < (1LL << 31), HYRES_E_SHAPE, "se_fwd_f16: too large");
+    hipLaunchKernelGGL(se_scale4_kernel<true>, dim3(pw_grid(n)), dim3(256), 0, st, (const float*)x, (const float*)sgate,
                        (float*)y, B, HW, C);
     return HY_LAUNCH_CHECK("se_scale_f16");
 }
@@ -671,8 +724,14 @@ static int se_bwd_impl(const float* x, const float* gy, const float* w1, const f
     rc = HY_LAUNCH_CHECK("se_fc_bwd");
     if (rc) return rc;
     long long n = (long long)B * HW * C;
-    hipLaunchKernelGGL(se_bwd_x_kernel<G>, dim3(grid_for_r(n)), dim3(256), 0, st, gy, sgate, (const float*)gpool, gx, B,
-                       HW, C);
+    const unsigned am = G ? 7u : 15u;
+    if (C % 4 == 0 && (reinterpret_cast<uintptr_t>(gy) & am) == 0 && (reinterpret_cast<uintptr_t>(gx) & am) == 0 &&
+        n / 4 < (1LL << 31))
+        hipLaunchKernelGGL(se_bwd_x4_kernel<G>, dim3(pw_grid(n / 4)), dim3(256), 0, st, gy, sgate, (const float*)gpool,
+                           gx, B, HW, C);
+    else
+        hipLaunchKernelGGL(se_bwd_x_kernel<G>, dim3(grid_for_r(n)), dim3(256), 0, st, gy, sgate, (const float*)gpool, gx,
+                           B, HW, C);
     return HY_LAUNCH_CHECK("se_bwd_x");
 }
 }  // extern "C++"
