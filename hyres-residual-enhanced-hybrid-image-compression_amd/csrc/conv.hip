@@ -83,6 +83,9 @@ template <bool H = false>
 __device__ __forceinline__ void epi_store(const hyres_epilogue& e, float* y, int ldy, long long pix, int n, float v,
                                           const EpiChannel& c) {
     switch (e.kind) {
+        case HYRES_EPI_ROWSCALE:  // the product scaled per output pixel first (aux1[pix * ld1]), then as BIAS
+            v *= e.aux1[pix * e.ld1];
+            [[fallthrough]];
         case HYRES_EPI_BIAS: {
             v += c.bias;
             if (e.res) v += ldv<H>(e.res, pix * e.ldres + n);
@@ -130,6 +133,12 @@ __device__ __forceinline__ void epi_store4(const hyres_epilogue& e, float* y, in
                                            float4 rpre = make_float4(0.f, 0.f, 0.f, 0.f)) {
     float o[4] = {v.x, v.y, v.z, v.w};
     switch (e.kind) {
+        case HYRES_EPI_ROWSCALE: {
+            const float sc = e.aux1[pix * e.ld1];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) o[c] *= sc;
+        }
+            [[fallthrough]];
         case HYRES_EPI_BIAS: {
             if (e.bias) { const float4 b = ld4(e.bias + n); o[0] += b.x; o[1] += b.y; o[2] += b.z; o[3] += b.w; }
             if (e.res) {  // rpre: the residual already loaded by the caller (same value, same order; passed by value:
@@ -2859,6 +2868,9 @@ int hyres_conv_forward(const hyres_conv_geom* g, const float* x, const float* w2
     }
     if (e->act == HYRES_ACT_RELU_MASK)
         HY_REQUIRE(e->aux0 && e->kind == HYRES_EPI_BIAS, HYRES_E_ARG, "conv: ReLU mask needs aux0, BIAS epilogue");
+    if (e->kind == HYRES_EPI_ROWSCALE)
+        HY_REQUIRE(e->aux1 && !e->square_input && !e->accumulate, HYRES_E_ARG,
+                   "conv: ROWSCALE needs aux1 (per-pixel scale), no square_input / accumulate");
     hipStream_t st = as_stream(s);
     if (ch.narrow) {
         a.nsplit = 1;

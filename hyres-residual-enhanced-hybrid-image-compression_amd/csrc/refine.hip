@@ -762,8 +762,8 @@ long long hyres_spatial_attn_workspace_bytes(int B, int H, int W) {
 
 int hyres_spatial_attn_fwd(const float* x, const float* w, float* pooled2, int* argmax, float* attn, float* y, int B,
                            int H, int W, int C, hyres_stream_t s) {
-    HY_REQUIRE(x && w && pooled2 && argmax && attn && y, HYRES_E_ARG, "spatial_attn_fwd: NULL");
-    HY_REQUIRE(C % 4 == 0 && C <= 1024 && aligned16(x) && aligned16(y), HYRES_E_ALIGN,
+    HY_REQUIRE(x && w && pooled2 && argmax && attn, HYRES_E_ARG, "spatial_attn_fwd: NULL");  // y NULL: map only
+    HY_REQUIRE(C % 4 == 0 && C <= 1024 && aligned16(x) && (!y || aligned16(y)), HYRES_E_ALIGN,
                "spatial_attn: C %% 4 == 0 and 16B-aligned x/y required");
     long long P = (long long)B * H * W;
     hipStream_t st = as_stream(s);
@@ -774,13 +774,14 @@ int hyres_spatial_attn_fwd(const float* x, const float* w, float* pooled2, int* 
     hipLaunchKernelGGL(sa_conv_kernel, dim3(grid_for_r(P)), dim3(256), 0, st, (const float*)pooled2, w, attn, B, H, W);
     rc = HY_LAUNCH_CHECK("sa_conv");
     if (rc) return rc;
+    if (!y) return ok();  // the attention map only (the multiply folded into the consumer: HYRES_EPI_ROWSCALE)
     hipLaunchKernelGGL(sa_mul_kernel<false>, dim3(grid_for_r(P * C / 4)), dim3(256), 0, st, x, (const float*)attn, y, P, C);
     return HY_LAUNCH_CHECK("sa_mul");
 }
 
 int hyres_spatial_attn_fwd_f16(const void* x, const float* w, float* pooled2, int* argmax, float* attn, void* y, int B,
                                int H, int W, int C, hyres_stream_t s) {
-    HY_REQUIRE(x && w && pooled2 && argmax && attn && y, HYRES_E_ARG, "spatial_attn_fwd_f16: NULL");
+    HY_REQUIRE(x && w && pooled2 && argmax && attn, HYRES_E_ARG, "spatial_attn_fwd_f16: NULL");  // y NULL: map only
     HY_REQUIRE(C % 4 == 0 && C <= 1024 && (reinterpret_cast<uintptr_t>(x) & 7) == 0 &&
                    (reinterpret_cast<uintptr_t>(y) & 7) == 0,
                HYRES_E_ALIGN, "spatial_attn_fwd_f16: C %% 4 == 0 and 8B-aligned x/y required");
@@ -793,6 +794,7 @@ int hyres_spatial_attn_fwd_f16(const void* x, const float* w, float* pooled2, in
     hipLaunchKernelGGL(sa_conv_kernel, dim3(grid_for_r(P)), dim3(256), 0, st, (const float*)pooled2, w, attn, B, H, W);
     rc = HY_LAUNCH_CHECK("sa_conv");
     if (rc) return rc;
+    if (!y) return ok();  // the attention map only
     hipLaunchKernelGGL(sa_mul_kernel<true>, dim3(grid_for_r(P * C / 4)), dim3(256), 0, st, (const float*)x,
                        (const float*)attn, (float*)y, P, C);
     return HY_LAUNCH_CHECK("sa_mul_f16");

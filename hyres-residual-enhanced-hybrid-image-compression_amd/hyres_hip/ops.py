@@ -844,7 +844,8 @@ def _act_backward(y: Node, gy: torch.Tensor, gy_ld: int, act: int, pre: Optional
 # --------------------------------------------------------------------------------------------------
 def conv2d(tape: Optional[Tape], x: Node, weight: torch.Tensor, bias: Optional[torch.Tensor], stride=1,
            pad=0, dil=1, act=L.ACT_NONE, slope=None, res: Optional[Node] = None, out: Optional[Node] = None,
-           mask: Optional[torch.Tensor] = None, computed: bool = False) -> Node:
+           mask: Optional[torch.Tensor] = None, computed: bool = False,
+           rowscale: Optional[torch.Tensor] = None) -> Node:
     """nn.Conv2d (+ fused bias / residual / ReLU / PReLU epilogue), NHWC, on MFMA.
 
     Reference call sites: models/layers/common.py:4-11, compressai conv() (k5 s2 p2),
@@ -852,7 +853,10 @@ def conv2d(tape: Optional[Tape], x: Node, weight: torch.Tensor, bias: Optional[t
     (models/layers/attention.py:26-29) and RBB's ``out + identity`` are the fused residual epilogue.
     ``mask`` implements CheckboardMaskedConv2d's weight masking (models/layers/checkerboard.py:46-47).
     A 1x1 conv may read only the first x.C of the weight's input channels (param_aggregation on
-    ``cat([latent_params, zeros])``, models/checkerboard.py:115-117: the zero half contributes nothing)."""
+    ``cat([latent_params, zeros])``, models/checkerboard.py:115-117: the zero half contributes nothing).
+    ``rowscale`` (inference, 1x1 only): conv(x * s[pixel]) formed as s[pixel] * conv_nobias(x) + bias in the
+    epilogue (HYRES_EPI_ROWSCALE) — SpatialAttention's multiply ahead of MultiScaleRefine's fusion 1x1
+    (enhancement.py:105-109) without writing and re-reading the scaled 192-channel map."""
     Co, Ci_w, KH, KW = weight.shape
     Ci = x.C
     assert Ci == Ci_w or (KH == 1 and KW == 1 and Ci < Ci_w and mask is None), (Ci_w, x.C)
@@ -871,6 +875,11 @@ def conv2d(tape: Optional[Tape], x: Node, weight: torch.Tensor, bias: Optional[t
     e.kind = L.EPI_BIAS
     e.act = act
     e.bias = L.ptr(bias)
+    if rowscale is not None:
+        assert tape is None and KH == 1 and KW == 1 and stride == 1 and rowscale.dtype == torch.float32
+        assert rowscale.numel() == B * Ho * Wo and rowscale.is_contiguous()
+        e.kind = L.EPI_ROWSCALE
+        e.aux1, e.ld1 = rowscale.data_ptr(), 1
     if res is not None:
         assert (res.B, res.H, res.W, res.C) == (B, Ho, Wo, Co) and res.half == y.half
         e.res = res.ptr()

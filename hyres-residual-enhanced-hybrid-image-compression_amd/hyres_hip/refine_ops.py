@@ -86,6 +86,21 @@ def se_block(tape: Optional[Tape], x: Node, w1: torch.Tensor, w2: torch.Tensor) 
     return y
 
 
+def spatial_attention_map(x: Node, w: torch.Tensor) -> torch.Tensor:
+    """SpatialAttention(x) alone (enhancement.py:7-21): the [B, H, W] sigmoid map, fp32, forward only — its
+    multiply is folded into the next 1x1 conv's epilogue (ops.conv2d ``rowscale``)."""
+    assert x.contiguous
+    B, H, W, C = x.B, x.H, x.W, x.C
+    dev = x.device
+    pooled2 = _empty((B, H, W, 2), dev)
+    argmax = torch.empty((B, H, W), dtype=torch.int32, device=dev)
+    attn = _empty((B, H, W), dev)
+    fn = "hyres_spatial_attn_fwd_f16" if x.half else "hyres_spatial_attn_fwd"
+    L.call(fn, x.ptr(), w.data_ptr(), pooled2.data_ptr(), argmax.data_ptr(), attn.data_ptr(), None, B, H, W, C,
+           L.stream())
+    return attn
+
+
 def spatial_attention_mul(tape: Optional[Tape], x: Node, w: torch.Tensor) -> Node:
     """multi * SpatialAttention(multi) (enhancement.py:7-21 and :105-106), fused."""
     assert x.contiguous

@@ -9,6 +9,8 @@ Data flow (NHWC, one HBM buffer ``multi`` [B,H,W,3*mid] replaces torch.cat):
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 
@@ -17,6 +19,10 @@ from hyres_hip import refine_ops as R
 from hyres_hip.layers import Conv2d, HipModule, PReLU, ReLU, Sequential
 from hyres_hip import ops as O
 from hyres_hip.ops import Node
+
+# inference: SpatialAttention's multiply folded into fusion[0]'s epilogue (HYRES_EPI_ROWSCALE); tests flip it,
+# HYRES_FOLD_SA_MUL=0 turns it off (A/B)
+FOLD_SA_MUL = os.environ.get("HYRES_FOLD_SA_MUL", "1") == "1"
 
 __all__ = ["SpatialAttention", "SEBlock", "dilated_conv", "MultiScaleRefine"]
 
@@ -125,10 +131,20 @@ class MultiScaleRefine(HipModule):
 
         # the three scales are independent: three HIP streams, disjoint channel slices of ``multi``
         _, f2, f3 = O.run_branches(tape, feat, [scale1, scale2, scale3])
-        m = self.spatial_att.hip_mul(tape, multi)
-        out = self.fusion.hip(tape, m)
         from hyres_hip.ops import Trace
+        if tape is None and FOLD_SA_MUL:
+            # inference: multi * attn is never materialised — fusion[0] is a 1x1 conv, so
+            # conv(multi * attn) = attn * conv_nobias(multi) + bias, formed in its epilogue (HYRES_EPI_ROWSCALE)
+            attn = R.spatial_attention_map(multi, self.spatial_att.conv.weight)
+            f0, f1, f2c = self.fusion[0], self.fusion[1], self.fusion[2]
+            h = O.conv2d(None, multi, f0.weight, f0.bias, act=L.ACT_PRELU, slope=f1.weight, rowscale=attn)
+            out = f2c.hip(None, h)
+            m = None
+        else:
+            m = self.spatial_att.hip_mul(tape, multi)
+            out = self.fusion.hip(tape, m)
         for name, n in (("refine_feat", feat), ("refine_f2", f2), ("refine_f3", f3), ("refine_multi", multi),
                         ("refine_multi_att", m), ("refined", out)):
-            Trace.add(name, n)
+            if n is not None:
+                Trace.add(name, n)
         return out

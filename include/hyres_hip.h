@@ -97,6 +97,9 @@ int hyres_conv_weight_prep_batch(const void* descs, int n, long long total, hyre
 #define HYRES_EPI_IGDN 2      /* n = acc + bias(beta');  y = aux0 * sqrt(n);  out2 = n   (IGDN) */
 #define HYRES_EPI_GDN_BWD 3   /* y = 2*aux0*acc + aux1 * rsqrt(aux2)                              */
 #define HYRES_EPI_IGDN_BWD 4  /* y = 2*aux0*acc + aux1 * sqrt(aux2)                               */
+#define HYRES_EPI_ROWSCALE 5  /* y = act(aux1[pix * ld1] * acc + bias (+ res)): a per-output-pixel scale of the
+                               * input folded into the GEMM (SpatialAttention's x * attn ahead of MultiScaleRefine's
+                               * fusion 1x1, enhancement.py:105-109: inference only)                          */
 #define HYRES_ACT_NONE 0
 #define HYRES_ACT_RELU 1
 #define HYRES_ACT_PRELU 2     /* single shared slope (nn.PReLU()), read from device pointer */

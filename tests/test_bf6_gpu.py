@@ -519,3 +519,35 @@ def test_wres_bf6_variants_bit_identical(variant):
         torch.cuda.synchronize()
         assert torch.equal(outs[0], outs[variant]), (B, H, W, act, (outs[0] - outs[variant]).abs().max().item())
 
+
+
+@pytest.mark.parametrize("autocast", [False, True])
+def test_refine_sa_mul_fold_matches_unfused(autocast):
+    """Inference MultiScaleRefine with SpatialAttention's multiply folded into fusion[0]'s epilogue
+    (models/layers/enhancement.py FOLD_SA_MUL, HYRES_EPI_ROWSCALE: attn[p] * conv_nobias(multi) + bias) against the
+    unfused multiply-then-conv, on the full model's refine output at 2 x 64 x 96 (fp32: 1e-6 normwise, the
+    reassociation of one fp32 multiply; autocast with fp16 activations: 2e-3, the fp16 rounding of multi * attn the
+    unfused path stores)."""
+    import models.layers.enhancement as EH
+    from hyres_hip import ops as O
+    from models import ResidualJPEGCompression
+    from hyres_hip.weights import synthetic_state_dict
+    D = dev()
+    net = ResidualJPEGCompression(jpeg_quality=50)
+    torch.nn.Module.load_state_dict(net, synthetic_state_dict(net.state_dict()), strict=True)
+    net = net.to(D).eval()
+    g = torch.Generator().manual_seed(7)
+    x = (torch.randint(0, 256, (2, 3, 64, 96), generator=g).float() / 255)
+    jpeg, bpp = net.jpeg(x)
+    outs = {}
+    for fold in (False, True):
+        EH.FOLD_SA_MUL = fold
+        try:
+            ctx = torch.autocast("cuda", dtype=torch.float16) if autocast else torch.autocast("cuda", enabled=False)
+            with torch.no_grad(), ctx:
+                outs[fold] = net.forward_device(x.to(D), jpeg.to(D), bpp)["x_hat"].double().cpu()
+        finally:
+            EH.FOLD_SA_MUL = True
+    err = rel_err(outs[True], outs[False])
+    print("autocast" if autocast else "fp32", f"x_hat folded vs unfused: {err:.2e}")
+    assert err < (2e-3 if autocast else 1e-6)
