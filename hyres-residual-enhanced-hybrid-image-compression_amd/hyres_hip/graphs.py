@@ -109,10 +109,14 @@ class CapturedStep:
         torch.cuda.synchronize(dev)
 
     def close(self) -> None:
-        """Wait for any replay in flight, then destroy the graph and release what it recorded."""
+        """Wait for any replay in flight, then destroy the graph and release what it recorded. The outputs the
+        capture allocated (``out``, ``crit``) live in the graph's private memory pool: they are dropped BEFORE the
+        graph is reset, so the pool is released with no block of it still in use (resetting first left tensors of a
+        released pool to be freed later — a host-heap corruption the drop-in loop hit at the next epoch's start)."""
         g = getattr(self, "graph", None)
         if g is not None:
             torch.cuda.synchronize(self.x.device)
+            self.out, self.crit = None, None
             g.reset()
             self.graph = None
         self._prep_table = None

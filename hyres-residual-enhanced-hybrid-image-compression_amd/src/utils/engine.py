@@ -253,6 +253,7 @@ def train_one_epoch(model, criterion, train_dataloader, optimizer, aux_optimizer
                   f"\ty_Bpp loss: {meters['y_bpp_loss'].val:.4f} |\tz_Bpp loss: {meters['z_bpp_loss'].val:.4f} |"
                   f"\tMSE loss: {meters['mse_loss'].val:.3f} |"
                   f"\tAux loss: {float(aux_loss.detach()) if aux_loss is not None else 0.0:.2f}")
+    crit = None  # the last replay's static outputs live in the graph's pool: no reference may outlive close()
     graphed.close()
     _drain(pending, meters, nan_flags)
     print(f"Train epoch {epoch}: Average losses:\tLoss: {meters['loss'].avg:.3f} |"
