@@ -112,13 +112,14 @@ def cpu_baseline(args, budget_s):
                       f"itself cannot run here (compressai absent)"}
 
 
-# scripts/profile_round.sh r3z: the fp32 line's dominant kernel, and the AMP leg's dominant kernel from the same passes
+# scripts/check.sh <tag> pmc: the fp32 line's dominant kernel, and the AMP leg's dominant kernel from the same passes;
 # committed PMC summaries, newest first: the first one collected for the kernel being priced is used
-# (r4i: the bf16x6 weight-resident conv; r4b: the native one, both after the XCD fix)
+# (r5s: the bf16x6 weight-resident conv with its pipelined fragment reads; r4i: its round-4 build; r4b: the native one)
 PMC_TRAFFIC = [os.path.join(REPO, "profiles", f) for f in
-               os.environ.get("HYRES_PMC_TRAFFIC", "r4i_pmc_traffic.json,r4b_pmc_traffic.json").split(",")]
+               os.environ.get("HYRES_PMC_TRAFFIC",
+                              "r5s_pmc_traffic.json,r4i_pmc_traffic.json,r4b_pmc_traffic.json").split(",")]
 PMC_TRAFFIC_AMP = [os.path.join(REPO, "profiles", f) for f in
-                   os.environ.get("HYRES_PMC_TRAFFIC_AMP", "r4i_pmc_traffic_amp.json").split(",")]
+                   os.environ.get("HYRES_PMC_TRAFFIC_AMP", "r5s_pmc_traffic_amp.json,r4i_pmc_traffic_amp.json").split(",")]
 EAGER_TIMED = 3  # eager steps behind the live per-launch roofline timing
 
 
