@@ -20,7 +20,7 @@
 //       -Lhyres-residual-enhanced-hybrid-image-compression_amd/hyres_hip -lhyres_hip \
 //       -Wl,-rpath,'$ORIGIN/../hyres-residual-enhanced-hybrid-image-compression_amd/hyres_hip' \
 //       -o scripts/bf6_interference_repro
-//   scripts/bf6_interference_repro [reps] [delay_us between the conv's launch and the victims'] [wres|native|igemm|ru]
+//   scripts/bf6_interference_repro [reps] [delay_us between the conv's launch and the victims'] [wres|native|igemm|ru|wg1x1|wghalo]
 #include <hip/hip_runtime.h>
 
 #include <chrono>
@@ -114,8 +114,12 @@ int main(int argc, char** argv) {
     // the kernel beside the victims: wres (the bf16x6 weight-resident 3x3, both allocations), native (the fp32-MFMA
     // weight-resident 3x3: 184 VGPRs, a 144-VGPR hole), igemm (a dilation-2 3x3 on the bf16x6 implicit GEMM
     // conv_fwd_b6_kernel), ru (the AMP fused ResidualUnit ru_fused_f16_kernel: 232 VGPRs, a 48-VGPR hole)
+    // (round 5) wg1x1 / wghalo: the bf16x6 weight gradients — wgrad1x1_bf6_kernel<2, 1, 2, 2> (256 threads, one block
+    // per CU by LDS, 168 VGPRs: a 344-VGPR hole per SIMD) and wgrad_halo_bf6_kernel<1, 3, 1, 1> (2 blocks, 208 VGPRs:
+    // 96) — both convert with v_cvt_pk_bf16_f32 and run bf16 MFMAs, as the two guarded kernels do
     const char* hogname = argc > 3 ? argv[3] : "wres";
     const bool ru = strcmp(hogname, "ru") == 0;
+    const bool wg1 = strcmp(hogname, "wg1x1") == 0, wgh = strcmp(hogname, "wghalo") == 0, wg = wg1 || wgh;
     const int B = 2, H = 256, W = 256, C = 64;
     const long long nx = (long long)B * H * W * C;
     std::vector<float> hx(nx), hf(nx), hw(C * C * 9), hb(C);
@@ -168,6 +172,26 @@ int main(int argc, char** argv) {
         CK(hipMemcpy(rw3, h13.data(), h13.size() * 4, hipMemcpyHostToDevice));
         CH(hyres_ru_fused_f16_ok(B, H, W, 128) ? 0 : 1);
     }
+    // weight-gradient hogs: P = dY [2*256*256][Co], Q = X [2*256*256][Ci]
+    hyres_wgrad_desc wd;
+    float *wp = nullptr, *wq = nullptr, *wdst = nullptr;
+    void* wws = nullptr;
+    long long wwsb = 0, wdn = 0;
+    if (wg) {
+        const int Ci = wg1 ? 128 : 64, Co = 64, K = wg1 ? 1 : 3;
+        CH(hyres_wgrad_desc_conv2d(&wd, B, H, W, Ci, Ci, Co, Co, K, K, 1, K / 2, 1));
+        wd.sm = Ci * K * K;
+        wwsb = hyres_wgrad_workspace_bytes(&wd);
+        wdn = (long long)Co * Ci * K * K;
+        std::vector<float> hp((long long)B * H * W * Ci);
+        for (auto& v : hp) v = u(rng);
+        CK(hipMalloc(&wp, (long long)B * H * W * Co * 4));
+        CK(hipMalloc(&wq, (long long)B * H * W * Ci * 4));
+        CK(hipMalloc(&wdst, wdn * 4));
+        CK(hipMalloc(&wws, wwsb + 256));
+        CK(hipMemcpy(wp, hp.data(), (long long)B * H * W * Co * 4, hipMemcpyHostToDevice));
+        CK(hipMemcpy(wq, hp.data(), (long long)B * H * W * Ci * 4, hipMemcpyHostToDevice));
+    }
     hyres_epilogue e;
     memset(&e, 0, sizeof e);
     e.kind = HYRES_EPI_BIAS;
@@ -177,7 +201,9 @@ int main(int argc, char** argv) {
     CH(hyres_conv_tuning(HYRES_TUNE_F32_GEMM, strcmp(hogname, "native") == 0 ? 0 : 1, nullptr));
     char kname[128];
     auto conv = [&]() {
-        if (ru)
+        if (wg)
+            CH(hyres_conv_wgrad(&wd, wp, wq, wdst, nullptr, wws, wwsb, sa));
+        else if (ru)
             CH(hyres_ru_fused_f16(rx, ry, B, H, W, 128, rw1, db, dw, db, rw3, rb3, 1, nullptr, nullptr, sa));
         else
             CH(hyres_conv_forward(&g, dfeat, dw2, 9 * C, dy, &e, nullptr, 0, sa));
@@ -197,12 +223,15 @@ int main(int argc, char** argv) {
         CH(hyres_conv_tuning(HYRES_TUNE_WRES_BF6_GUARD, guard, nullptr));
         conv();
         CK(hipStreamSynchronize(sa));
-        CK(hipMemcpy(y0.data(), ru ? ry : dy, nx * 4, hipMemcpyDeviceToHost));
+        if (wg) CK(hipMemcpy(y0.data(), wdst, wdn * 4, hipMemcpyDeviceToHost));
+        else CK(hipMemcpy(y0.data(), ru ? ry : dy, nx * 4, hipMemcpyDeviceToHost));
         if (wres)
             printf("== conv 3x3 64->64 2x256x256 bf16x6 weight-resident, %s\n",
                    guard ? "guarded (256 VGPRs: no room beside it)" : "UNGUARDED (224 VGPRs: a 64-VGPR hole per SIMD)");
         else
-            printf("== %s\n", ru ? "fused ResidualUnit f16 (ru_fused_f16_kernel, 2x256x256x128)"
+            printf("== %s\n", wg1 ? "1x1 weight gradient 128->64 2x256x256 (wgrad1x1_bf6_kernel)"
+                               : wgh ? "3x3 weight gradient 64->64 2x256x256 (wgrad_halo_bf6_kernel)"
+                               : ru ? "fused ResidualUnit f16 (ru_fused_f16_kernel, 2x256x256x128)"
                                   : (dil == 2 ? "dilation-2 3x3 64->64 2x256x256 on the bf16x6 implicit GEMM"
                                               : "3x3 64->64 2x256x256 fp32-MFMA weight-resident (native)"));
         for (int kind = 4; kind >= 0; --kind) {
@@ -222,7 +251,8 @@ int main(int argc, char** argv) {
                 }
                 for (int v = 0; v < NV; ++v) launch(kind, dout + v * 4 * NOUT, sb);
                 CK(hipDeviceSynchronize());
-                CK(hipMemcpy(y1.data(), ru ? ry : dy, nx * 4, hipMemcpyDeviceToHost));
+                if (wg) CK(hipMemcpy(y1.data(), wdst, wdn * 4, hipMemcpyDeviceToHost));
+                else CK(hipMemcpy(y1.data(), ru ? ry : dy, nx * 4, hipMemcpyDeviceToHost));
                 conv_bad += memcmp(y0.data(), y1.data(), nx * 4) != 0;
                 for (int v = 0; v < NV; ++v)
                     CK(hipMemcpy(got.data() + v * 4 * NOUT, dout + v * 4 * NOUT, vsz[kind] * 4, hipMemcpyDeviceToHost));
