@@ -1117,9 +1117,15 @@ constexpr int WF_LDS_H = HALO_NPX * WF_PK;
 // resources — an absent operand gets an empty resource, so its loads return 0 with no branch — and consumed only
 // after that chunk's 144 MFMAs. The generic epi_store4 issued each load behind its own branch and waited on it
 // (~8 serialised HBM round trips per tile; +14 % on a 3x3 with a residual).
-__global__ __launch_bounds__(512, 2) void conv3x3_wres_f32_kernel(const ConvArgs a, int ntiles, int groups) {
+__global__ __launch_bounds__(512, 1) void conv3x3_wres_f32_kernel(const ConvArgs a, int ntiles, int groups) {
     __shared__ __attribute__((aligned(16))) float lds[WF_LDS_W + WF_LDS_H];
     __shared__ int2 tapoff[9];
+    // the whole VGPR file of its SIMDs (2 waves x 256; the code needs 182). Round 5 saw one run-to-run difference in
+    // tests/test_bf6_gpu.py::test_bf6_refine_branch_determinism in the subset that runs this kernel (native fp32 GEMM on
+    // MultiScaleRefine's scale 1) beside bf16x6 convs on another branch stream; of the kernels in that configuration it
+    // is the one 512-thread persistent kernel whose allocation left a hole (144 VGPRs) other waves could share — a mix
+    // only tests make (the fp32 GEMM mode is global). Free: its 140 KB of LDS already limits the CU to one block
+    asm volatile("" ::: "v255");
     float* const Ws = lds;
     float* const Hs = lds + WF_LDS_W;
     const hyres_conv_geom& g = a.g;
@@ -2084,6 +2090,140 @@ __global__ __launch_bounds__(256) void conv_narrow_kernel(const ConvArgs a) {
     }
 }
 
+// Co <= 4 with register blocking along W (round 5). conv_narrow_kernel is VALU-bound, not memory-bound: on
+// MultiScaleRefine's 3x3 64 -> 3 at bs16 256^2 (215 us) the PMC passes read 270 MB (1.0x the input) while each 4-pixel
+// wave pass issues ~307 VALU instructions of which 108 are the FMAs — the rest is per-pixel index decode, 9 tap
+// addresses and bounds, and the fold (profiles/r5u_narrow_pmc.txt); its per-pixel weight re-reads add 27
+// ds_read_b128. Here a lane group (Ci / 4 lanes, 4 channels each) computes a STRIP of 4 consecutive base pixels of
+// one row: the phase's taps form a kh x kw grid of consecutive (dh, dw) offsets (every 3x3 conv and every phase of
+// the 5x5 stride-2 transposed conv: checked on the host), so the strip needs kh x (kw + 3) input pixels, loaded once
+// (<= 18 float4 per lane) and each reused by up to 3 taps; the weights of the phase live in VGPRs (9 taps x Co float4,
+// zero for absent taps) for the whole launch; index decode and addressing once per strip; the 4 x Co partial sums
+// folded with xor-shuffles and stored by lanes (r, co). Needs Wq % 4 == 0 (strips never cross a row).
+// Same products per output as conv_narrow_kernel, different summation order (fp32 FMAs).
+constexpr int NSTRIP = 4;
+template <int CO, int S, bool XH = false>
+__global__ __launch_bounds__(256) void conv_narrow_strip_kernel(const ConvArgs a) {
+    constexpr int CI = 64 * S, LP = 16 * S, GROUPS = 256 / LP, XES = XH ? 2 : 4;
+    constexpr int STRIPS = NARROW_PIX / NSTRIP, PASSES = STRIPS / GROUPS;
+    const hyres_conv_geom& g = a.g;
+    const int tid = threadIdx.x, lq = tid % LP, grp = tid / LP;
+    const int phase = blockIdx.y;
+    const int ntap = g.ntap[phase], tap0 = g.tap0[phase];
+    // the phase's taps as a kh x kw grid listed row-major with steps of +-1 in dh and dw (host-checked: the conv's
+    // taps ascend, the transposed conv's phases descend); (r, c) below count from the grid's smallest (dh, dw)
+    const int da = g.dh[tap0], wa = g.dw[tap0], dz = g.dh[tap0 + ntap - 1], wz = g.dw[tap0 + ntap - 1];
+    const int kh = (da > dz ? da - dz : dz - da) + 1, kw = (wa > wz ? wa - wz : wz - wa) + 1;
+    const int dh0 = min(da, dz), dw0 = min(wa, wz);
+    const bool rh = da > dz, rw = wa > wz;  // descending rows / columns
+    float4 w[3][3][CO];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const int t = (rh ? kh - 1 - r : r) * kw + (rw ? kw - 1 - c : c);
+#pragma unroll
+            for (int co = 0; co < CO; ++co)
+                w[r][c][co] = (r < kh && c < kw) ? ld4(a.w2 + (long long)co * a.ldw + (tap0 + t) * CI + 4 * lq)
+                                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    const int HqWq = g.Hq * g.Wq;
+    int bx = blockIdx.x;
+    if (a.xcd) {  // XCD-aware pixel-tile order, as conv_narrow_kernel
+        const int nb = gridDim.x, q = nb >> 3, r = nb & 7, x = bx & 7;
+        bx = x * q + min(x, r) + (bx >> 3);
+    }
+    const int b0 = (bx * NARROW_PIX) / HqWq;
+    const long long img = (long long)g.Hi * g.Wi * g.ldx;
+    const long long xrem = ((long long)g.B - b0) * img * XES;
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(reinterpret_cast<const char*>(a.x) + (long long)b0 * img * XES), (short)0,
+        (int)(xrem < 0x7FFFFFF0LL ? xrem : 0x7FFFFFF0LL), 0x00020000);
+    for (int it = 0; it < PASSES; ++it) {
+        const int m = bx * NARROW_PIX + (it * GROUPS + grp) * NSTRIP;  // first pixel of the strip
+        const bool ok = m < a.M;
+        const int mm = ok ? m : 0;
+        const int b = mm / HqWq, rr = mm - b * HqWq;
+        const int i = rr / g.Wq, j = rr - (rr / g.Wq) * g.Wq;
+        const int base = (int)((b - b0) * img);
+        const int ih0 = i * g.ish + dh0, iw0 = j * g.isw + dw0;
+        std::conditional_t<XH, half4_t, float4> xv[3][NSTRIP + 2];
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int c = 0; c < NSTRIP + 2; ++c) {
+                const int ih = ih0 + r, iw = iw0 + c;
+                const bool in = ok && r < kh && c < kw + NSTRIP - 1 && (unsigned)ih < (unsigned)g.Hi &&
+                                (unsigned)iw < (unsigned)g.Wi;
+                const int off = in ? (base + (ih * g.Wi + iw) * g.ldx + 4 * lq) * XES : (int)0x80000000;
+                if constexpr (XH) xv[r][c] = __builtin_bit_cast(half4_t, __builtin_amdgcn_raw_buffer_load_b64(xr, off, 0, 0));
+                else xv[r][c] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
+            }
+        float acc[NSTRIP][CO];
+#pragma unroll
+        for (int p = 0; p < NSTRIP; ++p)
+#pragma unroll
+            for (int co = 0; co < CO; ++co) acc[p][co] = 0.f;
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int c = 0; c < NSTRIP + 2; ++c) {
+                float4 xf;
+                if constexpr (XH) xf = make_float4((float)xv[r][c].x, (float)xv[r][c].y, (float)xv[r][c].z, (float)xv[r][c].w);
+                else xf = xv[r][c];
+#pragma unroll
+                for (int p = 0; p < NSTRIP; ++p) {
+                    const int t = c - p;  // this input column is tap column t of strip pixel p
+                    if (t < 0 || t > 2) continue;
+#pragma unroll
+                    for (int co = 0; co < CO; ++co) {
+                        acc[p][co] = fmaf(xf.x, w[r][t][co].x, acc[p][co]);
+                        acc[p][co] = fmaf(xf.y, w[r][t][co].y, acc[p][co]);
+                        acc[p][co] = fmaf(xf.z, w[r][t][co].z, acc[p][co]);
+                        acc[p][co] = fmaf(xf.w, w[r][t][co].w, acc[p][co]);
+                    }
+                }
+            }
+#pragma unroll
+        for (int p = 0; p < NSTRIP; ++p)
+#pragma unroll
+            for (int co = 0; co < CO; ++co) {
+                float v = acc[p][co];
+#pragma unroll
+                for (int off = LP / 2; off > 0; off >>= 1) v += __shfl_xor(v, off);
+                acc[p][co] = v;
+            }
+        // lane q < NSTRIP * CO stores pixel q / CO, channel q % CO
+        float v = 0.f;
+#pragma unroll
+        for (int p = 0; p < NSTRIP; ++p)
+#pragma unroll
+            for (int co = 0; co < CO; ++co) v = lq == p * CO + co ? acc[p][co] : v;
+        const int sp = lq / CO, sc = lq - sp * CO;
+        if (ok && lq < NSTRIP * CO && m + sp < a.M) {
+            const long long pix = (long long)(b * g.Ho + i * g.osh + g.oph[phase]) * g.Wo + (j + sp) * g.osw + g.opw[phase];
+            epi_store(a.e, a.y, g.ldy, pix, sc, v, epi_channel(a.e, sc));
+        }
+    }
+}
+
+// the strip kernel's host-side conditions: every phase's taps a row-major grid of consecutive offsets, <= 3 x 3,
+// unit input stride along W, strips inside rows
+static bool narrow_strip_ok(const hyres_conv_geom* g) {
+    if (g_tune[13] == 0 || g->Wq % NSTRIP != 0 || g->isw != 1) return false;
+    for (int p = 0; p < g->nphase; ++p) {
+        const int n = g->ntap[p], t0 = g->tap0[p];
+        if (n < 1) return false;
+        const int da = g->dh[t0], wa = g->dw[t0], dz = g->dh[t0 + n - 1], wz = g->dw[t0 + n - 1];
+        const int kh = std::abs(da - dz) + 1, kw = std::abs(wa - wz) + 1;
+        const int sh = dz >= da ? 1 : -1, sw = wz >= wa ? 1 : -1;
+        if (kh > 3 || kw > 3 || kh * kw != n) return false;
+        for (int t = 0; t < n; ++t)
+            if (g->dh[t0 + t] != da + sh * (t / kw) || g->dw[t0 + t] != wa + sw * (t % kw)) return false;
+    }
+    return true;
+}
+
 static bool narrow_ok(const hyres_conv_geom* g) {
     if (g->Co > 4 || (g->Ci != 64 && g->Ci != 128)) return false;
     int maxtap = 0;
@@ -2093,6 +2233,17 @@ static bool narrow_ok(const hyres_conv_geom* g) {
 
 template <int CO>
 static void launch_narrow(const ConvArgs& a, dim3 grid, hipStream_t st) {
+    if (narrow_strip_ok(&a.g)) {  // hyres_conv_tuning key 13 (default 1)
+        const bool h = (a.e.io_f16 & HYRES_IO_X16) != 0;
+        if (a.g.Ci == 64) {
+            if (h) hipLaunchKernelGGL((conv_narrow_strip_kernel<CO, 1, true>), grid, dim3(256), 0, st, a);
+            else hipLaunchKernelGGL((conv_narrow_strip_kernel<CO, 1>), grid, dim3(256), 0, st, a);
+        } else {
+            if (h) hipLaunchKernelGGL((conv_narrow_strip_kernel<CO, 2, true>), grid, dim3(256), 0, st, a);
+            else hipLaunchKernelGGL((conv_narrow_strip_kernel<CO, 2>), grid, dim3(256), 0, st, a);
+        }
+        return;
+    }
     if (a.e.io_f16 & HYRES_IO_X16) {
         if (a.g.Ci == 64) hipLaunchKernelGGL((conv_narrow_kernel<CO, 1, true>), grid, dim3(256), 0, st, a);
         else hipLaunchKernelGGL((conv_narrow_kernel<CO, 2, true>), grid, dim3(256), 0, st, a);
@@ -2319,7 +2470,7 @@ static void dense_taps(hyres_conv_geom* g, int KH, int KW, int sgn, int dil, int
 // key 7: fp32 GEMMs bf16x6 (0: native fp32 MFMA); key 8: fp16 streaming 1x1; key 9: the bf16x6 weight-resident 3x3's
 // whole-VGPR-file guard (0 = diagnostic unguarded build, DESIGN §4 "Cross-kernel interference"); key 10: the bf16x6
 // streaming 1x1 kernel (0 = those layers on the tiled implicit GEMM, for A/B)
-int g_tune[13] = {-1, -1, -1, -1, -1, -1, -1, 1, 1, 1, 1, 1, 1};
+int g_tune[14] = {-1, -1, -1, -1, -1, -1, -1, 1, 1, 1, 1, 1, 1, 1};
 
 }  // namespace hyres
 
@@ -2775,7 +2926,7 @@ static long long plan_ws_bytes(const hyres_conv_geom* g, const ConvPlan& p) {
 }
 
 int hyres_conv_tuning(int key, int value, int* old) {
-    HY_REQUIRE(key >= 0 && key < 13, HYRES_E_ARG, "conv_tuning: key %d", key);
+    HY_REQUIRE(key >= 0 && key < 14, HYRES_E_ARG, "conv_tuning: key %d", key);
     if (old) *old = g_tune[key];
     g_tune[key] = value;
     return ok();
@@ -2947,7 +3098,8 @@ int hyres_conv_kernel_name(const hyres_conv_geom* g, const hyres_epilogue* e, in
     HY_REQUIRE(g && e && buf && n > 0, HYRES_E_ARG, "conv_kernel_name: bad args");
     const ConvChoice ch = choose_conv(g, e, true);
     if (ch.narrow) {
-        snprintf(buf, n, "conv_narrow_kernel<%d, %d>", std::min(g->Co, 4), g->Ci == 64 ? 1 : 2);
+        snprintf(buf, n, "%s<%d, %d>", narrow_strip_ok(g) ? "conv_narrow_strip_kernel" : "conv_narrow_kernel",
+                 std::min(g->Co, 4), g->Ci == 64 ? 1 : 2);
         return 0;
     }
     if (ch.mode == 0 && wres32_ok(g, e)) {

@@ -179,6 +179,8 @@ int hyres_conv_plan(const hyres_conv_geom* g, const hyres_epilogue* e, int* tile
 #define HYRES_TUNE_WRES_BF6_V 12      /* conv3x3_wres_bf6_kernel variant: bit 0 (default 1) each tap's fragments read
                                        * one tap ahead, bit 1 static priority 1 for waves 4..7; 0: reads as the compiler
                                        * schedules them (A/B) */
+#define HYRES_TUNE_NARROW_STRIP 13    /* 1 (default): Co <= 4 convs whose phases' taps are <= 3x3 grids, Wq % 4 == 0, on
+                                       * conv_narrow_strip_kernel (4-pixel strips, weights in VGPRs); 0: conv_narrow_kernel */
 int hyres_conv_tuning(int key, int value, int* old);
 
 /* Weight gradient:  dW[t][m][n] = sum_q P[q][m] * Q[shift_t(q)][n]  over a base grid q (B,Hq,Wq).

@@ -551,3 +551,58 @@ def test_refine_sa_mul_fold_matches_unfused(autocast):
     err = rel_err(outs[True], outs[False])
     print("autocast" if autocast else "fp32", f"x_hat folded vs unfused: {err:.2e}")
     assert err < (2e-3 if autocast else 1e-6)
+
+
+@pytest.mark.parametrize("kind,B,Ci,H,W,f16x", [
+    ("conv3x3", 3, 64, 67, 132, False),    # MultiScaleRefine.fusion[2] (64 -> 3), partial last block
+    ("conv3x3", 2, 128, 45, 76, False),
+    ("deconv5x5", 2, 128, 33, 48, False),  # g_s's last deconv (128 -> 3: four phases, descending tap grids)
+    ("conv3x3", 2, 64, 40, 72, True),      # fp16 activations (autocast inference)
+    ("deconv5x5", 2, 128, 20, 36, True),
+])
+def test_narrow_strip_kernel_matches_fp64(kind, B, Ci, H, W, f16x):
+    """conv_narrow_strip_kernel (Co <= 4, 4-pixel strips with the inputs loaded once per strip and the weights in
+    VGPRs, hyres_conv_tuning key 13 = 1) against float64 torch and no worse than twice conv_narrow_kernel (key 13 = 0),
+    for MultiScaleRefine's 3x3 64 -> 3 and g_s's 5x5 stride-2 deconv 128 -> 3, fp32 and fp16 inputs, Co in {3, 1},
+    plus the accumulate epilogue (y += conv) the input-gradient path uses."""
+    import ctypes
+    from hyres_hip import _lib as L
+    from hyres_hip import ops as O
+    D = dev()
+    for Co in (3, 1):
+        x = _rand((B, Ci, H, W), 81).to(D)
+        if f16x:
+            x = x.half().float()
+        if kind == "conv3x3":
+            w = _rand((Co, Ci, 3, 3), 82, (Ci * 9) ** -0.5).to(D)
+            b = _rand((Co,), 83, 0.1).to(D)
+            ref = F.conv2d(x.double(), w.double(), b.double(), padding=1)
+        else:
+            w = _rand((Ci, Co, 5, 5), 82, (Ci * 25 / 4) ** -0.5).to(D)
+            b = _rand((Co,), 83, 0.1).to(D)
+            ref = F.conv_transpose2d(x.double(), w.double(), b.double(), stride=2, padding=2, output_padding=1)
+        errs, names = {}, {}
+        for key in (1, 0):
+            old = ctypes.c_int(0)
+            L.call("hyres_conv_tuning", 13, key, ctypes.byref(old))
+            try:
+                xn = O.to_nhwc(x)
+                if f16x:
+                    xn = O.Node(xn.v.half(), rg=False)
+                if kind == "conv3x3":
+                    yn = O.conv2d(None, xn, torch.nn.Parameter(w), b, pad=1)
+                    g = O._geom("hyres_geom_conv2d", B, H, W, Ci, Ci, Co, Co, 3, 3, 1, 1, 1)
+                else:
+                    yn = O.deconv2d(None, xn, torch.nn.Parameter(w), b)
+                    g = O._geom("hyres_geom_deconv2d", B, H, W, Ci, Ci, Co, Co, 5, 2, 1)
+                e = L.Epilogue()
+                e.io_f16 = L.IO_X16 if f16x else 0
+                names[key] = O.conv_variant(g, e, False)
+                y = O.to_nchw(yn).double()
+                torch.cuda.synchronize()
+            finally:
+                L.call("hyres_conv_tuning", 13, old.value, None)
+            errs[key] = rel_err(y.cpu(), ref.cpu())
+        print(kind, B, Ci, H, W, f16x, Co, names, f"error vs fp64: strip {errs[1]:.2e}, per-pixel {errs[0]:.2e}")
+        assert names[1].startswith("conv_narrow_strip_kernel") and names[0].startswith("conv_narrow_kernel"), names
+        assert errs[1] < 1e-5 and errs[1] <= 2 * errs[0] + 1e-9

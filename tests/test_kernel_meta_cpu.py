@@ -53,7 +53,7 @@ def test_other_cvt_mfma_persistent_kernels_take_the_whole_vgpr_file(meta):
     assert k["alloc"] == 256 and kernel_meta.residency(k)["hole_vgprs"] == 0, k
     (d,) = _find(meta, "ru_fused_f16_kernelILb0E")  # diagnostic build
     assert d["alloc"] == 232, d
-    for k in _find(meta, "conv3x3_wres_f16_kernel"):
+    for k in _find(meta, "conv3x3_wres_f16_kernel") + _find(meta, "conv3x3_wres_f32_kernel"):
         assert k["alloc"] == 256 and kernel_meta.residency(k)["hole_vgprs"] == 0, k
 
 

@@ -162,7 +162,7 @@ def _native_routing(L, e, g3, g3b, _geom, conv_variant):
     g1c = _geom("hyres_geom_conv2d", 16, 128, 128, 128, 128, 64, 64, 1, 1, 1, 0, 1)
     assert conv_variant(g1c, e, False) == "conv1x1_stream_kernel<2, 16>"
     gn = _geom("hyres_geom_conv2d", 16, 256, 256, 64, 64, 3, 3, 3, 3, 1, 1, 1)
-    assert conv_variant(gn, e, False) == "conv_narrow_kernel<3, 1>"
+    assert conv_variant(gn, e, False) == "conv_narrow_strip_kernel<3, 1>"
     gs = _geom("hyres_geom_conv2d", 16, 256, 256, 3, 3, 64, 64, 3, 3, 1, 1, 1)  # Ci = 3: scalar path
     assert conv_variant(gs, e, False) == "conv_fwd_kernel<1, 1, 2, 2, 2, false, false>"
     e.square_input = 1
