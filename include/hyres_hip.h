@@ -181,6 +181,8 @@ int hyres_conv_plan(const hyres_conv_geom* g, const hyres_epilogue* e, int* tile
                                        * schedules them (A/B) */
 #define HYRES_TUNE_NARROW_STRIP 13    /* 1 (default): Co <= 4 convs whose phases' taps are <= 3x3 grids, Wq % 4 == 0, on
                                        * conv_narrow_strip_kernel (4-pixel strips, weights in VGPRs); 0: conv_narrow_kernel */
+#define HYRES_TUNE_WRES32 14          /* 1 (default): fp32 3x3 Ci = 64 convs on the weight-resident kernels
+                                       * (conv3x3_wres_bf6 / _f32); 0: the implicit GEMM (A/B) */
 int hyres_conv_tuning(int key, int value, int* old);
 
 /* Weight gradient:  dW[t][m][n] = sum_q P[q][m] * Q[shift_t(q)][n]  over a base grid q (B,Hq,Wq).

@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--Co", type=int, default=64)
     ap.add_argument("--K", type=int, default=3)
     ap.add_argument("--stride", type=int, default=1)
+    ap.add_argument("--dil", type=int, default=1)
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--relu", action="store_true")
     ap.add_argument("--res", action="store_true", help="fused residual add (RU / RBB tail)")
@@ -56,13 +57,13 @@ def main():
     import contextlib
     with ctx, (O.f16_region() if a.io16 else contextlib.nullcontext()):
         for _ in range(3):
-            y = O.conv2d(None, x, w, b, stride=a.stride, pad=a.K // 2, act=act, res=res)
+            y = O.conv2d(None, x, w, b, stride=a.stride, pad=a.dil * (a.K // 2), dil=a.dil, act=act, res=res)
         torch.cuda.synchronize()
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(a.iters):
-            y = O.conv2d(None, x, w, b, stride=a.stride, pad=a.K // 2, act=act, res=res, out=y)
+            y = O.conv2d(None, x, w, b, stride=a.stride, pad=a.dil * (a.K // 2), dil=a.dil, act=act, res=res, out=y)
         e1.record()
     torch.cuda.synchronize()
     us = 1000 * e0.elapsed_time(e1) / a.iters
@@ -70,7 +71,7 @@ def main():
     flops = 2.0 * a.B * Ho * Ho * a.K * a.K * a.Ci * a.Co
     es = 2.0 if a.io16 else 4.0
     byts = es * (a.B * a.H * a.H * a.Ci + a.B * Ho * Ho * a.Co * (2 if a.res else 1)) + 4.0 * a.K * a.K * a.Ci * a.Co
-    print(f"conv B{a.B} {a.H}x{a.H}x{a.Ci} -> {Ho}x{Ho}x{a.Co} K{a.K} s{a.stride}{' +res' if a.res else ''}{' f16' if a.f16 else ''}{' io16' if a.io16 else ''}{' tiled' if a.no_stream_h or a.no_stream_b6 else ''}{f' cm{a.stream_cm}' if a.stream_cm != 1 else ''}{f' wres-v{a.wres_v}' if a.wres_v else ''}{' bf16x6' if a.bf6 else ''}: {us:.1f} us, "
+    print(f"conv B{a.B} {a.H}x{a.H}x{a.Ci} -> {Ho}x{Ho}x{a.Co} K{a.K} s{a.stride}{f' d{a.dil}' if a.dil > 1 else ''}{' +res' if a.res else ''}{' f16' if a.f16 else ''}{' io16' if a.io16 else ''}{' tiled' if a.no_stream_h or a.no_stream_b6 else ''}{f' cm{a.stream_cm}' if a.stream_cm != 1 else ''}{f' wres-v{a.wres_v}' if a.wres_v else ''}{' bf16x6' if a.bf6 else ''}: {us:.1f} us, "
           f"{flops / us / 1e6:.1f} TFLOP/s, {byts / us / 1e3:.0f} GB/s")
 
 
