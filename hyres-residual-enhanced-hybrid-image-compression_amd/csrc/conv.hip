@@ -1296,9 +1296,13 @@ __device__ __forceinline__ int bf6_off(int r, int k) { return r * 16 + ((((k >> 
 // register set (hand-issued ds_read_b128: the compiler sank its own reads next to their MFMAs, waiting on each) —
 // 133 -> 125 us at 128^2, 481 -> 453 us at 256^2 (profiles/r5i_wres_variants_micro.txt); bit 1 — waves 4..7 at static
 // priority 1: no effect (kept for the A/B). Every variant forms the same MFMAs in the same order (bit-identical)
-template <bool GUARD, int V>
+// D (round 5): the halo radius = the taps' largest offset, 1 (3x3) or 2 (MultiScaleRefine's dilation-2 3x3s,
+// enhancement.py:44-51): (4 + 2D) x (64 + 2D) halo pixels; at D = 2 the three halo planes are 52 KB, 159 KB of LDS in all
+template <bool GUARD, int V, int D = 1>
 __global__ __launch_bounds__(512, 1) void conv3x3_wres_bf6_kernel(const ConvArgs a, int ntiles, int groups) {
-    __shared__ __attribute__((aligned(16))) __bf16 lds[3 * BF6_WPL + 3 * BF6_HPL];
+    constexpr int HW = HALO_TW + 2 * D, NPX = (HALO_R + 2 * D) * HW;  // halo row length, pixels
+    constexpr int HPL = NPX * 16, HE = NPX * 4, HV = (HE + 511) / 512;  // bf16 per halo plane, float4 per chunk
+    __shared__ __attribute__((aligned(16))) __bf16 lds[3 * BF6_WPL + 3 * HPL];
     __shared__ int2 tapoff[9];
     __bf16* const Ws = lds;
     __bf16* const Hs = lds + 3 * BF6_WPL;
@@ -1348,38 +1352,38 @@ __global__ __launch_bounds__(512, 1) void conv3x3_wres_bf6_kernel(const ConvArgs
     };
     // halo chunks are prefetched TWO steps ahead (two register sets, alternating, as conv3x3_wres_f16_kernel): one
     // 16-channel step is 54 MFMAs per wave (~1.7k cycles), too short to cover an HBM load issued one step ahead
-    auto hload = [&](float4 (&hreg)[BF6_HV], int step) {  // step = 4 * tile + chunk (16 channels)
+    auto hload = [&](float4 (&hreg)[HV], int step) {  // step = 4 * tile + chunk (16 channels)
         int b, i0, j0;
         tile_of(step >> 2, b, i0, j0);
         const int c = step & 3;
         const int base = b * (int)img;
 #pragma unroll
-        for (int v = 0; v < BF6_HV; ++v) {
+        for (int v = 0; v < HV; ++v) {
             const int e = tid + 512 * v;
             const int px = e >> 2, c4 = e & 3;
-            const int hr = px / HALO_HW, hc = px - hr * HALO_HW;
-            const int ih = i0 - 1 + hr, iw = j0 - 1 + hc;
-            const bool ok = e < BF6_HE && (unsigned)ih < (unsigned)g.Hi && (unsigned)iw < (unsigned)g.Wi;
+            const int hr = px / HW, hc = px - hr * HW;
+            const int ih = i0 - D + hr, iw = j0 - D + hc;
+            const bool ok = e < HE && (unsigned)ih < (unsigned)g.Hi && (unsigned)iw < (unsigned)g.Wi;
             const int off = ok ? (base + (ih * g.Wi + iw) * g.ldx + 16 * c + 4 * c4) * 4 : (int)0x80000000;
             hreg[v] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
         }
     };
     // the next step's halo is split into its bf16 pieces in registers DURING this step's MFMAs (hsplit, independent
     // VALU work the scheduler interleaves with them); between the two barriers only the LDS stores remain (hput)
-    bf16x4_t sp[BF6_HV][3];
-    auto hsplit = [&](const float4 (&hreg)[BF6_HV]) {
+    bf16x4_t sp[HV][3];
+    auto hsplit = [&](const float4 (&hreg)[HV]) {
 #pragma unroll
-        for (int v = 0; v < BF6_HV; ++v) bf6_split4(hreg[v], sp[v][0], sp[v][1], sp[v][2]);
+        for (int v = 0; v < HV; ++v) bf6_split4(hreg[v], sp[v][0], sp[v][1], sp[v][2]);
     };
     auto hput = [&]() {
 #pragma unroll
-        for (int v = 0; v < BF6_HV; ++v) {
+        for (int v = 0; v < HV; ++v) {
             const int e = tid + 512 * v;
-            if (e < BF6_HE) {
+            if (e < HE) {
                 const int o = bf6_off(e >> 2, 4 * (e & 3));
                 *reinterpret_cast<bf16x4_t*>(&Hs[o]) = sp[v][0];
-                *reinterpret_cast<bf16x4_t*>(&Hs[BF6_HPL + o]) = sp[v][1];
-                *reinterpret_cast<bf16x4_t*>(&Hs[2 * BF6_HPL + o]) = sp[v][2];
+                *reinterpret_cast<bf16x4_t*>(&Hs[HPL + o]) = sp[v][1];
+                *reinterpret_cast<bf16x4_t*>(&Hs[2 * HPL + o]) = sp[v][2];
             }
         }
     };
@@ -1395,7 +1399,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_wres_bf6_kernel(const ConvArgs
     const __amdgpu_buffer_rsrc_t r_old = opnd_rsrc(e.accumulate ? a.y : nullptr, npix * g.ldy * 4);
     float4 ebias[4], eres[4], emask[4], eold[4];
     const int steps = mytiles * 4;
-    float4 hA[BF6_HV], hB[BF6_HV];
+    float4 hA[HV], hB[HV];
     if (steps > 0) {
         hload(hA, 0);
         hsplit(hA);
@@ -1404,7 +1408,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_wres_bf6_kernel(const ConvArgs
     if (steps > 1) hload(hB, 1);
     __syncthreads();
     // step s: the set that held step s's halo (stored) receives step s + 2; the other holds step s + 1
-    auto body = [&](int s, float4 (&hl)[BF6_HV], const float4 (&hs)[BF6_HV]) {
+    auto body = [&](int s, float4 (&hl)[HV], const float4 (&hs)[HV]) {
         const int k = s >> 2, c = s & 3;
         int b, i0, j0;
         tile_of(k, b, i0, j0);
@@ -1439,15 +1443,15 @@ __global__ __launch_bounds__(512, 1) void conv3x3_wres_bf6_kernel(const ConvArgs
             };
             auto frag = [&](int t, bf16x8_t (&wv)[3], bf16x8_t (&xv)[3]) {
                 const int wrow = (c * 9 + t) * 32 + lr;
-                const int hrow = (orow + 1 + g.dh[t]) * HALO_HW + 32 * ph + lr + 1 + g.dw[t];
+                const int hrow = (orow + D + g.dh[t]) * HW + 32 * ph + lr + D + g.dw[t];
                 const unsigned wo = wbase + 2u * (wrow * 16 + (((lh ^ (wrow >> 3)) & 1) << 3));
                 const unsigned ho = hbase + 2u * (hrow * 16 + (((lh ^ (hrow >> 3)) & 1) << 3));
                 wv[2] = rd(wo + 4u * BF6_WPL);
                 xv[0] = rd(ho);
                 wv[1] = rd(wo + 2u * BF6_WPL);
-                xv[1] = rd(ho + 2u * BF6_HPL);
+                xv[1] = rd(ho + 2u * HPL);
                 wv[0] = rd(wo);
-                xv[2] = rd(ho + 4u * BF6_HPL);
+                xv[2] = rd(ho + 4u * HPL);
             };
             bf16x8_t fw[2][3], fx[2][3];
             hsplit(hs);  // unconditional (unused after the last step): no branch inside the tap loop
@@ -1478,15 +1482,15 @@ __global__ __launch_bounds__(512, 1) void conv3x3_wres_bf6_kernel(const ConvArgs
         for (int t = 0; t < 9; ++t) {
             const int2 o = tapoff[t];
             const int wrow = (c * 9 + t) * 32 + lr;                                    // A: weights, row = co
-            const int hrow = (orow + 1 + o.x) * HALO_HW + 32 * ph + lr + 1 + o.y;     // B: halo, row = pixel
+            const int hrow = (orow + D + o.x) * HW + 32 * ph + lr + D + o.y;          // B: halo, row = pixel
             const int wo = wrow * 16 + (((lh ^ (wrow >> 3)) & 1) << 3);
             const int ho = hrow * 16 + (((lh ^ (hrow >> 3)) & 1) << 3);
             const bf16x8_t w0 = *reinterpret_cast<const bf16x8_t*>(&Ws[wo]);
             const bf16x8_t w1 = *reinterpret_cast<const bf16x8_t*>(&Ws[BF6_WPL + wo]);
             const bf16x8_t w2 = *reinterpret_cast<const bf16x8_t*>(&Ws[2 * BF6_WPL + wo]);
             const bf16x8_t x0 = *reinterpret_cast<const bf16x8_t*>(&Hs[ho]);
-            const bf16x8_t x1 = *reinterpret_cast<const bf16x8_t*>(&Hs[BF6_HPL + ho]);
-            const bf16x8_t x2 = *reinterpret_cast<const bf16x8_t*>(&Hs[2 * BF6_HPL + ho]);
+            const bf16x8_t x1 = *reinterpret_cast<const bf16x8_t*>(&Hs[HPL + ho]);
+            const bf16x8_t x2 = *reinterpret_cast<const bf16x8_t*>(&Hs[2 * HPL + ho]);
             // the small cross products first, the leading one last
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w2, x0, acc, 0, 0, 0);
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1, x1, acc, 0, 0, 0);
@@ -2470,7 +2474,7 @@ static void dense_taps(hyres_conv_geom* g, int KH, int KW, int sgn, int dil, int
 // key 7: fp32 GEMMs bf16x6 (0: native fp32 MFMA); key 8: fp16 streaming 1x1; key 9: the bf16x6 weight-resident 3x3's
 // whole-VGPR-file guard (0 = diagnostic unguarded build, DESIGN §4 "Cross-kernel interference"); key 10: the bf16x6
 // streaming 1x1 kernel (0 = those layers on the tiled implicit GEMM, for A/B)
-int g_tune[15] = {-1, -1, -1, -1, -1, -1, -1, 1, 1, 1, 1, 1, 1, 1, 1};
+int g_tune[16] = {-1, -1, -1, -1, -1, -1, -1, 1, 1, 1, 1, 1, 1, 1, 1, 1};
 
 }  // namespace hyres
 
@@ -2673,6 +2677,13 @@ static int launch_wres16(const ConvArgs& a, hipStream_t st) {
     return HY_LAUNCH_CHECK("conv3x3_wres_f16_kernel");
 }
 
+// the 3x3's largest tap offset (the weight-resident halo radius)
+static int wres_halo(const hyres_conv_geom* g) {
+    int d = 0;
+    for (int t = 0; t < 9; ++t) d = std::max(d, std::max(std::abs(g->dh[t]), std::abs(g->dw[t])));
+    return d;
+}
+
 // conv3x3_wres_f32_kernel: fp32 operands, the halo16 geometry with Ci == 64 and Co % 32 == 0, >= 2 tiles per
 // block
 static bool wres32_ok(const hyres_conv_geom* g, const hyres_epilogue* e) {
@@ -2687,8 +2698,8 @@ static bool wres32_ok(const hyres_conv_geom* g, const hyres_epilogue* e) {
     if (g->ish != 1 || g->isw != 1 || g->Hi != g->Ho || g->Wi != g->Wo || g->Hq != g->Ho || g->Wq != g->Wo ||
         g->Wo % HALO_TW != 0)
         return false;
-    for (int t = 0; t < 9; ++t)
-        if (g->dh[t] < -1 || g->dh[t] > 1 || g->dw[t] < -1 || g->dw[t] > 1) return false;
+    // halo radius 1, or 2 for the bf16x6 kernel (dilation-2 3x3s: its D = 2 build)
+    if (wres_halo(g) > (g_tune[7] == 1 && g_tune[9] != 0 ? 2 : 1)) return false;
     const long long tiles = (long long)g->B * ((g->Ho + HALO_R - 1) / HALO_R) * (g->Wo / HALO_TW);
     const int groups = g->Co / 32;
     return tiles >= 2LL * wres_blocks(groups) && (long long)g->B * g->Hi * g->Wi * g->ldx * 4 < 0x7FFFFFF0LL;
@@ -2704,7 +2715,9 @@ static int launch_wres32(const ConvArgs& a, hipStream_t st) {
     const int per = wres_blocks(groups);
     if (wres_bf6()) {
         const dim3 grid(per * groups);
-        if (g_tune[9] == 0)  // diagnostic only: the allocation that let other kernels' waves share its SIMDs
+        if (wres_halo(&g) == 2)  // dilation 2 (wres32_ok admits it only with the guard on): the pipelined build
+            hipLaunchKernelGGL((conv3x3_wres_bf6_kernel<true, 1, 2>), grid, dim3(512), 0, st, a, ntiles, groups);
+        else if (g_tune[9] == 0)  // diagnostic only: the allocation that let other kernels' waves share its SIMDs
             hipLaunchKernelGGL((conv3x3_wres_bf6_kernel<false, 0>), grid, dim3(512), 0, st, a, ntiles, groups);
         else if (g_tune[12] == 1)
             hipLaunchKernelGGL((conv3x3_wres_bf6_kernel<true, 1>), grid, dim3(512), 0, st, a, ntiles, groups);
@@ -2927,7 +2940,7 @@ static long long plan_ws_bytes(const hyres_conv_geom* g, const ConvPlan& p) {
 }
 
 int hyres_conv_tuning(int key, int value, int* old) {
-    HY_REQUIRE(key >= 0 && key < 15, HYRES_E_ARG, "conv_tuning: key %d", key);
+    HY_REQUIRE(key >= 0 && key < 16, HYRES_E_ARG, "conv_tuning: key %d", key);
     if (old) *old = g_tune[key];
     g_tune[key] = value;
     return ok();

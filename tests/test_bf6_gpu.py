@@ -606,3 +606,59 @@ def test_narrow_strip_kernel_matches_fp64(kind, B, Ci, H, W, f16x):
         print(kind, B, Ci, H, W, f16x, Co, names, f"error vs fp64: strip {errs[1]:.2e}, per-pixel {errs[0]:.2e}")
         assert names[1].startswith("conv_narrow_strip_kernel") and names[0].startswith("conv_narrow_kernel"), names
         assert errs[1] < 1e-5 and errs[1] <= 2 * errs[0] + 1e-9
+
+
+@pytest.mark.parametrize("B,H,W,act", [(4, 128, 128, "relu"), (1, 256, 384, "prelu"), (1, 256, 384, "relu"),
+                                       (4, 128, 128, "prelu"), (2, 128, 256, "prelu")])
+def test_wres_bf6_dilation2_matches_fp64(B, H, W, act):
+    """The weight-resident bf16x6 3x3 at halo radius 2 (conv3x3_wres_bf6_kernel<true, 1, 2>: MultiScaleRefine's
+    dilation-2 convs, enhancement.py:44-51) — forward with residual and the input gradient (a dilation-2 conv over dY)
+    — against float64 torch, and no worse than twice the implicit GEMM it replaces (hyres_conv_tuning key 14 = 0)."""
+    import ctypes
+    from hyres_hip import _lib as L
+    from hyres_hip import ops as O
+    D = dev()
+    C = 64
+    x = _rand((B, C, H, W), 91)
+    w = _rand((C, C, 3, 3), 92, (C * 9) ** -0.5)
+    b = _rand((C,), 93, 0.1)
+    r = _rand((B, C, H, W), 94)
+    gy = _rand((B, C, H, W), 95)
+    xr = x.double().requires_grad_()
+    pre = F.conv2d(xr, w.double(), b.double(), padding=2, dilation=2) + r.double()
+    yr = F.relu(pre) if act == "relu" else torch.where(pre >= 0, pre, 0.25 * pre)
+    yr.backward(gy.double())
+    slope = torch.tensor([0.25], device=D)
+    a = L.ACT_RELU if act == "relu" else L.ACT_PRELU
+    res, names = {}, {}
+    for key in (1, 0):
+        old = ctypes.c_int(0)
+        L.call("hyres_conv_tuning", 14, key, ctypes.byref(old))
+        try:
+            tape = O.Tape()
+            xn = O.to_nhwc(x.to(D), rg=True)
+            rn = O.to_nhwc(r.to(D))
+            wd = torch.nn.Parameter(w.to(D))
+            yn = O.conv2d(tape, xn, wd, b.to(D), pad=2, dil=2, act=a, slope=slope if act == "prelu" else None, res=rn)
+            yn.set_grad(O.nchw_grad_to_nhwc(gy.to(D)))
+            tape.backward()
+            torch.cuda.synchronize()
+            g = O._geom("hyres_geom_conv2d", B, H, W, C, C, C, C, 3, 3, 1, 2, 2)
+            e = L.Epilogue()
+            e.kind, e.act = L.EPI_BIAS, a
+            names[key] = O.conv_variant(g, e, False)
+            res[key] = (O.to_nchw(yn).double().cpu(), O.to_nchw_grad(xn).double().cpu())
+        finally:
+            L.call("hyres_conv_tuning", 14, old.value, None)
+    ey = {k: rel_err(v[0], yr.detach()) for k, v in res.items()}
+    # dx against the float64 conv input-gradient of dY masked by OUR activation: at 6.3M outputs a few land within
+    # fp32 rounding of 0, where a float64-masked reference flips whole gradient entries (seen: 2.5e-2 for both kernels)
+    def dx_ref(y):
+        gp = gy.double() * torch.where(y > 0, 1.0, 0.0 if act == "relu" else 0.25)
+        return torch.nn.grad.conv2d_input(x.shape, w.double(), gp, padding=2, dilation=2)
+    eg = {k: rel_err(v[1], dx_ref(v[0])) for k, v in res.items()}
+    print("dx vs float64-masked reference:", {k: f"{rel_err(v[1], xr.grad):.2e}" for k, v in res.items()})
+    print(B, H, W, act, names, f"y vs fp64: wres {ey[1]:.2e}, igemm {ey[0]:.2e}; dx: wres {eg[1]:.2e}, igemm {eg[0]:.2e}")
+    assert names[1] == "conv3x3_wres_bf6_kernel" and names[0] != names[1], names
+    assert ey[1] < 1e-5 and ey[1] <= 2 * ey[0] + 1e-9
+    assert eg[1] < 1e-5 and eg[1] <= 2 * eg[0] + 1e-9

@@ -35,7 +35,7 @@ def _find(meta, fragment):
 def test_wres_bf6_takes_the_whole_vgpr_file(meta):
     # GUARD = true: every instantiation a default launch can pick (the variants of hyres_conv_tuning key 12)
     ks = _find(meta, "conv3x3_wres_bf6_kernelILb1E")
-    assert len(ks) == 4
+    assert len(ks) == 5  # key 12 variants 0..3 and the dilation-2 build of variant 1
     for k in ks:
         r = kernel_meta.residency(k)
         assert k["threads"] == 512 and k["alloc"] == 256, k
