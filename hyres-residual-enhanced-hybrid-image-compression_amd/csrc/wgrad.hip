@@ -1846,7 +1846,11 @@ static WgradPlan wgrad_plan(const hyres_wgrad_desc* d) {
     const int tb = g_tune[3] > 0 ? g_tune[3] : (small ? 4096 : 2048);
     const int mc0 = g_tune[4] > 0 ? g_tune[4] : ((small && kt == KT && d->ntaps > 1) ? 4 : 8);
     const int mc = std::max(1, mc0 * KT / kt);
-    const int ms = g_tune[6] > 0 ? g_tune[6] : 512;
+    // <= 256 splits (<= 64 on the small grids): past that the split slab's write + reduce costs more than the
+    // extra blocks buy — step 32.79 -> 32.54 ms, AMP 19.10 -> 18.76 ms against 512 everywhere (isolated, kernel +
+    // reduce: 128^2 3x3 64->64 143 -> 137 us, 32^2 3x3 96->96 51.6 -> 43.4 us; one exception measured, 256^2 1x1
+    // 64->64 132 -> 160 us, but 512 splits for the 1x1s only gave no step gain; profiles/r5z_wgrad_split_ab.txt)
+    const int ms = g_tune[6] > 0 ? g_tune[6] : (small ? 64 : 256);
     const long long slab_cap = std::max<long long>(4, (16LL << 20) / ((long long)d->ntaps * d->M * d->N));
     const long long want = std::min<long long>(std::max<long long>(1, (tb + tiles - 1) / tiles), slab_cap);
     const long long maxsplit = std::max<long long>(1, p.nchunks / mc);
