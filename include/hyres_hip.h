@@ -158,7 +158,7 @@ int hyres_conv_plan(const hyres_conv_geom* g, const hyres_epilogue* e, int* tile
 #define HYRES_TUNE_WGRAD_BLOCKS 3     /* weight gradients: split-K target block count */
 #define HYRES_TUNE_WGRAD_MINCHUNKS 4  /* minimum 32-pixel chunks per split */
 #define HYRES_TUNE_WGRAD_NT 5         /* 1: no tap grouping (one tap per block column group) */
-#define HYRES_TUNE_WGRAD_MAXSPLIT 6   /* maximum split count */
+#define HYRES_TUNE_WGRAD_MAXSPLIT 6   /* maximum split count (default 256; 64 on <= 16384-pixel grids) */
 #define HYRES_TUNE_F32_GEMM 7         /* GEMM of the fp32 convolutions (forward, input-gradient, and the halo-staged /
                                        * 1x1 weight gradients): 1 bf16x6 (default: each fp32 operand split into 3 bf16
                                        * pieces, the 6 cross products with i + j <= 2, fp32 accumulation — per-product
