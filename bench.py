@@ -14,11 +14,15 @@ from __future__ import annotations
 
 import argparse
 import ctypes
+import faulthandler
 import json
 import math
 import os
 import sys
 import time
+
+# a host-side crash prints the Python stacks of every thread to stderr (DESIGN §13 "Open")
+faulthandler.enable()
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.join(REPO, "hyres-residual-enhanced-hybrid-image-compression_amd")
