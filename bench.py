@@ -237,6 +237,7 @@ def eval_legs(net, x, jpeg, jpeg_bpp, args, reps=20):
         ems = (time.time() - t0) * 1000 / 5
         npx = xe.shape[0] * xe.shape[2] * xe.shape[3]
         res[tag] = {"ms": round(ms, 3), "mpix_s": round(npx / ms / 1e3, 3), "eager_ms": round(ems, 3)}
+        cap.close()  # no replay output is held here (graphs.py lifetime rule)
         del cap
     # configs[4] precision: inference under torch.autocast(float16) -> fp16-operand f16 MFMA convs
     with torch.autocast("cuda", dtype=torch.float16):
@@ -250,6 +251,7 @@ def eval_legs(net, x, jpeg, jpeg_bpp, args, reps=20):
             ms = (time.time() - t0) * 1000 / reps
             npx = xe.shape[0] * xe.shape[2] * xe.shape[3]
             res[tag] = {"ms": round(ms, 3), "mpix_s": round(npx / ms / 1e3, 3)}
+            cap.close()
             del cap
     # A/B of the fused ResidualUnit / RBB inference kernel (csrc/ru_fused.hip): the bench batch under autocast with
     # the three-conv chain instead
@@ -264,6 +266,7 @@ def eval_legs(net, x, jpeg, jpeg_bpp, args, reps=20):
                 cap.replay()
             torch.cuda.synchronize()
             ms = (time.time() - t0) * 1000 / reps
+            cap.close()
             del cap
     finally:
         O.RU_FUSED = True
@@ -317,6 +320,7 @@ def amp_leg(net, opt, aux_opt, crit, x, jpeg, jpeg_bpp, args):
     torch.cuda.synchronize()
     ms = (time.time() - t0) * 1000 / args.steps
     loss = float(c["loss"].detach())
+    c = None  # a replay output (graph pool): dropped before the graph is closed
     B, _, H, W = x.shape
     # dominant f16 kernel, live (one eager AMP step, HIP events per launch, as for the fp32 line)
     O.KernelTimer.reset()
@@ -339,6 +343,8 @@ def amp_leg(net, opt, aux_opt, crit, x, jpeg, jpeg_bpp, args):
         opt.zero_grad()
     torch.cuda.synchronize()
     ms_a = (time.time() - t0) * 1000 / nrep
+    del out, cc  # the eager step's outputs (regular pool) — nothing of the graph's is held now
+    cap.close()
     del cap
     # round-4 A/B on the same box: the step with the unfused ResidualUnits, and with fp32 activation gradients and
     # the unfused ResidualUnits (round 3's AMP path) — the gains of the fused RU forward and of fp16 gradients
@@ -532,6 +538,8 @@ def analysis_synthesis(net, x, reps):
             g.replay()
         torch.cuda.synchronize()
         ms = (time.time() - t0) * 1000 / reps
+        g.reset()  # the capture's g_a / g_s outputs were dropped inside .hip(): nothing of its pool is held
+        del g
     ledger = B * 1.836e9
     res = {"ms": round(ms, 3), "ledger_bytes": ledger, "hbm_frac": round(ledger / (ms * 1e-3) / 8e12, 4),
            "tflops": round(B * 40.66e9 / (ms * 1e-3) / 1e12, 2),
@@ -691,6 +699,7 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.time() - t0
     loss_val = float(c["loss"].detach())
+    c = None  # replay outputs live in the graph's pool: none may be held when the graph is closed
     # dominant-kernel roofline, measured live with HIP events (on the stream each conv launch goes to:
     # torch's current stream, also inside the branch streams) around every conv_fwd_kernel launch of one
     # eager step of the same workload right after the timed region (a graph replay cannot carry
@@ -733,6 +742,8 @@ def main():
 
 
     if rank != 0:
+        if graphed is not None:
+            graphed.close()
         if dist:
             tdist.destroy_process_group()
         return
@@ -795,6 +806,8 @@ def main():
     host = None
     if world == 1 and not args.no_host_jpeg:
         host = host_jpeg_legs(net, step_eager_cpu, x_cpu, step_graph_cpu=step_graph_cpu if graphed is not None else None)
+    if graphed is not None:
+        graphed.close()  # every CapturedStep of this run is closed explicitly (DESIGN §13 "Open")
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, args.cpu_baseline_seconds)

@@ -362,6 +362,17 @@ __global__ __launch_bounds__(256 * G) void wgrad1x1_kernel(const WgradArgs a) {
     const int tid = threadIdx.x & 255, grp = threadIdx.x >> 8;
     float* const Psm = Psm_all + grp * (2 * KT * PP);
     float* const Qsm = Qsm_all + grp * (2 * KT * PQ);
+    // G > 1 (512 threads, LDS-limited to 1-2 blocks per CU): the blocks take the whole VGPR file of their SIMDs, as
+    // every persistent 512-thread kernel does (DESIGN §4 "Cross-kernel interference": the observed hogs were 512-thread,
+    // LDS-limited blocks leaving a hole other kernels' waves ran in, with or without v_cvt_pk). 1 block per CU: 2 waves
+    // x 256; 2 blocks: 4 waves x 128. Costs nothing: LDS, not registers, sets the occupancy.
+    if constexpr (G > 1) {
+        constexpr int lds_bytes = (int)sizeof(float) * G * 2 * KT * (PP + PQ);
+        constexpr int blocks = 163840 / lds_bytes;
+        static_assert(blocks >= 1 && blocks <= 2, "wgrad1x1_kernel<G>1>: 1 or 2 blocks per CU");
+        if constexpr (blocks == 2) asm volatile("" ::: "v127");
+        else asm volatile("" ::: "v255");
+    }
     const int bid = blockIdx.x;
     const int lb = (bid & 7) * (gridDim.x >> 3) + (bid >> 3);  // XCD-aware order, as wgrad_kernel
     if (lb >= a.nblocks) return;

@@ -26,11 +26,34 @@ Graph-safety of the captured region:
 from __future__ import annotations
 
 import contextlib
+import gc
+import weakref
 from typing import Callable, Optional
 
 import torch
 
 from . import ops as O
+
+
+class GraphOutputsAlive(RuntimeError):
+    """``CapturedStep.close()`` found a replay output (a tensor in the graph's private pool) still referenced by
+    the caller: the graph is NOT reset. Drop every reference to the replay's outputs, then close again."""
+
+
+def _tensors(obj):
+    """Every tensor in a (nested) dict / list / tuple of replay outputs."""
+    if isinstance(obj, torch.Tensor):
+        yield obj
+    elif isinstance(obj, dict):
+        for v in obj.values():
+            yield from _tensors(v)
+    elif isinstance(obj, (list, tuple)):
+        for v in obj:
+            yield from _tensors(v)
+
+
+# graphs whose close() found live outputs while running as a finalizer: kept here (not reset) until the process ends
+_KEPT = []
 
 
 def _prepare_noise(net: torch.nn.Module, device: torch.device) -> None:
@@ -102,21 +125,41 @@ class CapturedStep:
         # main thread captures (no collective is ever inside the graph)
         with torch.cuda.graph(self.graph, capture_error_mode=capture_error_mode):
             self.out, self.crit = run()
+        # weak references to every output the capture allocated (in the graph's private pool); the static inputs the
+        # forward passes through (jpeg_decoded, jpeg_bpp_loss) belong to this object and are not tracked
+        own = {t.untyped_storage().data_ptr() for t in (self.x, self.jpeg, self.bpp)}
+        self._out_refs = [weakref.ref(t) for t in _tensors((self.out, self.crit))
+                          if t.untyped_storage().data_ptr() not in own]
         O.bump_weight_epoch()  # eager calls must not reuse buffers only the graph writes
         # ... and the scratch buffers its kernels were recorded with: an eager call that grows a workspace slot
         # replaces the slot's tensor, and the old one must outlive the graph
         self._ws_keep = list(O.Workspace._bufs.values())
         torch.cuda.synchronize(dev)
 
+    def live_outputs(self) -> int:
+        """How many tensors the capture allocated are still alive (held by this object or by a caller)."""
+        return sum(1 for r in getattr(self, "_out_refs", ()) if r() is not None)
+
     def close(self) -> None:
-        """Wait for any replay in flight, then destroy the graph and release what it recorded. The outputs the
-        capture allocated (``out``, ``crit``) live in the graph's private memory pool: they are dropped BEFORE the
-        graph is reset, so the pool is released with no block of it still in use (resetting first left tensors of a
-        released pool to be freed later — a host-heap corruption the drop-in loop hit at the next epoch's start)."""
+        """Wait for any replay in flight, then destroy the graph and release what it recorded.
+
+        The outputs the capture allocated (``out``, ``crit``, returned by every ``replay()``) live in the graph's
+        private memory pool. The lifetime rule: a caller drops every reference to them BEFORE ``close()``, so the pool
+        is released with no block of it in use. ``close()`` enforces it: after dropping its own references it checks
+        the weak references taken at capture (cycles collected first); if any output is still alive it raises
+        ``GraphOutputsAlive`` and leaves the graph and its pool untouched (the step can no longer be replayed; call
+        ``close()`` again once the references are gone)."""
         g = getattr(self, "graph", None)
         if g is not None:
             torch.cuda.synchronize(self.x.device)
             self.out, self.crit = None, None
+            if self.live_outputs():
+                gc.collect()  # an autograd cycle (output -> grad_fn -> ctx -> output) is not a caller reference
+            n = self.live_outputs()
+            if n:
+                raise GraphOutputsAlive(
+                    f"CapturedStep.close(): {n} replay output tensor(s) still referenced; drop them before close() "
+                    "(the graph was not reset)")
             g.reset()
             self.graph = None
         self._prep_table = None
@@ -125,11 +168,14 @@ class CapturedStep:
     def __del__(self):
         # A finalizer may run while ANOTHER graph is being captured (garbage collection inside the capture): a
         # device synchronize there would invalidate that capture. Owners release graphs with close(); here the
-        # graph is only torn down when no capture is in progress, else it is left to the process's end.
+        # graph is only torn down when no capture is in progress, else it is left to the process's end. If a caller
+        # still holds replay outputs, the graph (and what it recorded) is parked in _KEPT instead of being reset.
         try:
             if torch.cuda.is_current_stream_capturing():
                 return
             self.close()
+        except GraphOutputsAlive:
+            _KEPT.append((self.graph, self._prep_table, self._ws_keep))
         except Exception:  # noqa: BLE001 - interpreter shutdown
             pass
 

@@ -28,26 +28,98 @@ def _tool(name: str) -> str:
 
 
 def available() -> bool:
-    return all(os.path.exists(_tool(t)) for t in ("llvm-objcopy", "clang-offload-bundler", "llvm-readelf"))
+    return all(os.path.exists(_tool(t)) for t in ("llvm-objcopy", "clang-offload-bundler", "llvm-readelf",
+                                                   "llvm-objdump"))
+
+
+def _code_objects(so_path: str, td: str, arch: str) -> list[str]:
+    """Unbundle the gfx950 code object of every translation unit in the library's .hip_fatbin into ``td``."""
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    fat = os.path.join(td, "fat")
+    subprocess.run([_tool("llvm-objcopy"), f"--dump-section=.hip_fatbin={fat}", so_path, os.path.join(td, "x")],
+                   check=True, capture_output=True)
+    blob = open(fat, "rb").read()
+    starts = [m.start() for m in re.finditer(re.escape(magic), blob)]  # one bundle per translation unit
+    cos = []
+    for i, s0 in enumerate(starts):
+        part, co = os.path.join(td, f"b{i}"), os.path.join(td, f"co{i}")
+        with open(part, "wb") as f:
+            f.write(blob[s0:starts[i + 1] if i + 1 < len(starts) else len(blob)])
+        subprocess.run([_tool("clang-offload-bundler"), "--unbundle", "--type=o", f"--input={part}",
+                        f"--targets=hipv4-amdgcn-amd-amdhsa--{arch}", f"--output={co}"], check=True,
+                       capture_output=True)
+        cos.append(co)
+    return cos
+
+
+def disassembly(so_path: str, arch: str = "gfx950") -> dict[str, list[str]]:
+    """{mangled kernel name: its instructions (one string each, comments stripped)} from llvm-objdump."""
+    out: dict[str, list[str]] = {}
+    with tempfile.TemporaryDirectory() as td:
+        for co in _code_objects(so_path, td, arch):
+            txt = subprocess.run([_tool("llvm-objdump"), "-d", "--no-show-raw-insn", co], check=True,
+                                 capture_output=True, text=True).stdout
+            cur = None
+            for line in txt.splitlines():
+                m = re.match(r"^[0-9a-f]+ <(.*)>:$", line)
+                if m:
+                    cur = out.setdefault(m.group(1), [])
+                    continue
+                ins = line.split("//")[0].strip()
+                if cur is not None and ins and not ins.endswith(":"):
+                    cur.append(ins)
+    return out
+
+
+_REG = re.compile(r"(?<![\w])([va])(?:\[(\d+):(\d+)\]|(\d+)(?!\w))")
+
+
+def _regs(text: str) -> set:
+    out = set()
+    for m in _REG.finditer(text):
+        if m.group(4) is not None:
+            out.add((m.group(1), int(m.group(4))))
+        else:
+            out.update((m.group(1), r) for r in range(int(m.group(2)), int(m.group(3)) + 1))
+    return out
+
+
+def lds_read_hazards(instrs: list[str]) -> list[tuple[str, str]]:
+    """Instructions that touch (read or overwrite) the destination VGPRs of an LDS read that has not been waited for.
+
+    Linear scan in program order: every LGKM operation (ds_*, s_load*, s_buffer_load*, s_sendmsg) joins an in-order
+    queue; ``s_waitcnt lgkmcnt(N)`` retires all but the N most recent; an instruction whose operands overlap the
+    destination of a still-queued ds_read is a hazard. This is the check a hand-issued ``ds_read_b128`` (inline asm,
+    waited for by a hand-counted ``s_waitcnt``, conv.hip conv3x3_wres_bf6_kernel V & 1) needs: the compiler treats an
+    asm output as ready at once and could place a copy of it before the wait. Compiler-issued reads pass by
+    construction, which makes the scan of every kernel its own calibration."""
+    q: list[tuple[str, set]] = []
+    bad = []
+    for ins in instrs:
+        op = ins.split()[0]
+        if op.startswith("s_waitcnt"):
+            m = re.search(r"lgkmcnt\((\d+)\)", ins)
+            if m:
+                n = int(m.group(1))
+                del q[:max(0, len(q) - n)]
+            continue
+        operands = ins[len(op):]
+        rs = _regs(operands)
+        for src, dst in q:
+            if dst & rs:
+                bad.append((src, ins))
+        if op.startswith(("ds_read", "ds_load")):
+            q.append((ins, _regs(operands.split(",")[0])))
+        elif op.startswith(("ds_", "s_load", "s_buffer_load", "s_sendmsg")):
+            q.append((ins, set()))
+    return bad
 
 
 def kernels(so_path: str, arch: str = "gfx950") -> list[dict]:
     """One dict per kernel: name, vgpr, agpr, accum_offset-free allocation, lds, threads, sgpr, scratch."""
-    magic = b"__CLANG_OFFLOAD_BUNDLE__"
     docs = []
     with tempfile.TemporaryDirectory() as td:
-        fat = os.path.join(td, "fat")
-        subprocess.run([_tool("llvm-objcopy"), f"--dump-section=.hip_fatbin={fat}", so_path, os.path.join(td, "x")],
-                       check=True, capture_output=True)
-        blob = open(fat, "rb").read()
-        starts = [m.start() for m in re.finditer(re.escape(magic), blob)]  # one bundle per translation unit
-        for i, s0 in enumerate(starts):
-            part, co = os.path.join(td, f"b{i}"), os.path.join(td, f"co{i}")
-            with open(part, "wb") as f:
-                f.write(blob[s0:starts[i + 1] if i + 1 < len(starts) else len(blob)])
-            subprocess.run([_tool("clang-offload-bundler"), "--unbundle", "--type=o", f"--input={part}",
-                            f"--targets=hipv4-amdgcn-amd-amdhsa--{arch}", f"--output={co}"], check=True,
-                           capture_output=True)
+        for co in _code_objects(so_path, td, arch):
             notes = subprocess.run([_tool("llvm-readelf"), "--notes", co], check=True, capture_output=True,
                                    text=True).stdout
             m = re.search(r"^\s*---\n(.*?)^\s*\.\.\.\s*$", notes, re.S | re.M)

@@ -159,6 +159,7 @@ def test_graphed_train_step_bs16_bit_identical_run_to_run(amp):
             assert not bad, f"replay {r}: {len(bad)} gradients differ"
     finally:
         net.residual_model.noise.injected = None
+        c = None  # the replay's outputs live in the graph's pool: dropped before close()
         cap.close()
 
 
@@ -181,4 +182,5 @@ def test_graphed_autocast_eval_bs16_bit_identical_run_to_run():
                 continue
             assert all(torch.equal(a, b) for a, b in zip(cur, first)), r
     finally:
+        out = None
         cap.close()

@@ -949,6 +949,8 @@ def test_captured_eval_matches_eager_and_reference():
     torch.cuda.synchronize()
     assert torch.equal(out["x_hat"], eager2["x_hat"])
     assert torch.equal(out["likelihoods"]["y"], eager2["likelihoods"]["y"])
+    out = None
+    cap.close()
 
 
 def test_captured_train_step_matches_eager():
@@ -991,6 +993,58 @@ def test_captured_train_step_matches_eager():
     l1 = float(cap2.replay()[1]["loss"])
     l2 = float(cap2.replay()[1]["loss"])
     assert l1 != l2 and abs(l1 - l2) < 0.05 * abs(l1)
+    cc = None
+    cap.close()
+    cap2.close()
+
+
+def test_captured_step_close_refuses_live_outputs():
+    """The graph-lifetime rule (hyres_hip/graphs.py CapturedStep.close): a replay's outputs live in the
+    graph's private pool, so close() with one of them still referenced raises GraphOutputsAlive and leaves the graph
+    alone (no reset: the held tensor keeps its values); once the reference is dropped close() resets the graph. The
+    static inputs the forward passes through (jpeg_decoded, jpeg_bpp_loss) are the step's own and are not tracked.
+    Reference loop the rule serves: /root/reference/src/utils/engine.py:28-56."""
+    from hyres_hip.graphs import CapturedStep, GraphOutputsAlive
+    from hyres_hip.loss import RateDistortionLoss
+    g = load_npz("hyres_train_b2_64.npz")
+    net, _ = _hip_model()
+    net.train()
+    D = dev()
+    x, j = g["x"].to(D), g["jpeg_decoded"].to(D)
+    crit = RateDistortionLoss(lmbda=0.045, alpha=0)
+    params = [p for p in net.parameters() if p.requires_grad]
+
+    def zero():
+        for p in params:
+            if p.grad is not None:
+                p.grad.zero_()
+
+    cap = CapturedStep(net, x, j, 0.25, criterion=crit, zero_grad=zero)
+    assert cap.live_outputs() > 5  # x_hat, both likelihoods, residual(s), the loss terms
+    out, c = cap.replay()
+    torch.cuda.synchronize()
+    loss = c["loss"]  # one held output is enough
+    want = float(loss)
+    x_hat = out["x_hat"].clone()
+    del out, c
+    with pytest.raises(GraphOutputsAlive):
+        cap.close()
+    assert cap.graph is not None, "close() must not reset the graph while an output is referenced"
+    assert cap.live_outputs() == 1
+    assert float(loss) == want  # the pool was not released under the held tensor
+    del loss
+    cap.close()
+    assert cap.graph is None and cap.live_outputs() == 0
+    # eval capture: outputs include the step's own static jpeg buffer, which close() does not count
+    net.eval()
+    cap = CapturedStep(net, x, j, 0.25)
+    out, _ = cap.replay()
+    jd = out["jpeg_decoded"]
+    assert jd.data_ptr() == cap.jpeg.data_ptr()
+    del out
+    cap.close()
+    assert cap.graph is None
+    assert x_hat.isfinite().all()
 
 
 def test_captured_step_survives_eager_step_with_new_layouts_and_bigger_workspace():
@@ -1055,6 +1109,7 @@ def test_captured_step_survives_eager_step_with_new_layouts_and_bigger_workspace
     for p, gr in zip(params, grads_r):
         assert torch.equal(p.grad, gr), p.shape
     rm.noise.injected = None
+    del cc
     cap.close()
 
 
@@ -1628,10 +1683,12 @@ def test_amp_matches_reference_autocast_fixture():
     # fp32 than the reference AMP (the rule of every other tensor above). refine.act_in moves with the last bits of
     # the refine's 64->3 output: 0.354 with conv_narrow_kernel, 1.10 with conv_narrow_strip_kernel (same fp32
     # products, another summation order; both within 1e-5 of fp64), against the reference AMP's 3.86
-    # (profiles/r5_ampfix_act_in_slope.log)
+    # (profiles/r5_ampfix_act_in_slope.log). Fixed bars, independent of the kernel that happens to run: refine.act_in
+    # <= 1.5 (the reference AMP run itself is 3.86 from fp32 there), every other slope < 0.5
     sl = [(own[n][0], n, own[n][1]) for n in slopes if n in own]
     print("PReLU slopes, distance from fp32 (this AMP, reference AMP):", sorted(sl, reverse=True))
-    assert all(e < 0.5 or e <= r for e, _, r in sl), sl
+    assert any(n == "refine.act_in.weight" for _, n, _ in sl), sorted(slopes)
+    assert all(e <= (1.5 if n == "refine.act_in.weight" else 0.5) for e, n, _ in sl), sl
     wrong = {(n, v) for n, v, h, h32 in signs if n not in slopes and h * h32 < 0}
     assert dval[len(dval) // 2][0] < 0.05 and len(wrong) <= max(2, nsamp // 100), (dval[:5], sorted(wrong)[:5])
     # every other tensor, whole, against this build's fp32 gradient (itself pinned to the reference's fp32 fixtures and
