@@ -103,6 +103,11 @@ __device__ __forceinline__ void epi_store(const hyres_epilogue& e, float* y, int
             v = (e.kind == HYRES_EPI_GDN) ? xv * (1.0f / sqrtf(nv)) : xv * sqrtf(nv);
             break;
         }
+        case HYRES_EPI_SA_BWD: {  // SpatialAttention's mean / max backward: + d mean / C, + d max at the argmax
+            const float* gm = e.aux0 + pix * e.ld0;
+            v = v + gm[0] + (n == reinterpret_cast<const int*>(e.aux2)[pix] ? gm[1] : 0.f);
+            break;
+        }
         case HYRES_EPI_GDN_BWD:
         case HYRES_EPI_IGDN_BWD: {  // H (AMP fp16 gradients): x, the incoming gradient and the norm all fp16
             const float xv = ld_aux<H>(e, e.aux0, pix * e.ld0 + n);
@@ -172,6 +177,14 @@ __device__ __forceinline__ void epi_store4(const hyres_epilogue& e, float* y, in
 #pragma unroll
             for (int c = 0; c < 4; ++c)
                 o[c] = (e.kind == HYRES_EPI_GDN) ? xv[c] * (1.0f / sqrtf(nv[c])) : xv[c] * sqrtf(nv[c]);
+            break;
+        }
+        case HYRES_EPI_SA_BWD: {  // as in epi_store: (acc + d mean / C) + (channel == argmax ? d max : 0)
+            const float* gm = e.aux0 + pix * e.ld0;
+            const float ga = gm[0], gx = gm[1];
+            const int mi = reinterpret_cast<const int*>(e.aux2)[pix];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) o[c] = o[c] + ga + (n + c == mi ? gx : 0.f);
             break;
         }
         case HYRES_EPI_GDN_BWD:
@@ -2985,8 +2998,10 @@ int hyres_conv_forward(const hyres_conv_geom* g, const float* x, const float* w2
     a.slab = nullptr;
     {
         auto al = [](const void* p, int ld) { return p == nullptr || (aligned16(p) && ld % 4 == 0); };
+        // HYRES_EPI_SA_BWD reads aux0 ([P][2]) and aux2 (argmax) one scalar per pixel: no alignment needed
+        const bool sa = e->kind == HYRES_EPI_SA_BWD;
         a.vec4 = g->Co % 4 == 0 && al(y, g->ldy) && al(e->bias, 4) && al(e->res, e->ldres) && al(e->out2, e->ldo2) &&
-                 al(e->aux0, e->ld0) && al(e->aux1, e->ld1) && al(e->aux2, e->ld2);
+                 (sa || al(e->aux0, e->ld0)) && al(e->aux1, e->ld1) && (sa || al(e->aux2, e->ld2));
     }
     {
         const long long npo = (long long)g->B * g->Ho * g->Wo;
@@ -3036,6 +3051,10 @@ int hyres_conv_forward(const hyres_conv_geom* g, const float* x, const float* w2
     if (e->kind == HYRES_EPI_ROWSCALE)
         HY_REQUIRE(e->aux1 && !e->square_input && !e->accumulate, HYRES_E_ARG,
                    "conv: ROWSCALE needs aux1 (per-pixel scale), no square_input / accumulate");
+    if (e->kind == HYRES_EPI_SA_BWD)
+        HY_REQUIRE(e->aux0 && e->aux2 && e->ld0 >= 2 && !e->square_input && e->act == HYRES_ACT_NONE && !e->res &&
+                       !e->out2 && !(e->io_f16 & 2),
+                   HYRES_E_ARG, "conv: SA_BWD needs aux0 ([P][ld0 >= 2]) and aux2 (argmax), no act / res / out2, fp32 Y");
     hipStream_t st = as_stream(s);
     if (ch.narrow) {
         a.nsplit = 1;

@@ -485,8 +485,10 @@ __global__ void sa_bwd_logit_kernel(const float* x, const float* gy, const float
     }
 }
 // bwd 2: g_pooled2 = transpose conv; weight-grad partials per block (wave shuffles, one barrier)
+// (C > 0: the mean's gradient is stored divided by C, the form HYRES_EPI_SA_BWD adds per channel)
 __global__ __launch_bounds__(256) void sa_bwd_conv_kernel(const float* glogit, const float* pooled2, const float* w,
-                                                          float* gpooled2, float* wpart, int B, int H, int W) {
+                                                          float* gpooled2, float* wpart, int B, int H, int W,
+                                                          int C = 0) {
     __shared__ float ws[98];
     __shared__ float red[4][98];
     if (threadIdx.x < 98) ws[threadIdx.x] = w[threadIdx.x];
@@ -521,7 +523,7 @@ __global__ __launch_bounds__(256) void sa_bwd_conv_kernel(const float* glogit, c
                 }
             }
         }
-        gpooled2[i * 2 + 0] = g0;
+        gpooled2[i * 2 + 0] = C > 0 ? g0 / (float)C : g0;
         gpooled2[i * 2 + 1] = g1;
     }
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -569,6 +571,76 @@ __global__ void sa_bwd_x_kernel(const float* gy, const float* attn, const float*
         v.z = v.z * a + gavg + (c + 2 == mi ? gmax : 0.f);
         v.w = v.w * a + gavg + (c + 3 == mi ? gmax : 0.f);
         stv4<G>(gx, 4 * i, v);
+    }
+}
+
+// ---- training with SpatialAttention's multiply folded into the fusion 1x1 (HYRES_EPI_ROWSCALE forward):
+// h = PReLU(pre), pre = attn[p] * (W multi)[p] + b. Per pixel (16 lanes, a float4 of the C <= 64 channels each):
+// gp = PReLU-backward(gy); gs = attn * gp (the fusion 1x1's weight- and input-gradient operand: d W = sum gs x multi,
+// d multi = W^T gs, exactly the reference's gradients through multi * attn); glogit = (1 - attn) * sum_o gp (pre - b),
+// which is attn (1 - attn) * sum_o gp z with attn z = pre - b (the gradient at the attention logit, no division by
+// attn). Per-block partials of d bias (sum gp) and d slope (sum over pre <= 0 of gy pre, prelu_bwd4_kernel's order).
+__global__ __launch_bounds__(256) void sa_fold_bwd_kernel(const float* pre, int ldpre, const float* gy, int ldg,
+                                                          const float* attn, const float* bias, const float* slope,
+                                                          float* gs, float* glogit, float* part, long long P, int C) {
+    __shared__ float rb[16][68];
+    __shared__ float rs[256];
+    const float a = slope[0];
+    const int l16 = threadIdx.x & 15, grp = threadIdx.x >> 4;
+    const int c = 4 * l16;
+    const bool cok = c < C;
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 b = cok ? *reinterpret_cast<const float4*>(bias + c) : z4;
+    float4 bs = z4;
+    float ss = 0.f;
+    // every lane of a 16-lane group walks the same pixels, so the group's xor-shuffles never mix groups
+    for (long long p = (long long)blockIdx.x * 16 + grp; p < P; p += (long long)gridDim.x * 16) {
+        const float4 pv = cok ? *reinterpret_cast<const float4*>(pre + p * ldpre + c) : z4;
+        const float4 gv = cok ? *reinterpret_cast<const float4*>(gy + p * ldg + c) : z4;
+        const float at = attn[p];
+        const float4 gp = make_float4(pv.x > 0.f ? gv.x : a * gv.x, pv.y > 0.f ? gv.y : a * gv.y,
+                                      pv.z > 0.f ? gv.z : a * gv.z, pv.w > 0.f ? gv.w : a * gv.w);
+        if (!(pv.x > 0.f)) ss += pv.x * gv.x;
+        if (!(pv.y > 0.f)) ss += pv.y * gv.y;
+        if (!(pv.z > 0.f)) ss += pv.z * gv.z;
+        if (!(pv.w > 0.f)) ss += pv.w * gv.w;
+        bs.x += gp.x; bs.y += gp.y; bs.z += gp.z; bs.w += gp.w;
+        float d = (gp.x * (pv.x - b.x) + gp.y * (pv.y - b.y)) + (gp.z * (pv.z - b.z) + gp.w * (pv.w - b.w));
+        if (cok) *reinterpret_cast<float4*>(gs + p * C + c) = make_float4(at * gp.x, at * gp.y, at * gp.z, at * gp.w);
+        for (int off = 8; off > 0; off >>= 1) d += __shfl_xor(d, off);
+        if (l16 == 0) glogit[p] = d * (1.0f - at);
+    }
+    if (cok) *reinterpret_cast<float4*>(&rb[grp][c]) = bs;
+    rs[threadIdx.x] = ss;
+    __syncthreads();
+    for (int k = 128; k > 0; k >>= 1) {
+        if (threadIdx.x < k) rs[threadIdx.x] += rs[threadIdx.x + k];
+        __syncthreads();
+    }
+    if (threadIdx.x < C) {
+        float t = 0.f;
+#pragma unroll
+        for (int g = 0; g < 16; ++g) t += rb[g][threadIdx.x];
+        part[(long long)blockIdx.x * (C + 1) + threadIdx.x] = t;
+    }
+    if (threadIdx.x == 0) part[(long long)blockIdx.x * (C + 1) + C] = rs[0];
+}
+// one block per output (C bias channels, then the slope): the partials folded in a fixed order, ADDED to the gradient
+__global__ __launch_bounds__(256) void sa_fold_final_kernel(const float* part, int nb, int C, float* dbias,
+                                                            float* dslope) {
+    __shared__ float red[256];
+    const int k = blockIdx.x;
+    float s = 0.f;
+    for (int i = threadIdx.x; i < nb; i += 256) s += part[(long long)i * (C + 1) + k];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        if (k < C) dbias[k] += red[0];
+        else dslope[0] += red[0];
     }
 }
 
@@ -834,6 +906,45 @@ static int spatial_attn_bwd_impl(const float* x, const float* w, const float* po
     return HY_LAUNCH_CHECK("sa_bwd_x");
 }
 }  // extern "C++"
+static int sa_fold_blocks(long long P) { return (int)std::max<long long>(1, std::min<long long>((P + 63) / 64, 1024)); }
+
+long long hyres_sa_fold_workspace_bytes(long long P, int C) { return (long long)sa_fold_blocks(P) * (C + 1) * 4 + 256; }
+
+int hyres_sa_fold_bwd(const float* pre, int ldpre, const float* gy, int ldg, const float* attn, const float* bias,
+                      const float* slope, float* gs, float* glogit, float* dbias, float* dslope, long long P, int C,
+                      void* ws, long long ws_bytes, hyres_stream_t s) {
+    HY_REQUIRE(pre && gy && attn && bias && slope && gs && glogit && dbias && dslope && P > 0, HYRES_E_ARG,
+               "sa_fold_bwd: NULL");
+    HY_REQUIRE(C % 4 == 0 && C > 0 && C <= 64 && ldpre % 4 == 0 && ldg % 4 == 0 && aligned16(pre) && aligned16(gy) &&
+                   aligned16(gs) && aligned16(bias),
+               HYRES_E_ALIGN, "sa_fold_bwd: C %% 4 == 0, C <= 64, 16B-aligned rows");
+    HY_REQUIRE(ws && ws_bytes >= hyres_sa_fold_workspace_bytes(P, C), HYRES_E_WORKSPACE, "sa_fold_bwd: workspace");
+    const int nb = sa_fold_blocks(P);
+    hipStream_t st = as_stream(s);
+    hipLaunchKernelGGL(sa_fold_bwd_kernel, dim3(nb), dim3(256), 0, st, pre, ldpre, gy, ldg, attn, bias, slope, gs, glogit,
+                       (float*)ws, P, C);
+    int rc = HY_LAUNCH_CHECK("sa_fold_bwd");
+    if (rc) return rc;
+    hipLaunchKernelGGL(sa_fold_final_kernel, dim3(C + 1), dim3(256), 0, st, (const float*)ws, nb, C, dbias, dslope);
+    return HY_LAUNCH_CHECK("sa_fold_final");
+}
+
+int hyres_spatial_attn_bwd_map(const float* glogit, const float* pooled2, const float* w, float* gpooled2, float* gw,
+                               int B, int H, int W, int C, void* ws, long long ws_bytes, hyres_stream_t s) {
+    HY_REQUIRE(glogit && pooled2 && w && gpooled2 && gw && C > 0, HYRES_E_ARG, "spatial_attn_bwd_map: NULL");
+    HY_REQUIRE(ws && ws_bytes >= hyres_spatial_attn_workspace_bytes(B, H, W), HYRES_E_WORKSPACE,
+               "spatial_attn_bwd_map: workspace");
+    const long long P = (long long)B * H * W;
+    float* wpart = (float*)ws;
+    const int nb = sa_bwd_blocks(P);
+    hipStream_t st = as_stream(s);
+    hipLaunchKernelGGL(sa_bwd_conv_kernel, dim3(nb), dim3(256), 0, st, glogit, pooled2, w, gpooled2, wpart, B, H, W, C);
+    int rc = HY_LAUNCH_CHECK("sa_bwd_conv");
+    if (rc) return rc;
+    hipLaunchKernelGGL(sa_bwd_wfinal_kernel, dim3(98), dim3(256), 0, st, (const float*)wpart, nb, gw);
+    return HY_LAUNCH_CHECK("sa_bwd_wfinal");
+}
+
 int hyres_spatial_attn_bwd(const float* x, const float* w, const float* pooled2, const int* argmax, const float* attn,
                            const float* gy, float* gx, float* gw, int B, int H, int W, int C, void* ws,
                            long long ws_bytes, hyres_stream_t s) {

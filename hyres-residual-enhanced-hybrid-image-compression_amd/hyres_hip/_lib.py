@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("HYRES_LIB_PATH") or os.path.join(HERE, "libhyres_hip.
 
 MAX_TAPS = 49
 WPREP_CONV, WPREP_CONV_DGRAD, WPREP_DECONV, WPREP_DECONV_DGRAD = 0, 1, 2, 3
-EPI_BIAS, EPI_GDN, EPI_IGDN, EPI_GDN_BWD, EPI_IGDN_BWD, EPI_ROWSCALE = 0, 1, 2, 3, 4, 5
+EPI_BIAS, EPI_GDN, EPI_IGDN, EPI_GDN_BWD, EPI_IGDN_BWD, EPI_ROWSCALE, EPI_SA_BWD = 0, 1, 2, 3, 4, 5, 6
 ACT_NONE, ACT_RELU, ACT_PRELU, ACT_RELU_MASK = 0, 1, 2, 3
 IO_X16, IO_Y16, IO_AUX16 = 1, 2, 4  # hyres_epilogue.io_f16 bits (fp16 activations in HBM)
 EB_REC = 64
@@ -164,6 +164,9 @@ _SIGS = {
     "hyres_spatial_attn_fwd_f16": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P]),
     "hyres_spatial_attn_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _LL, _P]),
     "hyres_spatial_attn_workspace_bytes": (_LL, [_I, _I, _I]),
+    "hyres_sa_fold_workspace_bytes": (_LL, [_LL, _I]),
+    "hyres_sa_fold_bwd": (_I, [_P, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _LL, _I, _P, _LL, _P]),
+    "hyres_spatial_attn_bwd_map": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _LL, _P]),
     "hyres_sum_log": (_I, [_P, _LL, _P, _P, _LL, _P]),
     "hyres_sum_sqdiff": (_I, [_P, _P, _LL, _P, _P, _LL, _P]),
     "hyres_reduce_workspace_bytes": (_LL, [_LL]),

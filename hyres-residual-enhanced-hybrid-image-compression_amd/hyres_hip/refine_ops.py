@@ -6,9 +6,12 @@ from __future__ import annotations
 
 from typing import Optional
 
+import ctypes
+
 import torch
 
 from . import _lib as L
+from . import ops as O
 from .ops import Node, Tape, _empty, accumulate, param_grad, _ws
 
 
@@ -86,9 +89,10 @@ def se_block(tape: Optional[Tape], x: Node, w1: torch.Tensor, w2: torch.Tensor) 
     return y
 
 
-def spatial_attention_map(x: Node, w: torch.Tensor) -> torch.Tensor:
-    """SpatialAttention(x) alone (enhancement.py:7-21): the [B, H, W] sigmoid map, fp32, forward only — its
-    multiply is folded into the next 1x1 conv's epilogue (ops.conv2d ``rowscale``)."""
+def spatial_attention_map(x: Node, w: torch.Tensor, keep: bool = False):
+    """SpatialAttention(x) alone (enhancement.py:7-21): the [B, H, W] sigmoid map, fp32 — its multiply is folded
+    into the next 1x1 conv's epilogue (ops.conv2d ``rowscale``; training: ``sa_fold_fusion``). ``keep``: also return
+    the pooled [B, H, W, 2] map and the channel argmax the backward needs."""
     assert x.contiguous
     B, H, W, C = x.B, x.H, x.W, x.C
     dev = x.device
@@ -98,7 +102,80 @@ def spatial_attention_map(x: Node, w: torch.Tensor) -> torch.Tensor:
     fn = "hyres_spatial_attn_fwd_f16" if x.half else "hyres_spatial_attn_fwd"
     L.call(fn, x.ptr(), w.data_ptr(), pooled2.data_ptr(), argmax.data_ptr(), attn.data_ptr(), None, B, H, W, C,
            L.stream())
-    return attn
+    return (attn, pooled2, argmax) if keep else attn
+
+
+def sa_fold_fusion(tape: Optional[Tape], multi: Node, w_sa: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor,
+                   slope: torch.Tensor) -> Node:
+    """PReLU(fusion[0](multi * SpatialAttention(multi))) of MultiScaleRefine (enhancement.py:105-109) in training,
+    with the attention multiply never materialised (fp32 activations).
+
+    Forward: the attention map, then ONE 1x1 conv whose epilogue forms attn[p] * (W multi)[p] + b (HYRES_EPI_ROWSCALE)
+    and the PReLU, saving the pre-activation. Backward (hyres_sa_fold_bwd): gs = attn * PReLU'(gy) and the attention
+    logit's gradient from the 64-channel pre-activation (no 192-channel pass); d W_sa and the pooled maps' gradients on
+    the 2-channel map (hyres_spatial_attn_bwd_map); d W = gs x multi (weight gradient on the side stream, bias from the
+    fold's own column sums); d multi = W^T gs with SpatialAttention's mean / max backward added in the input-gradient's
+    epilogue (HYRES_EPI_SA_BWD). Replaces sa_mul, sa_bwd_logit, sa_bwd_x and the PReLU backward of the unfused chain
+    (refine's 192-channel concat read and written three more times per step)."""
+    assert multi.contiguous and not multi.half
+    Co, Ci_w, KH, KW = weight.shape
+    assert KH == 1 and KW == 1 and Ci_w == multi.C and slope.numel() == 1
+    B, H, W, Ci = multi.B, multi.H, multi.W, multi.C
+    dev = multi.device
+    attn, pooled2, argmax = spatial_attention_map(multi, w_sa, keep=True)
+    y = Node.new(B, H, W, Co, dev)
+    pre = _empty((B, H, W, Co), dev)
+    g = O._geom("hyres_geom_conv2d", B, H, W, Ci, multi.ld, Co, y.ld, 1, 1, 1, 0, 1)
+    e = L.Epilogue()
+    e.kind = L.EPI_ROWSCALE
+    e.act = L.ACT_PRELU
+    e.bias = bias.data_ptr()
+    e.slope = slope.data_ptr()
+    e.aux1, e.ld1 = attn.data_ptr(), 1
+    e.out2, e.ldo2 = pre.data_ptr(), Co
+    O._launch_conv(g, multi.ptr(), weight, Ci_w, y.ptr(), e)
+    O.Trace.act(y, L.ACT_PRELU, pre)
+    if tape is None:
+        return y
+
+    def bwd():
+        gy = y.grad()
+        if gy is None:
+            return
+        assert gy.dtype == torch.float32
+        P = y.P
+        gs = _empty((B, H, W, Co), dev)
+        glogit = _empty((B, H, W), dev)
+        ws = _ws(L.load().hyres_sa_fold_workspace_bytes(P, Co), dev, slot=1)
+        dbias = param_grad(bias) if bias.requires_grad else _empty((Co,), dev)
+        dslope = param_grad(slope) if slope.requires_grad else _empty((1,), dev)
+        L.call("hyres_sa_fold_bwd", pre.data_ptr(), Co, gy.data_ptr(), y.grad_ld(), attn.data_ptr(), bias.data_ptr(),
+               slope.data_ptr(), gs.data_ptr(), glogit.data_ptr(), dbias.data_ptr(), dslope.data_ptr(), P, Co,
+               ws.data_ptr(), ws.numel(), L.stream())
+        gp2 = _empty((B, H, W, 2), dev)
+        gw_sa = param_grad(w_sa) if w_sa.requires_grad else _empty(w_sa.shape, dev)
+        ws2 = _ws(L.load().hyres_spatial_attn_workspace_bytes(B, H, W), dev, slot=1)
+        L.call("hyres_spatial_attn_bwd_map", glogit.data_ptr(), pooled2.data_ptr(), w_sa.data_ptr(), gp2.data_ptr(),
+               gw_sa.data_ptr(), B, H, W, Ci, ws2.data_ptr(), ws2.numel(), L.stream())
+        if weight.requires_grad:
+            d = L.WgradDesc()
+            L.call("hyres_wgrad_desc_conv2d", ctypes.byref(d), B, H, W, Ci, multi.ld, Co, Co, 1, 1, 1, 0, 1)
+            d.sm = Ci_w
+            d.accumulate = 1
+            O._wgrad(d, gs.data_ptr(), multi.ptr(), param_grad(weight), dev, None, keep=(gs, multi.v), side=True)
+        if multi.rg:
+            ed = L.Epilogue()
+            ed.kind = L.EPI_SA_BWD
+            ed.aux0, ed.ld0 = gp2.data_ptr(), 2
+            ed.aux2 = argmax.data_ptr()
+            tgt, acc = multi.grad_target()
+            gd = O._geom("hyres_geom_conv2d_dgrad", B, H, W, Ci, multi.grad_ld(), Co, Co, 1, 1, 1, 0, 1)
+            w2d = O._prepped(weight, gd, L.WPREP_CONV_DGRAD, Ci_w, Co, 1, 1, 0)
+            ed.accumulate = acc
+            O._launch_conv(gd, gs.data_ptr(), w2d, gd.ntaps * Co, tgt.data_ptr(), ed)
+
+    tape.push(bwd)
+    return y
 
 
 def spatial_attention_mul(tape: Optional[Tape], x: Node, w: torch.Tensor) -> Node:

@@ -20,8 +20,8 @@ from hyres_hip.layers import Conv2d, HipModule, PReLU, ReLU, Sequential
 from hyres_hip import ops as O
 from hyres_hip.ops import Node
 
-# inference: SpatialAttention's multiply folded into fusion[0]'s epilogue (HYRES_EPI_ROWSCALE); tests flip it,
-# HYRES_FOLD_SA_MUL=0 turns it off (A/B)
+# SpatialAttention's multiply folded into fusion[0]'s epilogue (HYRES_EPI_ROWSCALE): inference, and training with
+# fp32 activations (refine_ops.sa_fold_fusion); tests flip it, HYRES_FOLD_SA_MUL=0 turns it off (A/B)
 FOLD_SA_MUL = os.environ.get("HYRES_FOLD_SA_MUL", "1") == "1"
 
 __all__ = ["SpatialAttention", "SEBlock", "dilated_conv", "MultiScaleRefine"]
@@ -139,6 +139,12 @@ class MultiScaleRefine(HipModule):
             f0, f1, f2c = self.fusion[0], self.fusion[1], self.fusion[2]
             h = O.conv2d(None, multi, f0.weight, f0.bias, act=L.ACT_PRELU, slope=f1.weight, rowscale=attn)
             out = f2c.hip(None, h)
+            m = None
+        elif FOLD_SA_MUL and not multi.half and not O.f16_convs():
+            # training (fp32 activations): the same fold, with its backward (refine_ops.sa_fold_fusion)
+            f0, f1, f2c = self.fusion[0], self.fusion[1], self.fusion[2]
+            h = R.sa_fold_fusion(tape, multi, self.spatial_att.conv.weight, f0.weight, f0.bias, f1.weight)
+            out = f2c.hip(tape, h)
             m = None
         else:
             m = self.spatial_att.hip_mul(tape, multi)

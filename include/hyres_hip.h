@@ -99,7 +99,11 @@ int hyres_conv_weight_prep_batch(const void* descs, int n, long long total, hyre
 #define HYRES_EPI_IGDN_BWD 4  /* y = 2*aux0*acc + aux1 * sqrt(aux2)                               */
 #define HYRES_EPI_ROWSCALE 5  /* y = act(aux1[pix * ld1] * acc + bias (+ res)): a per-output-pixel scale of the
                                * input folded into the GEMM (SpatialAttention's x * attn ahead of MultiScaleRefine's
-                               * fusion 1x1, enhancement.py:105-109: inference only)                          */
+                               * fusion 1x1, enhancement.py:105-109)                                          */
+#define HYRES_EPI_SA_BWD 6    /* y = acc + aux0[pix * ld0] + (n == ((const int*)aux2)[pix] ? aux0[pix * ld0 + 1] : 0):
+                               * SpatialAttention's channel-mean / channel-max backward (enhancement.py:14-20)
+                               * folded into the input-gradient of MultiScaleRefine's fusion 1x1 (training with
+                               * the ROWSCALE forward): aux0 = [P][2] (d mean / C, d max), aux2 = argmax [P]  */
 #define HYRES_ACT_NONE 0
 #define HYRES_ACT_RELU 1
 #define HYRES_ACT_PRELU 2     /* single shared slope (nn.PReLU()), read from device pointer */
@@ -410,6 +414,21 @@ int hyres_spatial_attn_bwd(const float* x, const float* w, const float* pooled2,
                            const float* attn, const float* gy, float* gx, float* gw, int B, int H, int W,
                            int C, void* ws, long long ws_bytes, hyres_stream_t s);
 long long hyres_spatial_attn_workspace_bytes(int B, int H, int W);
+/* Training with SpatialAttention's multiply folded into MultiScaleRefine's fusion 1x1 (HYRES_EPI_ROWSCALE forward,
+ * enhancement.py:105-109): h = PReLU(attn[p] * (W multi)[p] + b), ``pre`` its pre-activation [P][C] (C = fusion
+ * width, ldpre), gy = dL/dh [P][ldg]. Writes gs = attn[p] * gp (gp = PReLU-backward of gy: the fusion 1x1's weight-
+ * and input-gradient operand), glogit[p] = (1 - attn[p]) * sum_o gp[p,o] * (pre[p,o] - b[o]) (= the gradient at the
+ * attention logit: attn * z = pre - b, no division), and ADDS dbias += sum_p gp, dslope += sum_{pre <= 0} gy * pre
+ * (deterministic per-block partials). C % 4 == 0, C <= 64, 16B-aligned rows; ws >= hyres_sa_fold_workspace_bytes(P, C). */
+long long hyres_sa_fold_workspace_bytes(long long P, int C);
+int hyres_sa_fold_bwd(const float* pre, int ldpre, const float* gy, int ldg, const float* attn, const float* bias,
+                      const float* slope, float* gs, float* glogit, float* dbias, float* dslope, long long P, int C,
+                      void* ws, long long ws_bytes, hyres_stream_t s);
+/* SpatialAttention's map backward from the logit gradient: gw += d conv7x7 weight, gpooled2 = [P][2] gradients of
+ * the channel mean (already divided by C, as HYRES_EPI_SA_BWD reads it) and the channel max. ws as
+ * hyres_spatial_attn_workspace_bytes(B, H, W). */
+int hyres_spatial_attn_bwd_map(const float* glogit, const float* pooled2, const float* w, float* gpooled2, float* gw,
+                               int B, int H, int W, int C, void* ws, long long ws_bytes, hyres_stream_t s);
 /* fp16-activation forwards (x and y fp16 in HBM, fp32 arithmetic; autocast inference, BASELINE
  * configs[4] "fp16 activations"): same semantics as the fp32 forwards above (bilinear without
  * accumulate; C % 4 == 0, ld % 4 == 0, 8B-aligned x/y). pooled / hidden / sgate / pooled2 / attn fp32. */

@@ -73,7 +73,7 @@ def main():
                        capture_error_mode="thread_local")
 
     opt.zero_grad()
-    _, c = cap.replay()
+    c = cap.replay()[1]
     red.all_reduce()
     torch.cuda.synchronize()
     g_ddp = opt.flat.grad.clone()
@@ -106,7 +106,7 @@ def main():
             cap1 = CapturedStep(net1, x_all[sl_].to(dev), jd1.to(dev), float(bpp1), criterion=crit,
                                 zero_grad=opt1.zero_grad)
             opt1.zero_grad()
-            _, c1 = cap1.replay()
+            c1 = cap1.replay()[1]
             torch.cuda.synchronize()
             return opt1.flat.grad.clone(), float(c1["loss"])
 

@@ -148,7 +148,7 @@ def test_graphed_train_step_bs16_bit_identical_run_to_run(amp):
     try:
         for r in range(3):
             zero()
-            _, c = cap.replay()
+            c = cap.replay()[1]
             torch.cuda.synchronize()
             cur = [float(c["loss"])] + [p.grad.detach().clone() for p in params]
             if first is None:

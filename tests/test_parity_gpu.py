@@ -312,6 +312,68 @@ def test_checkerboard_masked_conv(fp32_gemm):
     assert rel_err(m.bias.grad.cpu(), br.grad) < TOL
 
 
+@pytest.mark.parametrize("fold", [True, False])
+def test_refine_fusion_head_sa_fold_fwd_bwd(fp32_gemm, fold):
+    """MultiScaleRefine's head in training (enhancement.py:105-109): fusion[2](PReLU(fusion[0](multi *
+    SpatialAttention(multi)))) forward and backward vs fp64 torch — with the attention multiply folded into the fusion
+    1x1 (refine_ops.sa_fold_fusion: ROWSCALE forward, hyres_sa_fold_bwd, hyres_spatial_attn_bwd_map, the SA_BWD
+    input-gradient epilogue) and unfused (spatial_attention_mul + Sequential). Output, d multi, and every parameter
+    gradient (both 1x1 / 3x3 weights and biases, the PReLU slope, the 7x7 attention weight) at 1e-4 max-norm; the slope
+    at 1e-3 (one cancelled sum). 2 x 192 x 40 x 48: a partial last tile of pixels, both PReLU branches populated."""
+    import models.layers.enhancement as EH
+    from hyres_hip import ops as O
+    D = dev()
+    B, C, H, W = 2, 192, 40, 48
+    torch.manual_seed(11)
+    m = EH.MultiScaleRefine(3, 64)
+    multi = _rand((B, C, H, W), 41, 1.0)
+    gy = _rand((B, 3, H, W), 42)
+    sd = {k: v.detach().double().clone().requires_grad_(True) for k, v in m.state_dict().items()
+          if k.startswith(("fusion", "spatial_att"))}
+    sd["fusion.0.bias"].data.add_(0.05)  # the bias shifts pre-activations across 0: both PReLU sides
+    xr = multi.double().requires_grad_(True)
+    a = torch.sigmoid(F.conv2d(torch.cat([xr.mean(1, keepdim=True), xr.max(1, keepdim=True)[0]], 1),
+                               sd["spatial_att.conv.weight"], None, padding=3))
+    h = F.prelu(F.conv2d(xr * a, sd["fusion.0.weight"], sd["fusion.0.bias"]), sd["fusion.1.weight"])
+    yr = F.conv2d(h, sd["fusion.2.weight"], sd["fusion.2.bias"], padding=1)
+    yr.backward(gy.double())
+    m = m.to(D)
+    with torch.no_grad():
+        for k, v in m.named_parameters():
+            if k in sd:
+                v.copy_(sd[k].detach().float())
+    for p in m.parameters():
+        p.grad = None
+    tape = O.Tape()
+    xn = O.to_nhwc(multi.to(D), rg=True)
+    hn = R_sa_fold(tape, xn, m) if fold else _unfused_head(tape, xn, m)
+    yn = m.fusion[2].hip(tape, hn)
+    yn.set_grad(O.nchw_grad_to_nhwc(gy.to(D)))
+    tape.backward()
+    torch.cuda.synchronize()
+    neg = float((F.conv2d(xr * a, sd["fusion.0.weight"], sd["fusion.0.bias"]) < 0).double().mean())
+    assert 0.05 < neg < 0.95, neg
+    errs = {"y": rel_err(O.to_nchw(yn).cpu(), yr), "dmulti": rel_err(O.to_nchw_grad(xn).cpu(), xr.grad)}
+    for k, p in m.named_parameters():
+        if k in sd:
+            errs[k] = rel_err(p.grad.cpu(), sd[k].grad)
+    print("fold" if fold else "unfused", {k: f"{v:.1e}" for k, v in errs.items()})
+    bad = {k: v for k, v in errs.items() if v > (1e-3 if k == "fusion.1.weight" else TOL)}
+    assert not bad, errs
+
+
+def R_sa_fold(tape, xn, m):
+    from hyres_hip import refine_ops as R
+    return R.sa_fold_fusion(tape, xn, m.spatial_att.conv.weight, m.fusion[0].weight, m.fusion[0].bias,
+                            m.fusion[1].weight)
+
+
+def _unfused_head(tape, xn, m):
+    from hyres_hip import _lib as L
+    mm = m.spatial_att.hip_mul(tape, xn)
+    return m.fusion[0].hip(tape, mm, act=L.ACT_PRELU, slope=m.fusion[1].weight)
+
+
 @pytest.mark.parametrize("branch", ["scale1", "scale2", "scale3"])
 def test_refine_branch_fwd_bwd(branch):
     """One MultiScaleRefine branch (bilinear down -> conv+PReLU -> dilated conv+PReLU -> bilinear up) vs fp64."""
@@ -982,7 +1044,7 @@ def test_captured_train_step_matches_eager():
     grads_e = [p.grad.detach().clone() for p in params]
     zero()
     cap = CapturedStep(net, x, j, 0.25, criterion=crit, zero_grad=zero)
-    _, cc = cap.replay()
+    cc = cap.replay()[1]
     torch.cuda.synchronize()
     assert float(cc["loss"]) == loss_e
     for p, ge in zip(params, grads_e):
@@ -1097,7 +1159,7 @@ def test_captured_step_survives_eager_step_with_new_layouts_and_bigger_workspace
     torch.cuda.empty_cache()  # hand the replaced buffers back to the device: a dangling read would now fault
     rm.noise.injected = injected
     zero()
-    _, cc = cap.replay()
+    cc = cap.replay()[1]
     torch.cuda.synchronize()
     loss_r = float(cc["loss"])
     grads_r = [p.grad.detach().clone() for p in params]
