@@ -13,7 +13,7 @@ namespace hyres {
 constexpr int KT = 32;  // K chunk (floats)
 
 // tile / split-K overrides set through hyres_conv_tuning (conv.hip; -1 = the planners' heuristics)
-extern int g_tune[15];
+extern int g_tune[HYRES_TUNE_KEYS];
 
 // fp32 GEMMs on the bf16 MFMA (hyres_conv_tuning key 7 = 1, the default): "bf16x6"
 inline bool f32_gemm_bf6() { return g_tune[7] == 1; }

@@ -1302,6 +1302,169 @@ __global__ __launch_bounds__(256) void wgrad1x1_bf6_kernel(const WgradArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// wgrad1x1_bf6_kernel with its operand loads two chunks ahead (hyres_conv_tuning key 15 = 2). The 1x1 weight
+// gradient streams P and Q once (~3 TB/s at one 98 KB block per CU: 24.6 KB of loads in flight per CU, one HBM latency
+// per 32-pixel chunk). Here two register sets alternate: chunk k + 2's loads are issued while chunk k's MFMAs run and
+// chunk k + 1's registers go to LDS, so two chunks are in flight. Every load is an unconditional raw buffer load
+// (out-of-range rows / channels / chunks past the split: an offset past the buffer's end, which returns 0 without
+// touching memory): no branch around a load, so the compiler's vmcnt waits count only the older set. Same products in
+// the same order as wgrad1x1_bf6_kernel (bit-identical slabs).
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wg_rsrc(const void* p, long long bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)std::min<long long>(bytes, 0x7FFFFFF0LL),
+                                             0x00020000);
+}
+template <int TM, int TN, int WAVES_M, int WAVES_N>
+__global__ __launch_bounds__(256) void wgrad1x1_bf6_pf2_kernel(const WgradArgs a) {
+    constexpr int BM = 32 * TM * WAVES_M, BN = 32 * TN * WAVES_N;
+    constexpr int PP = BM + 32, PQ = BN + 32;  // bf16 row pitches
+    constexpr int PSZ = KT * PP, QSZ = KT * PQ, PLANE = PSZ + QSZ, BUF = 3 * PLANE;
+    constexpr int P_V = KT * BM / 4 / 256, Q_V = KT * BN / 4 / 256;
+    static_assert(P_V >= 1 && Q_V >= 1, "tile too small");
+    static_assert(PLANE % 4 == 0 && 2 * BUF * 2 <= 160 * 1024, "LDS");
+    constexpr int OOR = (int)0x80000000;
+    __shared__ __attribute__((aligned(16))) __bf16 smem[2 * BUF];
+    const hyres_wgrad_desc& d = a.d;
+    const int tid = threadIdx.x;
+    const int bid = blockIdx.x;
+    const int lb = (bid & 7) * (gridDim.x >> 3) + (bid >> 3);  // XCD-aware order, as wgrad_kernel
+    if (lb >= a.nblocks) return;
+    int rr = lb;
+    const int mt = rr % a.mtiles; rr /= a.mtiles;
+    const int nt = rr % a.ntiles; rr /= a.ntiles;
+    const int split = rr;
+    const int m0 = mt * BM, n0 = nt * BN;
+    const long long Qtot = (long long)d.B * d.Hq * d.Wq;
+    const int pc = (tid % (BM / 4)) * 4, prow0 = tid / (BM / 4);
+    const int qc = (tid % (BN / 4)) * 4, qrow0 = tid / (BN / 4);
+    constexpr int PRS = 256 / (BM / 4), QRS = 256 / (BN / 4);
+    const __amdgpu_buffer_rsrc_t rp_ = wg_rsrc(a.p, Qtot * d.ldp * 4);
+    const __amdgpu_buffer_rsrc_t rq_ = wg_rsrc(a.q, Qtot * d.ldq * 4);
+    const bool pc_ok = m0 + pc < d.M, qc_ok = n0 + qc < d.N;
+    const int kb = split * a.chunks_per_split;
+    const int ke = min(a.nchunks, kb + a.chunks_per_split);
+    auto load = [&](int kc, float4 (&rp)[P_V], float4 (&rq)[Q_V]) {
+        const long long k0 = (long long)kc * KT;
+#pragma unroll
+        for (int i = 0; i < P_V; ++i) {
+            const long long row = k0 + prow0 + i * PRS;
+            const int off = (kc < ke && row < Qtot && pc_ok) ? (int)((row * d.ldp + m0 + pc) * 4) : OOR;
+            rp[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rp_, off, 0, 0));
+        }
+#pragma unroll
+        for (int i = 0; i < Q_V; ++i) {
+            const long long row = k0 + qrow0 + i * QRS;
+            const int off = (kc < ke && row < Qtot && qc_ok) ? (int)((row * d.ldq + n0 + qc) * 4) : OOR;
+            rq[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rq_, off, 0, 0));
+        }
+    };
+    const bool do_bias = a.bias_slab != nullptr && nt == 0;
+    float4 bsum = make_float4(0.f, 0.f, 0.f, 0.f);
+    auto put = [&](__bf16* base, int o, const float4& v) {
+        bf16x4_t h, m, l;
+        bf6_split4(v, h, m, l);
+        *reinterpret_cast<bf16x4_t*>(&base[o]) = h;
+        *reinterpret_cast<bf16x4_t*>(&base[PLANE + o]) = m;
+        *reinterpret_cast<bf16x4_t*>(&base[2 * PLANE + o]) = l;
+    };
+    auto store = [&](int buf, const float4 (&rp)[P_V], const float4 (&rq)[Q_V]) {
+        __bf16* B0 = smem + buf * BUF;
+#pragma unroll
+        for (int i = 0; i < P_V; ++i) {
+            if (do_bias) { bsum.x += rp[i].x; bsum.y += rp[i].y; bsum.z += rp[i].z; bsum.w += rp[i].w; }
+            put(B0, (prow0 + i * PRS) * PP + pc, rp[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < Q_V; ++i) put(B0, PSZ + (qrow0 + i * QRS) * PQ + qc, rq[i]);
+    };
+    const int lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+    const int lh = lane >> 5, lg = (lane >> 4) & 1, lq = (lane >> 2) & 3, lp = lane & 3;
+    const int tr_row = 8 * lh + lq, tr_col = 16 * lg + 4 * lp;
+    auto frag = [&](const __bf16* p, int pitch) {
+        const halfx4_t lo = lds_tr4(reinterpret_cast<const _Float16*>(p));
+        const halfx4_t hi = lds_tr4(reinterpret_cast<const _Float16*>(p + 4 * pitch));
+        return __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+    };
+    floatx16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    float4 pA[P_V], qA[Q_V], pB[P_V], qB[Q_V];
+    if (kb < ke) {  // block-uniform
+        load(kb, pA, qA);
+        load(kb + 1, pB, qB);
+        store(0, pA, qA);
+    }
+    __syncthreads();
+    // chunk kc sits in LDS buffer ``cur``; ``hn`` holds chunk kc + 1 (in flight), ``hl`` (stored) receives kc + 2
+    auto body = [&](int kc, int cur, float4 (&pl)[P_V], float4 (&ql)[Q_V], const float4 (&pn)[P_V],
+                    const float4 (&qn)[Q_V]) {
+        load(kc + 2, pl, ql);
+        const __bf16* Ps = smem + cur * BUF;
+        const __bf16* Qs = Ps + PSZ;
+#pragma unroll
+        for (int s = 0; s < KT / 16; ++s) {
+            bf16x8_t af[TM][3], bf[TN][3];
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                for (int pl3 = 0; pl3 < 3; ++pl3)
+                    af[tm][pl3] = frag(Ps + pl3 * PLANE + (16 * s + tr_row) * PP + wm * TM * 32 + tm * 32 + tr_col, PP);
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+                for (int pl3 = 0; pl3 < 3; ++pl3)
+                    bf[tn][pl3] = frag(Qs + pl3 * PLANE + (16 * s + tr_row) * PQ + wn * TN * 32 + tn * 32 + tr_col, PQ);
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = bf6_mfma(af[tm], bf[tn], acc[tm][tn]);
+        }
+        if (kc + 1 < ke) store(cur ^ 1, pn, qn);  // block-uniform
+        __syncthreads();
+    };
+    for (int kc = kb; kc < ke; kc += 2) {
+        body(kc, 0, pA, qA, pB, qB);
+        if (kc + 1 < ke) body(kc + 1, 1, pB, qB, pA, qA);
+    }
+    if (do_bias) {  // block-uniform
+        float4* red = reinterpret_cast<float4*>(smem);  // the loop ended with a barrier
+        red[tid] = bsum;
+        __syncthreads();
+        if (tid < BM / 4) {
+            float4 s4 = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int r = 0; r < PRS; ++r) {
+                const float4 v = red[tid + r * (BM / 4)];
+                s4.x += v.x; s4.y += v.y; s4.z += v.z; s4.w += v.w;
+            }
+            float* dst = a.bias_slab + (long long)split * d.M + m0 + 4 * tid;
+            const float sv[4] = {s4.x, s4.y, s4.z, s4.w};
+            for (int c = 0; c < 4; ++c)
+                if (m0 + 4 * tid + c < d.M) dst[c] = sv[c];
+        }
+    }
+    const int lr = lane & 31;
+    const long long MN = (long long)d.M * d.N;
+    float* out = a.slab + (long long)split * MN;
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) {
+            const int n = n0 + wn * TN * 32 + tn * 32 + lr;
+            if (n >= d.N) continue;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + wm * TM * 32 + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                if (m < d.M) out[(long long)m * d.N + n] = acc[tm][tn][r];
+            }
+        }
+}
+
+// ------------------------------------------------------------------------------------------------
 // fp32 halo-staged weight gradient on the bf16 MFMA ("bf16x6", hyres_conv_tuning key 7 = 1, the default fp32 GEMM):
 // wgrad_halo_f16_kernel's schedule and transposed LDS images, with each fp32 operand split when staged into three
 // bf16 planes (x = x0 + x1 + x2, 24 significant bits) and every product formed from the six cross products with
@@ -2110,7 +2273,14 @@ static int wgrad_issue(const hyres_wgrad_desc* d0, const float* pp, const float*
     const bool one = !thin && !p.halo && !wgrad_f16_ok(d) && !sqr && !p.tapn && vp && vq &&
                      d->ntaps == 1 && d->dh[0] == 0 && d->dw[0] == 0 && d->sq == 1 && d->Hqq == d->Hq &&
                      d->Wqq == d->Wq && p.ngroups == 1;
-    if (one && f32_gemm_bf6()) {  // bf16x6 products (the plan keeps one 4-wave group per block for it)
+    const bool pf2 = g_tune[15] == 2 && (long long)d->B * d->Hq * d->Wq * std::max(d->ldp, d->ldq) * 4 < 0x7FFFFFF0LL;
+    if (one && f32_gemm_bf6() && pf2) {  // loads two chunks ahead (key 15 = 2)
+        if (p.TMc == 2 && p.TNc == 2) hipLaunchKernelGGL((wgrad1x1_bf6_pf2_kernel<2, 2, 2, 2>), grid, dim3(256), 0, st, a);
+        else if (p.TMc == 2) hipLaunchKernelGGL((wgrad1x1_bf6_pf2_kernel<2, 1, 2, 2>), grid, dim3(256), 0, st, a);
+        else if (p.WMc == 1) hipLaunchKernelGGL((wgrad1x1_bf6_pf2_kernel<1, 1, 1, 4>), grid, dim3(256), 0, st, a);
+        else if (p.WNc == 1) hipLaunchKernelGGL((wgrad1x1_bf6_pf2_kernel<1, 1, 4, 1>), grid, dim3(256), 0, st, a);
+        else hipLaunchKernelGGL((wgrad1x1_bf6_pf2_kernel<1, 1, 2, 2>), grid, dim3(256), 0, st, a);
+    } else if (one && f32_gemm_bf6()) {  // bf16x6 products (the plan keeps one 4-wave group per block for it)
         if (p.TMc == 2 && p.TNc == 2) hipLaunchKernelGGL((wgrad1x1_bf6_kernel<2, 2, 2, 2>), grid, dim3(256), 0, st, a);
         else if (p.TMc == 2) hipLaunchKernelGGL((wgrad1x1_bf6_kernel<2, 1, 2, 2>), grid, dim3(256), 0, st, a);
         else if (p.WMc == 1) hipLaunchKernelGGL((wgrad1x1_bf6_kernel<1, 1, 1, 4>), grid, dim3(256), 0, st, a);

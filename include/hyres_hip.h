@@ -187,6 +187,9 @@ int hyres_conv_plan(const hyres_conv_geom* g, const hyres_epilogue* e, int* tile
                                        * conv_narrow_strip_kernel (4-pixel strips, weights in VGPRs); 0: conv_narrow_kernel */
 #define HYRES_TUNE_WRES32 14          /* 1 (default): fp32 3x3 Ci = 64 convs on the weight-resident kernels
                                        * (conv3x3_wres_bf6 / _f32); 0: the implicit GEMM (A/B) */
+#define HYRES_TUNE_WGRAD_PF 15        /* bf16x6 1x1 weight gradients: 2 = operand loads two chunks ahead
+                                       * (wgrad1x1_bf6_pf2_kernel), 1 = one chunk ahead (wgrad1x1_bf6_kernel) */
+#define HYRES_TUNE_KEYS 20            /* keys 16..19 reserved */
 int hyres_conv_tuning(int key, int value, int* old);
 
 /* Weight gradient:  dW[t][m][n] = sum_q P[q][m] * Q[shift_t(q)][n]  over a base grid q (B,Hq,Wq).
