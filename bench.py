@@ -126,6 +126,10 @@ PMC_TRAFFIC = [os.path.join(REPO, "profiles", f) for f in
 PMC_TRAFFIC_AMP = [os.path.join(REPO, "profiles", f) for f in
                    os.environ.get("HYRES_PMC_TRAFFIC_AMP", "r5f_pmc_traffic_amp.json,r5s_pmc_traffic_amp.json").split(",")]
 EAGER_TIMED = 3  # eager steps behind the live per-launch roofline timing
+# N > 1 default: the graphed step cut at the "hyper" marker with the finished segments' all-reduce between the two
+# replays; HYRES_DIST_MODE=graph+allreduce (reduce after one replay) / eager-overlap select the others
+DIST_DEFAULT = "graph+overlap"
+SPLIT_AT = ("hyper",)
 
 
 # bf16x6 (csrc/conv.hip bf6_mfma): each fp32 product from six bf16 MFMA products -> the fp32-equivalent ceiling of
@@ -608,8 +612,8 @@ def main():
         # step with each gradient segment's all-reduce started at its backward-progress marker. (The round-3/4
         # "graph+overlap" mode — collectives started from events recorded inside the replay — was removed in
         # round 5: it needs more live streams than the 4 hardware queues per process)
-        dist_mode = "eager-overlap" if args.no_graph else os.environ.get("HYRES_DIST_MODE", "graph+allreduce")
-        assert dist_mode in ("eager-overlap", "graph+allreduce"), dist_mode
+        dist_mode = "eager-overlap" if args.no_graph else os.environ.get("HYRES_DIST_MODE", DIST_DEFAULT)
+        assert dist_mode in ("eager-overlap", "graph+allreduce", "graph+overlap"), dist_mode
     if dist:
         # RCCL all-reduce of refine / g_s / hyperprior gradient segments launched from backward-progress
         # markers (overlapped with the rest of backward), the remainder (g_a) after backward
@@ -633,13 +637,18 @@ def main():
         # forward + RD loss + backward captured once as a HIP graph (hyres_hip.graphs); the optimiser,
         # the RCCL all-reduce and the aux step stay eager (a handful of launches)
         from hyres_hip.graphs import CapturedStep
+        # graph+overlap: the capture is cut at the "hyper" backward-progress marker; between the two replays the
+        # refine / g_s / hyperprior gradient segments start their RCCL all-reduce, which runs while g_a's backward
+        # (the second graph) computes
         graphed = CapturedStep(net, x, jpeg, jpeg_bpp, noisequant=False, criterion=crit, zero_grad=opt.zero_grad,
-                               capture_error_mode="thread_local" if dist else "global")
+                               capture_error_mode="thread_local" if dist else "global",
+                               split_at=SPLIT_AT if dist_mode == "graph+overlap" else ())
 
     def fwd_bwd(eager=False, gr=None):
         gr = gr or graphed
         if gr is not None and not eager:
-            return gr.replay()[1]
+            between = reducer.launch_segments if (reducer is not None and gr.split_at) else None
+            return gr.replay(between=between)[1]
         out = net.forward_device(x, jpeg, jpeg_bpp, noisequant=False)
         c = crit(out, x)
         c["loss"].backward()

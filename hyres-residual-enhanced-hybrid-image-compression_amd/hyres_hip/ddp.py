@@ -120,6 +120,17 @@ class FlatGradReducer:
         else:
             self._launch(ranges)
 
+    def launch_segments(self, names) -> None:
+        """Start the all-reduce of the named segments (those not started yet) on the current stream's order: the
+        split-graph step calls it between two replays (hyres_hip.graphs.CapturedStep ``between``), so the
+        collectives run while the next graph computes (on an accumulation boundary only: the caller decides, as DDP's
+        no_sync). ``all_reduce()`` reduces the rest and waits."""
+        for name in names:
+            ranges = self.segments.get(name)
+            if ranges and name not in self.fired:
+                self.fired.append(name)
+                self._launch(ranges)
+
     def all_reduce(self, async_op: bool = False):
         if self.fired:
             ranges = list(self.rest)

@@ -28,7 +28,7 @@ from __future__ import annotations
 import contextlib
 import gc
 import weakref
-from typing import Callable, Optional
+from typing import Callable, Optional, Sequence
 
 import torch
 
@@ -70,16 +70,24 @@ class CapturedStep:
 
     ``criterion``: a RateDistortionLoss for training capture (None = eval forward under no_grad).
     ``zero_grad``: called after the warm-up runs (their backward accumulated into the gradients).
+    ``split_at`` (training): backward-progress markers (hyres_hip.ops.GradReady names, e.g. ``("hyper",)``) at which
+    the capture is cut into consecutive graphs sharing one memory pool. ``replay(between=f)`` replays them in order
+    and calls ``f(segments)`` between two of them with the marker names whose gradients are final at that point — the
+    data-parallel step starts those segments' RCCL all-reduce there, so it runs while the next graph (the rest of
+    backward) computes (configs[3]: "grad all-reduce overlapped with backward"; reference src/training.py:211-212,
+    src/utils/engine.py:50-56). No collective is inside any graph, and no stream is added: the collective waits on
+    the replay stream.
     """
 
     def __init__(self, net: torch.nn.Module, x: torch.Tensor, jpeg_decoded: torch.Tensor, jpeg_bpp: float = 0.0,
                  noisequant: bool = False, criterion: Optional[Callable] = None,
                  zero_grad: Optional[Callable[[], None]] = None, warmup: int = 2,
                  capture_error_mode: str = "global", amp: bool = False,
-                 loss_scale: Optional[torch.Tensor] = None):
+                 loss_scale: Optional[torch.Tensor] = None, split_at: Sequence[str] = ()):
         assert x.is_cuda, "CapturedStep needs device tensors"
         self.net = net
         self.train = criterion is not None
+        self.split_at = tuple(split_at) if self.train else ()
         dev = x.device
         self.x = x.detach().clone()
         self.jpeg = jpeg_decoded.detach().clone()
@@ -115,7 +123,9 @@ class CapturedStep:
         torch.cuda.synchronize(dev)
         if zero_grad is not None:
             zero_grad()
-        self.graph = torch.cuda.CUDAGraph()
+        self.graphs = [torch.cuda.CUDAGraph() for _ in range(len(self.split_at) + 1)]
+        self.graph = self.graphs[0]
+        self.segments_done = []  # per cut: the markers whose gradients are final when the graphs before it end
         O.PrepBatch.prepare(dev)  # descriptor table uploaded now: the capture records ONE batched re-layout
         O.bump_weight_epoch()  # record every weight re-layout inside the graph
         # the graph's batched re-layout reads this descriptor table by address: keep it alive for the graph's
@@ -123,8 +133,11 @@ class CapturedStep:
         self._prep_table = O.PrepBatch.table(dev)
         # "thread_local" when an RCCL process group exists: its watchdog thread polls events while the
         # main thread captures (no collective is ever inside the graph)
-        with torch.cuda.graph(self.graph, capture_error_mode=capture_error_mode):
-            self.out, self.crit = run()
+        if not self.split_at:
+            with torch.cuda.graph(self.graph, capture_error_mode=capture_error_mode):
+                self.out, self.crit = run()
+        else:
+            self.out, self.crit = self._capture_split(run, dev, capture_error_mode)
         # weak references to every output the capture allocated (in the graph's private pool); the static inputs the
         # forward passes through (jpeg_decoded, jpeg_bpp_loss) belong to this object and are not tracked
         own = {t.untyped_storage().data_ptr() for t in (self.x, self.jpeg, self.bpp)}
@@ -135,6 +148,48 @@ class CapturedStep:
         # replaces the slot's tensor, and the old one must outlive the graph
         self._ws_keep = list(O.Workspace._bufs.values())
         torch.cuda.synchronize(dev)
+
+    def _capture_split(self, run, dev, capture_error_mode):
+        """Capture ``run`` as len(split_at) + 1 graphs: a GradReady listener ends the current capture and begins the
+        next one (same memory pool, same capture stream) when a split marker fires in the tape backward — every
+        weight-gradient reduce of the finished segments is flushed by the marker first (GradReady.mark), and the
+        side stream, if used, is joined so the capture closes with no forked stream open. The markers are placed at
+        module boundaries, where the branch streams are joined."""
+        st = {"on": False, "idx": 0, "seen": []}
+
+        def cut(name):
+            st["seen"].append(name)
+            if not st["on"] or name not in self.split_at:
+                return
+            O.SideStream.join()
+            i = st["idx"]
+            self.graphs[i].capture_end()
+            self.segments_done.append(list(st["seen"]))
+            st["idx"] = i + 1
+            self.graphs[i + 1].capture_begin(pool=self.graphs[0].pool(), capture_error_mode=capture_error_mode)
+
+        O.GradReady.listeners.append(cut)  # before the forward: GradReady.mark records markers only with listeners
+        try:
+            torch.cuda.synchronize(dev)
+            gc.collect()
+            torch.cuda.empty_cache()
+            cap = torch.cuda.Stream(device=dev)
+            cap.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(cap):
+                st["on"] = True
+                self.graphs[0].capture_begin(capture_error_mode=capture_error_mode)
+                try:
+                    out = run()
+                finally:
+                    st["on"] = False
+                    self.graphs[st["idx"]].capture_end()
+            torch.cuda.current_stream(dev).wait_stream(cap)
+        finally:
+            O.GradReady.listeners.remove(cut)
+        if st["idx"] != len(self.split_at):
+            raise RuntimeError(f"CapturedStep: split markers {self.split_at} fired {st['idx']} time(s) in the captured "
+                               f"backward (markers seen: {st['seen']})")
+        return out
 
     def live_outputs(self) -> int:
         """How many tensors the capture allocated are still alive (held by this object or by a caller)."""
@@ -160,8 +215,10 @@ class CapturedStep:
                 raise GraphOutputsAlive(
                     f"CapturedStep.close(): {n} replay output tensor(s) still referenced; drop them before close() "
                     "(the graph was not reset)")
-            g.reset()
+            for gi in reversed(self.graphs):
+                gi.reset()
             self.graph = None
+            self.graphs = []
         self._prep_table = None
         self._ws_keep = []
 
@@ -175,19 +232,24 @@ class CapturedStep:
                 return
             self.close()
         except GraphOutputsAlive:
-            _KEPT.append((self.graph, self._prep_table, self._ws_keep))
+            _KEPT.append((self.graphs, self._prep_table, self._ws_keep))
         except Exception:  # noqa: BLE001 - interpreter shutdown
             pass
 
     def replay(self, x: Optional[torch.Tensor] = None, jpeg_decoded: Optional[torch.Tensor] = None,
-               jpeg_bpp: Optional[float] = None):
+               jpeg_bpp: Optional[float] = None, between: Optional[Callable[[list], None]] = None):
         """Run the captured step on the current stream; returns (outputs, loss dict or None) — static
-        tensors overwritten by the next replay."""
+        tensors overwritten by the next replay. A split capture replays its graphs in order and calls
+        ``between(markers)`` after each graph but the last (markers: the GradReady names whose gradients are final)."""
         if x is not None:
             self.x.copy_(x, non_blocking=True)
         if jpeg_decoded is not None:
             self.jpeg.copy_(jpeg_decoded, non_blocking=True)
         if jpeg_bpp is not None:
             self.bpp.fill_(float(jpeg_bpp))
-        self.graph.replay()
+        last = len(self.graphs) - 1
+        for i, g in enumerate(self.graphs):
+            g.replay()
+            if between is not None and i < last:
+                between(self.segments_done[i])
         return self.out, self.crit

@@ -85,8 +85,11 @@ class _GraphedStep:
             raise RuntimeError(f"DDP ranks reached different graph-capture keys (this rank {key}); every rank must "
                                "see the same batch shapes (DistributedSampler shards are equal-length)")
 
-    def __call__(self, d, noisequant, boundary_start, reducer):
-        """Returns the static loss dict of the replayed step, or None (run this step eagerly)."""
+    def __call__(self, d, noisequant, boundary_start, reducer, boundary_end=True):
+        """Returns the static loss dict of the replayed step, or None (run this step eagerly). With a reducer the
+        capture is cut at the "hyper" backward-progress marker (HYRES_DIST_SPLIT=0: one graph) and, on the
+        accumulation boundary (``boundary_end``), the finished gradient segments start their all-reduce between the
+        two replays, overlapping g_a's backward (bench.py's graph+overlap)."""
         if not self.enabled or d.device.type != "cpu" or not hasattr(self.model, "forward_device"):
             return None
         key = (tuple(d.shape), bool(noisequant), bool(self.amp))
@@ -107,9 +110,11 @@ class _GraphedStep:
                 reducer.armed = False  # no collective inside warm-up or capture
             err = None
             try:
+                split = ("hyper",) if reducer is not None and os.environ.get("HYRES_DIST_SPLIT", "1") == "1" else ()
                 cap = CapturedStep(self.model, x, jd, float(bpp), noisequant=noisequant, criterion=self.criterion,
                                    zero_grad=self.zero_grad, amp=self.amp, loss_scale=self.ls,
-                                   capture_error_mode="thread_local" if reducer is not None else "global")
+                                   capture_error_mode="thread_local" if reducer is not None else "global",
+                                   split_at=split)
             except Exception as exc:  # noqa: BLE001 - any capture failure: stay correct, run eagerly
                 err = exc
             finally:
@@ -124,7 +129,8 @@ class _GraphedStep:
                 return None
             self.caps[key] = cap
         self.last = cap
-        return cap.replay(x, jd, float(bpp))[1]
+        between = reducer.launch_segments if (reducer is not None and boundary_end and cap.split_at) else None
+        return cap.replay(x, jd, float(bpp), between=between)[1]
 
     def close(self) -> None:
         """Release every captured graph explicitly (end of the epoch), not from a finalizer."""
@@ -200,7 +206,8 @@ def train_one_epoch(model, criterion, train_dataloader, optimizer, aux_optimizer
     for i, (d, d_next) in enumerate(_lookahead(train_dataloader)):
         if d_next is not None and hasattr(jpeg, "prefetch"):
             jpeg.prefetch(d_next)  # the next batch's host JPEG overlaps this step's device work
-        crit = graphed(d, noisequant, i % gradient_accumulation_steps == 0, reducer)
+        crit = graphed(d, noisequant, i % gradient_accumulation_steps == 0, reducer,
+                       (i + 1) % gradient_accumulation_steps == 0)
         step_graphed = crit is not None
         if crit is not None:
             pending.append(_metrics(crit))

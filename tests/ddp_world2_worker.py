@@ -69,11 +69,17 @@ def main():
     net.residual_model.noise.injected = {"z": nz_all[sl].to(dev), "y": ny_all[sl].to(dev)}
 
     red = FlatGradReducer(opt.flat, world, names=names, segments=HYRES_SEGMENTS)
+    # HYRES_DDP_SPLIT=1: bench.py's graph+overlap mode — the capture cut at the "hyper" marker, the finished segments'
+    # all-reduce started between the two replays (while g_a's backward replays), the rest after
+    split = os.environ.get("HYRES_DDP_SPLIT", "0") == "1"
     cap = CapturedStep(net, x, j, float(bpp), criterion=crit, zero_grad=opt.zero_grad,
-                       capture_error_mode="thread_local")
+                       capture_error_mode="thread_local", split_at=("hyper",) if split else ())
+    between = red.launch_segments if split else None
+    if split:
+        assert len(cap.graphs) == 2 and cap.segments_done == [["refine", "g_s", "hyper"]], cap.segments_done
 
     opt.zero_grad()
-    c = cap.replay()[1]
+    c = cap.replay(between=between)[1]
     red.all_reduce()
     torch.cuda.synchronize()
     g_ddp = opt.flat.grad.clone()
@@ -82,10 +88,12 @@ def main():
     loss_mean = float(loss) / world
 
     opt.zero_grad()
-    cap.replay()
+    cap.replay(between=between)
     red.all_reduce()
     torch.cuda.synchronize()
     same_after = bool(torch.equal(opt.flat.grad, g_ddp))
+    c = None
+    cap.close()
 
     opt.step()
     torch.cuda.synchronize()

@@ -27,9 +27,12 @@ def _port():
         return s.getsockname()[1]
 
 
-def test_world2_graphed_ddp_gradient_parity(tmp_path):
+@pytest.mark.parametrize("split", [False, True])
+def test_world2_graphed_ddp_gradient_parity(tmp_path, split):
+    """split: bench.py's default N > 1 mode (graph+overlap) — the captured step cut into two graphs at the "hyper"
+    marker, the refine / g_s / hyperprior segments' all-reduce started between the replays."""
     out = tmp_path / "ddp2.npz"
-    env = dict(os.environ, HYRES_JPEG_PROCS="0", OMP_NUM_THREADS="4")
+    env = dict(os.environ, HYRES_JPEG_PROCS="0", OMP_NUM_THREADS="4", HYRES_DDP_SPLIT="1" if split else "0")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={_port()}",
            os.path.join(REPO, "tests", "ddp_world2_worker.py"), str(out)]

@@ -1217,10 +1217,12 @@ def test_overlapped_rccl_reducer_single_rank():
         tdist.destroy_process_group()
 
 
-def test_captured_step_with_rccl_group_single_rank():
+@pytest.mark.parametrize("split", [False, True])
+def test_captured_step_with_rccl_group_single_rank(split):
     """The N > 1 bench path: the train step captured (capture_error_mode thread_local) while an RCCL
     process group is live, replayed, then the flat gradients all-reduced after the replay in buckets; the
-    reduced gradients equal the eager step's."""
+    reduced gradients equal the eager step's. split (graph+overlap, the default N > 1 mode): the capture cut at the
+    "hyper" marker into two graphs, the finished segments' RCCL all-reduce started between the replays."""
     import os
     import socket
     import torch.distributed as tdist
@@ -1252,14 +1254,18 @@ def test_captured_step_with_rccl_group_single_rank():
         red.all_reduce()  # a completed collective before the capture (the watchdog has work to poll)
         opt.zero_grad()
         cap = CapturedStep(net, x, j, 0.0, criterion=crit, zero_grad=opt.zero_grad,
-                           capture_error_mode="thread_local")
+                           capture_error_mode="thread_local", split_at=("hyper",) if split else ())
+        assert len(cap.graphs) == (2 if split else 1)
         for _ in range(2):
             opt.zero_grad()
-            cap.replay()
+            cap.replay(between=red.launch_segments if split else None)
+            if split:
+                assert red.fired == ["refine", "g_s", "hyper"]
             red.all_reduce()
             torch.cuda.synchronize()
             assert red.fired == []
             assert torch.equal(opt.flat.grad, ref)
+        cap.close()
     finally:
         tdist.destroy_process_group()
 
