@@ -79,7 +79,9 @@ __device__ __forceinline__ float4 ld_aux4(const hyres_epilogue& e, const float* 
 
 // Apply the epilogue to one GEMM result v for output pixel ``pix`` / channel n and store it
 // (H: y and the activation operands res / aux0 / out2 are fp16 in HBM).
-template <bool H = false>
+// SAB: the HYRES_EPI_SA_BWD case compiled in (only conv_fwd_body, the one kernel family the launcher routes that
+// epilogue to: every other caller keeps its register allocation — the case cost the weight-resident f16 kernels a spill)
+template <bool H = false, bool SAB = false>
 __device__ __forceinline__ void epi_store(const hyres_epilogue& e, float* y, int ldy, long long pix, int n, float v,
                                           const EpiChannel& c) {
     switch (e.kind) {
@@ -104,8 +106,10 @@ __device__ __forceinline__ void epi_store(const hyres_epilogue& e, float* y, int
             break;
         }
         case HYRES_EPI_SA_BWD: {  // SpatialAttention's mean / max backward: + d mean / C, + d max at the argmax
-            const float* gm = e.aux0 + pix * e.ld0;
-            v = v + gm[0] + (n == reinterpret_cast<const int*>(e.aux2)[pix] ? gm[1] : 0.f);
+            if constexpr (SAB) {
+                const float* gm = e.aux0 + pix * e.ld0;
+                v = v + gm[0] + (n == reinterpret_cast<const int*>(e.aux2)[pix] ? gm[1] : 0.f);
+            }
             break;
         }
         case HYRES_EPI_GDN_BWD:
@@ -132,7 +136,7 @@ __device__ __forceinline__ void epi_store(const hyres_epilogue& e, float* y, int
 __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
 
 // float4 variant of epi_store for channels n..n+3 (all operands 16B aligned).
-template <bool H = false>
+template <bool H = false, bool SAB = false>
 __device__ __forceinline__ void epi_store4(const hyres_epilogue& e, float* y, int ldy, long long pix, int n, float4 v,
                                            float slope, bool use_pre = false,
                                            float4 rpre = make_float4(0.f, 0.f, 0.f, 0.f)) {
@@ -180,11 +184,13 @@ __device__ __forceinline__ void epi_store4(const hyres_epilogue& e, float* y, in
             break;
         }
         case HYRES_EPI_SA_BWD: {  // as in epi_store: (acc + d mean / C) + (channel == argmax ? d max : 0)
-            const float* gm = e.aux0 + pix * e.ld0;
-            const float ga = gm[0], gx = gm[1];
-            const int mi = reinterpret_cast<const int*>(e.aux2)[pix];
+            if constexpr (SAB) {
+                const float* gm = e.aux0 + pix * e.ld0;
+                const float ga = gm[0], gx = gm[1];
+                const int mi = reinterpret_cast<const int*>(e.aux2)[pix];
 #pragma unroll
-            for (int c = 0; c < 4; ++c) o[c] = o[c] + ga + (n + c == mi ? gx : 0.f);
+                for (int c = 0; c < 4; ++c) o[c] = o[c] + ga + (n + c == mi ? gx : 0.f);
+            }
             break;
         }
         case HYRES_EPI_GDN_BWD:
@@ -696,12 +702,12 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
                 pix = (long long)(b * g.Ho + i * g.osh + oph) * g.Wo + j * g.osw + opw;
             }
             if (a.vec4) {
-                epi_store4<YH>(a.e, a.y, g.ldy, pix, n, v, slope);
+                epi_store4<YH, true>(a.e, a.y, g.ldy, pix, n, v, slope);
             } else {
                 const float vv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
                 for (int c = 0; c < 4; ++c)
-                    if (n + c < g.Co) epi_store<YH>(a.e, a.y, g.ldy, pix, n + c, vv[c], epi_channel(a.e, n + c));
+                    if (n + c < g.Co) epi_store<YH, true>(a.e, a.y, g.ldy, pix, n + c, vv[c], epi_channel(a.e, n + c));
             }
         }
     }
@@ -1951,7 +1957,7 @@ __global__ void conv_splitk_reduce_kernel(const ConvArgs a) {
         const int rr = m - b * HqWq;
         const int i = rr / g.Wq, j = rr - (rr / g.Wq) * g.Wq;
         const long long pix = (long long)(b * g.Ho + i * g.osh + g.oph[phase]) * g.Wo + j * g.osw + g.opw[phase];
-        epi_store<H>(a.e, a.y, g.ldy, pix, n, v, epi_channel(a.e, n));
+        epi_store<H, true>(a.e, a.y, g.ldy, pix, n, v, epi_channel(a.e, n));
     }
 }
 
@@ -1982,7 +1988,7 @@ __global__ __launch_bounds__(256) void conv_splitk_reduce4_kernel(const ConvArgs
         const int rr = m - b * HqWq;
         const int i = rr / g.Wq, j = rr - (rr / g.Wq) * g.Wq;
         const long long pix = (long long)(b * g.Ho + i * g.osh + g.oph[phase]) * g.Wo + j * g.osw + g.opw[phase];
-        epi_store4<H>(a.e, a.y, g.ldy, pix, n, v, slope);
+        epi_store4<H, true>(a.e, a.y, g.ldy, pix, n, v, slope);
     }
 }
 

@@ -1623,6 +1623,177 @@ __global__ __launch_bounds__(256, 1) void wgrad_halo_bf6_kernel(const WgradArgs 
 }
 
 // ------------------------------------------------------------------------------------------------
+// wgrad_halo_bf6_kernel (one kernel row of taps per block, KR = 1) with its operand loads two chunks ahead
+// (hyres_conv_tuning key 16 = 2), as wgrad1x1_bf6_pf2_kernel: two register sets alternate, every load an
+// unconditional raw buffer load (an offset past the buffer's end for the halo's out-of-image pixels, channels past N
+// and chunks past the split: 0 without a memory access), so no branch sits around a load. Same products in the same
+// order (bit-identical slabs).
+// ------------------------------------------------------------------------------------------------
+// MINB: blocks per CU the LDS allows (2 for the 3-tap rows and the stride-1 5-tap rows, 1 for the stride-2 5x5): the
+// register bound keeps the compiler from spending the second block's VGPRs on the second register set
+template <int KW, int SQ, int DIL = 1, int MINB = 2>
+__global__ __launch_bounds__(256, MINB) void wgrad_halo_bf6_pf2_kernel(const WgradArgs a, int dhg, int dwg) {
+    constexpr int KR = 1;
+    constexpr int BM = 64, BN = 64, NT = KR * KW, HC = 31 * SQ + DIL * (KW - 1) + 1;
+    constexpr int PP = BM + 32, PQ = BN + 32;
+    constexpr int PSZ = KT * PP, HSZ = KR * HC * PQ, PLANE = PSZ + HSZ, BUF = 3 * PLANE;
+    constexpr int P_V = KT * BM / 4 / 256;
+    constexpr int H_E = KR * HC * (BN / 4);
+    constexpr int H_V = (H_E + 255) / 256;
+    constexpr int OOR = (int)0x80000000;
+    static_assert(PLANE % 4 == 0, "8-byte aligned planes for the transposed reads");
+    static_assert(2 * BUF * 2 <= 160 * 1024, "LDS");
+    __shared__ __attribute__((aligned(16))) __bf16 smem[2 * BUF];
+    const hyres_wgrad_desc& d = a.d;
+    const int tid = threadIdx.x;
+    const int bid = blockIdx.x;
+    const int lb = (bid & 7) * (gridDim.x >> 3) + (bid >> 3);  // XCD-aware order, as wgrad_kernel
+    if (lb >= a.nblocks) return;
+    int rr = lb;
+    const int mt = rr % a.mtiles; rr /= a.mtiles;
+    const int nt = rr % a.ntiles; rr /= a.ntiles;
+    const int grp = rr % a.ngroups;
+    const int split = rr / a.ngroups;
+    const int m0 = mt * BM, n0 = nt * BN;
+    const int t0 = grp * NT;
+    const int dh0 = dhg + grp * KR * DIL;
+    const int cpr = d.Wq / 32;
+    const int pc = (tid % (BM / 4)) * 4, prow0 = tid / (BM / 4);
+    const long long Qtot = (long long)d.B * d.Hq * d.Wq;
+    const __amdgpu_buffer_rsrc_t rp_ = wg_rsrc(a.p, Qtot * d.ldp * 4);
+    const __amdgpu_buffer_rsrc_t rq_ = wg_rsrc(a.q, (long long)d.B * d.Hqq * d.Wqq * d.ldq * 4);
+    const bool pc_ok = m0 + pc < d.M;
+    const int kb = split * a.chunks_per_split;
+    const int ke = min(a.nchunks, kb + a.chunks_per_split);
+    auto load = [&](int kc, float4 (&rp)[P_V], float4 (&rh)[H_V]) {
+        const bool live = kc < ke;
+        const int kcc = live ? kc : kb;
+        const int b = kcc / (d.Hq * cpr);
+        const int rem = kcc - b * d.Hq * cpr;
+        const int i = rem / cpr;
+        const int j0 = (rem - i * cpr) * 32;
+        const long long q0 = (long long)kcc * 32;
+#pragma unroll
+        for (int q = 0; q < P_V; ++q) {
+            const int off = (live && pc_ok) ? (int)(((q0 + prow0 + 16 * q) * d.ldp + m0 + pc) * 4) : OOR;
+            rp[q] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rp_, off, 0, 0));
+        }
+#pragma unroll
+        for (int q = 0; q < H_V; ++q) {
+            const int e = tid + 256 * q;
+            const int pix = e / (BN / 4), c = (e % (BN / 4)) * 4;
+            const int hr = pix / HC, hc = pix - (pix / HC) * HC;
+            const int ih = i * SQ + dh0 + DIL * hr, iw = j0 * SQ + dwg + hc;
+            const bool ok = live && e < H_E && (unsigned)ih < (unsigned)d.Hqq && (unsigned)iw < (unsigned)d.Wqq &&
+                            n0 + c < d.N;
+            const int off = ok ? (int)(((((long long)b * d.Hqq + ih) * d.Wqq + iw) * d.ldq + n0 + c) * 4) : OOR;
+            rh[q] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rq_, off, 0, 0));
+        }
+    };
+    const bool do_bias = a.bias_slab != nullptr && nt == 0 && grp == 0;
+    float4 bsum = make_float4(0.f, 0.f, 0.f, 0.f);
+    auto put = [&](__bf16* base, int o, const float4& v) {
+        bf16x4_t h, m, l;
+        bf6_split4(v, h, m, l);
+        *reinterpret_cast<bf16x4_t*>(&base[o]) = h;
+        *reinterpret_cast<bf16x4_t*>(&base[PLANE + o]) = m;
+        *reinterpret_cast<bf16x4_t*>(&base[2 * PLANE + o]) = l;
+    };
+    auto store = [&](int buf, const float4 (&rp)[P_V], const float4 (&rh)[H_V]) {
+        __bf16* B0 = smem + buf * BUF;
+#pragma unroll
+        for (int q = 0; q < P_V; ++q) {
+            if (do_bias) { bsum.x += rp[q].x; bsum.y += rp[q].y; bsum.z += rp[q].z; bsum.w += rp[q].w; }
+            put(B0, (prow0 + 16 * q) * PP + pc, rp[q]);
+        }
+#pragma unroll
+        for (int q = 0; q < H_V; ++q) {
+            const int e = tid + 256 * q;
+            if (e < H_E) put(B0, PSZ + (e / (BN / 4)) * PQ + (e % (BN / 4)) * 4, rh[q]);
+        }
+    };
+    const int lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int lh = lane >> 5, lg = (lane >> 4) & 1, lq = (lane >> 2) & 3, lp = lane & 3;
+    const int tr_row = 8 * lh + lq, tr_col = 16 * lg + 4 * lp;
+    auto frag = [&](const __bf16* p, int pitch) {
+        const halfx4_t lo = lds_tr4(reinterpret_cast<const _Float16*>(p));
+        const halfx4_t hi = lds_tr4(reinterpret_cast<const _Float16*>(p + 4 * pitch));
+        return __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+    };
+    floatx16 acc[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+    float4 pA[P_V], hA[H_V], pB[P_V], hB[H_V];
+    if (kb < ke) {  // block-uniform
+        load(kb, pA, hA);
+        load(kb + 1, pB, hB);
+        store(0, pA, hA);
+    }
+    __syncthreads();
+    auto body = [&](int kc, int cur, float4 (&pl)[P_V], float4 (&hl)[H_V], const float4 (&pn)[P_V],
+                    const float4 (&hn)[H_V]) {
+        load(kc + 2, pl, hl);
+        const __bf16* Ps = smem + cur * BUF;
+        const __bf16* Hs = Ps + PSZ;
+#pragma unroll
+        for (int s = 0; s < KT / 16; ++s) {
+            bf16x8_t af[3];
+#pragma unroll
+            for (int pl3 = 0; pl3 < 3; ++pl3)
+                af[pl3] = frag(Ps + pl3 * PLANE + (16 * s + tr_row) * PP + wm * 32 + tr_col, PP);
+            static_for<NT>([&](auto J) {
+                constexpr int t = decltype(J)::value;
+                constexpr int hr = t / KW, hc = t % KW;
+                const int ob = (hr * HC + DIL * hc + SQ * (16 * s + tr_row)) * PQ + wn * 32 + tr_col;
+                bf16x8_t bf[3];
+#pragma unroll
+                for (int pl3 = 0; pl3 < 3; ++pl3) bf[pl3] = frag(Hs + pl3 * PLANE + ob, SQ * PQ);
+                acc[t] = bf6_mfma(af, bf, acc[t]);
+            });
+        }
+        if (kc + 1 < ke) store(cur ^ 1, pn, hn);  // block-uniform
+        __syncthreads();
+    };
+    for (int kc = kb; kc < ke; kc += 2) {
+        body(kc, 0, pA, hA, pB, hB);
+        if (kc + 1 < ke) body(kc + 1, 1, pB, hB, pA, hA);
+    }
+    if (do_bias) {  // block-uniform
+        float4* red = reinterpret_cast<float4*>(smem);  // the loop ended with a barrier
+        red[tid] = bsum;
+        __syncthreads();
+        if (tid < BM / 4) {
+            float4 s4 = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int r = 0; r < 256 / (BM / 4); ++r) {
+                const float4 v = red[tid + r * (BM / 4)];
+                s4.x += v.x; s4.y += v.y; s4.z += v.z; s4.w += v.w;
+            }
+            float* dst = a.bias_slab + (long long)split * d.M + m0 + 4 * tid;
+            const float sv[4] = {s4.x, s4.y, s4.z, s4.w};
+            for (int c = 0; c < 4; ++c)
+                if (m0 + 4 * tid + c < d.M) dst[c] = sv[c];
+        }
+    }
+    const int lr = lane & 31;
+    const long long MN = (long long)d.M * d.N;
+    static_for<NT>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        const int n = n0 + wn * 32 + lr;
+        if (n < d.N) {
+            float* out = a.slab + ((long long)split * d.ntaps + t0 + j) * MN + n;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                if (m < d.M) out[(long long)m * d.N] = acc[j][r];
+            }
+        }
+    });
+}
+
+// ------------------------------------------------------------------------------------------------
 // Thin-operand weight gradient: dW[t][m][n] = sum_q P[q][m] * Q[shift_t(q)][n] with N <= 4 (the 3-channel
 // image side: refine conv 3->64 / 64->3 at 256^2 (the latter through the swapped descriptor), g_a's 5x5 s2
 // conv 3->128, g_s's deconv 128->3) and M = 64*MW wide channels. An MFMA tile would be >90 % padding and
@@ -2321,6 +2492,16 @@ static int wgrad_issue(const hyres_wgrad_desc* d0, const float* pp, const float*
         else if (io == 2) halo16g(std::integral_constant<int, 2>{});
         else if (io == 3) halo16g(std::integral_constant<int, 3>{});
         else halo16g(std::integral_constant<int, 0>{});
+    } else if (p.halo && f32_gemm_bf6() && g_tune[16] == 2 && (p.NT == 3 || p.hk == 5) &&
+               (long long)d->B * d->Hqq * d->Wqq * d->ldq * 4 < 0x7FFFFFF0LL &&
+               (long long)d->B * d->Hq * d->Wq * d->ldp * 4 < 0x7FFFFFF0LL) {  // loads two chunks ahead (key 16 = 2)
+        if (p.hk == 3 && p.hdil == 2)
+            hipLaunchKernelGGL((wgrad_halo_bf6_pf2_kernel<3, 1, 2>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
+        else if (p.hk == 3)
+            hipLaunchKernelGGL((wgrad_halo_bf6_pf2_kernel<3, 1, 1>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
+        else if (d->sq == 1)
+            hipLaunchKernelGGL((wgrad_halo_bf6_pf2_kernel<5, 1, 1>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
+        else hipLaunchKernelGGL((wgrad_halo_bf6_pf2_kernel<5, 2, 1, 1>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);
     } else if (p.halo && f32_gemm_bf6()) {  // fp32 operands (fp16 ones were converted above), bf16x6 products
         if (p.hk == 3 && p.NT == 3 && p.hdil == 2)
             hipLaunchKernelGGL((wgrad_halo_bf6_kernel<1, 3, 1, 2>), grid, dim3(256), 0, st, a, p.hdh, p.hdw);

@@ -189,7 +189,9 @@ int hyres_conv_plan(const hyres_conv_geom* g, const hyres_epilogue* e, int* tile
                                        * (conv3x3_wres_bf6 / _f32); 0: the implicit GEMM (A/B) */
 #define HYRES_TUNE_WGRAD_PF 15        /* bf16x6 1x1 weight gradients: 2 = operand loads two chunks ahead
                                        * (wgrad1x1_bf6_pf2_kernel), 1 = one chunk ahead (wgrad1x1_bf6_kernel) */
-#define HYRES_TUNE_KEYS 20            /* keys 16..19 reserved */
+#define HYRES_TUNE_WGRAD_HALO_PF 16   /* bf16x6 halo weight gradients (one kernel row of taps per block): 2 = operand
+                                       * loads two chunks ahead (wgrad_halo_bf6_pf2_kernel), 1 = one chunk ahead */
+#define HYRES_TUNE_KEYS 20            /* keys 17..19 reserved */
 int hyres_conv_tuning(int key, int value, int* old);
 
 /* Weight gradient:  dW[t][m][n] = sum_q P[q][m] * Q[shift_t(q)][n]  over a base grid q (B,Hq,Wq).

@@ -127,8 +127,10 @@ def kernels(so_path: str, arch: str = "gfx950") -> list[dict]:
     out = []
     for k in (k for d in docs for k in d["amdhsa.kernels"]):
         vg, ag = int(k[".vgpr_count"]), int(k.get(".agpr_count", 0))
-        # gfx90a+: AGPRs follow the arch VGPRs at accum_offset (a multiple of 4); the allocation granule is 8
-        total = (((vg + 3) // 4) * 4 + ag) if ag else vg
+        # gfx90a+: .vgpr_count is already the unified total (the arch VGPRs aligned to 4, then the AGPRs at
+        # accum_offset; LLVM's NumVGPRsForWavesPerEU) — 395 on a kernel cannot be arch registers alone (v0..v255).
+        # The allocation granule is 8
+        total = vg
         alloc = max(GRANULE, -(-total // GRANULE) * GRANULE)
         out.append({"name": k[".name"], "vgpr": vg, "agpr": ag, "alloc": alloc,
                     "lds": int(k[".group_segment_fixed_size"]), "threads": int(k[".max_flat_workgroup_size"]),
