@@ -425,30 +425,6 @@ __global__ __launch_bounds__(256) void sa_pool_kernel(const float* x, float* poo
         amax[p] = mi;
     }
 }
-__global__ void sa_conv_kernel(const float* pooled2, const float* w, float* attn, int B, int H, int W) {
-    // 7x7, 2 -> 1, pad 3, no bias, then sigmoid. w: [1][2][7][7]
-    __shared__ float ws[98];
-    if (threadIdx.x < 98) ws[threadIdx.x] = w[threadIdx.x];
-    __syncthreads();
-    const long long n = (long long)B * H * W;
-    GRID_STRIDE(i, n) {
-        const int ww = (int)(i % W);
-        const int hh = (int)((i / W) % H);
-        const int b = (int)(i / ((long long)W * H));
-        float s = 0.f;
-        for (int ch = 0; ch < 2; ++ch)
-            for (int kh = 0; kh < 7; ++kh) {
-                int ih = hh + kh - 3;
-                if (ih < 0 || ih >= H) continue;
-                for (int kw = 0; kw < 7; ++kw) {
-                    int iw = ww + kw - 3;
-                    if (iw < 0 || iw >= W) continue;
-                    s += ws[ch * 49 + kh * 7 + kw] * pooled2[(((long long)b * H + ih) * W + iw) * 2 + ch];
-                }
-            }
-        attn[i] = 1.0f / (1.0f + expf(-s));
-    }
-}
 // y = x * attn[p], float4 over channels (C % 4 == 0)
 template <bool H = false>
 __global__ void sa_mul_kernel(const float* x, const float* attn, float* y, long long P, int C) {
@@ -484,59 +460,110 @@ __global__ void sa_bwd_logit_kernel(const float* x, const float* gy, const float
         glogit[p] = s * a * (1.0f - a);
     }
 }
-// bwd 2: g_pooled2 = transpose conv; weight-grad partials per block (wave shuffles, one barrier)
-// (C > 0: the mean's gradient is stored divided by C, the form HYRES_EPI_SA_BWD adds per channel)
-__global__ __launch_bounds__(256) void sa_bwd_conv_kernel(const float* glogit, const float* pooled2, const float* w,
-                                                          float* gpooled2, float* wpart, int B, int H, int W,
-                                                          int C = 0) {
+// ---- SpatialAttention's 7x7 (2 -> 1) conv on 16 x 16 pixel tiles staged with their 3-pixel halo in LDS (the
+// per-pixel kernels above gather every tap from global memory: 71 us forward / 179 us backward at 16 x 256^2).
+constexpr int SA_T = 16, SA_L = SA_T + 6;
+__device__ __forceinline__ void sa_tile_of(int B, int H, int W, int& b, int& h0, int& w0) {
+    const int tw = (W + SA_T - 1) / SA_T, th = (H + SA_T - 1) / SA_T;
+    int t = blockIdx.x;
+    const int tx = t % tw; t /= tw;
+    const int ty = t % th;
+    b = t / th;
+    h0 = ty * SA_T;
+    w0 = tx * SA_T;
+}
+// forward: attn = sigmoid(sum_{ch, kh, kw} w * pooled2), the per-pixel kernel's summation order (bit-identical)
+__global__ __launch_bounds__(256) void sa_conv_tiled_kernel(const float* pooled2, const float* w, float* attn, int B,
+                                                            int H, int W) {
     __shared__ float ws[98];
-    __shared__ float red[4][98];
-    if (threadIdx.x < 98) ws[threadIdx.x] = w[threadIdx.x];
+    __shared__ float pl[2][SA_L][SA_L + 1];
+    int b, h0, w0;
+    sa_tile_of(B, H, W, b, h0, w0);
+    const int tid = threadIdx.x;
+    if (tid < 98) ws[tid] = w[tid];
+    for (int e = tid; e < SA_L * SA_L; e += 256) {
+        const int ly = e / SA_L, lx = e - ly * SA_L;
+        const int ih = h0 - 3 + ly, iw = w0 - 3 + lx;
+        const bool ok = (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+        const float2 v = ok ? *reinterpret_cast<const float2*>(pooled2 + (((long long)b * H + ih) * W + iw) * 2)
+                            : make_float2(0.f, 0.f);
+        pl[0][ly][lx] = v.x;
+        pl[1][ly][lx] = v.y;
+    }
     __syncthreads();
-    const long long n = (long long)B * H * W;
-    float gw[98];
-#pragma unroll
-    for (int k = 0; k < 98; ++k) gw[k] = 0.f;
-    GRID_STRIDE(i, n) {
-        const int ww = (int)(i % W);
-        const int hh = (int)((i / W) % H);
-        const int b = (int)(i / ((long long)W * H));
-        float g0 = 0.f, g1 = 0.f;
-        const float gl = glogit[i];
+    const int ty = tid / SA_T, tx = tid % SA_T;
+    const int hh = h0 + ty, ww = w0 + tx;
+    if (hh >= H || ww >= W) return;
+    float s = 0.f;
+    for (int ch = 0; ch < 2; ++ch)
 #pragma unroll
         for (int kh = 0; kh < 7; ++kh) {
+            const int ih = hh + kh - 3;
+            if (ih < 0 || ih >= H) continue;
 #pragma unroll
             for (int kw = 0; kw < 7; ++kw) {
-                // input-gradient: output (hh - kh + 3, ww - kw + 3) used input (hh, ww) with tap (kh,kw)
-                int oh = hh - kh + 3, ow = ww - kw + 3;
-                if (oh >= 0 && oh < H && ow >= 0 && ow < W) {
-                    float go = glogit[((long long)b * H + oh) * W + ow];
+                const int iw = ww + kw - 3;
+                if (iw < 0 || iw >= W) continue;
+                s += ws[ch * 49 + kh * 7 + kw] * pl[ch][ty + kh][tx + kw];
+            }
+        }
+    attn[((long long)b * H + hh) * W + ww] = 1.0f / (1.0f + expf(-s));
+}
+// backward: gpooled2 (the per-pixel kernel's order: bit-identical) and per-tile weight-gradient partials (98 taps x 2
+// half-tiles of 8 rows, summed in a fixed order); C > 0: the mean's gradient stored divided by C (HYRES_EPI_SA_BWD)
+__global__ __launch_bounds__(256) void sa_bwd_conv_tiled_kernel(const float* glogit, const float* pooled2,
+                                                                const float* w, float* gpooled2, float* wpart, int B,
+                                                                int H, int W, int C) {
+    __shared__ float ws[98];
+    __shared__ float gl[SA_L][SA_L + 1];
+    __shared__ float pl[2][SA_L][SA_L + 1];
+    __shared__ float half2s[98];
+    int b, h0, w0;
+    sa_tile_of(B, H, W, b, h0, w0);
+    const int tid = threadIdx.x;
+    if (tid < 98) ws[tid] = w[tid];
+    for (int e = tid; e < SA_L * SA_L; e += 256) {
+        const int ly = e / SA_L, lx = e - ly * SA_L;
+        const int ih = h0 - 3 + ly, iw = w0 - 3 + lx;
+        const bool ok = (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+        const long long p = ((long long)b * H + ih) * W + iw;
+        const float2 v = ok ? *reinterpret_cast<const float2*>(pooled2 + p * 2) : make_float2(0.f, 0.f);
+        gl[ly][lx] = ok ? glogit[p] : 0.f;
+        pl[0][ly][lx] = v.x;
+        pl[1][ly][lx] = v.y;
+    }
+    __syncthreads();
+    {
+        const int ty = tid / SA_T, tx = tid % SA_T;
+        const int hh = h0 + ty, ww = w0 + tx;
+        if (hh < H && ww < W) {
+            float g0 = 0.f, g1 = 0.f;
+#pragma unroll
+            for (int kh = 0; kh < 7; ++kh)
+#pragma unroll
+                for (int kw = 0; kw < 7; ++kw) {
+                    const float go = gl[ty + 6 - kh][tx + 6 - kw];  // output (hh - kh + 3, ww - kw + 3); 0 outside
                     g0 += ws[kh * 7 + kw] * go;
                     g1 += ws[49 + kh * 7 + kw] * go;
                 }
-                // weight-gradient: this output pixel i times input (hh + kh - 3, ww + kw - 3)
-                int ih = hh + kh - 3, iw = ww + kw - 3;
-                if (ih >= 0 && ih < H && iw >= 0 && iw < W) {
-                    const float* pp = pooled2 + (((long long)b * H + ih) * W + iw) * 2;
-                    gw[kh * 7 + kw] += gl * pp[0];
-                    gw[49 + kh * 7 + kw] += gl * pp[1];
-                }
-            }
+            const long long i = ((long long)b * H + hh) * W + ww;
+            gpooled2[i * 2 + 0] = C > 0 ? g0 / (float)C : g0;
+            gpooled2[i * 2 + 1] = g1;
         }
-        gpooled2[i * 2 + 0] = C > 0 ? g0 / (float)C : g0;
-        gpooled2[i * 2 + 1] = g1;
     }
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    // weight gradient: tap k = (ch, kh, kw) sums glogit[p] * pooled2[ch][p + (kh - 3, kw - 3)] over the tile's pixels
+    // (glogit is 0 outside the image), rows [8 * hf, 8 * hf + 8) per half
+    float acc = 0.f;
+    const int k = tid % 98, hf = tid / 98;
+    if (tid < 196) {
+        const int ch = k / 49, kh = (k % 49) / 7, kw = k % 7;
+        for (int ty = 8 * hf; ty < 8 * hf + 8; ++ty)
 #pragma unroll
-    for (int k = 0; k < 98; ++k) {
-        float v = gw[k];
-        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-        if (lane == 0) red[wave][k] = v;
+            for (int tx = 0; tx < SA_T; ++tx) acc += gl[ty + 3][tx + 3] * pl[ch][ty + kh][tx + kw];
+        if (hf == 1) half2s[k] = acc;
     }
     __syncthreads();
-    if (threadIdx.x < 98)
-        wpart[(long long)blockIdx.x * 98 + threadIdx.x] =
-            (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]);
+    if (tid < 98) wpart[(long long)blockIdx.x * 98 + tid] = acc + half2s[tid];
 }
 // one block per weight tap: 256 threads fold the per-block partials (deterministic order)
 __global__ void sa_bwd_wfinal_kernel(const float* wpart, int nb, float* gw) {
@@ -826,10 +853,14 @@ static int sa_bwd_blocks(long long n) {  // >= 4 pixels per thread: the 98-tap w
     return (int)std::max<long long>(1, std::min<long long>((n + 255) / 256, 1024));
 }
 
+static long long sa_tiles(int B, int H, int W) {
+    return (long long)B * ((H + SA_T - 1) / SA_T) * ((W + SA_T - 1) / SA_T);
+}
+
 long long hyres_spatial_attn_workspace_bytes(int B, int H, int W) {
     long long n = (long long)B * H * W;
-    int nb = sa_bwd_blocks(n);
-    return (long long)nb * 98 * 4 + n * 4 + n * 2 * 4 + 1024;
+    const long long nb = std::max<long long>(sa_bwd_blocks(n), sa_tiles(B, H, W));
+    return nb * 98 * 4 + n * 4 + n * 2 * 4 + 1024;
 }
 
 int hyres_spatial_attn_fwd(const float* x, const float* w, float* pooled2, int* argmax, float* attn, float* y, int B,
@@ -843,7 +874,8 @@ int hyres_spatial_attn_fwd(const float* x, const float* w, float* pooled2, int* 
     hipLaunchKernelGGL(sa_pool_kernel<false>, dim3((unsigned)((P + 15) / 16)), dim3(256), 0, st, x, pooled2, argmax, P, C);
     int rc = HY_LAUNCH_CHECK("sa_pool");
     if (rc) return rc;
-    hipLaunchKernelGGL(sa_conv_kernel, dim3(grid_for_r(P)), dim3(256), 0, st, (const float*)pooled2, w, attn, B, H, W);
+    hipLaunchKernelGGL(sa_conv_tiled_kernel, dim3((unsigned)sa_tiles(B, H, W)), dim3(256), 0, st, (const float*)pooled2,
+                       w, attn, B, H, W);
     rc = HY_LAUNCH_CHECK("sa_conv");
     if (rc) return rc;
     if (!y) return ok();  // the attention map only (the multiply folded into the consumer: HYRES_EPI_ROWSCALE)
@@ -863,7 +895,8 @@ int hyres_spatial_attn_fwd_f16(const void* x, const float* w, float* pooled2, in
                        argmax, P, C);
     int rc = HY_LAUNCH_CHECK("sa_pool_f16");
     if (rc) return rc;
-    hipLaunchKernelGGL(sa_conv_kernel, dim3(grid_for_r(P)), dim3(256), 0, st, (const float*)pooled2, w, attn, B, H, W);
+    hipLaunchKernelGGL(sa_conv_tiled_kernel, dim3((unsigned)sa_tiles(B, H, W)), dim3(256), 0, st, (const float*)pooled2,
+                       w, attn, B, H, W);
     rc = HY_LAUNCH_CHECK("sa_conv");
     if (rc) return rc;
     if (!y) return ok();  // the attention map only
@@ -893,9 +926,9 @@ static int spatial_attn_bwd_impl(const float* x, const float* w, const float* po
                        glogit, P, C);
     int rc = HY_LAUNCH_CHECK("sa_bwd_logit");
     if (rc) return rc;
-    int nb = sa_bwd_blocks(P);
-    hipLaunchKernelGGL(sa_bwd_conv_kernel, dim3(nb), dim3(256), 0, st, (const float*)glogit, pooled2, w, gp2, wpart, B,
-                       H, W);
+    const int nb = (int)sa_tiles(B, H, W);
+    hipLaunchKernelGGL(sa_bwd_conv_tiled_kernel, dim3(nb), dim3(256), 0, st, (const float*)glogit, pooled2, w, gp2,
+                       wpart, B, H, W, 0);
     rc = HY_LAUNCH_CHECK("sa_bwd_conv");
     if (rc) return rc;
     hipLaunchKernelGGL(sa_bwd_wfinal_kernel, dim3(98), dim3(256), 0, st, (const float*)wpart, nb, gw);
@@ -936,9 +969,11 @@ int hyres_spatial_attn_bwd_map(const float* glogit, const float* pooled2, const 
                "spatial_attn_bwd_map: workspace");
     const long long P = (long long)B * H * W;
     float* wpart = (float*)ws;
-    const int nb = sa_bwd_blocks(P);
+    const int nb = (int)sa_tiles(B, H, W);
+    (void)P;
     hipStream_t st = as_stream(s);
-    hipLaunchKernelGGL(sa_bwd_conv_kernel, dim3(nb), dim3(256), 0, st, glogit, pooled2, w, gpooled2, wpart, B, H, W, C);
+    hipLaunchKernelGGL(sa_bwd_conv_tiled_kernel, dim3(nb), dim3(256), 0, st, glogit, pooled2, w, gpooled2, wpart, B, H,
+                       W, C);
     int rc = HY_LAUNCH_CHECK("sa_bwd_conv");
     if (rc) return rc;
     hipLaunchKernelGGL(sa_bwd_wfinal_kernel, dim3(98), dim3(256), 0, st, (const float*)wpart, nb, gw);
