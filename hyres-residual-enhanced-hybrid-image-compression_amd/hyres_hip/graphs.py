@@ -154,7 +154,13 @@ class CapturedStep:
         next one (same memory pool, same capture stream) when a split marker fires in the tape backward — every
         weight-gradient reduce of the finished segments is flushed by the marker first (GradReady.mark), and the
         side stream, if used, is joined so the capture closes with no forked stream open. The markers are placed at
-        module boundaries, where the branch streams are joined."""
+        module boundaries, where the branch streams are joined.
+
+        The capture runs in "relaxed" mode: the cut happens inside the tape backward, i.e. on torch's autograd device
+        thread, and a thread-local capture may only be ended by the thread that began it (HIP refuses with
+        hipErrorStreamCaptureWrongThread); a global one would treat the RCCL watchdog thread's event polling as an
+        unsafe call. Relaxed capture checks neither — no collective and no synchronising call is inside the graphs."""
+        capture_error_mode = "relaxed"
         st = {"on": False, "idx": 0, "seen": []}
 
         def cut(name):

@@ -187,10 +187,11 @@ int hyres_conv_plan(const hyres_conv_geom* g, const hyres_epilogue* e, int* tile
                                        * conv_narrow_strip_kernel (4-pixel strips, weights in VGPRs); 0: conv_narrow_kernel */
 #define HYRES_TUNE_WRES32 14          /* 1 (default): fp32 3x3 Ci = 64 convs on the weight-resident kernels
                                        * (conv3x3_wres_bf6 / _f32); 0: the implicit GEMM (A/B) */
-#define HYRES_TUNE_WGRAD_PF 15        /* bf16x6 1x1 weight gradients: 2 = operand loads two chunks ahead
+#define HYRES_TUNE_WGRAD_PF 15        /* bf16x6 1x1 weight gradients: 2 (default) = operand loads two chunks ahead
                                        * (wgrad1x1_bf6_pf2_kernel), 1 = one chunk ahead (wgrad1x1_bf6_kernel) */
-#define HYRES_TUNE_WGRAD_HALO_PF 16   /* bf16x6 halo weight gradients (one kernel row of taps per block): 2 = operand
-                                       * loads two chunks ahead (wgrad_halo_bf6_pf2_kernel), 1 = one chunk ahead */
+#define HYRES_TUNE_WGRAD_HALO_PF 16   /* bf16x6 3x3 halo weight gradients (one kernel row of 3 taps per block): 2
+                                       * (default) = operand loads two chunks ahead (wgrad_halo_bf6_pf2_kernel), 1 = one
+                                       * chunk ahead; the 5x5s stay on wgrad_halo_bf6_kernel (slower two ahead) */
 #define HYRES_TUNE_KEYS 20            /* keys 17..19 reserved */
 int hyres_conv_tuning(int key, int value, int* old);
 

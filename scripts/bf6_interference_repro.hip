@@ -20,7 +20,12 @@
 //       -Lhyres-residual-enhanced-hybrid-image-compression_amd/hyres_hip -lhyres_hip \
 //       -Wl,-rpath,'$ORIGIN/../hyres-residual-enhanced-hybrid-image-compression_amd/hyres_hip' \
 //       -o scripts/bf6_interference_repro
-//   scripts/bf6_interference_repro [reps] [delay_us between the conv's launch and the victims'] [wres|native|igemm|ru|wg1x1|wghalo]
+//   scripts/bf6_interference_repro [reps] [delay_us between the conv's launch and the victims'] [wres|native|igemm|ru|wg1x1|wghalo|native-b6v]
+//
+// native-b6v (round 6, the r5v pairing of profiles/r5v_refine_determinism_fail.log): the native fp32-MFMA weight-resident
+// 3x3 as the hog and, as an extra victim, a bf16x6 conv of the library (3x3 64->64 on the bf16x6 implicit GEMM,
+// conv_fwd_b6_kernel: hyres_conv_tuning key 7 = 1 and key 14 = 0 while the victim is enqueued, key 7 = 0 and key 14 = 1
+// while the hog is) — the mixed-GEMM configuration in which the native kernel's hole was hit.
 #include <hip/hip_runtime.h>
 
 #include <chrono>
@@ -105,7 +110,7 @@ static double wall() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-static const char* KNAME[] = {"bilin(pk_f32)", "scalar(v_fma)", "copy", "copy4", "lib bilinear"};
+static const char* KNAME[] = {"bilin(pk_f32)", "scalar(v_fma)", "copy", "copy4", "lib bilinear", "lib bf16x6 conv"};
 constexpr long long NOUT = 2LL * 128 * 128 * 64;
 
 int main(int argc, char** argv) {
@@ -120,6 +125,8 @@ int main(int argc, char** argv) {
     const char* hogname = argc > 3 ? argv[3] : "wres";
     const bool ru = strcmp(hogname, "ru") == 0;
     const bool wg1 = strcmp(hogname, "wg1x1") == 0, wgh = strcmp(hogname, "wghalo") == 0, wg = wg1 || wgh;
+    const bool b6v = strcmp(hogname, "native-b6v") == 0;
+    const bool native = b6v || strcmp(hogname, "native") == 0;
     const int B = 2, H = 256, W = 256, C = 64;
     const long long nx = (long long)B * H * W * C;
     std::vector<float> hx(nx), hf(nx), hw(C * C * 9), hb(C);
@@ -198,9 +205,20 @@ int main(int argc, char** argv) {
     e.act = HYRES_ACT_PRELU;
     e.bias = db;
     e.slope = dslope;
-    CH(hyres_conv_tuning(HYRES_TUNE_F32_GEMM, strcmp(hogname, "native") == 0 ? 0 : 1, nullptr));
+    CH(hyres_conv_tuning(HYRES_TUNE_F32_GEMM, native ? 0 : 1, nullptr));
     char kname[128];
+    // the bf16x6 victim conv: x [2][256][256][64] -> [2][256][256][64] (4 * NOUT floats), its own weight layout
+    float* dw2v = nullptr;
+    if (b6v) {
+        CK(hipMalloc(&dw2v, hw.size() * 4));
+        CH(hyres_conv_weight_prep(&g, dw, dw2v, HYRES_WPREP_CONV, C, C, 3, 3, 1, nullptr, sa));
+        CK(hipStreamSynchronize(sa));
+    }
     auto conv = [&]() {
+        if (b6v) {  // the hog: the native weight-resident kernel
+            CH(hyres_conv_tuning(HYRES_TUNE_F32_GEMM, 0, nullptr));
+            CH(hyres_conv_tuning(HYRES_TUNE_WRES32, 1, nullptr));
+        }
         if (wg)
             CH(hyres_conv_wgrad(&wd, wp, wq, wdst, nullptr, wws, wwsb, sa));
         else if (ru)
@@ -215,8 +233,13 @@ int main(int argc, char** argv) {
         if (kind == 2) hipLaunchKernelGGL(victim<2>, grid, dim3(256), 0, s, dx, out);
         if (kind == 3) hipLaunchKernelGGL(victim<3>, grid, dim3(256), 0, s, dx, out);
         if (kind == 4) CH(hyres_bilinear_fwd(dx, 64, out, 64, 2, 256, 256, 128, 128, 64, 2.0f, 2.0f, 0, s));
+        if (kind == 5) {  // bf16x6 implicit GEMM while the hog's keys are restored by the next conv()
+            CH(hyres_conv_tuning(HYRES_TUNE_F32_GEMM, 1, nullptr));
+            CH(hyres_conv_tuning(HYRES_TUNE_WRES32, 0, nullptr));
+            CH(hyres_conv_forward(&g, dx, dw2v, 9 * C, out, &e, nullptr, 0, s));
+        }
     };
-    const long long vsz[5] = {NOUT, NOUT, NOUT, 4 * NOUT, NOUT};
+    const long long vsz[6] = {NOUT, NOUT, NOUT, 4 * NOUT, NOUT, 4 * NOUT};
     std::vector<float> ref(4 * NOUT), got(4 * NOUT * NV), y0(nx), y1(nx);
     const bool wres = strcmp(hogname, "wres") == 0;
     for (int guard = wres ? 0 : 1; guard < 2; ++guard) {
@@ -233,8 +256,9 @@ int main(int argc, char** argv) {
                                : wgh ? "3x3 weight gradient 64->64 2x256x256 (wgrad_halo_bf6_kernel)"
                                : ru ? "fused ResidualUnit f16 (ru_fused_f16_kernel, 2x256x256x128)"
                                   : (dil == 2 ? "dilation-2 3x3 64->64 2x256x256 on the bf16x6 implicit GEMM"
+                                              : b6v ? "3x3 64->64 2x256x256 fp32-MFMA weight-resident (native), bf16x6 conv victim"
                                               : "3x3 64->64 2x256x256 fp32-MFMA weight-resident (native)"));
-        for (int kind = 4; kind >= 0; --kind) {
+        for (int kind = b6v ? 5 : 4; kind >= (b6v ? 4 : 0); --kind) {
             launch(kind, dref, sa);
             CK(hipStreamSynchronize(sa));
             CK(hipMemcpy(ref.data(), dref, vsz[kind] * 4, hipMemcpyDeviceToHost));

@@ -662,3 +662,51 @@ def test_wres_bf6_dilation2_matches_fp64(B, H, W, act):
     assert names[1] == "conv3x3_wres_bf6_kernel" and names[0] != names[1], names
     assert ey[1] < 1e-5 and ey[1] <= 2 * ey[0] + 1e-9
     assert eg[1] < 1e-5 and eg[1] <= 2 * eg[0] + 1e-9
+
+
+@pytest.mark.parametrize("K,B,H,W,Ci,Co,key", [
+    (1, 2, 30, 30, 96, 160, 15),    # 1x1: ragged pixel chunks (1800 px) and channel tiles
+    (1, 4, 64, 64, 64, 128, 15),
+    (1, 2, 128, 128, 128, 64, 15),
+    (3, 2, 64, 64, 64, 64, 16),     # 3x3 rows of taps on the halo kernel
+    (3, 3, 32, 96, 96, 96, 16),     # 96 channels: a partial 64-wide tile
+    (3, 2, 128, 128, 64, 128, 16),
+])
+def test_wgrad_prefetch2_kernels_bit_identical(K, B, H, W, Ci, Co, key):
+    """wgrad1x1_bf6_pf2_kernel (hyres_conv_tuning key 15) and wgrad_halo_bf6_pf2_kernel (key 16): operand loads two
+    32-pixel chunks ahead through unconditional buffer loads — the same products in the same order as the one-ahead
+    kernels, so weight and bias gradients are equal bit for bit (ragged chunks and tiles included), and within fp32
+    accuracy of the fp64 reference (reference: the weight gradients of models/layers/attention.py:11-30's convs)."""
+    import ctypes
+    from hyres_hip import _lib as L
+    D = dev()
+    g = torch.Generator().manual_seed(5)
+    x = (torch.rand((B, H, W, Ci), generator=g) * 2 - 1).to(D)
+    gy = (torch.rand((B, H, W, Co), generator=g) * 2 - 1).to(D)
+    d = L.WgradDesc()
+    L.call("hyres_wgrad_desc_conv2d", ctypes.byref(d), B, H, W, Ci, Ci, Co, Co, K, K, 1, K // 2, 1)
+    d.sm = Ci * K * K
+    nb = L.load().hyres_wgrad_workspace_bytes(ctypes.byref(d))
+    ws = torch.empty(nb // 4 + 16, device=D)
+    old = ctypes.c_int(0)
+    L.call("hyres_conv_tuning", 7, 1, ctypes.byref(old))
+    res = {}
+    try:
+        for v in (1, 2):
+            L.call("hyres_conv_tuning", key, v, None)
+            dw = torch.zeros((Co, Ci, K, K), device=D)
+            db = torch.zeros((Co,), device=D)
+            L.call("hyres_conv_wgrad", ctypes.byref(d), gy.data_ptr(), x.data_ptr(), dw.data_ptr(), db.data_ptr(),
+                   ws.data_ptr(), nb, L.stream())
+            torch.cuda.synchronize()
+            res[v] = (dw.cpu(), db.cpu())
+    finally:
+        L.call("hyres_conv_tuning", key, 2, None)
+        L.call("hyres_conv_tuning", 7, old.value, None)
+    assert torch.equal(res[1][0], res[2][0]) and torch.equal(res[1][1], res[2][1])
+    xr = x.cpu().double().permute(0, 3, 1, 2)
+    gr = gy.cpu().double().permute(0, 3, 1, 2)
+    ref = torch.nn.grad.conv2d_weight(xr, (Co, Ci, K, K), gr, padding=K // 2)
+    err = float((res[2][0].double() - ref).abs().max() / ref.abs().max())
+    assert err < 1e-5, err
+    assert float((res[2][1].double() - gr.sum((0, 2, 3))).abs().max()) < 1e-3
