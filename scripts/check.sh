@@ -53,6 +53,9 @@ for ph in "$@"; do
            grep -h "us," gpurun_out/bf16x6_probe.log gpurun_out/bf6_micro.log gpurun_out/bf6_families.log > gpurun_out/${tag}_bf6_micro.txt ;;
     wgpf)  scripts/gpu_run.sh "wgpf:300:for s in '--H 128 --Ci 64 --Co 128' '--H 128 --Ci 128 --Co 64' '--H 128 --Ci 128 --Co 128' '--H 256 --Ci 64 --Co 64' '--H 256 --Ci 64 --Co 192' '--H 64 --Ci 64 --Co 128' '--H 32 --Ci 96 --Co 192' '--H 32 --Ci 640 --Co 768'; do python3 scripts/wgrad_micro.py \$s --K 1 --ab 15=1,2,1,2; done; for s in '--H 128 --Ci 64 --Co 64' '--H 256 --Ci 64 --Co 64' '--H 64 --Ci 64 --Co 64' '--H 128 --Ci 128 --Co 128' '--H 32 --Ci 96 --Co 96'; do python3 scripts/wgrad_micro.py \$s --K 3 --ab 16=1,2,1,2; done; python3 scripts/wgrad_micro.py --H 32 --Ci 192 --Co 384 --K 5 --ab 16=1,2,1,2" || exit $?
            grep -h "key1[56]" gpurun_out/wgpf.log > gpurun_out/${tag}_wgrad_pf_ab.txt ;;
+    serial) scripts/gpu_run.sh "serial_fp32:300:rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${tag}_serial -o run -- python3 scripts/step_profile.py --marker --serial --steps 10" || exit $?
+           python3 scripts/prof_summary.py gpurun_out/${tag}_serial/run_kernel_trace.csv 10 > gpurun_out/${tag}_train_serial_summary.txt ;;
+    pmcfam) bash scripts/pmc_families.sh $tag || exit $? ;;
     repro) scripts/gpu_run.sh "repro_native_b6v:200:scripts/bf6_interference_repro 20 30 native-b6v" || exit $?
            cp gpurun_out/repro_native_b6v.log gpurun_out/${tag}_repro_native_b6v.txt ;;
     *) echo "unknown phase $ph"; exit 2 ;;

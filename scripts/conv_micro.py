@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--relu", action="store_true")
     ap.add_argument("--res", action="store_true", help="fused residual add (RU / RBB tail)")
+    ap.add_argument("--mask", action="store_true",
+                    help="1x1 with the ReLU-mask epilogue (the input-gradient into a ReLU output), fp32 only")
     ap.add_argument("--f16", action="store_true", help="fp16 operands (autocast)")
     ap.add_argument("--tile", type=int, default=-1, help="force a conv tile (hyres_conv_tuning key 0)")
     ap.add_argument("--bf6", action="store_true", help="fp32 GEMM on the bf16 MFMA (hyres_conv_tuning key 7; default here: native)")
@@ -53,6 +55,30 @@ def main():
     b = torch.randn(a.Co, device=dev)
     act = L.ACT_RELU if a.relu else L.ACT_NONE
     res = O.Node(torch.randn(a.B, a.H // a.stride, a.H // a.stride, a.Co, device=dev).to(adt), rg=False) if a.res else None
+    if a.mask:  # low-level launch: the mask operand (a ReLU output) rides in aux0, as ops.relu_mask_epilogue sets it
+        assert a.K == 1 and not a.io16
+        yo = torch.relu(torch.randn(a.B, a.H, a.H, a.Co, device=dev))
+        y = torch.empty(a.B, a.H, a.H, a.Co, device=dev)
+        g = O._geom("hyres_geom_conv2d", a.B, a.H, a.H, a.Ci, a.Ci, a.Co, a.Co, 1, 1, 1, 0, 1)
+        e = L.Epilogue()
+        e.kind = L.EPI_BIAS
+        e.act = L.ACT_RELU_MASK
+        e.aux0, e.ld0 = yo.data_ptr(), a.Co
+        for _ in range(3):
+            O._launch_conv(g, x.ptr(), w.view(a.Co, a.Ci), a.Ci, y.data_ptr(), e)
+        torch.cuda.synchronize()
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(a.iters):
+            O._launch_conv(g, x.ptr(), w.view(a.Co, a.Ci), a.Ci, y.data_ptr(), e)
+        e1.record()
+        torch.cuda.synchronize()
+        us = 1000 * e0.elapsed_time(e1) / a.iters
+        byts = 4.0 * a.B * a.H * a.H * (a.Ci + 2 * a.Co)
+        print(f"conv B{a.B} {a.H}x{a.H}x{a.Ci} -> {a.H}x{a.H}x{a.Co} K1 +mask{' bf16x6' if a.bf6 else ''}: {us:.1f} us, "
+              f"{2.0 * a.B * a.H * a.H * a.Ci * a.Co / us / 1e6:.1f} TFLOP/s, {byts / us / 1e3:.0f} GB/s")
+        return
     ctx = torch.autocast("cuda", dtype=torch.float16) if a.f16 else torch.autocast("cuda", enabled=False)
     import contextlib
     with ctx, (O.f16_region() if a.io16 else contextlib.nullcontext()):
