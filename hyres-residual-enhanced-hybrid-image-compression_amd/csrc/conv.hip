@@ -1745,6 +1745,129 @@ __global__ __launch_bounds__(256, 2) void conv1x1_stream_h_kernel(const ConvArgs
 }
 
 // ------------------------------------------------------------------------------------------------
+// Streaming 1x1 conv with fp16 activations AND streamed epilogue operands (round 6, AMP training: the ResidualUnit /
+// RBB tails relu(W x + b + residual) and the input-gradients with the ReLU mask and the accumulated gradient; io_f16 =
+// 3, every operand fp16), K = Ci in {64, 128}, Co = 32 * NT in {64, 128}, F: residual (1) | ReLU mask (2) |
+// accumulate (4). conv1x1_stream_h_kernel's X stream and f16 products (C^T = W X^T: the tiled kernel's products, bit-
+// identical), with conv1x1_stream_b6_kernel's two fixes for the streamed operands: co tile t + 1's operands are in
+// flight while co tile t multiplies (two register sets), and every operand / store moves as pixel rows — the
+// accumulator goes through a per-wave LDS scratch (MFMA layout in, rows out: lane l -> pixel p0 + (l >> 3) + 8q,
+// channels 32t + 4 (l & 7) .. + 3), so an instruction covers 8 pixel rows x 64 contiguous bytes instead of the lane
+// layout's 32 rows x 8 B (profiles/r5h_access_probe.txt: the narrow pieces cap a read+write stream near 3 TB/s). The
+// round-5 version without the row-shaped epilogue measured 2-10 % slower than the tiles (profiles/r5g_stream_hf_ab.txt).
+// Arithmetic: fp16 operands, fp32 accumulation and epilogue ((acc + b) + residual, mask, + old y), one fp16 rounding
+// at the store — the tiled f16 kernel's (tests/test_stream_h_gpu.py: bit for bit).
+template <int NT, int KC, int F>
+__global__ __launch_bounds__(256, 2) void conv1x1_stream_hf_kernel(const ConvArgs a) {
+    constexpr int K = 16 * KC, KP = K + 8, CO = 32 * NT, EP = 36;
+    constexpr bool RES = (F & 1) != 0, MASK = (F & 2) != 0, ACC = (F & 4) != 0;
+    static_assert(NT % 2 == 0, "operands alternate between two register sets per co tile");
+    __shared__ __attribute__((aligned(16))) _Float16 Ws[CO * KP];
+    __shared__ __attribute__((aligned(16))) float bs[CO];
+    __shared__ __attribute__((aligned(16))) float Es[4 * 32 * EP];
+    const hyres_conv_geom& g = a.g;
+    const hyres_epilogue& e = a.e;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int lr = lane & 31, lh = lane >> 5;
+    for (int i = tid; i < CO * (K / 4); i += 256) {
+        const int co = i / (K / 4), k4 = i - co * (K / 4);
+        const float4 w = ld4(a.w2 + (long long)co * a.ldw + 4 * k4);
+        *reinterpret_cast<half4_t*>(&Ws[co * KP + 4 * k4]) = half4_t{(_Float16)w.x, (_Float16)w.y, (_Float16)w.z,
+                                                                     (_Float16)w.w};
+    }
+    for (int i = tid; i < CO; i += 256) bs[i] = e.bias ? e.bias[i] : 0.f;
+    __syncthreads();
+    const long long npix = a.M;
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, a.x_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t r_res = opnd_rsrc(RES ? e.res : nullptr, npix * e.ldres * 2);
+    const __amdgpu_buffer_rsrc_t r_mask = opnd_rsrc(MASK ? e.aux0 : nullptr, npix * e.ld0 * 2);
+    const __amdgpu_buffer_rsrc_t r_old = opnd_rsrc(ACC ? a.y : nullptr, npix * g.ldy * 2);
+    constexpr int OOR = (int)0x80000000;
+    _Float16* const y = reinterpret_cast<_Float16*>(a.y);
+    const int ntile = (a.M + 31) / 32;
+    const int gw = blockIdx.x * 4 + wave, nw = gridDim.x * 4;
+    auto load_x = [&](int tile, int j) -> half8s_t {
+        const int p = tile * 32 + lr;
+        const int off = (tile < ntile && p < a.M) ? (p * g.ldx + 16 * j + 8 * lh) * 2 : OOR;
+        return __builtin_bit_cast(half8s_t, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
+    };
+    const int cr = lane >> 3, cc = 4 * (lane & 7);
+    auto ooff = [&](int tile, int ld, int t, int q) -> int {
+        const int p = tile * 32 + cr + 8 * q;
+        return (tile < ntile && p < a.M) ? (p * ld + 32 * t + cc) * 2 : OOR;
+    };
+    half4_t eres[RES ? 2 : 1][4], emask[MASK ? 2 : 1][4], eold[ACC ? 2 : 1][4];
+    auto load_epi = [&](int tile, int t, int set) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if constexpr (RES) eres[set][q] = bload4h(r_res, ooff(tile, e.ldres, t, q));
+            if constexpr (MASK) emask[set][q] = bload4h(r_mask, ooff(tile, e.ld0, t, q));
+            if constexpr (ACC) eold[set][q] = bload4h(r_old, ooff(tile, g.ldy, t, q));
+        }
+    };
+    half8s_t xv[KC];
+#pragma unroll
+    for (int j = 0; j < KC; ++j) xv[j] = load_x(gw, j);
+    load_epi(gw, 0, 0);
+    float* const es = Es + wave * 32 * EP;
+    for (int tile = gw; tile < ntile; tile += nw) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const int cur = t & 1;
+            if (t + 1 < NT) load_epi(tile, t + 1, cur ^ 1);
+            else load_epi(tile + nw, 0, cur ^ 1);
+            floatx16 acc;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+            for (int j = 0; j < KC; ++j) {
+                const half8s_t w = *reinterpret_cast<const half8s_t*>(&Ws[(32 * t + lr) * KP + 16 * j + 8 * lh]);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(w, xv[j], acc, 0, 0, 0);
+                if (t == NT - 1) xv[j] = load_x(tile + nw, j);  // the next tile's X after its last use
+            }
+            // accumulator -> the wave's scratch in the MFMA layout -> back as pixel rows (LDS instructions of one wave
+            // run in order; the fences keep the compiler from moving the previous co tile's reads past these writes)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                *reinterpret_cast<float4*>(&es[lr * EP + 8 * q + 4 * lh]) =
+                    make_float4(acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int n = 32 * t + cc;
+                const float4 b4 = *reinterpret_cast<const float4*>(&bs[n]);
+                const float4 av = *reinterpret_cast<const float4*>(&es[(cr + 8 * q) * EP + cc]);
+                const int p = tile * 32 + cr + 8 * q;
+                float o[4] = {av.x + b4.x, av.y + b4.y, av.z + b4.z, av.w + b4.w};
+                if constexpr (RES) {
+                    const float4 r = h2f4(eres[cur][q]);
+                    o[0] += r.x; o[1] += r.y; o[2] += r.z; o[3] += r.w;
+                }
+                if constexpr (MASK) {
+                    const float4 m = h2f4(emask[cur][q]);
+                    o[0] = m.x > 0.f ? o[0] : 0.f;
+                    o[1] = m.y > 0.f ? o[1] : 0.f;
+                    o[2] = m.z > 0.f ? o[2] : 0.f;
+                    o[3] = m.w > 0.f ? o[3] : 0.f;
+                } else if (e.act == HYRES_ACT_RELU) {
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) o[c] = fmaxf(o[c], 0.f);
+                }
+                if constexpr (ACC) {
+                    const float4 v = h2f4(eold[cur][q]);
+                    o[0] += v.x; o[1] += v.y; o[2] += v.z; o[3] += v.w;
+                }
+                if (p < a.M)
+                    *reinterpret_cast<half4_t*>(y + (long long)p * g.ldy + n) =
+                        half4_t{(_Float16)o[0], (_Float16)o[1], (_Float16)o[2], (_Float16)o[3]};
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
 // Streaming 1x1 conv on the bf16 MFMA with fp32 accuracy (bf16x6, round 5): the fp32 ResidualUnit / RBB 1x1 layers and
 // their input-gradients, K = Ci in {64, 128}, Co = 32 * NT in {64, 128}, with the streamed epilogue operands the tiled
 // kernel fuses: residual (F & 1), ReLU mask (F & 2), accumulate into y (F & 4). These layers are HBM-bound (at bs 16,
@@ -2814,6 +2937,25 @@ static int stream_h_nt(const hyres_conv_geom* g, const hyres_epilogue* e) {
     return g->Co / 32;
 }
 
+// conv1x1_stream_hf_kernel eligibility (hyres_conv_tuning key 17 = 1, default): fp16 X and Y / operands (io_f16 = 3),
+// f16 operands, single-tap stride-1 1x1, (Ci, Co) in {64, 128}^2, >= 16384 output pixels, BIAS epilogue with none /
+// ReLU / ReLU mask and at least one streamed operand (residual, mask, old y; without one: conv1x1_stream_h_kernel),
+// no out2, 16-byte X rows / 8-byte Y rows. Returns NT | KC << 4 | F << 8, or 0.
+static int stream_hf_cfg(const hyres_conv_geom* g, const hyres_epilogue* e) {
+    if (g_tune[17] == 0 || (e->io_f16 & 3) != 3 || !e->f16_operands || e->square_input || e->kind != HYRES_EPI_BIAS ||
+        e->out2)
+        return 0;
+    if (e->act != HYRES_ACT_NONE && e->act != HYRES_ACT_RELU && e->act != HYRES_ACT_RELU_MASK) return 0;
+    if (g->nphase != 1 || g->ntaps != 1 || g->ish != 1 || g->isw != 1 || g->dh[0] != 0 || g->dw[0] != 0) return 0;
+    if (g->Hi != g->Hq || g->Wi != g->Wq || g->Ho != g->Hq || g->Wo != g->Wq) return 0;
+    if ((long long)g->B * g->Hq * g->Wq < 16384) return 0;
+    if ((g->Ci != 64 && g->Ci != 128) || (g->Co != 64 && g->Co != 128)) return 0;
+    if (g->ldx % 8 || g->ldy % 4 || (e->res && e->ldres % 4) || (e->act == HYRES_ACT_RELU_MASK && e->ld0 % 4)) return 0;
+    const int F = (e->res ? 1 : 0) | (e->act == HYRES_ACT_RELU_MASK ? 2 : 0) | (e->accumulate ? 4 : 0);
+    if (!F) return 0;
+    return (g->Co / 32) | ((g->Ci / 16) << 4) | (F << 8);
+}
+
 // conv1x1_stream_b6_kernel eligibility (bf16x6 fp32 GEMMs, hyres_conv_tuning key 10 = 1): fp32 X / Y, single-tap
 // stride-1 1x1 with (Ci, Co) in {(64, 64), (64, 128), (128, 64)}, BIAS epilogue with none / ReLU / PReLU / ReLU mask,
 // any of residual / mask / accumulate, grids >= 65536 output pixels. Returns the packed choice NT | KS << 4 | F << 8,
@@ -2888,6 +3030,44 @@ static int launch_stream_b6(const ConvArgs& a, int cfg, hipStream_t st) {
     if (nt == 4 && ks == 4) return launch_stream_b6_f<4, 4>(a, f, st);
     if (nt == 2 && ks == 8) return launch_stream_b6_f<2, 8>(a, f, st);
     return set_error(HYRES_E_ARG, "conv1x1_stream_b6: no instantiation for NT=%d KS=%d", nt, ks);
+}
+
+extern "C++" {
+template <int NT, int KC, int F>
+static int launch_stream_hf_one(const ConvArgs& a, hipStream_t st) {
+    static int occ = -1;
+    if (occ < 0) {
+        int n = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, conv1x1_stream_hf_kernel<NT, KC, F>, 256, 0) != hipSuccess ||
+            n < 1)
+            n = 1;
+        occ = n;
+    }
+    const int blocks = std::max(1, std::min(ceil_div(ceil_div(a.M, 32), 4), num_cus() * occ));
+    hipLaunchKernelGGL((conv1x1_stream_hf_kernel<NT, KC, F>), dim3(blocks), dim3(256), 0, st, a);
+    return HY_LAUNCH_CHECK("conv1x1_stream_hf_kernel");
+}
+template <int NT, int KC>
+static int launch_stream_hf_f(const ConvArgs& a, int f, hipStream_t st) {
+    switch (f) {
+        case 1: return launch_stream_hf_one<NT, KC, 1>(a, st);
+        case 2: return launch_stream_hf_one<NT, KC, 2>(a, st);
+        case 3: return launch_stream_hf_one<NT, KC, 3>(a, st);
+        case 4: return launch_stream_hf_one<NT, KC, 4>(a, st);
+        case 5: return launch_stream_hf_one<NT, KC, 5>(a, st);
+        case 6: return launch_stream_hf_one<NT, KC, 6>(a, st);
+        default: return launch_stream_hf_one<NT, KC, 7>(a, st);
+    }
+}
+}  // extern "C++"
+
+static int launch_stream_hf(const ConvArgs& a, int cfg, hipStream_t st) {
+    const int nt = cfg & 15, kc = (cfg >> 4) & 15, f = cfg >> 8;
+    if (nt == 2 && kc == 4) return launch_stream_hf_f<2, 4>(a, f, st);
+    if (nt == 2 && kc == 8) return launch_stream_hf_f<2, 8>(a, f, st);
+    if (nt == 4 && kc == 4) return launch_stream_hf_f<4, 4>(a, f, st);
+    if (nt == 4 && kc == 8) return launch_stream_hf_f<4, 8>(a, f, st);
+    return set_error(HYRES_E_ARG, "conv1x1_stream_hf: no instantiation for NT=%d KC=%d", nt, kc);
 }
 
 static int launch_stream_h(const ConvArgs& a, int nt, int kc, hipStream_t st) {
@@ -3101,6 +3281,17 @@ int hyres_conv_forward(const hyres_conv_geom* g, const float* x, const float* w2
         }
     }
     {
+        const int cfg = stream_hf_cfg(g, e);
+        const long long xb = (long long)a.M * g->ldx * 2;
+        if (cfg && mode == 0 && a.rsrc_ok && xb < 0x7FFFFFF0LL && aligned16(x) && aligned16(w2) && ldw % 4 == 0 &&
+            (reinterpret_cast<uintptr_t>(y) & 7) == 0 && (reinterpret_cast<uintptr_t>(e->res) & 7) == 0 &&
+            (reinterpret_cast<uintptr_t>(e->aux0) & 7) == 0) {
+            a.x_bytes = (int)xb;
+            a.nsplit = 1;
+            return launch_stream_hf(a, cfg, st);
+        }
+    }
+    {
         const int nt = stream_h_nt(g, e);
         const long long xb = (long long)a.M * g->ldx * 2;
         if (nt && mode == 0 && xb < 0x7FFFFFF0LL && aligned16(x) && aligned16(w2) && ldw % 4 == 0 &&
@@ -3161,6 +3352,11 @@ int hyres_conv_kernel_name(const hyres_conv_geom* g, const hyres_epilogue* e, in
         const int nt = stream_nt(g, e);
         if (nt && ch.mode == 0) {
             snprintf(buf, n, "conv1x1_stream_kernel<%d, %d%s>", nt, g->Ci / 8, e->f16_operands ? ", true" : "");
+            return 0;
+        }
+        const int chf = stream_hf_cfg(g, e);
+        if (chf && ch.mode == 0) {
+            snprintf(buf, n, "conv1x1_stream_hf_kernel<%d, %d, %d>", chf & 15, (chf >> 4) & 15, chf >> 8);
             return 0;
         }
         const int nth = stream_h_nt(g, e);

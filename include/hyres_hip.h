@@ -192,7 +192,9 @@ int hyres_conv_plan(const hyres_conv_geom* g, const hyres_epilogue* e, int* tile
 #define HYRES_TUNE_WGRAD_HALO_PF 16   /* bf16x6 3x3 halo weight gradients (one kernel row of 3 taps per block): 2
                                        * (default) = operand loads two chunks ahead (wgrad_halo_bf6_pf2_kernel), 1 = one
                                        * chunk ahead; the 5x5s stay on wgrad_halo_bf6_kernel (slower two ahead) */
-#define HYRES_TUNE_KEYS 20            /* keys 17..19 reserved */
+#define HYRES_TUNE_STREAM_HF 17       /* 1 (default): fp16-IO 1x1 convs (Ci, Co in {64, 128}, >= 16384 px) with a residual /
+                                       * ReLU-mask / accumulate operand on conv1x1_stream_hf_kernel; 0: the f16 tiles */
+#define HYRES_TUNE_KEYS 20            /* keys 18..19 reserved */
 int hyres_conv_tuning(int key, int value, int* old);
 
 /* Weight gradient:  dW[t][m][n] = sum_q P[q][m] * Q[shift_t(q)][n]  over a base grid q (B,Hq,Wq).

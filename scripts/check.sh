@@ -56,6 +56,7 @@ for ph in "$@"; do
     serial) scripts/gpu_run.sh "serial_fp32:300:rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${tag}_serial -o run -- python3 scripts/step_profile.py --marker --serial --steps 10" || exit $?
            python3 scripts/prof_summary.py gpurun_out/${tag}_serial/run_kernel_trace.csv 10 > gpurun_out/${tag}_train_serial_summary.txt ;;
     pmcfam) bash scripts/pmc_families.sh $tag || exit $? ;;
+    tuneab) bash scripts/tune_ab.sh $tag "default=" "nopf2=HYRES_TUNE=15=1,16=1" "nohf=HYRES_TUNE=17=0" "nofold=HYRES_FOLD_SA_MUL=0" || exit $? ;;
     repro) scripts/gpu_run.sh "repro_native_b6v:200:scripts/bf6_interference_repro 20 30 native-b6v" || exit $?
            cp gpurun_out/repro_native_b6v.log gpurun_out/${tag}_repro_native_b6v.txt ;;
     *) echo "unknown phase $ph"; exit 2 ;;

@@ -1,6 +1,7 @@
 """The fp16-activation streaming 1x1 conv (csrc/conv.hip conv1x1_stream_h_kernel: io_f16 = 3, Ci / Co in {64, 96, 128},
->= 16384 pixels, no streamed epilogue operand) and the tiled kernel the layers WITH one (residual, ReLU mask, old y)
-stay on. Against torch float64 on the same fp16 values (X fp16, W rounded to fp16, fp32 bias, fp16 residual / mask /
+>= 16384 pixels, no streamed epilogue operand) and, for the layers WITH one (residual, ReLU mask, old y),
+conv1x1_stream_hf_kernel (round 6: operands a co tile ahead, row-shaped epilogue through LDS), which must equal the
+f16 tiles it replaces bit for bit (hyres_conv_tuning key 17 = 0 routes them back). Against torch float64 on the same fp16 values (X fp16, W rounded to fp16, fp32 bias, fp16 residual / mask /
 old y), rounded to fp16 once at the end: within one fp16 ulp of the output plus fp32 summation-order slack (2e-3
 max-norm); strided X / Y and a ragged pixel count; the routing checked by name."""
 import ctypes
@@ -29,9 +30,12 @@ def _rand(shape, seed, scale=1.0):
     (16384, 128, 64, "none", False, False, 0),
     (4 * 64 * 64 + 17, 96, 96, "relu", False, False, 0),  # ragged last 32-pixel tile
     (16384, 128, 128, "none", False, False, 24),            # strided X / Y rows
-    (16384, 64, 128, "relu", True, False, 0),               # residual: tiled
-    (16384, 128, 64, "mask", False, True, 0),               # dgrad: ReLU mask + accumulate: tiled
-    (16384, 64, 128, "mask", True, True, 32),               # residual + mask + accumulate, strided: tiled
+    (16384, 64, 128, "relu", True, False, 0),               # residual
+    (16384, 128, 64, "mask", False, True, 0),               # dgrad: ReLU mask + accumulate
+    (16384, 64, 128, "mask", True, True, 32),               # residual + mask + accumulate, strided
+    (4 * 64 * 64 + 17, 128, 128, "relu", True, False, 0),    # residual, ragged last tile
+    (65536, 64, 64, "none", False, True, 0),                # accumulate only
+    (16384, 128, 128, "mask", False, False, 8),             # mask only, strided
 ])
 def test_stream_h_matches_torch(case):
     from hyres_hip import _lib as L
@@ -59,11 +63,22 @@ def test_stream_h_matches_torch(case):
     e.f16_operands = 1
     e.io_f16 = L.IO_X16 | L.IO_Y16
     streamed = res is not None or mask is not None or acc
-    want = "conv_fwd_h_kernel" if streamed else "conv1x1_stream_h_kernel"
+    want = "conv1x1_stream_hf_kernel" if streamed else "conv1x1_stream_h_kernel"
     assert O.conv_variant(g, e, False).startswith(want), O.conv_variant(g, e, False)
     L.call("hyres_conv_forward", ctypes.byref(g), x.data_ptr(), w.data_ptr(), Ci, y.data_ptr(), ctypes.byref(e),
            None, 0, L.stream())
     torch.cuda.synchronize()
+    if streamed:  # the f16 tiles it replaces: the same products and epilogue, bit for bit
+        yt = y0.clone()
+        L.call("hyres_conv_tuning", 17, 0, None)
+        try:
+            assert O.conv_variant(g, e, False).startswith("conv_fwd_h_kernel"), O.conv_variant(g, e, False)
+            L.call("hyres_conv_forward", ctypes.byref(g), x.data_ptr(), w.data_ptr(), Ci, yt.data_ptr(),
+                   ctypes.byref(e), None, 0, L.stream())
+            torch.cuda.synchronize()
+        finally:
+            L.call("hyres_conv_tuning", 17, 1, None)
+        assert torch.equal(y, yt), float((y.float() - yt.float()).abs().max())
     ref = x[:, :Ci].double() @ w.half().double().t() + b.double()
     if res is not None:
         ref = ref + res[:, :Co].double()
