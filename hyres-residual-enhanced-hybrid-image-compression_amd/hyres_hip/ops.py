@@ -635,7 +635,8 @@ def _launch_conv(g: L.ConvGeom, x_ptr: int, w2: torch.Tensor, ldw: int, y_ptr: i
         if KernelTimer.all_convs:
             desc = (f"B{g.B} {g.Hi}x{g.Wi}x{g.Ci}->{g.Ho}x{g.Wo}x{g.Co} taps{g.ntaps} ph{g.nphase} "
                     f"s{g.ish} epi{e.kind}{'+acc' if e.accumulate else ''}{'+res' if e.res else ''}"
-                    f"{' io%d' % e.io_f16 if e.io_f16 else ''}")
+                    f"{'+mask' if e.act == L.ACT_RELU_MASK else ''}{' io%d' % e.io_f16 if e.io_f16 else ''} "
+                    f"[{conv_variant(g, e, conv_split(g, e) > 1)}{'' if x_ptr % 16 == 0 else ', x not 16B-aligned'}]")
             KernelTimer.table.append((desc, s0, s1, conv_flops(g), conv_bytes(g, e)))
 
 
