@@ -1410,13 +1410,15 @@ __global__ __launch_bounds__(512, 1) void conv3x3_wres_bf6_kernel(const ConvArgs
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
     const hyres_epilogue& e = a.e;
-    const float slope = (e.act == HYRES_ACT_PRELU) ? e.slope[0] : 0.f;
+    const float slope = (e.act == HYRES_ACT_PRELU || e.act == HYRES_ACT_PRELU_MASK) ? e.slope[0] : 0.f;
     const long long npix = (long long)g.B * g.Ho * g.Wo;
     const __amdgpu_buffer_rsrc_t r_bias = opnd_rsrc(e.bias, (long long)g.Co * 4);
     const __amdgpu_buffer_rsrc_t r_res = opnd_rsrc(e.res, npix * e.ldres * 4);
-    const __amdgpu_buffer_rsrc_t r_mask = opnd_rsrc(e.act == HYRES_ACT_RELU_MASK ? e.aux0 : nullptr, npix * e.ld0 * 4);
+    const __amdgpu_buffer_rsrc_t r_mask = opnd_rsrc(
+        (e.act == HYRES_ACT_RELU_MASK || e.act == HYRES_ACT_PRELU_MASK) ? e.aux0 : nullptr, npix * e.ld0 * 4);
     const __amdgpu_buffer_rsrc_t r_old = opnd_rsrc(e.accumulate ? a.y : nullptr, npix * g.ldy * 4);
     float4 ebias[4], eres[4], emask[4], eold[4];
+    float pslope = 0.f;  // HYRES_ACT_PRELU_MASK: this thread's share of sum_{pre <= 0} pre * gradient
     const int steps = mytiles * 4;
     float4 hA[HV], hB[HV];
     if (steps > 0) {
@@ -1539,6 +1541,13 @@ __global__ __launch_bounds__(512, 1) void conv3x3_wres_bf6_kernel(const ConvArgs
                         o[1] = emask[qd].y > 0.f ? o[1] : 0.f;
                         o[2] = emask[qd].z > 0.f ? o[2] : 0.f;
                         o[3] = emask[qd].w > 0.f ? o[3] : 0.f;
+                    } else if (e.act == HYRES_ACT_PRELU_MASK) {  // as prelu_bwd4_kernel, per element
+                        const float pv[4] = {emask[qd].x, emask[qd].y, emask[qd].z, emask[qd].w};
+#pragma unroll
+                        for (int kk = 0; kk < 4; ++kk) {
+                            if (!(pv[kk] > 0.f)) pslope += pv[kk] * o[kk];
+                            o[kk] = pv[kk] > 0.f ? o[kk] : slope * o[kk];
+                        }
                     }
                     st4(a.y + pix * g.ldy + n,
                         make_float4(o[0] + eold[qd].x, o[1] + eold[qd].y, o[2] + eold[qd].z, o[3] + eold[qd].w));
@@ -1558,6 +1567,30 @@ __global__ __launch_bounds__(512, 1) void conv3x3_wres_bf6_kernel(const ConvArgs
         body(s, hA, hB);
         if (s + 1 < steps) body(s + 1, hB, hA);
     }
+    if (e.act == HYRES_ACT_PRELU_MASK) {  // block partial of the slope gradient (every body ended with a barrier)
+        float* red = reinterpret_cast<float*>(lds);
+        red[tid] = pslope;
+        __syncthreads();
+        for (int k = 256; k > 0; k >>= 1) {
+            if (tid < k) red[tid] += red[tid + k];
+            __syncthreads();
+        }
+        if (tid == 0) const_cast<float*>(e.aux2)[blockIdx.x] = red[0];
+    }
+}
+
+// HYRES_ACT_PRELU_MASK's second kernel: the block partials summed in a fixed order, added to the slope gradient
+__global__ __launch_bounds__(256) void prelu_slope_sum_kernel(const float* part, int n, float* dst) {
+    __shared__ float red[256];
+    float s = 0.f;
+    for (int i = threadIdx.x; i < n; i += 256) s += part[i];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int k = 128; k > 0; k >>= 1) {
+        if (threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) dst[0] += red[0];
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2869,7 +2902,11 @@ static int launch_wres32(const ConvArgs& a, hipStream_t st) {
             hipLaunchKernelGGL((conv3x3_wres_bf6_kernel<true, 3>), grid, dim3(512), 0, st, a, ntiles, groups);
         else
             hipLaunchKernelGGL((conv3x3_wres_bf6_kernel<true, 0>), grid, dim3(512), 0, st, a, ntiles, groups);
-        return HY_LAUNCH_CHECK("conv3x3_wres_bf6_kernel");
+        const int rc = HY_LAUNCH_CHECK("conv3x3_wres_bf6_kernel");
+        if (rc || a.e.act != HYRES_ACT_PRELU_MASK) return rc;
+        hipLaunchKernelGGL(prelu_slope_sum_kernel, dim3(1), dim3(256), 0, st, a.e.aux2, (int)grid.x,
+                           const_cast<float*>(a.e.aux1));
+        return HY_LAUNCH_CHECK("prelu_slope_sum_kernel");
     }
     hipLaunchKernelGGL(conv3x3_wres_f32_kernel, dim3(per * groups), dim3(512), 0, st, a, ntiles, groups);
     return HY_LAUNCH_CHECK("conv3x3_wres_f32_kernel");
@@ -3094,11 +3131,15 @@ static ConvChoice choose_conv(const hyres_conv_geom* g, const hyres_epilogue* e,
     const bool f16 = e->f16_operands && c.mode != 2;
     const bool short_k = c.mode != 2 && g->nphase == 1 && g->ntaps == 1 && g->Ci <= 4 * KT;
     const long long mtot = (long long)g->B * g->Hq * g->Wq * g->nphase;
-    if (short_k && g->Co > 64) c.tile = 3;
+    // fp32 small grids (round 6, profiles/r6g_tile32.txt, 32^2 bs16 bf16x6): the 1x1 96 -> 192 (+res) 14.9 -> 13.1 us on
+    // 64x64 tiles, 640 -> 512 102 -> 81 us on 128x128
+    // (hyres_conv_tuning key 18 = 0: the round-5 rule, A/B)
+    const bool r6 = g_tune[18] != 0;
+    if (short_k && g->Co > 64 && !(r6 && !f16 && mtot <= small_px && g->Co <= 192)) c.tile = 3;
     else if (short_k && g->Co > 32) c.tile = 4;
     else if (c.mode != 2 && g->Co > 32 && mtot <= small_px) {
         if (f16) c.tile = g->Co >= 192 ? 0 : 4;
-        else c.tile = g->Co > 192 ? 3 : 4;
+        else c.tile = (r6 && g->Co >= 512) ? 0 : g->Co > 192 ? 3 : 4;
     }
     else if (c.mode == 2 && g->Co > 32) c.tile = g->Co > 64 ? 3 : 4;  // scalar-load path: 64-row tiles
     else if (g->Co > 64) c.tile = 0;
@@ -3234,6 +3275,15 @@ int hyres_conv_forward(const hyres_conv_geom* g, const float* x, const float* w2
     }
     if (e->act == HYRES_ACT_RELU_MASK)
         HY_REQUIRE(e->aux0 && e->kind == HYRES_EPI_BIAS, HYRES_E_ARG, "conv: ReLU mask needs aux0, BIAS epilogue");
+    if (e->act == HYRES_ACT_PRELU_MASK) {
+        HY_REQUIRE(e->aux0 && e->aux1 && e->aux2 && e->slope && e->kind == HYRES_EPI_BIAS && !e->accumulate &&
+                       !e->out2 && e->io_f16 == 0 && !e->f16_operands && e->ld2 >= HYRES_PRELU_PARTIALS,
+                   HYRES_E_ARG, "conv: PReLU mask needs aux0 (pre-activation), aux1 (slope gradient), aux2 (>= %d "
+                   "partials), slope; BIAS, no accumulate / out2, fp32", HYRES_PRELU_PARTIALS);
+        HY_REQUIRE(mode == 0 && a.vec4 && wres32_ok(g, e) && wres_bf6() &&
+                       wres_blocks(g->Co / 32) * (g->Co / 32) <= HYRES_PRELU_PARTIALS,
+                   HYRES_E_ARG, "conv: the PReLU-mask epilogue runs on conv3x3_wres_bf6_kernel only");
+    }
     if (e->kind == HYRES_EPI_ROWSCALE)
         HY_REQUIRE(e->aux1 && !e->square_input && !e->accumulate, HYRES_E_ARG,
                    "conv: ROWSCALE needs aux1 (per-pixel scale), no square_input / accumulate");

@@ -19,7 +19,8 @@ LIB_PATH = os.environ.get("HYRES_LIB_PATH") or os.path.join(HERE, "libhyres_hip.
 MAX_TAPS = 49
 WPREP_CONV, WPREP_CONV_DGRAD, WPREP_DECONV, WPREP_DECONV_DGRAD = 0, 1, 2, 3
 EPI_BIAS, EPI_GDN, EPI_IGDN, EPI_GDN_BWD, EPI_IGDN_BWD, EPI_ROWSCALE, EPI_SA_BWD = 0, 1, 2, 3, 4, 5, 6
-ACT_NONE, ACT_RELU, ACT_PRELU, ACT_RELU_MASK = 0, 1, 2, 3
+ACT_NONE, ACT_RELU, ACT_PRELU, ACT_RELU_MASK, ACT_PRELU_MASK = 0, 1, 2, 3, 4
+PRELU_PARTIALS = 2048  # HYRES_PRELU_PARTIALS
 IO_X16, IO_Y16, IO_AUX16 = 1, 2, 4  # hyres_epilogue.io_f16 bits (fp16 activations in HBM)
 EB_REC = 64
 

@@ -72,7 +72,7 @@ class Node:
     """NHWC activation [B,H,W,C]; ``v`` may be a channel slice of a wider buffer (pixel stride ld)."""
 
     __slots__ = ("v", "B", "H", "W", "C", "ld", "rg", "parent", "c0", "_g", "gflag", "relu_out", "gmasked",
-                 "pending")
+                 "pending", "prelu", "pmasked")
 
     def __init__(self, v: torch.Tensor, rg: bool = True, parent: "Node" = None, c0: int = 0):
         assert v.dim() == 4 and v.stride(3) == 1, "Node expects an NHWC tensor with unit channel stride"
@@ -90,6 +90,11 @@ class Node:
         # whose input-gradient epilogue applied it as the FIRST contribution; cleared by any later one).
         self.relu_out = False
         self.gmasked = False
+        # PReLU-backward fusion: ``prelu`` = (pre-activation, slope) when v is the output of a PReLU fused into its
+        # producer (training); ``pmasked`` = the one gradient writer applied the PReLU backward in its epilogue
+        # (HYRES_ACT_PRELU_MASK) — unlike the ReLU mask it is not idempotent, so no second contribution may follow
+        self.prelu = None
+        self.pmasked = False
         # deferred residual gradient (tensor, pixel stride): added by the next input-gradient conv's
         # epilogue (``grad_target_epi``) instead of a separate add pass, or materialised on first access
         self.pending = None
@@ -187,6 +192,8 @@ class Node:
             self._g = _empty(self.v.shape, self.v.device, self.gdt)
         acc = 1 if self.gflag else 0
         if acc:
+            if self.pmasked:
+                raise RuntimeError("a second gradient contribution to a node whose PReLU backward was folded")
             self.gmasked = False  # a later, unmasked contribution: the producer re-applies the mask
         self.gflag = True
         return self._g, acc
@@ -199,7 +206,32 @@ class Node:
             e.ld0 = self.ld
             self.gmasked = True
 
+    def prelu_mask_epilogue(self, e: "L.Epilogue", acc: int, g: "L.ConvGeom") -> None:
+        """Let the input-gradient conv writing this node's gradient apply the PReLU backward (HYRES_ACT_PRELU_MASK,
+        include/hyres_hip.h): this node is a fused PReLU's output, the conv is its first writer, fp32, and the launcher
+        routes it to conv3x3_wres_bf6_kernel (MultiScaleRefine's scale blocks, enhancement.py:89-95: the dilation-2
+        conv's input-gradient). Replaces prelu_bwd of that PReLU; its slope gradient sum is added by the same call."""
+        if not (FOLD_PRELU and acc == 0 and self.prelu is not None and self.parent is None and not self.half
+                and e.act == L.ACT_NONE and e.kind == L.EPI_BIAS and not e.accumulate and not e.io_f16):
+            return
+        pre, slope = self.prelu
+        if pre.dtype != torch.float32 or not pre.is_contiguous():
+            return
+        e.act = L.ACT_PRELU_MASK
+        e.aux0, e.ld0 = pre.data_ptr(), self.C
+        if not conv_variant(g, e, False).startswith("conv3x3_wres_bf6_kernel"):
+            e.act, e.aux0, e.ld0 = L.ACT_NONE, None, 0
+            return
+        dslope = param_grad(slope) if slope.requires_grad else _empty((1,), self.device)
+        part = _empty((L.PRELU_PARTIALS,), self.device)
+        e.slope = slope.data_ptr()
+        e.aux1 = dslope.data_ptr()
+        e.aux2, e.ld2 = part.data_ptr(), L.PRELU_PARTIALS
+        self.pmasked = True
+
     def _zeroed_grad(self):
+        if self.pmasked:
+            raise RuntimeError("a second gradient contribution to a node whose PReLU backward was folded")
         if self.pending is not None:
             self._materialize()
         self.gmasked = False  # the caller accumulates an unmasked contribution
@@ -585,6 +617,9 @@ def f16_convs() -> bool:
 
 
 F16_ACT = os.environ.get("HYRES_F16_ACT", "1") == "1"
+# PReLU backward folded into the input-gradient conv that writes the PReLU output's gradient (Node.prelu_mask_epilogue);
+# HYRES_FOLD_PRELU=0: the separate prelu_bwd pass (A/B)
+FOLD_PRELU = os.environ.get("HYRES_FOLD_PRELU", "1") == "1"
 # AMP training stores the f16_region's activations (forward outputs saved for backward) as fp16 too, like
 # torch autocast, whose conv outputs are fp16 tensors (src/utils/engine.py:32); gradients stay fp32
 AMP_F16_ACT = os.environ.get("HYRES_AMP_F16_ACT", "1") == "1"
@@ -818,7 +853,7 @@ def _wgrad_launch(desc, p_ptr, q_ptr, dst, device, dbias, slot):
 def _act_backward(y: Node, gy: torch.Tensor, gy_ld: int, act: int, pre: Optional[torch.Tensor],
                   slope: Optional[torch.Tensor]):
     """Gradient wrt the pre-activation (contiguous [P,C] buffer or the incoming view)."""
-    if act == L.ACT_NONE or (act == L.ACT_RELU and y.gmasked):
+    if act == L.ACT_NONE or (act == L.ACT_RELU and y.gmasked) or (act == L.ACT_PRELU and y.pmasked):
         return gy, gy_ld
     gp = _empty((y.B, y.H, y.W, y.C), y.device, gy.dtype)
     g16 = int(gy.dtype == torch.float16)
@@ -903,6 +938,8 @@ def conv2d(tape: Optional[Tape], x: Node, weight: torch.Tensor, bias: Optional[t
     Trace.act(y, act, pre)
     if tape is None:
         return y
+    if pre is not None:
+        y.prelu = (pre, slope)
 
     def bwd():
         gy = y.grad()
@@ -937,6 +974,7 @@ def conv2d(tape: Optional[Tape], x: Node, weight: torch.Tensor, bias: Optional[t
             ed.f16_operands = f16
             ed.io_f16 = _dgrad_io(gp, x)
             x.relu_mask_epilogue(ed, acc)
+            x.prelu_mask_epilogue(ed, acc, gd)
             _launch_conv(gd, gp.data_ptr(), w2d, gd.ntaps * Co, tgt.data_ptr(), ed)
 
     tape.push(bwd)
@@ -994,6 +1032,7 @@ def deconv2d(tape: Optional[Tape], x: Node, weight: torch.Tensor, bias: Optional
             ed.f16_operands = f16
             ed.io_f16 = _dgrad_io(gp, x)
             x.relu_mask_epilogue(ed, acc)
+            x.prelu_mask_epilogue(ed, acc, gd)
             _launch_conv(gd, gp.data_ptr(), w2d, gd.ntaps * Co, tgt.data_ptr(), ed)
 
     tape.push(bwd)

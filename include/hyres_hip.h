@@ -109,6 +109,15 @@ int hyres_conv_weight_prep_batch(const void* descs, int n, long long total, hyre
 #define HYRES_ACT_PRELU 2     /* single shared slope (nn.PReLU()), read from device pointer */
 #define HYRES_ACT_RELU_MASK 3 /* ReLU backward fused into an input-gradient: y = (aux0 > 0) ? y : 0,
                                  aux0 = the ReLU output of the layer whose gradient is produced */
+#define HYRES_ACT_PRELU_MASK 4 /* PReLU backward fused into an input-gradient (round 6; the 3x3 Ci = Co = 64 layers on
+                                * conv3x3_wres_bf6_kernel only, HYRES_E_ARG elsewhere): y = (aux0 > 0) ? v : slope[0] * v,
+                                * aux0 = the saved pre-activation (fp32, pitch ld0), and the slope gradient
+                                * sum_{aux0 <= 0} aux0 * v is ADDED to ((float*)aux1)[0] — per-block partials in aux2
+                                * (capacity ld2 floats >= HYRES_PRELU_PARTIALS), summed in a fixed order by a second
+                                * kernel of the same call (deterministic). kind BIAS, accumulate 0, fp32 IO.
+                                * Replaces prelu_bwd of MultiScaleRefine's scale blocks (enhancement.py:44-51,
+                                * 89-95): the dilation-2 conv's input-gradient writes the PReLU'd gradient directly */
+#define HYRES_PRELU_PARTIALS 2048
 
 #define HYRES_IO_X16 1   /* hyres_epilogue.io_f16 bits */
 #define HYRES_IO_Y16 2
@@ -194,7 +203,10 @@ int hyres_conv_plan(const hyres_conv_geom* g, const hyres_epilogue* e, int* tile
                                        * chunk ahead; the 5x5s stay on wgrad_halo_bf6_kernel (slower two ahead) */
 #define HYRES_TUNE_STREAM_HF 17       /* 1 (default): fp16-IO 1x1 convs (Ci, Co in {64, 128}, >= 16384 px) with a residual /
                                        * ReLU-mask / accumulate operand on conv1x1_stream_hf_kernel; 0: the f16 tiles */
-#define HYRES_TUNE_KEYS 20            /* keys 18..19 reserved */
+#define HYRES_TUNE_SMALL_TILE 18      /* 1 (default): fp32 implicit-GEMM tiles on <= 65536-pixel grids by the round-6 rule
+                                       * (64x64 for the short-K 1x1s with Co <= 192, 128x128 for Co >= 512;
+                                       * profiles/r6g_tile32.txt); 0: the round-5 rule (A/B) */
+#define HYRES_TUNE_KEYS 20            /* key 19 reserved */
 int hyres_conv_tuning(int key, int value, int* old);
 
 /* Weight gradient:  dW[t][m][n] = sum_q P[q][m] * Q[shift_t(q)][n]  over a base grid q (B,Hq,Wq).

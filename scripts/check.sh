@@ -59,6 +59,12 @@ for ph in "$@"; do
     tuneab) bash scripts/tune_ab.sh $tag "default=" "nopf2=HYRES_TUNE=15=1,16=1" "nohf=HYRES_TUNE=17=0" "nofold=HYRES_FOLD_SA_MUL=0" || exit $? ;;
     repro) scripts/gpu_run.sh "repro_native_b6v:200:scripts/bf6_interference_repro 20 30 native-b6v" || exit $?
            cp gpurun_out/repro_native_b6v.log gpurun_out/${tag}_repro_native_b6v.txt ;;
+    split32) scripts/gpu_run.sh "split32:400:for T in '' 1=1024 1=2048 1=4096 1=2048,2=2; do for s in '--H 32 --Ci 96 --Co 96 --K 3 --relu' '--H 32 --Ci 192 --Co 96 --K 1 --relu' '--H 32 --Ci 96 --Co 192 --K 1 --res --relu' '--H 32 --Ci 384 --Co 192 --K 3 --relu' '--H 64 --Ci 64 --Co 128 --K 3 --relu'; do echo \"T=\$T\"; HYRES_TUNE=\$T python3 scripts/conv_micro.py \$s --bf6; done; done; for T in '' 3=1024 3=2048 3=2048,4=2; do for s in '--H 32 --Ci 96 --Co 96 --K 3' '--H 32 --Ci 96 --Co 192 --K 1' '--H 32 --Ci 192 --Co 96 --K 1'; do echo \"T=\$T\"; HYRES_TUNE=\$T python3 scripts/wgrad_micro.py \$s; done; done" || exit $?
+           grep -h "T=\|us" gpurun_out/split32.log > gpurun_out/${tag}_split32.txt ;;
+    tile32) scripts/gpu_run.sh "tile32:400:for t in -1 0 1 2 3 4; do for s in '--H 32 --Ci 96 --Co 96 --K 3 --relu' '--H 32 --Ci 192 --Co 96 --K 1 --relu' '--H 32 --Ci 96 --Co 192 --K 1 --res --relu' '--H 32 --Ci 384 --Co 192 --K 3 --relu' '--H 64 --Ci 64 --Co 128 --K 3 --relu' '--H 32 --Ci 640 --Co 512 --K 1'; do python3 scripts/conv_micro.py \$s --bf6 --tile \$t | sed \"s/^/tile \$t /\"; done; done" || exit $?
+           grep -h "us" gpurun_out/tile32.log > gpurun_out/${tag}_tile32.txt ;;
+    t6)    scripts/gpu_run.sh "t6:400:python -u -m pytest tests/test_parity_gpu.py -x -v --timeout 180 --timeout-method thread -m gpu -s -k 'prelu or refine or checkerboard_masked or captured'" || exit $? ;;
+    ab6)   bash scripts/tune_ab.sh $tag "default=" "noprelu=HYRES_FOLD_PRELU=0" "tile5=HYRES_TUNE=18=0" || exit $? ;;
     *) echo "unknown phase $ph"; exit 2 ;;
   esac
 done

@@ -414,6 +414,98 @@ def test_refine_branch_fwd_bwd(branch):
     assert not bad, errs
 
 
+@pytest.mark.parametrize("shape", [(2, 256, 128), (4, 128, 128)])
+def test_refine_block_prelu_fold_matches_unfused(shape, monkeypatch):
+    """A MultiScaleRefine scale block in training (enhancement.py:89-95) with its first PReLU's backward folded into the
+    dilation-2 conv's input-gradient (HYRES_ACT_PRELU_MASK on conv3x3_wres_bf6_kernel, ops.Node.prelu_mask_epilogue)
+    against the unfused prelu_bwd pass (HYRES_FOLD_PRELU=0) on the same inputs: d x, both conv weight / bias
+    gradients and the second PReLU's slope gradient bit for bit; the folded slope's gradient (the same products
+    summed in another order) at 1e-5. Sizes at the weight-resident kernel's tile floor (>= 2 tiles per block); the
+    fold must fire, and both PReLU sides are populated."""
+    from hyres_hip import _lib as L
+    from hyres_hip import ops as O
+    from hyres_hip.layers import Sequential, PReLU
+    from models.layers.enhancement import dilated_conv
+    D = dev()
+    B, H, W = shape
+    C = 64
+    torch.manual_seed(7)
+    blk = Sequential(dilated_conv(C, C, 1), PReLU(), dilated_conv(C, C, 2), PReLU()).to(D)
+    with torch.no_grad():
+        blk[0].bias.add_(0.02)
+    x = _rand((B, C, H, W), 51)
+    gy = _rand((B, C, H, W), 52)
+    fired = []
+    orig = O.Node.prelu_mask_epilogue
+
+    def spy(self, e, acc, g):
+        orig(self, e, acc, g)
+        fired.append(self.pmasked)
+
+    monkeypatch.setattr(O.Node, "prelu_mask_epilogue", spy)
+    old = ctypes.c_int(0)
+    L.call("hyres_conv_tuning", 7, 1, ctypes.byref(old))  # the bf16x6 GEMM (the default)
+
+    def run(fold):
+        monkeypatch.setattr(O, "FOLD_PRELU", fold)
+        for p in blk.parameters():
+            p.grad = None
+        fired.clear()
+        tape = O.Tape()
+        xn = O.to_nhwc(x.to(D), rg=True)
+        yn = blk.hip(tape, xn)
+        yn.set_grad(O.nchw_grad_to_nhwc(gy.to(D)))
+        tape.backward()
+        torch.cuda.synchronize()
+        return (O.to_nchw_grad(xn).cpu(), {k: p.grad.cpu().clone() for k, p in blk.named_parameters()},
+                any(fired))
+
+    try:
+        dx0, g0, f0 = run(False)
+        dx1, g1, f1 = run(True)
+    finally:
+        L.call("hyres_conv_tuning", 7, old.value, None)
+    assert f1 and not f0, (f0, f1)
+    pre = F.conv2d(x.to(D), blk[0].weight, blk[0].bias, padding=1)
+    neg = float((pre < 0).float().mean())
+    assert 0.05 < neg < 0.95, neg
+    assert torch.equal(dx0, dx1), float((dx0 - dx1).abs().max())
+    for k in g0:
+        if k == "1.weight":
+            assert rel_err(g1[k], g0[k]) < 1e-5, (k, g0[k], g1[k])
+        else:
+            assert torch.equal(g0[k], g1[k]), (k, float((g0[k] - g1[k]).abs().max()))
+
+
+def test_prelu_mask_epilogue_refused_off_the_weight_resident_kernel():
+    """HYRES_ACT_PRELU_MASK is implemented by conv3x3_wres_bf6_kernel only: a 1x1 input-gradient asking for it gets
+    HYRES_E_ARG, nothing launched (the caller, ops.Node.prelu_mask_epilogue, checks the route first)."""
+    from hyres_hip import _lib as L
+    from hyres_hip import ops as O
+    D = dev()
+    P, C = 4096, 64
+    x = torch.randn(P, C, device=D)
+    w = torch.randn(C, C, device=D)
+    y = torch.zeros(P, C, device=D)
+    pre = torch.randn(P, C, device=D)
+    slope = torch.full((1,), 0.25, device=D)
+    ds = torch.zeros(1, device=D)
+    part = torch.zeros(L.PRELU_PARTIALS, device=D)
+    g = O._geom("hyres_geom_conv2d", 1, 64, 64, C, C, C, C, 1, 1, 1, 0, 1)
+    e = L.Epilogue()
+    e.kind = L.EPI_BIAS
+    e.act = L.ACT_PRELU_MASK
+    e.aux0, e.ld0 = pre.data_ptr(), C
+    e.slope, e.aux1 = slope.data_ptr(), ds.data_ptr()
+    e.aux2, e.ld2 = part.data_ptr(), L.PRELU_PARTIALS
+    assert not O.conv_variant(g, e, False).startswith("conv3x3_wres_bf6_kernel")
+    with pytest.raises(L.HipError, match="conv3x3_wres_bf6_kernel only"):
+        L.call("hyres_conv_forward", ctypes.byref(g), x.data_ptr(), w.data_ptr(), C, y.data_ptr(), ctypes.byref(e),
+               None, 0, L.stream())
+    torch.cuda.synchronize()
+    assert float(y.abs().max()) == 0.0 and float(ds[0]) == 0.0
+
+
 # ------------------------------------------------------------------------------------------------ model
 def _hip_model():
     from models import ResidualJPEGCompression
