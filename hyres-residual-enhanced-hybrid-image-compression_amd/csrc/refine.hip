@@ -21,6 +21,7 @@ static inline int pw_grid(long long n4) {
 }
 
 constexpr int PW_UNR = 4;  // float4 per thread in flight in the pointwise kernels below
+constexpr int SE_PRELU_PARTS = 2048;  // hyres_se_bwd_prelu's slope partials (<= pw_grid's 2048 blocks)
 
 // torch area_pixel_compute_source_index (linear, align_corners=False): max(scale*(o+0.5)-0.5, 0)
 __device__ __forceinline__ void src_index(float scale, int o, int in, int& i0, int& i1, float& l0, float& l1) {
@@ -378,6 +379,65 @@ __global__ __launch_bounds__(256) void se_bwd_x4_kernel(const float* gy, const f
                                              v[u].w * gt.w + gp.w));
         }
     }
+}
+// the same with the producing PReLU's backward folded in (hyres_se_bwd_prelu, fp32): gx = PReLU'(pre) * (gy * gate + gpool)
+// and this block's share of the slope gradient sum_{pre <= 0} pre * (gy * gate + gpool) in part[blockIdx.x], elements
+// in the same order as prelu_bwd4_kernel's per-thread sums
+__global__ __launch_bounds__(256) void se_bwd_x4_prelu_kernel(const float* gy, const float* sgate, const float* gpool,
+                                                              float* gx, int B, int HW, int C, const float* pre,
+                                                              const float* slope, float* part) {
+    const int C4 = C >> 2, HWC4 = HW * C4;
+    const int n = B * HWC4;
+    const int stride = gridDim.x * 256;
+    const float a = slope[0];
+    float ps = 0.f;
+    for (int i0 = blockIdx.x * 256 + threadIdx.x; i0 < n; i0 += stride * PW_UNR) {
+        float4 v[PW_UNR], pv[PW_UNR];
+#pragma unroll
+        for (int u = 0; u < PW_UNR; ++u) {
+            const int i = i0 + u * stride;
+            if (i < n) {
+                v[u] = ld4(gy + 4LL * i);
+                pv[u] = ld4(pre + 4LL * i);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < PW_UNR; ++u) {
+            const int i = i0 + u * stride;
+            if (i >= n) continue;
+            const int b = i / HWC4;
+            const int c = 4 * (i - (i / C4) * C4);
+            const float4 gt = ld4(sgate + b * C + c), gp = ld4(gpool + b * C + c);
+            float o[4] = {v[u].x * gt.x + gp.x, v[u].y * gt.y + gp.y, v[u].z * gt.z + gp.z, v[u].w * gt.w + gp.w};
+            const float q[4] = {pv[u].x, pv[u].y, pv[u].z, pv[u].w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (!(q[k] > 0.f)) ps += q[k] * o[k];
+                o[k] = q[k] > 0.f ? o[k] : a * o[k];
+            }
+            *reinterpret_cast<float4*>(gx + 4LL * i) = make_float4(o[0], o[1], o[2], o[3]);
+        }
+    }
+    __shared__ float red[256];
+    red[threadIdx.x] = ps;
+    __syncthreads();
+    for (int k = 128; k > 0; k >>= 1) {
+        if (threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+__global__ __launch_bounds__(256) void se_prelu_slope_sum_kernel(const float* part, int n, float* dst) {
+    __shared__ float red[256];
+    float v = 0.f;
+    for (int i = threadIdx.x; i < n; i += 256) v += part[i];
+    red[threadIdx.x] = v;
+    __syncthreads();
+    for (int k = 128; k > 0; k >>= 1) {
+        if (threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) dst[0] += red[0];
 }
 template <bool G = false>
 __global__ void se_bwd_x_kernel(const float* gy, const float* sgate, const float* gpool, float* gx, int B, int HW,
@@ -802,10 +862,11 @@ extern "C++" {
 template <bool H, bool G>
 static int se_bwd_impl(const float* x, const float* gy, const float* w1, const float* w2, const float* pooled,
                        const float* hidden, const float* sgate, float* gx, float* gw1, float* gw2, int B, int HW, int C,
-                       int Cr, void* ws, long long ws_bytes, hyres_stream_t s) {
+                       int Cr, void* ws, long long ws_bytes, hyres_stream_t s, const float* pre = nullptr,
+                       const float* slope = nullptr, float* dslope = nullptr) {
     HY_REQUIRE(x && gy && w1 && w2 && pooled && hidden && sgate && gx && gw1 && gw2, HYRES_E_ARG, "se_bwd: NULL");
     const int nch = se_chunks(HW);
-    const long long need = (long long)B * nch * C * 4 + (long long)B * C * 4;
+    const long long need = (long long)B * nch * C * 4 + (long long)B * C * 4 + (pre ? SE_PRELU_PARTS * 4 : 0);
     HY_REQUIRE(ws && ws_bytes >= need, HYRES_E_WORKSPACE, "se_bwd: workspace");
     HY_REQUIRE((long long)B * (C + Cr) * 4 <= 60000, HYRES_E_SHAPE, "se_bwd: batch too large for LDS");
     const int per = (HW + nch - 1) / nch;
@@ -824,6 +885,16 @@ static int se_bwd_impl(const float* x, const float* gy, const float* w1, const f
     if (rc) return rc;
     long long n = (long long)B * HW * C;
     const unsigned am = G ? 7u : 15u;
+    if (pre) {  // the PReLU-folded form (fp32 only; checked by the entry point)
+        float* pp = gpool + (long long)B * C;
+        const int nb = std::min(pw_grid(n / 4), SE_PRELU_PARTS);
+        hipLaunchKernelGGL(se_bwd_x4_prelu_kernel, dim3(nb), dim3(256), 0, st, gy, sgate, (const float*)gpool, gx, B, HW,
+                           C, pre, slope, pp);
+        rc = HY_LAUNCH_CHECK("se_bwd_x4_prelu");
+        if (rc) return rc;
+        hipLaunchKernelGGL(se_prelu_slope_sum_kernel, dim3(1), dim3(256), 0, st, (const float*)pp, nb, dslope);
+        return HY_LAUNCH_CHECK("se_prelu_slope_sum");
+    }
     if (C % 4 == 0 && (reinterpret_cast<uintptr_t>(gy) & am) == 0 && (reinterpret_cast<uintptr_t>(gx) & am) == 0 &&
         n / 4 < (1LL << 31))
         hipLaunchKernelGGL(se_bwd_x4_kernel<G>, dim3(pw_grid(n / 4)), dim3(256), 0, st, gy, sgate, (const float*)gpool,
@@ -838,6 +909,16 @@ int hyres_se_bwd(const float* x, const float* gy, const float* w1, const float* 
                  const float* hidden, const float* sgate, float* gx, float* gw1, float* gw2, int B, int HW, int C,
                  int Cr, void* ws, long long ws_bytes, hyres_stream_t s) {
     return se_bwd_impl<false, false>(x, gy, w1, w2, pooled, hidden, sgate, gx, gw1, gw2, B, HW, C, Cr, ws, ws_bytes, s);
+}
+int hyres_se_bwd_prelu(const float* x, const float* gy, const float* w1, const float* w2, const float* pooled,
+                       const float* hidden, const float* sgate, float* gx, float* gw1, float* gw2, int B, int HW, int C,
+                       int Cr, const float* pre, const float* slope, float* dslope, void* ws, long long ws_bytes,
+                       hyres_stream_t s) {
+    HY_REQUIRE(pre && slope && dslope && C % 4 == 0 && aligned16(gy) && aligned16(gx) && aligned16(pre) &&
+                   (long long)B * HW * C / 4 < (1LL << 31),
+               HYRES_E_ARG, "se_bwd_prelu: needs pre / slope / dslope, C %% 4 == 0, 16B-aligned gy / gx / pre");
+    return se_bwd_impl<false, false>(x, gy, w1, w2, pooled, hidden, sgate, gx, gw1, gw2, B, HW, C, Cr, ws, ws_bytes, s,
+                                     pre, slope, dslope);
 }
 int hyres_se_bwd_f16(const void* x, const void* gy, const float* w1, const float* w2, const float* pooled,
                      const float* hidden, const float* sgate, void* gx, float* gw1, float* gw2, int B, int HW, int C,

@@ -424,6 +424,14 @@ int hyres_se_fwd(const float* x, const float* w1, const float* w2, float* y, flo
 int hyres_se_bwd(const float* x, const float* gy, const float* w1, const float* w2,
                  const float* pooled, const float* hidden, const float* sgate, float* gx, float* gw1,
                  float* gw2, int B, int HW, int C, int Cr, void* ws, long long ws_bytes, hyres_stream_t s);
+/* hyres_se_bwd with the backward of the PReLU that produced x folded in (round 6; MultiScaleRefine's
+ * SE(PReLU(conv_in(x))), enhancement.py:107-110): gx = PReLU'(pre) * dL/dx, the slope gradient
+ * sum_{pre <= 0} pre * dL/dx ADDED to dslope[0] (block partials in the workspace, fixed-order sum). fp32; the
+ * workspace is hyres_se_workspace_bytes + B*C*4 + 2048*4 bytes. Replaces prelu_bwd after the SE backward. */
+int hyres_se_bwd_prelu(const float* x, const float* gy, const float* w1, const float* w2, const float* pooled,
+                       const float* hidden, const float* sgate, float* gx, float* gw1, float* gw2, int B, int HW, int C,
+                       int Cr, const float* pre, const float* slope, float* dslope, void* ws, long long ws_bytes,
+                       hyres_stream_t s);
 long long hyres_se_workspace_bytes(int B, int HW, int C);
 /* SpatialAttention (enhancement.py:7-21) fused: a = sigmoid(conv7x7([mean_c, max_c])); y = x * a.
  * pooled2 [P][2] and argmax [P] (first maximal channel, torch.max semantics) are saved for backward.

@@ -65,6 +65,10 @@ for ph in "$@"; do
            grep -h "us" gpurun_out/tile32.log > gpurun_out/${tag}_tile32.txt ;;
     t6)    scripts/gpu_run.sh "t6:400:python -u -m pytest tests/test_parity_gpu.py -x -v --timeout 180 --timeout-method thread -m gpu -s -k 'prelu or refine or checkerboard_masked or captured'" || exit $? ;;
     ab6)   bash scripts/tune_ab.sh $tag "default=" "noprelu=HYRES_FOLD_PRELU=0" "tile5=HYRES_TUNE=18=0" || exit $? ;;
+    serialab) scripts/gpu_run.sh "serial_fold1:300:rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${tag}_serial_f1 -o run -- python3 scripts/step_profile.py --marker --serial --steps 10" \
+                "serial_fold0:300:HYRES_FOLD_PRELU=0 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${tag}_serial_f0 -o run -- python3 scripts/step_profile.py --marker --serial --steps 10" || exit $?
+           python3 scripts/prof_summary.py gpurun_out/${tag}_serial_f1/run_kernel_trace.csv 10 > gpurun_out/${tag}_serial_fold1.txt
+           python3 scripts/prof_summary.py gpurun_out/${tag}_serial_f0/run_kernel_trace.csv 10 > gpurun_out/${tag}_serial_fold0.txt ;;
     *) echo "unknown phase $ph"; exit 2 ;;
   esac
 done

@@ -477,6 +477,72 @@ def test_refine_block_prelu_fold_matches_unfused(shape, monkeypatch):
             assert torch.equal(g0[k], g1[k]), (k, float((g0[k] - g1[k]).abs().max()))
 
 
+def test_refine_input_se_prelu_fold_matches_unfused(monkeypatch):
+    """MultiScaleRefine's input stage in training, SE(PReLU(conv_in(x))) (enhancement.py:107-110), with act_in's
+    backward folded into the SE block's input-gradient (hyres_se_bwd_prelu) against the unfused prelu_bwd pass
+    (HYRES_FOLD_PRELU=0): d x, conv_in's weight / bias and both SE weights bit for bit; act_in's slope gradient (same
+    products, another summation order) at 1e-5; the fold fires; both PReLU sides populated. Against fp64 torch too."""
+    import models.layers.enhancement as EH
+    from hyres_hip import _lib as L
+    from hyres_hip import ops as O
+    from hyres_hip import refine_ops as R
+    D = dev()
+    B, H, W = 2, 64, 96
+    torch.manual_seed(9)
+    m = EH.MultiScaleRefine(3, 64).to(D)
+    x = _rand((B, 3, H, W), 61)
+    gy = _rand((B, 64, H, W), 62)
+    calls = []
+    orig_call = L.call
+
+    def spy(name, *args):
+        calls.append(name)
+        return orig_call(name, *args)
+
+    monkeypatch.setattr(L, "call", spy)
+
+    def run(fold):
+        monkeypatch.setattr(O, "FOLD_PRELU", fold)
+        for p in m.parameters():
+            p.grad = None
+        calls.clear()
+        tape = O.Tape()
+        xn = O.to_nhwc(x.to(D), rg=True)
+        feat = m.conv_in.hip(tape, xn, act=L.ACT_PRELU, slope=m.act_in.weight)
+        yn = m.se_block.hip(tape, feat)
+        yn.set_grad(O.nchw_grad_to_nhwc(gy.to(D)))
+        tape.backward()
+        torch.cuda.synchronize()
+        names = ("conv_in.weight", "conv_in.bias", "act_in.weight", "se_block.fc.0.weight", "se_block.fc.2.weight")
+        grads = {k: p.grad.cpu().clone() for k, p in m.named_parameters() if k in names}
+        return O.to_nchw_grad(xn).cpu(), grads, O.to_nchw(yn).cpu(), list(calls)
+
+    dx0, g0, y0, c0 = run(False)
+    dx1, g1, y1, c1 = run(True)
+    assert "hyres_se_bwd_prelu" in c1 and "hyres_prelu_bwd" not in c1, c1
+    assert "hyres_prelu_bwd" in c0 and "hyres_se_bwd_prelu" not in c0, c0
+    assert torch.equal(y0, y1) and torch.equal(dx0, dx1), float((dx0 - dx1).abs().max())
+    for k in g0:
+        if k == "act_in.weight":
+            assert rel_err(g1[k], g0[k]) < 1e-5, (g0[k], g1[k])
+        else:
+            assert torch.equal(g0[k], g1[k]), (k, float((g0[k] - g1[k]).abs().max()))
+    # fp64 torch reference of the same stage
+    sd = {k: v.detach().cpu().double().clone().requires_grad_(True) for k, v in m.state_dict().items()
+          if k.startswith(("conv_in", "act_in", "se_block"))}
+    xr = x.double().requires_grad_(True)
+    pre = F.conv2d(xr, sd["conv_in.weight"], sd["conv_in.bias"], padding=1)
+    neg = float((pre < 0).double().mean())
+    assert 0.05 < neg < 0.95, neg
+    f = F.prelu(pre, sd["act_in.weight"])
+    s = torch.sigmoid(F.linear(F.relu(F.linear(f.mean((2, 3)), sd["se_block.fc.0.weight"])),
+                               sd["se_block.fc.2.weight"]))
+    (f * s[:, :, None, None]).backward(gy.double())
+    assert rel_err(dx1, xr.grad) < TOL
+    for k in g1:
+        assert rel_err(g1[k], sd[k].grad) < (1e-3 if k == "act_in.weight" else TOL), k
+
+
 def test_prelu_mask_epilogue_refused_off_the_weight_resident_kernel():
     """HYRES_ACT_PRELU_MASK is implemented by conv3x3_wres_bf6_kernel only: a 1x1 input-gradient asking for it gets
     HYRES_E_ARG, nothing launched (the caller, ops.Node.prelu_mask_epilogue, checks the route first)."""
