@@ -549,11 +549,11 @@ def analysis_synthesis(net, x, reps):
            "tflops": round(B * 40.66e9 / (ms * 1e-3) / 1e12, 2),
            "mfma_fp32_frac": round(B * 40.66e9 / (ms * 1e-3) / 1e12 / MI355X_FP32_PEAK_TFLOPS, 4),
            "target": "north_star: >= 0.40 of the HBM roofline, i.e. <= 9.2 ms at bs=16"}
-    # the SAME pass's HBM bytes measured with PMC counters (scripts/as_traffic.py, profiles/r3_as_traffic.json):
+    # the SAME pass's HBM bytes measured with PMC counters (scripts/as_traffic.py, profiles/r6k_as_traffic.json: round 6 build, scripts/check.sh phase "as"):
     # the fused kernels move far fewer bytes than the eager per-op ledger, so the honest HBM fraction is lower —
     # this pass is MFMA-bound (mfma_fp32_frac), not HBM-bound
     try:
-        with open(os.path.join(REPO, "profiles", "r3_as_traffic.json")) as f:
+        with open(os.path.join(REPO, "profiles", "r6k_as_traffic.json")) as f:
             pmc = json.load(f)
         if pmc.get("ledger_bytes_per_pass") == ledger:
             res["pmc_bytes"] = pmc["bytes_per_pass"]

@@ -35,6 +35,8 @@ struct ConvArgs {
     int prio;    // 1: raise the wave priority while it issues its MFMA cluster (s_setprio)
     int x_bytes; // conv1x1_stream_kernel: bytes of X (buffer-resource range)
     int rsrc_ok; // every epilogue operand / output spans < 2 GB: the epilogues may address them by buffer resources
+    int b6sw;    // bf16x6 implicit GEMM: 64-B LDS rows with the 16-B slot XOR-swizzled by row bits 2..3 (round 6,
+                 // hyres_conv_tuning key 19, default 1) instead of 80-B padded rows
 };
 
 // Buffer resource of an epilogue operand: an absent operand (p == NULL) gets an empty resource, so its loads return
@@ -250,8 +252,14 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
     float* const Bs = smem + BM * PADK;
     _Float16* const Ah = reinterpret_cast<_Float16*>(smem);
     _Float16* const Bh = Ah + BM * PADH;
-    __bf16* const Pb = reinterpret_cast<__bf16*>(smem);  // B6: plane p = Pb + p * (BM + BN) * PADH, A rows then B
-    constexpr int PLANE = (BM + BN) * PADH;
+    __bf16* const Pb = reinterpret_cast<__bf16*>(smem);  // B6: plane p = Pb + p * PLANE, A rows then B
+    // B6 row layout (round 6): b6sw = 1 (default) 32-half rows, 16-B slot s of row r stored at slot s ^ ((r >> 2) & 3):
+    // the split stores (ds_write_b64, 16-lane groups = two consecutive rows, banks mod 32) then fill complementary
+    // halves of the 32 banks, and every ds_read_b128 lane group (16 rows, banks mod 64) meets 16 distinct slots.
+    // b6sw = 0: the 40-half padded rows (reads conflict-free, the stores 2-way: SQ_LDS_BANK_CONFLICT 0.33 of the LDS
+    // cycles at 32^2, profiles/r6f_pmc_families.txt). Same products in the same order either way.
+    const int b6p = (B6 && a.b6sw) ? 32 : PADH;
+    const int PLANE = (BM + BN) * b6p;
 
     const hyres_conv_geom& g = a.g;
     const int tid = threadIdx.x;
@@ -384,11 +392,12 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
     };
     auto store_chunk = [&]() {
         if constexpr (B6) {
+            const int sx = a.b6sw ? (((c4 >> 1) ^ ((tid >> 5) & 3)) << 3) + 4 * (c4 & 1) : 4 * c4;  // row bits 2..3 = tid bits 5..6
 #pragma unroll
             for (int q = 0; q < A_V; ++q) {
                 bf16x4_t h, m, l;
                 bf6_split4(ra[q], h, m, l);
-                const int o = (tid / 8 + 32 * q) * PADH + 4 * c4;
+                const int o = (tid / 8 + 32 * q) * b6p + sx;
                 *reinterpret_cast<bf16x4_t*>(&Pb[o]) = h;
                 *reinterpret_cast<bf16x4_t*>(&Pb[PLANE + o]) = m;
                 *reinterpret_cast<bf16x4_t*>(&Pb[2 * PLANE + o]) = l;
@@ -397,7 +406,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
             for (int q = 0; q < B_V; ++q) {
                 bf16x4_t h, m, l;
                 bf6_split4(rb[q], h, m, l);
-                const int o = (BM + tid / 8 + 32 * q) * PADH + 4 * c4;
+                const int o = (BM + tid / 8 + 32 * q) * b6p + sx;
                 *reinterpret_cast<bf16x4_t*>(&Pb[o]) = h;
                 *reinterpret_cast<bf16x4_t*>(&Pb[PLANE + o]) = m;
                 *reinterpret_cast<bf16x4_t*>(&Pb[2 * PLANE + o]) = l;
@@ -472,19 +481,21 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
         if (kc + 1 < kend) load_chunk(kc + 1);
         if constexpr (B6) {
             if (a.prio) __builtin_amdgcn_s_setprio(1);
+            const int rx = a.b6sw ? (lr >> 2) & 3 : 0;  // the row's slot swizzle (tile bases are multiples of 32 rows)
 #pragma unroll
             for (int s16 = 0; s16 < 2; ++s16) {
                 bf16x8_t af[TM][3], bf[TN][3];
+                const int ko = ((2 * s16 + lh) ^ rx) << 3;
 #pragma unroll
                 for (int p = 0; p < 3; ++p) {
 #pragma unroll
                     for (int tm = 0; tm < TM; ++tm)
                         af[tm][p] = *reinterpret_cast<const bf16x8_t*>(
-                            &Pb[p * PLANE + (wm * TM * 32 + tm * 32 + lr) * PADH + 16 * s16 + 8 * lh]);
+                            &Pb[p * PLANE + (wm * TM * 32 + tm * 32 + lr) * b6p + ko]);
 #pragma unroll
                     for (int tn = 0; tn < TN; ++tn)
                         bf[tn][p] = *reinterpret_cast<const bf16x8_t*>(
-                            &Pb[p * PLANE + (BM + wn * TN * 32 + tn * 32 + lr) * PADH + 16 * s16 + 8 * lh]);
+                            &Pb[p * PLANE + (BM + wn * TN * 32 + tn * 32 + lr) * b6p + ko]);
                 }
 #pragma unroll
                 for (int tm = 0; tm < TM; ++tm)
@@ -2649,7 +2660,7 @@ static void dense_taps(hyres_conv_geom* g, int KH, int KW, int sgn, int dil, int
 // key 7: fp32 GEMMs bf16x6 (0: native fp32 MFMA); key 8: fp16 streaming 1x1; key 9: the bf16x6 weight-resident 3x3's
 // whole-VGPR-file guard (0 = diagnostic unguarded build, DESIGN §4 "Cross-kernel interference"); key 10: the bf16x6
 // streaming 1x1 kernel (0 = those layers on the tiled implicit GEMM, for A/B)
-int g_tune[HYRES_TUNE_KEYS] = {-1, -1, -1, -1, -1, -1, -1, 1, 1, 1, 1, 1, 1, 1, 1, 2, 2, 1, 1, 1};
+int g_tune[HYRES_TUNE_KEYS] = {-1, -1, -1, -1, -1, -1, -1, 1, 1, 1, 1, 1, 1, 1, 1, 2, 2, 1, 1, 1};  // key 19: b6sw
 
 }  // namespace hyres
 
@@ -3218,6 +3229,7 @@ int hyres_conv_forward(const hyres_conv_geom* g, const float* x, const float* w2
     a.M = g->B * g->Hq * g->Wq;
     a.xcd = 1;
     a.prio = 1;
+    a.b6sw = g_tune[19] != 0;
     const ConvChoice ch = choose_conv(g, e, aligned16(x) && aligned16(w2) && g->ldx % 4 == 0 && ldw % 4 == 0);
     ConvPlan plan = conv_plan(g, ch.tile);
     a.nsplit = 1;

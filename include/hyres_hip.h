@@ -206,7 +206,10 @@ int hyres_conv_plan(const hyres_conv_geom* g, const hyres_epilogue* e, int* tile
 #define HYRES_TUNE_SMALL_TILE 18      /* 1 (default): fp32 implicit-GEMM tiles on <= 65536-pixel grids by the round-6 rule
                                        * (64x64 for the short-K 1x1s with Co <= 192, 128x128 for Co >= 512;
                                        * profiles/r6g_tile32.txt); 0: the round-5 rule (A/B) */
-#define HYRES_TUNE_KEYS 20            /* key 19 reserved */
+#define HYRES_TUNE_B6_SWIZZLE 19      /* 1 (default): the bf16x6 implicit GEMM stages its split planes in 64-B LDS rows with the
+                                       * 16-B slots XOR-swizzled by row (conflict-free stores and reads); 0: 80-B padded rows
+                                       * (2-way store conflicts), A/B; bit-identical */
+#define HYRES_TUNE_KEYS 20
 int hyres_conv_tuning(int key, int value, int* old);
 
 /* Weight gradient:  dW[t][m][n] = sum_q P[q][m] * Q[shift_t(q)][n]  over a base grid q (B,Hq,Wq).

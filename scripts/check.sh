@@ -69,6 +69,12 @@ for ph in "$@"; do
                 "serial_fold0:300:HYRES_FOLD_PRELU=0 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${tag}_serial_f0 -o run -- python3 scripts/step_profile.py --marker --serial --steps 10" || exit $?
            python3 scripts/prof_summary.py gpurun_out/${tag}_serial_f1/run_kernel_trace.csv 10 > gpurun_out/${tag}_serial_fold1.txt
            python3 scripts/prof_summary.py gpurun_out/${tag}_serial_f0/run_kernel_trace.csv 10 > gpurun_out/${tag}_serial_fold0.txt ;;
+    as)    scripts/gpu_run.sh \
+             "as_fetch:300:rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/${tag}_as_f -o run -- python3 scripts/as_traffic.py" \
+             "as_write:300:rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/${tag}_as_w -o run -- python3 scripts/as_traffic.py" || exit $?
+           python3 scripts/as_traffic.py --summarize gpurun_out/${tag}_as_f gpurun_out/${tag}_as_w --out gpurun_out/${tag}_as_traffic.json ;;
+    b6sw)  scripts/gpu_run.sh "b6sw:400:for t in 1 0 1 0; do for s in '--H 32 --Ci 96 --Co 96 --K 3 --relu' '--H 32 --Ci 192 --Co 96 --K 1 --relu' '--H 32 --Ci 384 --Co 192 --K 3 --relu' '--H 64 --Ci 64 --Co 128 --K 3 --relu' '--H 32 --Ci 640 --Co 512 --K 1' '--H 128 --Ci 128 --Co 128 --K 5 --stride 2'; do HYRES_TUNE=19=\$t python3 scripts/conv_micro.py \$s --bf6 | sed \"s/^/b6sw=\$t /\"; done; done" || exit $?
+           grep -h "us" gpurun_out/b6sw.log > gpurun_out/${tag}_b6sw.txt ;;
     *) echo "unknown phase $ph"; exit 2 ;;
   esac
 done
