@@ -151,7 +151,7 @@ FP32_GEMM_NOTE = {
 def kernel_peak(kernel):
     """The peak a kernel's fp32 flops are priced against: the bf16x6 ceiling for the bf16x6 kernels, else the dense
     fp32 MFMA peak."""
-    return BF6_PEAK_TFLOPS if ("bf6" in kernel or "b6_kernel" in kernel) else MI355X_FP32_PEAK_TFLOPS
+    return BF6_PEAK_TFLOPS if ("bf6" in kernel or "b6_kernel" in kernel or "b6db_kernel" in kernel) else MI355X_FP32_PEAK_TFLOPS
 
 
 def peak_note(kernel):

@@ -228,7 +228,8 @@ __device__ __forceinline__ void epi_store4(const hyres_epilogue& e, float* y, in
 
 // bf16x8_t / bf16x4_t, bf6_split4, bf6_mfma: conv_common.h (shared with the bf16x6 weight gradients)
 
-template <int TM, int TN, int WAVES_M, int WAVES_N, int MODE, bool SPLITK, bool F16, int IO, bool B6 = false>
+template <int TM, int TN, int WAVES_M, int WAVES_N, int MODE, bool SPLITK, bool F16, int IO, bool B6 = false,
+          bool DB = false>
 __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
     // MODE 0: Ci % 32 == 0 (float4 loads); 1: same + square A (GDN); 2: generic scalar (small Ci).
     // F16: operands rounded to fp16 when staged into LDS ([row][32 halves], pitch PADH halves) and
@@ -240,25 +241,28 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
     static_assert(!F16 || MODE != 2, "fp16 operands on the Ci % 32 == 0 paths only");
     static_assert(!B6 || (!F16 && IO == 0 && MODE != 2), "bf16x6: fp32 operands on the vector path");
     static_assert(!(IO & 1) || MODE != 2, "fp16 X on the Ci % 32 == 0 paths only");
+    // DB (round 6, bf16x6 only): two LDS buffers of swizzled 64-B rows, one barrier per K chunk — chunk k + 1 is split
+    // and stored into the other buffer right after chunk k's MFMAs, while other waves may still read chunk k
+    static_assert(!DB || B6, "double-buffered staging: the bf16x6 path");
     constexpr bool XH = (IO & 1) != 0, YH = (IO & 2) != 0;
     constexpr int XES = XH ? 2 : 4;  // X element bytes
     constexpr int PADH = 40;
     constexpr int BM = 32 * TM * WAVES_M;
     constexpr int BN = 32 * TN * WAVES_N;
-    constexpr int SOP = B6 ? 3 * (BM + BN) * PADH / 2 : (BM + BN) * PADK;  // operand staging (floats)
+    constexpr int SOP = DB ? 2 * 3 * (BM + BN) * 32 / 2 : B6 ? 3 * (BM + BN) * PADH / 2 : (BM + BN) * PADK;  // staging (floats)
     constexpr int SMEM = (SOP > BM * (32 * WAVES_N + 8)) ? SOP : BM * (32 * WAVES_N + 8);
     __shared__ __attribute__((aligned(16))) float smem[SMEM];
     float* const As = smem;
     float* const Bs = smem + BM * PADK;
     _Float16* const Ah = reinterpret_cast<_Float16*>(smem);
     _Float16* const Bh = Ah + BM * PADH;
-    __bf16* const Pb = reinterpret_cast<__bf16*>(smem);  // B6: plane p = Pb + p * PLANE, A rows then B
+    __bf16* const Pb0 = reinterpret_cast<__bf16*>(smem);  // B6: plane p = Pb0 + p * PLANE, A rows then B (DB: + buffer)
     // B6 row layout (round 6): b6sw = 1 (default) 32-half rows, 16-B slot s of row r stored at slot s ^ ((r >> 2) & 3):
     // the split stores (ds_write_b64, 16-lane groups = two consecutive rows, banks mod 32) then fill complementary
     // halves of the 32 banks, and every ds_read_b128 lane group (16 rows, banks mod 64) meets 16 distinct slots.
     // b6sw = 0: the 40-half padded rows (reads conflict-free, the stores 2-way: SQ_LDS_BANK_CONFLICT 0.33 of the LDS
     // cycles at 32^2, profiles/r6f_pmc_families.txt). Same products in the same order either way.
-    const int b6p = (B6 && a.b6sw) ? 32 : PADH;
+    const int b6p = (DB || (B6 && a.b6sw)) ? 32 : PADH;
     const int PLANE = (BM + BN) * b6p;
 
     const hyres_conv_geom& g = a.g;
@@ -390,9 +394,10 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
             }
         }
     };
-    auto store_chunk = [&]() {
+    auto store_chunk = [&](int buf = 0) {
         if constexpr (B6) {
-            const int sx = a.b6sw ? (((c4 >> 1) ^ ((tid >> 5) & 3)) << 3) + 4 * (c4 & 1) : 4 * c4;  // row bits 2..3 = tid bits 5..6
+            __bf16* const Pb = Pb0 + buf * 3 * PLANE;
+            const int sx = b6p == 32 ? (((c4 >> 1) ^ ((tid >> 5) & 3)) << 3) + 4 * (c4 & 1) : 4 * c4;  // row bits 2..3 = tid bits 5..6
 #pragma unroll
             for (int q = 0; q < A_V; ++q) {
                 bf16x4_t h, m, l;
@@ -473,15 +478,10 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
         ld_t = kbeg / cpt;
         ld_c = (kbeg - ld_t * cpt) * KT;
     }
-    if (kbeg < kend) load_chunk(kbeg);
-    for (int kc = kbeg; kc < kend; ++kc) {
-        __syncthreads();
-        store_chunk();
-        __syncthreads();
-        if (kc + 1 < kend) load_chunk(kc + 1);
-        if constexpr (B6) {
+    auto b6_compute = [&](int buf) {
+        const __bf16* const Pb = Pb0 + buf * 3 * PLANE;
             if (a.prio) __builtin_amdgcn_s_setprio(1);
-            const int rx = a.b6sw ? (lr >> 2) & 3 : 0;  // the row's slot swizzle (tile bases are multiples of 32 rows)
+            const int rx = b6p == 32 ? (lr >> 2) & 3 : 0;  // the row's slot swizzle (tile bases are multiples of 32 rows)
 #pragma unroll
             for (int s16 = 0; s16 < 2; ++s16) {
                 bf16x8_t af[TM][3], bf[TN][3];
@@ -503,6 +503,31 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
                     for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = bf6_mfma(af[tm], bf[tn], acc[tm][tn]);
             }
             if (a.prio) __builtin_amdgcn_s_setprio(0);
+    };
+    if constexpr (DB) {
+        if (kbeg < kend) {
+            load_chunk(kbeg);
+            store_chunk(0);
+        }
+        __syncthreads();
+        int cur = 0;
+        for (int kc = kbeg; kc < kend; ++kc) {
+            const bool nxt = kc + 1 < kend;  // block-uniform
+            if (nxt) load_chunk(kc + 1);
+            b6_compute(cur);
+            if (nxt) store_chunk(cur ^ 1);
+            __syncthreads();
+            cur ^= 1;
+        }
+    } else {
+    if (kbeg < kend) load_chunk(kbeg);
+    for (int kc = kbeg; kc < kend; ++kc) {
+        __syncthreads();
+        store_chunk();
+        __syncthreads();
+        if (kc + 1 < kend) load_chunk(kc + 1);
+        if constexpr (B6) {
+            b6_compute(0);
             continue;
         }
         if constexpr (F16) {
@@ -552,6 +577,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
                     }
         }
         if (a.prio) __builtin_amdgcn_s_setprio(0);
+    }
     }
 
     // ---- epilogue: stage the accumulators through LDS one TN column slice at a time (static register
@@ -747,6 +773,11 @@ void conv_fwd_kernel(const ConvArgs a) {
 template <int TM, int TN, int WAVES_M, int WAVES_N, int MODE, bool SPLITK>
 __global__ __launch_bounds__(256) void conv_fwd_b6_kernel(const ConvArgs a) {
     conv_fwd_body<TM, TN, WAVES_M, WAVES_N, MODE, SPLITK, false, 0, true>(a);
+}
+// the same with double-buffered staging (conv_fwd_body DB; round 6, the 64x64 tile only: hyres_conv_tuning key 20)
+template <int TM, int TN, int WAVES_M, int WAVES_N, int MODE, bool SPLITK>
+__global__ __launch_bounds__(256) void conv_fwd_b6db_kernel(const ConvArgs a) {
+    conv_fwd_body<TM, TN, WAVES_M, WAVES_N, MODE, SPLITK, false, 0, true, true>(a);
 }
 
 // fp16 activations in HBM (IO = 1: X fp16, 2: Y fp16, 3: both); fp16 MFMA operands except on the
@@ -2567,6 +2598,23 @@ static int launch_fwd(const ConvArgs& a, int mode, hipStream_t st) {
         return HY_LAUNCH_CHECK("conv_fwd_kernel(f16)");
     }
     if (g_tune[7] == 1 && mode != 2) {  // fp32 GEMM on the bf16 MFMA (bf16x6)
+        if constexpr (TM == 1 && TN == 1 && WM_ == 2 && WN_ == 2) {
+            // double-buffered staging (key 20 = 1, or -1: on for the <= 16384-pixel grids). Isolated it wins at 32^2
+            // (3x3 96 -> 96 39.6 -> 37.3 us, 1x1 192 -> 96 13.9 -> 13.1 us) and loses on the larger-K 64^2 / 5x5 layers
+            // (+2..5 %: the 49 KB of LDS cost the 4th block per CU, profiles/r6m_b6db.txt); in the graphed step the
+            // small-grid rule measured 0.2-0.3 ms SLOWER (profiles/r6n_b6db_step_ab.txt: those layers run beside the
+            // branch streams' kernels), so the default is off
+            if (g_tune[20] == 1 || (g_tune[20] < 0 && a.M <= 16384)) {
+                if (a.nsplit > 1) {
+                    if (mode == 0) hipLaunchKernelGGL((conv_fwd_b6db_kernel<1, 1, 2, 2, 0, true>), grid, dim3(256), 0, st, a);
+                    else hipLaunchKernelGGL((conv_fwd_b6db_kernel<1, 1, 2, 2, 1, true>), grid, dim3(256), 0, st, a);
+                } else {
+                    if (mode == 0) hipLaunchKernelGGL((conv_fwd_b6db_kernel<1, 1, 2, 2, 0, false>), grid, dim3(256), 0, st, a);
+                    else hipLaunchKernelGGL((conv_fwd_b6db_kernel<1, 1, 2, 2, 1, false>), grid, dim3(256), 0, st, a);
+                }
+                return HY_LAUNCH_CHECK("conv_fwd_b6db_kernel");
+            }
+        }
         if (a.nsplit > 1) {
             if (mode == 0) hipLaunchKernelGGL((conv_fwd_b6_kernel<TM, TN, WM_, WN_, 0, true>), grid, dim3(256), 0, st, a);
             else hipLaunchKernelGGL((conv_fwd_b6_kernel<TM, TN, WM_, WN_, 1, true>), grid, dim3(256), 0, st, a);
@@ -2660,7 +2708,7 @@ static void dense_taps(hyres_conv_geom* g, int KH, int KW, int sgn, int dil, int
 // key 7: fp32 GEMMs bf16x6 (0: native fp32 MFMA); key 8: fp16 streaming 1x1; key 9: the bf16x6 weight-resident 3x3's
 // whole-VGPR-file guard (0 = diagnostic unguarded build, DESIGN §4 "Cross-kernel interference"); key 10: the bf16x6
 // streaming 1x1 kernel (0 = those layers on the tiled implicit GEMM, for A/B)
-int g_tune[HYRES_TUNE_KEYS] = {-1, -1, -1, -1, -1, -1, -1, 1, 1, 1, 1, 1, 1, 1, 1, 2, 2, 1, 1, 1};  // key 19: b6sw
+int g_tune[HYRES_TUNE_KEYS] = {-1, -1, -1, -1, -1, -1, -1, 1, 1, 1, 1, 1, 1, 1, 1, 2, 2, 1, 1, 1, 0, -1, -1, -1};
 
 }  // namespace hyres
 
@@ -3435,7 +3483,10 @@ int hyres_conv_kernel_name(const hyres_conv_geom* g, const hyres_epilogue* e, in
         return 0;
     }
     if (g_tune[7] == 1 && !f16 && ch.mode != 2) {
-        snprintf(buf, n, "conv_fwd_b6_kernel<%s, %d, %s>", tiles[ch.tile], ch.mode, split ? "true" : "false");
+        const long long M = (long long)g->B * g->Hq * g->Wq;
+        const bool db = ch.tile == 4 && (g_tune[20] == 1 || (g_tune[20] < 0 && M <= 16384));
+        snprintf(buf, n, "%s<%s, %d, %s>", db ? "conv_fwd_b6db_kernel" : "conv_fwd_b6_kernel", tiles[ch.tile], ch.mode,
+                 split ? "true" : "false");
         return 0;
     }
     snprintf(buf, n, "conv_fwd_kernel<%s, %d, %s, %s>", tiles[ch.tile], ch.mode, split ? "true" : "false",

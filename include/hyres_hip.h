@@ -209,7 +209,10 @@ int hyres_conv_plan(const hyres_conv_geom* g, const hyres_epilogue* e, int* tile
 #define HYRES_TUNE_B6_SWIZZLE 19      /* 1 (default): the bf16x6 implicit GEMM stages its split planes in 64-B LDS rows with the
                                        * 16-B slots XOR-swizzled by row (conflict-free stores and reads); 0: 80-B padded rows
                                        * (2-way store conflicts), A/B; bit-identical */
-#define HYRES_TUNE_KEYS 20
+#define HYRES_TUNE_B6_DB 20           /* the bf16x6 implicit GEMM's 64x64 tile staging K chunks in two LDS buffers (one barrier
+                                       * per chunk, conv_fwd_b6db_kernel): 1 always, -1 on grids of <= 16384 output pixels,
+                                       * 0 (default) never (one buffer, two barriers; faster in the graphed step); bit-identical */
+#define HYRES_TUNE_KEYS 24            /* keys 21..23 reserved */
 int hyres_conv_tuning(int key, int value, int* old);
 
 /* Weight gradient:  dW[t][m][n] = sum_q P[q][m] * Q[shift_t(q)][n]  over a base grid q (B,Hq,Wq).

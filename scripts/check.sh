@@ -75,6 +75,11 @@ for ph in "$@"; do
            python3 scripts/as_traffic.py --summarize gpurun_out/${tag}_as_f gpurun_out/${tag}_as_w --out gpurun_out/${tag}_as_traffic.json ;;
     b6sw)  scripts/gpu_run.sh "b6sw:400:for t in 1 0 1 0; do for s in '--H 32 --Ci 96 --Co 96 --K 3 --relu' '--H 32 --Ci 192 --Co 96 --K 1 --relu' '--H 32 --Ci 384 --Co 192 --K 3 --relu' '--H 64 --Ci 64 --Co 128 --K 3 --relu' '--H 32 --Ci 640 --Co 512 --K 1' '--H 128 --Ci 128 --Co 128 --K 5 --stride 2'; do HYRES_TUNE=19=\$t python3 scripts/conv_micro.py \$s --bf6 | sed \"s/^/b6sw=\$t /\"; done; done" || exit $?
            grep -h "us" gpurun_out/b6sw.log > gpurun_out/${tag}_b6sw.txt ;;
+    b6db)  scripts/gpu_run.sh "b6db:400:for t in 0 1 0 1; do for s in '--H 32 --Ci 96 --Co 96 --K 3 --relu' '--H 32 --Ci 192 --Co 96 --K 1 --relu' '--H 32 --Ci 384 --Co 192 --K 3 --relu' '--H 128 --Ci 128 --Co 128 --K 5 --stride 2' '--H 64 --Ci 64 --Co 128 --K 3 --relu' '--H 64 --Ci 128 --Co 128 --K 3 --relu'; do HYRES_TUNE=20=\$t python3 scripts/conv_micro.py \$s --bf6 | sed \"s/^/b6db=\$t /\"; done; done" \
+             "b6dbtest:300:python -u -m pytest tests/test_bf6_gpu.py -x -v --timeout 120 --timeout-method thread -m gpu -k staging" || exit $?
+           grep -h "us" gpurun_out/b6db.log > gpurun_out/${tag}_b6db.txt ;;
+    tb6)   scripts/gpu_run.sh "tb6:500:python -u -m pytest tests/test_bf6_gpu.py tests/test_coresidency_gpu.py -x -v --timeout 180 --timeout-method thread -m gpu" || exit $? ;;
+    ab7)   bash scripts/tune_ab.sh $tag "default=" "nodb=HYRES_TUNE=20=0" || exit $? ;;
     *) echo "unknown phase $ph"; exit 2 ;;
   esac
 done

@@ -102,7 +102,7 @@ def test_bf6_implicit_gemm_conv_as_accurate_as_fp32(case):
     torch.cuda.synchronize()
     e32, e6 = rel_err(outs[False].cpu(), ref.cpu()), rel_err(outs[True].cpu(), ref.cpu())
     print(case, names, f"error vs fp64: native {e32:.2e}, bf16x6 {e6:.2e}")
-    assert names[True].startswith("conv_fwd_b6_kernel") or names[True].startswith("conv3x3_wres_bf6")
+    assert names[True].startswith(("conv_fwd_b6_kernel", "conv_fwd_b6db_kernel", "conv3x3_wres_bf6")), names[True]
     assert e6 <= 2.0 * e32 + 1e-9 and e6 < 1e-5
 
 
@@ -710,3 +710,44 @@ def test_wgrad_prefetch2_kernels_bit_identical(K, B, H, W, Ci, Co, key):
     err = float((res[2][0].double() - ref).abs().max() / ref.abs().max())
     assert err < 1e-5, err
     assert float((res[2][1].double() - gr.sum((0, 2, 3))).abs().max()) < 1e-3
+
+
+@pytest.mark.parametrize("B,H,Ci,Co,K,stride,swz_off", [
+    (16, 32, 96, 96, 3, 1, False),     # AttentionBlock(192)'s RU 3x3 at 32^2 (the 64x64 tile)
+    (16, 32, 192, 96, 1, 1, False),    # its 1x1 192 -> 96
+    (4, 64, 128, 128, 5, 2, False),    # 5x5 stride 2 (g_a)
+    (2, 16, 384, 192, 3, 1, True),     # a split-K grid; and the 80-B padded rows (key 19 = 0) as the reference
+])
+def test_bf6_implicit_gemm_staging_variants_bit_identical(B, H, Ci, Co, K, stride, swz_off):
+    """The bf16x6 implicit GEMM's LDS staging variants change where the split planes sit and when they are stored,
+    not the MFMAs or their order: the double-buffered 64x64-tile kernel (hyres_conv_tuning key 20 = 1,
+    conv_fwd_b6db_kernel) and the XOR-swizzled 64-B rows (key 19, default) must equal the single-buffered kernel and
+    (swz_off) the 80-B padded rows bit for bit — forward with bias + ReLU and the residual epilogue."""
+    import ctypes
+    from hyres_hip import _lib as L
+    from hyres_hip import ops as O
+    D = dev()
+    x = _rand((B, Ci, H, H), 71).to(D)
+    w = torch.nn.Parameter(_rand((Co, Ci, K, K), 72, (Ci * K * K) ** -0.5).to(D))
+    b = _rand((Co,), 73, 0.1).to(D)
+    Ho = H // stride
+    r = _rand((B, Co, Ho, Ho), 74).to(D)
+
+    def run(db, sw):
+        olds = [ctypes.c_int(0), ctypes.c_int(0)]
+        with _Bf6(True):
+            L.call("hyres_conv_tuning", 20, db, ctypes.byref(olds[0]))
+            L.call("hyres_conv_tuning", 19, sw, ctypes.byref(olds[1]))
+            try:
+                xn, rn = O.to_nhwc(x), O.to_nhwc(r)
+                yn = O.conv2d(None, xn, w, b, stride=stride, pad=K // 2, act=L.ACT_RELU, res=rn)
+                torch.cuda.synchronize()
+                return O.to_nchw(yn).clone()
+            finally:
+                L.call("hyres_conv_tuning", 20, olds[0].value, None)
+                L.call("hyres_conv_tuning", 19, olds[1].value, None)
+
+    ref = run(0, 0 if swz_off else 1)
+    for db, sw in ((1, 1), (0, 1)):
+        got = run(db, sw)
+        assert torch.equal(ref, got), (db, sw, float((ref - got).abs().max()))
