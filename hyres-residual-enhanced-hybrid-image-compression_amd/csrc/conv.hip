@@ -3197,8 +3197,16 @@ static ConvChoice choose_conv(const hyres_conv_geom* g, const hyres_epilogue* e,
     if (short_k && g->Co > 64 && !(r6 && !f16 && mtot <= small_px && g->Co <= 192)) c.tile = 3;
     else if (short_k && g->Co > 32) c.tile = 4;
     else if (c.mode != 2 && g->Co > 32 && mtot <= small_px) {
+        // K depth of the deepest phase: the K-heavy single-phase layers take the bigger tiles (fragment reuse) —
+        // 128^2 -> 64^2 5x5 s2 128 -> 128 434 -> 347 us on 128x128, 32^2 3x3 384 -> 192 195 -> 183 us and 64^2 -> 32^2
+        // 5x5 s2 128 -> 192 183 -> 172 us on 128x64 (profiles/r6p_tile5.txt)
+        int maxtap = 0;
+        for (int ph = 0; ph < g->nphase; ++ph) maxtap = std::max(maxtap, g->ntap[ph]);
+        const bool kheavy = g->nphase == 1 && (long long)maxtap * g->Ci >= 1024;
         if (f16) c.tile = g->Co >= 192 ? 0 : 4;
-        else c.tile = (r6 && g->Co >= 512) ? 0 : g->Co > 192 ? 3 : 4;
+        else if (r6 && (g->Co >= 512 || (kheavy && mtot >= small_px && g->Co >= 128))) c.tile = 0;
+        else if (r6 && kheavy && g->Co == 192) c.tile = 1;
+        else c.tile = g->Co > 192 ? 3 : 4;
     }
     else if (c.mode == 2 && g->Co > 32) c.tile = g->Co > 64 ? 3 : 4;  // scalar-load path: 64-row tiles
     else if (g->Co > 64) c.tile = 0;

@@ -80,6 +80,11 @@ for ph in "$@"; do
            grep -h "us" gpurun_out/b6db.log > gpurun_out/${tag}_b6db.txt ;;
     tb6)   scripts/gpu_run.sh "tb6:500:python -u -m pytest tests/test_bf6_gpu.py tests/test_coresidency_gpu.py -x -v --timeout 180 --timeout-method thread -m gpu" || exit $? ;;
     ab7)   bash scripts/tune_ab.sh $tag "default=" "nodb=HYRES_TUNE=20=0" || exit $? ;;
+    tile5) scripts/gpu_run.sh "tile5:400:for t in -1 0 1 3 4; do for s in '--H 128 --Ci 128 --Co 128 --K 5 --stride 2' '--H 64 --Ci 128 --Co 192 --K 5 --stride 2' '--H 32 --Ci 384 --Co 192 --K 3 --relu' '--H 64 --Ci 128 --Co 128 --K 3 --relu' '--H 32 --Ci 192 --Co 384 --K 3'; do python3 scripts/conv_micro.py \$s --bf6 --tile \$t | sed \"s/^/tile \$t /\"; done; done" || exit $?
+           grep -h "us" gpurun_out/tile5.log > gpurun_out/${tag}_tile5.txt ;;
+    tile6) scripts/gpu_run.sh "tile6:400:for t in 1 0 1 0; do for s in '--H 128 --Ci 128 --Co 128 --K 5 --stride 2' '--H 64 --Ci 128 --Co 192 --K 5 --stride 2' '--H 32 --Ci 384 --Co 192 --K 3 --relu' '--H 32 --Ci 96 --Co 192 --K 1 --res --relu' '--H 32 --Ci 640 --Co 512 --K 1'; do HYRES_TUNE=18=\$t python3 scripts/conv_micro.py \$s --bf6 | sed \"s/^/rule18=\$t /\"; done; done" || exit $?
+           grep -h "us" gpurun_out/tile6.log > gpurun_out/${tag}_tile6.txt
+           bash scripts/tune_ab.sh $tag "default=" "r5tile=HYRES_TUNE=18=0" || exit $? ;;
     *) echo "unknown phase $ph"; exit 2 ;;
   esac
 done
