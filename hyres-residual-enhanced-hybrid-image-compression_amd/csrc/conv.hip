@@ -1971,10 +1971,15 @@ constexpr int stream_b6_vgprs() {
     return 256;
 }
 template <int NT, int KS, int F, bool CE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(512 / stream_b6_vgprs<NT, KS, F>())))
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 6 ? 1 : 512 / stream_b6_vgprs<NT, KS, F>())))
 void conv1x1_stream_b6_kernel(const ConvArgs a) {
     constexpr int K = 16 * KS, KP = K + 8, CO = 32 * NT;
     constexpr bool RES = (F & 1) != 0, MASK = (F & 2) != 0, ACC = (F & 4) != 0;
+    // SAB (F & 8, round 6): the HYRES_EPI_SA_BWD epilogue of MultiScaleRefine's fusion-1x1 input-gradient (64 -> 192 at
+    // 256^2): o = (acc + aux0[p][0]) + (n == aux2[p] ? aux0[p][1] : 0), epi_store's order; no bias, no activation.
+    // The per-pixel operands are loaded once per 32-pixel tile, the next tile's while this one multiplies
+    constexpr bool SAB = (F & 8) != 0;
+    static_assert(!SAB || (CE && !RES && !MASK), "SA_BWD: the coalesced epilogue, no residual / mask");
     constexpr int WPL = CO * KP;  // bf16 per weight plane
     __shared__ __attribute__((aligned(16))) __bf16 Ws[3 * WPL];
     __shared__ __attribute__((aligned(16))) float bs[CO];
@@ -1982,8 +1987,10 @@ void conv1x1_stream_b6_kernel(const ConvArgs a) {
     // land on 16 distinct 4-bank groups)
     constexpr int EP = 36;
     __shared__ __attribute__((aligned(16))) float Es[CE ? 4 * 32 * EP : 4];
-    // exactly 2 or 4 waves' worth of VGPRs: no room for another kernel's wave on these SIMDs
-    if constexpr (stream_b6_vgprs<NT, KS, F>() == 128) asm volatile("" ::: "v127");
+    // exactly 2 or 4 waves' worth of VGPRs: no room for another kernel's wave on these SIMDs. NT = 6 (the 64 -> 192
+    // SA_BWD form): 102 KB of LDS admit one block per CU, i.e. one wave per SIMD — it takes all 512 registers
+    if constexpr (NT == 6) asm volatile("" ::: "v255", "a255");
+    else if constexpr (stream_b6_vgprs<NT, KS, F>() == 128) asm volatile("" ::: "v127");
     else asm volatile("" ::: "v255");
     const hyres_conv_geom& g = a.g;
     const hyres_epilogue& e = a.e;
@@ -2035,6 +2042,22 @@ void conv1x1_stream_b6_kernel(const ConvArgs a) {
     constexpr int SETS = stream_b6_vgprs<NT, KS, F>() == 128 ? 1 : 2;
     float4 xv[KS][2];
     float4 eres[RES ? SETS : 1][4], emask[MASK ? SETS : 1][4], eold[ACC ? SETS : 1][4];
+    // SAB: this tile's (d mean / C, d max) and argmax per epilogue row q, and the next tile's in flight
+    float2 sg[SAB ? 4 : 1], sgn[SAB ? 4 : 1];
+    int si[SAB ? 4 : 1], sin_[SAB ? 4 : 1];
+    const __amdgpu_buffer_rsrc_t r_sg = opnd_rsrc(SAB ? e.aux0 : nullptr, npix * e.ld0 * 4);
+    const __amdgpu_buffer_rsrc_t r_si = opnd_rsrc(SAB ? e.aux2 : nullptr, npix * 4);
+    auto load_sab = [&](int tile, float2 (&g2)[SAB ? 4 : 1], int (&i1)[SAB ? 4 : 1]) {
+        if constexpr (SAB) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int p = tile * 32 + cr + 8 * q;
+                const bool ok = tile < ntile && p < a.M;
+                g2[q] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(r_sg, ok ? p * e.ld0 * 4 : OOR, 0, 0));
+                i1[q] = __builtin_bit_cast(int, __builtin_amdgcn_raw_buffer_load_b32(r_si, ok ? p * 4 : OOR, 0, 0));
+            }
+        }
+    };
     auto load_epi = [&](int tile, int t, int set) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -2048,7 +2071,9 @@ void conv1x1_stream_b6_kernel(const ConvArgs a) {
 #pragma unroll
         for (int u = 0; u < 2; ++u) xv[s][u] = bload4(xr, xoff(gw, s, u));
     load_epi(gw, 0, 0);
+    load_sab(gw, sg, si);
     for (int tile = gw; tile < ntile; tile += nw) {
+        load_sab(tile + nw, sgn, sin_);
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
             const int cur = SETS == 2 ? (t & 1) : 0;
@@ -2106,6 +2131,11 @@ void conv1x1_stream_b6_kernel(const ConvArgs a) {
                 const int p = CE ? tile * 32 + cr + 8 * q : tile * 32 + lr;
                 const bool pok = p < a.M;
                 float o[4] = {av.x + b4.x, av.y + b4.y, av.z + b4.z, av.w + b4.w};
+                if constexpr (SAB) {
+                    const float av4[4] = {av.x, av.y, av.z, av.w};
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) o[c] = av4[c] + sg[q].x + (n + c == si[q] ? sg[q].y : 0.f);
+                }
                 if constexpr (RES) {
                     o[0] += eres[cur][q].x; o[1] += eres[cur][q].y; o[2] += eres[cur][q].z; o[3] += eres[cur][q].w;
                 }
@@ -2132,6 +2162,13 @@ void conv1x1_stream_b6_kernel(const ConvArgs a) {
                 else load_epi(tile + nw, 0, 0);
             }
             __builtin_amdgcn_sched_barrier(0);  // keep the next co tile's LDS reads and splits out of this one
+        }
+        if constexpr (SAB) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                sg[q] = sgn[q];
+                si[q] = sin_[q];
+            }
         }
     }
 }
@@ -2708,7 +2745,7 @@ static void dense_taps(hyres_conv_geom* g, int KH, int KW, int sgn, int dil, int
 // key 7: fp32 GEMMs bf16x6 (0: native fp32 MFMA); key 8: fp16 streaming 1x1; key 9: the bf16x6 weight-resident 3x3's
 // whole-VGPR-file guard (0 = diagnostic unguarded build, DESIGN §4 "Cross-kernel interference"); key 10: the bf16x6
 // streaming 1x1 kernel (0 = those layers on the tiled implicit GEMM, for A/B)
-int g_tune[HYRES_TUNE_KEYS] = {-1, -1, -1, -1, -1, -1, -1, 1, 1, 1, 1, 1, 1, 1, 1, 2, 2, 1, 1, 1, 0, -1, -1, -1};
+int g_tune[HYRES_TUNE_KEYS] = {-1, -1, -1, -1, -1, -1, -1, 1, 1, 1, 1, 1, 1, 1, 1, 2, 2, 1, 1, 1, 0, 1, -1, -1};
 
 }  // namespace hyres
 
@@ -3058,7 +3095,15 @@ static int stream_hf_cfg(const hyres_conv_geom* g, const hyres_epilogue* e) {
 // or 0.
 static int stream_b6_cfg(const hyres_conv_geom* g, const hyres_epilogue* e) {
     if (g_tune[7] != 1 || g_tune[10] == 0) return 0;
-    if (e->io_f16 || e->f16_operands || e->square_input || e->kind != HYRES_EPI_BIAS) return 0;
+    if (e->io_f16 || e->f16_operands || e->square_input) return 0;
+    if (e->kind == HYRES_EPI_SA_BWD) {  // round 6: the fusion 1x1's input-gradient, 64 -> 192 (coalesced epilogue only)
+        if (g_tune[11] == 0 || g_tune[21] == 0 || g->Ci != 64 || g->Co != 192 || e->act != HYRES_ACT_NONE || e->res ||
+            e->out2 || g->nphase != 1 || g->ntaps != 1 || g->ish != 1 || g->isw != 1 || g->dh[0] != 0 || g->dw[0] != 0 ||
+            g->Hi != g->Hq || g->Wi != g->Wq || g->Ho != g->Hq || g->Wo != g->Wq || (long long)g->B * g->Hq * g->Wq < 65536)
+            return 0;
+        return 6 | (4 << 4) | ((8 | (e->accumulate ? 4 : 0)) << 8);
+    }
+    if (e->kind != HYRES_EPI_BIAS) return 0;
     if (g->nphase != 1 || g->ntaps != 1 || g->ish != 1 || g->isw != 1 || g->dh[0] != 0 || g->dw[0] != 0) return 0;
     if (g->Hi != g->Hq || g->Wi != g->Wq || g->Ho != g->Hq || g->Wo != g->Wq) return 0;
     if ((long long)g->B * g->Hq * g->Wq < 65536) return 0;
@@ -3122,6 +3167,8 @@ static int launch_stream_b6_f(const ConvArgs& a, int f, hipStream_t st) {
 
 static int launch_stream_b6(const ConvArgs& a, int cfg, hipStream_t st) {
     const int nt = cfg & 15, ks = (cfg >> 4) & 15, f = cfg >> 8;
+    if (nt == 6 && ks == 4 && f == 8) return launch_stream_b6_ce<6, 4, 8, true>(a, st);
+    if (nt == 6 && ks == 4 && f == 12) return launch_stream_b6_ce<6, 4, 12, true>(a, st);
     if (nt == 2 && ks == 4) return launch_stream_b6_f<2, 4>(a, f, st);
     if (nt == 4 && ks == 4) return launch_stream_b6_f<4, 4>(a, f, st);
     if (nt == 2 && ks == 8) return launch_stream_b6_f<2, 8>(a, f, st);

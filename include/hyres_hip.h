@@ -212,7 +212,9 @@ int hyres_conv_plan(const hyres_conv_geom* g, const hyres_epilogue* e, int* tile
 #define HYRES_TUNE_B6_DB 20           /* the bf16x6 implicit GEMM's 64x64 tile staging K chunks in two LDS buffers (one barrier
                                        * per chunk, conv_fwd_b6db_kernel): 1 always, -1 on grids of <= 16384 output pixels,
                                        * 0 (default) never (one buffer, two barriers; faster in the graphed step); bit-identical */
-#define HYRES_TUNE_KEYS 24            /* keys 21..23 reserved */
+#define HYRES_TUNE_STREAM_SAB 21      /* 1 (default): the SA_BWD input-gradient of MultiScaleRefine's fusion 1x1 (64 -> 192 on
+                                       * >= 65536 pixels) on conv1x1_stream_b6_kernel<6, 4, 8 | acc>; 0: the implicit GEMM */
+#define HYRES_TUNE_KEYS 24            /* keys 22..23 reserved */
 int hyres_conv_tuning(int key, int value, int* old);
 
 /* Weight gradient:  dW[t][m][n] = sum_q P[q][m] * Q[shift_t(q)][n]  over a base grid q (B,Hq,Wq).

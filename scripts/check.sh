@@ -85,6 +85,12 @@ for ph in "$@"; do
     tile6) scripts/gpu_run.sh "tile6:400:for t in 1 0 1 0; do for s in '--H 128 --Ci 128 --Co 128 --K 5 --stride 2' '--H 64 --Ci 128 --Co 192 --K 5 --stride 2' '--H 32 --Ci 384 --Co 192 --K 3 --relu' '--H 32 --Ci 96 --Co 192 --K 1 --res --relu' '--H 32 --Ci 640 --Co 512 --K 1'; do HYRES_TUNE=18=\$t python3 scripts/conv_micro.py \$s --bf6 | sed \"s/^/rule18=\$t /\"; done; done" || exit $?
            grep -h "us" gpurun_out/tile6.log > gpurun_out/${tag}_tile6.txt
            bash scripts/tune_ab.sh $tag "default=" "r5tile=HYRES_TUNE=18=0" || exit $? ;;
+    tile1x1) scripts/gpu_run.sh "tile1x1:400:for t in -1 0 1 2 3 4; do for s in '--H 256 --Ci 64 --Co 192 --K 1' '--H 256 --Ci 192 --Co 64 --K 1 --relu' '--H 128 --Ci 128 --Co 128 --K 1' '--H 128 --Ci 128 --Co 128 --K 1 --relu'; do python3 scripts/conv_micro.py \$s --bf6 --tile \$t | sed \"s/^/tile \$t /\"; done; done" || exit $?
+           grep -h "us" gpurun_out/tile1x1.log > gpurun_out/${tag}_tile1x1.txt ;;
+    sab)   scripts/gpu_run.sh "sabtest:300:python -u -m pytest tests/test_stream_b6_gpu.py tests/test_parity_gpu.py -x -v --timeout 180 --timeout-method thread -m gpu -k 'sa_bwd or sa_fold or c2_size'" \
+             "sabmicro:300:for t in 1 0 1 0; do HYRES_TUNE=21=\$t python3 scripts/layer_table.py > gpurun_out/sab_layers_\$t.txt 2>&1 && grep 'epi6' gpurun_out/sab_layers_\$t.txt | sed \"s/^/sab=\$t /\"; done" || exit $?
+           grep -h "sab=" gpurun_out/sabmicro.log > gpurun_out/${tag}_sab.txt
+           bash scripts/tune_ab.sh $tag "default=" "nosab=HYRES_TUNE=21=0" || exit $? ;;
     *) echo "unknown phase $ph"; exit 2 ;;
   esac
 done

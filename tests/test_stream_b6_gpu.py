@@ -104,3 +104,55 @@ def test_stream_b6_matches_fp64(Ci, Co, F):
     assert not name_t.startswith("conv1x1_stream_b6"), name_t
     for err in (err_s, err_m):
         assert err < 2e-6 and err <= 2 * err_t + 1e-9
+
+
+def _run_sab(acc, stream_on):
+    """The HYRES_EPI_SA_BWD input-gradient of MultiScaleRefine's fusion 1x1 (64 -> 192): y = (W^T g + gm[p][0]) +
+    (n == argmax[p] ? gm[p][1] : 0) (+ old y), through the C-ABI on the streaming kernel or the implicit GEMM."""
+    from hyres_hip import _lib as L
+    from hyres_hip import ops as O
+    D = dev()
+    B, H, W = 5, 117, 117
+    P, Ci, Co = B * H * W, 64, 192
+    x = _rand((P, Ci), 11).to(D)
+    w = _rand((Co, Ci, 1, 1), 12, Ci ** -0.5).to(D)
+    gm = _rand((P, 2), 13).to(D)
+    am = torch.randint(0, Co, (P,), generator=torch.Generator().manual_seed(14), dtype=torch.int32).to(D)
+    old = _rand((P, Co), 15).to(D)
+    y = old.clone() if acc else torch.full((P, Co), float("nan"), device=D)
+    g = O._geom("hyres_geom_conv2d", B, H, W, Ci, Ci, Co, Co, 1, 1, 1, 0, 1)
+    w2 = torch.empty((Co, Ci), device=D)
+    L.call("hyres_conv_weight_prep", ctypes.byref(g), w.data_ptr(), w2.data_ptr(), 0, Ci, Co, 1, 1, 0, None, L.stream())
+    e = L.Epilogue()
+    e.kind = L.EPI_SA_BWD
+    e.aux0, e.ld0 = gm.data_ptr(), 2
+    e.aux2 = am.data_ptr()
+    e.accumulate = int(acc)
+    old_key = ctypes.c_int(0)
+    L.call("hyres_conv_tuning", 21, 1 if stream_on else 0, ctypes.byref(old_key))
+    try:
+        name = O.conv_variant(g, e, False)
+        L.call("hyres_conv_forward", ctypes.byref(g), x.data_ptr(), w2.data_ptr(), Ci, y.data_ptr(), ctypes.byref(e),
+               None, 0, L.stream())
+        torch.cuda.synchronize()
+    finally:
+        L.call("hyres_conv_tuning", 21, old_key.value, None)
+    r = x.double() @ w.double().reshape(Co, Ci).t() + gm[:, :1].double()
+    r = r + torch.where(torch.arange(Co, device=D)[None, :] == am[:, None].long(), gm[:, 1:].double(),
+                        torch.zeros((), dtype=torch.float64, device=D))
+    if acc:
+        r = r + old.double()
+    return name, rel_err(y.double().cpu(), r.cpu())
+
+
+@pytest.mark.parametrize("acc", [False, True])
+def test_stream_b6_sa_bwd_matches_fp64(acc):
+    """conv1x1_stream_b6_kernel<6, 4, 8 | acc> (round 6, hyres_conv_tuning key 21): the SA_BWD input-gradient 64 -> 192
+    on a ragged pixel count vs fp64 (2e-6 normwise, no worse than twice the implicit GEMM it replaces on the same
+    call)."""
+    name_s, err_s = _run_sab(acc, True)
+    name_t, err_t = _run_sab(acc, False)
+    print(f"SA_BWD 64->192 acc={acc}: {name_s} {err_s:.2e}, {name_t} {err_t:.2e}")
+    assert name_s == f"conv1x1_stream_b6_kernel<6, 4, {8 | (4 if acc else 0)}, true>", name_s
+    assert not name_t.startswith("conv1x1_stream_b6"), name_t
+    assert err_s < 2e-6 and err_s <= 2 * err_t + 1e-9, (err_s, err_t)
