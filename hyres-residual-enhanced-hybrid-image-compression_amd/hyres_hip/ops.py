@@ -151,9 +151,12 @@ class Node:
         return self.parent.grad_ld() if self.parent is not None else self.C
 
     def defer_residual(self, g: torch.Tensor, ld: int) -> bool:
-        """Record the residual-branch gradient ``g`` (pixel stride ``ld``) as this node's first contribution,
-        to be added inside the next writer's epilogue (False: not deferrable, the caller adds it now)."""
-        if self.parent is not None or self.gflag or self.pending is not None:
+        """Record the residual-branch gradient ``g`` (pixel stride ``ld``) to be added inside the next writer's
+        epilogue (False: not deferrable, the caller adds it now). Round 6: also onto a node that already holds a
+        gradient (an AttentionBlock input: the gate's identity term arrives first) — the next input-gradient conv
+        then writes old + (conv + g) with accumulate on, instead of an add2d pass before it (DEFER_ON_GRAD=False:
+        the round-5 rule, first contribution only)."""
+        if self.parent is not None or (self.gflag and not DEFER_ON_GRAD) or self.pending is not None:
             return False
         self.pending = (g, ld)
         return True
@@ -170,7 +173,7 @@ class Node:
         (tensor, accumulate, keep-alive tensor or None)."""
         # the conv reads e.res in the dtype of the gradient it writes: fold only a same-dtype pending gradient
         # (a mixed pair, e.g. an fp16 gradient deferred onto an fp32-gradient node, goes through add2d)
-        if (self.pending is not None and self.parent is None and not self.gflag
+        if (self.pending is not None and self.parent is None and (DEFER_ON_GRAD or not self.gflag)
                 and self.pending[0].dtype == self.gdt):
             g, ld = self.pending
             self.pending = None
@@ -620,6 +623,9 @@ F16_ACT = os.environ.get("HYRES_F16_ACT", "1") == "1"
 # PReLU backward folded into the input-gradient conv that writes the PReLU output's gradient (Node.prelu_mask_epilogue);
 # HYRES_FOLD_PRELU=0: the separate prelu_bwd pass (A/B)
 FOLD_PRELU = os.environ.get("HYRES_FOLD_PRELU", "1") == "1"
+# a residual-branch gradient deferred into the next input-gradient conv's epilogue also when the node already holds a
+# gradient (Node.defer_residual); HYRES_DEFER_ON_GRAD=0: only as the first contribution (A/B)
+DEFER_ON_GRAD = os.environ.get("HYRES_DEFER_ON_GRAD", "1") == "1"
 # AMP training stores the f16_region's activations (forward outputs saved for backward) as fp16 too, like
 # torch autocast, whose conv outputs are fp16 tensors (src/utils/engine.py:32); gradients stay fp32
 AMP_F16_ACT = os.environ.get("HYRES_AMP_F16_ACT", "1") == "1"

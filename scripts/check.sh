@@ -91,6 +91,7 @@ for ph in "$@"; do
              "sabmicro:300:for t in 1 0 1 0; do HYRES_TUNE=21=\$t python3 scripts/layer_table.py > gpurun_out/sab_layers_\$t.txt 2>&1 && grep 'epi6' gpurun_out/sab_layers_\$t.txt | sed \"s/^/sab=\$t /\"; done" || exit $?
            grep -h "sab=" gpurun_out/sabmicro.log > gpurun_out/${tag}_sab.txt
            bash scripts/tune_ab.sh $tag "default=" "nosab=HYRES_TUNE=21=0" || exit $? ;;
+    ab8)   bash scripts/tune_ab.sh $tag "default=" "nodefer=HYRES_DEFER_ON_GRAD=0" || exit $? ;;
     *) echo "unknown phase $ph"; exit 2 ;;
   esac
 done
