@@ -131,6 +131,38 @@ __global__ void attn_gate_fwd_kernel(const float* a, const float* b, const float
         out[i] = a[i] * s + x[i];
     }
 }
+// fp32, 4 elements per thread (round 6: the scalar kernels above ran the 32^2 AttentionBlock gates at ~0.9 TB/s); same
+// arithmetic per element (bit-identical). MASK (backward): the gradient of a — the last ResidualUnit's ReLU output —
+// with that ReLU's backward folded in, (a > 0) ? g * s : 0 (ops.attn_gate marks a's gradient masked)
+__global__ __launch_bounds__(256) void attn_gate_fwd4_kernel(const float* a, const float* b, const float* x, float* out,
+                                                             long long n4) {
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+        const float4 av = ld4(a + 4 * i), bv = ld4(b + 4 * i), xv = ld4(x + 4 * i);
+        const float s[4] = {1.0f / (1.0f + expf(-bv.x)), 1.0f / (1.0f + expf(-bv.y)), 1.0f / (1.0f + expf(-bv.z)),
+                            1.0f / (1.0f + expf(-bv.w))};
+        *reinterpret_cast<float4*>(out + 4 * i) =
+            make_float4(av.x * s[0] + xv.x, av.y * s[1] + xv.y, av.z * s[2] + xv.z, av.w * s[3] + xv.w);
+    }
+}
+template <bool MASK>
+__global__ __launch_bounds__(256) void attn_gate_bwd4_kernel(const float* a, const float* b, const float* g, float* ga,
+                                                             float* gb, long long n4) {
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+        const float4 av4 = ld4(a + 4 * i), bv4 = ld4(b + 4 * i), gv4 = ld4(g + 4 * i);
+        const float av[4] = {av4.x, av4.y, av4.z, av4.w}, bv[4] = {bv4.x, bv4.y, bv4.z, bv4.w};
+        const float gv[4] = {gv4.x, gv4.y, gv4.z, gv4.w};
+        float oa[4], ob[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const float s = 1.0f / (1.0f + expf(-bv[c]));
+            oa[c] = gv[c] * s;
+            if constexpr (MASK) oa[c] = av[c] > 0.f ? oa[c] : 0.f;
+            ob[c] = gv[c] * av[c] * s * (1.0f - s);
+        }
+        *reinterpret_cast<float4*>(ga + 4 * i) = make_float4(oa[0], oa[1], oa[2], oa[3]);
+        *reinterpret_cast<float4*>(gb + 4 * i) = make_float4(ob[0], ob[1], ob[2], ob[3]);
+    }
+}
 // fp16 activations (autocast inference): a, b, x, out fp16, 4 elements per thread, fp32 arithmetic
 __global__ void attn_gate_fwd4h_kernel(const float* a, const float* b, const float* x, float* out, long long n4) {
     for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
@@ -586,8 +618,13 @@ int hyres_prelu_bwd_f16(const void* x, int ldx, const void* g, int ldg, void* gx
     return prelu_bwd_impl<true, false>((const float*)x, ldx, (const float*)g, ldg, (float*)gx, ldgx, P, C, slope, dslope,
                                        ws, ws_bytes, s);
 }
+static bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 int hyres_attn_gate_fwd(const float* a, const float* b, const float* x, float* out, long long n, hyres_stream_t s) {
     HY_REQUIRE(a && b && x && out, HYRES_E_ARG, "attn_gate_fwd: NULL");
+    if (n % 4 == 0 && al16(a) && al16(b) && al16(x) && al16(out)) {
+        hipLaunchKernelGGL(attn_gate_fwd4_kernel, dim3(grid_for(n / 4)), dim3(256), 0, as_stream(s), a, b, x, out, n / 4);
+        return HY_LAUNCH_CHECK("attn_gate_fwd4");
+    }
     hipLaunchKernelGGL(attn_gate_fwd_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(s), a, b, x, out, n);
     return HY_LAUNCH_CHECK("attn_gate_fwd");
 }
@@ -597,9 +634,22 @@ int hyres_attn_gate_fwd_f16(const void* a, const void* b, const void* x, void* o
                        (const float*)b, (const float*)x, (float*)out, n / 4);
     return HY_LAUNCH_CHECK("attn_gate_fwd_f16");
 }
+int hyres_attn_gate_bwd_relu(const float* a, const float* b, const float* g, float* ga, float* gb, long long n,
+                             hyres_stream_t s) {
+    HY_REQUIRE(a && b && g && ga && gb && n % 4 == 0 && al16(a) && al16(b) && al16(g) && al16(ga) && al16(gb), HYRES_E_ARG,
+               "attn_gate_bwd_relu: NULL, n %% 4 != 0 or an operand not 16B-aligned");
+    hipLaunchKernelGGL(attn_gate_bwd4_kernel<true>, dim3(grid_for(n / 4)), dim3(256), 0, as_stream(s), a, b, g, ga, gb,
+                       n / 4);
+    return HY_LAUNCH_CHECK("attn_gate_bwd4");
+}
 int hyres_attn_gate_bwd(const float* a, const float* b, const float* g, float* ga, float* gb, long long n,
                         hyres_stream_t s) {
     HY_REQUIRE(a && b && g && ga && gb, HYRES_E_ARG, "attn_gate_bwd: NULL");
+    if (n % 4 == 0 && al16(a) && al16(b) && al16(g) && al16(ga) && al16(gb)) {
+        hipLaunchKernelGGL(attn_gate_bwd4_kernel<false>, dim3(grid_for(n / 4)), dim3(256), 0, as_stream(s), a, b, g, ga,
+                           gb, n / 4);
+        return HY_LAUNCH_CHECK("attn_gate_bwd4");
+    }
     hipLaunchKernelGGL((attn_gate_bwd_kernel<false, false>), dim3(grid_for(n)), dim3(256), 0, as_stream(s), a, b, g,
                        ga, gb, n);
     return HY_LAUNCH_CHECK("attn_gate_bwd");

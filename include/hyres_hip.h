@@ -317,6 +317,10 @@ int hyres_attn_gate_fwd(const float* a, const float* b, const float* x, float* o
 int hyres_attn_gate_fwd_f16(const void* a, const void* b, const void* x, void* out, long long n, hyres_stream_t s);
 int hyres_attn_gate_bwd(const float* a, const float* b, const float* g, float* ga, float* gb,
                         long long n, hyres_stream_t s);
+/* The same with the ReLU backward of a folded in (a = the last ResidualUnit's ReLU output, models/layers/attention.py:
+ * 11-30, 44-47): ga = (a > 0) ? g * sigmoid(b) : 0. n % 4 == 0, every operand 16B-aligned (round 6). */
+int hyres_attn_gate_bwd_relu(const float* a, const float* b, const float* g, float* ga, float* gb, long long n,
+                             hyres_stream_t s);
 /* Backward passes with fp16 SAVED activations (AMP training: the forward wrote y / pre / a, b / x / norm as
  * fp16; fp32 arithmetic; 8B-aligned fp16 operands): same semantics as the fp32 entry points of the same name
  * without the suffix. g16 = 1: the gradients in and out (g, gx / ga, gb) are fp16 as well — autocast's own

@@ -92,6 +92,8 @@ for ph in "$@"; do
            grep -h "sab=" gpurun_out/sabmicro.log > gpurun_out/${tag}_sab.txt
            bash scripts/tune_ab.sh $tag "default=" "nosab=HYRES_TUNE=21=0" || exit $? ;;
     ab8)   bash scripts/tune_ab.sh $tag "default=" "nodefer=HYRES_DEFER_ON_GRAD=0" || exit $? ;;
+    ab9)   scripts/gpu_run.sh "t9:300:python -u -m pytest tests/test_parity_gpu.py tests/test_amp_f16_act_gpu.py -x -v --timeout 180 --timeout-method thread -m gpu -k 'attn_gate or train or c2_size or attention or residual_unit'" || exit $?
+           bash scripts/serial_one.sh $tag || exit $? ;;
     *) echo "unknown phase $ph"; exit 2 ;;
   esac
 done

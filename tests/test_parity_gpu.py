@@ -543,6 +543,34 @@ def test_refine_input_se_prelu_fold_matches_unfused(monkeypatch):
         assert rel_err(g1[k], sd[k].grad) < (1e-3 if k == "act_in.weight" else TOL), k
 
 
+def test_attn_gate_float4_and_relu_fold():
+    """AttentionBlock's gate (models/layers/attention.py:44-47) on the round-6 float4 kernels: forward a * sigmoid(b) + x
+    and backward vs fp64 torch (1e-6), and the backward with the last ResidualUnit's ReLU folded in
+    (hyres_attn_gate_bwd_relu) equal bit for bit to the gate backward followed by the ReLU backward."""
+    from hyres_hip import _lib as L
+    D = dev()
+    P, C = 16 * 32 * 32, 192
+    a = torch.relu(_rand((P, C), 81)).to(D)
+    b = _rand((P, C), 82, 3.0).to(D)
+    x = _rand((P, C), 83).to(D)
+    g = _rand((P, C), 84).to(D)
+    out = torch.empty_like(a)
+    L.call("hyres_attn_gate_fwd", a.data_ptr(), b.data_ptr(), x.data_ptr(), out.data_ptr(), P * C, L.stream())
+    ga, gb, gam, gbm, gar = (torch.empty_like(a) for _ in range(5))
+    L.call("hyres_attn_gate_bwd", a.data_ptr(), b.data_ptr(), g.data_ptr(), ga.data_ptr(), gb.data_ptr(), P * C,
+           L.stream())
+    L.call("hyres_relu_bwd_2d", a.data_ptr(), C, ga.data_ptr(), C, gar.data_ptr(), C, P, C, L.stream())
+    L.call("hyres_attn_gate_bwd_relu", a.data_ptr(), b.data_ptr(), g.data_ptr(), gam.data_ptr(), gbm.data_ptr(), P * C,
+           L.stream())
+    torch.cuda.synchronize()
+    s = torch.sigmoid(b.double())
+    assert rel_err(out.double().cpu(), (a.double() * s + x.double()).cpu()) < 1e-6
+    assert rel_err(ga.double().cpu(), (g.double() * s).cpu()) < 1e-6
+    assert rel_err(gb.double().cpu(), (g.double() * a.double() * s * (1 - s)).cpu()) < 1e-6
+    assert torch.equal(gam, gar) and torch.equal(gbm, gb)
+    assert float((gam[a == 0]).abs().max()) == 0.0 and bool((a == 0).any())
+
+
 def test_prelu_mask_epilogue_refused_off_the_weight_resident_kernel():
     """HYRES_ACT_PRELU_MASK is implemented by conv3x3_wres_bf6_kernel only: a 1x1 input-gradient asking for it gets
     HYRES_E_ARG, nothing launched (the caller, ops.Node.prelu_mask_epilogue, checks the route first)."""
