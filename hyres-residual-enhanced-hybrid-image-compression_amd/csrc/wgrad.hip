@@ -2492,7 +2492,7 @@ static int wgrad_issue(const hyres_wgrad_desc* d0, const float* pp, const float*
         else if (io == 2) halo16g(std::integral_constant<int, 2>{});
         else if (io == 3) halo16g(std::integral_constant<int, 3>{});
         else halo16g(std::integral_constant<int, 0>{});
-    } else if (p.halo && f32_gemm_bf6() && g_tune[16] == 2 && p.NT == 3 &&
+    } else if (p.halo && f32_gemm_bf6() && g_tune[16] == 2 && (p.NT == 3 || (p.NT == 5 && g_tune[22] != 0)) &&
                (long long)d->B * d->Hqq * d->Wqq * d->ldq * 4 < 0x7FFFFFF0LL &&
                (long long)d->B * d->Hq * d->Wq * d->ldp * 4 < 0x7FFFFFF0LL) {  // loads two chunks ahead (key 16 = 2)
         if (p.hk == 3 && p.hdil == 2)

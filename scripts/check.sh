@@ -94,6 +94,10 @@ for ph in "$@"; do
     ab8)   bash scripts/tune_ab.sh $tag "default=" "nodefer=HYRES_DEFER_ON_GRAD=0" || exit $? ;;
     ab9)   scripts/gpu_run.sh "t9:300:python -u -m pytest tests/test_parity_gpu.py tests/test_amp_f16_act_gpu.py -x -v --timeout 180 --timeout-method thread -m gpu -k 'attn_gate or train or c2_size or attention or residual_unit'" || exit $?
            bash scripts/serial_one.sh $tag || exit $? ;;
+    wg5)   scripts/gpu_run.sh "wg5test:300:python -u -m pytest tests/test_bf6_gpu.py -x -v --timeout 180 --timeout-method thread -m gpu -k prefetch2" \
+             "wg5:300:for s in '--H 128 --Ci 128 --Co 128 --K 5 --stride 2' '--H 64 --Ci 128 --Co 192 --K 5 --stride 2' '--H 32 --Ci 192 --Co 384 --K 5' '--H 16 --Ci 192 --Co 128 --K 5 --stride 2'; do python3 scripts/wgrad_micro.py \$s --ab 22=0,1,0,1; done" || exit $?
+           grep -h "key22" gpurun_out/wg5.log > gpurun_out/${tag}_wg5.txt
+           bash scripts/tune_ab.sh $tag "default=" "nowg5=HYRES_TUNE=22=0" || exit $? ;;
     *) echo "unknown phase $ph"; exit 2 ;;
   esac
 done

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--Co", type=int, default=128)
     ap.add_argument("--K", type=int, default=1)
     ap.add_argument("--dil", type=int, default=1)
+    ap.add_argument("--stride", type=int, default=1)
     ap.add_argument("--f16", action="store_true", help="AMP: fp16 operands (f16 MFMA)")
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--ab", default=None, help="key=v1,v2: time each value of hyres_conv_tuning key and compare the "
@@ -30,11 +31,11 @@ def main():
     from hyres_hip import _lib as L
     dev = torch.device("cuda:0")
     x = torch.randn(a.B, a.H, a.H, a.Ci, device=dev)
-    gy = torch.randn(a.B, a.H, a.H, a.Co, device=dev)
+    gy = torch.randn(a.B, a.H // a.stride, a.H // a.stride, a.Co, device=dev)
     dw = torch.zeros(a.Co, a.Ci, a.K, a.K, device=dev)
     db = torch.zeros(a.Co, device=dev)
     d = L.WgradDesc()
-    L.call("hyres_wgrad_desc_conv2d", ctypes.byref(d), a.B, a.H, a.H, a.Ci, a.Ci, a.Co, a.Co, a.K, a.K, 1, a.dil * (a.K // 2), a.dil)
+    L.call("hyres_wgrad_desc_conv2d", ctypes.byref(d), a.B, a.H, a.H, a.Ci, a.Ci, a.Co, a.Co, a.K, a.K, a.stride, a.dil * (a.K // 2), a.dil)
     d.f16_operands = int(a.f16)
     d.sm = a.Ci * a.K * a.K
     nb = L.load().hyres_wgrad_workspace_bytes(ctypes.byref(d))

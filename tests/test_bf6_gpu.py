@@ -664,15 +664,17 @@ def test_wres_bf6_dilation2_matches_fp64(B, H, W, act):
     assert eg[1] < 1e-5 and eg[1] <= 2 * eg[0] + 1e-9
 
 
-@pytest.mark.parametrize("K,B,H,W,Ci,Co,key", [
-    (1, 2, 30, 30, 96, 160, 15),    # 1x1: ragged pixel chunks (1800 px) and channel tiles
-    (1, 4, 64, 64, 64, 128, 15),
-    (1, 2, 128, 128, 128, 64, 15),
-    (3, 2, 64, 64, 64, 64, 16),     # 3x3 rows of taps on the halo kernel
-    (3, 3, 32, 96, 96, 96, 16),     # 96 channels: a partial 64-wide tile
-    (3, 2, 128, 128, 64, 128, 16),
+@pytest.mark.parametrize("K,B,H,W,Ci,Co,key,S", [
+    (1, 2, 30, 30, 96, 160, 15, 1),    # 1x1: ragged pixel chunks (1800 px) and channel tiles
+    (1, 4, 64, 64, 64, 128, 15, 1),
+    (1, 2, 128, 128, 128, 64, 15, 1),
+    (3, 2, 64, 64, 64, 64, 16, 1),     # 3x3 rows of taps on the halo kernel
+    (3, 3, 32, 96, 96, 96, 16, 1),     # 96 channels: a partial 64-wide tile
+    (3, 2, 128, 128, 64, 128, 16, 1),
+    (5, 2, 64, 64, 128, 128, 16, 2),   # round 6: 5-tap rows, stride 2 (g_a / h_a's 5x5 s2 convs)
+    (5, 2, 32, 32, 96, 96, 16, 1),     # 5-tap rows, stride 1 (the masked 5x5 context conv's shape)
 ])
-def test_wgrad_prefetch2_kernels_bit_identical(K, B, H, W, Ci, Co, key):
+def test_wgrad_prefetch2_kernels_bit_identical(K, B, H, W, Ci, Co, key, S):
     """wgrad1x1_bf6_pf2_kernel (hyres_conv_tuning key 15) and wgrad_halo_bf6_pf2_kernel (key 16): operand loads two
     32-pixel chunks ahead through unconditional buffer loads — the same products in the same order as the one-ahead
     kernels, so weight and bias gradients are equal bit for bit (ragged chunks and tiles included), and within fp32
@@ -682,9 +684,9 @@ def test_wgrad_prefetch2_kernels_bit_identical(K, B, H, W, Ci, Co, key):
     D = dev()
     g = torch.Generator().manual_seed(5)
     x = (torch.rand((B, H, W, Ci), generator=g) * 2 - 1).to(D)
-    gy = (torch.rand((B, H, W, Co), generator=g) * 2 - 1).to(D)
+    gy = (torch.rand((B, H // S, W // S, Co), generator=g) * 2 - 1).to(D)
     d = L.WgradDesc()
-    L.call("hyres_wgrad_desc_conv2d", ctypes.byref(d), B, H, W, Ci, Ci, Co, Co, K, K, 1, K // 2, 1)
+    L.call("hyres_wgrad_desc_conv2d", ctypes.byref(d), B, H, W, Ci, Ci, Co, Co, K, K, S, K // 2, 1)
     d.sm = Ci * K * K
     nb = L.load().hyres_wgrad_workspace_bytes(ctypes.byref(d))
     ws = torch.empty(nb // 4 + 16, device=D)
@@ -706,7 +708,7 @@ def test_wgrad_prefetch2_kernels_bit_identical(K, B, H, W, Ci, Co, key):
     assert torch.equal(res[1][0], res[2][0]) and torch.equal(res[1][1], res[2][1])
     xr = x.cpu().double().permute(0, 3, 1, 2)
     gr = gy.cpu().double().permute(0, 3, 1, 2)
-    ref = torch.nn.grad.conv2d_weight(xr, (Co, Ci, K, K), gr, padding=K // 2)
+    ref = torch.nn.grad.conv2d_weight(xr, (Co, Ci, K, K), gr, stride=S, padding=K // 2)
     err = float((res[2][0].double() - ref).abs().max() / ref.abs().max())
     assert err < 1e-5, err
     assert float((res[2][1].double() - gr.sum((0, 2, 3))).abs().max()) < 1e-3
