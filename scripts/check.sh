@@ -98,6 +98,8 @@ for ph in "$@"; do
              "wg5:300:for s in '--H 128 --Ci 128 --Co 128 --K 5 --stride 2' '--H 64 --Ci 128 --Co 192 --K 5 --stride 2' '--H 32 --Ci 192 --Co 384 --K 5' '--H 16 --Ci 192 --Co 128 --K 5 --stride 2'; do python3 scripts/wgrad_micro.py \$s --ab 22=0,1,0,1; done" || exit $?
            grep -h "key22" gpurun_out/wg5.log > gpurun_out/${tag}_wg5.txt
            bash scripts/tune_ab.sh $tag "default=" "nowg5=HYRES_TUNE=22=0" || exit $? ;;
+    tiledc) scripts/gpu_run.sh "tiledc:400:for t in -1 0 1 3 4; do for s in '--H 64 --Ci 128 --Co 128 --deconv' '--H 32 --Ci 192 --Co 128 --deconv' '--H 16 --Ci 128 --Co 128 --deconv' '--H 8 --Ci 128 --Co 128 --deconv'; do python3 scripts/conv_micro.py \$s --bf6 --tile \$t | sed \"s/^/tile \$t /\"; done; done" || exit $?
+           grep -h "us" gpurun_out/tiledc.log > gpurun_out/${tag}_tiledc.txt ;;
     *) echo "unknown phase $ph"; exit 2 ;;
   esac
 done

@@ -35,6 +35,7 @@ def main():
                     help="bf16x6 fp32 1x1 on the tiled kernel (hyres_conv_tuning key 10 = 0)")
     ap.add_argument("--stream-cm", type=int, default=1,
                     help="streaming bf16x6 1x1 access mode (hyres_conv_tuning key 11: 0 MFMA layout, 1 LDS-staged epilogue)")
+    ap.add_argument("--deconv", action="store_true", help="compressai deconv (ConvTranspose2d k5 s2 p2 op1, 4 phases)")
     ap.add_argument("--wres-v", type=int, default=0, help="conv3x3_wres_bf6_kernel variant (hyres_conv_tuning key 12)")
     a = ap.parse_args()
     from hyres_hip import _lib as L
@@ -78,6 +79,22 @@ def main():
         byts = 4.0 * a.B * a.H * a.H * (a.Ci + 2 * a.Co)
         print(f"conv B{a.B} {a.H}x{a.H}x{a.Ci} -> {a.H}x{a.H}x{a.Co} K1 +mask{' bf16x6' if a.bf6 else ''}: {us:.1f} us, "
               f"{2.0 * a.B * a.H * a.H * a.Ci * a.Co / us / 1e6:.1f} TFLOP/s, {byts / us / 1e3:.0f} GB/s")
+        return
+    if a.deconv:
+        wd = torch.randn(a.Ci, a.Co, 5, 5, device=dev) / (a.Ci * 25) ** 0.5
+        for _ in range(3):
+            y = O.deconv2d(None, x, wd, b)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(a.iters):
+            y = O.deconv2d(None, x, wd, b, out=y)
+        e1.record()
+        torch.cuda.synchronize()
+        us = 1000 * e0.elapsed_time(e1) / a.iters
+        flops = 2.0 * a.B * a.H * a.H * 25 * a.Ci * a.Co
+        print(f"deconv B{a.B} {a.H}x{a.H}x{a.Ci} -> {2 * a.H}x{2 * a.H}x{a.Co} K5{' bf16x6' if a.bf6 else ''}: {us:.1f} us, "
+              f"{flops / us / 1e6:.1f} TFLOP/s")
         return
     ctx = torch.autocast("cuda", dtype=torch.float16) if a.f16 else torch.autocast("cuda", enabled=False)
     import contextlib
