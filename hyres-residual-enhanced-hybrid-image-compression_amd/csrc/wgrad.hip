@@ -1814,7 +1814,7 @@ constexpr int THIN_STAGE = (THIN_ROWS * THIN_COLS + 255) / 256;  // staged windo
 
 template <int MW, int NC, int TG, int SQ, bool PH = false>  // PH: P (the wide operand) fp16 in HBM
 __global__ __launch_bounds__(256) void wgrad_thin_kernel(const WgradArgs a, int rpb, int dhmin, int dwmin, int nrow,
-                                                         int ncol) {
+                                                         int ncol, int win) {
     constexpr int PCH = 64 / MW;            // pixels per P chunk (PCH x 64*MW floats = 16 KB)
     constexpr int PV = PCH * 16 * MW / 256;  // float4 per thread per chunk
     constexpr int PPW = PCH / 4;             // pixels per wave per chunk
@@ -1891,6 +1891,55 @@ __global__ __launch_bounds__(256) void wgrad_thin_kernel(const WgradArgs a, int 
             for (int k = 0; k < PV; ++k) *reinterpret_cast<float4*>(&Ps[4 * (tid + 256 * k)]) = q2f(pr4[k]);
             __syncthreads();
             if (c0 + PCH < d.Wq) load_chunk(c0 + PCH);  // next chunk in flight during this chunk's FMAs
+            if constexpr (MW == 1 && TG == 9 && SQ == 1) {
+                // win = 1: one group of the 3x3 taps in row-major order, 2: the same reversed (the swapped descriptor of
+                // the 64 -> 3 convs: dh, dw negated); host-checked, Wq <= 256
+                auto window = [&](auto REVC) {
+                    constexpr bool REV = decltype(REVC)::value;
+                    // round 6: the 3 x 3 Q window of the wave's current pixel in registers, sliding one column per
+                    // pixel (3 LDS reads per pixel instead of 9: the per-tap broadcast reads and their waits were the
+                    // limit, profiles/r6y_pmc_families.txt); logical column c of pixel uu sits in slot (c + uu) % 3.
+                    // Same FMAs per accumulator in the same pixel order: bit-identical
+                    const int jb = c0 + wave * PPW;
+                    float4 qw[3][3];
+#pragma unroll
+                    for (int r = 0; r < 3; ++r)
+#pragma unroll
+                        for (int c = 0; c < 3; ++c)
+                            qw[r][c] = *reinterpret_cast<const float4*>(Qs + (r * THIN_COLS + jb + c) * 4);
+#pragma unroll
+                    for (int uu = 0; uu < PPW; ++uu) {
+                        if (jb + uu < d.Wq) {  // wave-uniform
+                            const float pv = Ps[(wave * PPW + uu) * 64 + lane];
+#pragma unroll
+                            for (int r = 0; r < 3; ++r)
+#pragma unroll
+                                for (int c = 0; c < 3; ++c) {
+                                    const float4 q = qw[r][(c + uu) % 3];
+                                    float4& A = acc[0][REV ? 8 - (r * 3 + c) : r * 3 + c];
+                                    A.x = fmaf(pv, q.x, A.x);
+                                    if (NC > 1) A.y = fmaf(pv, q.y, A.y);
+                                    if (NC > 2) A.z = fmaf(pv, q.z, A.z);
+                                    if (NC > 3) A.w = fmaf(pv, q.w, A.w);
+                                }
+                            bsum[0] += pv;
+                        }
+                        if (uu + 1 < PPW) {
+#pragma unroll
+                            for (int r = 0; r < 3; ++r)
+                                qw[r][uu % 3] = *reinterpret_cast<const float4*>(Qs + (r * THIN_COLS + jb + uu + 3) * 4);
+                        }
+                    }
+                };
+                if (win == 1) {  // block-uniform
+                    window(std::false_type{});
+                    continue;
+                }
+                if (win == 2) {
+                    window(std::true_type{});
+                    continue;
+                }
+            }
 #pragma unroll 2
             for (int uu = 0; uu < PPW; ++uu) {
                 const int pl = wave * PPW + uu;
@@ -2282,7 +2331,7 @@ __global__ void half_to_float_2d_kernel(const _Float16* src, int ld, float* dst,
 
 // thin-operand weight-gradient plan (wgrad_thin_kernel): N <= 4, M in {64, 128}, the staged Q window fits
 struct ThinPlan {
-    int mw, nc, tg, ngroups, rpb, nblk, dhmin, dwmin, nrow, ncol, sq;
+    int mw, nc, tg, ngroups, rpb, nblk, dhmin, dwmin, nrow, ncol, sq, win;
 };
 
 static bool thin_plan(const hyres_wgrad_desc* d, ThinPlan* tp) {
@@ -2307,6 +2356,14 @@ static bool thin_plan(const hyres_wgrad_desc* d, ThinPlan* tp) {
     const int R = d->B * d->Hq;
     p.rpb = std::max(1, ceil_div(R * p.ngroups, 1024));  // ~1024 blocks (4 per CU)
     p.nblk = ceil_div(R, p.rpb);
+    // the sliding-window loop (hyres_conv_tuning key 23, default 1): the 3x3 taps in row-major order, one group
+    const bool w3 = g_tune[23] != 0 && p.mw == 1 && p.tg == 9 && p.sq == 1 && d->ntaps == 9 && d->Wq <= 256;
+    bool fwd = w3, rev = w3;
+    for (int t = 0; t < 9 && w3; ++t) {
+        fwd = fwd && d->dh[t] == t / 3 - 1 && d->dw[t] == t % 3 - 1;
+        rev = rev && d->dh[t] == 1 - t / 3 && d->dw[t] == 1 - t % 3;
+    }
+    p.win = fwd ? 1 : rev ? 2 : 0;
     *tp = p;
     return true;
 }
@@ -2317,14 +2374,14 @@ static void launch_thin(const WgradArgs& a, const ThinPlan& p, bool ph, hipStrea
         constexpr int MW_ = decltype(mw)::value, NC_ = decltype(nc)::value, TG_ = decltype(tg)::value;
         if (p.sq == 1) {
             if (ph) hipLaunchKernelGGL((wgrad_thin_kernel<MW_, NC_, TG_, 1, true>), grid, dim3(256), 0, st, a, p.rpb,
-                                       p.dhmin, p.dwmin, p.nrow, p.ncol);
+                                       p.dhmin, p.dwmin, p.nrow, p.ncol, p.win);
             else hipLaunchKernelGGL((wgrad_thin_kernel<MW_, NC_, TG_, 1>), grid, dim3(256), 0, st, a, p.rpb, p.dhmin,
-                                    p.dwmin, p.nrow, p.ncol);
+                                    p.dwmin, p.nrow, p.ncol, p.win);
         } else {
             if (ph) hipLaunchKernelGGL((wgrad_thin_kernel<MW_, NC_, TG_, 2, true>), grid, dim3(256), 0, st, a, p.rpb,
-                                       p.dhmin, p.dwmin, p.nrow, p.ncol);
+                                       p.dhmin, p.dwmin, p.nrow, p.ncol, p.win);
             else hipLaunchKernelGGL((wgrad_thin_kernel<MW_, NC_, TG_, 2>), grid, dim3(256), 0, st, a, p.rpb, p.dhmin,
-                                    p.dwmin, p.nrow, p.ncol);
+                                    p.dwmin, p.nrow, p.ncol, p.win);
         }
     };
     using I1 = std::integral_constant<int, 1>;

@@ -217,7 +217,9 @@ int hyres_conv_plan(const hyres_conv_geom* g, const hyres_epilogue* e, int* tile
 #define HYRES_TUNE_WGRAD_HALO5_PF 22  /* 1: the 5-tap-row halo weight gradients (5x5, stride 1 / 2) also on the two-chunks-
                                        * ahead kernel (with key 16 = 2; bit-identical); 0 (default): one chunk ahead — no
                                        * gain per launch or in the step (profiles/r6v_wg5.txt, r6v_wg5_step_ab.txt) */
-#define HYRES_TUNE_KEYS 24            /* key 23 reserved */
+#define HYRES_TUNE_THIN_WINDOW 23     /* 1 (default): the thin (3-channel) 3x3 weight gradients keep each pixel's 3 x 3 Q window
+                                       * in registers, sliding one column per pixel (bit-identical); 0: nine LDS reads per pixel */
+#define HYRES_TUNE_KEYS 24
 int hyres_conv_tuning(int key, int value, int* old);
 
 /* Weight gradient:  dW[t][m][n] = sum_q P[q][m] * Q[shift_t(q)][n]  over a base grid q (B,Hq,Wq).

@@ -100,6 +100,10 @@ for ph in "$@"; do
            bash scripts/tune_ab.sh $tag "default=" "nowg5=HYRES_TUNE=22=0" || exit $? ;;
     tiledc) scripts/gpu_run.sh "tiledc:400:for t in -1 0 1 3 4; do for s in '--H 64 --Ci 128 --Co 128 --deconv' '--H 32 --Ci 192 --Co 128 --deconv' '--H 16 --Ci 128 --Co 128 --deconv' '--H 8 --Ci 128 --Co 128 --deconv'; do python3 scripts/conv_micro.py \$s --bf6 --tile \$t | sed \"s/^/tile \$t /\"; done; done" || exit $?
            grep -h "us" gpurun_out/tiledc.log > gpurun_out/${tag}_tiledc.txt ;;
+    thinpmc) bash scripts/pmc_families.sh $tag thin || exit $? ;;
+    thin)  scripts/gpu_run.sh "thintest:300:python -u -m pytest tests/test_bf6_gpu.py -x -v --timeout 180 --timeout-method thread -m gpu -k thin_window" \
+             "thinmicro:300:for s in '--H 256 --Ci 3 --Co 64 --K 3' '--H 256 --Ci 64 --Co 3 --K 3'; do python3 scripts/wgrad_micro.py \$s --ab 23=0,1,0,1; done" || exit $?
+           grep -h "key23" gpurun_out/thinmicro.log > gpurun_out/${tag}_thin.txt ;;
     *) echo "unknown phase $ph"; exit 2 ;;
   esac
 done

@@ -25,6 +25,12 @@ fam() {  # name kernel-substring micro-args... (MICRO=scripts/wgrad_micro.py for
     python3 -c "import json,sys; d=json.load(sys.stdin); print('  kernel', d['kernel'][:70]); print('  HBM bytes per launch (2 x FETCH + WRITE)', round(d['traffic_bytes_per_launch'] / 1e6, 2), 'MB')" >> $out
   python3 scripts/pmc_sq.py ${d}_sq --kernel "$k" >> $out
 }
+if [ "$2" = thin ]; then  # the image-side thin weight gradients (wgrad_thin_kernel)
+  MICRO=scripts/wgrad_micro.py fam thin_3to64 wgrad_thin --H 256 --Ci 3 --Co 64 --K 3 &&
+  MICRO=scripts/wgrad_micro.py fam thin_64to3 wgrad_thin --H 256 --Ci 64 --Co 3 --K 3 &&
+  MICRO=scripts/wgrad_micro.py fam thin_5x5s2 wgrad_thin --H 256 --Ci 3 --Co 128 --K 5 --stride 2
+  exit $?
+fi
 MICRO=scripts/wgrad_micro.py fam wg_halo_128 wgrad_halo_bf6 --H 128 --Ci 64 --Co 64 --K 3 &&
 MICRO=scripts/wgrad_micro.py fam wg_1x1_128 wgrad1x1_bf6 --H 128 --Ci 128 --Co 128 --K 1 &&
 fam b6_32_3x3 conv_fwd_b6_kernel --H 32 --Ci 96 --Co 96 --K 3 --relu --bf6 &&

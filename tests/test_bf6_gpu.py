@@ -753,3 +753,38 @@ def test_bf6_implicit_gemm_staging_variants_bit_identical(B, H, Ci, Co, K, strid
     for db, sw in ((1, 1), (0, 1)):
         got = run(db, sw)
         assert torch.equal(ref, got), (db, sw, float((ref - got).abs().max()))
+
+
+@pytest.mark.parametrize("B,H,W,Ci,Co", [(2, 64, 96, 3, 64), (2, 48, 256, 64, 3), (1, 37, 200, 3, 64)])
+def test_wgrad_thin_window_bit_identical(B, H, W, Ci, Co):
+    """wgrad_thin_kernel's sliding 3x3 Q window (round 6, hyres_conv_tuning key 23): the same FMAs per accumulator in
+    the same pixel order as the nine-reads-per-pixel loop, so the weight and bias gradients of the image-side 3x3 convs
+    (MultiScaleRefine's conv_in 3 -> 64 and its output conv 64 -> 3, through the swapped descriptor) are equal bit for
+    bit, on ragged widths (a partial last 64-pixel chunk), and within 1e-5 of fp64."""
+    import ctypes
+    from hyres_hip import _lib as L
+    D = dev()
+    g = torch.Generator().manual_seed(9)
+    x = (torch.rand((B, H, W, Ci), generator=g) * 2 - 1).to(D)
+    gy = (torch.rand((B, H, W, Co), generator=g) * 2 - 1).to(D)
+    d = L.WgradDesc()
+    L.call("hyres_wgrad_desc_conv2d", ctypes.byref(d), B, H, W, Ci, Ci, Co, Co, 3, 3, 1, 1, 1)
+    d.sm = Ci * 9
+    nb = L.load().hyres_wgrad_workspace_bytes(ctypes.byref(d))
+    ws = torch.empty(nb // 4 + 16, device=D)
+    res = {}
+    try:
+        for v in (0, 1):
+            L.call("hyres_conv_tuning", 23, v, None)
+            dw = torch.zeros((Co, Ci, 3, 3), device=D)
+            db = torch.zeros((Co,), device=D)
+            L.call("hyres_conv_wgrad", ctypes.byref(d), gy.data_ptr(), x.data_ptr(), dw.data_ptr(), db.data_ptr(),
+                   ws.data_ptr(), nb, L.stream())
+            torch.cuda.synchronize()
+            res[v] = (dw.cpu(), db.cpu())
+    finally:
+        L.call("hyres_conv_tuning", 23, 1, None)
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    ref = torch.nn.grad.conv2d_weight(x.cpu().double().permute(0, 3, 1, 2), (Co, Ci, 3, 3),
+                                      gy.cpu().double().permute(0, 3, 1, 2), padding=1)
+    assert float((res[1][0].double() - ref).abs().max() / ref.abs().max()) < 1e-5
