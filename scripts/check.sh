@@ -104,6 +104,7 @@ for ph in "$@"; do
     thin)  scripts/gpu_run.sh "thintest:300:python -u -m pytest tests/test_bf6_gpu.py -x -v --timeout 180 --timeout-method thread -m gpu -k thin_window" \
              "thinmicro:300:for s in '--H 256 --Ci 3 --Co 64 --K 3' '--H 256 --Ci 64 --Co 3 --K 3'; do python3 scripts/wgrad_micro.py \$s --ab 23=0,1,0,1; done" || exit $?
            grep -h "key23" gpurun_out/thinmicro.log > gpurun_out/${tag}_thin.txt ;;
+    serialamp) bash scripts/serial_one.sh ${tag}amp --amp || exit $? ;;
     *) echo "unknown phase $ph"; exit 2 ;;
   esac
 done

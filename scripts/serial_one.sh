@@ -3,10 +3,11 @@
 # full per-kernel list -> gpurun_out/<tag>_train_serial_full.txt
 set -o pipefail
 tag=${1:-serial}
+extra=$2   # e.g. --amp
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/${tag}_serial1 -o run -- \
-  python3 scripts/step_profile.py --marker --serial --steps 10 > gpurun_out/${tag}_serial1.log 2>&1 || exit $?
+  python3 scripts/step_profile.py --marker --serial --steps 10 $extra > gpurun_out/${tag}_serial1.log 2>&1 || exit $?
 python3 - "$tag" <<'PY'
 import sys
 sys.path.insert(0, "scripts")
