@@ -102,7 +102,7 @@ for ph in "$@"; do
            grep -h "us" gpurun_out/tiledc.log > gpurun_out/${tag}_tiledc.txt ;;
     thinpmc) bash scripts/pmc_families.sh $tag thin || exit $? ;;
     thin)  scripts/gpu_run.sh "thintest:300:python -u -m pytest tests/test_bf6_gpu.py -x -v --timeout 180 --timeout-method thread -m gpu -k thin_window" \
-             "thinmicro:300:for s in '--H 256 --Ci 3 --Co 64 --K 3' '--H 256 --Ci 64 --Co 3 --K 3'; do python3 scripts/wgrad_micro.py \$s --ab 23=0,1,0,1; done" || exit $?
+             "thinmicro:300:for s in '--H 256 --Ci 3 --Co 64 --K 3' '--H 256 --Ci 64 --Co 3 --K 3' '--H 256 --Ci 3 --Co 128 --K 5 --stride 2'; do python3 scripts/wgrad_micro.py \$s --ab 23=0,1,0,1; done" || exit $?
            grep -h "key23" gpurun_out/thinmicro.log > gpurun_out/${tag}_thin.txt ;;
     serialamp) bash scripts/serial_one.sh ${tag}amp --amp || exit $? ;;
     tileh) scripts/gpu_run.sh "tileh:400:for t in -1 0 1 3 4; do for s in '--H 32 --Ci 96 --Co 96 --K 3 --relu' '--H 32 --Ci 192 --Co 96 --K 1 --relu' '--H 32 --Ci 96 --Co 192 --K 1 --res --relu' '--H 32 --Ci 384 --Co 192 --K 3 --relu' '--H 32 --Ci 640 --Co 512 --K 1' '--H 64 --Ci 128 --Co 192 --K 5 --stride 2'; do python3 scripts/conv_micro.py \$s --f16 --tile \$t | sed \"s/^/tile \$t /\"; done; done" || exit $?
