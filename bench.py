@@ -602,16 +602,14 @@ def main():
     opt = FusedAdam(main_p, lr=3e-4, max_grad_norm=1.0)
     aux_opt = FusedAdam(aux_p, lr=3e-4)
     reducer = None
-    # N > 1: the captured forward/backward graph replays, then the flat gradients are all-reduced in two
-    # 32 MB RCCL buckets (measured at N=1: 44.5 ms graph vs 49 ms for the eager step whose all-reduce
-    # overlaps backward — the eager host enqueue costs more than an unoverlapped 41.5 MB all-reduce over
-    # xGMI). HYRES_DIST_MODE=eager-overlap (or --no-graph) selects the eager overlapped path.
+    # N > 1: the captured forward/backward replays on every rank and the flat gradient is all-reduced over
+    # RCCL; HYRES_DIST_MODE=eager-overlap (or --no-graph) selects the eager step with overlapped collectives.
     dist_mode = None
     if dist:
-        # default "graph+allreduce": replay, then the flat gradient in 32 MB buckets; "eager-overlap": the eager
-        # step with each gradient segment's all-reduce started at its backward-progress marker. (The round-3/4
-        # "graph+overlap" mode — collectives started from events recorded inside the replay — was removed in
-        # round 5: it needs more live streams than the 4 hardware queues per process)
+        # default "graph+overlap" (round 6): the step captured as two graphs cut at the "hyper" backward marker, the
+        # finished refine / g_s / hyperprior segments' all-reduce launched between the two replays (no event node
+        # inside a graph, no extra stream); "graph+allreduce": one replay, then the whole flat gradient;
+        # "eager-overlap": the eager step with each segment's all-reduce started at its backward-progress marker
         dist_mode = "eager-overlap" if args.no_graph else os.environ.get("HYRES_DIST_MODE", DIST_DEFAULT)
         assert dist_mode in ("eager-overlap", "graph+allreduce", "graph+overlap"), dist_mode
     if dist:
