@@ -144,11 +144,12 @@ __global__ __launch_bounds__(256) void attn_gate_fwd4_kernel(const float* a, con
             make_float4(av.x * s[0] + xv.x, av.y * s[1] + xv.y, av.z * s[2] + xv.z, av.w * s[3] + xv.w);
     }
 }
-template <bool MASK>
+// H: a, b fp16 (AMP's saved activations); G: g, ga, gb fp16 (AMP's fp16 gradients) — as attn_gate_bwd_kernel<H, G>
+template <bool H, bool G, bool MASK>
 __global__ __launch_bounds__(256) void attn_gate_bwd4_kernel(const float* a, const float* b, const float* g, float* ga,
                                                              float* gb, long long n4) {
     for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
-        const float4 av4 = ld4(a + 4 * i), bv4 = ld4(b + 4 * i), gv4 = ld4(g + 4 * i);
+        const float4 av4 = ldv4<H>(a, 4 * i), bv4 = ldv4<H>(b, 4 * i), gv4 = ldv4<G>(g, 4 * i);
         const float av[4] = {av4.x, av4.y, av4.z, av4.w}, bv[4] = {bv4.x, bv4.y, bv4.z, bv4.w};
         const float gv[4] = {gv4.x, gv4.y, gv4.z, gv4.w};
         float oa[4], ob[4];
@@ -159,8 +160,8 @@ __global__ __launch_bounds__(256) void attn_gate_bwd4_kernel(const float* a, con
             if constexpr (MASK) oa[c] = av[c] > 0.f ? oa[c] : 0.f;
             ob[c] = gv[c] * av[c] * s * (1.0f - s);
         }
-        *reinterpret_cast<float4*>(ga + 4 * i) = make_float4(oa[0], oa[1], oa[2], oa[3]);
-        *reinterpret_cast<float4*>(gb + 4 * i) = make_float4(ob[0], ob[1], ob[2], ob[3]);
+        stv4<G>(ga, 4 * i, make_float4(oa[0], oa[1], oa[2], oa[3]));
+        stv4<G>(gb, 4 * i, make_float4(ob[0], ob[1], ob[2], ob[3]));
     }
 }
 // fp16 activations (autocast inference): a, b, x, out fp16, 4 elements per thread, fp32 arithmetic
@@ -638,25 +639,55 @@ int hyres_attn_gate_bwd_relu(const float* a, const float* b, const float* g, flo
                              hyres_stream_t s) {
     HY_REQUIRE(a && b && g && ga && gb && n % 4 == 0 && al16(a) && al16(b) && al16(g) && al16(ga) && al16(gb), HYRES_E_ARG,
                "attn_gate_bwd_relu: NULL, n %% 4 != 0 or an operand not 16B-aligned");
-    hipLaunchKernelGGL(attn_gate_bwd4_kernel<true>, dim3(grid_for(n / 4)), dim3(256), 0, as_stream(s), a, b, g, ga, gb,
-                       n / 4);
+    hipLaunchKernelGGL((attn_gate_bwd4_kernel<false, false, true>), dim3(grid_for(n / 4)), dim3(256), 0, as_stream(s), a,
+                       b, g, ga, gb, n / 4);
     return HY_LAUNCH_CHECK("attn_gate_bwd4");
 }
 int hyres_attn_gate_bwd(const float* a, const float* b, const float* g, float* ga, float* gb, long long n,
                         hyres_stream_t s) {
     HY_REQUIRE(a && b && g && ga && gb, HYRES_E_ARG, "attn_gate_bwd: NULL");
     if (n % 4 == 0 && al16(a) && al16(b) && al16(g) && al16(ga) && al16(gb)) {
-        hipLaunchKernelGGL(attn_gate_bwd4_kernel<false>, dim3(grid_for(n / 4)), dim3(256), 0, as_stream(s), a, b, g, ga,
-                           gb, n / 4);
+        hipLaunchKernelGGL((attn_gate_bwd4_kernel<false, false, false>), dim3(grid_for(n / 4)), dim3(256), 0, as_stream(s),
+                           a, b, g, ga, gb, n / 4);
         return HY_LAUNCH_CHECK("attn_gate_bwd4");
     }
     hipLaunchKernelGGL((attn_gate_bwd_kernel<false, false>), dim3(grid_for(n)), dim3(256), 0, as_stream(s), a, b, g,
                        ga, gb, n);
     return HY_LAUNCH_CHECK("attn_gate_bwd");
 }
+static bool al8(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 7u) == 0; }
+// the vector path of the fp16-activation gate backward: n % 4 == 0, fp16 operands 8B-aligned, fp32 ones 16B-aligned
+static bool gate_f16_vec(const void* a, const void* b, const void* g, const void* ga, const void* gb, long long n,
+                         int g16) {
+    auto gal = [&](const void* p) { return g16 ? al8(p) : al16(p); };
+    return n % 4 == 0 && al8(a) && al8(b) && gal(g) && gal(ga) && gal(gb);
+}
+extern "C++" {
+template <bool MASK>
+static void launch_gate_bwd4h(const void* a, const void* b, const void* g, void* ga, void* gb, long long n, int g16,
+                              hipStream_t st) {
+    if (g16)
+        hipLaunchKernelGGL((attn_gate_bwd4_kernel<true, true, MASK>), dim3(grid_for(n / 4)), dim3(256), 0, st,
+                           (const float*)a, (const float*)b, (const float*)g, (float*)ga, (float*)gb, n / 4);
+    else
+        hipLaunchKernelGGL((attn_gate_bwd4_kernel<true, false, MASK>), dim3(grid_for(n / 4)), dim3(256), 0, st,
+                           (const float*)a, (const float*)b, (const float*)g, (float*)ga, (float*)gb, n / 4);
+}
+}  // extern "C++"
+int hyres_attn_gate_bwd_relu_f16(const void* a, const void* b, const void* g, void* ga, void* gb, long long n, int g16,
+                                 hyres_stream_t s) {
+    HY_REQUIRE(a && b && g && ga && gb && gate_f16_vec(a, b, g, ga, gb, n, g16), HYRES_E_ARG,
+               "attn_gate_bwd_relu_f16: NULL, n %% 4 != 0 or a misaligned operand");
+    launch_gate_bwd4h<true>(a, b, g, ga, gb, n, g16, as_stream(s));
+    return HY_LAUNCH_CHECK("attn_gate_bwd4h");
+}
 int hyres_attn_gate_bwd_f16(const void* a, const void* b, const void* g, void* ga, void* gb, long long n, int g16,
                             hyres_stream_t s) {
     HY_REQUIRE(a && b && g && ga && gb, HYRES_E_ARG, "attn_gate_bwd_f16: NULL");
+    if (gate_f16_vec(a, b, g, ga, gb, n, g16)) {
+        launch_gate_bwd4h<false>(a, b, g, ga, gb, n, g16, as_stream(s));
+        return HY_LAUNCH_CHECK("attn_gate_bwd4h");
+    }
     if (g16)
         hipLaunchKernelGGL((attn_gate_bwd_kernel<true, true>), dim3(grid_for(n)), dim3(256), 0, as_stream(s),
                            (const float*)a, (const float*)b, (const float*)g, (float*)ga, (float*)gb, n);

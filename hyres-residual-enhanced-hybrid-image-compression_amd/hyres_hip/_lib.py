@@ -119,6 +119,7 @@ _SIGS = {
     "hyres_attn_gate_bwd": (_I, [_P, _P, _P, _P, _P, _LL, _P]),
     "hyres_attn_gate_bwd_relu": (_I, [_P, _P, _P, _P, _P, _LL, _P]),
     "hyres_attn_gate_bwd_f16": (_I, [_P, _P, _P, _P, _P, _LL, _I, _P]),
+    "hyres_attn_gate_bwd_relu_f16": (_I, [_P, _P, _P, _P, _P, _LL, _I, _P]),
     "hyres_relu_bwd_2d_f16": (_I, [_P, _I, _P, _I, _P, _I, _LL, _I, _I, _P]),
     "hyres_prelu_bwd_f16": (_I, [_P, _I, _P, _I, _P, _I, _LL, _I, _P, _P, _P, _LL, _I, _P]),
     "hyres_gdn_dnorm_f16": (_I, [_P, _P, _P, _P, _LL, _I, _I, _I, _P]),

@@ -1182,8 +1182,14 @@ def attn_gate(tape: Optional[Tape], a: Node, b: Node, x: Node) -> Node:
         assert acc_a == 0 and acc_b == 0, "gate inputs are single-consumer"
         if a.half:
             assert ga.dtype == gb.dtype == g.dtype
-            L.call("hyres_attn_gate_bwd_f16", a.ptr(), b.ptr(), g.data_ptr(), ga.data_ptr(), gb.data_ptr(), n,
-                   int(g.dtype == torch.float16), L.stream())
+            g16 = int(g.dtype == torch.float16)
+            if a.relu_out and a.parent is None and n % 4 == 0:  # the ReLU backward folded in, as below
+                L.call("hyres_attn_gate_bwd_relu_f16", a.ptr(), b.ptr(), g.data_ptr(), ga.data_ptr(), gb.data_ptr(), n,
+                       g16, L.stream())
+                a.gmasked = True
+            else:
+                L.call("hyres_attn_gate_bwd_f16", a.ptr(), b.ptr(), g.data_ptr(), ga.data_ptr(), gb.data_ptr(), n, g16,
+                       L.stream())
         elif a.relu_out and a.parent is None and n % 4 == 0:
             # the last ResidualUnit's ReLU backward folded in: a's gradient leaves here masked (its producer skips it)
             L.call("hyres_attn_gate_bwd_relu", a.ptr(), b.ptr(), g.data_ptr(), ga.data_ptr(), gb.data_ptr(), n,

@@ -338,6 +338,10 @@ int hyres_prelu_bwd_f16(const void* x, int ldx, const void* g, int ldg, void* gx
                         hyres_stream_t s);
 int hyres_attn_gate_bwd_f16(const void* a, const void* b, const void* g, void* ga, void* gb, long long n, int g16,
                             hyres_stream_t s);
+/* ... and with the last ResidualUnit's ReLU backward folded in, as hyres_attn_gate_bwd_relu (round 6); n % 4 == 0,
+ * fp16 operands 8B-aligned, fp32 ones 16B-aligned */
+int hyres_attn_gate_bwd_relu_f16(const void* a, const void* b, const void* g, void* ga, void* gb, long long n, int g16,
+                                 hyres_stream_t s);
 /* y (+)= x  (gradient fan-in); _f16: both fp16 */
 int hyres_accumulate(const float* x, float* y, long long n, hyres_stream_t s);
 int hyres_accumulate_f16(const void* x, void* y, long long n, hyres_stream_t s);

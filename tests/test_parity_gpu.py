@@ -571,6 +571,48 @@ def test_attn_gate_float4_and_relu_fold():
     assert float((gam[a == 0]).abs().max()) == 0.0 and bool((a == 0).any())
 
 
+@pytest.mark.parametrize("g16", [0, 1])
+def test_attn_gate_f16_vector_and_relu_fold(g16):
+    """The AMP gate backward (fp16 a, b; fp16 or fp32 gradients) on the round-6 vector kernel equals the scalar kernel
+    (the one a ragged n runs on) bit for bit with fp32 gradients and within 1 fp16 ulp with fp16 ones, and the ReLU-folded variant (hyres_attn_gate_bwd_relu_f16) equals
+    the gate backward followed by hyres_relu_bwd_2d_f16 bit for bit."""
+    from hyres_hip import _lib as L
+    D = dev()
+    P, C = 8 * 32 * 32, 192
+    n = P * C
+    gdt = torch.float16 if g16 else torch.float32
+    a = torch.relu(_rand((P, C), 91)).to(D).half()
+    b = _rand((P, C), 92, 3.0).to(D).half()
+    g = _rand((P, C), 93).to(D).to(gdt)
+    ga, gb, gam, gbm, gar = (torch.empty(P, C, device=D, dtype=gdt) for _ in range(5))
+    gas, gbs = (torch.zeros(P, C, device=D, dtype=gdt) for _ in range(2))
+    L.call("hyres_attn_gate_bwd_f16", a.data_ptr(), b.data_ptr(), g.data_ptr(), ga.data_ptr(), gb.data_ptr(), n, g16,
+           L.stream())
+    # n - 1: not a multiple of 4, the scalar kernel; the last element is compared separately below
+    L.call("hyres_attn_gate_bwd_f16", a.data_ptr(), b.data_ptr(), g.data_ptr(), gas.data_ptr(), gbs.data_ptr(), n - 1,
+           g16, L.stream())
+    L.call("hyres_relu_bwd_2d_f16", a.data_ptr(), C, ga.data_ptr(), C, gar.data_ptr(), C, P, C, g16, L.stream())
+    L.call("hyres_attn_gate_bwd_relu_f16", a.data_ptr(), b.data_ptr(), g.data_ptr(), gam.data_ptr(), gbm.data_ptr(), n,
+           g16, L.stream())
+    torch.cuda.synchronize()
+    if g16:
+        # the scalar kernel's fp16 stores compile to v_fma_mixlo_f16 (product rounded once, straight to fp16: the
+        # contraction -ffp-contract=fast allows); the vector kernel rounds the fp32 product, then packs to fp16 (the
+        # source's literal semantics) — at most 1 fp16 ulp apart (zeros' signs aside), on a small fraction of the elements
+        for u, v in ((ga, gas), (gb, gbs)):
+            u, v = u.view(-1)[:-1] + 0, v.view(-1)[:-1] + 0  # -0 -> +0 (gb = g * a * ... at a == 0 keeps g's sign)
+            du = (u.view(torch.int16).int() - v.view(torch.int16).int()).abs()
+            assert int(du.max()) <= 1 and float((du > 0).float().mean()) < 0.05
+    else:
+        assert torch.equal(ga.view(-1)[:-1], gas.view(-1)[:-1]) and torch.equal(gb.view(-1)[:-1], gbs.view(-1)[:-1])
+    s = torch.sigmoid(b.double())
+    tol = 2e-3 if g16 else 1e-6
+    assert rel_err(ga.double().cpu(), (g.double() * s).cpu()) < tol
+    assert rel_err(gb.double().cpu(), (g.double() * a.double() * s * (1 - s)).cpu()) < tol
+    assert torch.equal(gam, gar) and torch.equal(gbm, gb)
+    assert bool((a == 0).any()) and float(gam[a == 0].abs().max()) == 0.0
+
+
 def test_prelu_mask_epilogue_refused_off_the_weight_resident_kernel():
     """HYRES_ACT_PRELU_MASK is implemented by conv3x3_wres_bf6_kernel only: a 1x1 input-gradient asking for it gets
     HYRES_E_ARG, nothing launched (the caller, ops.Node.prelu_mask_epilogue, checks the route first)."""
