@@ -1832,10 +1832,15 @@ __global__ __launch_bounds__(256, 2) void conv1x1_stream_h_kernel(const ConvArgs
 // round-5 version without the row-shaped epilogue measured 2-10 % slower than the tiles (profiles/r5g_stream_hf_ab.txt).
 // Arithmetic: fp16 operands, fp32 accumulation and epilogue ((acc + b) + residual, mask, + old y), one fp16 rounding
 // at the store — the tiled f16 kernel's (tests/test_stream_h_gpu.py: bit for bit).
+// F & 8 (round 6, AMP training with SpatialAttention folded into MultiScaleRefine's fusion 1x1): HYRES_EPI_SA_BWD, the
+// fusion's input-gradient 64 -> 192 (NT = 6, KC = 4) with SpatialAttention's mean / max backward added per pixel —
+// acc + d mean / C + (channel == argmax ? d max : 0) (+ old y), epi_store4's SA_BWD arithmetic; the per-pixel operands
+// (aux0 [P][ld0] fp32 pairs, aux2 int argmax) roll a tile ahead like the others.
 template <int NT, int KC, int F>
 __global__ __launch_bounds__(256, 2) void conv1x1_stream_hf_kernel(const ConvArgs a) {
     constexpr int K = 16 * KC, KP = K + 8, CO = 32 * NT, EP = 36;
-    constexpr bool RES = (F & 1) != 0, MASK = (F & 2) != 0, ACC = (F & 4) != 0;
+    constexpr bool RES = (F & 1) != 0, MASK = (F & 2) != 0, ACC = (F & 4) != 0, SAB = (F & 8) != 0;
+    static_assert(!SAB || (!RES && !MASK), "SA_BWD: no residual / mask");
     static_assert(NT % 2 == 0, "operands alternate between two register sets per co tile");
     __shared__ __attribute__((aligned(16))) _Float16 Ws[CO * KP];
     __shared__ __attribute__((aligned(16))) float bs[CO];
@@ -1857,6 +1862,8 @@ __global__ __launch_bounds__(256, 2) void conv1x1_stream_hf_kernel(const ConvArg
     const __amdgpu_buffer_rsrc_t r_res = opnd_rsrc(RES ? e.res : nullptr, npix * e.ldres * 2);
     const __amdgpu_buffer_rsrc_t r_mask = opnd_rsrc(MASK ? e.aux0 : nullptr, npix * e.ld0 * 2);
     const __amdgpu_buffer_rsrc_t r_old = opnd_rsrc(ACC ? a.y : nullptr, npix * g.ldy * 2);
+    const __amdgpu_buffer_rsrc_t r_gm = opnd_rsrc(SAB ? e.aux0 : nullptr, npix * e.ld0 * 4);
+    const __amdgpu_buffer_rsrc_t r_am = opnd_rsrc(SAB ? e.aux2 : nullptr, npix * 4);
     constexpr int OOR = (int)0x80000000;
     _Float16* const y = reinterpret_cast<_Float16*>(a.y);
     const int ntile = (a.M + 31) / 32;
@@ -1880,17 +1887,38 @@ __global__ __launch_bounds__(256, 2) void conv1x1_stream_hf_kernel(const ConvArg
             if constexpr (ACC) eold[set][q] = bload4h(r_old, ooff(tile, g.ldy, t, q));
         }
     };
+    // SA_BWD's per-pixel operands: one set per tile, two sets (the next tile's are issued with its X)
+    float2 sgm[SAB ? 2 : 1][4];
+    int sam[SAB ? 2 : 1][4];
+    auto load_sab = [&](int tile, int set) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int p = tile * 32 + cr + 8 * q;
+            const bool ok = tile < ntile && p < a.M;
+            sgm[set][q] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(r_gm, ok ? p * e.ld0 * 4 : OOR,
+                                                                                          0, 0));
+            sam[set][q] = __builtin_amdgcn_raw_buffer_load_b32(r_am, ok ? p * 4 : OOR, 0, 0);
+        }
+    };
     half8s_t xv[KC];
 #pragma unroll
     for (int j = 0; j < KC; ++j) xv[j] = load_x(gw, j);
     load_epi(gw, 0, 0);
+    if constexpr (SAB) load_sab(gw, 0);
     float* const es = Es + wave * 32 * EP;
-    for (int tile = gw; tile < ntile; tile += nw) {
+    int tset = 0;
+    for (int tile = gw; tile < ntile; tile += nw, tset ^= 1) {
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
             const int cur = t & 1;
             if (t + 1 < NT) load_epi(tile, t + 1, cur ^ 1);
             else load_epi(tile + nw, 0, cur ^ 1);
+            if constexpr (SAB) {
+                if (t == NT - 1) {  // constant set indices (a dynamic one puts the arrays in scratch)
+                    if (tset) load_sab(tile + nw, 0);
+                    else load_sab(tile + nw, 1);
+                }
+            }
             floatx16 acc;
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[r] = 0.f;
@@ -1915,6 +1943,14 @@ __global__ __launch_bounds__(256, 2) void conv1x1_stream_hf_kernel(const ConvArg
                 const float4 av = *reinterpret_cast<const float4*>(&es[(cr + 8 * q) * EP + cc]);
                 const int p = tile * 32 + cr + 8 * q;
                 float o[4] = {av.x + b4.x, av.y + b4.y, av.z + b4.z, av.w + b4.w};
+                if constexpr (SAB) {  // epi_store4's SA_BWD: (acc + d mean / C) + (channel == argmax ? d max : 0)
+                    const float2 gm = tset ? sgm[1][q] : sgm[0][q];
+                    const int mi = tset ? sam[1][q] : sam[0][q];
+                    o[0] = av.x + gm.x + (n == mi ? gm.y : 0.f);
+                    o[1] = av.y + gm.x + (n + 1 == mi ? gm.y : 0.f);
+                    o[2] = av.z + gm.x + (n + 2 == mi ? gm.y : 0.f);
+                    o[3] = av.w + gm.x + (n + 3 == mi ? gm.y : 0.f);
+                }
                 if constexpr (RES) {
                     const float4 r = h2f4(eres[cur][q]);
                     o[0] += r.x; o[1] += r.y; o[2] += r.z; o[3] += r.w;
@@ -3075,9 +3111,16 @@ static int stream_h_nt(const hyres_conv_geom* g, const hyres_epilogue* e) {
 // ReLU / ReLU mask and at least one streamed operand (residual, mask, old y; without one: conv1x1_stream_h_kernel),
 // no out2, 16-byte X rows / 8-byte Y rows. Returns NT | KC << 4 | F << 8, or 0.
 static int stream_hf_cfg(const hyres_conv_geom* g, const hyres_epilogue* e) {
-    if (g_tune[17] == 0 || (e->io_f16 & 3) != 3 || !e->f16_operands || e->square_input || e->kind != HYRES_EPI_BIAS ||
-        e->out2)
-        return 0;
+    if (g_tune[17] == 0 || (e->io_f16 & 3) != 3 || !e->f16_operands || e->square_input || e->out2) return 0;
+    if (e->kind == HYRES_EPI_SA_BWD) {  // round 6: the fusion 1x1's input-gradient under AMP, 64 -> 192
+        if (g_tune[21] == 0 || g->Ci != 64 || g->Co != 192 || e->act != HYRES_ACT_NONE || e->res || g->nphase != 1 ||
+            g->ntaps != 1 || g->ish != 1 || g->isw != 1 || g->dh[0] != 0 || g->dw[0] != 0 || g->Hi != g->Hq ||
+            g->Wi != g->Wq || g->Ho != g->Hq || g->Wo != g->Wq || (long long)g->B * g->Hq * g->Wq < 16384 ||
+            g->ldx % 8 || g->ldy % 4 || e->ld0 % 2)
+            return 0;
+        return 6 | (4 << 4) | ((8 | (e->accumulate ? 4 : 0)) << 8);
+    }
+    if (e->kind != HYRES_EPI_BIAS) return 0;
     if (e->act != HYRES_ACT_NONE && e->act != HYRES_ACT_RELU && e->act != HYRES_ACT_RELU_MASK) return 0;
     if (g->nphase != 1 || g->ntaps != 1 || g->ish != 1 || g->isw != 1 || g->dh[0] != 0 || g->dw[0] != 0) return 0;
     if (g->Hi != g->Hq || g->Wi != g->Wq || g->Ho != g->Hq || g->Wo != g->Wq) return 0;
@@ -3206,6 +3249,8 @@ static int launch_stream_hf_f(const ConvArgs& a, int f, hipStream_t st) {
 
 static int launch_stream_hf(const ConvArgs& a, int cfg, hipStream_t st) {
     const int nt = cfg & 15, kc = (cfg >> 4) & 15, f = cfg >> 8;
+    if (nt == 6 && kc == 4 && f == 8) return launch_stream_hf_one<6, 4, 8>(a, st);
+    if (nt == 6 && kc == 4 && f == 12) return launch_stream_hf_one<6, 4, 12>(a, st);
     if (nt == 2 && kc == 4) return launch_stream_hf_f<2, 4>(a, f, st);
     if (nt == 2 && kc == 8) return launch_stream_hf_f<2, 8>(a, f, st);
     if (nt == 4 && kc == 4) return launch_stream_hf_f<4, 4>(a, f, st);
@@ -3404,8 +3449,9 @@ int hyres_conv_forward(const hyres_conv_geom* g, const float* x, const float* w2
                    "conv: ROWSCALE needs aux1 (per-pixel scale), no square_input / accumulate");
     if (e->kind == HYRES_EPI_SA_BWD)
         HY_REQUIRE(e->aux0 && e->aux2 && e->ld0 >= 2 && !e->square_input && e->act == HYRES_ACT_NONE && !e->res &&
-                       !e->out2 && !(e->io_f16 & 2),
-                   HYRES_E_ARG, "conv: SA_BWD needs aux0 ([P][ld0 >= 2]) and aux2 (argmax), no act / res / out2, fp32 Y");
+                       !e->out2 && (!(e->io_f16 & 2) || stream_hf_cfg(g, e)),
+                   HYRES_E_ARG, "conv: SA_BWD needs aux0 ([P][ld0 >= 2]) and aux2 (argmax), no act / res / out2, fp32 Y "
+                   "(fp16 Y: conv1x1_stream_hf_kernel's 64 -> 192 only)");
     hipStream_t st = as_stream(s);
     if (ch.narrow) {
         a.nsplit = 1;
@@ -3456,6 +3502,9 @@ int hyres_conv_forward(const hyres_conv_geom* g, const float* x, const float* w2
             return launch_stream_hf(a, cfg, st);
         }
     }
+    // no other kernel implements SA_BWD with an fp16 Y (its epi_store4 instantiations leave the case out)
+    HY_REQUIRE(!(e->kind == HYRES_EPI_SA_BWD && (e->io_f16 & 2)), HYRES_E_ARG,
+               "conv: an fp16-Y SA_BWD input-gradient needs conv1x1_stream_hf_kernel (alignment / size / split mode)");
     {
         const int nt = stream_h_nt(g, e);
         const long long xb = (long long)a.M * g->ldx * 2;

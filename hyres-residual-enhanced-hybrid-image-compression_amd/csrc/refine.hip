@@ -712,6 +712,93 @@ __global__ __launch_bounds__(256) void sa_fold_bwd_kernel(const float* pre, int 
     }
     if (threadIdx.x == 0) part[(long long)blockIdx.x * (C + 1) + C] = rs[0];
 }
+// The fp16-activation build (AMP training): 8 lanes per pixel, 8 channels (one 16-byte fp16 row piece) each — the
+// 16-lane float4 mapping above moves fp16 rows as 8-byte pieces and measured 169 us at 256^2 x 16 (r7h). Same
+// arithmetic per element, d summed over 8 lanes (xor 4, 2, 1), per-block partials in the same layout.
+template <bool G>
+__global__ __launch_bounds__(256) void sa_fold_bwd_h8_kernel(const float* pre, int ldpre, const float* gy, int ldg,
+                                                             const float* attn, const float* bias, const float* slope,
+                                                             float* gs, float* glogit, float* part, long long P,
+                                                             int C) {
+    typedef _Float16 h8_t __attribute__((ext_vector_type(8)));
+    __shared__ float rb[32][68];
+    __shared__ float rs[256];
+    const float a = slope[0];
+    const int l8 = threadIdx.x & 7, grp = threadIdx.x >> 3;
+    const int c = 8 * l8;
+    const bool cok = c < C;
+    float b[8], bs[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        b[k] = cok ? bias[c + k] : 0.f;
+        bs[k] = 0.f;
+    }
+    float ss = 0.f;
+    const _Float16* preh = reinterpret_cast<const _Float16*>(pre);
+    // every lane of an 8-lane group walks the same pixels, so the group's xor-shuffles never mix groups
+    for (long long p = (long long)blockIdx.x * 32 + grp; p < P; p += (long long)gridDim.x * 32) {
+        float pv[8], gv[8];
+        if (cok) {
+            const h8_t ph = *reinterpret_cast<const h8_t*>(preh + p * ldpre + c);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) pv[k] = (float)ph[k];
+            if constexpr (G) {
+                const h8_t gh = *reinterpret_cast<const h8_t*>(reinterpret_cast<const _Float16*>(gy) + p * ldg + c);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) gv[k] = (float)gh[k];
+            } else {
+                const float4 g0 = *reinterpret_cast<const float4*>(gy + p * ldg + c);
+                const float4 g1 = *reinterpret_cast<const float4*>(gy + p * ldg + c + 4);
+                gv[0] = g0.x; gv[1] = g0.y; gv[2] = g0.z; gv[3] = g0.w;
+                gv[4] = g1.x; gv[5] = g1.y; gv[6] = g1.z; gv[7] = g1.w;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) pv[k] = gv[k] = 0.f;
+        }
+        const float at = attn[p];
+        float gp[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            gp[k] = pv[k] > 0.f ? gv[k] : a * gv[k];
+            if (!(pv[k] > 0.f)) ss += pv[k] * gv[k];
+            bs[k] += gp[k];
+        }
+        // sa_fold_bwd_kernel's pairing within each float4, then the two halves
+        float d = ((gp[0] * (pv[0] - b[0]) + gp[1] * (pv[1] - b[1])) + (gp[2] * (pv[2] - b[2]) + gp[3] * (pv[3] - b[3]))) +
+                  ((gp[4] * (pv[4] - b[4]) + gp[5] * (pv[5] - b[5])) + (gp[6] * (pv[6] - b[6]) + gp[7] * (pv[7] - b[7])));
+        if (cok) {
+            if constexpr (G) {
+                h8_t o;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) o[k] = (_Float16)(at * gp[k]);
+                *reinterpret_cast<h8_t*>(reinterpret_cast<_Float16*>(gs) + p * C + c) = o;
+            } else {
+                *reinterpret_cast<float4*>(gs + p * C + c) = make_float4(at * gp[0], at * gp[1], at * gp[2], at * gp[3]);
+                *reinterpret_cast<float4*>(gs + p * C + c + 4) = make_float4(at * gp[4], at * gp[5], at * gp[6], at * gp[7]);
+            }
+        }
+        for (int off = 4; off > 0; off >>= 1) d += __shfl_xor(d, off);
+        if (l8 == 0) glogit[p] = d * (1.0f - at);
+    }
+    if (cok) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) rb[grp][c + k] = bs[k];
+    }
+    rs[threadIdx.x] = ss;
+    __syncthreads();
+    for (int k = 128; k > 0; k >>= 1) {
+        if (threadIdx.x < k) rs[threadIdx.x] += rs[threadIdx.x + k];
+        __syncthreads();
+    }
+    if (threadIdx.x < C) {
+        float t = 0.f;
+#pragma unroll
+        for (int g = 0; g < 32; ++g) t += rb[g][threadIdx.x];
+        part[(long long)blockIdx.x * (C + 1) + threadIdx.x] = t;
+    }
+    if (threadIdx.x == 0) part[(long long)blockIdx.x * (C + 1) + C] = rs[0];
+}
 // one block per output (C bias channels, then the slope): the partials folded in a fixed order, ADDED to the gradient
 __global__ __launch_bounds__(256) void sa_fold_final_kernel(const float* part, int nb, int C, float* dbias,
                                                             float* dslope) {
@@ -1038,6 +1125,29 @@ int hyres_sa_fold_bwd(const float* pre, int ldpre, const float* gy, int ldg, con
     hipLaunchKernelGGL(sa_fold_bwd_kernel, dim3(nb), dim3(256), 0, st, pre, ldpre, gy, ldg, attn, bias, slope, gs, glogit,
                        (float*)ws, P, C);
     int rc = HY_LAUNCH_CHECK("sa_fold_bwd");
+    if (rc) return rc;
+    hipLaunchKernelGGL(sa_fold_final_kernel, dim3(C + 1), dim3(256), 0, st, (const float*)ws, nb, C, dbias, dslope);
+    return HY_LAUNCH_CHECK("sa_fold_final");
+}
+
+int hyres_sa_fold_bwd_f16(const void* pre, int ldpre, const void* gy, int ldg, const float* attn, const float* bias,
+                          const float* slope, void* gs, float* glogit, float* dbias, float* dslope, long long P, int C,
+                          void* ws, long long ws_bytes, int g16, hyres_stream_t s) {
+    HY_REQUIRE(pre && gy && attn && bias && slope && gs && glogit && dbias && dslope && P > 0, HYRES_E_ARG,
+               "sa_fold_bwd_f16: NULL");
+    HY_REQUIRE(C % 8 == 0 && C > 0 && C <= 64 && ldpre % 8 == 0 && ldg % 8 == 0 && aligned16(pre) && aligned16(gy) &&
+                   aligned16(gs),
+               HYRES_E_ALIGN, "sa_fold_bwd_f16: C %% 8 == 0, C <= 64, 16B-aligned rows");
+    HY_REQUIRE(ws && ws_bytes >= hyres_sa_fold_workspace_bytes(P, C), HYRES_E_WORKSPACE, "sa_fold_bwd_f16: workspace");
+    const int nb = sa_fold_blocks(P);
+    hipStream_t st = as_stream(s);
+    if (g16)
+        hipLaunchKernelGGL(sa_fold_bwd_h8_kernel<true>, dim3(nb), dim3(256), 0, st, (const float*)pre, ldpre,
+                           (const float*)gy, ldg, attn, bias, slope, (float*)gs, glogit, (float*)ws, P, C);
+    else
+        hipLaunchKernelGGL(sa_fold_bwd_h8_kernel<false>, dim3(nb), dim3(256), 0, st, (const float*)pre, ldpre,
+                           (const float*)gy, ldg, attn, bias, slope, (float*)gs, glogit, (float*)ws, P, C);
+    int rc = HY_LAUNCH_CHECK("sa_fold_bwd_f16");
     if (rc) return rc;
     hipLaunchKernelGGL(sa_fold_final_kernel, dim3(C + 1), dim3(256), 0, st, (const float*)ws, nb, C, dbias, dslope);
     return HY_LAUNCH_CHECK("sa_fold_final");

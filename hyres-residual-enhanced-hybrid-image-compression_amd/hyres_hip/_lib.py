@@ -170,6 +170,7 @@ _SIGS = {
     "hyres_spatial_attn_workspace_bytes": (_LL, [_I, _I, _I]),
     "hyres_sa_fold_workspace_bytes": (_LL, [_LL, _I]),
     "hyres_sa_fold_bwd": (_I, [_P, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _LL, _I, _P, _LL, _P]),
+    "hyres_sa_fold_bwd_f16": (_I, [_P, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _LL, _I, _P, _LL, _I, _P]),
     "hyres_spatial_attn_bwd_map": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _LL, _P]),
     "hyres_sum_log": (_I, [_P, _LL, _P, _P, _LL, _P]),
     "hyres_sum_sqdiff": (_I, [_P, _P, _LL, _P, _P, _LL, _P]),

@@ -128,15 +128,20 @@ def sa_fold_fusion(tape: Optional[Tape], multi: Node, w_sa: torch.Tensor, weight
     the 2-channel map (hyres_spatial_attn_bwd_map); d W = gs x multi (weight gradient on the side stream, bias from the
     fold's own column sums); d multi = W^T gs with SpatialAttention's mean / max backward added in the input-gradient's
     epilogue (HYRES_EPI_SA_BWD). Replaces sa_mul, sa_bwd_logit, sa_bwd_x and the PReLU backward of the unfused chain
-    (refine's 192-channel concat read and written three more times per step)."""
-    assert multi.contiguous and not multi.half
+    (refine's 192-channel concat read and written three more times per step).
+
+    Round 6, AMP training (``sa_fold_amp_ok``): fp16 ``multi``, output, pre-activation and gradients, fp16 operands on
+    the f16 MFMA; backward hyres_sa_fold_bwd_f16, the input-gradient on conv1x1_stream_hf_kernel's SA_BWD build."""
+    assert multi.contiguous and (not multi.half or sa_fold_amp_ok(tape, multi, weight.shape[0]))
     Co, Ci_w, KH, KW = weight.shape
     assert KH == 1 and KW == 1 and Ci_w == multi.C and slope.numel() == 1
     B, H, W, Ci = multi.B, multi.H, multi.W, multi.C
     dev = multi.device
     attn, pooled2, argmax = spatial_attention_map(multi, w_sa, keep=True)
-    y = Node.new(B, H, W, Co, dev)
-    pre = _empty((B, H, W, Co), dev)
+    f16 = int(O.f16_convs())
+    ydt = torch.float16 if Co > 4 and O.act_f16(tape, H, W) else torch.float32
+    y = Node.new(B, H, W, Co, dev, dtype=ydt)
+    pre = _empty((B, H, W, Co), dev, ydt)  # stored by the epilogue in y's dtype
     g = O._geom("hyres_geom_conv2d", B, H, W, Ci, multi.ld, Co, y.ld, 1, 1, 1, 0, 1)
     e = L.Epilogue()
     e.kind = L.EPI_ROWSCALE
@@ -145,6 +150,8 @@ def sa_fold_fusion(tape: Optional[Tape], multi: Node, w_sa: torch.Tensor, weight
     e.slope = slope.data_ptr()
     e.aux1, e.ld1 = attn.data_ptr(), 1
     e.out2, e.ldo2 = pre.data_ptr(), Co
+    e.io_f16 = O._io_flags(multi, y, tape)
+    e.f16_operands = f16
     O._launch_conv(g, multi.ptr(), weight, Ci_w, y.ptr(), e)
     O.Trace.act(y, L.ACT_PRELU, pre)
     if tape is None:
@@ -154,16 +161,21 @@ def sa_fold_fusion(tape: Optional[Tape], multi: Node, w_sa: torch.Tensor, weight
         gy = y.grad()
         if gy is None:
             return
-        assert gy.dtype == torch.float32
+        assert gy.dtype == torch.float32 or pre.dtype == torch.float16
         P = y.P
-        gs = _empty((B, H, W, Co), dev)
+        gs = _empty((B, H, W, Co), dev, gy.dtype)
         glogit = _empty((B, H, W), dev)
         ws = _ws(L.load().hyres_sa_fold_workspace_bytes(P, Co), dev, slot=1)
         dbias = param_grad(bias) if bias.requires_grad else _empty((Co,), dev)
         dslope = param_grad(slope) if slope.requires_grad else _empty((1,), dev)
-        L.call("hyres_sa_fold_bwd", pre.data_ptr(), Co, gy.data_ptr(), y.grad_ld(), attn.data_ptr(), bias.data_ptr(),
-               slope.data_ptr(), gs.data_ptr(), glogit.data_ptr(), dbias.data_ptr(), dslope.data_ptr(), P, Co,
-               ws.data_ptr(), ws.numel(), L.stream())
+        if pre.dtype == torch.float16:
+            L.call("hyres_sa_fold_bwd_f16", pre.data_ptr(), Co, gy.data_ptr(), y.grad_ld(), attn.data_ptr(),
+                   bias.data_ptr(), slope.data_ptr(), gs.data_ptr(), glogit.data_ptr(), dbias.data_ptr(),
+                   dslope.data_ptr(), P, Co, ws.data_ptr(), ws.numel(), int(gy.dtype == torch.float16), L.stream())
+        else:
+            L.call("hyres_sa_fold_bwd", pre.data_ptr(), Co, gy.data_ptr(), y.grad_ld(), attn.data_ptr(),
+                   bias.data_ptr(), slope.data_ptr(), gs.data_ptr(), glogit.data_ptr(), dbias.data_ptr(),
+                   dslope.data_ptr(), P, Co, ws.data_ptr(), ws.numel(), L.stream())
         gp2 = _empty((B, H, W, 2), dev)
         gw_sa = param_grad(w_sa) if w_sa.requires_grad else _empty(w_sa.shape, dev)
         ws2 = _ws(L.load().hyres_spatial_attn_workspace_bytes(B, H, W), dev, slot=1)
@@ -174,6 +186,8 @@ def sa_fold_fusion(tape: Optional[Tape], multi: Node, w_sa: torch.Tensor, weight
             L.call("hyres_wgrad_desc_conv2d", ctypes.byref(d), B, H, W, Ci, multi.ld, Co, Co, 1, 1, 1, 0, 1)
             d.sm = Ci_w
             d.accumulate = 1
+            d.f16_operands = f16 * O.AMP_WGRAD_F16
+            d.io_f16 = (1 if gs.dtype == torch.float16 else 0) | (2 if multi.half else 0)
             O._wgrad(d, gs.data_ptr(), multi.ptr(), param_grad(weight), dev, None, keep=(gs, multi.v), side=True)
         if multi.rg:
             ed = L.Epilogue()
@@ -184,10 +198,29 @@ def sa_fold_fusion(tape: Optional[Tape], multi: Node, w_sa: torch.Tensor, weight
             gd = O._geom("hyres_geom_conv2d_dgrad", B, H, W, Ci, multi.grad_ld(), Co, Co, 1, 1, 1, 0, 1)
             w2d = O._prepped(weight, gd, L.WPREP_CONV_DGRAD, Ci_w, Co, 1, 1, 0)
             ed.accumulate = acc
+            ed.f16_operands = f16
+            ed.io_f16 = O._dgrad_io(gs, multi)
             O._launch_conv(gd, gs.data_ptr(), w2d, gd.ntaps * Co, tgt.data_ptr(), ed)
 
     tape.push(bwd)
     return y
+
+
+def sa_fold_amp_ok(tape: Optional[Tape], multi: Node, Co: int) -> bool:
+    """sa_fold_fusion under AMP training: fp16 ``multi`` with fp16 gradients, an fp16 fusion output, and the fusion's
+    input-gradient (Co -> multi.C with HYRES_EPI_SA_BWD) routed to conv1x1_stream_hf_kernel — the one kernel with an
+    fp16-Y SA_BWD epilogue (checked through the launcher's own choice, ops.conv_variant)."""
+    if tape is None or not multi.half or not multi.ghalf or not multi.contiguous or not O.f16_convs():
+        return False
+    if not (Co > 4 and O.act_f16(tape, multi.H, multi.W)) or not O.AMP_F16_GRAD:
+        return False
+    gd = O._geom("hyres_geom_conv2d_dgrad", multi.B, multi.H, multi.W, multi.C, multi.C, Co, Co, 1, 1, 1, 0, 1)
+    ed = L.Epilogue()
+    ed.kind = L.EPI_SA_BWD
+    ed.ld0 = 2
+    ed.f16_operands = 1
+    ed.io_f16 = L.IO_X16 | L.IO_Y16
+    return O.conv_variant(gd, ed, False).startswith("conv1x1_stream_hf_kernel")
 
 
 def spatial_attention_mul(tape: Optional[Tape], x: Node, w: torch.Tensor) -> Node:

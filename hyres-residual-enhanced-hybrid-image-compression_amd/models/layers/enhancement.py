@@ -140,8 +140,10 @@ class MultiScaleRefine(HipModule):
             h = O.conv2d(None, multi, f0.weight, f0.bias, act=L.ACT_PRELU, slope=f1.weight, rowscale=attn)
             out = f2c.hip(None, h)
             m = None
-        elif FOLD_SA_MUL and not multi.half and not O.f16_convs():
-            # training (fp32 activations): the same fold, with its backward (refine_ops.sa_fold_fusion)
+        elif FOLD_SA_MUL and ((not multi.half and not O.f16_convs())
+                              or R.sa_fold_amp_ok(tape, multi, self.fusion[0].weight.shape[0])):
+            # training (fp32 activations; round 6: also AMP with fp16 activations and gradients): the same fold, with
+            # its backward (refine_ops.sa_fold_fusion)
             f0, f1, f2c = self.fusion[0], self.fusion[1], self.fusion[2]
             h = R.sa_fold_fusion(tape, multi, self.spatial_att.conv.weight, f0.weight, f0.bias, f1.weight)
             out = f2c.hip(tape, h)

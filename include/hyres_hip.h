@@ -473,6 +473,11 @@ long long hyres_sa_fold_workspace_bytes(long long P, int C);
 int hyres_sa_fold_bwd(const float* pre, int ldpre, const float* gy, int ldg, const float* attn, const float* bias,
                       const float* slope, float* gs, float* glogit, float* dbias, float* dslope, long long P, int C,
                       void* ws, long long ws_bytes, hyres_stream_t s);
+/* ... under AMP training (round 6): ``pre`` fp16 (fp16 activations); g16 = 1: gy and gs fp16 as well (fp16
+ * gradients), 0: fp32. fp32 arithmetic; attn, bias, glogit, dbias, dslope fp32. C % 8 == 0, C <= 64, rows 16B-aligned. */
+int hyres_sa_fold_bwd_f16(const void* pre, int ldpre, const void* gy, int ldg, const float* attn, const float* bias,
+                          const float* slope, void* gs, float* glogit, float* dbias, float* dslope, long long P, int C,
+                          void* ws, long long ws_bytes, int g16, hyres_stream_t s);
 /* SpatialAttention's map backward from the logit gradient: gw += d conv7x7 weight, gpooled2 = [P][2] gradients of
  * the channel mean (already divided by C, as HYRES_EPI_SA_BWD reads it) and the channel max. ws as
  * hyres_spatial_attn_workspace_bytes(B, H, W). */

@@ -180,9 +180,10 @@ def test_f16_gradient_backward_entry_points_match_rounded_fp32():
     check(ga16, ga32, "gate a")
     check(gb16, gb32, "gate b")
     nrm = _h(_rand((P, C), 4).abs() + 0.5).to(D)
+    nrm16 = nrm.half()  # held for the call (a temporary's block returns to the allocator before the kernel runs)
     for inv in (0, 1):
         L.call("hyres_gdn_dnorm", g.data_ptr(), y.data_ptr(), nrm.data_ptr(), gx32.data_ptr(), P, C, inv, s)
-        L.call("hyres_gdn_dnorm_f16", gh.data_ptr(), yh.data_ptr(), nrm.half().data_ptr(), gx16.data_ptr(), P, C, inv,
+        L.call("hyres_gdn_dnorm_f16", gh.data_ptr(), yh.data_ptr(), nrm16.data_ptr(), gx16.data_ptr(), P, C, inv,
                1, s)
         check(gx16, gx32, f"gdn dnorm inv={inv}")
     # add2d with every storage combination, accumulate on and off
@@ -212,9 +213,9 @@ def test_f16_gradient_backward_entry_points_match_rounded_fp32():
     for (Hi, Wi, Ho, Wo, sc) in ((H, W, 2 * H, 2 * W, 0.5), (H, W, H // 2, W // 2, 2.0)):
         gy = _h(_rand((B * Ho * Wo, C), 6)).to(D)
         base = _h(_rand((P, C), 7)).to(D)
-        o32, o16 = base.clone(), base.half()
+        o32, o16, gy16 = base.clone(), base.half(), gy.half()
         L.call("hyres_bilinear_bwd", gy.data_ptr(), C, o32.data_ptr(), C, B, Hi, Wi, Ho, Wo, C, sc, sc, 1, s)
-        L.call("hyres_bilinear_bwd_f16", gy.half().data_ptr(), C, o16.data_ptr(), C, B, Hi, Wi, Ho, Wo, C, sc, sc, 1, s)
+        L.call("hyres_bilinear_bwd_f16", gy16.data_ptr(), C, o16.data_ptr(), C, B, Hi, Wi, Ho, Wo, C, sc, sc, 1, s)
         check(o16, o32, f"bilinear bwd {Ho}x{Wo}")
     # SE / spatial attention backward with fp16 gy / gx
     Cr = 4
@@ -437,3 +438,157 @@ def test_residual_unit_chain_fp16_activations_vs_torch():
     for i in range(3):
         assert rel_err(wp[i].grad.cpu(), wd[i].grad.float()) < 1e-4, i
         assert rel_err(bp[i].grad.cpu(), bd[i].grad.float()) < 1e-4, i
+
+
+@pytest.mark.parametrize("acc", [0, 1])
+def test_stream_hf_sa_bwd_epilogue(acc):
+    """conv1x1_stream_hf_kernel's SA_BWD build (round 6): MultiScaleRefine's fusion input-gradient 64 -> 192 under AMP
+    with SpatialAttention's mean / max backward in the epilogue — y = fp16((W^T gs + d mean / C) + [c == argmax] d max
+    (+ old y)), fp16 gs and W on the f16 MFMA. vs float64 torch on the same fp16 operands: one fp16 rounding (1e-3
+    max-norm); the launcher's own label names the kernel."""
+    from hyres_hip import _lib as L
+    from hyres_hip import ops as O
+    D = dev()
+    B, H, W = 2, 96, 96
+    P = B * H * W
+    gs = _h(_rand((P, 64), 61)).half().to(D)
+    w = _rand((192, 64), 62, 0.125).to(D)
+    gm = _rand((P, 2), 63).to(D)
+    am = torch.randint(0, 192, (P,), generator=torch.Generator().manual_seed(64), dtype=torch.int32).to(D)
+    old = _h(_rand((P, 192), 65)).half().to(D)
+    y = old.clone() if acc else torch.empty(P, 192, device=D, dtype=torch.float16)
+    g = O._geom("hyres_geom_conv2d", B, H, W, 64, 64, 192, 192, 1, 1, 1, 0, 1)
+    e = L.Epilogue()
+    e.kind = L.EPI_SA_BWD
+    e.aux0, e.ld0 = gm.data_ptr(), 2
+    e.aux2 = am.data_ptr()
+    e.f16_operands = 1
+    e.io_f16 = L.IO_X16 | L.IO_Y16
+    e.accumulate = acc
+    assert O.conv_variant(g, e, False) == f"conv1x1_stream_hf_kernel<6, 4, {8 | 4 * acc}>"
+    O._launch_conv(g, gs.data_ptr(), w, 64, y.data_ptr(), e)
+    torch.cuda.synchronize()
+    gmd = gm.double().cpu()
+    ref = gs.double().cpu() @ w.half().double().cpu().T + gmd[:, :1]
+    ref += torch.nn.functional.one_hot(am.long().cpu(), 192).double() * gmd[:, 1:]
+    if acc:
+        ref += old.double().cpu()
+    assert rel_err(y.float().cpu(), ref) < 1e-3
+
+
+def _amp_head(fold, m, multi, gy, D):
+    from hyres_hip import _lib as L
+    from hyres_hip import ops as O
+    from hyres_hip import refine_ops as R
+    for p in m.parameters():
+        p.grad = None
+    tape = O.Tape()
+    xn = O.Node(O.to_nhwc(multi.to(D), rg=True).v.half(), rg=True)
+    with torch.autocast("cuda", dtype=torch.float16), O.f16_region():
+        assert R.sa_fold_amp_ok(tape, xn, 64)
+        if fold:
+            hn = R.sa_fold_fusion(tape, xn, m.spatial_att.conv.weight, m.fusion[0].weight, m.fusion[0].bias,
+                                  m.fusion[1].weight)
+        else:
+            hn = m.fusion[0].hip(tape, m.spatial_att.hip_mul(tape, xn), act=L.ACT_PRELU, slope=m.fusion[1].weight)
+        assert hn.half
+        yn = m.fusion[2].hip(tape, hn)
+    yn.set_grad(O.nchw_grad_to_nhwc(gy.to(D)))
+    tape.backward()
+    torch.cuda.synchronize()
+    assert xn.grad().dtype == torch.float16
+    out = {"y": O.to_nchw(yn).float().cpu(), "dmulti": O.to_nchw_grad(xn).float().cpu()}
+    for k, p in m.named_parameters():
+        if k.startswith(("fusion", "spatial_att")):
+            out[k] = p.grad.cpu()
+    return out
+
+
+def test_refine_fusion_head_sa_fold_amp():
+    """MultiScaleRefine's head (enhancement.py:105-109) in AMP training with fp16 activations and gradients: the
+    SpatialAttention multiply folded into the fusion 1x1 (refine_ops.sa_fold_fusion's round-6 AMP build: ROWSCALE
+    forward on fp16 operands, hyres_sa_fold_bwd_f16, the SA_BWD epilogue on conv1x1_stream_hf_kernel) and unfused
+    (spatial_attention_mul + Sequential), each vs float64 torch without fp16 rounding: output, d multi and every
+    parameter gradient within the AMP rounding (2e-2 max-norm; the slope, one cancelled sum, 5e-2; d multi 6e-2: the
+    unfused chain measures 4.8e-2 on it here, the fold 4.7e-2 — fp16 gradients through the 7x7 map), and the fold
+    no less accurate than the unfused chain on any of them (1.5x + 1e-3). One channel per pixel holds the unique
+    maximum (1.0): fp16 ties at the max would move the max-pool's gradient between channels in either path."""
+    import models.layers.enhancement as EH
+    D = dev()
+    B, C, H, W = 2, 192, 96, 96
+    torch.manual_seed(11)
+    m = EH.MultiScaleRefine(3, 64)
+    multi = _h(_rand((B, C, H, W), 41, 0.9))
+    top = torch.randint(0, C, (B, 1, H, W), generator=torch.Generator().manual_seed(43))
+    multi.scatter_(1, top, 1.0)
+    gy = _rand((B, 3, H, W), 42)
+    sd = {k: v.detach().double().clone().requires_grad_(True) for k, v in m.state_dict().items()
+          if k.startswith(("fusion", "spatial_att"))}
+    sd["fusion.0.bias"].data.add_(0.05)
+    xr = multi.double().requires_grad_(True)
+    a = torch.sigmoid(F.conv2d(torch.cat([xr.mean(1, keepdim=True), xr.max(1, keepdim=True)[0]], 1),
+                               sd["spatial_att.conv.weight"], None, padding=3))
+    h = F.prelu(F.conv2d(xr * a, sd["fusion.0.weight"], sd["fusion.0.bias"]), sd["fusion.1.weight"])
+    yr = F.conv2d(h, sd["fusion.2.weight"], sd["fusion.2.bias"], padding=1)
+    yr.backward(gy.double())
+    ref = {"y": yr.detach(), "dmulti": xr.grad}
+    ref.update({k: v.grad for k, v in sd.items()})
+    m = m.to(D)
+    with torch.no_grad():
+        for k, v in m.named_parameters():
+            if k in sd:
+                v.copy_(sd[k].detach().float())
+    errs = {}
+    for fold in (True, False):
+        got = _amp_head(fold, m, multi, gy, D)
+        errs[fold] = {k: rel_err(got[k], ref[k]) for k in ref}
+        print("fold" if fold else "unfused", {k: f"{v:.1e}" for k, v in errs[fold].items()})
+    for fold in (True, False):
+        bad = {k: v for k, v in errs[fold].items() if v > {"fusion.1.weight": 5e-2, "dmulti": 6e-2}.get(k, 2e-2)}
+        assert not bad, (fold, errs[fold])
+    worse = {k: (errs[True][k], errs[False][k]) for k in ref if errs[True][k] > 1.5 * errs[False][k] + 1e-3}
+    assert not worse, worse
+
+
+@pytest.mark.parametrize("g16", [1, 0])
+def test_sa_fold_bwd_f16_matches_fp32_kernel(g16):
+    """hyres_sa_fold_bwd_f16 (fp16 pre-activation; fp16 or fp32 gy / gs) vs hyres_sa_fold_bwd on the same fp16-
+    representable values: gs within one fp16 rounding of the fp32 kernel's (1 ulp), glogit / d bias / d slope to fp32
+    summation order (1e-5). A ragged pixel count, both PReLU sides, accumulation into existing d bias / d slope."""
+    from hyres_hip import _lib as L
+    D = dev()
+    P, C = 2 * 37 * 41, 64
+    pre = _h(_rand((P, C), 71)).to(D)
+    gy = _h(_rand((P, C), 72)).to(D)
+    attn = torch.rand(P, generator=torch.Generator().manual_seed(73)).to(D)
+    bias = _rand((C,), 74, 0.1).to(D)
+    slope = torch.full((1,), 0.25, device=D)
+    ws = torch.empty(L.load().hyres_sa_fold_workspace_bytes(P, C) // 4 + 1, device=D)
+    gdt = torch.float16 if g16 else torch.float32
+    pre16, gyc = pre.half(), gy.to(gdt)  # held: a temporary's pointer would be recycled before the call
+    outs = {}
+    for name, f16 in (("f32", False), ("f16", True)):
+        gs = torch.empty(P, C, device=D, dtype=gdt if f16 else torch.float32)
+        gl = torch.empty(P, device=D)
+        db = torch.full((C,), 0.5, device=D)
+        ds = torch.full((1,), 0.5, device=D)
+        if f16:
+            L.call("hyres_sa_fold_bwd_f16", pre16.data_ptr(), C, gyc.data_ptr(), C, attn.data_ptr(),
+                   bias.data_ptr(), slope.data_ptr(), gs.data_ptr(), gl.data_ptr(), db.data_ptr(), ds.data_ptr(), P, C,
+                   ws.data_ptr(), ws.numel() * 4, g16, L.stream())
+        else:
+            L.call("hyres_sa_fold_bwd", pre.data_ptr(), C, gy.data_ptr(), C, attn.data_ptr(), bias.data_ptr(),
+                   slope.data_ptr(), gs.data_ptr(), gl.data_ptr(), db.data_ptr(), ds.data_ptr(), P, C, ws.data_ptr(),
+                   ws.numel() * 4, L.stream())
+        torch.cuda.synchronize()
+        outs[name] = (gs.clone(), gl.clone(), db.clone(), ds.clone())
+    (gs32, gl32, db32, ds32), (gs16, gl16, db16, ds16) = outs["f32"], outs["f16"]
+    assert bool((pre < 0).any()) and bool((pre > 0).any())
+    if g16:
+        a = gs16.view(-1) + 0
+        b = gs32.half().view(-1) + 0
+        assert int((a.view(torch.int16).int() - b.view(torch.int16).int()).abs().max()) <= 1
+    else:
+        assert rel_err(gs16.cpu(), gs32.cpu()) < 1e-6
+    assert rel_err(gl16.cpu(), gl32.cpu()) < 1e-5
+    assert rel_err(db16.cpu(), db32.cpu()) < 1e-5 and rel_err(ds16.cpu(), ds32.cpu()) < 1e-5
