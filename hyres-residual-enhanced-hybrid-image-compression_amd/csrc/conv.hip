@@ -2006,8 +2006,13 @@ template <int NT, int KS, int F>
 constexpr int stream_b6_vgprs() {
     return 256;
 }
+// the forms whose LDS (weight planes + epilogue scratch > 80 KB) admits one block per CU: one wave per SIMD
+template <int NT, int KS>
+constexpr bool stream_b6_one_block() {
+    return NT == 6 || KS == 12;
+}
 template <int NT, int KS, int F, bool CE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 6 ? 1 : 512 / stream_b6_vgprs<NT, KS, F>())))
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(stream_b6_one_block<NT, KS>() ? 1 : 512 / stream_b6_vgprs<NT, KS, F>())))
 void conv1x1_stream_b6_kernel(const ConvArgs a) {
     constexpr int K = 16 * KS, KP = K + 8, CO = 32 * NT;
     constexpr bool RES = (F & 1) != 0, MASK = (F & 2) != 0, ACC = (F & 4) != 0;
@@ -2016,6 +2021,11 @@ void conv1x1_stream_b6_kernel(const ConvArgs a) {
     // The per-pixel operands are loaded once per 32-pixel tile, the next tile's while this one multiplies
     constexpr bool SAB = (F & 8) != 0;
     static_assert(!SAB || (CE && !RES && !MASK), "SA_BWD: the coalesced epilogue, no residual / mask");
+    // RS (F & 16, round 6): HYRES_EPI_ROWSCALE — MultiScaleRefine's fusion 1x1 in training with SpatialAttention folded
+    // (192 -> 64 at 256^2, refine_ops.sa_fold_fusion): o = acc * aux1[p] + bias, then out2 (the pre-activation) and the
+    // PReLU; the per-pixel scale is loaded once per tile like SAB's operands
+    constexpr bool RS = (F & 16) != 0;
+    static_assert(!RS || (CE && !RES && !MASK && !ACC && !SAB), "ROWSCALE: the coalesced epilogue, no other operand");
     constexpr int WPL = CO * KP;  // bf16 per weight plane
     __shared__ __attribute__((aligned(16))) __bf16 Ws[3 * WPL];
     __shared__ __attribute__((aligned(16))) float bs[CO];
@@ -2024,8 +2034,9 @@ void conv1x1_stream_b6_kernel(const ConvArgs a) {
     constexpr int EP = 36;
     __shared__ __attribute__((aligned(16))) float Es[CE ? 4 * 32 * EP : 4];
     // exactly 2 or 4 waves' worth of VGPRs: no room for another kernel's wave on these SIMDs. NT = 6 (the 64 -> 192
-    // SA_BWD form): 102 KB of LDS admit one block per CU, i.e. one wave per SIMD — it takes all 512 registers
-    if constexpr (NT == 6) asm volatile("" ::: "v255", "a255");
+    // SA_BWD form, 102 KB of LDS) and KS = 12 (the 192 -> 64 ROWSCALE form, 95 KB) admit one block per CU, i.e. one
+    // wave per SIMD — they take all 512 registers
+    if constexpr (stream_b6_one_block<NT, KS>()) asm volatile("" ::: "v255", "a255");
     else if constexpr (stream_b6_vgprs<NT, KS, F>() == 128) asm volatile("" ::: "v127");
     else asm volatile("" ::: "v255");
     const hyres_conv_geom& g = a.g;
@@ -2094,6 +2105,18 @@ void conv1x1_stream_b6_kernel(const ConvArgs a) {
             }
         }
     };
+    float rsc[RS ? 4 : 1], rscn[RS ? 4 : 1];
+    const __amdgpu_buffer_rsrc_t r_rs = opnd_rsrc(RS ? e.aux1 : nullptr, npix * e.ld1 * 4);
+    auto load_rs = [&](int tile, float (&r1)[RS ? 4 : 1]) {
+        if constexpr (RS) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int p = tile * 32 + cr + 8 * q;
+                const bool ok = tile < ntile && p < a.M;
+                r1[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r_rs, ok ? p * e.ld1 * 4 : OOR, 0, 0));
+            }
+        }
+    };
     auto load_epi = [&](int tile, int t, int set) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -2108,8 +2131,10 @@ void conv1x1_stream_b6_kernel(const ConvArgs a) {
         for (int u = 0; u < 2; ++u) xv[s][u] = bload4(xr, xoff(gw, s, u));
     load_epi(gw, 0, 0);
     load_sab(gw, sg, si);
+    load_rs(gw, rsc);
     for (int tile = gw; tile < ntile; tile += nw) {
         load_sab(tile + nw, sgn, sin_);
+        load_rs(tile + nw, rscn);
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
             const int cur = SETS == 2 ? (t & 1) : 0;
@@ -2172,6 +2197,12 @@ void conv1x1_stream_b6_kernel(const ConvArgs a) {
 #pragma unroll
                     for (int c = 0; c < 4; ++c) o[c] = av4[c] + sg[q].x + (n + c == si[q] ? sg[q].y : 0.f);
                 }
+                if constexpr (RS) {  // epi_store4's ROWSCALE: (acc * scale) + bias
+                    o[0] = av.x * rsc[q] + b4.x;
+                    o[1] = av.y * rsc[q] + b4.y;
+                    o[2] = av.z * rsc[q] + b4.z;
+                    o[3] = av.w * rsc[q] + b4.w;
+                }
                 if constexpr (RES) {
                     o[0] += eres[cur][q].x; o[1] += eres[cur][q].y; o[2] += eres[cur][q].z; o[3] += eres[cur][q].w;
                 }
@@ -2205,6 +2236,10 @@ void conv1x1_stream_b6_kernel(const ConvArgs a) {
                 sg[q] = sgn[q];
                 si[q] = sin_[q];
             }
+        }
+        if constexpr (RS) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) rsc[q] = rscn[q];
         }
     }
 }
@@ -3146,10 +3181,16 @@ static int stream_b6_cfg(const hyres_conv_geom* g, const hyres_epilogue* e) {
             return 0;
         return 6 | (4 << 4) | ((8 | (e->accumulate ? 4 : 0)) << 8);
     }
-    if (e->kind != HYRES_EPI_BIAS) return 0;
     if (g->nphase != 1 || g->ntaps != 1 || g->ish != 1 || g->isw != 1 || g->dh[0] != 0 || g->dw[0] != 0) return 0;
     if (g->Hi != g->Hq || g->Wi != g->Wq || g->Ho != g->Hq || g->Wo != g->Wq) return 0;
     if ((long long)g->B * g->Hq * g->Wq < 65536) return 0;
+    if (e->kind == HYRES_EPI_ROWSCALE) {  // round 6: the fusion 1x1 forward with SpatialAttention folded, 192 -> 64
+        if (g_tune[11] == 0 || g_tune[21] == 0 || g->Ci != 192 || g->Co != 64 || e->res || e->accumulate ||
+            (e->act != HYRES_ACT_NONE && e->act != HYRES_ACT_RELU && e->act != HYRES_ACT_PRELU))
+            return 0;
+        return 2 | (12 << 4) | (16 << 8);
+    }
+    if (e->kind != HYRES_EPI_BIAS) return 0;
     const bool shape = (g->Ci == 64 && (g->Co == 64 || g->Co == 128)) || (g->Ci == 128 && g->Co == 64);
     if (!shape) return 0;
     const int F = (e->res ? 1 : 0) | (e->act == HYRES_ACT_RELU_MASK ? 2 : 0) | (e->accumulate ? 4 : 0);
@@ -3212,6 +3253,7 @@ static int launch_stream_b6(const ConvArgs& a, int cfg, hipStream_t st) {
     const int nt = cfg & 15, ks = (cfg >> 4) & 15, f = cfg >> 8;
     if (nt == 6 && ks == 4 && f == 8) return launch_stream_b6_ce<6, 4, 8, true>(a, st);
     if (nt == 6 && ks == 4 && f == 12) return launch_stream_b6_ce<6, 4, 12, true>(a, st);
+    if (nt == 2 && ks == 12 && f == 16) return launch_stream_b6_ce<2, 12, 16, true>(a, st);
     if (nt == 2 && ks == 4) return launch_stream_b6_f<2, 4>(a, f, st);
     if (nt == 4 && ks == 4) return launch_stream_b6_f<4, 4>(a, f, st);
     if (nt == 2 && ks == 8) return launch_stream_b6_f<2, 8>(a, f, st);
@@ -3385,10 +3427,11 @@ int hyres_conv_forward(const hyres_conv_geom* g, const float* x, const float* w2
     a.slab = nullptr;
     {
         auto al = [](const void* p, int ld) { return p == nullptr || (aligned16(p) && ld % 4 == 0); };
-        // HYRES_EPI_SA_BWD reads aux0 ([P][2]) and aux2 (argmax) one scalar per pixel: no alignment needed
-        const bool sa = e->kind == HYRES_EPI_SA_BWD;
+        // HYRES_EPI_SA_BWD reads aux0 ([P][2]) and aux2 (argmax), HYRES_EPI_ROWSCALE aux1 (the scale), one scalar per
+        // pixel: no alignment needed
+        const bool sa = e->kind == HYRES_EPI_SA_BWD, rs = e->kind == HYRES_EPI_ROWSCALE;
         a.vec4 = g->Co % 4 == 0 && al(y, g->ldy) && al(e->bias, 4) && al(e->res, e->ldres) && al(e->out2, e->ldo2) &&
-                 (sa || al(e->aux0, e->ld0)) && al(e->aux1, e->ld1) && (sa || al(e->aux2, e->ld2));
+                 (sa || al(e->aux0, e->ld0)) && (rs || al(e->aux1, e->ld1)) && (sa || al(e->aux2, e->ld2));
     }
     {
         const long long npo = (long long)g->B * g->Ho * g->Wo;

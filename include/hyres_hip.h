@@ -213,7 +213,9 @@ int hyres_conv_plan(const hyres_conv_geom* g, const hyres_epilogue* e, int* tile
                                        * per chunk, conv_fwd_b6db_kernel): 1 always, -1 on grids of <= 16384 output pixels,
                                        * 0 (default) never (one buffer, two barriers; faster in the graphed step); bit-identical */
 #define HYRES_TUNE_STREAM_SAB 21      /* 1 (default): the SA_BWD input-gradient of MultiScaleRefine's fusion 1x1 (64 -> 192 on
-                                       * >= 65536 pixels) on conv1x1_stream_b6_kernel<6, 4, 8 | acc>; 0: the implicit GEMM */
+                                       * >= 65536 pixels) on conv1x1_stream_b6_kernel<6, 4, 8 | acc>, its ROWSCALE forward
+                                       * (192 -> 64) on <2, 12, 16>, and under AMP the SA_BWD input-gradient on
+                                       * conv1x1_stream_hf_kernel<6, 4, 8 | acc>; 0: the implicit GEMMs */
 #define HYRES_TUNE_WGRAD_HALO5_PF 22  /* 1: the 5-tap-row halo weight gradients (5x5, stride 1 / 2) also on the two-chunks-
                                        * ahead kernel (with key 16 = 2; bit-identical); 0 (default): one chunk ahead — no
                                        * gain per launch or in the step (profiles/r6v_wg5.txt, r6v_wg5_step_ab.txt) */

@@ -156,3 +156,65 @@ def test_stream_b6_sa_bwd_matches_fp64(acc):
     assert name_s == f"conv1x1_stream_b6_kernel<6, 4, {8 | (4 if acc else 0)}, true>", name_s
     assert not name_t.startswith("conv1x1_stream_b6"), name_t
     assert err_s < 2e-6 and err_s <= 2 * err_t + 1e-9, (err_s, err_t)
+
+
+def _run_rowscale(act, stream_on):
+    """The HYRES_EPI_ROWSCALE forward of MultiScaleRefine's fusion 1x1 with SpatialAttention folded (192 -> 64):
+    y = act(attn[p] * (W x)[p] + b), out2 = the pre-activation, through the C-ABI on the streaming kernel or the
+    implicit GEMM."""
+    from hyres_hip import _lib as L
+    from hyres_hip import ops as O
+    D = dev()
+    B, H, W = 5, 117, 117
+    P, Ci, Co = B * H * W, 192, 64
+    x = _rand((P, Ci), 21).to(D)
+    w = _rand((Co, Ci, 1, 1), 22, Ci ** -0.5).to(D)
+    b = _rand((Co,), 23, 0.1).to(D)
+    sc = torch.rand(P, generator=torch.Generator().manual_seed(24)).to(D)
+    slope = torch.full((1,), 0.25, device=D)
+    y = torch.full((P, Co), float("nan"), device=D)
+    pre = torch.full((P, Co), float("nan"), device=D)
+    g = O._geom("hyres_geom_conv2d", B, H, W, Ci, Ci, Co, Co, 1, 1, 1, 0, 1)
+    w2 = torch.empty((Co, Ci), device=D)
+    L.call("hyres_conv_weight_prep", ctypes.byref(g), w.data_ptr(), w2.data_ptr(), 0, Ci, Co, 1, 1, 0, None, L.stream())
+    e = L.Epilogue()
+    e.kind = L.EPI_ROWSCALE
+    e.act = act
+    e.bias = b.data_ptr()
+    e.slope = slope.data_ptr()
+    e.aux1, e.ld1 = sc.data_ptr(), 1
+    e.out2, e.ldo2 = pre.data_ptr(), Co
+    old_key = ctypes.c_int(0)
+    L.call("hyres_conv_tuning", 21, 1 if stream_on else 0, ctypes.byref(old_key))
+    try:
+        name = O.conv_variant(g, e, False)
+        L.call("hyres_conv_forward", ctypes.byref(g), x.data_ptr(), w2.data_ptr(), Ci, y.data_ptr(), ctypes.byref(e),
+               None, 0, L.stream())
+        torch.cuda.synchronize()
+    finally:
+        L.call("hyres_conv_tuning", 21, old_key.value, None)
+    r = (x.double() @ w.double().reshape(Co, Ci).t()) * sc.double()[:, None] + b.double()
+    ra = r
+    if act == L.ACT_PRELU:
+        ra = torch.where(r >= 0, r, 0.25 * r)
+    elif act == L.ACT_RELU:
+        ra = r.clamp_min(0)
+    return name, max(rel_err(y.double().cpu(), ra.cpu()), rel_err(pre.double().cpu(), r.cpu())), y
+
+
+@pytest.mark.parametrize("act", ["prelu", "none", "relu"])
+def test_stream_b6_rowscale_matches_fp64(act):
+    """conv1x1_stream_b6_kernel<2, 12, 16> (round 6, hyres_conv_tuning key 21): the fusion 1x1's ROWSCALE forward
+    192 -> 64 with the pre-activation copy, on a ragged pixel count vs fp64 (2e-6 normwise, no worse than twice the
+    implicit GEMM it replaces on the same call)."""
+    from hyres_hip import _lib as L
+    a = {"prelu": L.ACT_PRELU, "none": L.ACT_NONE, "relu": L.ACT_RELU}[act]
+    name_s, err_s, y_s = _run_rowscale(a, True)
+    name_t, err_t, y_t = _run_rowscale(a, False)
+    # the two kernels sum K in different orders: equal outputs would mean the stream build never ran (the label is
+    # the launcher's choice function, which does not see pointer alignment)
+    assert not torch.equal(y_s, y_t)
+    print(f"ROWSCALE 192->64 {act}: {name_s} {err_s:.2e}, {name_t} {err_t:.2e}")
+    assert name_s == "conv1x1_stream_b6_kernel<2, 12, 16, true>", name_s
+    assert not name_t.startswith("conv1x1_stream_b6"), name_t
+    assert err_s < 2e-6 and err_s <= 2 * err_t + 1e-9, (err_s, err_t)
