@@ -111,6 +111,7 @@ for ph in "$@"; do
     gate)  scripts/gpu_run.sh "gate:200:python -u -m pytest tests -x -v --timeout 120 --timeout-method thread -m gpu -s -k 'attn_gate or amp or sa_fold or stream_hf or refine'" || exit $? ;;
     rs)    scripts/gpu_run.sh "rstest:300:python -u -m pytest tests/test_stream_b6_gpu.py tests/test_parity_gpu.py -x -v --timeout 180 --timeout-method thread -m gpu -k 'rowscale or sa_bwd or sa_fold or c2_size'" || exit $?
            bash scripts/serial_one.sh $tag || exit $? ;;
+    ab11)  bash scripts/tune_ab.sh $tag "default=" "nosa21=HYRES_TUNE=21=0" || exit $? ;;
     *) echo "unknown phase $ph"; exit 2 ;;
   esac
 done
