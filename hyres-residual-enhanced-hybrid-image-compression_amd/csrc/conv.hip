@@ -2009,7 +2009,7 @@ constexpr int stream_b6_vgprs() {
 // the forms whose LDS (weight planes + epilogue scratch > 80 KB) admits one block per CU: one wave per SIMD
 template <int NT, int KS>
 constexpr bool stream_b6_one_block() {
-    return NT == 6 || KS == 12;
+    return NT == 6 || KS == 12 || (NT == 4 && KS == 8);
 }
 template <int NT, int KS, int F, bool CE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(stream_b6_one_block<NT, KS>() ? 1 : 512 / stream_b6_vgprs<NT, KS, F>())))
@@ -3191,9 +3191,13 @@ static int stream_b6_cfg(const hyres_conv_geom* g, const hyres_epilogue* e) {
         return 2 | (12 << 4) | (16 << 8);
     }
     if (e->kind != HYRES_EPI_BIAS) return 0;
-    const bool shape = (g->Ci == 64 && (g->Co == 64 || g->Co == 128)) || (g->Ci == 128 && g->Co == 64);
+    const bool shape = (g->Ci == 64 && (g->Co == 64 || g->Co == 128)) || (g->Ci == 128 && g->Co == 64) ||
+                       (g->Ci == 128 && g->Co == 128);
     if (!shape) return 0;
     const int F = (e->res ? 1 : 0) | (e->act == HYRES_ACT_RELU_MASK ? 2 : 0) | (e->accumulate ? 4 : 0);
+    // 128 -> 128 (round 6, the GDN-side 1x1s at 128^2): 122 KB of LDS, one wave per SIMD — built for the operand-free
+    // and ReLU-mask forms only
+    if (g->Ci == 128 && g->Co == 128 && F != 0 && F != 2) return 0;
     return (g->Co / 32) | ((g->Ci / 16) << 4) | (F << 8);
 }
 
@@ -3257,6 +3261,8 @@ static int launch_stream_b6(const ConvArgs& a, int cfg, hipStream_t st) {
     if (nt == 2 && ks == 4) return launch_stream_b6_f<2, 4>(a, f, st);
     if (nt == 4 && ks == 4) return launch_stream_b6_f<4, 4>(a, f, st);
     if (nt == 2 && ks == 8) return launch_stream_b6_f<2, 8>(a, f, st);
+    if (nt == 4 && ks == 8 && f == 0) return launch_stream_b6_one<4, 8, 0>(a, st);
+    if (nt == 4 && ks == 8 && f == 2) return launch_stream_b6_one<4, 8, 2>(a, st);
     return set_error(HYRES_E_ARG, "conv1x1_stream_b6: no instantiation for NT=%d KS=%d", nt, ks);
 }
 

@@ -131,11 +131,12 @@ def test_hand_issued_lds_reads_are_waited_for_before_use(disasm):
 def test_stream_b6_kernels_fill_the_vgpr_file(meta):
     """conv1x1_stream_b6_kernel (bf16x6 streaming 1x1, round 5) converts with v_cvt_pk_bf16_f32 and runs bf16 MFMAs:
     every instantiation (either epilogue path) allocates exactly 256 VGPRs (2 waves per SIMD) — no hole — and spills
-    nothing; the round-6 SA_BWD (NT = 6) and ROWSCALE (KS = 12) forms, one block per CU by their LDS, take all 512."""
+    nothing; the round-6 SA_BWD (NT = 6), ROWSCALE (KS = 12) and 128 -> 128 (NT = 4, KS = 8) forms, one block per CU by
+    their LDS, take all 512."""
     ks = _find(meta, "conv1x1_stream_b6_kernel")
     # (NT, KS) in {(2, 4), (4, 4), (2, 8)} x 8 epilogue-operand sets x coalesced epilogue on / off, + <6, 4, 8 | 12, true>
-    # + the ROWSCALE form <2, 12, 16, true>
-    assert len(ks) == 51
+    # + the ROWSCALE form <2, 12, 16, true> + <4, 8, 0 | 2> (128 -> 128) x coalesced on / off
+    assert len(ks) == 55
     for k in ks:
-        full = 512 if ("kernelILi6E" in k["name"] or "ELi12E" in k["name"]) else 256
+        full = 512 if ("kernelILi6E" in k["name"] or "ELi12E" in k["name"] or "kernelILi4ELi8E" in k["name"]) else 256
         assert k["alloc"] == full and kernel_meta.residency(k)["hole_vgprs"] == 0 and k["scratch"] == 0, k

@@ -88,9 +88,10 @@ def _run(Ci, Co, F, act, out2, stream_on, ce=1):
     return name, max(errs)
 
 
-@pytest.mark.parametrize("F", range(8))
-@pytest.mark.parametrize("Ci,Co", [(64, 128), (128, 64), (64, 64)])
+@pytest.mark.parametrize("Ci,Co,F", [(c, o, f) for (c, o) in ((64, 128), (128, 64), (64, 64)) for f in range(8)]
+                         + [(128, 128, 0), (128, 128, 2)])
 def test_stream_b6_matches_fp64(Ci, Co, F):
+    """(128, 128) (round 6): the operand-free and ReLU-mask forms only (one wave per SIMD by its LDS)."""
     from hyres_hip import _lib as L
     acts = [L.ACT_RELU, L.ACT_PRELU, L.ACT_NONE]
     act = acts[(F + Ci // 64) % 3]
