@@ -107,10 +107,39 @@ __device__ __forceinline__ void bw_range(float inv, int t, int in, int out, int&
 
 // one block row per input row (blockIdx.y = b*Hi + h): the vertical output range and weights are
 // block-uniform; threads over (w, channel group)
-template <int VEC, bool G = false>  // G: gy / gx fp16 (AMP fp16 gradients), fp32 sums
+// the bilinear PReLU fold's block partials (one per 256-thread block: 16,384 at 128^2 x 16) summed in a fixed order and
+// ADDED to the slope gradient, 8 loads in flight per thread
+__global__ __launch_bounds__(256) void slope_sum8_kernel(const float* part, int n, float* dst) {
+    __shared__ float red[256];
+    float s8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    int i = threadIdx.x;
+    for (; i + 7 * 256 < n; i += 8 * 256)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s8[k] += part[i + k * 256];
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+        if (i + k * 256 < n) s8[k] += part[i + k * 256];
+    red[threadIdx.x] = ((s8[0] + s8[1]) + (s8[2] + s8[3])) + ((s8[4] + s8[5]) + (s8[6] + s8[7]));
+    __syncthreads();
+    for (int k = 128; k > 0; k >>= 1) {
+        if (threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) dst[0] += red[0];
+}
+
+// PM (round 6, VEC == 4, acc == 0): the PReLU backward of the layer that produced the up-sampled map folded in —
+// MultiScaleRefine's scales 2 and 3 end in conv + PReLU before the up-sample (enhancement.py:89-95,98-103): gx =
+// pre > 0 ? g : slope * g with g the (G: fp16-rounded) gather sum, as prelu_bwd4_kernel on the stored gradient, and this
+// block's share of sum_{pre <= 0} pre * g in part[block] (PM = 1: pre fp32, 2: pre fp16)
+template <int VEC, bool G = false, int PM = 0>  // G: gy / gx fp16 (AMP fp16 gradients), fp32 sums
 __global__ __launch_bounds__(256) void bilinear_bwd_kernel(const float* gy, int ldgy, float* gx, int ldgx, int B,
                                                            int Hi, int Wi, int Ho, int Wo, int C, float sh, float sw,
-                                                           int acc) {
+                                                           int acc, const float* pre, int ldpre, const float* slope,
+                                                           float* part) {
+    static_assert(PM == 0 || VEC == 4, "the PReLU fold runs on the vector kernel");
+    float pslope = 0.f;
+    const float a = PM ? slope[0] : 0.f;
     const int CG = C / VEC;
     const int row = blockIdx.y;
     const int b = row / Hi, h = row - b * Hi;
@@ -145,7 +174,20 @@ __global__ __launch_bounds__(256) void bilinear_bwd_kernel(const float* gy, int 
             s.x += wh * rs.x; s.y += wh * rs.y; s.z += wh * rs.z; s.w += wh * rs.w;
         }
         const long long gp = gr + (long long)w * ldgx + c;
-        if constexpr (VEC == 4) {
+        if constexpr (PM != 0) {
+            if constexpr (G) {  // the unfused chain's stored fp16 gradient
+                s = make_float4((float)(_Float16)s.x, (float)(_Float16)s.y, (float)(_Float16)s.z, (float)(_Float16)s.w);
+            }
+            const float4 pv4 = ldv4<PM == 2>(pre, (long long)row * Wi * ldpre + (long long)w * ldpre + c);
+            const float pv[4] = {pv4.x, pv4.y, pv4.z, pv4.w};
+            float o[4] = {s.x, s.y, s.z, s.w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (!(pv[k] > 0.f)) pslope += pv[k] * o[k];
+                o[k] = pv[k] > 0.f ? o[k] : a * o[k];
+            }
+            stv4<G>(gx, gp, make_float4(o[0], o[1], o[2], o[3]));
+        } else if constexpr (VEC == 4) {
             if (acc) {
                 const float4 o = ldv4<G>(gx, gp);
                 s.x += o.x; s.y += o.y; s.z += o.z; s.w += o.w;
@@ -154,6 +196,13 @@ __global__ __launch_bounds__(256) void bilinear_bwd_kernel(const float* gy, int 
         } else {
             stv<G>(gx, gp, acc ? ldv<G>(gx, gp) + s.x : s.x);
         }
+    }
+    if constexpr (PM != 0) {  // wave sums (xor shuffles, a fixed order), then the four waves': one barrier per block
+        __shared__ float red[4];
+        for (int off = 32; off > 0; off >>= 1) pslope += __shfl_xor(pslope, off);
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = pslope;
+        __syncthreads();
+        if (threadIdx.x == 0) part[(long long)blockIdx.y * gridDim.x + blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
     }
 }
 
@@ -872,13 +921,55 @@ static int bilinear_bwd_impl(const float* gy, int ldgy, float* gx, int ldgx, int
     }
     if (vec)
         hipLaunchKernelGGL((bilinear_bwd_kernel<4, G>), grid, dim3(256), 0, as_stream(s), gy, ldgy, gx, ldgx, B, Hi, Wi,
-                           Ho, Wo, C, scale_h, scale_w, accumulate);
+                           Ho, Wo, C, scale_h, scale_w, accumulate, nullptr, 0, nullptr, nullptr);
     else
         hipLaunchKernelGGL((bilinear_bwd_kernel<1, G>), grid, dim3(256), 0, as_stream(s), gy, ldgy, gx, ldgx, B, Hi, Wi,
-                           Ho, Wo, C, scale_h, scale_w, accumulate);
+                           Ho, Wo, C, scale_h, scale_w, accumulate, nullptr, 0, nullptr, nullptr);
     return HY_LAUNCH_CHECK("bilinear_bwd");
 }
+static dim3 bilinear_bwd_grid(int B, int Hi, int Wi, int C) { return dim3(ceil_div((long long)Wi * (C / 4), 256), B * Hi); }
 }  // extern "C++"
+long long hyres_bilinear_bwd_prelu_workspace_bytes(int B, int Hi, int Wi, int C) {
+    const dim3 g = bilinear_bwd_grid(B, Hi, Wi, C);
+    return (long long)g.x * g.y * 4;
+}
+int hyres_bilinear_bwd_prelu(const void* gy, int ldgy, void* gx, int ldgx, int B, int Hi, int Wi, int Ho, int Wo, int C,
+                             float scale_h, float scale_w, const void* pre, int ldpre, const float* slope, float* dslope,
+                             void* ws, long long ws_bytes, int io, hyres_stream_t s) {
+    HY_REQUIRE(gy && gx && pre && slope && dslope && ws && io >= 0 && io <= 3, HYRES_E_ARG, "bilinear_bwd_prelu: NULL / io");
+    const bool G = io & 1, H = io & 2;
+    const unsigned ag = G ? 7u : 15u, ap = H ? 7u : 15u;
+    HY_REQUIRE(C % 4 == 0 && ldgy % 4 == 0 && ldgx % 4 == 0 && ldpre % 4 == 0 &&
+                   (reinterpret_cast<uintptr_t>(gy) & ag) == 0 && (reinterpret_cast<uintptr_t>(gx) & ag) == 0 &&
+                   (reinterpret_cast<uintptr_t>(pre) & ap) == 0,
+               HYRES_E_ALIGN, "bilinear_bwd_prelu: C %% 4 == 0, aligned rows");
+    HY_REQUIRE((long long)B * Hi <= 65535 && (long long)Wi * C < (1LL << 30), HYRES_E_SHAPE, "bilinear_bwd_prelu: too large");
+    HY_REQUIRE(ws_bytes >= hyres_bilinear_bwd_prelu_workspace_bytes(B, Hi, Wi, C), HYRES_E_WORKSPACE,
+               "bilinear_bwd_prelu: workspace");
+    const dim3 grid = bilinear_bwd_grid(B, Hi, Wi, C);
+    hipStream_t st = as_stream(s);
+    const float* g = (const float*)gy;
+    float* x = (float*)gx;
+    const float* p = (const float*)pre;
+    float* part = (float*)ws;
+#define HY_BBP(GG, PMV)                                                                                                  \
+    hipLaunchKernelGGL((bilinear_bwd_kernel<4, GG, PMV>), grid, dim3(256), 0, st, g, ldgy, x, ldgx, B, Hi, Wi, Ho, Wo, C, \
+                       scale_h, scale_w, 0, p, ldpre, slope, part)
+    if (G && H) {
+        HY_BBP(true, 2);
+    } else if (G) {
+        HY_BBP(true, 1);
+    } else if (H) {
+        HY_BBP(false, 2);
+    } else {
+        HY_BBP(false, 1);
+    }
+#undef HY_BBP
+    int rc = HY_LAUNCH_CHECK("bilinear_bwd_prelu");
+    if (rc) return rc;
+    hipLaunchKernelGGL(slope_sum8_kernel, dim3(1), dim3(256), 0, st, (const float*)part, (int)(grid.x * grid.y), dslope);
+    return HY_LAUNCH_CHECK("bilinear_bwd_prelu_final");
+}
 int hyres_bilinear_bwd(const float* gy, int ldgy, float* gx, int ldgx, int B, int Hi, int Wi, int Ho, int Wo, int C,
                        float scale_h, float scale_w, int accumulate, hyres_stream_t s) {
     return bilinear_bwd_impl<false>(gy, ldgy, gx, ldgx, B, Hi, Wi, Ho, Wo, C, scale_h, scale_w, accumulate, s);

@@ -158,6 +158,8 @@ _SIGS = {
     "hyres_bilinear_fwd": (_I, [_P, _I, _P, _I, _I, _I, _I, _I, _I, _I, _F, _F, _I, _P]),
     "hyres_bilinear_bwd": (_I, [_P, _I, _P, _I, _I, _I, _I, _I, _I, _I, _F, _F, _I, _P]),
     "hyres_bilinear_bwd_f16": (_I, [_P, _I, _P, _I, _I, _I, _I, _I, _I, _I, _F, _F, _I, _P]),
+    "hyres_bilinear_bwd_prelu_workspace_bytes": (_LL, [_I, _I, _I, _I]),
+    "hyres_bilinear_bwd_prelu": (_I, [_P, _I, _P, _I, _I, _I, _I, _I, _I, _I, _F, _F, _P, _I, _P, _P, _P, _LL, _I, _P]),
     "hyres_se_fwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _LL, _P]),
     "hyres_se_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _LL, _P]),
     "hyres_se_bwd_prelu": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _LL, _P]),

@@ -37,6 +37,19 @@ def bilinear(tape: Optional[Tape], x: Node, Ho: int, Wo: int, scale_h: float, sc
             return
         tgt, acc = x.grad_target()
         assert g.dtype == tgt.dtype
+        if (O.FOLD_PRELU and acc == 0 and x.prelu is not None and x.parent is None and Ho > x.H and Wo > x.W
+                and x.C % 4 == 0 and x.prelu[0].is_contiguous()):
+            # round 6: MultiScaleRefine's scales 2 / 3 end in conv + PReLU, whose output only this up-sample reads
+            # (enhancement.py:89-103): the PReLU backward rides on the up-sample's backward (its one gradient writer)
+            pre, slope = x.prelu
+            dslope = param_grad(slope) if slope.requires_grad else _empty((1,), x.device)
+            ws = _ws(L.load().hyres_bilinear_bwd_prelu_workspace_bytes(x.B, x.H, x.W, x.C), x.device, slot=1)
+            io = (1 if g.dtype == torch.float16 else 0) | (2 if pre.dtype == torch.float16 else 0)
+            L.call("hyres_bilinear_bwd_prelu", g.data_ptr(), y.grad_ld(), tgt.data_ptr(), x.grad_ld(), x.B, x.H, x.W,
+                   Ho, Wo, x.C, float(scale_h), float(scale_w), pre.data_ptr(), x.C, slope.data_ptr(),
+                   dslope.data_ptr(), ws.data_ptr(), ws.numel(), io, L.stream())
+            x.pmasked = True
+            return
         fn = "hyres_bilinear_bwd_f16" if g.dtype == torch.float16 else "hyres_bilinear_bwd"  # AMP fp16 gradients
         L.call(fn, g.data_ptr(), y.grad_ld(), tgt.data_ptr(), x.grad_ld(), x.B, x.H, x.W, Ho, Wo,
                x.C, float(scale_h), float(scale_w), acc, L.stream())

@@ -505,6 +505,15 @@ int hyres_spatial_attn_bwd_f16(const void* x, const float* w, const float* poole
 /* bilinear backward over fp16 gy / gx (AMP fp16 gradients; fp32 sums; 8B-aligned when C % 4 == 0) */
 int hyres_bilinear_bwd_f16(const void* gy, int ldgy, void* gx, int ldgx, int B, int Hi, int Wi, int Ho, int Wo,
                            int C, float scale_h, float scale_w, int accumulate, hyres_stream_t s);
+/* Round 6: the up-sample's backward with the PReLU backward of the layer that produced its input folded in
+ * (MultiScaleRefine scales 2 / 3: conv + PReLU, then the bilinear up-sample, enhancement.py:89-103): writes
+ * gx = pre > 0 ? g : slope * g (g = the gather sum, rounded to fp16 first with fp16 gradients) — NOT accumulated, the
+ * caller is the first writer — and ADDS dslope += sum_{pre <= 0} pre * g (deterministic block partials in ws).
+ * io: bit 0 gy / gx fp16, bit 1 pre fp16. C % 4 == 0, aligned rows; ws >= hyres_bilinear_bwd_prelu_workspace_bytes. */
+long long hyres_bilinear_bwd_prelu_workspace_bytes(int B, int Hi, int Wi, int C);
+int hyres_bilinear_bwd_prelu(const void* gy, int ldgy, void* gx, int ldgx, int B, int Hi, int Wi, int Ho, int Wo, int C,
+                             float scale_h, float scale_w, const void* pre, int ldpre, const float* slope, float* dslope,
+                             void* ws, long long ws_bytes, int io, hyres_stream_t s);
 
 /* ------------------------------------------------------------------------------------------ */
 /* losses and optimiser (src/losses/rd_loss.py:18-44, src/utils/engine.py:56-90)              */

@@ -108,7 +108,7 @@ for ph in "$@"; do
     tileh) scripts/gpu_run.sh "tileh:400:for t in -1 0 1 3 4; do for s in '--H 32 --Ci 96 --Co 96 --K 3 --relu' '--H 32 --Ci 192 --Co 96 --K 1 --relu' '--H 32 --Ci 96 --Co 192 --K 1 --res --relu' '--H 32 --Ci 384 --Co 192 --K 3 --relu' '--H 32 --Ci 640 --Co 512 --K 1' '--H 64 --Ci 128 --Co 192 --K 5 --stride 2'; do python3 scripts/conv_micro.py \$s --f16 --tile \$t | sed \"s/^/tile \$t /\"; done; done" || exit $?
            grep -h "us" gpurun_out/tileh.log > gpurun_out/${tag}_tileh.txt ;;
     ab10)  bash scripts/tune_ab.sh $tag "default=" "split128=HYRES_TUNE=6=128" "split192=HYRES_TUNE=6=192" || exit $? ;;
-    gate)  scripts/gpu_run.sh "gate:200:python -u -m pytest tests -x -v --timeout 120 --timeout-method thread -m gpu -s -k 'attn_gate or amp or sa_fold or stream_hf or refine'" || exit $? ;;
+    gate)  scripts/gpu_run.sh "gate:200:python -u -m pytest tests -x -v --timeout 120 --timeout-method thread -m gpu -s -k 'attn_gate or amp or sa_fold or stream_hf or refine or prelu or bilinear'" || exit $? ;;
     rs)    scripts/gpu_run.sh "rstest:300:python -u -m pytest tests/test_stream_b6_gpu.py tests/test_parity_gpu.py -x -v --timeout 180 --timeout-method thread -m gpu -k 'rowscale or sa_bwd or sa_fold or c2_size'" || exit $?
            bash scripts/serial_one.sh $tag || exit $? ;;
     ab11)  bash scripts/tune_ab.sh $tag "default=" "nosa21=HYRES_TUNE=21=0" || exit $? ;;

@@ -6,6 +6,7 @@ Tolerances (fp32 everywhere, BASELINE.json north_star: "within 1e-4 relative fp3
   * end-to-end x_hat / likelihoods: same bound, on elements whose quantisation decision agrees with the
     reference (a round() boundary flip changes y_hat by exactly 1 — reported as a fraction, must be rare).
 """
+import contextlib
 import ctypes
 
 import pytest
@@ -412,6 +413,68 @@ def test_refine_branch_fwd_bwd(branch):
         errs[k] = rel_err(p.grad.cpu(), ref[k].grad)
     bad = {k: v for k, v in errs.items() if v > (1e-3 if k in ("1.weight", "3.weight") else TOL)}
     assert not bad, errs
+
+
+@pytest.mark.parametrize("amp", [False, True])
+def test_bilinear_up_prelu_fold_matches_unfused(amp, monkeypatch):
+    """MultiScaleRefine's scales 2 / 3 (enhancement.py:89-103): conv + PReLU, then the bilinear up-sample. Round 6
+    folds the PReLU backward into the up-sample's backward (hyres_bilinear_bwd_prelu, refine_ops.bilinear) — against
+    the unfused prelu_bwd pass (HYRES_FOLD_PRELU=0) on the same inputs: d x and the conv's weight / bias gradients bit
+    for bit in fp32 (within fp16 rounding, 2e-3, under AMP with fp16 activations and gradients: the folded and the
+    separate kernel may contract slope * g into the fp16 store differently); the slope's gradient (the same products
+    summed in another order) at 1e-5 (AMP 1e-3). Both PReLU sides are populated and the fold must fire."""
+    from hyres_hip import _lib as L
+    from hyres_hip import ops as O
+    from hyres_hip import refine_ops as R
+    from hyres_hip.layers import Conv2d, PReLU, Sequential
+    D = dev()
+    B, C, H, W = 2, 64, 48, 40
+    torch.manual_seed(9)
+    blk = Sequential(Conv2d(C, C, 3, padding=1), PReLU()).to(D)
+    with torch.no_grad():
+        blk[0].bias.add_(0.02)
+    x = _rand((B, C, H, W), 61)
+    gy = _rand((B, C, 2 * H, 2 * W), 62)
+    calls = []
+    orig = L.call
+
+    def spy(fn, *a):
+        calls.append(fn)
+        return orig(fn, *a)
+
+    def run(fold):
+        monkeypatch.setattr(O, "FOLD_PRELU", fold)
+        for p in blk.parameters():
+            p.grad = None
+        calls.clear()
+        tape = O.Tape()
+        xn = O.to_nhwc(x.to(D), rg=True)
+        ctx = (torch.autocast("cuda", dtype=torch.float16), O.f16_region()) if amp else ()
+        with contextlib.ExitStack() as st:
+            for c in ctx:
+                st.enter_context(c)
+            h = blk.hip(tape, xn)
+            assert h.half == amp
+            yn = R.bilinear(tape, h, 2 * H, 2 * W, 0.5, 0.5)
+        yn.set_grad(O.nchw_grad_to_nhwc(gy.to(D)))
+        monkeypatch.setattr(L, "call", spy)
+        tape.backward()
+        monkeypatch.setattr(L, "call", orig)
+        torch.cuda.synchronize()
+        return (O.to_nchw_grad(xn).float().cpu(), {k: p.grad.cpu().clone() for k, p in blk.named_parameters()},
+                "hyres_bilinear_bwd_prelu" in calls)
+
+    dx0, g0, f0 = run(False)
+    dx1, g1, f1 = run(True)
+    assert f1 and not f0
+    for k in g0:
+        if k.endswith("1.weight"):  # the PReLU slope
+            assert rel_err(g1[k], g0[k]) < (1e-3 if amp else 1e-5), k
+        elif amp:
+            assert rel_err(g1[k], g0[k]) < 2e-3, k
+        else:
+            assert torch.equal(g1[k], g0[k]), k
+    assert torch.equal(dx1, dx0) if not amp else rel_err(dx1, dx0) < 2e-3
 
 
 @pytest.mark.parametrize("shape", [(2, 256, 128), (4, 128, 128)])
