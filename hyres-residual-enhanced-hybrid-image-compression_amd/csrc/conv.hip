@@ -1841,6 +1841,10 @@ __global__ __launch_bounds__(256, 2) void conv1x1_stream_hf_kernel(const ConvArg
     constexpr int K = 16 * KC, KP = K + 8, CO = 32 * NT, EP = 36;
     constexpr bool RES = (F & 1) != 0, MASK = (F & 2) != 0, ACC = (F & 4) != 0, SAB = (F & 8) != 0;
     static_assert(!SAB || (!RES && !MASK), "SA_BWD: no residual / mask");
+    // RS (F & 16, round 6, AMP training with SpatialAttention folded): HYRES_EPI_ROWSCALE, the fusion 1x1 forward
+    // 192 -> 64 (NT = 2, KC = 12) — o = acc * aux1[p] + bias, the pre-activation copy to out2 (fp16), then ReLU / PReLU
+    constexpr bool RS = (F & 16) != 0;
+    static_assert(!RS || (!RES && !MASK && !ACC && !SAB), "ROWSCALE: no other operand");
     static_assert(NT % 2 == 0, "operands alternate between two register sets per co tile");
     __shared__ __attribute__((aligned(16))) _Float16 Ws[CO * KP];
     __shared__ __attribute__((aligned(16))) float bs[CO];
@@ -1864,6 +1868,9 @@ __global__ __launch_bounds__(256, 2) void conv1x1_stream_hf_kernel(const ConvArg
     const __amdgpu_buffer_rsrc_t r_old = opnd_rsrc(ACC ? a.y : nullptr, npix * g.ldy * 2);
     const __amdgpu_buffer_rsrc_t r_gm = opnd_rsrc(SAB ? e.aux0 : nullptr, npix * e.ld0 * 4);
     const __amdgpu_buffer_rsrc_t r_am = opnd_rsrc(SAB ? e.aux2 : nullptr, npix * 4);
+    const __amdgpu_buffer_rsrc_t r_rs = opnd_rsrc(RS ? e.aux1 : nullptr, npix * e.ld1 * 4);
+    const float slope = (RS && e.act == HYRES_ACT_PRELU) ? e.slope[0] : 0.f;
+    _Float16* const o2 = reinterpret_cast<_Float16*>(e.out2);
     constexpr int OOR = (int)0x80000000;
     _Float16* const y = reinterpret_cast<_Float16*>(a.y);
     const int ntile = (a.M + 31) / 32;
@@ -1887,9 +1894,18 @@ __global__ __launch_bounds__(256, 2) void conv1x1_stream_hf_kernel(const ConvArg
             if constexpr (ACC) eold[set][q] = bload4h(r_old, ooff(tile, g.ldy, t, q));
         }
     };
-    // SA_BWD's per-pixel operands: one set per tile, two sets (the next tile's are issued with its X)
+    // SA_BWD's / ROWSCALE's per-pixel operands: one set per tile, two sets (the next tile's are issued with its X)
     float2 sgm[SAB ? 2 : 1][4];
     int sam[SAB ? 2 : 1][4];
+    float srs[RS ? 2 : 1][4];
+    auto load_rs = [&](int tile, int set) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int p = tile * 32 + cr + 8 * q;
+            const bool ok = tile < ntile && p < a.M;
+            srs[set][q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r_rs, ok ? p * e.ld1 * 4 : OOR, 0, 0));
+        }
+    };
     auto load_sab = [&](int tile, int set) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -1905,6 +1921,7 @@ __global__ __launch_bounds__(256, 2) void conv1x1_stream_hf_kernel(const ConvArg
     for (int j = 0; j < KC; ++j) xv[j] = load_x(gw, j);
     load_epi(gw, 0, 0);
     if constexpr (SAB) load_sab(gw, 0);
+    if constexpr (RS) load_rs(gw, 0);
     float* const es = Es + wave * 32 * EP;
     int tset = 0;
     for (int tile = gw; tile < ntile; tile += nw, tset ^= 1) {
@@ -1917,6 +1934,12 @@ __global__ __launch_bounds__(256, 2) void conv1x1_stream_hf_kernel(const ConvArg
                 if (t == NT - 1) {  // constant set indices (a dynamic one puts the arrays in scratch)
                     if (tset) load_sab(tile + nw, 0);
                     else load_sab(tile + nw, 1);
+                }
+            }
+            if constexpr (RS) {
+                if (t == NT - 1) {
+                    if (tset) load_rs(tile + nw, 0);
+                    else load_rs(tile + nw, 1);
                 }
             }
             floatx16 acc;
@@ -1950,6 +1973,20 @@ __global__ __launch_bounds__(256, 2) void conv1x1_stream_hf_kernel(const ConvArg
                     o[1] = av.y + gm.x + (n + 1 == mi ? gm.y : 0.f);
                     o[2] = av.z + gm.x + (n + 2 == mi ? gm.y : 0.f);
                     o[3] = av.w + gm.x + (n + 3 == mi ? gm.y : 0.f);
+                }
+                if constexpr (RS) {  // epi_store4's ROWSCALE: (acc * scale) + bias, out2, then the activation
+                    const float sc = tset ? srs[1][q] : srs[0][q];
+                    o[0] = av.x * sc + b4.x;
+                    o[1] = av.y * sc + b4.y;
+                    o[2] = av.z * sc + b4.z;
+                    o[3] = av.w * sc + b4.w;
+                    if (p < a.M)
+                        *reinterpret_cast<half4_t*>(o2 + (long long)p * e.ldo2 + n) =
+                            half4_t{(_Float16)o[0], (_Float16)o[1], (_Float16)o[2], (_Float16)o[3]};
+                    if (e.act == HYRES_ACT_PRELU) {
+#pragma unroll
+                        for (int c = 0; c < 4; ++c) o[c] = o[c] >= 0.f ? o[c] : slope * o[c];
+                    }
                 }
                 if constexpr (RES) {
                     const float4 r = h2f4(eres[cur][q]);
@@ -3146,7 +3183,17 @@ static int stream_h_nt(const hyres_conv_geom* g, const hyres_epilogue* e) {
 // ReLU / ReLU mask and at least one streamed operand (residual, mask, old y; without one: conv1x1_stream_h_kernel),
 // no out2, 16-byte X rows / 8-byte Y rows. Returns NT | KC << 4 | F << 8, or 0.
 static int stream_hf_cfg(const hyres_conv_geom* g, const hyres_epilogue* e) {
-    if (g_tune[17] == 0 || (e->io_f16 & 3) != 3 || !e->f16_operands || e->square_input || e->out2) return 0;
+    if (g_tune[17] == 0 || (e->io_f16 & 3) != 3 || !e->f16_operands || e->square_input) return 0;
+    if (e->kind == HYRES_EPI_ROWSCALE) {  // round 6: the fusion 1x1 forward under AMP with SpatialAttention folded
+        if (g_tune[21] == 0 || g->Ci != 192 || g->Co != 64 || e->res || e->accumulate || !e->out2 || e->ldo2 % 4 ||
+            (e->act != HYRES_ACT_NONE && e->act != HYRES_ACT_RELU && e->act != HYRES_ACT_PRELU) || g->nphase != 1 ||
+            g->ntaps != 1 || g->ish != 1 || g->isw != 1 || g->dh[0] != 0 || g->dw[0] != 0 || g->Hi != g->Hq ||
+            g->Wi != g->Wq || g->Ho != g->Hq || g->Wo != g->Wq || (long long)g->B * g->Hq * g->Wq < 16384 ||
+            g->ldx % 8 || g->ldy % 4)
+            return 0;
+        return 2 | (12 << 4) | (16 << 8);
+    }
+    if (e->out2) return 0;
     if (e->kind == HYRES_EPI_SA_BWD) {  // round 6: the fusion 1x1's input-gradient under AMP, 64 -> 192
         if (g_tune[21] == 0 || g->Ci != 64 || g->Co != 192 || e->act != HYRES_ACT_NONE || e->res || g->nphase != 1 ||
             g->ntaps != 1 || g->ish != 1 || g->isw != 1 || g->dh[0] != 0 || g->dw[0] != 0 || g->Hi != g->Hq ||
@@ -3299,6 +3346,7 @@ static int launch_stream_hf(const ConvArgs& a, int cfg, hipStream_t st) {
     const int nt = cfg & 15, kc = (cfg >> 4) & 15, f = cfg >> 8;
     if (nt == 6 && kc == 4 && f == 8) return launch_stream_hf_one<6, 4, 8>(a, st);
     if (nt == 6 && kc == 4 && f == 12) return launch_stream_hf_one<6, 4, 12>(a, st);
+    if (nt == 2 && kc == 12 && f == 16) return launch_stream_hf_one<2, 12, 16>(a, st);
     if (nt == 2 && kc == 4) return launch_stream_hf_f<2, 4>(a, f, st);
     if (nt == 2 && kc == 8) return launch_stream_hf_f<2, 8>(a, f, st);
     if (nt == 4 && kc == 4) return launch_stream_hf_f<4, 4>(a, f, st);
@@ -3545,7 +3593,7 @@ int hyres_conv_forward(const hyres_conv_geom* g, const float* x, const float* w2
         const long long xb = (long long)a.M * g->ldx * 2;
         if (cfg && mode == 0 && a.rsrc_ok && xb < 0x7FFFFFF0LL && aligned16(x) && aligned16(w2) && ldw % 4 == 0 &&
             (reinterpret_cast<uintptr_t>(y) & 7) == 0 && (reinterpret_cast<uintptr_t>(e->res) & 7) == 0 &&
-            (reinterpret_cast<uintptr_t>(e->aux0) & 7) == 0) {
+            (reinterpret_cast<uintptr_t>(e->aux0) & 7) == 0 && (reinterpret_cast<uintptr_t>(e->out2) & 7) == 0) {
             a.x_bytes = (int)xb;
             a.nsplit = 1;
             return launch_stream_hf(a, cfg, st);

@@ -592,3 +592,54 @@ def test_sa_fold_bwd_f16_matches_fp32_kernel(g16):
         assert rel_err(gs16.cpu(), gs32.cpu()) < 1e-6
     assert rel_err(gl16.cpu(), gl32.cpu()) < 1e-5
     assert rel_err(db16.cpu(), db32.cpu()) < 1e-5 and rel_err(ds16.cpu(), ds32.cpu()) < 1e-5
+
+
+@pytest.mark.parametrize("act", ["prelu", "none"])
+def test_stream_hf_rowscale_matches_tiles(act):
+    """conv1x1_stream_hf_kernel's ROWSCALE build (round 6): the AMP fusion forward 192 -> 64 with SpatialAttention
+    folded — y = act(attn[p] * (W x)[p] + b) and the fp16 pre-activation copy — against the tiled f16 kernel
+    (hyres_conv_tuning key 17 = 0) on the same call: the same fp16 products, at most 1 fp16 ulp apart (the epilogue's
+    multiply-add may contract differently); and vs float64 on the fp16 operands at 1e-3 (one fp16 rounding)."""
+    import ctypes
+    from hyres_hip import _lib as L
+    from hyres_hip import ops as O
+    D = dev()
+    B, H, W = 2, 96, 96
+    P, Ci, Co = B * H * W, 192, 64
+    x = _h(_rand((P, Ci), 81)).half().to(D)
+    w = _rand((Co, Ci), 82, Ci ** -0.5).to(D)
+    b = _rand((Co,), 83, 0.1).to(D)
+    sc = torch.rand(P, generator=torch.Generator().manual_seed(84)).to(D)
+    slope = torch.full((1,), 0.25, device=D)
+    g = O._geom("hyres_geom_conv2d", B, H, W, Ci, Ci, Co, Co, 1, 1, 1, 0, 1)
+    res = {}
+    for key in (1, 0):
+        y = torch.empty(P, Co, device=D, dtype=torch.float16)
+        pre = torch.empty(P, Co, device=D, dtype=torch.float16)
+        e = L.Epilogue()
+        e.kind = L.EPI_ROWSCALE
+        e.act = L.ACT_PRELU if act == "prelu" else L.ACT_NONE
+        e.bias = b.data_ptr()
+        e.slope = slope.data_ptr()
+        e.aux1, e.ld1 = sc.data_ptr(), 1
+        e.out2, e.ldo2 = pre.data_ptr(), Co
+        e.f16_operands = 1
+        e.io_f16 = L.IO_X16 | L.IO_Y16
+        old = ctypes.c_int(0)
+        L.call("hyres_conv_tuning", 17, key, ctypes.byref(old))
+        try:
+            name = O.conv_variant(g, e, False)
+            O._launch_conv(g, x.data_ptr(), w, Ci, y.data_ptr(), e)
+            torch.cuda.synchronize()
+        finally:
+            L.call("hyres_conv_tuning", 17, old.value, None)
+        res[key] = (name, y, pre)
+    assert res[1][0] == "conv1x1_stream_hf_kernel<2, 12, 16>", res[1][0]
+    assert not res[0][0].startswith("conv1x1_stream_hf"), res[0][0]
+    for i in (1, 2):
+        u = res[1][i].view(-1) + 0
+        v = res[0][i].view(-1) + 0
+        assert int((u.view(torch.int16).int() - v.view(torch.int16).int()).abs().max()) <= 1
+    r = (x.double() @ w.half().double().t()) * sc.double()[:, None] + b.double()
+    ra = torch.where(r >= 0, r, 0.25 * r) if act == "prelu" else r
+    assert rel_err(res[1][2].double().cpu(), r.cpu()) < 1e-3 and rel_err(res[1][1].double().cpu(), ra.cpu()) < 1e-3
