@@ -118,13 +118,13 @@ def cpu_baseline(args, budget_s):
 
 # scripts/check.sh <tag> pmc: the fp32 line's dominant kernel, and the AMP leg's dominant kernel from the same passes;
 # committed PMC summaries, newest first: the first one collected for the kernel being priced is used
-# (r6x: the final round-6 build; r6o: an earlier round-6 build, the D = 1 weight-resident launches; r5f: the bf16x6 weight-resident conv incl. its dilation-2 launches; r5s: before those; r4i: its round-4 build;
+# (r7w: the final round-6 build after the late folds; r6x: the round-6 build before them; r6o: an earlier round-6 build, the D = 1 weight-resident launches; r5f: the bf16x6 weight-resident conv incl. its dilation-2 launches; r5s: before those; r4i: its round-4 build;
 # r4b: the native fp32 one)
 PMC_TRAFFIC = [os.path.join(REPO, "profiles", f) for f in
                os.environ.get("HYRES_PMC_TRAFFIC",
-                              "r6x_pmc_traffic.json,r6o_pmc_traffic.json,r5f_pmc_traffic.json,r5s_pmc_traffic.json,r4i_pmc_traffic.json,r4b_pmc_traffic.json").split(",")]
+                              "r7w_pmc_traffic.json,r6x_pmc_traffic.json,r6o_pmc_traffic.json,r5f_pmc_traffic.json,r5s_pmc_traffic.json,r4i_pmc_traffic.json,r4b_pmc_traffic.json").split(",")]
 PMC_TRAFFIC_AMP = [os.path.join(REPO, "profiles", f) for f in
-                   os.environ.get("HYRES_PMC_TRAFFIC_AMP", "r6x_pmc_traffic_amp.json,r6o_pmc_traffic_amp.json,r5f_pmc_traffic_amp.json,r5s_pmc_traffic_amp.json").split(",")]
+                   os.environ.get("HYRES_PMC_TRAFFIC_AMP", "r7w_pmc_traffic_amp.json,r6x_pmc_traffic_amp.json,r6o_pmc_traffic_amp.json,r5f_pmc_traffic_amp.json,r5s_pmc_traffic_amp.json").split(",")]
 EAGER_TIMED = 3  # eager steps behind the live per-launch roofline timing
 # N > 1 default: the graphed step cut at the "hyper" marker with the finished segments' all-reduce between the two
 # replays; HYRES_DIST_MODE=graph+allreduce (reduce after one replay) / eager-overlap select the others
