@@ -215,7 +215,8 @@ class Node:
         routes it to conv3x3_wres_bf6_kernel (MultiScaleRefine's scale blocks, enhancement.py:89-95: the dilation-2
         conv's input-gradient). Replaces prelu_bwd of that PReLU; its slope gradient sum is added by the same call."""
         if not (FOLD_PRELU and acc == 0 and self.prelu is not None and self.parent is None and not self.half
-                and e.act == L.ACT_NONE and e.kind == L.EPI_BIAS and not e.accumulate and not e.io_f16):
+                and e.act == L.ACT_NONE and e.kind == L.EPI_BIAS and not e.accumulate and not e.io_f16
+                and not Trace.traced(self)):
             return
         pre, slope = self.prelu
         if pre.dtype != torch.float32 or not pre.is_contiguous():
@@ -340,6 +341,12 @@ class Trace:
                 d = to_nchw(node) > 0
             out[kind].append(d.cpu())
         return out
+
+    @classmethod
+    def traced(cls, node: "Node") -> bool:
+        """``node`` is a named trace point: the PReLU-backward folds skip it, since they store the gradient of the
+        pre-activation in the node's gradient buffer, and the trace reads the gradient of the node's own value."""
+        return cls.nodes is not None and any(v is node for v in cls.nodes.values())
 
     @classmethod
     def value(cls, name: str) -> torch.Tensor:

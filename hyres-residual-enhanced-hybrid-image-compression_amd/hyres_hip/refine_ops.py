@@ -38,7 +38,7 @@ def bilinear(tape: Optional[Tape], x: Node, Ho: int, Wo: int, scale_h: float, sc
         tgt, acc = x.grad_target()
         assert g.dtype == tgt.dtype
         if (O.FOLD_PRELU and acc == 0 and x.prelu is not None and x.parent is None and Ho > x.H and Wo > x.W
-                and x.C % 4 == 0 and x.prelu[0].is_contiguous()):
+                and x.C % 4 == 0 and x.prelu[0].is_contiguous() and not O.Trace.traced(x)):
             # round 6: MultiScaleRefine's scales 2 / 3 end in conv + PReLU, whose output only this up-sample reads
             # (enhancement.py:89-103): the PReLU backward rides on the up-sample's backward (its one gradient writer)
             pre, slope = x.prelu
@@ -87,6 +87,7 @@ def se_block(tape: Optional[Tape], x: Node, w1: torch.Tensor, w2: torch.Tensor) 
         assert g.dtype == tgt.dtype
         gx = tgt if acc == 0 else _empty((x.B, x.H, x.W, C), dev, tgt.dtype)
         if (O.FOLD_PRELU and acc == 0 and x.prelu is not None and x.parent is None and not x.half
+                and not O.Trace.traced(x)
                 and g.dtype == torch.float32 and x.prelu[0].dtype == torch.float32 and C % 4 == 0):
             # the producing PReLU's backward folded in (conv_in's act_in, enhancement.py:107-110): the SE block is
             # the only reader of PReLU(conv_in(x)), so its input-gradient is the PReLU output's whole gradient
