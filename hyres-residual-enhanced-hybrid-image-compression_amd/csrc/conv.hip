@@ -1845,6 +1845,10 @@ __global__ __launch_bounds__(256, 2) void conv1x1_stream_hf_kernel(const ConvArg
     // 192 -> 64 (NT = 2, KC = 12) — o = acc * aux1[p] + bias, the pre-activation copy to out2 (fp16), then ReLU / PReLU
     constexpr bool RS = (F & 16) != 0;
     static_assert(!RS || (!RES && !MASK && !ACC && !SAB), "ROWSCALE: no other operand");
+    // PM (F & 32, with SAB): conv1x1_stream_b6_kernel's PReLU mask on channels [0, 64), pre fp16; the gradient is
+    // rounded to fp16 first (the unfused chain's stored value)
+    constexpr bool PM = (F & 32) != 0;
+    static_assert(!PM || (SAB && !ACC), "PReLU mask: the SA_BWD form without accumulate");
     static_assert(NT % 2 == 0, "operands alternate between two register sets per co tile");
     __shared__ __attribute__((aligned(16))) _Float16 Ws[CO * KP];
     __shared__ __attribute__((aligned(16))) float bs[CO];
@@ -1885,13 +1889,17 @@ __global__ __launch_bounds__(256, 2) void conv1x1_stream_hf_kernel(const ConvArg
         const int p = tile * 32 + cr + 8 * q;
         return (tile < ntile && p < a.M) ? (p * ld + 32 * t + cc) * 2 : OOR;
     };
-    half4_t eres[RES ? 2 : 1][4], emask[MASK ? 2 : 1][4], eold[ACC ? 2 : 1][4];
+    half4_t eres[RES ? 2 : 1][4], emask[MASK ? 2 : 1][4], eold[ACC ? 2 : 1][4], epre[PM ? 2 : 1][4];
+    const __amdgpu_buffer_rsrc_t r_pm = opnd_rsrc(PM ? e.aux1 : nullptr, npix * e.ld1 * 2);
+    const float pslope_a = PM ? e.slope[0] : 0.f;
+    float pslope = 0.f;
     auto load_epi = [&](int tile, int t, int set) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             if constexpr (RES) eres[set][q] = bload4h(r_res, ooff(tile, e.ldres, t, q));
             if constexpr (MASK) emask[set][q] = bload4h(r_mask, ooff(tile, e.ld0, t, q));
             if constexpr (ACC) eold[set][q] = bload4h(r_old, ooff(tile, g.ldy, t, q));
+            if constexpr (PM) epre[set][q] = bload4h(r_pm, t < 2 ? ooff(tile, e.ld1, t, q) : OOR);
         }
     };
     // SA_BWD's / ROWSCALE's per-pixel operands: one set per tile, two sets (the next tile's are issued with its X)
@@ -1974,6 +1982,18 @@ __global__ __launch_bounds__(256, 2) void conv1x1_stream_hf_kernel(const ConvArg
                     o[2] = av.z + gm.x + (n + 2 == mi ? gm.y : 0.f);
                     o[3] = av.w + gm.x + (n + 3 == mi ? gm.y : 0.f);
                 }
+                if constexpr (PM) {
+                    if (t < 2 && p < a.M) {
+                        const float4 pv4 = h2f4(epre[cur][q]);
+                        const float pv[4] = {pv4.x, pv4.y, pv4.z, pv4.w};
+#pragma unroll
+                        for (int c = 0; c < 4; ++c) {
+                            o[c] = (float)(_Float16)o[c];
+                            if (!(pv[c] > 0.f)) pslope += pv[c] * o[c];
+                            o[c] = pv[c] > 0.f ? o[c] : pslope_a * o[c];
+                        }
+                    }
+                }
                 if constexpr (RS) {  // epi_store4's ROWSCALE: (acc * scale) + bias, out2, then the activation
                     const float sc = tset ? srs[1][q] : srs[0][q];
                     o[0] = av.x * sc + b4.x;
@@ -2012,6 +2032,13 @@ __global__ __launch_bounds__(256, 2) void conv1x1_stream_hf_kernel(const ConvArg
             }
             __builtin_amdgcn_sched_barrier(0);
         }
+    }
+    if constexpr (PM) {  // wave sums (xor shuffles), then the four waves' in a fixed order
+        __shared__ float pred[4];
+        for (int off = 32; off > 0; off >>= 1) pslope += __shfl_xor(pslope, off);
+        if (lane == 0) pred[wave] = pslope;
+        __syncthreads();
+        if (tid == 0) e.out2[blockIdx.x] = (pred[0] + pred[1]) + (pred[2] + pred[3]);
     }
 }
 
@@ -2063,6 +2090,12 @@ void conv1x1_stream_b6_kernel(const ConvArgs a) {
     // PReLU; the per-pixel scale is loaded once per tile like SAB's operands
     constexpr bool RS = (F & 16) != 0;
     static_assert(!RS || (CE && !RES && !MASK && !ACC && !SAB), "ROWSCALE: the coalesced epilogue, no other operand");
+    // PM (F & 32, round 6, with SAB): HYRES_ACT_PRELU_MASK on output channels [0, 64) — MultiScaleRefine's scale-1
+    // block writes PReLU(.) into multi[..., 0:64], so d multi's first 64 channels are that PReLU output's whole
+    // gradient: o = pre > 0 ? o : slope * o (pre = aux1 [P][ld1]), sum_{pre <= 0} pre * o into this block's partial
+    // (out2[block]); the slope gradient (res, ADDED) by prelu_slope_sum_kernel after the launch
+    constexpr bool PM = (F & 32) != 0;
+    static_assert(!PM || (SAB && !ACC && NT >= 2), "PReLU mask: the SA_BWD form without accumulate");
     constexpr int WPL = CO * KP;  // bf16 per weight plane
     __shared__ __attribute__((aligned(16))) __bf16 Ws[3 * WPL];
     __shared__ __attribute__((aligned(16))) float bs[CO];
@@ -2126,6 +2159,10 @@ void conv1x1_stream_b6_kernel(const ConvArgs a) {
     constexpr int SETS = stream_b6_vgprs<NT, KS, F>() == 128 ? 1 : 2;
     float4 xv[KS][2];
     float4 eres[RES ? SETS : 1][4], emask[MASK ? SETS : 1][4], eold[ACC ? SETS : 1][4];
+    float4 epre[PM ? SETS : 1][4];
+    const __amdgpu_buffer_rsrc_t r_pm = opnd_rsrc(PM ? e.aux1 : nullptr, npix * e.ld1 * 4);
+    const float pslope_a = PM ? e.slope[0] : 0.f;
+    float pslope = 0.f;
     // SAB: this tile's (d mean / C, d max) and argmax per epilogue row q, and the next tile's in flight
     float2 sg[SAB ? 4 : 1], sgn[SAB ? 4 : 1];
     int si[SAB ? 4 : 1], sin_[SAB ? 4 : 1];
@@ -2160,6 +2197,7 @@ void conv1x1_stream_b6_kernel(const ConvArgs a) {
             if constexpr (RES) eres[set][q] = bload4(r_res, ooff(tile, e.ldres, t, q));
             if constexpr (MASK) emask[set][q] = bload4(r_mask, ooff(tile, e.ld0, t, q));
             if constexpr (ACC) eold[set][q] = bload4(r_old, ooff(tile, g.ldy, t, q));
+            if constexpr (PM) epre[set][q] = bload4(r_pm, t < 2 ? ooff(tile, e.ld1, t, q) : OOR);
         }
     };
 #pragma unroll
@@ -2234,6 +2272,16 @@ void conv1x1_stream_b6_kernel(const ConvArgs a) {
 #pragma unroll
                     for (int c = 0; c < 4; ++c) o[c] = av4[c] + sg[q].x + (n + c == si[q] ? sg[q].y : 0.f);
                 }
+                if constexpr (PM) {
+                    if (t < 2 && pok) {  // as prelu_bwd4_kernel on the stored gradient
+                        const float pv[4] = {epre[cur][q].x, epre[cur][q].y, epre[cur][q].z, epre[cur][q].w};
+#pragma unroll
+                        for (int c = 0; c < 4; ++c) {
+                            if (!(pv[c] > 0.f)) pslope += pv[c] * o[c];
+                            o[c] = pv[c] > 0.f ? o[c] : pslope_a * o[c];
+                        }
+                    }
+                }
                 if constexpr (RS) {  // epi_store4's ROWSCALE: (acc * scale) + bias
                     o[0] = av.x * rsc[q] + b4.x;
                     o[1] = av.y * rsc[q] + b4.y;
@@ -2243,7 +2291,9 @@ void conv1x1_stream_b6_kernel(const ConvArgs a) {
                 if constexpr (RES) {
                     o[0] += eres[cur][q].x; o[1] += eres[cur][q].y; o[2] += eres[cur][q].z; o[3] += eres[cur][q].w;
                 }
-                if (pok && e.out2) st4(e.out2 + (long long)p * e.ldo2 + n, make_float4(o[0], o[1], o[2], o[3]));
+                if constexpr (!PM) {  // (PM: out2 holds the slope partials)
+                    if (pok && e.out2) st4(e.out2 + (long long)p * e.ldo2 + n, make_float4(o[0], o[1], o[2], o[3]));
+                }
                 if constexpr (MASK) {
                     o[0] = emask[cur][q].x > 0.f ? o[0] : 0.f;
                     o[1] = emask[cur][q].y > 0.f ? o[1] : 0.f;
@@ -2278,6 +2328,13 @@ void conv1x1_stream_b6_kernel(const ConvArgs a) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) rsc[q] = rscn[q];
         }
+    }
+    if constexpr (PM) {  // wave sums (xor shuffles), then the four waves' in a fixed order
+        __shared__ float pred[4];
+        for (int off = 32; off > 0; off >>= 1) pslope += __shfl_xor(pslope, off);
+        if (lane == 0) pred[wave] = pslope;
+        __syncthreads();
+        if (tid == 0) e.out2[blockIdx.x] = (pred[0] + pred[1]) + (pred[2] + pred[3]);
     }
 }
 
@@ -3193,15 +3250,17 @@ static int stream_hf_cfg(const hyres_conv_geom* g, const hyres_epilogue* e) {
             return 0;
         return 2 | (12 << 4) | (16 << 8);
     }
-    if (e->out2) return 0;
     if (e->kind == HYRES_EPI_SA_BWD) {  // round 6: the fusion 1x1's input-gradient under AMP, 64 -> 192
-        if (g_tune[21] == 0 || g->Ci != 64 || g->Co != 192 || e->act != HYRES_ACT_NONE || e->res || g->nphase != 1 ||
+        const bool pm = e->act == HYRES_ACT_PRELU_MASK && !e->accumulate;  // + the scale-1 PReLU backward
+        if (g_tune[21] == 0 || g->Ci != 64 || g->Co != 192 || (e->act != HYRES_ACT_NONE && !pm) || (e->res && !pm) ||
+            (e->out2 && !pm) || (pm && (!e->aux1 || e->ld1 < 64 || e->ld1 % 4 || !e->res)) || g->nphase != 1 ||
             g->ntaps != 1 || g->ish != 1 || g->isw != 1 || g->dh[0] != 0 || g->dw[0] != 0 || g->Hi != g->Hq ||
             g->Wi != g->Wq || g->Ho != g->Hq || g->Wo != g->Wq || (long long)g->B * g->Hq * g->Wq < 16384 ||
             g->ldx % 8 || g->ldy % 4 || e->ld0 % 2)
             return 0;
-        return 6 | (4 << 4) | ((8 | (e->accumulate ? 4 : 0)) << 8);
+        return 6 | (4 << 4) | ((pm ? 40 : (8 | (e->accumulate ? 4 : 0))) << 8);
     }
+    if (e->out2) return 0;
     if (e->kind != HYRES_EPI_BIAS) return 0;
     if (e->act != HYRES_ACT_NONE && e->act != HYRES_ACT_RELU && e->act != HYRES_ACT_RELU_MASK) return 0;
     if (g->nphase != 1 || g->ntaps != 1 || g->ish != 1 || g->isw != 1 || g->dh[0] != 0 || g->dw[0] != 0) return 0;
@@ -3222,11 +3281,13 @@ static int stream_b6_cfg(const hyres_conv_geom* g, const hyres_epilogue* e) {
     if (g_tune[7] != 1 || g_tune[10] == 0) return 0;
     if (e->io_f16 || e->f16_operands || e->square_input) return 0;
     if (e->kind == HYRES_EPI_SA_BWD) {  // round 6: the fusion 1x1's input-gradient, 64 -> 192 (coalesced epilogue only)
-        if (g_tune[11] == 0 || g_tune[21] == 0 || g->Ci != 64 || g->Co != 192 || e->act != HYRES_ACT_NONE || e->res ||
-            e->out2 || g->nphase != 1 || g->ntaps != 1 || g->ish != 1 || g->isw != 1 || g->dh[0] != 0 || g->dw[0] != 0 ||
+        const bool pm = e->act == HYRES_ACT_PRELU_MASK && !e->accumulate;
+        if (g_tune[11] == 0 || g_tune[21] == 0 || g->Ci != 64 || g->Co != 192 || (e->act != HYRES_ACT_NONE && !pm) ||
+            (e->res && !pm) || (e->out2 && !pm) || (pm && (!e->aux1 || e->ld1 < 64 || e->ld1 % 4 || !e->res)) ||
+            g->nphase != 1 || g->ntaps != 1 || g->ish != 1 || g->isw != 1 || g->dh[0] != 0 || g->dw[0] != 0 ||
             g->Hi != g->Hq || g->Wi != g->Wq || g->Ho != g->Hq || g->Wo != g->Wq || (long long)g->B * g->Hq * g->Wq < 65536)
             return 0;
-        return 6 | (4 << 4) | ((8 | (e->accumulate ? 4 : 0)) << 8);
+        return 6 | (4 << 4) | ((pm ? 40 : (8 | (e->accumulate ? 4 : 0))) << 8);
     }
     if (g->nphase != 1 || g->ntaps != 1 || g->ish != 1 || g->isw != 1 || g->dh[0] != 0 || g->dw[0] != 0) return 0;
     if (g->Hi != g->Hq || g->Wi != g->Wq || g->Ho != g->Hq || g->Wo != g->Wq) return 0;
@@ -3279,6 +3340,13 @@ static int launch_stream_b6_ce(const ConvArgs& a, hipStream_t st) {
     }
     const int blocks = std::max(1, std::min(ceil_div(ceil_div(a.M, 32), 4), num_cus() * occ));
     hipLaunchKernelGGL((conv1x1_stream_b6_kernel<NT, KS, F, CE>), dim3(blocks), dim3(256), 0, st, a);
+    if constexpr ((F & 32) != 0) {  // the PReLU mask's slope partials, summed in a fixed order and added
+        const int rc = HY_LAUNCH_CHECK("conv1x1_stream_b6_kernel");
+        if (rc) return rc;
+        hipLaunchKernelGGL(prelu_slope_sum_kernel, dim3(1), dim3(256), 0, st, (const float*)a.e.out2, blocks,
+                           const_cast<float*>(a.e.res));
+        return HY_LAUNCH_CHECK("prelu_slope_sum_kernel");
+    }
     return HY_LAUNCH_CHECK("conv1x1_stream_b6_kernel");
 }
 template <int NT, int KS, int F>
@@ -3304,6 +3372,7 @@ static int launch_stream_b6(const ConvArgs& a, int cfg, hipStream_t st) {
     const int nt = cfg & 15, ks = (cfg >> 4) & 15, f = cfg >> 8;
     if (nt == 6 && ks == 4 && f == 8) return launch_stream_b6_ce<6, 4, 8, true>(a, st);
     if (nt == 6 && ks == 4 && f == 12) return launch_stream_b6_ce<6, 4, 12, true>(a, st);
+    if (nt == 6 && ks == 4 && f == 40) return launch_stream_b6_ce<6, 4, 40, true>(a, st);
     if (nt == 2 && ks == 12 && f == 16) return launch_stream_b6_ce<2, 12, 16, true>(a, st);
     if (nt == 2 && ks == 4) return launch_stream_b6_f<2, 4>(a, f, st);
     if (nt == 4 && ks == 4) return launch_stream_b6_f<4, 4>(a, f, st);
@@ -3326,6 +3395,13 @@ static int launch_stream_hf_one(const ConvArgs& a, hipStream_t st) {
     }
     const int blocks = std::max(1, std::min(ceil_div(ceil_div(a.M, 32), 4), num_cus() * occ));
     hipLaunchKernelGGL((conv1x1_stream_hf_kernel<NT, KC, F>), dim3(blocks), dim3(256), 0, st, a);
+    if constexpr ((F & 32) != 0) {  // the PReLU mask's slope partials, summed in a fixed order and added
+        const int rc = HY_LAUNCH_CHECK("conv1x1_stream_hf_kernel");
+        if (rc) return rc;
+        hipLaunchKernelGGL(prelu_slope_sum_kernel, dim3(1), dim3(256), 0, st, (const float*)a.e.out2, blocks,
+                           const_cast<float*>(a.e.res));
+        return HY_LAUNCH_CHECK("prelu_slope_sum_kernel");
+    }
     return HY_LAUNCH_CHECK("conv1x1_stream_hf_kernel");
 }
 template <int NT, int KC>
@@ -3346,6 +3422,7 @@ static int launch_stream_hf(const ConvArgs& a, int cfg, hipStream_t st) {
     const int nt = cfg & 15, kc = (cfg >> 4) & 15, f = cfg >> 8;
     if (nt == 6 && kc == 4 && f == 8) return launch_stream_hf_one<6, 4, 8>(a, st);
     if (nt == 6 && kc == 4 && f == 12) return launch_stream_hf_one<6, 4, 12>(a, st);
+    if (nt == 6 && kc == 4 && f == 40) return launch_stream_hf_one<6, 4, 40>(a, st);
     if (nt == 2 && kc == 12 && f == 16) return launch_stream_hf_one<2, 12, 16>(a, st);
     if (nt == 2 && kc == 4) return launch_stream_hf_f<2, 4>(a, f, st);
     if (nt == 2 && kc == 8) return launch_stream_hf_f<2, 8>(a, f, st);
@@ -3532,7 +3609,12 @@ int hyres_conv_forward(const hyres_conv_geom* g, const float* x, const float* w2
     }
     if (e->act == HYRES_ACT_RELU_MASK)
         HY_REQUIRE(e->aux0 && e->kind == HYRES_EPI_BIAS, HYRES_E_ARG, "conv: ReLU mask needs aux0, BIAS epilogue");
-    if (e->act == HYRES_ACT_PRELU_MASK) {
+    if (e->act == HYRES_ACT_PRELU_MASK && e->kind == HYRES_EPI_SA_BWD) {  // round 6: the scale-1 PReLU on SA_BWD
+        HY_REQUIRE(e->aux1 && e->ld1 >= 64 && e->slope && e->res && e->out2 && e->ldo2 >= HYRES_PRELU_PARTIALS &&
+                       !e->accumulate,
+                   HYRES_E_ARG, "conv: SA_BWD + PReLU mask needs aux1 (pre-activation of channels 0..63, ld1 >= 64), "
+                   "slope, res (slope gradient), out2 (>= %d partials), no accumulate", HYRES_PRELU_PARTIALS);
+    } else if (e->act == HYRES_ACT_PRELU_MASK) {
         HY_REQUIRE(e->aux0 && e->aux1 && e->aux2 && e->slope && e->kind == HYRES_EPI_BIAS && !e->accumulate &&
                        !e->out2 && e->io_f16 == 0 && !e->f16_operands && e->ld2 >= HYRES_PRELU_PARTIALS,
                    HYRES_E_ARG, "conv: PReLU mask needs aux0 (pre-activation), aux1 (slope gradient), aux2 (>= %d "
@@ -3545,8 +3627,9 @@ int hyres_conv_forward(const hyres_conv_geom* g, const float* x, const float* w2
         HY_REQUIRE(e->aux1 && !e->square_input && !e->accumulate, HYRES_E_ARG,
                    "conv: ROWSCALE needs aux1 (per-pixel scale), no square_input / accumulate");
     if (e->kind == HYRES_EPI_SA_BWD)
-        HY_REQUIRE(e->aux0 && e->aux2 && e->ld0 >= 2 && !e->square_input && e->act == HYRES_ACT_NONE && !e->res &&
-                       !e->out2 && (!(e->io_f16 & 2) || stream_hf_cfg(g, e)),
+        HY_REQUIRE(e->aux0 && e->aux2 && e->ld0 >= 2 && !e->square_input &&
+                       ((e->act == HYRES_ACT_NONE && !e->res && !e->out2) || e->act == HYRES_ACT_PRELU_MASK) &&
+                       (!(e->io_f16 & 2) || stream_hf_cfg(g, e)),
                    HYRES_E_ARG, "conv: SA_BWD needs aux0 ([P][ld0 >= 2]) and aux2 (argmax), no act / res / out2, fp32 Y "
                    "(fp16 Y: conv1x1_stream_hf_kernel's 64 -> 192 only)");
     hipStream_t st = as_stream(s);
@@ -3600,8 +3683,9 @@ int hyres_conv_forward(const hyres_conv_geom* g, const float* x, const float* w2
         }
     }
     // no other kernel implements SA_BWD with an fp16 Y (its epi_store4 instantiations leave the case out)
-    HY_REQUIRE(!(e->kind == HYRES_EPI_SA_BWD && (e->io_f16 & 2)), HYRES_E_ARG,
-               "conv: an fp16-Y SA_BWD input-gradient needs conv1x1_stream_hf_kernel (alignment / size / split mode)");
+    HY_REQUIRE(!(e->kind == HYRES_EPI_SA_BWD && ((e->io_f16 & 2) || e->act == HYRES_ACT_PRELU_MASK)), HYRES_E_ARG,
+               "conv: an fp16-Y or PReLU-mask SA_BWD input-gradient needs the streaming kernels (alignment / size / "
+               "split mode)");
     {
         const int nt = stream_h_nt(g, e);
         const long long xb = (long long)a.M * g->ldx * 2;

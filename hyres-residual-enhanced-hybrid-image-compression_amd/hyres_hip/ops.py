@@ -72,7 +72,7 @@ class Node:
     """NHWC activation [B,H,W,C]; ``v`` may be a channel slice of a wider buffer (pixel stride ld)."""
 
     __slots__ = ("v", "B", "H", "W", "C", "ld", "rg", "parent", "c0", "_g", "gflag", "relu_out", "gmasked",
-                 "pending", "prelu", "pmasked")
+                 "pending", "prelu", "pmasked", "prelu_slices")
 
     def __init__(self, v: torch.Tensor, rg: bool = True, parent: "Node" = None, c0: int = 0):
         assert v.dim() == 4 and v.stride(3) == 1, "Node expects an NHWC tensor with unit channel stride"
@@ -95,6 +95,9 @@ class Node:
         # (HYRES_ACT_PRELU_MASK) — unlike the ReLU mask it is not idempotent, so no second contribution may follow
         self.prelu = None
         self.pmasked = False
+        # channel slices of this node written by a conv with a fused PReLU (training): the writer of this node's
+        # gradient may apply their PReLU backward (refine_ops.sa_fold_fusion: MultiScaleRefine's scale 1 in multi)
+        self.prelu_slices = None
         # deferred residual gradient (tensor, pixel stride): added by the next input-gradient conv's
         # epilogue (``grad_target_epi``) instead of a separate add pass, or materialised on first access
         self.pending = None
@@ -953,6 +956,8 @@ def conv2d(tape: Optional[Tape], x: Node, weight: torch.Tensor, bias: Optional[t
         return y
     if pre is not None:
         y.prelu = (pre, slope)
+        if y.parent is not None:
+            y.parent.prelu_slices = (y.parent.prelu_slices or []) + [y]
 
     def bwd():
         gy = y.grad()

@@ -214,10 +214,40 @@ def sa_fold_fusion(tape: Optional[Tape], multi: Node, w_sa: torch.Tensor, weight
             ed.accumulate = acc
             ed.f16_operands = f16
             ed.io_f16 = O._dgrad_io(gs, multi)
+            sl = _prelu_slice0(multi, tgt.dtype) if acc == 0 else None
+            if sl is not None:
+                # round 6: multi[..., 0:64] is scale 1's PReLU output and this conv its one gradient writer: its
+                # PReLU backward rides on the epilogue (HYRES_ACT_PRELU_MASK on the streaming SA_BWD kernels)
+                pre1, slope1 = sl.prelu
+                dslope1 = param_grad(slope1) if slope1.requires_grad else _empty((1,), dev)
+                part = _empty((L.PRELU_PARTIALS,), dev)
+                ed.act = L.ACT_PRELU_MASK
+                ed.aux1, ed.ld1 = pre1.data_ptr(), sl.C
+                ed.slope = slope1.data_ptr()
+                ed.res = dslope1.data_ptr()
+                ed.out2, ed.ldo2 = part.data_ptr(), L.PRELU_PARTIALS
+                if ", 40" not in O.conv_variant(gd, ed, False):  # the streaming kernels' PReLU-mask form only
+                    ed.act, ed.aux1, ed.ld1, ed.slope, ed.res, ed.out2, ed.ldo2 = L.ACT_NONE, None, 0, None, None, None, 0
+                    sl = None
             O._launch_conv(gd, gs.data_ptr(), w2d, gd.ntaps * Co, tgt.data_ptr(), ed)
+            if sl is not None:
+                sl.pmasked = True
 
     tape.push(bwd)
     return y
+
+
+def _prelu_slice0(multi: Node, gdt: torch.dtype) -> Optional[Node]:
+    """The 64-channel slice at channel 0 of ``multi`` written by a conv with a fused PReLU (MultiScaleRefine's
+    scale 1), when its PReLU backward may be folded into multi's gradient writer: folds on, not a trace point, the
+    pre-activation contiguous and in the gradient's dtype (the SA_BWD kernels read it beside Y)."""
+    if not O.FOLD_PRELU:
+        return None
+    for n in multi.prelu_slices or []:
+        if (n.c0 == 0 and n.C == 64 and n.prelu is not None and not O.Trace.traced(n)
+                and n.prelu[0].is_contiguous() and n.prelu[0].dtype == gdt):
+            return n
+    return None
 
 
 def sa_fold_amp_ok(tape: Optional[Tape], multi: Node, Co: int) -> bool:

@@ -135,8 +135,9 @@ def test_stream_b6_kernels_fill_the_vgpr_file(meta):
     their LDS, take all 512."""
     ks = _find(meta, "conv1x1_stream_b6_kernel")
     # (NT, KS) in {(2, 4), (4, 4), (2, 8)} x 8 epilogue-operand sets x coalesced epilogue on / off, + <6, 4, 8 | 12, true>
-    # + the ROWSCALE form <2, 12, 16, true> + <4, 8, 0 | 2> (128 -> 128) x coalesced on / off
-    assert len(ks) == 55
+    # + the ROWSCALE form <2, 12, 16, true> + <4, 8, 0 | 2> (128 -> 128) x coalesced on / off + <6, 4, 40, true>
+    # (SA_BWD with the scale-1 PReLU mask)
+    assert len(ks) == 56
     for k in ks:
         full = 512 if ("kernelILi6E" in k["name"] or "ELi12E" in k["name"] or "kernelILi4ELi8E" in k["name"]) else 256
         assert k["alloc"] == full and kernel_meta.residency(k)["hole_vgprs"] == 0 and k["scratch"] == 0, k

@@ -416,6 +416,68 @@ def test_refine_branch_fwd_bwd(branch):
 
 
 @pytest.mark.parametrize("amp", [False, True])
+def test_multiscale_refine_prelu_folds_match_unfused(amp, monkeypatch):
+    """The whole MultiScaleRefine (enhancement.py:84-110) in training with every PReLU-backward fold on — round 6's
+    last one included: scale 1's PReLU applied by the SA_BWD streaming input-gradient that writes multi[..., 0:64]
+    (conv1x1_stream_b6_kernel / conv1x1_stream_hf_kernel <6, 4, 40>) — against HYRES_FOLD_PRELU=0 on the same inputs:
+    d x and every weight / bias gradient bit for bit in fp32 (2e-3 under AMP, fp16 activations and gradients), the
+    PReLU slopes (the same products summed in other orders) at 1e-5 (AMP 2e-3). The scale-1 fold must fire."""
+    import models.layers.enhancement as EH
+    from hyres_hip import ops as O
+    D = dev()
+    B, C, H, W = 4, 3, 128, 128
+    torch.manual_seed(5)
+    m = EH.MultiScaleRefine(C, 64).to(D)
+    with torch.no_grad():
+        for mod in m.modules():
+            if isinstance(mod, torch.nn.Conv2d) and mod.bias is not None:
+                mod.bias.add_(0.02)
+    x = _rand((B, C, H, W), 91)
+    gy = _rand((B, C, H, W), 92)
+    names = []
+    orig = O.conv_variant
+
+    def spy(g, e, sk):
+        r = orig(g, e, sk)
+        names.append(r)
+        return r
+
+    monkeypatch.setattr(O, "conv_variant", spy)
+
+    def run(fold):
+        monkeypatch.setattr(O, "FOLD_PRELU", fold)
+        for p in m.parameters():
+            p.grad = None
+        names.clear()
+        tape = O.Tape()
+        xn = O.to_nhwc(x.to(D), rg=True)
+        with contextlib.ExitStack() as st:
+            if amp:
+                st.enter_context(torch.autocast("cuda", dtype=torch.float16))
+                st.enter_context(O.f16_region())
+            yn = m.hip(tape, xn)
+        yn.set_grad(O.nchw_grad_to_nhwc(gy.to(D)))
+        tape.backward()
+        torch.cuda.synchronize()
+        return (O.to_nchw_grad(xn).float().cpu(), {k: p.grad.cpu().clone() for k, p in m.named_parameters()},
+                any(", 40" in n for n in names))
+
+    dx0, g0, f0 = run(False)
+    dx1, g1, f1 = run(True)
+    assert f1 and not f0, (f0, f1)
+    slopes = [k for k, p in m.named_parameters() if p.numel() == 1]
+    assert len(slopes) >= 5, slopes
+    for k in g0:
+        if k in slopes:
+            assert rel_err(g1[k], g0[k]) < (2e-3 if amp else 1e-5), k
+        elif amp:
+            assert rel_err(g1[k], g0[k]) < 2e-3, k
+        else:
+            assert torch.equal(g1[k], g0[k]), k
+    assert torch.equal(dx1, dx0) if not amp else rel_err(dx1, dx0) < 2e-3
+
+
+@pytest.mark.parametrize("amp", [False, True])
 def test_bilinear_up_prelu_fold_matches_unfused(amp, monkeypatch):
     """MultiScaleRefine's scales 2 / 3 (enhancement.py:89-103): conv + PReLU, then the bilinear up-sample. Round 6
     folds the PReLU backward into the up-sample's backward (hyres_bilinear_bwd_prelu, refine_ops.bilinear) — against
