@@ -116,7 +116,12 @@ int hyres_conv_weight_prep_batch(const void* descs, int n, long long total, hyre
                                 * (capacity ld2 floats >= HYRES_PRELU_PARTIALS), summed in a fixed order by a second
                                 * kernel of the same call (deterministic). kind BIAS, accumulate 0, fp32 IO.
                                 * Replaces prelu_bwd of MultiScaleRefine's scale blocks (enhancement.py:44-51,
-                                * 89-95): the dilation-2 conv's input-gradient writes the PReLU'd gradient directly */
+                                * 89-95): the dilation-2 conv's input-gradient writes the PReLU'd gradient directly.
+                                * With kind HYRES_EPI_SA_BWD (round 6, the streaming 64 -> 192 input-gradients only):
+                                * output channels [0, 64) get the PReLU backward — aux1 = their pre-activation (Y's
+                                * dtype, pitch ld1), slope gradient ADDED to ((float*)res)[0], partials in out2
+                                * (ldo2 >= HYRES_PRELU_PARTIALS); no accumulate. Replaces MultiScaleRefine scale 1's
+                                * prelu_bwd (its PReLU output is multi[..., 0:64], enhancement.py:113-115) */
 #define HYRES_PRELU_PARTIALS 2048
 
 #define HYRES_IO_X16 1   /* hyres_epilogue.io_f16 bits */
