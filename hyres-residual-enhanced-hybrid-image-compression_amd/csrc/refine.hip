@@ -504,7 +504,10 @@ __global__ void se_bwd_x_kernel(const float* gy, const float* sgate, const float
 // argmax (torch.max(dim=1) on CPU keeps the first maximal index; the backward routes g_max there).
 // channel mean / max (+ first argmax, torch.max semantics) per pixel: 16 lanes per pixel (4 pixels per wave,
 // each lane a float4 stride over the channels), folded with 4 xor-shuffles
-template <bool H = false>
+// NC > 0 (round 6: C = 64 * NC, MultiScaleRefine's 192): the lane's NC float4 loads are all issued before the first
+// compare — the runtime-bounded loop waited on each in turn (191 us at 256^2 x 16 x 192 fp32, ~4.2 TB/s); the same
+// order of sums and compares, bit-identical
+template <bool H = false, int NC = 0>
 __global__ __launch_bounds__(256) void sa_pool_kernel(const float* x, float* pooled2, int* amax, long long P, int C) {
     const int l16 = threadIdx.x & 15;
     const long long p = (long long)blockIdx.x * 16 + (threadIdx.x >> 4);
@@ -512,7 +515,23 @@ __global__ __launch_bounds__(256) void sa_pool_kernel(const float* x, float* poo
     const long long xp = (ok ? p : 0) * C;
     float s = 0.f, m = -INFINITY;
     int mi = 0x7fffffff;
-    if (ok) {
+    if constexpr (NC > 0) {
+        if (ok) {
+            float4 vv[NC];
+#pragma unroll
+            for (int k = 0; k < NC; ++k) vv[k] = ldv4<H>(x, xp + 4 * l16 + 64 * k);
+#pragma unroll
+            for (int k = 0; k < NC; ++k) {
+                const int c = 4 * l16 + 64 * k;
+                const float4 v = vv[k];
+                s += (v.x + v.y) + (v.z + v.w);
+                if (v.x > m) { m = v.x; mi = c; }
+                if (v.y > m) { m = v.y; mi = c + 1; }
+                if (v.z > m) { m = v.z; mi = c + 2; }
+                if (v.w > m) { m = v.w; mi = c + 3; }
+            }
+        }
+    } else if (ok) {
         for (int c = 4 * l16; c < C; c += 64) {
             const float4 v = ldv4<H>(x, xp + c);
             s += (v.x + v.y) + (v.z + v.w);
@@ -1130,7 +1149,12 @@ int hyres_spatial_attn_fwd(const float* x, const float* w, float* pooled2, int* 
     long long P = (long long)B * H * W;
     hipStream_t st = as_stream(s);
     HY_REQUIRE(C % 4 == 0 && aligned16(x), HYRES_E_ALIGN, "spatial_attn_fwd: C %% 4 and 16B-aligned x needed");
-    hipLaunchKernelGGL(sa_pool_kernel<false>, dim3((unsigned)((P + 15) / 16)), dim3(256), 0, st, x, pooled2, argmax, P, C);
+    if (C == 192)
+        hipLaunchKernelGGL((sa_pool_kernel<false, 3>), dim3((unsigned)((P + 15) / 16)), dim3(256), 0, st, x, pooled2, argmax,
+                           P, C);
+    else
+        hipLaunchKernelGGL(sa_pool_kernel<false>, dim3((unsigned)((P + 15) / 16)), dim3(256), 0, st, x, pooled2, argmax, P,
+                           C);
     int rc = HY_LAUNCH_CHECK("sa_pool");
     if (rc) return rc;
     hipLaunchKernelGGL(sa_conv_tiled_kernel, dim3((unsigned)sa_tiles(B, H, W)), dim3(256), 0, st, (const float*)pooled2,
@@ -1150,8 +1174,12 @@ int hyres_spatial_attn_fwd_f16(const void* x, const float* w, float* pooled2, in
                HYRES_E_ALIGN, "spatial_attn_fwd_f16: C %% 4 == 0 and 8B-aligned x/y required");
     const long long P = (long long)B * H * W;
     hipStream_t st = as_stream(s);
-    hipLaunchKernelGGL(sa_pool_kernel<true>, dim3((unsigned)((P + 15) / 16)), dim3(256), 0, st, (const float*)x, pooled2,
-                       argmax, P, C);
+    if (C == 192)
+        hipLaunchKernelGGL((sa_pool_kernel<true, 3>), dim3((unsigned)((P + 15) / 16)), dim3(256), 0, st, (const float*)x,
+                           pooled2, argmax, P, C);
+    else
+        hipLaunchKernelGGL(sa_pool_kernel<true>, dim3((unsigned)((P + 15) / 16)), dim3(256), 0, st, (const float*)x,
+                           pooled2, argmax, P, C);
     int rc = HY_LAUNCH_CHECK("sa_pool_f16");
     if (rc) return rc;
     hipLaunchKernelGGL(sa_conv_tiled_kernel, dim3((unsigned)sa_tiles(B, H, W)), dim3(256), 0, st, (const float*)pooled2,
