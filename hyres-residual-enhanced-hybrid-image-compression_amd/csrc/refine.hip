@@ -431,7 +431,9 @@ __global__ __launch_bounds__(256) void se_bwd_x4_kernel(const float* gy, const f
 }
 // the same with the producing PReLU's backward folded in (hyres_se_bwd_prelu, fp32): gx = PReLU'(pre) * (gy * gate + gpool)
 // and this block's share of the slope gradient sum_{pre <= 0} pre * (gy * gate + gpool) in part[blockIdx.x], elements
-// in the same order as prelu_bwd4_kernel's per-thread sums
+// in the same order as prelu_bwd4_kernel's per-thread sums. Round 6, AMP: H = pre fp16 (fp16 activations), G = gy / gx
+// fp16 (fp16 gradients: the gradient is rounded to fp16 first, the unfused chain's stored value)
+template <bool H = false, bool G = false>
 __global__ __launch_bounds__(256) void se_bwd_x4_prelu_kernel(const float* gy, const float* sgate, const float* gpool,
                                                               float* gx, int B, int HW, int C, const float* pre,
                                                               const float* slope, float* part) {
@@ -446,8 +448,8 @@ __global__ __launch_bounds__(256) void se_bwd_x4_prelu_kernel(const float* gy, c
         for (int u = 0; u < PW_UNR; ++u) {
             const int i = i0 + u * stride;
             if (i < n) {
-                v[u] = ld4(gy + 4LL * i);
-                pv[u] = ld4(pre + 4LL * i);
+                v[u] = ldv4<G>(gy, 4LL * i);
+                pv[u] = ldv4<H>(pre, 4LL * i);
             }
         }
 #pragma unroll
@@ -461,10 +463,11 @@ __global__ __launch_bounds__(256) void se_bwd_x4_prelu_kernel(const float* gy, c
             const float q[4] = {pv[u].x, pv[u].y, pv[u].z, pv[u].w};
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
+                if constexpr (G) o[k] = (float)(_Float16)o[k];
                 if (!(q[k] > 0.f)) ps += q[k] * o[k];
                 o[k] = q[k] > 0.f ? o[k] : a * o[k];
             }
-            *reinterpret_cast<float4*>(gx + 4LL * i) = make_float4(o[0], o[1], o[2], o[3]);
+            stv4<G>(gx, 4LL * i, make_float4(o[0], o[1], o[2], o[3]));
         }
     }
     __shared__ float red[256];
@@ -1082,11 +1085,11 @@ static int se_bwd_impl(const float* x, const float* gy, const float* w1, const f
     if (rc) return rc;
     long long n = (long long)B * HW * C;
     const unsigned am = G ? 7u : 15u;
-    if (pre) {  // the PReLU-folded form (fp32 only; checked by the entry point)
+    if (pre) {  // the PReLU-folded form (alignment checked by the entry points)
         float* pp = gpool + (long long)B * C;
         const int nb = std::min(pw_grid(n / 4), SE_PRELU_PARTS);
-        hipLaunchKernelGGL(se_bwd_x4_prelu_kernel, dim3(nb), dim3(256), 0, st, gy, sgate, (const float*)gpool, gx, B, HW,
-                           C, pre, slope, pp);
+        hipLaunchKernelGGL((se_bwd_x4_prelu_kernel<H, G>), dim3(nb), dim3(256), 0, st, gy, sgate, (const float*)gpool, gx,
+                           B, HW, C, pre, slope, pp);
         rc = HY_LAUNCH_CHECK("se_bwd_x4_prelu");
         if (rc) return rc;
         hipLaunchKernelGGL(se_prelu_slope_sum_kernel, dim3(1), dim3(256), 0, st, (const float*)pp, nb, dslope);
@@ -1116,6 +1119,21 @@ int hyres_se_bwd_prelu(const float* x, const float* gy, const float* w1, const f
                HYRES_E_ARG, "se_bwd_prelu: needs pre / slope / dslope, C %% 4 == 0, 16B-aligned gy / gx / pre");
     return se_bwd_impl<false, false>(x, gy, w1, w2, pooled, hidden, sgate, gx, gw1, gw2, B, HW, C, Cr, ws, ws_bytes, s,
                                      pre, slope, dslope);
+}
+int hyres_se_bwd_prelu_f16(const void* x, const void* gy, const float* w1, const float* w2, const float* pooled,
+                           const float* hidden, const float* sgate, void* gx, float* gw1, float* gw2, int B, int HW, int C,
+                           int Cr, const void* pre, const float* slope, float* dslope, void* ws, long long ws_bytes,
+                           int g16, hyres_stream_t s) {
+    const unsigned ag = g16 ? 7u : 15u;
+    HY_REQUIRE(pre && slope && dslope && C % 4 == 0 && (reinterpret_cast<uintptr_t>(gy) & ag) == 0 &&
+                   (reinterpret_cast<uintptr_t>(gx) & ag) == 0 && (reinterpret_cast<uintptr_t>(pre) & 7u) == 0 &&
+                   (long long)B * HW * C / 4 < (1LL << 31),
+               HYRES_E_ARG, "se_bwd_prelu_f16: needs pre / slope / dslope, C %% 4 == 0, aligned gy / gx / pre");
+    if (g16)
+        return se_bwd_impl<true, true>((const float*)x, (const float*)gy, w1, w2, pooled, hidden, sgate, (float*)gx, gw1,
+                                       gw2, B, HW, C, Cr, ws, ws_bytes, s, (const float*)pre, slope, dslope);
+    return se_bwd_impl<true, false>((const float*)x, (const float*)gy, w1, w2, pooled, hidden, sgate, (float*)gx, gw1,
+                                    gw2, B, HW, C, Cr, ws, ws_bytes, s, (const float*)pre, slope, dslope);
 }
 int hyres_se_bwd_f16(const void* x, const void* gy, const float* w1, const float* w2, const float* pooled,
                      const float* hidden, const float* sgate, void* gx, float* gw1, float* gw2, int B, int HW, int C,

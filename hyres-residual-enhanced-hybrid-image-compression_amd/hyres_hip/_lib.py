@@ -163,6 +163,7 @@ _SIGS = {
     "hyres_se_fwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _LL, _P]),
     "hyres_se_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _LL, _P]),
     "hyres_se_bwd_prelu": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _LL, _P]),
+    "hyres_se_bwd_prelu_f16": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _LL, _I, _P]),
     "hyres_se_workspace_bytes": (_LL, [_I, _I, _I]),
     "hyres_spatial_attn_fwd": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P]),
     "hyres_bilinear_fwd_f16": (_I, [_P, _I, _P, _I, _I, _I, _I, _I, _I, _I, _F, _F, _P]),

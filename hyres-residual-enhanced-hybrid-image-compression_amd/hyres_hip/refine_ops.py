@@ -86,17 +86,24 @@ def se_block(tape: Optional[Tape], x: Node, w1: torch.Tensor, w2: torch.Tensor) 
         tgt, acc = x.grad_target()
         assert g.dtype == tgt.dtype
         gx = tgt if acc == 0 else _empty((x.B, x.H, x.W, C), dev, tgt.dtype)
-        if (O.FOLD_PRELU and acc == 0 and x.prelu is not None and x.parent is None and not x.half
-                and not O.Trace.traced(x)
-                and g.dtype == torch.float32 and x.prelu[0].dtype == torch.float32 and C % 4 == 0):
+        if (O.FOLD_PRELU and acc == 0 and x.prelu is not None and x.parent is None and not O.Trace.traced(x)
+                and x.prelu[0].dtype == x.v.dtype and x.prelu[0].is_contiguous() and C % 4 == 0):
             # the producing PReLU's backward folded in (conv_in's act_in, enhancement.py:107-110): the SE block is
             # the only reader of PReLU(conv_in(x)), so its input-gradient is the PReLU output's whole gradient
             pre, slope = x.prelu
             dslope = param_grad(slope) if slope.requires_grad else _empty((1,), dev)
             ws2 = _ws(wsb + B * C * 4 + 2048 * 4, dev, slot=1)
-            L.call("hyres_se_bwd_prelu", x.ptr(), g.data_ptr(), w1.data_ptr(), w2.data_ptr(), pooled.data_ptr(),
-                   hidden.data_ptr(), sgate.data_ptr(), gx.data_ptr(), gw1.data_ptr(), gw2.data_ptr(), B, HW, C, Cr,
-                   pre.data_ptr(), slope.data_ptr(), dslope.data_ptr(), ws2.data_ptr(), ws2.numel(), L.stream())
+            if x.half:  # AMP (round 6): fp16 pre-activation, fp16 or fp32 gradients
+                L.call("hyres_se_bwd_prelu_f16", x.ptr(), g.data_ptr(), w1.data_ptr(), w2.data_ptr(), pooled.data_ptr(),
+                       hidden.data_ptr(), sgate.data_ptr(), gx.data_ptr(), gw1.data_ptr(), gw2.data_ptr(), B, HW, C, Cr,
+                       pre.data_ptr(), slope.data_ptr(), dslope.data_ptr(), ws2.data_ptr(), ws2.numel(),
+                       int(g.dtype == torch.float16), L.stream())
+            else:
+                assert g.dtype == torch.float32
+                L.call("hyres_se_bwd_prelu", x.ptr(), g.data_ptr(), w1.data_ptr(), w2.data_ptr(), pooled.data_ptr(),
+                       hidden.data_ptr(), sgate.data_ptr(), gx.data_ptr(), gw1.data_ptr(), gw2.data_ptr(), B, HW, C,
+                       Cr, pre.data_ptr(), slope.data_ptr(), dslope.data_ptr(), ws2.data_ptr(), ws2.numel(),
+                       L.stream())
             x.pmasked = True
             return
         ws2 = _ws(wsb + B * C * 4, dev, slot=1)

@@ -504,6 +504,12 @@ int hyres_spatial_attn_fwd_f16(const void* x, const float* w, float* pooled2, in
 int hyres_se_bwd_f16(const void* x, const void* gy, const float* w1, const float* w2, const float* pooled,
                      const float* hidden, const float* sgate, void* gx, float* gw1, float* gw2, int B, int HW,
                      int C, int Cr, void* ws, long long ws_bytes, int g16, hyres_stream_t s);
+/* ... with the producing PReLU's backward folded in under AMP (round 6): pre fp16 (fp16 activations); g16 = 1: gy /
+ * gx fp16 (the gradient rounded to fp16 before the PReLU, as the unfused chain stores it). As hyres_se_bwd_prelu. */
+int hyres_se_bwd_prelu_f16(const void* x, const void* gy, const float* w1, const float* w2, const float* pooled,
+                           const float* hidden, const float* sgate, void* gx, float* gw1, float* gw2, int B, int HW, int C,
+                           int Cr, const void* pre, const float* slope, float* dslope, void* ws, long long ws_bytes,
+                           int g16, hyres_stream_t s);
 int hyres_spatial_attn_bwd_f16(const void* x, const float* w, const float* pooled2, const int* argmax,
                                const float* attn, const void* gy, void* gx, float* gw, int B, int H, int W,
                                int C, void* ws, long long ws_bytes, int g16, hyres_stream_t s);
