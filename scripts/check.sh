@@ -115,6 +115,7 @@ for ph in "$@"; do
     s128)  scripts/gpu_run.sh "s128test:300:python -u -m pytest tests/test_stream_b6_gpu.py -x -v --timeout 180 --timeout-method thread -m gpu -k 'matches_fp64'" \
              "s128:300:for r in 1 2; do for m in '' '--mask' '--relu'; do for o in '' '--no-stream-b6'; do python3 scripts/conv_micro.py --H 128 --Ci 128 --Co 128 --K 1 --bf6 \$m \$o | sed \"s/^/[\$m \$o] /\"; done; done; done" || exit $?
            grep -h "us" gpurun_out/s128.log > gpurun_out/${tag}_s128.txt ;;
+    ab12)  bash scripts/tune_ab.sh $tag "default=" "nofold=HYRES_FOLD_PRELU=0" || exit $? ;;
     *) echo "unknown phase $ph"; exit 2 ;;
   esac
 done
